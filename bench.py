@@ -1,0 +1,272 @@
+#!/usr/bin/env python3
+"""Headline benchmark: liquid-dsp's streaming channelizer / filter hot path on MI355X.
+
+Metric (BASELINE.json): "Msamples/s: firfilt_crcf h=64 & firpfbch2_crcf M=1024;
+%HBM roofline".
+
+Workload of `value` (configs[3]): firpfbch2_crcf analyzer, M = 1024, m = 4,
+Kaiser As = 60, one independent 128M-sample complex-float stream per GPU
+(synthetic U(-0.5,0.5) data, resident in HBM before timing).  A step = one
+firpfbch2_crcf_execute_block_dev() over the whole 128M-sample stream
+(262,144 analyzer blocks, continuing the stream's state step after step).
+`value` = input samples of all ranks / max-over-ranks time (Msamples/s).
+The second headline workload, firfilt_crcf h=64 (configs[0] shape, 2^28
+samples per GPU so the 4 GB working set is far above the 256 MB Infinity
+Cache), is timed the same way and reported under "firfilt_crcf_h64".
+
+Multi-GPU: one process per GPU (torch.distributed.run); streams are
+independent, so per-GPU work is fixed (weak scaling) and the only
+collectives are RCCL all-reduces of the counters (max time, sample counts).
+
+roofline: algorithmic bytes of the dominant kernel per launch (24 B per
+input sample for the analyzer: 8 B read + 16 B written; 16 B per sample for
+firfilt) / its average launch duration measured with HIP events on the
+stream the kernel runs on; peak 8000 GB/s (MI355X HBM3E spec).
+
+cpu_baseline: the CPU oracle (oracle/oracle.c, a restatement of the
+reference firpfbch2.c analyzer; "port") on one host core, rank 0 at N=1
+only, over a bounded sample of the same workload (>= ~10 s of CPU work).
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "liquid-dsp_amd"))
+
+import torch  # noqa: E402  (import before the library: one HIP runtime per process)
+import torch.distributed as dist  # noqa: E402
+
+import liquidmi as LQ  # noqa: E402
+
+HBM_PEAK_GBPS = 8000.0
+
+
+def parse():
+    p = argparse.ArgumentParser()
+    p.add_argument("--gpus", type=int, default=1)
+    p.add_argument("--steps", type=int, default=20)
+    p.add_argument("--warmup", type=int, default=3)
+    p.add_argument("--samples", type=int, default=1 << 27, help="firpfbch2 input samples per GPU")
+    p.add_argument("--fir-samples", type=int, default=1 << 28, help="firfilt samples per GPU")
+    p.add_argument("--cpu-seconds", type=float, default=10.0, help="CPU baseline budget (rank 0, N=1)")
+    p.add_argument("--no-cpu-baseline", action="store_true")
+    p.add_argument("--no-firfilt", action="store_true")
+    p.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic.json"),
+                   help="PMC-derived HBM bytes per launch (from a separate rocprofv3 --pmc run)")
+    return p.parse_args()
+
+
+def setup_dist():
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    if world > 1:
+        dist.init_process_group(backend="nccl", init_method="env://")
+    return world, rank, local
+
+
+def barrier(world):
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+
+
+def allreduce_max(v, world):
+    t = torch.tensor([v], dtype=torch.float64, device="cuda")
+    if world > 1:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return float(t.item())
+
+
+def allreduce_sum(v, world):
+    t = torch.tensor([v], dtype=torch.float64, device="cuda")
+    if world > 1:
+        dist.all_reduce(t, op=dist.ReduceOp.SUM)
+    return float(t.item())
+
+
+def synth_complex(n, seed):
+    g = torch.Generator(device="cuda")
+    g.manual_seed(seed)
+    x = torch.rand(2 * n, generator=g, device="cuda", dtype=torch.float32) - 0.5
+    return x
+
+
+def time_steps(run_step, steps, warmup, world, stream):
+    for _ in range(warmup):
+        run_step()
+    barrier(world)
+    ev0 = torch.cuda.Event(enable_timing=True)
+    ev1 = torch.cuda.Event(enable_timing=True)
+    t0 = time.perf_counter()
+    ev0.record(stream)
+    for _ in range(steps):
+        run_step()
+    ev1.record(stream)
+    barrier(world)
+    wall = time.perf_counter() - t0
+    gpu_ms = ev0.elapsed_time(ev1)
+    return wall, gpu_ms
+
+
+def bench_firpfbch2(args, world, rank, stream):
+    M, m = 1024, 4
+    n = args.samples - args.samples % (M // 2)
+    nblocks = n // (M // 2)
+    x = synth_complex(n, 1234 + rank)
+    y = torch.empty(2 * nblocks * M, dtype=torch.float32, device="cuda")
+    q = LQ.FirPfbch2(LQ.LIQUID_ANALYZER, M, m, 60.0)
+    q.set_stream(stream.cuda_stream)
+
+    def step():
+        q.execute_block_dev(x.data_ptr(), nblocks, y.data_ptr())
+
+    wall, gpu_ms = time_steps(step, args.steps, args.warmup, world, stream)
+    res = {"n": n, "nblocks": nblocks, "wall": wall, "gpu_ms": gpu_ms}
+    q.destroy()
+    del x, y
+    torch.cuda.empty_cache()
+    return res
+
+
+def bench_firfilt(args, world, rank, stream):
+    n = args.fir_samples
+    x = synth_complex(n, 777 + rank)
+    y = torch.empty(2 * n, dtype=torch.float32, device="cuda")
+    g = torch.Generator()
+    g.manual_seed(5)
+    h = (torch.rand(64, generator=g) - 0.5).numpy()
+    q = LQ.FirFilt("crcf", h)
+    q.set_stream(stream.cuda_stream)
+
+    def step():
+        q.execute_block_dev(x.data_ptr(), n, y.data_ptr())
+
+    wall, gpu_ms = time_steps(step, args.steps, args.warmup, world, stream)
+    res = {"n": n, "wall": wall, "gpu_ms": gpu_ms}
+    q.destroy()
+    del x, y
+    torch.cuda.empty_cache()
+    return res
+
+
+def copy_bandwidth():
+    """Measured device copy rate (read+write GB/s) as a practical HBM ceiling."""
+    a = torch.empty(1 << 28, dtype=torch.float32, device="cuda")
+    b = torch.empty_like(a)
+    for _ in range(3):
+        b.copy_(a)
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(10):
+        b.copy_(a)
+    e1.record()
+    torch.cuda.synchronize()
+    ms = e0.elapsed_time(e1) / 10
+    gbps = 2 * a.numel() * 4 / (ms * 1e-3) / 1e9
+    del a, b
+    torch.cuda.empty_cache()
+    return gbps
+
+
+def cpu_baseline(seconds):
+    """Oracle firpfbch2 analyzer (M=1024, m=4) on one core, bounded sample."""
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    import numpy as np
+
+    import oracle_lib as O
+    q = O.FirPfbch2(O.ANALYZER, 1024, 4, 60.0)
+    rng = np.random.default_rng(9)
+    chunk = 1 << 20
+    x = (rng.uniform(-0.5, 0.5, chunk) + 1j * rng.uniform(-0.5, 0.5, chunk)).astype(np.complex64)
+    done = 0
+    t0 = time.perf_counter()
+    while True:
+        q.execute_block(x)
+        done += chunk
+        el = time.perf_counter() - t0
+        if el >= seconds:
+            break
+    return {"value": done / el / 1e6, "unit": "Msamples/s", "cores": 1, "kind": "port",
+            "sample": "oracle firpfbch2_crcf analyzer M=1024 m=4 As=60 on %d x 2^20 complex samples "
+                      "(%.1f s, 1 thread)" % (done // chunk, el)}
+
+
+def main():
+    args = parse()
+    world, rank, local = setup_dist()
+    # a dedicated (non-null) stream: the library's objects launch on it and
+    # the HIP events below are recorded on it
+    stream = torch.cuda.Stream()
+
+    pfb = bench_firpfbch2(args, world, rank, stream)
+    t_pfb = allreduce_max(pfb["wall"], world)
+    g_pfb = allreduce_max(pfb["gpu_ms"], world)
+    tot_pfb = allreduce_sum(pfb["n"] * args.steps, world)
+
+    fir = None
+    if not args.no_firfilt:
+        fir = bench_firfilt(args, world, rank, stream)
+        t_fir = allreduce_max(fir["wall"], world)
+        g_fir = allreduce_max(fir["gpu_ms"], world)
+        tot_fir = allreduce_sum(fir["n"] * args.steps, world)
+
+    copy_gbps = copy_bandwidth() if rank == 0 else None
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        cpu = cpu_baseline(args.cpu_seconds)
+
+    if rank == 0:
+        # dominant kernel: firpfbch2 analyzer, one launch per step (+ a tiny
+        # history-window update launch on the same stream)
+        launch_ms = g_pfb / args.steps
+        alg_bytes = 24.0 * pfb["n"]
+        achieved = alg_bytes / (launch_ms * 1e-3) / 1e9
+        traffic = None
+        if os.path.exists(args.traffic_json):
+            with open(args.traffic_json) as f:
+                tj = json.load(f)
+            traffic = tj.get("firpfbch2_bytes_per_launch")
+        out = {
+            "metric": "Msamples/s: firfilt_crcf h=64 & firpfbch2_crcf M=1024; %HBM roofline",
+            "value": tot_pfb / t_pfb / 1e6,
+            "unit": "Msamples/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": t_pfb / args.steps * 1e3,
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "f32",
+            "data": "synthetic U(-0.5,0.5) complex float32, HBM resident",
+            "config": {"workload": "firpfbch2_crcf analyzer M=1024 m=4 As=60, %d samples/GPU (BASELINE configs[3])"
+                                   % pfb["n"], "M": 1024, "m": 4, "samples_per_gpu": pfb["n"],
+                       "blocks_per_step": pfb["nblocks"], "parallelism": "stream-per-gpu x%d" % world},
+            "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBPS, "unit": "GB/s",
+                         "frac": achieved / HBM_PEAK_GBPS, "traffic": traffic,
+                         "bytes_per_unit": "24 B/input sample (8 read + 16 write)",
+                         "launch_ms": launch_ms, "measured_copy_GBps": copy_gbps},
+            "cpu_baseline": cpu,
+        }
+        if fir is not None:
+            fl_ms = g_fir / args.steps
+            fach = 16.0 * fir["n"] / (fl_ms * 1e-3) / 1e9
+            out["firfilt_crcf_h64"] = {"value": tot_fir / t_fir / 1e6, "unit": "Msamples/s",
+                                       "samples_per_gpu": fir["n"], "ms_per_step": t_fir / args.steps * 1e3,
+                                       "roofline": {"bound": "hbm", "achieved": fach, "peak": HBM_PEAK_GBPS,
+                                                    "unit": "GB/s", "frac": fach / HBM_PEAK_GBPS,
+                                                    "bytes_per_unit": "16 B/sample", "launch_ms": fl_ms}}
+        print(json.dumps(out))
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,223 @@
+/*
+ * liquid_mi355x.h -- drop-in replacement for the streaming filter /
+ * channelizer subset of liquid-dsp's include/liquid.h (liquid-dsp 1.2.0),
+ * executed on AMD Instinct MI355X (gfx950) by hand-written HIP kernels.
+ *
+ * Every declaration in the "liquid.h subset" sections keeps the reference
+ * signature and semantics (create / execute / destroy, opaque handles,
+ * unsigned sizes, liquid_float_complex samples, invalid arguments print to
+ * stderr and exit(1)).  The line references name the liquid.h declaration
+ * each symbol replaces.  A program that only uses these objects compiles
+ * against this header unchanged and links -lliquid_mi355x instead of
+ * -lliquid.
+ *
+ * The "extensions" sections are additive (new names): batched and
+ * device-pointer entry points, explicit stream control.  liquid.h's per-call
+ * granularity (e.g. firpfbch2_crcf_execute = M/2 samples) cannot feed a GPU;
+ * the block/batch forms can.  All original symbols still return only after
+ * their output is written.
+ *
+ * There is no CPU fallback: without a usable HIP device every constructor
+ * prints an error and exits (same failure style as the reference).
+ */
+#ifndef LIQUID_MI355X_H
+#define LIQUID_MI355X_H
+
+#ifdef __cplusplus
+extern "C" {
+#define LIQUID_USE_COMPLEX_H 0
+#else
+#define LIQUID_USE_COMPLEX_H 1
+#endif
+
+/* liquid.h:49-50 */
+#define LIQUID_VERSION "1.2.0"
+#define LIQUID_VERSION_NUMBER 1002000
+
+/* liquid.h:55-57 */
+extern const char liquid_version[];
+const char *liquid_libversion(void);
+int liquid_libversion_number(void);
+
+/* liquid.h:77-88: C99 complex in C, std::complex<float> in C++ (same layout) */
+#if LIQUID_USE_COMPLEX_H == 1
+#include <complex.h>
+#define LIQUID_DEFINE_COMPLEX(R, C) typedef R _Complex C
+#elif defined _GLIBCXX_COMPLEX || defined _LIBCPP_COMPLEX
+#define LIQUID_DEFINE_COMPLEX(R, C) typedef std::complex<R> C
+#else
+#define LIQUID_DEFINE_COMPLEX(R, C) typedef struct { R real; R imag; } C;
+#endif
+LIQUID_DEFINE_COMPLEX(float, liquid_float_complex);
+
+/* liquid.h:5651-5652 */
+#define LIQUID_ANALYZER 0
+#define LIQUID_SYNTHESIZER 1
+
+/* ------------------------------------------------------------------------ */
+/* filter design (liquid.h:1476 kaiser_beta_As, :1548 liquid_firdes_kaiser)  */
+/* ------------------------------------------------------------------------ */
+float kaiser_beta_As(float _As);
+void liquid_firdes_kaiser(unsigned int _n, float _fc, float _As, float _mu, float *_h);
+
+/* ------------------------------------------------------------------------ */
+/* dotprod (liquid.h:503-560): rrrf, crcf, cccf                              */
+/* ------------------------------------------------------------------------ */
+#define LQMI_DOTPROD_API(DOTPROD, TO, TC, TI)                                                   \
+    typedef struct DOTPROD##_s *DOTPROD;                                                        \
+    void DOTPROD##_run(TC *_h, TI *_x, unsigned int _n, TO *_y);                                \
+    void DOTPROD##_run4(TC *_h, TI *_x, unsigned int _n, TO *_y);                               \
+    DOTPROD DOTPROD##_create(TC *_v, unsigned int _n);                                          \
+    DOTPROD DOTPROD##_recreate(DOTPROD _q, TC *_v, unsigned int _n);                            \
+    void DOTPROD##_destroy(DOTPROD _q);                                                         \
+    void DOTPROD##_print(DOTPROD _q);                                                           \
+    void DOTPROD##_execute(DOTPROD _q, TI *_v, TO *_y);                                         \
+    /* extension: Y[v] = dot(h, X[v*_n .. v*_n+_n)), host pointers */                          \
+    void DOTPROD##_execute_batch(DOTPROD _q, TI *_X, unsigned long long _nvec, TO *_Y);         \
+    /* extension: same on device pointers, asynchronous on the object's stream */               \
+    void DOTPROD##_execute_batch_dev(DOTPROD _q, const TI *_dX, unsigned long long _nvec,       \
+                                     TO *_dY);                                                  \
+    void DOTPROD##_set_stream(DOTPROD _q, void *_hip_stream);                                   \
+    void *DOTPROD##_get_stream(DOTPROD _q);
+
+LQMI_DOTPROD_API(dotprod_rrrf, float, float, float)
+LQMI_DOTPROD_API(dotprod_crcf, liquid_float_complex, float, liquid_float_complex)
+LQMI_DOTPROD_API(dotprod_cccf, liquid_float_complex, liquid_float_complex, liquid_float_complex)
+
+/* ------------------------------------------------------------------------ */
+/* firfilt (liquid.h:1985-2090): rrrf, crcf, cccf                            */
+/* ------------------------------------------------------------------------ */
+#define LQMI_FIRFILT_API(FIRFILT, TO, TC, TI)                                                   \
+    typedef struct FIRFILT##_s *FIRFILT;                                                        \
+    FIRFILT FIRFILT##_create(TC *_h, unsigned int _n);                                          \
+    FIRFILT FIRFILT##_create_kaiser(unsigned int _n, float _fc, float _As, float _mu);          \
+    FIRFILT FIRFILT##_create_rect(unsigned int _n);                                             \
+    FIRFILT FIRFILT##_recreate(FIRFILT _q, TC *_h, unsigned int _n);                            \
+    void FIRFILT##_destroy(FIRFILT _q);                                                         \
+    void FIRFILT##_reset(FIRFILT _q);                                                           \
+    void FIRFILT##_print(FIRFILT _q);                                                           \
+    void FIRFILT##_set_scale(FIRFILT _q, TC _scale);                                            \
+    void FIRFILT##_push(FIRFILT _q, TI _x);                                                     \
+    void FIRFILT##_execute(FIRFILT _q, TO *_y);                                                 \
+    void FIRFILT##_execute_block(FIRFILT _q, TI *_x, unsigned int _n, TO *_y);                  \
+    unsigned int FIRFILT##_get_length(FIRFILT _q);                                              \
+    /* extension: device pointers (x == y allowed), asynchronous on the object's stream */      \
+    void FIRFILT##_execute_block_dev(FIRFILT _q, const TI *_dx, unsigned long long _n,          \
+                                     TO *_dy);                                                  \
+    void FIRFILT##_set_stream(FIRFILT _q, void *_hip_stream);                                   \
+    void *FIRFILT##_get_stream(FIRFILT _q);                                                     \
+    void FIRFILT##_synchronize(FIRFILT _q);
+
+LQMI_FIRFILT_API(firfilt_rrrf, float, float, float)
+LQMI_FIRFILT_API(firfilt_crcf, liquid_float_complex, float, liquid_float_complex)
+LQMI_FIRFILT_API(firfilt_cccf, liquid_float_complex, liquid_float_complex, liquid_float_complex)
+
+/* ------------------------------------------------------------------------ */
+/* firdecim (liquid.h:2664-2735): crcf                                       */
+/* ------------------------------------------------------------------------ */
+typedef struct firdecim_crcf_s *firdecim_crcf;
+firdecim_crcf firdecim_crcf_create(unsigned int _M, float *_h, unsigned int _h_len);
+firdecim_crcf firdecim_crcf_create_kaiser(unsigned int _M, unsigned int _m, float _As);
+void firdecim_crcf_destroy(firdecim_crcf _q);
+void firdecim_crcf_print(firdecim_crcf _q);
+void firdecim_crcf_clear(firdecim_crcf _q);
+void firdecim_crcf_execute(firdecim_crcf _q, liquid_float_complex *_x, liquid_float_complex *_y);
+void firdecim_crcf_execute_block(firdecim_crcf _q, liquid_float_complex *_x, unsigned int _n,
+                                 liquid_float_complex *_y);
+/* extension: _n = number of outputs; _dx holds _n*M samples (device) */
+void firdecim_crcf_execute_block_dev(firdecim_crcf _q, const liquid_float_complex *_dx,
+                                     unsigned long long _n, liquid_float_complex *_dy);
+void firdecim_crcf_set_stream(firdecim_crcf _q, void *_hip_stream);
+
+/* ------------------------------------------------------------------------ */
+/* firinterp (liquid.h:2496-2565): crcf                                      */
+/* ------------------------------------------------------------------------ */
+typedef struct firinterp_crcf_s *firinterp_crcf;
+firinterp_crcf firinterp_crcf_create(unsigned int _M, float *_h, unsigned int _h_len);
+firinterp_crcf firinterp_crcf_create_kaiser(unsigned int _M, unsigned int _m, float _As);
+void firinterp_crcf_destroy(firinterp_crcf _q);
+void firinterp_crcf_print(firinterp_crcf _q);
+void firinterp_crcf_reset(firinterp_crcf _q);
+void firinterp_crcf_execute(firinterp_crcf _q, liquid_float_complex _x, liquid_float_complex *_y);
+void firinterp_crcf_execute_block(firinterp_crcf _q, liquid_float_complex *_x, unsigned int _n,
+                                  liquid_float_complex *_y);
+/* extension: _n inputs -> _n*M outputs, device pointers */
+void firinterp_crcf_execute_block_dev(firinterp_crcf _q, const liquid_float_complex *_dx,
+                                      unsigned long long _n, liquid_float_complex *_dy);
+void firinterp_crcf_set_stream(firinterp_crcf _q, void *_hip_stream);
+
+/* ------------------------------------------------------------------------ */
+/* fftfilt (liquid.h:2192-2240): crcf                                        */
+/* ------------------------------------------------------------------------ */
+typedef struct fftfilt_crcf_s *fftfilt_crcf;
+fftfilt_crcf fftfilt_crcf_create(float *_h, unsigned int _h_len, unsigned int _n);
+void fftfilt_crcf_destroy(fftfilt_crcf _q);
+void fftfilt_crcf_reset(fftfilt_crcf _q);
+void fftfilt_crcf_print(fftfilt_crcf _q);
+void fftfilt_crcf_set_scale(fftfilt_crcf _q, float _scale);
+void fftfilt_crcf_execute(fftfilt_crcf _q, liquid_float_complex *_x, liquid_float_complex *_y);
+unsigned int fftfilt_crcf_get_length(fftfilt_crcf _q);
+/* extension: arbitrary-length stream (any _n), host / device pointers */
+void fftfilt_crcf_execute_block(fftfilt_crcf _q, liquid_float_complex *_x, unsigned long long _n,
+                                liquid_float_complex *_y);
+void fftfilt_crcf_execute_block_dev(fftfilt_crcf _q, const liquid_float_complex *_dx,
+                                    unsigned long long _n, liquid_float_complex *_dy);
+void fftfilt_crcf_set_stream(fftfilt_crcf _q, void *_hip_stream);
+
+/* ------------------------------------------------------------------------ */
+/* firpfbch (liquid.h:5667-5739): crcf                                       */
+/* ------------------------------------------------------------------------ */
+typedef struct firpfbch_crcf_s *firpfbch_crcf;
+firpfbch_crcf firpfbch_crcf_create(int _type, unsigned int _M, unsigned int _p, float *_h);
+firpfbch_crcf firpfbch_crcf_create_kaiser(int _type, unsigned int _M, unsigned int _m, float _As);
+void firpfbch_crcf_destroy(firpfbch_crcf _q);
+void firpfbch_crcf_reset(firpfbch_crcf _q);
+void firpfbch_crcf_print(firpfbch_crcf _q);
+void firpfbch_crcf_synthesizer_execute(firpfbch_crcf _q, liquid_float_complex *_x,
+                                       liquid_float_complex *_y);
+void firpfbch_crcf_analyzer_execute(firpfbch_crcf _q, liquid_float_complex *_x,
+                                    liquid_float_complex *_y);
+/* extension: _nblocks consecutive calls (M in, M out each), host / device pointers */
+void firpfbch_crcf_execute_block(firpfbch_crcf _q, liquid_float_complex *_x,
+                                 unsigned long long _nblocks, liquid_float_complex *_y);
+void firpfbch_crcf_execute_block_dev(firpfbch_crcf _q, const liquid_float_complex *_dx,
+                                     unsigned long long _nblocks, liquid_float_complex *_dy);
+void firpfbch_crcf_set_stream(firpfbch_crcf _q, void *_hip_stream);
+
+/* ------------------------------------------------------------------------ */
+/* firpfbch2 (liquid.h:5754-5799): crcf                                      */
+/* ------------------------------------------------------------------------ */
+typedef struct firpfbch2_crcf_s *firpfbch2_crcf;
+firpfbch2_crcf firpfbch2_crcf_create(int _type, unsigned int _M, unsigned int _m, float *_h);
+firpfbch2_crcf firpfbch2_crcf_create_kaiser(int _type, unsigned int _M, unsigned int _m, float _As);
+void firpfbch2_crcf_destroy(firpfbch2_crcf _q);
+void firpfbch2_crcf_reset(firpfbch2_crcf _q);
+void firpfbch2_crcf_print(firpfbch2_crcf _q);
+void firpfbch2_crcf_execute(firpfbch2_crcf _q, liquid_float_complex *_x, liquid_float_complex *_y);
+/* extension: _nblocks consecutive execute() calls.  analyzer: _x = _nblocks*M/2 inputs,
+ * _y = _nblocks*M outputs; synthesizer: _nblocks*M in, _nblocks*M/2 out */
+void firpfbch2_crcf_execute_block(firpfbch2_crcf _q, liquid_float_complex *_x,
+                                  unsigned long long _nblocks, liquid_float_complex *_y);
+void firpfbch2_crcf_execute_block_dev(firpfbch2_crcf _q, const liquid_float_complex *_dx,
+                                      unsigned long long _nblocks, liquid_float_complex *_dy);
+void firpfbch2_crcf_set_stream(firpfbch2_crcf _q, void *_hip_stream);
+void *firpfbch2_crcf_get_stream(firpfbch2_crcf _q);
+void firpfbch2_crcf_synchronize(firpfbch2_crcf _q);
+
+/* ------------------------------------------------------------------------ */
+/* runtime extensions                                                        */
+/* ------------------------------------------------------------------------ */
+/* device memory helpers for callers without their own HIP code */
+void *liquid_mi355x_malloc(unsigned long long _bytes);
+void liquid_mi355x_free(void *_p);
+void liquid_mi355x_memcpy_h2d(void *_dst, const void *_src, unsigned long long _bytes);
+void liquid_mi355x_memcpy_d2h(void *_dst, const void *_src, unsigned long long _bytes);
+void liquid_mi355x_device_synchronize(void);
+/* build identification (gfx target the kernels were compiled for) */
+const char *liquid_mi355x_build_target(void);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* LIQUID_MI355X_H */

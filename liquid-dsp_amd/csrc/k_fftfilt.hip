@@ -1,0 +1,111 @@
+// k_fftfilt.hip -- FFT fast convolution for fftfilt_{crcf,rrrf,cccf}.
+//
+// Reference: src/filter/src/fftfilt.c:193-260 runs overlap-ADD with a 2n-point
+// transform per n-sample call; its output is the causal linear convolution
+// y = s * (h * x) (verified against the oracle, tests/test_oracle.py).  Because
+// the result does not depend on the block geometry (up to rounding), the GPU
+// path uses overlap-SAVE with one fixed 4096-point transform per workgroup:
+// each workgroup loads 4096 inputs (its L = 4096 - (h-1) new samples plus the
+// h-1 sample halo), runs forward FFT -> multiply by H -> inverse FFT entirely
+// in LDS and writes its L outputs.  No state crosses workgroups, so every
+// segment of a long stream runs in parallel; between calls only the last h-1
+// inputs are carried.
+#include "lq_device.h"
+#include "lq_kernels.h"
+
+#include <cstdio>
+#include <cstdlib>
+
+namespace {
+
+constexpr int NT = 256;
+constexpr int NFFT = 4096;
+
+// kind 0: real input/output (rrrf), otherwise complex
+template <bool REAL>
+__global__ __launch_bounds__(NT) void k_fftfilt(int hm1, const float2 *__restrict__ H, const void *__restrict__ hist,
+                                                const void *__restrict__ xin, long long n, void *__restrict__ yout,
+                                                float sre, float sim, const float2 *__restrict__ tw)
+{
+    __shared__ __attribute__((aligned(16))) float2 a[NFFT];
+    __shared__ __attribute__((aligned(16))) float2 b[NFFT];
+    const int L = NFFT - hm1;
+    const long long s0 = (long long)blockIdx.x * L;
+    for (int u = threadIdx.x; u < NFFT; u += NT) {
+        const long long s = s0 - hm1 + u;
+        float2 v = make_float2(0.f, 0.f);
+        if (REAL) {
+            const float *x = (const float *)xin;
+            const float *hs = (const float *)hist;
+            if (s < 0) v.x = hs[hm1 + s];
+            else if (s < n) v.x = x[s];
+        } else {
+            const float2 *x = (const float2 *)xin;
+            const float2 *hs = (const float2 *)hist;
+            if (s < 0) v = hs[hm1 + s];
+            else if (s < n) v = x[s];
+        }
+        a[u] = v;
+    }
+    __syncthreads();
+    float2 *F = lds_fft<NFFT, 1, NT>(a, b, tw, +1);
+    for (int u = threadIdx.x; u < NFFT; u += NT) F[u] = cmul(F[u], H[u]);
+    __syncthreads();
+    float2 *other = (F == a) ? b : a;
+    float2 *T = lds_fft<NFFT, 1, NT>(F, other, tw, -1);
+    for (int k = threadIdx.x; k < L; k += NT) {
+        const long long t = s0 + k;
+        if (t >= n) break;
+        const float2 r = T[hm1 + k];
+        if (REAL) {
+            ((float *)yout)[t] = r.x * sre;
+        } else {
+            ((float2 *)yout)[t] = make_float2(r.x * sre - r.y * sim, r.x * sim + r.y * sre);
+        }
+    }
+}
+
+} // namespace
+
+extern "C" void lqk_fftfilt_run(int real_io, unsigned int hlen, const void *H, const void *hist, const void *x,
+                                unsigned long long n, void *y, float scale_re, float scale_im, void *stream)
+{
+    if (n == 0) return;
+    if (hlen < 1 || hlen - 1 >= NFFT / 2 + 1) {
+        fprintf(stderr, "error: fftfilt: filter length %u exceeds the GPU transform limit (%d)\n", hlen,
+                NFFT / 2 + 1);
+        exit(1);
+    }
+    hipStream_t st = (hipStream_t)stream;
+    const int hm1 = (int)hlen - 1;
+    const int L = NFFT - hm1;
+    const long long nseg = ((long long)n + L - 1) / L;
+    const float2 *tw = (const float2 *)lqrt_twiddles();
+    if (real_io)
+        hipLaunchKernelGGL(k_fftfilt<true>, dim3((unsigned)nseg), dim3(NT), 0, st, hm1, (const float2 *)H, hist, x,
+                           (long long)n, y, scale_re, scale_im, tw);
+    else
+        hipLaunchKernelGGL(k_fftfilt<false>, dim3((unsigned)nseg), dim3(NT), 0, st, hm1, (const float2 *)H, hist, x,
+                           (long long)n, y, scale_re, scale_im, tw);
+    LQ_CHECK_LAUNCH();
+}
+
+extern "C" unsigned int lqk_fftfilt_nfft(void) { return NFFT; }
+
+// H[k] = FFT_4096(h zero padded)  (h real or complex), computed on the device
+__global__ void k_pad_coef(const void *h, int hlen, int is_complex, float2 *buf)
+{
+    int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= NFFT) return;
+    float2 v = make_float2(0.f, 0.f);
+    if (i < hlen) v = is_complex ? ((const float2 *)h)[i] : make_float2(((const float *)h)[i], 0.f);
+    buf[i] = v;
+}
+
+extern "C" void lqk_fftfilt_make_H(const void *h_dev, unsigned int hlen, int is_complex, void *H, void *stream)
+{
+    hipStream_t st = (hipStream_t)stream;
+    hipLaunchKernelGGL(k_pad_coef, dim3(NFFT / 256), dim3(256), 0, st, h_dev, (int)hlen, is_complex, (float2 *)H);
+    LQ_CHECK_LAUNCH();
+    lqk_fft_batch(NFFT, +1, H, H, 1, stream);
+}

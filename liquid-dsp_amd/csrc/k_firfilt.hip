@@ -1,0 +1,408 @@
+// k_firfilt.hip -- streaming FIR kernels: firfilt, firdecim, firinterp, the
+// per-sample single-output path, and window (history) maintenance.
+//
+// Reference semantics restated (not translated):
+//   firfilt  src/filter/src/firfilt.c:297-359  y[t] = scale * sum_k h[k] x[t-k]
+//   firdecim src/filter/src/firdecim.c:189-223 y[o] = sum_k h[k] x[o*M - k]
+//   firinterp src/filter/src/firinterp.c:187-215 via firpfb.c:325-345
+//            y[i*M+p] = sum_l h'[p + l*M] x[i - l]
+// The reference walks a ring buffer one sample at a time; here every output is
+// independent: a workgroup stages one contiguous input tile (plus the h-1
+// sample halo) in LDS once, and each lane produces R consecutive outputs from
+// a sliding register window, with the coefficients in scalar registers
+// (uniform across the wave), so the inner loop is pure FMA.
+#include "lq_device.h"
+#include "lq_kernels.h"
+
+namespace {
+
+constexpr int NT = 256;      // threads per workgroup
+constexpr int R = 16;        // consecutive outputs per lane
+constexpr int TILE = NT * R; // outputs per workgroup
+
+template <int KIND>
+struct kt;
+template <>
+struct kt<0> {
+    typedef float T;
+    typedef float TC;
+};
+template <>
+struct kt<1> {
+    typedef float2 T;
+    typedef float TC;
+};
+template <>
+struct kt<2> {
+    typedef float2 T;
+    typedef float2 TC;
+};
+
+template <typename T>
+__device__ __forceinline__ T zero();
+template <>
+__device__ __forceinline__ float zero<float>() { return 0.0f; }
+template <>
+__device__ __forceinline__ float2 zero<float2>() { return make_float2(0.0f, 0.0f); }
+
+// acc += h * v for the three type combinations
+__device__ __forceinline__ void mac(float &acc, float h, float v) { acc = fmaf(h, v, acc); }
+__device__ __forceinline__ void mac(float2 &acc, float h, float2 v)
+{
+    acc.x = fmaf(h, v.x, acc.x);
+    acc.y = fmaf(h, v.y, acc.y);
+}
+__device__ __forceinline__ void mac(float2 &acc, float2 h, float2 v)
+{
+    acc.x = fmaf(h.x, v.x, acc.x);
+    acc.x = fmaf(-h.y, v.y, acc.x);
+    acc.y = fmaf(h.x, v.y, acc.y);
+    acc.y = fmaf(h.y, v.x, acc.y);
+}
+
+__device__ __forceinline__ float apply_scale(float a, float sre, float) { return a * sre; }
+__device__ __forceinline__ float2 apply_scale(float2 a, float sre, float sim)
+{
+    return make_float2(a.x * sre - a.y * sim, a.x * sim + a.y * sre);
+}
+__device__ __forceinline__ float2 apply_scale_real(float2 a, float s) { return make_float2(a.x * s, a.y * s); }
+
+__device__ __forceinline__ float vadd(float a, float b) { return a + b; }
+__device__ __forceinline__ float2 vadd(float2 a, float2 b) { return make_float2(a.x + b.x, a.y + b.y); }
+
+__host__ __device__ __forceinline__ int lds_idx(int u) { return u + (u >> 4); } // 1 pad slot per 16 samples
+
+// ------------------------------------------------------------------ firfilt
+// Grid: one workgroup per TILE outputs.  LDS holds samples [t0-HP, t0+TILE)
+// (HP = padded filter length) with one pad slot per 16 samples, so that the
+// 64 lanes of a wave, whose windows start 16 samples apart, hit 64 distinct
+// banks on every ds_read_b64.
+template <int KIND, int HC>
+__global__ __launch_bounds__(NT) void k_firfilt(const typename kt<KIND>::T *__restrict__ hist,
+                                                const typename kt<KIND>::T *x, long long n,
+                                                typename kt<KIND>::T *y,
+                                                const typename kt<KIND>::TC *__restrict__ hpad,
+                                                int nchunk, float sre, float sim,
+                                                const typename kt<KIND>::T *__restrict__ halo)
+{
+    typedef typename kt<KIND>::T T;
+    typedef typename kt<KIND>::TC TC;
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    T *tile = reinterpret_cast<T *>(smem);
+
+    const int HP = HC * nchunk;
+    const long long t0 = (long long)blockIdx.x * TILE;
+    const int S = TILE + HP;
+
+    for (int u = threadIdx.x; u < S; u += NT) {
+        const long long s = t0 - HP + u;
+        T v;
+        if (s < 0)
+            v = (s >= -(long long)(HP - 1)) ? hist[HP - 1 + s] : zero<T>();
+        else if (s >= n)
+            v = zero<T>();
+        else if (halo != nullptr && u < HP && blockIdx.x > 0)
+            v = halo[(size_t)blockIdx.x * HP + u];
+        else
+            v = x[s];
+        tile[lds_idx(u)] = v;
+    }
+    __syncthreads();
+
+    T acc[R];
+#pragma unroll
+    for (int r = 0; r < R; r++) acc[r] = zero<T>();
+
+    for (int c = 0; c < nchunk; c++) {
+        const TC *hc = hpad + c * HC;
+        // first window sample u = R*tid + HP - c*HC - HC + 1 = 16*(tid+q) + 1
+        const int q = (HP - c * HC - HC) >> 4;
+        const T *base = tile + 17 * (threadIdx.x + q);
+#pragma unroll
+        for (int d = 0; d < HC + R - 1; d++) {
+            const T v = base[(1 + d) + ((1 + d) >> 4)];
+#pragma unroll
+            for (int r = 0; r < R; r++) {
+                const int kk = r - d + HC - 1;
+                if (kk >= 0 && kk < HC) mac(acc[r], hc[kk], v);
+            }
+        }
+    }
+
+    const long long tb = t0 + (long long)R * threadIdx.x;
+#pragma unroll
+    for (int r = 0; r < R; r++)
+        if (tb + r < n) y[tb + r] = apply_scale(acc[r], sre, sim);
+}
+
+template <int KIND>
+__global__ void k_halo_copy(const typename kt<KIND>::T *x, long long n, int HP, long long ntiles,
+                            typename kt<KIND>::T *halo)
+{
+    long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+    long long tot = ntiles * HP;
+    if (i >= tot) return;
+    long long tile = i / HP;
+    int u = (int)(i - tile * HP);
+    if (tile == 0) return;
+    long long s = tile * TILE - HP + u;
+    halo[i] = (s >= 0 && s < n) ? x[s] : zero<typename kt<KIND>::T>();
+}
+
+// dst[i] = last L samples of (src ++ x[0..n))
+template <typename T>
+__global__ void k_window_append(const T *__restrict__ src, int L, const T *__restrict__ x, long long n,
+                                T *__restrict__ dst)
+{
+    int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= L) return;
+    long long j = (long long)i + n; // index into (src ++ x)
+    dst[i] = (j < L) ? src[j] : x[j - L];
+}
+
+// one output from the window (oldest first, HP samples): y = scale*sum_k h[k] win[HP-1-k]
+template <int KIND>
+__global__ void k_fir_single(const typename kt<KIND>::TC *__restrict__ hpad, int HP, int hlen,
+                             const typename kt<KIND>::T *__restrict__ win, float sre, float sim,
+                             typename kt<KIND>::T *y)
+{
+    typedef typename kt<KIND>::T T;
+    __shared__ T part[64];
+    T acc = zero<T>();
+    for (int k = threadIdx.x; k < hlen; k += 64) mac(acc, hpad[k], win[HP - 1 - k]);
+    part[threadIdx.x] = acc;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        T s = zero<T>();
+        for (int i = 0; i < 64; i++) s = vadd(s, part[i]);
+        y[0] = apply_scale(s, sre, sim);
+    }
+}
+
+// ------------------------------------------------------------------ firdecim
+// one output per lane; LDS tile covers [o0*M - (HP-1), (o0+NT)*M)
+template <int KIND>
+__global__ __launch_bounds__(NT) void k_firdecim(const typename kt<KIND>::T *__restrict__ hist,
+                                                 const typename kt<KIND>::T *__restrict__ x,
+                                                 long long nout, int M,
+                                                 typename kt<KIND>::T *__restrict__ y,
+                                                 const typename kt<KIND>::TC *__restrict__ hpad,
+                                                 int HP, int hlen)
+{
+    typedef typename kt<KIND>::T T;
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    T *tile = reinterpret_cast<T *>(smem);
+    const long long o0 = (long long)blockIdx.x * NT;
+    const long long s0 = o0 * M - (HP - 1);
+    const int S = NT * M + HP - 1;
+    const long long nin = nout * M;
+    for (int u = threadIdx.x; u < S; u += NT) {
+        long long s = s0 + u;
+        T v;
+        if (s < 0) v = hist[HP - 1 + s];
+        else if (s < nin) v = x[s];
+        else v = zero<T>();
+        tile[u] = v;
+    }
+    __syncthreads();
+    const long long o = o0 + threadIdx.x;
+    if (o >= nout) return;
+    // newest sample of output o is x[o*M] -> tile index (HP-1) + threadIdx.x*M
+    const T *w = tile + (HP - 1) + threadIdx.x * M;
+    T acc = zero<T>();
+    for (int k = 0; k < hlen; k++) mac(acc, hpad[k], w[-k]);
+    y[o] = acc;
+}
+
+// ------------------------------------------------------------------ firinterp
+// one input sample per lane -> M outputs; hpoly[p*L + l] = h'[p + l*M]
+template <int KIND>
+__global__ __launch_bounds__(NT) void k_firinterp(const typename kt<KIND>::T *__restrict__ hist,
+                                                  const typename kt<KIND>::T *__restrict__ x,
+                                                  long long n, int M, int L,
+                                                  const typename kt<KIND>::TC *__restrict__ hpoly,
+                                                  float scale, typename kt<KIND>::T *__restrict__ y)
+{
+    typedef typename kt<KIND>::T T;
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    T *tile = reinterpret_cast<T *>(smem);
+    const long long i0 = (long long)blockIdx.x * NT;
+    const int S = NT + L - 1;
+    for (int u = threadIdx.x; u < S; u += NT) {
+        long long s = i0 - (L - 1) + u;
+        T v;
+        if (s < 0) v = (L > 1) ? hist[L - 1 + s] : zero<T>();
+        else if (s < n) v = x[s];
+        else v = zero<T>();
+        tile[u] = v;
+    }
+    __syncthreads();
+    const long long i = i0 + threadIdx.x;
+    if (i >= n) return;
+    const T *w = tile + threadIdx.x + (L - 1); // w[-l] = x[i-l]
+    for (int p = 0; p < M; p++) {
+        T acc = zero<T>();
+        for (int l = 0; l < L; l++) mac(acc, hpoly[p * L + l], w[-l]);
+        y[i * M + p] = apply_scale(acc, scale, 0.0f);
+    }
+}
+
+template <int KIND, int HC>
+void launch_firfilt(const lqk_fir_desc *d, const void *hist, const void *x, long long n, void *y,
+                    const void *halo, hipStream_t st)
+{
+    typedef typename kt<KIND>::T T;
+    typedef typename kt<KIND>::TC TC;
+    const int HP = HC * (int)d->nchunk;
+    const long long ntiles = (n + TILE - 1) / TILE;
+    const size_t lds = (size_t)lds_idx(TILE + HP) * sizeof(T) + 16;
+    if (lds > 160 * 1024) {
+        fprintf(stderr, "error: firfilt: filter length %u exceeds the GPU tile limit\n", d->hlen);
+        exit(1);
+    }
+    hipLaunchKernelGGL((k_firfilt<KIND, HC>), dim3((unsigned)ntiles), dim3(NT), lds, st, (const T *)hist,
+                       (const T *)x, n, (T *)y, (const TC *)d->hpad, (int)d->nchunk, d->scale_re,
+                       d->scale_im, (const T *)halo);
+    LQ_CHECK_LAUNCH();
+}
+
+template <int KIND>
+void dispatch_firfilt(const lqk_fir_desc *d, const void *hist, const void *x, long long n, void *y,
+                      const void *halo, hipStream_t st)
+{
+    switch (d->hc) {
+    case 16: launch_firfilt<KIND, 16>(d, hist, x, n, y, halo, st); break;
+    case 32: launch_firfilt<KIND, 32>(d, hist, x, n, y, halo, st); break;
+    case 64: launch_firfilt<KIND, 64>(d, hist, x, n, y, halo, st); break;
+    default:
+        fprintf(stderr, "error: firfilt: invalid chunk class %u\n", d->hc);
+        exit(1);
+    }
+}
+
+size_t elem_size(int kind) { return kind == 0 ? sizeof(float) : sizeof(float2); }
+
+} // namespace
+
+extern "C" size_t lqk_firfilt_scratch_bytes(const lqk_fir_desc *d, unsigned long long n)
+{
+    const long long ntiles = ((long long)n + TILE - 1) / TILE;
+    return (size_t)ntiles * d->hc * d->nchunk * elem_size(d->kind);
+}
+
+extern "C" void lqk_firfilt(const lqk_fir_desc *d, const void *hist, const void *x, unsigned long long n,
+                            void *y, void *scratch, void *stream)
+{
+    if (n == 0) return;
+    hipStream_t st = (hipStream_t)stream;
+    const void *halo = nullptr;
+    if (x == y) {
+        // in place: save each tile's halo before any workgroup overwrites it
+        const int HP = (int)(d->hc * d->nchunk);
+        const long long ntiles = ((long long)n + TILE - 1) / TILE;
+        const long long tot = ntiles * HP;
+        const unsigned nb = (unsigned)((tot + 255) / 256);
+        if (d->kind == 0)
+            hipLaunchKernelGGL(k_halo_copy<0>, dim3(nb), dim3(256), 0, st, (const float *)x, (long long)n, HP,
+                               ntiles, (float *)scratch);
+        else
+            hipLaunchKernelGGL(k_halo_copy<1>, dim3(nb), dim3(256), 0, st, (const float2 *)x, (long long)n, HP,
+                               ntiles, (float2 *)scratch);
+        LQ_CHECK_LAUNCH();
+        halo = scratch;
+    }
+    switch (d->kind) {
+    case 0: dispatch_firfilt<0>(d, hist, x, (long long)n, y, halo, st); break;
+    case 1: dispatch_firfilt<1>(d, hist, x, (long long)n, y, halo, st); break;
+    case 2: dispatch_firfilt<2>(d, hist, x, (long long)n, y, halo, st); break;
+    }
+}
+
+extern "C" void lqk_window_append(int is_complex, const void *src_hist, unsigned int L, const void *x,
+                                  unsigned long long n, void *dst_hist, void *stream)
+{
+    if (L == 0) return;
+    hipStream_t st = (hipStream_t)stream;
+    unsigned nb = (L + 255) / 256;
+    if (is_complex)
+        hipLaunchKernelGGL(k_window_append<float2>, dim3(nb), dim3(256), 0, st, (const float2 *)src_hist,
+                           (int)L, (const float2 *)x, (long long)n, (float2 *)dst_hist);
+    else
+        hipLaunchKernelGGL(k_window_append<float>, dim3(nb), dim3(256), 0, st, (const float *)src_hist,
+                           (int)L, (const float *)x, (long long)n, (float *)dst_hist);
+    LQ_CHECK_LAUNCH();
+}
+
+extern "C" void lqk_fir_single(const lqk_fir_desc *d, const void *win, void *y, void *stream)
+{
+    hipStream_t st = (hipStream_t)stream;
+    const int HP = (int)(d->hc * d->nchunk);
+    switch (d->kind) {
+    case 0:
+        hipLaunchKernelGGL(k_fir_single<0>, dim3(1), dim3(64), 0, st, (const float *)d->hpad, HP, (int)d->hlen,
+                           (const float *)win, d->scale_re, d->scale_im, (float *)y);
+        break;
+    case 1:
+        hipLaunchKernelGGL(k_fir_single<1>, dim3(1), dim3(64), 0, st, (const float *)d->hpad, HP, (int)d->hlen,
+                           (const float2 *)win, d->scale_re, d->scale_im, (float2 *)y);
+        break;
+    case 2:
+        hipLaunchKernelGGL(k_fir_single<2>, dim3(1), dim3(64), 0, st, (const float2 *)d->hpad, HP, (int)d->hlen,
+                           (const float2 *)win, d->scale_re, d->scale_im, (float2 *)y);
+        break;
+    }
+    LQ_CHECK_LAUNCH();
+}
+
+extern "C" void lqk_firdecim(const lqk_fir_desc *d, unsigned int M, const void *hist, const void *x,
+                             unsigned long long nout, void *y, void *stream)
+{
+    if (nout == 0) return;
+    hipStream_t st = (hipStream_t)stream;
+    const int HP = (int)(d->hc * d->nchunk);
+    const unsigned nb = (unsigned)((nout + NT - 1) / NT);
+    const size_t lds = (size_t)(NT * M + HP) * elem_size(d->kind);
+    if (lds > 160 * 1024) {
+        fprintf(stderr, "error: firdecim: decimation/filter length exceeds the GPU tile limit\n");
+        exit(1);
+    }
+    switch (d->kind) {
+    case 0:
+        hipLaunchKernelGGL(k_firdecim<0>, dim3(nb), dim3(NT), lds, st, (const float *)hist, (const float *)x,
+                           (long long)nout, (int)M, (float *)y, (const float *)d->hpad, HP, (int)d->hlen);
+        break;
+    case 1:
+        hipLaunchKernelGGL(k_firdecim<1>, dim3(nb), dim3(NT), lds, st, (const float2 *)hist, (const float2 *)x,
+                           (long long)nout, (int)M, (float2 *)y, (const float *)d->hpad, HP, (int)d->hlen);
+        break;
+    case 2:
+        hipLaunchKernelGGL(k_firdecim<2>, dim3(nb), dim3(NT), lds, st, (const float2 *)hist, (const float2 *)x,
+                           (long long)nout, (int)M, (float2 *)y, (const float2 *)d->hpad, HP, (int)d->hlen);
+        break;
+    }
+    LQ_CHECK_LAUNCH();
+}
+
+extern "C" void lqk_firinterp(int kind, const void *hpoly, unsigned int M, unsigned int L, float scale,
+                              const void *hist, const void *x, unsigned long long n, void *y, void *stream)
+{
+    if (n == 0) return;
+    hipStream_t st = (hipStream_t)stream;
+    const unsigned nb = (unsigned)((n + NT - 1) / NT);
+    const size_t lds = (size_t)(NT + L) * elem_size(kind);
+    switch (kind) {
+    case 0:
+        hipLaunchKernelGGL(k_firinterp<0>, dim3(nb), dim3(NT), lds, st, (const float *)hist, (const float *)x,
+                           (long long)n, (int)M, (int)L, (const float *)hpoly, scale, (float *)y);
+        break;
+    case 1:
+        hipLaunchKernelGGL(k_firinterp<1>, dim3(nb), dim3(NT), lds, st, (const float2 *)hist, (const float2 *)x,
+                           (long long)n, (int)M, (int)L, (const float *)hpoly, scale, (float2 *)y);
+        break;
+    case 2:
+        hipLaunchKernelGGL(k_firinterp<2>, dim3(nb), dim3(NT), lds, st, (const float2 *)hist, (const float2 *)x,
+                           (long long)n, (int)M, (int)L, (const float2 *)hpoly, scale, (float2 *)y);
+        break;
+    }
+    LQ_CHECK_LAUNCH();
+}

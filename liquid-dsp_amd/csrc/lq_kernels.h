@@ -1,0 +1,115 @@
+/*
+ * lq_kernels.h -- the thin C-ABI between the C host objects (host/ *.c) and the
+ * hand-written HIP kernels (csrc/ *.hip).  Plain pointers and sizes only.
+ *
+ * Device pointers are `void *` (complex samples are interleaved float pairs,
+ * 8 bytes).  Every launcher enqueues on the given HIP stream and returns
+ * immediately; errors abort with a message (lqrt_check).
+ */
+#ifndef LQ_KERNELS_H
+#define LQ_KERNELS_H
+
+#include <stddef.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* ---------------------------------------------------------------- runtime */
+void   lqrt_require_device(const char *who);    /* abort if no usable GPU */
+void  *lqrt_malloc(size_t bytes);               /* device memory, zeroed   */
+void   lqrt_free(void *p);
+void  *lqrt_host_alloc(size_t bytes);           /* pinned host memory      */
+void   lqrt_host_free(void *p);
+void  *lqrt_stream_create(void);
+void   lqrt_stream_destroy(void *s);
+void   lqrt_h2d(void *dst, const void *src, size_t bytes, void *stream);
+void   lqrt_d2h(void *dst, const void *src, size_t bytes, void *stream);
+void   lqrt_d2d(void *dst, const void *src, size_t bytes, void *stream);
+void   lqrt_memset(void *dst, size_t bytes, void *stream);
+void   lqrt_sync(void *stream);
+int    lqrt_is_device_ptr(const void *p);
+const float *lqrt_twiddles(void);               /* W_4096^e = exp(-2 pi i e/4096), e<4096 */
+
+/* ---------------------------------------------------------------- dotprod
+ * Y[v] = sum_i h[i] X[v*stride + i], v < nvec.  kind: 0 rrrf, 1 crcf, 2 cccf */
+void lqk_dotprod_batch(int kind, const void *h, unsigned int n, const void *X,
+                       unsigned long long stride, unsigned long long nvec, void *Y, void *stream);
+
+/* ---------------------------------------------------------------- firfilt
+ * Streaming FIR: y[i] = scale * sum_{k<hlen} h[k] ext[i-k], where ext[t] = x[t]
+ * for t >= 0 and hist[hlen-1+t] for t < 0 (hist holds the previous hlen-1
+ * inputs, oldest first).  hpad: coefficients in natural order, zero padded to
+ * nchunk*hc.  kind: 0 rrrf, 1 crcf, 2 cccf.  x == y allowed (in-place). */
+typedef struct {
+    int kind;
+    unsigned int hlen;       /* logical length */
+    unsigned int hc;         /* compile-time chunk class: 8,16,32,64 */
+    unsigned int nchunk;     /* padded length = hc*nchunk */
+    const void *hpad;        /* device coefficients (float or float2) */
+    float scale_re, scale_im;
+} lqk_fir_desc;
+
+void lqk_firfilt(const lqk_fir_desc *d, const void *hist, const void *x, unsigned long long n,
+                 void *y, void *scratch, void *stream);
+/* bytes of scratch lqk_firfilt needs for an in-place call of n samples */
+size_t lqk_firfilt_scratch_bytes(const lqk_fir_desc *d, unsigned long long n);
+
+/* window maintenance: dst[0..L) = last L samples of (src_hist[0..L) ++ x[0..n)) */
+void lqk_window_append(int is_complex, const void *src_hist, unsigned int L, const void *x,
+                       unsigned long long n, void *dst_hist, void *stream);
+
+/* one output of a dot product of hr (reversed coefficients, hlen) against
+ * win (oldest first), times scale: the per-sample firfilt_execute() path */
+void lqk_fir_single(const lqk_fir_desc *d, const void *win, void *y, void *stream);
+
+/* ---------------------------------------------------------------- firdecim / firinterp
+ * decim: y[o] = sum_k h[k] ext[o*M + phase - k]  (o < nout)
+ * interp: y[i*M + p] = scale * sum_{l<L} h[p + l*M] ext[i - l]  (i < n) */
+void lqk_firdecim(const lqk_fir_desc *d, unsigned int M, const void *hist, const void *x,
+                  unsigned long long nout, void *y, void *stream);
+void lqk_firinterp(int kind, const void *hpoly /* M x L, h[p + l*M] */, unsigned int M,
+                   unsigned int L, float scale, const void *hist, const void *x,
+                   unsigned long long n, void *y, void *stream);
+
+/* ---------------------------------------------------------------- firpfbch2 analyzer
+ * nblocks consecutive analyzer blocks over x (nblocks*M/2 samples); hist holds
+ * the previous 2*m*M - M/2 inputs; p0 = parity of the first block.
+ * hsub: M x 2m table, hsub[i*2m + n] = h[i + n*M].  Y: nblocks x M, already
+ * divided by M (firpfbch2.c:277-278). */
+void lqk_firpfbch2_analyzer(unsigned int M, unsigned int m, const void *hsub, const void *hist,
+                            const void *x, unsigned long long nblocks, int p0, void *Y,
+                            void *stream);
+/* synthesizer: nblocks x M channel inputs -> nblocks x M/2 outputs.
+ * state: the previous 4m-1 IFFT vectors (M each), zscratch (4m-1+nblocks)*M;
+ * see csrc/k_channelizer.hip */
+void lqk_firpfbch2_synthesizer(unsigned int M, unsigned int m, const void *hsub_syn,
+                               void *state, void *zscratch, const void *X,
+                               unsigned long long nblocks, int p0, void *Y, void *stream);
+
+/* ---------------------------------------------------------------- firpfbch (critically sampled)
+ * analyzer: block b consumes x[bM .. bM+M); window i receives x[bM + M-1-i]
+ * X[M-1-i] = sum_n h[i + n*M] win_i, Y = FFT_forward(X).  hsub[i*p + n] = h[i+n*M] */
+void lqk_firpfbch_analyzer(unsigned int M, unsigned int p, const void *hsub, const void *hist,
+                           const void *x, unsigned long long nblocks, void *Y, void *stream);
+void lqk_firpfbch_synthesizer(unsigned int M, unsigned int p, const void *hsub, void *state,
+                              void *zscratch, const void *X, unsigned long long nblocks, void *y,
+                              void *stream);
+
+/* ---------------------------------------------------------------- FFT / fftfilt */
+/* batched complex FFT of power-of-two size n (2..4096): dir +1 forward, -1 backward */
+void lqk_fft_batch(unsigned int n, int dir, const void *x, void *y, unsigned long long batch,
+                   void *stream);
+/* overlap-save fast convolution (fixed 4096-point transform, hlen <= 2049):
+ * y[t] = scale * sum_k h[k] ext[t-k], t < n; H = FFT_4096(h zero padded) (unscaled);
+ * scale = user scale / 4096; hist = previous hlen-1 inputs.  x must not alias y. */
+void lqk_fftfilt_run(int real_io, unsigned int hlen, const void *H, const void *hist, const void *x,
+                     unsigned long long n, void *y, float scale_re, float scale_im, void *stream);
+void lqk_fftfilt_make_H(const void *h_dev, unsigned int hlen, int is_complex, void *H, void *stream);
+unsigned int lqk_fftfilt_nfft(void);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif

@@ -1,0 +1,146 @@
+// lq_runtime.hip -- device, stream and memory plumbing behind the C-ABI.
+//
+// The reference reports every error by fprintf(stderr) + exit(1)
+// (e.g. src/filter/src/firfilt.c:66-69); HIP failures here do the same with
+// the HIP error string, so a missing or broken GPU fails loudly -- there is no
+// CPU fallback anywhere in this library.
+#include <hip/hip_runtime.h>
+
+#include <cmath>
+#include <cstdio>
+#include <cstdlib>
+#include <mutex>
+
+#include "lq_kernels.h"
+#include "lq_device.h"
+
+void lq_check(hipError_t e, const char *what, const char *file, int line)
+{
+    if (e != hipSuccess) {
+        fprintf(stderr, "error: liquid-mi355x: %s failed at %s:%d: %s\n", what, file, line,
+                hipGetErrorString(e));
+        exit(1);
+    }
+}
+
+extern "C" void lqrt_require_device(const char *who)
+{
+    static int checked = 0;
+    if (checked) return;
+    int n = 0;
+    hipError_t e = hipGetDeviceCount(&n);
+    if (e != hipSuccess || n == 0) {
+        fprintf(stderr,
+                "error: %s: no HIP device available (liquid-mi355x runs the filter path on the GPU "
+                "only; there is no CPU fallback)\n",
+                who ? who : "liquid-mi355x");
+        exit(1);
+    }
+    checked = 1;
+}
+
+extern "C" void *lqrt_malloc(size_t bytes)
+{
+    lqrt_require_device("lqrt_malloc");
+    void *p = nullptr;
+    if (bytes == 0) bytes = 16;
+    LQ_CHECK(hipMalloc(&p, bytes));
+    LQ_CHECK(hipMemset(p, 0, bytes));
+    return p;
+}
+
+extern "C" void lqrt_free(void *p)
+{
+    if (p) LQ_CHECK(hipFree(p));
+}
+
+extern "C" void *lqrt_host_alloc(size_t bytes)
+{
+    lqrt_require_device("lqrt_host_alloc");
+    void *p = nullptr;
+    if (bytes == 0) bytes = 16;
+    LQ_CHECK(hipHostMalloc(&p, bytes, hipHostMallocDefault));
+    return p;
+}
+
+extern "C" void lqrt_host_free(void *p)
+{
+    if (p) LQ_CHECK(hipHostFree(p));
+}
+
+extern "C" void *lqrt_stream_create(void)
+{
+    lqrt_require_device("lqrt_stream_create");
+    hipStream_t s;
+    LQ_CHECK(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
+    return (void *)s;
+}
+
+extern "C" void lqrt_stream_destroy(void *s)
+{
+    if (s) LQ_CHECK(hipStreamDestroy((hipStream_t)s));
+}
+
+extern "C" void lqrt_h2d(void *dst, const void *src, size_t bytes, void *stream)
+{
+    if (!bytes) return;
+    LQ_CHECK(hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, (hipStream_t)stream));
+}
+
+extern "C" void lqrt_d2h(void *dst, const void *src, size_t bytes, void *stream)
+{
+    if (!bytes) return;
+    LQ_CHECK(hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToHost, (hipStream_t)stream));
+}
+
+extern "C" void lqrt_d2d(void *dst, const void *src, size_t bytes, void *stream)
+{
+    if (!bytes) return;
+    LQ_CHECK(hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToDevice, (hipStream_t)stream));
+}
+
+extern "C" void lqrt_memset(void *dst, size_t bytes, void *stream)
+{
+    if (!bytes) return;
+    LQ_CHECK(hipMemsetAsync(dst, 0, bytes, (hipStream_t)stream));
+}
+
+extern "C" void lqrt_sync(void *stream)
+{
+    LQ_CHECK(hipStreamSynchronize((hipStream_t)stream));
+}
+
+extern "C" int lqrt_is_device_ptr(const void *p)
+{
+    hipPointerAttribute_t a;
+    if (hipPointerGetAttributes(&a, p) != hipSuccess) {
+        (void)hipGetLastError();
+        return 0;
+    }
+    return a.type == hipMemoryTypeDevice;
+}
+
+// One twiddle table per device: W_4096^e = exp(-2*pi*i*e/4096), computed in
+// double on the host and rounded once to float.  Every power-of-two transform
+// up to 4096 points indexes it with stride 4096/N.
+extern "C" const float *lqrt_twiddles(void)
+{
+    static std::mutex mu;
+    static float *tables[64] = {nullptr};
+    int dev = 0;
+    LQ_CHECK(hipGetDevice(&dev));
+    std::lock_guard<std::mutex> g(mu);
+    if (!tables[dev]) {
+        float h[2 * LQ_TW_N];
+        for (int e = 0; e < LQ_TW_N; e++) {
+            double a = -2.0 * M_PI * (double)e / (double)LQ_TW_N;
+            h[2 * e] = (float)cos(a);
+            h[2 * e + 1] = (float)sin(a);
+        }
+        float *d = nullptr;
+        LQ_CHECK(hipMalloc(&d, sizeof(h)));
+        LQ_CHECK(hipMemcpy(d, h, sizeof(h), hipMemcpyHostToDevice));
+        tables[dev] = d;
+    }
+    return tables[dev];
+}

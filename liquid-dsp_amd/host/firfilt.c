@@ -1,0 +1,291 @@
+/*
+ * firfilt.c -- firfilt_{rrrf,crcf,cccf} on the MI355X.
+ *
+ * API and semantics: include/liquid.h:1985-2090, src/filter/src/firfilt.c:62-404
+ *   y[t] = scale * sum_{k<h} h[k] x[t-k], zero initial history;
+ *   push() appends one sample, execute() reads the current window without
+ *   pushing, execute_block() = push+execute per sample (in place allowed).
+ *
+ * State model.  The filter state is the window of the last HP samples
+ * (HP = length padded to the kernel's chunk class), oldest first, kept on
+ * the device (two ping-pong buffers) with a host mirror for the per-sample
+ * push() path.  Exactly one copy is authoritative at a time; the other is
+ * refreshed lazily.  Every output sample, including the per-sample
+ * execute(), is computed by a HIP kernel.
+ */
+#include <complex.h>
+
+#include "lq_host.h"
+
+struct lq_firfilt_s {
+    int kind;
+    unsigned int hlen, HP;
+    size_t esz;        /* sample size: 4 (rrrf) or 8 */
+    size_t csz;        /* coefficient size: 4 or 8 (cccf) */
+    float *h;          /* natural-order coefficients (host copy) */
+    void *d_hpad;      /* device, zero padded to HP */
+    lqk_fir_desc d;
+    void *d_win[2];    /* device windows, HP samples each */
+    int cur;
+    unsigned char *h_win; /* host mirror */
+    int host_valid, dev_valid;
+    lq_ctx ctx;
+    lq_devbuf xbuf, ybuf, scratch, one;
+};
+
+static void lq_firfilt_layout(lq_firfilt *q, unsigned int n)
+{
+    q->hlen = n;
+    if (n <= 16) {
+        q->d.hc = 16;
+        q->d.nchunk = 1;
+    } else if (n <= 32) {
+        q->d.hc = 32;
+        q->d.nchunk = 1;
+    } else {
+        q->d.hc = 64;
+        q->d.nchunk = (n + 63) / 64;
+    }
+    q->HP = q->d.hc * q->d.nchunk;
+    q->d.hlen = n;
+}
+
+static void lq_firfilt_alloc_state(lq_firfilt *q)
+{
+    q->d_hpad = lqrt_malloc((size_t)q->HP * q->csz);
+    q->d_win[0] = lqrt_malloc((size_t)q->HP * q->esz);
+    q->d_win[1] = lqrt_malloc((size_t)q->HP * q->esz);
+    q->h_win = (unsigned char *)lq_xmalloc((size_t)q->HP * q->esz);
+    q->cur = 0;
+    q->host_valid = q->dev_valid = 1;
+}
+
+static void lq_firfilt_free_state(lq_firfilt *q)
+{
+    lqrt_free(q->d_hpad);
+    lqrt_free(q->d_win[0]);
+    lqrt_free(q->d_win[1]);
+    free(q->h_win);
+}
+
+static void lq_firfilt_upload_coefs(lq_firfilt *q)
+{
+    size_t bytes = (size_t)q->HP * q->csz;
+    unsigned char *pad = (unsigned char *)lq_xmalloc(bytes);
+    memcpy(pad, q->h, (size_t)q->hlen * q->csz);
+    lqrt_h2d(q->d_hpad, pad, bytes, q->ctx.stream);
+    lqrt_sync(q->ctx.stream);
+    free(pad);
+    q->d.hpad = q->d_hpad;
+}
+
+lq_firfilt *lq_firfilt_create(int kind, const float *h, unsigned int n, const char *who)
+{
+    if (n == 0) LQ_FAIL("error: %s_create(), filter length must be greater than zero\n", who);
+    lqrt_require_device(who);
+    lq_firfilt *q = (lq_firfilt *)lq_xmalloc(sizeof(*q));
+    q->kind = kind;
+    q->esz = kind == LQ_RRRF ? sizeof(float) : 2 * sizeof(float);
+    q->csz = kind == LQ_CCCF ? 2 * sizeof(float) : sizeof(float);
+    q->d.kind = kind;
+    q->d.scale_re = 1.0f;
+    q->d.scale_im = 0.0f;
+    lq_firfilt_layout(q, n);
+    q->h = (float *)lq_xmalloc((size_t)n * q->csz);
+    memcpy(q->h, h, (size_t)n * q->csz);
+    lq_ctx_init(&q->ctx);
+    lq_firfilt_alloc_state(q);
+    lq_firfilt_upload_coefs(q);
+    return q;
+}
+
+/* src/filter/src/firfilt.c:201-237: new taps; a length change restarts the
+ * buffer (the reference leaves it uninitialised; here it is cleared) */
+lq_firfilt *lq_firfilt_recreate(lq_firfilt *q, const float *h, unsigned int n)
+{
+    if (n == 0) LQ_FAIL("error: firfilt_recreate(), filter length must be greater than zero\n");
+    lqrt_sync(q->ctx.stream);
+    if (n != q->hlen) {
+        lq_firfilt_free_state(q);
+        lq_firfilt_layout(q, n);
+        free(q->h);
+        q->h = (float *)lq_xmalloc((size_t)n * q->csz);
+        lq_firfilt_alloc_state(q);
+    }
+    memcpy(q->h, h, (size_t)n * q->csz);
+    lq_firfilt_upload_coefs(q);
+    return q;
+}
+
+void lq_firfilt_destroy(lq_firfilt *q)
+{
+    lqrt_sync(q->ctx.stream);
+    lq_firfilt_free_state(q);
+    lq_devbuf_free(&q->xbuf);
+    lq_devbuf_free(&q->ybuf);
+    lq_devbuf_free(&q->scratch);
+    lq_devbuf_free(&q->one);
+    lq_ctx_free(&q->ctx);
+    free(q->h);
+    free(q);
+}
+
+void lq_firfilt_reset(lq_firfilt *q)
+{
+    lqrt_memset(q->d_win[0], (size_t)q->HP * q->esz, q->ctx.stream);
+    lqrt_memset(q->d_win[1], (size_t)q->HP * q->esz, q->ctx.stream);
+    lqrt_sync(q->ctx.stream);
+    memset(q->h_win, 0, (size_t)q->HP * q->esz);
+    q->host_valid = q->dev_valid = 1;
+}
+
+void lq_firfilt_print(lq_firfilt *q)
+{
+    static const char *ext[] = {"rrrf", "crcf", "cccf"};
+    printf("firfilt_%s:\n", ext[q->kind]);
+    for (unsigned int i = 0; i < q->hlen; i++) {
+        if (q->kind == LQ_CCCF)
+            printf("  h(%3u) = %12.8f + j*%12.8f\n", i + 1, q->h[2 * i], q->h[2 * i + 1]);
+        else
+            printf("  h(%3u) = %12.8f\n", i + 1, q->h[i]);
+    }
+    if (q->kind == LQ_CCCF)
+        printf("  scale = %12.8f + j*%12.8f\n", q->d.scale_re, q->d.scale_im);
+    else
+        printf("  scale = %12.8f\n", q->d.scale_re);
+}
+
+void lq_firfilt_set_scale(lq_firfilt *q, float re, float im)
+{
+    q->d.scale_re = re;
+    q->d.scale_im = im;
+}
+
+static void lq_firfilt_need_host(lq_firfilt *q)
+{
+    if (q->host_valid) return;
+    lqrt_d2h(q->h_win, q->d_win[q->cur], (size_t)q->HP * q->esz, q->ctx.stream);
+    lqrt_sync(q->ctx.stream);
+    q->host_valid = 1;
+}
+
+static void lq_firfilt_need_dev(lq_firfilt *q)
+{
+    if (q->dev_valid) return;
+    lqrt_h2d(q->d_win[q->cur], q->h_win, (size_t)q->HP * q->esz, q->ctx.stream);
+    q->dev_valid = 1;
+}
+
+void lq_firfilt_push(lq_firfilt *q, const void *x)
+{
+    lq_firfilt_need_host(q);
+    memmove(q->h_win, q->h_win + q->esz, (size_t)(q->HP - 1) * q->esz);
+    memcpy(q->h_win + (size_t)(q->HP - 1) * q->esz, x, q->esz);
+    q->dev_valid = 0;
+}
+
+void lq_firfilt_execute(lq_firfilt *q, void *y)
+{
+    lq_firfilt_need_dev(q);
+    void *dy = lq_devbuf_get(&q->one, 16);
+    lqk_fir_single(&q->d, q->d_win[q->cur], dy, q->ctx.stream);
+    lqrt_d2h(y, dy, q->esz, q->ctx.stream);
+    lqrt_sync(q->ctx.stream);
+}
+
+/* device-resident block: window update first (reads x before an in-place
+ * overwrite), then the filter kernel on the old window's last HP-1 samples */
+void lq_firfilt_execute_block_dev(lq_firfilt *q, const void *dx, unsigned long long n, void *dy)
+{
+    if (n == 0) return;
+    lq_firfilt_need_dev(q);
+    void *wold = q->d_win[q->cur];
+    void *wnew = q->d_win[q->cur ^ 1];
+    lqk_window_append(q->kind != LQ_RRRF, wold, q->HP, dx, n, wnew, q->ctx.stream);
+    void *scr = NULL;
+    if (dx == dy) scr = lq_devbuf_get(&q->scratch, lqk_firfilt_scratch_bytes(&q->d, n));
+    lqk_firfilt(&q->d, (const unsigned char *)wold + q->esz, dx, n, dy, scr, q->ctx.stream);
+    q->cur ^= 1;
+    q->host_valid = 0;
+}
+
+void lq_firfilt_execute_block(lq_firfilt *q, const void *x, unsigned long long n, void *y)
+{
+    if (n == 0) return;
+    size_t bytes = (size_t)n * q->esz;
+    void *dx = lq_devbuf_get(&q->xbuf, bytes);
+    void *dy = lq_devbuf_get(&q->ybuf, bytes);
+    lqrt_h2d(dx, x, bytes, q->ctx.stream);
+    lq_firfilt_execute_block_dev(q, dx, n, dy);
+    lqrt_d2h(y, dy, bytes, q->ctx.stream);
+    lqrt_sync(q->ctx.stream);
+}
+
+unsigned int lq_firfilt_get_length(lq_firfilt *q) { return q->hlen; }
+lq_ctx *lq_firfilt_ctx(lq_firfilt *q) { return &q->ctx; }
+
+/* ----------------------------------------------------------------- typed front ends */
+
+#define LQ_FIRFILT_FRONT(NAME, KIND, TO, TC, TI, SCALE_RE, SCALE_IM)                                \
+    struct NAME##_s {                                                                               \
+        lq_firfilt *f;                                                                              \
+    };                                                                                              \
+    NAME NAME##_create(TC *_h, unsigned int _n)                                                     \
+    {                                                                                               \
+        NAME q = (NAME)lq_xmalloc(sizeof(*q));                                                      \
+        q->f = lq_firfilt_create(KIND, (const float *)_h, _n, #NAME);                               \
+        return q;                                                                                   \
+    }                                                                                               \
+    NAME NAME##_create_kaiser(unsigned int _n, float _fc, float _As, float _mu)                     \
+    {                                                                                               \
+        if (_n == 0) LQ_FAIL("error: " #NAME "_create_kaiser(), filter length must be greater than zero\n"); \
+        float *hf = (float *)lq_xmalloc(_n * sizeof(float));                                        \
+        TC *hc = (TC *)lq_xmalloc(_n * sizeof(TC));                                                 \
+        lq_firdes_kaiser(_n, _fc, _As, _mu, hf);                                                    \
+        for (unsigned int i = 0; i < _n; i++) hc[i] = (TC)hf[i];                                    \
+        NAME q = NAME##_create(hc, _n);                                                             \
+        free(hf);                                                                                   \
+        free(hc);                                                                                   \
+        return q;                                                                                   \
+    }                                                                                               \
+    NAME NAME##_create_rect(unsigned int _n)                                                        \
+    {                                                                                               \
+        if (_n == 0 || _n > 1024) LQ_FAIL("error: " #NAME "_create_rect(), filter length must be in [1,1024]\n"); \
+        TC *hc = (TC *)lq_xmalloc(_n * sizeof(TC));                                                 \
+        for (unsigned int i = 0; i < _n; i++) hc[i] = (TC)1.0f;                                     \
+        NAME q = NAME##_create(hc, _n);                                                             \
+        free(hc);                                                                                   \
+        return q;                                                                                   \
+    }                                                                                               \
+    NAME NAME##_recreate(NAME _q, TC *_h, unsigned int _n)                                          \
+    {                                                                                               \
+        _q->f = lq_firfilt_recreate(_q->f, (const float *)_h, _n);                                  \
+        return _q;                                                                                  \
+    }                                                                                               \
+    void NAME##_destroy(NAME _q)                                                                    \
+    {                                                                                               \
+        lq_firfilt_destroy(_q->f);                                                                  \
+        free(_q);                                                                                   \
+    }                                                                                               \
+    void NAME##_reset(NAME _q) { lq_firfilt_reset(_q->f); }                                         \
+    void NAME##_print(NAME _q) { lq_firfilt_print(_q->f); }                                         \
+    void NAME##_set_scale(NAME _q, TC _scale) { lq_firfilt_set_scale(_q->f, SCALE_RE, SCALE_IM); }  \
+    void NAME##_push(NAME _q, TI _x) { lq_firfilt_push(_q->f, &_x); }                               \
+    void NAME##_execute(NAME _q, TO *_y) { lq_firfilt_execute(_q->f, _y); }                         \
+    void NAME##_execute_block(NAME _q, TI *_x, unsigned int _n, TO *_y)                             \
+    {                                                                                               \
+        lq_firfilt_execute_block(_q->f, _x, _n, _y);                                                \
+    }                                                                                               \
+    unsigned int NAME##_get_length(NAME _q) { return lq_firfilt_get_length(_q->f); }                \
+    void NAME##_execute_block_dev(NAME _q, const TI *_dx, unsigned long long _n, TO *_dy)           \
+    {                                                                                               \
+        lq_firfilt_execute_block_dev(_q->f, _dx, _n, _dy);                                          \
+    }                                                                                               \
+    void NAME##_set_stream(NAME _q, void *_s) { lq_ctx_set_stream(lq_firfilt_ctx(_q->f), _s); }     \
+    void *NAME##_get_stream(NAME _q) { return lq_firfilt_ctx(_q->f)->stream; }                      \
+    void NAME##_synchronize(NAME _q) { lqrt_sync(lq_firfilt_ctx(_q->f)->stream); }
+
+LQ_FIRFILT_FRONT(firfilt_rrrf, LQ_RRRF, float, float, float, _scale, 0.0f)
+LQ_FIRFILT_FRONT(firfilt_crcf, LQ_CRCF, liquid_float_complex, float, liquid_float_complex, _scale, 0.0f)
+LQ_FIRFILT_FRONT(firfilt_cccf, LQ_CCCF, liquid_float_complex, liquid_float_complex, liquid_float_complex,
+                 crealf(_scale), cimagf(_scale))

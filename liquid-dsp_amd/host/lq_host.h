@@ -1,0 +1,83 @@
+/*
+ * lq_host.h -- internal helpers shared by the C host objects.
+ *
+ * The objects keep the reference's create/execute/destroy contract
+ * (include/liquid.h) and its failure style (message on stderr, exit(1)).
+ * All sample arithmetic happens in the HIP kernels behind csrc/lq_kernels.h;
+ * the host side only designs coefficients (create time, as the reference
+ * does), validates arguments, moves buffers and tracks per-object state.
+ */
+#ifndef LQ_HOST_H
+#define LQ_HOST_H
+
+#include <stddef.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include "../csrc/lq_kernels.h"
+#include "liquid_mi355x.h"
+
+#define LQ_FAIL(...)                                                                               \
+    do {                                                                                           \
+        fprintf(stderr, __VA_ARGS__);                                                              \
+        exit(1);                                                                                   \
+    } while (0)
+
+/* sample kinds (also the kernel `kind` codes) */
+enum { LQ_RRRF = 0, LQ_CRCF = 1, LQ_CCCF = 2 };
+
+/* grow-on-demand device buffer */
+typedef struct {
+    void *p;
+    size_t cap;
+} lq_devbuf;
+
+void *lq_devbuf_get(lq_devbuf *b, size_t bytes);
+void lq_devbuf_free(lq_devbuf *b);
+
+/* per-object execution context: a HIP stream (owned unless supplied) */
+typedef struct {
+    void *stream;
+    int own;
+} lq_ctx;
+
+void lq_ctx_init(lq_ctx *c);
+void lq_ctx_free(lq_ctx *c);
+void lq_ctx_set_stream(lq_ctx *c, void *stream);
+
+void *lq_xmalloc(size_t bytes);
+unsigned int lq_msb_index(unsigned int x);
+int lq_is_pow2(unsigned int x);
+
+/* host-side design routines (create time only; src/filter/src/firdes.c) */
+float lq_kaiser_beta_As(float As);
+void lq_firdes_kaiser(unsigned int n, float fc, float As, float mu, float *h);
+
+/* generic firfilt engine used by the three typed front ends */
+typedef struct lq_firfilt_s lq_firfilt;
+lq_firfilt *lq_firfilt_create(int kind, const float *h, unsigned int n, const char *who);
+lq_firfilt *lq_firfilt_recreate(lq_firfilt *q, const float *h, unsigned int n);
+void lq_firfilt_destroy(lq_firfilt *q);
+void lq_firfilt_reset(lq_firfilt *q);
+void lq_firfilt_print(lq_firfilt *q);
+void lq_firfilt_set_scale(lq_firfilt *q, float re, float im);
+void lq_firfilt_push(lq_firfilt *q, const void *x);
+void lq_firfilt_execute(lq_firfilt *q, void *y);
+void lq_firfilt_execute_block(lq_firfilt *q, const void *x, unsigned long long n, void *y);
+void lq_firfilt_execute_block_dev(lq_firfilt *q, const void *dx, unsigned long long n, void *dy);
+unsigned int lq_firfilt_get_length(lq_firfilt *q);
+lq_ctx *lq_firfilt_ctx(lq_firfilt *q);
+
+/* generic dotprod engine */
+typedef struct lq_dotprod_s lq_dotprod;
+lq_dotprod *lq_dotprod_create(int kind, const float *h, unsigned int n);
+lq_dotprod *lq_dotprod_recreate(lq_dotprod *q, const float *h, unsigned int n);
+void lq_dotprod_destroy(lq_dotprod *q);
+void lq_dotprod_print(lq_dotprod *q);
+void lq_dotprod_execute_batch(lq_dotprod *q, const void *X, unsigned long long nvec, void *Y);
+void lq_dotprod_execute_batch_dev(lq_dotprod *q, const void *dX, unsigned long long nvec, void *dY);
+void lq_dotprod_run(int kind, const float *h, const void *x, unsigned int n, void *y);
+lq_ctx *lq_dotprod_ctx(lq_dotprod *q);
+
+#endif

@@ -1,0 +1,449 @@
+"""ctypes mirror of the liquid_mi355x C-ABI (include/liquid_mi355x.h).
+
+This is the host-side Python view of the drop-in library used by the test
+suite and bench.py.  Object names, argument meaning and error behaviour follow
+liquid-dsp's liquid.h (firfilt_crcf_create / _execute_block / _destroy ...);
+the library itself is C + HIP and runs every sample on the GPU.  Loading the
+library never touches the GPU; the first object constructor does, and exits
+with a message if no HIP device exists (no CPU fallback).
+
+When torch is imported in the same process, import it BEFORE this module so
+that the library binds torch's HIP runtime (one runtime per process).
+"""
+import ctypes as C
+import os
+import re
+import subprocess
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(HERE)
+LIB_PATH = os.path.join(HERE, "lib", "libliquid_mi355x.so")
+HEADER = os.path.join(ROOT, "include", "liquid_mi355x.h")
+
+LIQUID_ANALYZER, LIQUID_SYNTHESIZER = 0, 1
+RRRF, CRCF, CCCF = "rrrf", "crcf", "cccf"
+
+_lib = None
+
+
+class cfloat(C.Structure):
+    """liquid_float_complex passed by value (two packed floats)."""
+    _fields_ = [("re", C.c_float), ("im", C.c_float)]
+
+
+def build():
+    subprocess.check_call(["make", "-s", "-j8", "-C", HERE])
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            build()
+        _lib = C.CDLL(LIB_PATH)
+        _declare(_lib)
+    return _lib
+
+
+def header_functions():
+    """Every function the public header declares (macros expanded by cpp)."""
+    out = subprocess.check_output(["gcc", "-E", "-P", "-I", os.path.join(ROOT, "include"), HEADER],
+                                  text=True)
+    names = set()
+    for m in re.finditer(r"\b([A-Za-z_][A-Za-z0-9_]*)\s*\(", out):
+        name = m.group(1)
+        if name in ("if", "while", "for", "sizeof", "return") or name.startswith("__"):
+            continue
+        names.add(name)
+    # drop typedef'd struct tags and type names that precede '('
+    return sorted(n for n in names if not n.endswith("_s") and n not in ("_Complex",))
+
+
+vp, u, f, i, ull = C.c_void_p, C.c_uint, C.c_float, C.c_int, C.c_ulonglong
+
+
+def _declare(L):
+    sig = {}
+    for t in (RRRF, CRCF, CCCF):
+        tc = cfloat if t == CCCF else f
+        sig.update({
+            "dotprod_%s_run" % t: (None, [vp, vp, u, vp]),
+            "dotprod_%s_run4" % t: (None, [vp, vp, u, vp]),
+            "dotprod_%s_create" % t: (vp, [vp, u]),
+            "dotprod_%s_recreate" % t: (vp, [vp, vp, u]),
+            "dotprod_%s_destroy" % t: (None, [vp]),
+            "dotprod_%s_print" % t: (None, [vp]),
+            "dotprod_%s_execute" % t: (None, [vp, vp, vp]),
+            "dotprod_%s_execute_batch" % t: (None, [vp, vp, ull, vp]),
+            "dotprod_%s_execute_batch_dev" % t: (None, [vp, vp, ull, vp]),
+            "dotprod_%s_set_stream" % t: (None, [vp, vp]),
+            "dotprod_%s_get_stream" % t: (vp, [vp]),
+            "firfilt_%s_create" % t: (vp, [vp, u]),
+            "firfilt_%s_create_kaiser" % t: (vp, [u, f, f, f]),
+            "firfilt_%s_create_rect" % t: (vp, [u]),
+            "firfilt_%s_recreate" % t: (vp, [vp, vp, u]),
+            "firfilt_%s_destroy" % t: (None, [vp]),
+            "firfilt_%s_reset" % t: (None, [vp]),
+            "firfilt_%s_print" % t: (None, [vp]),
+            "firfilt_%s_set_scale" % t: (None, [vp, tc]),
+            "firfilt_%s_push" % t: (None, [vp, f if t == RRRF else cfloat]),
+            "firfilt_%s_execute" % t: (None, [vp, vp]),
+            "firfilt_%s_execute_block" % t: (None, [vp, vp, u, vp]),
+            "firfilt_%s_get_length" % t: (u, [vp]),
+            "firfilt_%s_execute_block_dev" % t: (None, [vp, vp, ull, vp]),
+            "firfilt_%s_set_stream" % t: (None, [vp, vp]),
+            "firfilt_%s_get_stream" % t: (vp, [vp]),
+            "firfilt_%s_synchronize" % t: (None, [vp]),
+        })
+    sig.update({
+        "liquid_firdes_kaiser": (None, [u, f, f, f, vp]),
+        "kaiser_beta_As": (f, [f]),
+        "liquid_libversion_number": (i, []),
+        "liquid_mi355x_malloc": (vp, [ull]),
+        "liquid_mi355x_free": (None, [vp]),
+        "liquid_mi355x_memcpy_h2d": (None, [vp, vp, ull]),
+        "liquid_mi355x_memcpy_d2h": (None, [vp, vp, ull]),
+        "liquid_mi355x_device_synchronize": (None, []),
+        "firdecim_crcf_create": (vp, [u, vp, u]),
+        "firdecim_crcf_create_kaiser": (vp, [u, u, f]),
+        "firdecim_crcf_destroy": (None, [vp]),
+        "firdecim_crcf_clear": (None, [vp]),
+        "firdecim_crcf_execute": (None, [vp, vp, vp]),
+        "firdecim_crcf_execute_block": (None, [vp, vp, u, vp]),
+        "firdecim_crcf_execute_block_dev": (None, [vp, vp, ull, vp]),
+        "firinterp_crcf_create": (vp, [u, vp, u]),
+        "firinterp_crcf_create_kaiser": (vp, [u, u, f]),
+        "firinterp_crcf_destroy": (None, [vp]),
+        "firinterp_crcf_reset": (None, [vp]),
+        "firinterp_crcf_execute": (None, [vp, cfloat, vp]),
+        "firinterp_crcf_execute_block": (None, [vp, vp, u, vp]),
+        "firinterp_crcf_execute_block_dev": (None, [vp, vp, ull, vp]),
+        "fftfilt_crcf_create": (vp, [vp, u, u]),
+        "fftfilt_crcf_destroy": (None, [vp]),
+        "fftfilt_crcf_reset": (None, [vp]),
+        "fftfilt_crcf_set_scale": (None, [vp, f]),
+        "fftfilt_crcf_execute": (None, [vp, vp, vp]),
+        "fftfilt_crcf_get_length": (u, [vp]),
+        "fftfilt_crcf_execute_block": (None, [vp, vp, ull, vp]),
+        "fftfilt_crcf_execute_block_dev": (None, [vp, vp, ull, vp]),
+        "fftfilt_crcf_set_stream": (None, [vp, vp]),
+        "firpfbch_crcf_create": (vp, [i, u, u, vp]),
+        "firpfbch_crcf_create_kaiser": (vp, [i, u, u, f]),
+        "firpfbch_crcf_destroy": (None, [vp]),
+        "firpfbch_crcf_reset": (None, [vp]),
+        "firpfbch_crcf_analyzer_execute": (None, [vp, vp, vp]),
+        "firpfbch_crcf_synthesizer_execute": (None, [vp, vp, vp]),
+        "firpfbch_crcf_execute_block": (None, [vp, vp, ull, vp]),
+        "firpfbch_crcf_execute_block_dev": (None, [vp, vp, ull, vp]),
+        "firpfbch2_crcf_create": (vp, [i, u, u, vp]),
+        "firpfbch2_crcf_create_kaiser": (vp, [i, u, u, f]),
+        "firpfbch2_crcf_destroy": (None, [vp]),
+        "firpfbch2_crcf_reset": (None, [vp]),
+        "firpfbch2_crcf_execute": (None, [vp, vp, vp]),
+        "firpfbch2_crcf_execute_block": (None, [vp, vp, ull, vp]),
+        "firpfbch2_crcf_execute_block_dev": (None, [vp, vp, ull, vp]),
+        "firpfbch2_crcf_set_stream": (None, [vp, vp]),
+        "firpfbch2_crcf_get_stream": (vp, [vp]),
+        "firpfbch2_crcf_synchronize": (None, [vp]),
+    })
+    for name, (res, args) in sig.items():
+        fn = getattr(L, name)
+        fn.restype = res
+        fn.argtypes = args
+
+
+def ptr(a):
+    return a.ctypes.data_as(C.c_void_p)
+
+
+def _samples(x, t):
+    return np.ascontiguousarray(x, dtype=np.float32 if t == RRRF else np.complex64)
+
+
+def _coefs(h, t):
+    return np.ascontiguousarray(h, dtype=np.complex64 if t == CCCF else np.float32)
+
+
+# ------------------------------------------------------------------ device buffers
+class DeviceBuffer:
+    """Device allocation made through the library (liquid_mi355x_malloc)."""
+
+    def __init__(self, nbytes):
+        self.nbytes = int(nbytes)
+        self.p = lib().liquid_mi355x_malloc(self.nbytes)
+
+    @classmethod
+    def from_array(cls, a):
+        a = np.ascontiguousarray(a)
+        b = cls(a.nbytes)
+        lib().liquid_mi355x_memcpy_h2d(b.p, ptr(a), a.nbytes)
+        return b
+
+    def to_array(self, dtype, count):
+        a = np.empty(count, dtype)
+        lib().liquid_mi355x_memcpy_d2h(ptr(a), self.p, a.nbytes)
+        return a
+
+    def free(self):
+        if self.p:
+            lib().liquid_mi355x_free(self.p)
+            self.p = None
+
+    def __del__(self):
+        try:
+            self.free()
+        except Exception:
+            pass
+
+
+def firdes_kaiser(n, fc, As, mu=0.0):
+    h = np.zeros(n, np.float32)
+    lib().liquid_firdes_kaiser(n, fc, As, mu, ptr(h))
+    return h
+
+
+# ------------------------------------------------------------------ objects
+class _Obj:
+    prefix = None
+
+    def _fn(self, name):
+        return getattr(lib(), self.prefix + name)
+
+    def destroy(self):
+        if getattr(self, "q", None):
+            self._fn("_destroy")(self.q)
+            self.q = None
+
+    def __del__(self):
+        try:
+            self.destroy()
+        except Exception:
+            pass
+
+    def set_stream(self, s):
+        self._fn("_set_stream")(self.q, s)
+
+
+class FirFilt(_Obj):
+    def __init__(self, t, h=None, kaiser=None):
+        self.t = t
+        self.prefix = "firfilt_%s" % t
+        if kaiser is not None:
+            self.q = self._fn("_create_kaiser")(*kaiser)
+        else:
+            self._h = _coefs(h, t)
+            self.q = self._fn("_create")(ptr(self._h), len(self._h))
+
+    def set_scale(self, s):
+        if self.t == CCCF:
+            s = complex(s)
+            self._fn("_set_scale")(self.q, cfloat(s.real, s.imag))
+        else:
+            self._fn("_set_scale")(self.q, float(s))
+
+    def reset(self):
+        self._fn("_reset")(self.q)
+
+    def push(self, v):
+        if self.t == RRRF:
+            self._fn("_push")(self.q, float(v))
+        else:
+            v = complex(v)
+            self._fn("_push")(self.q, cfloat(v.real, v.imag))
+
+    def execute(self):
+        y = _samples([0], self.t)
+        self._fn("_execute")(self.q, ptr(y))
+        return y[0]
+
+    def execute_block(self, x):
+        x = _samples(x, self.t)
+        y = np.zeros_like(x)
+        self._fn("_execute_block")(self.q, ptr(x), len(x), ptr(y))
+        return y
+
+    def execute_block_dev(self, dx, n, dy):
+        self._fn("_execute_block_dev")(self.q, dx, n, dy)
+
+    def synchronize(self):
+        self._fn("_synchronize")(self.q)
+
+    def get_length(self):
+        return self._fn("_get_length")(self.q)
+
+
+class DotProd(_Obj):
+    def __init__(self, t, h):
+        self.t = t
+        self.prefix = "dotprod_%s" % t
+        self._h = _coefs(h, t)
+        self.n = len(self._h)
+        self.q = self._fn("_create")(ptr(self._h), self.n)
+
+    def execute(self, x):
+        x = _samples(x, self.t)
+        y = _samples([0], self.t)
+        self._fn("_execute")(self.q, ptr(x), ptr(y))
+        return y[0]
+
+    def execute_batch(self, X):
+        X = _samples(X, self.t)
+        nvec = X.size // self.n
+        Y = np.zeros(nvec, X.dtype)
+        self._fn("_execute_batch")(self.q, ptr(X), nvec, ptr(Y))
+        return Y
+
+    def execute_batch_dev(self, dX, nvec, dY):
+        self._fn("_execute_batch_dev")(self.q, dX, nvec, dY)
+
+
+def dotprod_run(t, h, x):
+    h = _coefs(h, t)
+    x = _samples(x, t)
+    y = _samples([0], t)
+    getattr(lib(), "dotprod_%s_run" % t)(ptr(h), ptr(x), len(h), ptr(y))
+    return y[0]
+
+
+class FirDecim(_Obj):
+    prefix = "firdecim_crcf"
+
+    def __init__(self, M, h=None, m=None, As=None):
+        self.M = M
+        if h is None:
+            self.q = self._fn("_create_kaiser")(M, m, As)
+        else:
+            self._h = _coefs(h, CRCF)
+            self.q = self._fn("_create")(M, ptr(self._h), len(self._h))
+
+    def execute_block(self, x):
+        x = _samples(x, CRCF)
+        n = len(x) // self.M
+        y = np.zeros(n, np.complex64)
+        self._fn("_execute_block")(self.q, ptr(x), n, ptr(y))
+        return y
+
+    def execute(self, x):
+        x = _samples(x, CRCF)
+        y = np.zeros(1, np.complex64)
+        self._fn("_execute")(self.q, ptr(x), ptr(y))
+        return y[0]
+
+
+class FirInterp(_Obj):
+    prefix = "firinterp_crcf"
+
+    def __init__(self, M, h=None, m=None, As=None):
+        self.M = M
+        if h is None:
+            self.q = self._fn("_create_kaiser")(M, m, As)
+        else:
+            self._h = _coefs(h, CRCF)
+            self.q = self._fn("_create")(M, ptr(self._h), len(self._h))
+
+    def execute_block(self, x):
+        x = _samples(x, CRCF)
+        y = np.zeros(len(x) * self.M, np.complex64)
+        self._fn("_execute_block")(self.q, ptr(x), len(x), ptr(y))
+        return y
+
+    def execute(self, v):
+        v = complex(v)
+        y = np.zeros(self.M, np.complex64)
+        self._fn("_execute")(self.q, cfloat(v.real, v.imag), ptr(y))
+        return y
+
+
+class FftFilt(_Obj):
+    prefix = "fftfilt_crcf"
+
+    def __init__(self, h, n):
+        self.n = n
+        self._h = _coefs(h, CRCF)
+        self.q = self._fn("_create")(ptr(self._h), len(self._h), n)
+
+    def set_scale(self, s):
+        self._fn("_set_scale")(self.q, float(s))
+
+    def execute(self, x):
+        x = _samples(x, CRCF)
+        assert len(x) == self.n
+        y = np.zeros_like(x)
+        self._fn("_execute")(self.q, ptr(x), ptr(y))
+        return y
+
+    def execute_block(self, x):
+        x = _samples(x, CRCF)
+        y = np.zeros_like(x)
+        self._fn("_execute_block")(self.q, ptr(x), len(x), ptr(y))
+        return y
+
+    def execute_block_dev(self, dx, n, dy):
+        self._fn("_execute_block_dev")(self.q, dx, n, dy)
+
+
+class FirPfbch(_Obj):
+    prefix = "firpfbch_crcf"
+
+    def __init__(self, typ, M, p=None, h=None, m=None, As=None):
+        self.typ, self.M = typ, M
+        if h is None:
+            self.q = self._fn("_create_kaiser")(typ, M, m, As)
+        else:
+            self._h = _coefs(h, CRCF)
+            self.q = self._fn("_create")(typ, M, p, ptr(self._h))
+
+    def execute(self, x):
+        x = _samples(x, CRCF)
+        y = np.zeros(self.M, np.complex64)
+        fn = "_analyzer_execute" if self.typ == LIQUID_ANALYZER else "_synthesizer_execute"
+        self._fn(fn)(self.q, ptr(x), ptr(y))
+        return y
+
+    def execute_block(self, x):
+        x = _samples(x, CRCF)
+        nb = len(x) // self.M
+        y = np.zeros(nb * self.M, np.complex64)
+        self._fn("_execute_block")(self.q, ptr(x), nb, ptr(y))
+        return y
+
+
+class FirPfbch2(_Obj):
+    prefix = "firpfbch2_crcf"
+
+    def __init__(self, typ, M, m, As=None, h=None):
+        self.typ, self.M, self.m = typ, M, m
+        if h is None:
+            self.q = self._fn("_create_kaiser")(typ, M, m, As)
+        else:
+            self._h = _coefs(h, CRCF)
+            self.q = self._fn("_create")(typ, M, m, ptr(self._h))
+        self.nin = M // 2 if typ == LIQUID_ANALYZER else M
+        self.nout = M if typ == LIQUID_ANALYZER else M // 2
+
+    def reset(self):
+        self._fn("_reset")(self.q)
+
+    def execute(self, x):
+        x = _samples(x, CRCF)
+        y = np.zeros(self.nout, np.complex64)
+        self._fn("_execute")(self.q, ptr(x), ptr(y))
+        return y
+
+    def execute_block(self, x):
+        x = _samples(x, CRCF)
+        nb = len(x) // self.nin
+        y = np.zeros(nb * self.nout, np.complex64)
+        self._fn("_execute_block")(self.q, ptr(x), nb, ptr(y))
+        return y
+
+    def execute_block_dev(self, dx, nblocks, dy):
+        self._fn("_execute_block_dev")(self.q, dx, nblocks, dy)
+
+    def synchronize(self):
+        self._fn("_synchronize")(self.q)
+
+    def get_stream(self):
+        return self._fn("_get_stream")(self.q)
