@@ -70,15 +70,64 @@ __device__ __forceinline__ float2 apply_scale_real(float2 a, float s) { return m
 __device__ __forceinline__ float vadd(float a, float b) { return a + b; }
 __device__ __forceinline__ float2 vadd(float2 a, float2 b) { return make_float2(a.x + b.x, a.y + b.y); }
 
-__host__ __device__ __forceinline__ int lds_idx(int u) { return u + (u >> 4); } // 1 pad slot per 16 samples
+// LDS image of a sample tile: rows of 16 samples followed by 16 bytes of pad.
+// Lanes whose windows start 16 samples apart then hit disjoint bank sets on
+// every ds_read_b128 (complex: 36-dword row pitch; real: 20-dword pitch), and
+// every 16-byte vector of samples stays 16-byte aligned.
+template <typename T>
+__host__ __device__ __forceinline__ int lds_off(int u) // in bytes
+{
+    return u * (int)sizeof(T) + 16 * (u >> 4);
+}
+template <typename T>
+__host__ __device__ __forceinline__ int lds_bytes(int nsamp)
+{
+    return lds_off<T>(nsamp) + 16;
+}
+
+template <typename T>
+struct vec16;
+template <>
+struct vec16<float> {
+    static constexpr int N = 4;
+};
+template <>
+struct vec16<float2> {
+    static constexpr int N = 2;
+};
+
+// 16-byte vector of samples
+template <typename T>
+__device__ __forceinline__ void load16(const T *p, T (&o)[vec16<T>::N])
+{
+    const float4 v = *reinterpret_cast<const float4 *>(p);
+    if constexpr (sizeof(T) == 8) {
+        o[0] = make_float2(v.x, v.y);
+        o[1] = make_float2(v.z, v.w);
+    } else {
+        o[0] = v.x;
+        o[1] = v.y;
+        o[2] = v.z;
+        o[3] = v.w;
+    }
+}
+template <typename T>
+__device__ __forceinline__ float4 pack16(const T (&o)[vec16<T>::N])
+{
+    if constexpr (sizeof(T) == 8) return make_float4(o[0].x, o[0].y, o[1].x, o[1].y);
+    else return make_float4(o[0], o[1], o[2], o[3]);
+}
 
 // ------------------------------------------------------------------ firfilt
-// Grid: one workgroup per TILE outputs.  LDS holds samples [t0-HP, t0+TILE)
-// (HP = padded filter length) with one pad slot per 16 samples, so that the
-// 64 lanes of a wave, whose windows start 16 samples apart, hit 64 distinct
-// banks on every ds_read_b64.
+// Grid: one workgroup per TILE outputs.  LDS holds samples [t0-HP, t0+TILE).
+// Lane tid computes outputs t0 + R*tid + r (r < R) with the R x HC tap block
+// fully unrolled: coefficients are wave-uniform (scalar loads / SGPR
+// operands), window samples come from LDS 16 bytes at a time, one row of 16
+// samples per 16-tap group, so the inner body is pure FMA.  Outputs are
+// transposed back through LDS and written with coalesced 16-byte stores.
+// `win` = the previous HP samples (oldest first); ext[t<0] = win[HP + t].
 template <int KIND, int HC>
-__global__ __launch_bounds__(NT) void k_firfilt(const typename kt<KIND>::T *__restrict__ hist,
+__global__ __launch_bounds__(NT) void k_firfilt(const typename kt<KIND>::T *__restrict__ win,
                                                 const typename kt<KIND>::T *x, long long n,
                                                 typename kt<KIND>::T *y,
                                                 const typename kt<KIND>::TC *__restrict__ hpad,
@@ -87,25 +136,28 @@ __global__ __launch_bounds__(NT) void k_firfilt(const typename kt<KIND>::T *__re
 {
     typedef typename kt<KIND>::T T;
     typedef typename kt<KIND>::TC TC;
+    constexpr int VE = vec16<T>::N;
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-    T *tile = reinterpret_cast<T *>(smem);
 
     const int HP = HC * nchunk;
     const long long t0 = (long long)blockIdx.x * TILE;
     const int S = TILE + HP;
 
-    for (int u = threadIdx.x; u < S; u += NT) {
+    for (int e = threadIdx.x; e < S / VE; e += NT) {
+        const int u = e * VE;
         const long long s = t0 - HP + u;
-        T v;
-        if (s < 0)
-            v = (s >= -(long long)(HP - 1)) ? hist[HP - 1 + s] : zero<T>();
-        else if (s >= n)
-            v = zero<T>();
-        else if (halo != nullptr && u < HP && blockIdx.x > 0)
-            v = halo[(size_t)blockIdx.x * HP + u];
-        else
-            v = x[s];
-        tile[lds_idx(u)] = v;
+        T o[VE];
+        if (s < 0) {
+            load16(win + HP + s, o);
+        } else if (halo != nullptr && u < HP && blockIdx.x > 0) {
+            load16(halo + (size_t)blockIdx.x * HP + u, o);
+        } else if (s + VE <= n) {
+            load16(x + s, o);
+        } else {
+#pragma unroll
+            for (int i = 0; i < VE; i++) o[i] = (s + i < n) ? x[s + i] : zero<T>();
+        }
+        *reinterpret_cast<float4 *>(smem + lds_off<T>(u)) = pack16(o);
     }
     __syncthreads();
 
@@ -115,24 +167,62 @@ __global__ __launch_bounds__(NT) void k_firfilt(const typename kt<KIND>::T *__re
 
     for (int c = 0; c < nchunk; c++) {
         const TC *hc = hpad + c * HC;
-        // first window sample u = R*tid + HP - c*HC - HC + 1 = 16*(tid+q) + 1
-        const int q = (HP - c * HC - HC) >> 4;
-        const T *base = tile + 17 * (threadIdx.x + q);
+        // window sample a' (0 <= a' < HC+R) of this chunk is tile sample
+        // u = R*tid + HP - c*HC - HC + a'  (a row start when a' % 16 == 0)
+        const int row0 = threadIdx.x + ((HP - c * HC - HC) >> 4);
+        const unsigned char *rb = smem + lds_off<T>(16 * row0);
+        T v[HC + R];
+        // newest row first: a' in [HC, HC+16)
 #pragma unroll
-        for (int d = 0; d < HC + R - 1; d++) {
-            const T v = base[(1 + d) + ((1 + d) >> 4)];
+        for (int i = 0; i < 16 / VE; i++) {
+            T o[VE];
+            load16(reinterpret_cast<const T *>(rb + lds_off<T>(HC + i * VE)), o);
 #pragma unroll
-            for (int r = 0; r < R; r++) {
-                const int kk = r - d + HC - 1;
-                if (kk >= 0 && kk < HC) mac(acc[r], hc[kk], v);
+            for (int k = 0; k < VE; k++) v[HC + i * VE + k] = o[k];
+        }
+#pragma unroll
+        for (int g = 0; g < HC / 16; g++) {
+            // bring in the next older row: a' in [HC-16g-16, HC-16g)
+#pragma unroll
+            for (int i = 0; i < 16 / VE; i++) {
+                const int a = HC - 16 * g - 16 + i * VE;
+                T o[VE];
+                load16(reinterpret_cast<const T *>(rb + lds_off<T>(a)), o);
+#pragma unroll
+                for (int k = 0; k < VE; k++) v[a + k] = o[k];
+            }
+#pragma unroll
+            for (int j = 0; j < 16; j++) {
+                const TC hv = hc[16 * g + j];
+#pragma unroll
+                for (int r = 0; r < R; r++) mac(acc[r], hv, v[r - (16 * g + j) + HC]);
             }
         }
     }
 
-    const long long tb = t0 + (long long)R * threadIdx.x;
+    // transpose through LDS for coalesced stores
+    __syncthreads();
 #pragma unroll
-    for (int r = 0; r < R; r++)
-        if (tb + r < n) y[tb + r] = apply_scale(acc[r], sre, sim);
+    for (int i = 0; i < R / VE; i++) {
+        T o[VE];
+#pragma unroll
+        for (int k = 0; k < VE; k++) o[k] = apply_scale(acc[i * VE + k], sre, sim);
+        *reinterpret_cast<float4 *>(smem + lds_off<T>(R * threadIdx.x + i * VE)) = pack16(o);
+    }
+    __syncthreads();
+    const long long nt = n - t0 < TILE ? n - t0 : TILE;
+    for (int e = threadIdx.x; e < TILE / VE; e += NT) {
+        const int u = e * VE;
+        if (u >= nt) break;
+        const float4 val = *reinterpret_cast<const float4 *>(smem + lds_off<T>(u));
+        if (u + VE <= nt) {
+            *reinterpret_cast<float4 *>(y + t0 + u) = val;
+        } else {
+            T o[VE];
+            load16(reinterpret_cast<const T *>(smem + lds_off<T>(u)), o);
+            for (int k = 0; k < VE && u + k < nt; k++) y[t0 + u + k] = o[k];
+        }
+    }
 }
 
 template <int KIND>
@@ -255,7 +345,7 @@ void launch_firfilt(const lqk_fir_desc *d, const void *hist, const void *x, long
     typedef typename kt<KIND>::TC TC;
     const int HP = HC * (int)d->nchunk;
     const long long ntiles = (n + TILE - 1) / TILE;
-    const size_t lds = (size_t)lds_idx(TILE + HP) * sizeof(T) + 16;
+    const size_t lds = (size_t)lds_bytes<T>(TILE + HP);
     if (lds > 160 * 1024) {
         fprintf(stderr, "error: firfilt: filter length %u exceeds the GPU tile limit\n", d->hlen);
         exit(1);

@@ -38,8 +38,8 @@ void lqk_dotprod_batch(int kind, const void *h, unsigned int n, const void *X,
 
 /* ---------------------------------------------------------------- firfilt
  * Streaming FIR: y[i] = scale * sum_{k<hlen} h[k] ext[i-k], where ext[t] = x[t]
- * for t >= 0 and hist[hlen-1+t] for t < 0 (hist holds the previous hlen-1
- * inputs, oldest first).  hpad: coefficients in natural order, zero padded to
+ * for t >= 0 and win[HP+t] for t < 0 (win = the previous HP = hc*nchunk
+ * inputs, oldest first, 16-byte aligned).  hpad: coefficients in natural order, zero padded to
  * nchunk*hc.  kind: 0 rrrf, 1 crcf, 2 cccf.  x == y allowed (in-place). */
 typedef struct {
     int kind;
@@ -80,6 +80,12 @@ void lqk_firinterp(int kind, const void *hpoly /* M x L, h[p + l*M] */, unsigned
 void lqk_firpfbch2_analyzer(unsigned int M, unsigned int m, const void *hsub, const void *hist,
                             const void *x, unsigned long long nblocks, int p0, void *Y,
                             void *stream);
+/* M = 1024 (m = 2 or 4) register/LDS-streaming fast path; returns 0 if the
+ * shape is not covered (caller then uses lqk_firpfbch2_analyzer).  B0 = global
+ * index of the first block (only its parity matters). */
+int lqk_firpfbch2_analyzer_fast(unsigned int M, unsigned int m, const void *hsub, const void *hist,
+                                const void *x, unsigned long long nblocks, long long B0, void *Y,
+                                void *stream);
 /* synthesizer: nblocks x M channel inputs -> nblocks x M/2 outputs.
  * state: the previous 4m-1 IFFT vectors (M each), zscratch (4m-1+nblocks)*M;
  * see csrc/k_channelizer.hip */

@@ -204,7 +204,7 @@ void lq_firfilt_execute_block_dev(lq_firfilt *q, const void *dx, unsigned long l
     lqk_window_append(q->kind != LQ_RRRF, wold, q->HP, dx, n, wnew, q->ctx.stream);
     void *scr = NULL;
     if (dx == dy) scr = lq_devbuf_get(&q->scratch, lqk_firfilt_scratch_bytes(&q->d, n));
-    lqk_firfilt(&q->d, (const unsigned char *)wold + q->esz, dx, n, dy, scr, q->ctx.stream);
+    lqk_firfilt(&q->d, wold, dx, n, dy, scr, q->ctx.stream);
     q->cur ^= 1;
     q->host_valid = 0;
 }

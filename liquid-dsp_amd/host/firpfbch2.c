@@ -124,7 +124,9 @@ void firpfbch2_crcf_execute_block_dev(firpfbch2_crcf _q, const liquid_float_comp
     if (_nblocks == 0) return;
     if (_q->type == LIQUID_ANALYZER) {
         void *hold = _q->d_hist[_q->cur], *hnew = _q->d_hist[_q->cur ^ 1];
-        lqk_firpfbch2_analyzer(_q->M, _q->m, _q->d_hsub, hold, _dx, _nblocks, _q->flag, _dy, _q->ctx.stream);
+        if (!lqk_firpfbch2_analyzer_fast(_q->M, _q->m, _q->d_hsub, hold, _dx, _nblocks, _q->flag, _dy,
+                                         _q->ctx.stream))
+            lqk_firpfbch2_analyzer(_q->M, _q->m, _q->d_hsub, hold, _dx, _nblocks, _q->flag, _dy, _q->ctx.stream);
         lqk_window_append(1, hold, _q->HL, _dx, _nblocks * (_q->M / 2), hnew, _q->ctx.stream);
         _q->cur ^= 1;
     } else {
