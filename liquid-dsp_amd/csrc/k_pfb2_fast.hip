@@ -210,25 +210,25 @@ __global__ __launch_bounds__(NT, 2) void k_pfb2_an1024(Params P, const float *__
             if (gg < ge) {
             const long long c0 = 2 * gg;
             const int s0 = 2 * ph, s1 = 2 * ph + 1;
-            {
-                float4 lo, hi;
-                load_row(c0, lo, hi);
-                win[0][s0] = make_float2(lo.x, lo.y);
-                win[1][s0] = make_float2(lo.z, lo.w);
-                win[2][s0] = make_float2(hi.x, hi.y);
-                win[3][s0] = make_float2(hi.z, hi.w);
-                load_row(c0 + 1, lo, hi);
-                win[0][s1] = make_float2(lo.x, lo.y);
-                win[1][s1] = make_float2(lo.z, lo.w);
-                win[2][s1] = make_float2(hi.x, hi.y);
-                win[3][s1] = make_float2(hi.z, hi.w);
-            }
+            // both rows are fetched up front; row c0+1 enters the ring only
+            // after row c0's dot products (its slot still holds row c0-7)
+            float4 lo0, hi0, lo1, hi1;
+            load_row(c0, lo0, hi0);
+            load_row(c0 + 1, lo1, hi1);
+            win[0][s0] = make_float2(lo0.x, lo0.y);
+            win[1][s0] = make_float2(lo0.z, lo0.w);
+            win[2][s0] = make_float2(hi0.x, hi0.y);
+            win[3][s0] = make_float2(hi0.z, hi0.w);
             const long long b0 = 4 * gg;
             // row c0: lo bins -> blocks b0 (E), b0+1 (O); hi bins -> b0+1 (O), b0+2 (E)
             put(b0, M2 - 2 - colA, dotq(1, s0, hE(1)), dotq(0, s0, hE(0)));
             put(b0 + 1, M2 - 2 - colA, dotq(1, s0, hO(1)), dotq(0, s0, hO(0)));
             put(b0 + 1, M - 2 - colA, dotq(3, s0, hO(3)), dotq(2, s0, hO(2)));
             put(b0 + 2, M - 2 - colA, dotq(3, s0, hE(3)), dotq(2, s0, hE(2)));
+            win[0][s1] = make_float2(lo1.x, lo1.y);
+            win[1][s1] = make_float2(lo1.z, lo1.w);
+            win[2][s1] = make_float2(hi1.x, hi1.y);
+            win[3][s1] = make_float2(hi1.z, hi1.w);
             // row c0+1: lo -> b0+2 (E), b0+3 (O); hi -> b0+3 (O), b0+4 (E)
             put(b0 + 2, M2 - 2 - colA, dotq(1, s1, hE(1)), dotq(0, s1, hE(0)));
             put(b0 + 3, M2 - 2 - colA, dotq(1, s1, hO(1)), dotq(0, s1, hO(0)));

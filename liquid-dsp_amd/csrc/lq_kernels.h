@@ -28,6 +28,7 @@ void   lqrt_d2h(void *dst, const void *src, size_t bytes, void *stream);
 void   lqrt_d2d(void *dst, const void *src, size_t bytes, void *stream);
 void   lqrt_memset(void *dst, size_t bytes, void *stream);
 void   lqrt_sync(void *stream);
+void   lqrt_device_sync(void);
 int    lqrt_is_device_ptr(const void *p);
 const float *lqrt_twiddles(void);               /* W_4096^e = exp(-2 pi i e/4096), e<4096 */
 

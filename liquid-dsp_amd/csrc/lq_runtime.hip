@@ -45,7 +45,10 @@ extern "C" void *lqrt_malloc(size_t bytes)
     void *p = nullptr;
     if (bytes == 0) bytes = 16;
     LQ_CHECK(hipMalloc(&p, bytes));
-    LQ_CHECK(hipMemset(p, 0, bytes));
+    // the memset runs on the null stream, which does not order with the
+    // objects' non-blocking streams: wait for it before anyone reads p
+    LQ_CHECK(hipMemsetAsync(p, 0, bytes, nullptr));
+    LQ_CHECK(hipStreamSynchronize(nullptr));
     return p;
 }
 
@@ -140,7 +143,13 @@ extern "C" const float *lqrt_twiddles(void)
         float *d = nullptr;
         LQ_CHECK(hipMalloc(&d, sizeof(h)));
         LQ_CHECK(hipMemcpy(d, h, sizeof(h), hipMemcpyHostToDevice));
+        LQ_CHECK(hipDeviceSynchronize());
         tables[dev] = d;
     }
     return tables[dev];
+}
+
+extern "C" void lqrt_device_sync(void)
+{
+    LQ_CHECK(hipDeviceSynchronize());
 }

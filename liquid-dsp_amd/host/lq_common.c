@@ -184,4 +184,4 @@ void liquid_mi355x_memcpy_d2h(void *_dst, const void *_src, unsigned long long _
     lqrt_sync(s);
 }
 
-void liquid_mi355x_device_synchronize(void) { lqrt_sync(NULL); }
+void liquid_mi355x_device_synchronize(void) { lqrt_device_sync(); }
