@@ -10,11 +10,14 @@
 //        X_b[j] = sum_n h[i + nM] row[c - n][col],  i = j (b even) or j ^ M/2 (b odd),
 //    c = row of the block's newest sample.  Row c completes blocks 2c
 //    (lower bins; upper bins came from row c-1) and 2c+1, and starts 2c+2.
-//  * A workgroup (4 waves) owns all 1024 columns (4 per lane), streams rows
-//    through an 8-deep register ring per column (coefficients pinned in
-//    registers), so every input sample is read from HBM once per workgroup
-//    segment.  Two rows per iteration produce four complete blocks.
-//  * X of each block goes to an LDS ring (6 block buffers); after a barrier
+//  * A workgroup (8 waves, one per CU) owns all 1024 columns: lane t holds
+//    column t (bin 511-t) and column 512+t (bin 1023-t), whose even-block taps
+//    are each other's odd-block taps, so 2 x L coefficients and an 8-deep
+//    register ring per column cover both.  Rows stream through the ring, so
+//    every input sample is read from HBM once per workgroup segment.  Four
+//    rows per iteration complete eight blocks; the next four rows are
+//    prefetched into registers while the FFTs run.
+//  * X of each block goes to an LDS ring (9 block buffers); after a barrier
 //    each wave runs one 1024-point IFFT in registers: 16-point DFT over the
 //    lane's 16 bins (j = lane + 64k), twiddle, LDS transpose (row stride 68
 //    keeps ds_read_b64 conflict-free), 16-point DFT, twiddle, and a 4-point
@@ -34,9 +37,9 @@ namespace {
 
 constexpr int M = 1024;
 constexpr int M2 = M / 2;
-constexpr int NT = 256;
+constexpr int NT = 512;
 constexpr int NS = 8;      // register ring depth (rows)
-constexpr int NBUF = 6;    // LDS block buffers
+constexpr int NBUF = 9;    // LDS block buffers (writes b0..b0+8, FFT reads b0..b0+7)
 constexpr int BSTR = 1088; // floats2 per block buffer (16 x 68 transpose)
 constexpr int TSTR = 68;
 
@@ -86,6 +89,15 @@ __device__ __forceinline__ float2 shfl_xor2(float2 v, int m)
     return make_float2(__shfl_xor(v.x, m, 64), __shfl_xor(v.y, m, 64));
 }
 
+typedef float v2f __attribute__((ext_vector_type(2)));
+
+// streaming (non-temporal) store of one complex sample: output is written once
+__device__ __forceinline__ void st_nt(float2 *p, float2 v)
+{
+    v2f w = {v.x, v.y};
+    __builtin_nontemporal_store(w, reinterpret_cast<v2f *>(p));
+}
+
 __device__ __forceinline__ void lds_fence()
 {
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
@@ -97,16 +109,16 @@ struct Params {
     const float2 *hist;
     const float2 *x;
     long long n_in;   // input samples in this call
-    long long B0;     // global index of the call's first block
+    long long B0;     // global index of the call's first block (parity matters)
     long long nblk;   // blocks in this call
-    long long gs0;    // first global group (4 blocks) handled by workgroup 0 (multiple of 4)
-    int gpw;          // groups per workgroup (multiple of 4)
+    long long gs0;    // first global 8-block group of workgroup 0 (even)
+    int gpw;          // groups per workgroup (even)
     long long gend;   // one past the last group needed
     float2 *Y;
 };
 
 template <int L>
-__global__ __launch_bounds__(NT, 2) void k_pfb2_an1024(Params P, const float *__restrict__ hsub,
+__global__ __launch_bounds__(NT, 1) void k_pfb2_an1024(Params P, const float *__restrict__ hsub,
                                                        const float2 *__restrict__ tw4096)
 {
     static_assert(L <= NS, "ring too small");
@@ -129,158 +141,140 @@ __global__ __launch_bounds__(NT, 2) void k_pfb2_an1024(Params P, const float *__
         tw2[tid] = make_float2(w.x, -w.y);
     }
 
-    // columns of this lane: lo pair (2t, 2t+1) -> bins 511-2t, 510-2t;
-    //                       hi pair (512+2t, 513+2t) -> bins 1023-2t, 1022-2t
-    const int colA = 2 * tid;
-    int jb[4] = {M2 - 1 - colA, M2 - 2 - colA, M - 1 - colA, M - 2 - colA};
-    // bins of the hi columns are the lo bins xor M/2, so the odd-block taps of
-    // one pair are the even-block taps of the other: 4 x L coefficients per lane
-    float hc[4][L];
+    // lane column pair: lo column tid -> bin jl = M/2-1-tid, hi column M/2+tid
+    // -> bin jh = M-1-tid = jl ^ M/2.  Even blocks use taps h[j + nM], odd
+    // blocks h[(j ^ M/2) + nM]: the lo column's odd taps are the hi column's
+    // even taps and vice versa.  1/M folded in (exact).
+    const int jl = M2 - 1 - tid, jh = M - 1 - tid;
+    float hl[L], hh[L];
     const float inv = 1.0f / (float)M;
 #pragma unroll
-    for (int q = 0; q < 4; q++)
-#pragma unroll
-        for (int n = 0; n < L; n++) hc[q][n] = hsub[jb[q] * L + n] * inv;
-#define hE(q) hc[(q)]
-#define hO(q) hc[(q) ^ 2]
+    for (int n = 0; n < L; n++) {
+        hl[n] = hsub[jl * L + n] * inv;
+        hh[n] = hsub[jh * L + n] * inv;
+    }
 
-    float2 win[4][NS];
+    float2 wl[NS], wh[NS];
 #pragma unroll
-    for (int q = 0; q < 4; q++)
-#pragma unroll
-        for (int s = 0; s < NS; s++) win[q][s] = make_float2(0.f, 0.f);
+    for (int s = 0; s < NS; s++) wl[s] = wh[s] = make_float2(0.f, 0.f);
 
     const long long gs = P.gs0 + (long long)blockIdx.x * P.gpw;
     long long ge = gs + P.gpw;
     if (ge > P.gend) ge = P.gend;
     const long long base_off = P.B0 * M2; // stream index of local sample 0
+    const long long HL = 2 * (L / 2) * M - M2;
 
-    auto load_row = [&](long long c, float4 &lo, float4 &hi) {
-        const long long i0 = c * M + colA - base_off;
-        const long long i1 = i0 + M2;
-        const float4 z = make_float4(0.f, 0.f, 0.f, 0.f);
-        const int HL = 2 * (L / 2) * M - M2;
-        if (i0 >= 0 && i0 < P.n_in) lo = *reinterpret_cast<const float4 *>(P.x + i0);
-        else if (i0 < 0 && i0 >= -HL) lo = *reinterpret_cast<const float4 *>(P.hist + HL + i0);
-        else lo = z;
-        if (i1 >= 0 && i1 < P.n_in) hi = *reinterpret_cast<const float4 *>(P.x + i1);
-        else if (i1 < 0 && i1 >= -HL) hi = *reinterpret_cast<const float4 *>(P.hist + HL + i1);
-        else hi = z;
+    // branch-free fetch: always-valid address, then select
+    auto fetch = [&](long long i) -> float2 {
+        const bool in_x = (i >= 0) && (i < P.n_in);
+        const bool in_h = (i < 0) && (i >= -HL);
+        const float2 *p = in_x ? P.x + i : (in_h ? P.hist + (HL + i) : P.hist);
+        const float2 v = *p;
+        return (in_x || in_h) ? v : make_float2(0.f, 0.f);
     };
-
-    // warm-up: rows 2gs-8 .. 2gs-2 fill ring slots 0..6; row 2gs-1 (slot 7)
-    // also yields the upper-bin half of block 4gs.
-#pragma unroll
-    for (int s = 0; s < NS; s++) {
-        float4 lo, hi;
-        load_row(2 * gs - NS + s, lo, hi);
-        win[0][s] = make_float2(lo.x, lo.y);
-        win[1][s] = make_float2(lo.z, lo.w);
-        win[2][s] = make_float2(hi.x, hi.y);
-        win[3][s] = make_float2(hi.z, hi.w);
-    }
-    __syncthreads(); // tables ready
-
-    auto dotq = [&](int q, int newest, const float (&h)[L]) -> float2 {
+    auto dot = [&](const float2 (&w)[NS], int newest, const float (&h)[L]) -> float2 {
         float2 acc = make_float2(0.f, 0.f);
 #pragma unroll
         for (int n = 0; n < L; n++) {
-            const float2 v = win[q][(newest - n) & (NS - 1)];
+            const float2 v = w[(newest - n) & (NS - 1)];
             acc.x = fmaf(h[n], v.x, acc.x);
             acc.y = fmaf(h[n], v.y, acc.y);
         }
         return acc;
     };
-    // write the two lo-bin or hi-bin values of block b as one 16-byte store
-    auto put = [&](long long b, int jlow, float2 vlow, float2 vhigh) {
-        float2 *B = xb + (int)(b % NBUF) * BSTR;
-        *reinterpret_cast<float4 *>(B + jlow) = make_float4(vlow.x, vlow.y, vhigh.x, vhigh.y);
-    };
+    auto buf = [&](long long b) -> float2 * { return xb + (int)(b % NBUF) * BSTR; };
 
-    // upper half of block 4gs from row 2gs-1 (ring slot 7): even block -> hE
-    {
-        const long long b = 4 * gs;
-        put(b, M - 2 - colA, dotq(3, NS - 1, hE(3)), dotq(2, NS - 1, hE(2)));
+    // warm-up: rows 4gs-8 .. 4gs-1 fill ring slots 0..7; the last of them gives
+    // the hi-bin half of block 8gs (even block: hi column even taps = hh)
+#pragma unroll
+    for (int s = 0; s < NS; s++) {
+        const long long i = (4 * gs - NS + s) * M + tid - base_off;
+        wl[s] = fetch(i);
+        wh[s] = fetch(i + M2);
+    }
+    buf(8 * gs)[jh] = dot(wh, NS - 1, hh);
+    __syncthreads(); // twiddle tables ready
+
+    float2 pl[4], ph_[4];
+#pragma unroll
+    for (int r = 0; r < 4; r++) {
+        const long long i = (4 * gs + r) * M + tid - base_off;
+        pl[r] = fetch(i);
+        ph_[r] = fetch(i + M2);
     }
 
-    for (long long g = gs; g < ge; g += 4) {
+    for (long long g = gs; g < ge; g += 2) {
 #pragma unroll
-        for (int ph = 0; ph < 4; ph++) {
+        for (int ph = 0; ph < 2; ph++) {
             const long long gg = g + ph;
             if (gg < ge) {
-            const long long c0 = 2 * gg;
-            const int s0 = 2 * ph, s1 = 2 * ph + 1;
-            // both rows are fetched up front; row c0+1 enters the ring only
-            // after row c0's dot products (its slot still holds row c0-7)
-            float4 lo0, hi0, lo1, hi1;
-            load_row(c0, lo0, hi0);
-            load_row(c0 + 1, lo1, hi1);
-            win[0][s0] = make_float2(lo0.x, lo0.y);
-            win[1][s0] = make_float2(lo0.z, lo0.w);
-            win[2][s0] = make_float2(hi0.x, hi0.y);
-            win[3][s0] = make_float2(hi0.z, hi0.w);
-            const long long b0 = 4 * gg;
-            // row c0: lo bins -> blocks b0 (E), b0+1 (O); hi bins -> b0+1 (O), b0+2 (E)
-            put(b0, M2 - 2 - colA, dotq(1, s0, hE(1)), dotq(0, s0, hE(0)));
-            put(b0 + 1, M2 - 2 - colA, dotq(1, s0, hO(1)), dotq(0, s0, hO(0)));
-            put(b0 + 1, M - 2 - colA, dotq(3, s0, hO(3)), dotq(2, s0, hO(2)));
-            put(b0 + 2, M - 2 - colA, dotq(3, s0, hE(3)), dotq(2, s0, hE(2)));
-            win[0][s1] = make_float2(lo1.x, lo1.y);
-            win[1][s1] = make_float2(lo1.z, lo1.w);
-            win[2][s1] = make_float2(hi1.x, hi1.y);
-            win[3][s1] = make_float2(hi1.z, hi1.w);
-            // row c0+1: lo -> b0+2 (E), b0+3 (O); hi -> b0+3 (O), b0+4 (E)
-            put(b0 + 2, M2 - 2 - colA, dotq(1, s1, hE(1)), dotq(0, s1, hE(0)));
-            put(b0 + 3, M2 - 2 - colA, dotq(1, s1, hO(1)), dotq(0, s1, hO(0)));
-            put(b0 + 3, M - 2 - colA, dotq(3, s1, hO(3)), dotq(2, s1, hO(2)));
-            put(b0 + 4, M - 2 - colA, dotq(3, s1, hE(3)), dotq(2, s1, hE(2)));
-            __syncthreads();
+                const long long b0 = 8 * gg;
+#pragma unroll
+                for (int r = 0; r < 4; r++) {
+                    // row c = 4gg + r: completes block 2c's lo bins and block
+                    // 2c+1, starts block 2c+2's hi bins
+                    const int s = 4 * ph + r;
+                    wl[s] = pl[r];
+                    wh[s] = ph_[r];
+                    const long long bc = b0 + 2 * r;
+                    buf(bc)[jl] = dot(wl, s, hl);     // lo, even
+                    buf(bc + 1)[jl] = dot(wl, s, hh); // lo, odd
+                    buf(bc + 1)[jh] = dot(wh, s, hl); // hi, odd
+                    buf(bc + 2)[jh] = dot(wh, s, hh); // hi, even
+                }
+                if (gg + 1 < ge) {
+#pragma unroll
+                    for (int r = 0; r < 4; r++) {
+                        const long long i = (4 * (gg + 1) + r) * M + tid - base_off;
+                        pl[r] = fetch(i);
+                        ph_[r] = fetch(i + M2);
+                    }
+                }
+                __syncthreads();
 
-            // ---- one 1024-point IFFT per wave: block b0 + wave
-            {
-                const long long b = b0 + wave;
-                float2 *B = xb + (int)(b % NBUF) * BSTR;
-                float2 v[16];
+                // ---- one 1024-point IFFT per wave: block b0 + wave
+                {
+                    const long long b = b0 + wave;
+                    float2 *B = buf(b);
+                    float2 v[16];
 #pragma unroll
-                for (int k = 0; k < 16; k++) v[k] = B[lane + 64 * k];
-                dft16_bwd(v);
+                    for (int k = 0; k < 16; k++) v[k] = B[lane + 64 * k];
+                    dft16_bwd(v);
 #pragma unroll
-                for (int k1 = 1; k1 < 16; k1++) v[k1] = cmul(v[k1], tw1[k1 * 64 + lane]);
-                lds_fence();
+                    for (int k1 = 1; k1 < 16; k1++) v[k1] = cmul(v[k1], tw1[k1 * 64 + lane]);
+                    lds_fence();
 #pragma unroll
-                for (int k1 = 0; k1 < 16; k1++) B[k1 * TSTR + lane] = v[k1];
-                lds_fence();
-                const int k1 = lane >> 2, bq = lane & 3;
+                    for (int k1 = 0; k1 < 16; k1++) B[k1 * TSTR + lane] = v[k1];
+                    lds_fence();
+                    const int k1 = lane >> 2, bq = lane & 3;
 #pragma unroll
-                for (int a = 0; a < 16; a++) v[a] = B[k1 * TSTR + 4 * a + bq];
-                dft16_bwd(v);
+                    for (int a = 0; a < 16; a++) v[a] = B[k1 * TSTR + 4 * a + bq];
+                    dft16_bwd(v);
 #pragma unroll
-                for (int r = 1; r < 16; r++) v[r] = cmul(v[r], tw2[r * 4 + bq]);
-                // 4-point DFT over bq across the lane quad (radix-2 x 2):
-                // stage 1 pairs bq, bq^2; twiddle W4^{+1} on (bq=3); stage 2 pairs bq, bq^1.
-                const bool hi2 = (bq & 2) != 0, hi1 = (bq & 1) != 0;
+                    for (int r = 1; r < 16; r++) v[r] = cmul(v[r], tw2[r * 4 + bq]);
+                    // 4-point DFT over bq across the lane quad (radix-2 x 2):
+                    // stage 1 pairs bq, bq^2; twiddle W4^{+1} on bq=3; stage 2 pairs bq, bq^1
+                    const bool hi2 = (bq & 2) != 0, hi1 = (bq & 1) != 0;
 #pragma unroll
-                for (int r = 0; r < 16; r++) {
-                    float2 p = shfl_xor2(v[r], 2);
-                    float2 u = hi2 ? csub(p, v[r]) : cadd(v[r], p);
-                    if (bq == 3) u = cmul_pj(u);
-                    float2 p2 = shfl_xor2(u, 1);
-                    v[r] = hi1 ? csub(p2, u) : cadd(u, p2);
+                    for (int r = 0; r < 16; r++) {
+                        float2 p = shfl_xor2(v[r], 2);
+                        float2 u = hi2 ? csub(p, v[r]) : cadd(v[r], p);
+                        if (bq == 3) u = cmul_pj(u);
+                        float2 p2 = shfl_xor2(u, 1);
+                        v[r] = hi1 ? csub(p2, u) : cadd(u, p2);
+                    }
+                    // lane (k1, bq) holds Y[k1 + 16 r + 256 s], s = bitrev2(bq)
+                    if (b >= P.B0 && b < P.B0 + P.nblk) {
+                        const int s = ((bq & 1) << 1) | (bq >> 1);
+                        float2 *Yb = P.Y + (b - P.B0) * M + k1 + 256 * s;
+#pragma unroll
+                        for (int r = 0; r < 16; r++) st_nt(Yb + 16 * r, v[r]);
+                    }
                 }
-                // lane (k1, bq) now holds Y[k1 + 16 r + 256 s], s = bitrev2(bq)
-                if (b >= P.B0 && b < P.B0 + P.nblk) {
-                    const int s = ((bq & 1) << 1) | (bq >> 1);
-                    float2 *Yb = P.Y + (b - P.B0) * M + k1 + 256 * s;
-#pragma unroll
-                    for (int r = 0; r < 16; r++) Yb[16 * r] = v[r];
-                }
-            }
-            __syncthreads();
+                __syncthreads();
             }
         }
     }
-#undef hE
-#undef hO
 }
 
 } // namespace
@@ -291,7 +285,7 @@ extern "C" int lqk_firpfbch2_analyzer_fast(unsigned int Mch, unsigned int m, con
                                            void *stream)
 {
     if (Mch != (unsigned)M || !(m == 4 || m == 2)) return 0;
-    if (((uintptr_t)x & 15) || ((uintptr_t)hist & 15)) return 0;
+    if (((uintptr_t)x & 7) || ((uintptr_t)hist & 7)) return 0;
     if (nblocks == 0) return 1;
     hipStream_t st = (hipStream_t)stream;
     Params P;
@@ -301,13 +295,13 @@ extern "C" int lqk_firpfbch2_analyzer_fast(unsigned int Mch, unsigned int m, con
     P.B0 = B0;
     P.nblk = (long long)nblocks;
     P.Y = (float2 *)Y;
-    const long long gfirst = (B0 / 4) & ~3LL;            // group containing B0, aligned to 4 groups
-    const long long glast = (B0 + (long long)nblocks - 1) / 4; // inclusive
+    const long long gfirst = (B0 / 8) & ~1LL;             // 8-block group containing B0, even
+    const long long glast = (B0 + (long long)nblocks - 1) / 8; // inclusive
     const long long ngroups = glast - gfirst + 1;
-    // ~2 workgroups per CU, each at least 16 groups (64 blocks)
-    long long gpw = (ngroups + 511) / 512;
-    if (gpw < 16) gpw = 16;
-    gpw = (gpw + 3) & ~3LL;
+    // one workgroup per CU (LDS-bound), each at least 8 groups (64 blocks)
+    long long gpw = (ngroups + 255) / 256;
+    if (gpw < 8) gpw = 8;
+    gpw = (gpw + 1) & ~1LL;
     const long long nwg = (ngroups + gpw - 1) / gpw;
     P.gs0 = gfirst;
     P.gpw = (int)gpw;

@@ -1,0 +1,41 @@
+#!/usr/bin/env python3
+"""Short driver for profiling: the two headline kernels, a few launches each,
+device-resident synthetic data (same shapes as bench.py)."""
+import argparse
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "liquid-dsp_amd"))
+import torch  # noqa: E402
+
+import liquidmi as LQ  # noqa: E402
+
+p = argparse.ArgumentParser()
+p.add_argument("--iters", type=int, default=3)
+p.add_argument("--what", default="both", choices=["both", "pfb2", "fir"])
+a = p.parse_args()
+s = torch.cuda.Stream()
+if a.what in ("both", "pfb2"):
+    n = 1 << 27
+    x = torch.rand(2 * n, device="cuda") - 0.5
+    y = torch.empty(4 * n, device="cuda")
+    q = LQ.FirPfbch2(0, 1024, 4, 60.0)
+    q.set_stream(s.cuda_stream)
+    for _ in range(a.iters):
+        q.execute_block_dev(x.data_ptr(), n // 512, y.data_ptr())
+    q.synchronize()
+    q.destroy()
+    del x, y
+if a.what in ("both", "fir"):
+    n = 1 << 28
+    x = torch.rand(2 * n, device="cuda") - 0.5
+    y = torch.empty(2 * n, device="cuda")
+    f = LQ.FirFilt("crcf", (torch.rand(64) - 0.5).numpy())
+    f.set_stream(s.cuda_stream)
+    for _ in range(a.iters):
+        f.execute_block_dev(x.data_ptr(), n, y.data_ptr())
+    f.synchronize()
+    f.destroy()
+torch.cuda.synchronize()
+print("done")
