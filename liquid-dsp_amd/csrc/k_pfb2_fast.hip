@@ -10,15 +10,14 @@
 //        X_b[j] = sum_n h[i + nM] row[c - n][col],  i = j (b even) or j ^ M/2 (b odd),
 //    c = row of the block's newest sample.  Row c completes blocks 2c
 //    (lower bins; upper bins came from row c-1) and 2c+1, and starts 2c+2.
-//  * A workgroup (8 waves, one per CU) owns all 1024 columns: lane t holds
-//    column t (bin 511-t) and column 512+t (bin 1023-t), whose even-block taps
-//    are each other's odd-block taps, so 2 x L coefficients and an 8-deep
-//    register ring per column cover both.  Rows stream through the ring, so
-//    every input sample is read from HBM once per workgroup segment.  Four
-//    rows per iteration complete eight blocks; the next four rows are
-//    prefetched into registers while the FFTs run.
-//  * X of each block goes to an LDS ring (9 block buffers); after a barrier
-//    each wave runs one 1024-point IFFT in registers: 16-point DFT over the
+//  * A workgroup of 16 waves (1024 lanes, one workgroup per CU, 4 waves per
+//    SIMD) owns all 1024 columns, one per lane, with the column's even- and
+//    odd-block taps and an 8-deep register ring.  Rows stream through the
+//    ring, so every input sample is read from HBM once per workgroup
+//    segment.  Eight rows per iteration complete sixteen blocks; the next
+//    eight rows are prefetched into registers while the FFTs run.
+//  * X of each block goes to an LDS ring (17 block buffers, 148 KB); after a
+//    barrier each wave runs one 1024-point IFFT in registers: 16-point DFT over the
 //    lane's 16 bins (j = lane + 64k), twiddle, LDS transpose (row stride 68
 //    keeps ds_read_b64 conflict-free), 16-point DFT, twiddle, and a 4-point
 //    DFT across lane quads with DPP-level shuffles.  1/M is folded into the
@@ -37,9 +36,9 @@ namespace {
 
 constexpr int M = 1024;
 constexpr int M2 = M / 2;
-constexpr int NT = 512;
+constexpr int NT = 1024;
 constexpr int NS = 8;      // register ring depth (rows)
-constexpr int NBUF = 9;    // LDS block buffers (writes b0..b0+8, FFT reads b0..b0+7)
+constexpr int NBUF = 17;   // LDS block buffers (writes b0..b0+16, FFT reads b0..b0+15)
 constexpr int BSTR = 1088; // floats2 per block buffer (16 x 68 transpose)
 constexpr int TSTR = 68;
 
@@ -111,8 +110,8 @@ struct Params {
     long long n_in;   // input samples in this call
     long long B0;     // global index of the call's first block (parity matters)
     long long nblk;   // blocks in this call
-    long long gs0;    // first global 8-block group of workgroup 0 (even)
-    int gpw;          // groups per workgroup (even)
+    long long gs0;    // first global 16-block group of workgroup 0
+    int gpw;          // groups per workgroup
     long long gend;   // one past the last group needed
     float2 *Y;
 };
@@ -130,10 +129,10 @@ __global__ __launch_bounds__(NT, 1) void k_pfb2_an1024(Params P, const float *__
     const int lane = tid & 63;
     const int wave = tid >> 6;
 
-    for (int e = tid; e < 16 * 64; e += NT) {
-        const int k1 = e >> 6, t = e & 63;
+    {
+        const int k1 = tid >> 6, t = tid & 63;
         float2 w = tw4096[(4 * t * k1) & 4095];
-        tw1[e] = make_float2(w.x, -w.y);
+        tw1[tid] = make_float2(w.x, -w.y);
     }
     if (tid < 64) {
         const int r = tid >> 2, b = tid & 3;
@@ -141,38 +140,60 @@ __global__ __launch_bounds__(NT, 1) void k_pfb2_an1024(Params P, const float *__
         tw2[tid] = make_float2(w.x, -w.y);
     }
 
-    // lane column pair: lo column tid -> bin jl = M/2-1-tid, hi column M/2+tid
-    // -> bin jh = M-1-tid = jl ^ M/2.  Even blocks use taps h[j + nM], odd
-    // blocks h[(j ^ M/2) + nM]: the lo column's odd taps are the hi column's
-    // even taps and vice versa.  1/M folded in (exact).
-    const int jl = M2 - 1 - tid, jh = M - 1 - tid;
-    float hl[L], hh[L];
-    const float inv = 1.0f / (float)M;
+    // lane column: tid < M/2 -> lo column, bin j = M/2-1-tid, feeds blocks
+    // 2c (even taps) and 2c+1 (odd taps) from row c; tid >= M/2 -> hi column,
+    // bin j = 3M/2-1-tid, feeds 2c+1 (odd) and 2c+2 (even).  Even taps
+    // h[j + nM], odd taps h[(j ^ M/2) + nM]; 1/M folded in (exact).
+    const bool lo = tid < M2;
+    const int j = lo ? (M2 - 1 - tid) : (3 * M2 - 1 - tid);
+    // taps are re-read (L1/L2 hits) at each dot phase instead of being held
+    // in registers across the FFT phase; hsub is pre-scaled by 1/M on the host
+    const float *hpe = hsub + j * L, *hpo = hsub + (j ^ M2) * L;
+    float he[L], ho[L];
+    auto load_taps = [&]() {
+        int oe = j * L, oo = (j ^ M2) * L;
+        asm volatile("" : "+v"(oe), "+v"(oo)); // keep the reload inside the loop
 #pragma unroll
-    for (int n = 0; n < L; n++) {
-        hl[n] = hsub[jl * L + n] * inv;
-        hh[n] = hsub[jh * L + n] * inv;
-    }
+        for (int n = 0; n < L; n++) {
+            he[n] = hsub[oe + n];
+            ho[n] = hsub[oo + n];
+        }
+    };
+    (void)hpe;
+    (void)hpo;
+    load_taps();
+    // first / second block fed by row c: lo: (2c, E), (2c+1, O); hi: (2c+1, O), (2c+2, E)
+    const int dA = lo ? 0 : 1;
 
-    float2 wl[NS], wh[NS];
+    float2 w[NS];
 #pragma unroll
-    for (int s = 0; s < NS; s++) wl[s] = wh[s] = make_float2(0.f, 0.f);
+    for (int s = 0; s < NS; s++) w[s] = make_float2(0.f, 0.f);
 
     const long long gs = P.gs0 + (long long)blockIdx.x * P.gpw;
     long long ge = gs + P.gpw;
     if (ge > P.gend) ge = P.gend;
-    const long long base_off = P.B0 * M2; // stream index of local sample 0
     const long long HL = 2 * (L / 2) * M - M2;
-
-    // branch-free fetch: always-valid address, then select
-    auto fetch = [&](long long i) -> float2 {
-        const bool in_x = (i >= 0) && (i < P.n_in);
-        const bool in_h = (i < 0) && (i >= -HL);
-        const float2 *p = in_x ? P.x + i : (in_h ? P.hist + (HL + i) : P.hist);
-        const float2 v = *p;
-        return (in_x || in_h) ? v : make_float2(0.f, 0.f);
+    // Row fetches go through two buffer descriptors whose range checks do the
+    // boundary work: x (n_in samples) and the history (HL samples before x).
+    // For any row exactly one of the two byte offsets is in range (or none,
+    // past either end) and out-of-range buffer loads return 0, so the sum of
+    // both loads is the sample -- no branches, 32-bit offsets (the host keeps
+    // each launch below 2^28 samples).
+    const __amdgpu_buffer_rsrc_t rx =
+        __builtin_amdgcn_make_buffer_rsrc((void *)P.x, (short)0, (int)(P.n_in * 8), 0x00020000);
+    const __amdgpu_buffer_rsrc_t rh =
+        __builtin_amdgcn_make_buffer_rsrc((void *)P.hist, (short)0, (int)(HL * 8), 0x00020000);
+    // local index of row (8gs - NS)'s sample for this lane; rows step by M
+    const long long ibase = (8 * gs - NS) * M + (long long)tid - P.B0 * M2;
+    const unsigned ox0 = (unsigned)(ibase * 8), oh0 = (unsigned)((HL + ibase) * 8);
+    auto fetch = [&](long long c) -> float2 {
+        const unsigned k = (unsigned)(c - (8 * gs - NS)) * (unsigned)(M * 8);
+        const float2 a = __builtin_bit_cast(float2, __builtin_amdgcn_raw_buffer_load_b64(rx, ox0 + k, 0, 0));
+        const float2 b = __builtin_bit_cast(float2, __builtin_amdgcn_raw_buffer_load_b64(rh, oh0 + k, 0, 0));
+        return make_float2(a.x + b.x, a.y + b.y);
     };
-    auto dot = [&](const float2 (&w)[NS], int newest, const float (&h)[L]) -> float2 {
+    const float inv = 1.0f / (float)M; // output scale 1/M: exact for M = 2^10
+    auto dot = [&](int newest, const float (&h)[L]) -> float2 {
         float2 acc = make_float2(0.f, 0.f);
 #pragma unroll
         for (int n = 0; n < L; n++) {
@@ -180,106 +201,102 @@ __global__ __launch_bounds__(NT, 1) void k_pfb2_an1024(Params P, const float *__
             acc.x = fmaf(h[n], v.x, acc.x);
             acc.y = fmaf(h[n], v.y, acc.y);
         }
-        return acc;
+        return make_float2(acc.x * inv, acc.y * inv);
     };
-    auto buf = [&](long long b) -> float2 * { return xb + (int)(b % NBUF) * BSTR; };
 
-    // warm-up: rows 4gs-8 .. 4gs-1 fill ring slots 0..7; the last of them gives
-    // the hi-bin half of block 8gs (even block: hi column even taps = hh)
+    // warm-up: rows 8gs-8 .. 8gs-1 fill the ring; the last gives the hi-bin
+    // half of block 16gs (hi lanes, even taps)
 #pragma unroll
-    for (int s = 0; s < NS; s++) {
-        const long long i = (4 * gs - NS + s) * M + tid - base_off;
-        wl[s] = fetch(i);
-        wh[s] = fetch(i + M2);
-    }
-    buf(8 * gs)[jh] = dot(wh, NS - 1, hh);
+    for (int s = 0; s < NS; s++) w[s] = fetch(8 * gs - NS + s);
+    int slot0 = (int)((16 * gs) % NBUF); // buffer of block 16g (advances by 16 mod 17 = -1)
+    if (!lo) xb[slot0 * BSTR + j] = dot(NS - 1, he);
     __syncthreads(); // twiddle tables ready
 
-    float2 pl[4], ph_[4];
+    // next iteration's first PF rows are prefetched into registers while the
+    // FFTs run; the rest are fetched as the rows are consumed
+    constexpr int PF = 4;
+    float2 pf[PF];
 #pragma unroll
-    for (int r = 0; r < 4; r++) {
-        const long long i = (4 * gs + r) * M + tid - base_off;
-        pl[r] = fetch(i);
-        ph_[r] = fetch(i + M2);
-    }
+    for (int r = 0; r < PF; r++) pf[r] = fetch(8 * gs + r);
 
-    for (long long g = gs; g < ge; g += 2) {
+    for (long long g = gs; g < ge; g++) {
+        const long long b0 = 16 * g;
+        load_taps();
 #pragma unroll
-        for (int ph = 0; ph < 2; ph++) {
-            const long long gg = g + ph;
-            if (gg < ge) {
-                const long long b0 = 8 * gg;
+        for (int r = 0; r < 8; r++) {
+            // row c = 8g + r -> blocks b0 + 2r + dA (first), b0 + 2r + dA + 1 (second)
+            w[r] = r < PF ? pf[r] : fetch(8 * g + r);
+            int s1 = slot0 + 2 * r + dA;
+            s1 -= (s1 >= NBUF) ? NBUF : 0;
+            int s2 = s1 + 1;
+            s2 -= (s2 >= NBUF) ? NBUF : 0;
+            xb[s1 * BSTR + j] = dot(r, lo ? he : ho);
+            xb[s2 * BSTR + j] = dot(r, lo ? ho : he);
+        }
+        if (g + 1 < ge) {
 #pragma unroll
-                for (int r = 0; r < 4; r++) {
-                    // row c = 4gg + r: completes block 2c's lo bins and block
-                    // 2c+1, starts block 2c+2's hi bins
-                    const int s = 4 * ph + r;
-                    wl[s] = pl[r];
-                    wh[s] = ph_[r];
-                    const long long bc = b0 + 2 * r;
-                    buf(bc)[jl] = dot(wl, s, hl);     // lo, even
-                    buf(bc + 1)[jl] = dot(wl, s, hh); // lo, odd
-                    buf(bc + 1)[jh] = dot(wh, s, hl); // hi, odd
-                    buf(bc + 2)[jh] = dot(wh, s, hh); // hi, even
-                }
-                if (gg + 1 < ge) {
-#pragma unroll
-                    for (int r = 0; r < 4; r++) {
-                        const long long i = (4 * (gg + 1) + r) * M + tid - base_off;
-                        pl[r] = fetch(i);
-                        ph_[r] = fetch(i + M2);
-                    }
-                }
-                __syncthreads();
+            for (int r = 0; r < PF; r++) pf[r] = fetch(8 * (g + 1) + r);
+        }
+        __syncthreads();
 
-                // ---- one 1024-point IFFT per wave: block b0 + wave
-                {
-                    const long long b = b0 + wave;
-                    float2 *B = buf(b);
-                    float2 v[16];
+        // ---- one 1024-point IFFT per wave: block b0 + wave
+        {
+            const long long b = b0 + wave;
+            int sb = slot0 + wave;
+            sb -= (sb >= NBUF) ? NBUF : 0;
+            float2 *B = xb + sb * BSTR;
+            float2 v[16];
 #pragma unroll
-                    for (int k = 0; k < 16; k++) v[k] = B[lane + 64 * k];
-                    dft16_bwd(v);
+            for (int k = 0; k < 16; k++) v[k] = B[lane + 64 * k];
+            dft16_bwd(v);
+            // twiddles in groups of four: bounds the loads in flight (VGPRs)
 #pragma unroll
-                    for (int k1 = 1; k1 < 16; k1++) v[k1] = cmul(v[k1], tw1[k1 * 64 + lane]);
-                    lds_fence();
+            for (int k1 = 1; k1 < 16; k1++) {
+                if ((k1 & 3) == 0) __builtin_amdgcn_sched_barrier(0);
+                v[k1] = cmul(v[k1], tw1[k1 * 64 + lane]);
+            }
+            lds_fence();
 #pragma unroll
-                    for (int k1 = 0; k1 < 16; k1++) B[k1 * TSTR + lane] = v[k1];
-                    lds_fence();
-                    const int k1 = lane >> 2, bq = lane & 3;
+            for (int k1 = 0; k1 < 16; k1++) B[k1 * TSTR + lane] = v[k1];
+            lds_fence();
+            const int k1 = lane >> 2, bq = lane & 3;
 #pragma unroll
-                    for (int a = 0; a < 16; a++) v[a] = B[k1 * TSTR + 4 * a + bq];
-                    dft16_bwd(v);
+            for (int a = 0; a < 16; a++) v[a] = B[k1 * TSTR + 4 * a + bq];
+            dft16_bwd(v);
 #pragma unroll
-                    for (int r = 1; r < 16; r++) v[r] = cmul(v[r], tw2[r * 4 + bq]);
-                    // 4-point DFT over bq across the lane quad (radix-2 x 2):
-                    // stage 1 pairs bq, bq^2; twiddle W4^{+1} on bq=3; stage 2 pairs bq, bq^1
-                    const bool hi2 = (bq & 2) != 0, hi1 = (bq & 1) != 0;
+            for (int r = 1; r < 16; r++) {
+                if ((r & 3) == 0) __builtin_amdgcn_sched_barrier(0);
+                v[r] = cmul(v[r], tw2[r * 4 + bq]);
+            }
+            // 4-point DFT over bq across the lane quad (radix-2 x 2):
+            // stage 1 pairs bq, bq^2; twiddle W4^{+1} on bq=3; stage 2 pairs bq, bq^1
+            const bool hi2 = (bq & 2) != 0, hi1 = (bq & 1) != 0;
 #pragma unroll
-                    for (int r = 0; r < 16; r++) {
-                        float2 p = shfl_xor2(v[r], 2);
-                        float2 u = hi2 ? csub(p, v[r]) : cadd(v[r], p);
-                        if (bq == 3) u = cmul_pj(u);
-                        float2 p2 = shfl_xor2(u, 1);
-                        v[r] = hi1 ? csub(p2, u) : cadd(u, p2);
-                    }
-                    // lane (k1, bq) holds Y[k1 + 16 r + 256 s], s = bitrev2(bq)
-                    if (b >= P.B0 && b < P.B0 + P.nblk) {
-                        const int s = ((bq & 1) << 1) | (bq >> 1);
-                        float2 *Yb = P.Y + (b - P.B0) * M + k1 + 256 * s;
+            for (int r = 0; r < 16; r++) {
+                float2 p = shfl_xor2(v[r], 2);
+                float2 u = hi2 ? csub(p, v[r]) : cadd(v[r], p);
+                if (bq == 3) u = cmul_pj(u);
+                float2 p2 = shfl_xor2(u, 1);
+                v[r] = hi1 ? csub(p2, u) : cadd(u, p2);
+            }
+            // lane (k1, bq) holds Y[k1 + 16 r + 256 s], s = bitrev2(bq)
+            if (b >= P.B0 && b < P.B0 + P.nblk) {
+                const int s = ((bq & 1) << 1) | (bq >> 1);
+                float2 *Yb = P.Y + (b - P.B0) * M + k1 + 256 * s;
 #pragma unroll
-                        for (int r = 0; r < 16; r++) st_nt(Yb + 16 * r, v[r]);
-                    }
-                }
-                __syncthreads();
+                for (int r = 0; r < 16; r++) st_nt(Yb + 16 * r, v[r]);
             }
         }
+        slot0 = slot0 == 0 ? NBUF - 1 : slot0 - 1; // (16(g+1)) mod 17
+        __syncthreads();
     }
 }
 
 } // namespace
 
-// Returns 1 if handled by the fast path.
+// Returns 1 if handled by the fast path.  Launches cover at most 2^18 blocks
+// (2^27 input samples) so every buffer offset fits 31 bits; later chunks take
+// their history straight from the preceding input.
 extern "C" int lqk_firpfbch2_analyzer_fast(unsigned int Mch, unsigned int m, const void *hsub, const void *hist,
                                            const void *x, unsigned long long nblocks, long long B0, void *Y,
                                            void *stream)
@@ -288,29 +305,33 @@ extern "C" int lqk_firpfbch2_analyzer_fast(unsigned int Mch, unsigned int m, con
     if (((uintptr_t)x & 7) || ((uintptr_t)hist & 7)) return 0;
     if (nblocks == 0) return 1;
     hipStream_t st = (hipStream_t)stream;
-    Params P;
-    P.hist = (const float2 *)hist;
-    P.x = (const float2 *)x;
-    P.n_in = (long long)nblocks * M2;
-    P.B0 = B0;
-    P.nblk = (long long)nblocks;
-    P.Y = (float2 *)Y;
-    const long long gfirst = (B0 / 8) & ~1LL;             // 8-block group containing B0, even
-    const long long glast = (B0 + (long long)nblocks - 1) / 8; // inclusive
-    const long long ngroups = glast - gfirst + 1;
-    // one workgroup per CU (LDS-bound), each at least 8 groups (64 blocks)
-    long long gpw = (ngroups + 255) / 256;
-    if (gpw < 8) gpw = 8;
-    gpw = (gpw + 1) & ~1LL;
-    const long long nwg = (ngroups + gpw - 1) / gpw;
-    P.gs0 = gfirst;
-    P.gpw = (int)gpw;
-    P.gend = glast + 1;
     const float2 *tw = (const float2 *)lqrt_twiddles();
-    if (m == 4)
-        hipLaunchKernelGGL(k_pfb2_an1024<8>, dim3((unsigned)nwg), dim3(NT), 0, st, P, (const float *)hsub, tw);
-    else
-        hipLaunchKernelGGL(k_pfb2_an1024<4>, dim3((unsigned)nwg), dim3(NT), 0, st, P, (const float *)hsub, tw);
-    LQ_CHECK_LAUNCH();
+    const long long HL = 2LL * m * M - M2;
+    const long long CH = 1LL << 18;
+    for (long long ob = 0; ob < (long long)nblocks; ob += CH) {
+        const long long nb = ((long long)nblocks - ob) < CH ? ((long long)nblocks - ob) : CH;
+        Params P;
+        P.x = (const float2 *)x + ob * M2;
+        P.hist = ob == 0 ? (const float2 *)hist : P.x - HL;
+        P.n_in = nb * M2;
+        P.B0 = B0 + ob;
+        P.nblk = nb;
+        P.Y = (float2 *)Y + ob * M;
+        const long long gfirst = P.B0 / 16;                // 16-block group containing the first block
+        const long long glast = (P.B0 + nb - 1) / 16;      // inclusive
+        const long long ngroups = glast - gfirst + 1;
+        // one workgroup per CU (LDS-bound), each at least 4 groups (64 blocks)
+        long long gpw = (ngroups + 255) / 256;
+        if (gpw < 4) gpw = 4;
+        const long long nwg = (ngroups + gpw - 1) / gpw;
+        P.gs0 = gfirst;
+        P.gpw = (int)gpw;
+        P.gend = glast + 1;
+        if (m == 4)
+            hipLaunchKernelGGL(k_pfb2_an1024<8>, dim3((unsigned)nwg), dim3(NT), 0, st, P, (const float *)hsub, tw);
+        else
+            hipLaunchKernelGGL(k_pfb2_an1024<4>, dim3((unsigned)nwg), dim3(NT), 0, st, P, (const float *)hsub, tw);
+        LQ_CHECK_LAUNCH();
+    }
     return 1;
 }
