@@ -83,9 +83,15 @@ __device__ __forceinline__ void dft16_bwd(float2 (&v)[16])
     }
 }
 
-__device__ __forceinline__ float2 shfl_xor2(float2 v, int m)
+// exchange with the partner lane inside a quad through DPP (a VALU operand
+// modifier, no LDS crossbar): quad_perm [1,0,3,2] for xor 1, [2,3,0,1] for xor 2
+template <int X>
+__device__ __forceinline__ float2 quad_xor(float2 v)
 {
-    return make_float2(__shfl_xor(v.x, m, 64), __shfl_xor(v.y, m, 64));
+    constexpr int ctrl = X == 1 ? 0xB1 : 0x4E;
+    const int a = __builtin_amdgcn_mov_dpp(__float_as_int(v.x), ctrl, 0xF, 0xF, false);
+    const int b = __builtin_amdgcn_mov_dpp(__float_as_int(v.y), ctrl, 0xF, 0xF, false);
+    return make_float2(__int_as_float(a), __int_as_float(b));
 }
 
 typedef float v2f __attribute__((ext_vector_type(2)));
@@ -273,10 +279,10 @@ __global__ __launch_bounds__(NT, 1) void k_pfb2_an1024(Params P, const float *__
             const bool hi2 = (bq & 2) != 0, hi1 = (bq & 1) != 0;
 #pragma unroll
             for (int r = 0; r < 16; r++) {
-                float2 p = shfl_xor2(v[r], 2);
+                float2 p = quad_xor<2>(v[r]);
                 float2 u = hi2 ? csub(p, v[r]) : cadd(v[r], p);
                 if (bq == 3) u = cmul_pj(u);
-                float2 p2 = shfl_xor2(u, 1);
+                float2 p2 = quad_xor<1>(u);
                 v[r] = hi1 ? csub(p2, u) : cadd(u, p2);
             }
             // lane (k1, bq) holds Y[k1 + 16 r + 256 s], s = bitrev2(bq)
