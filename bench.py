@@ -54,6 +54,8 @@ def parse():
     p.add_argument("--cpu-seconds", type=float, default=10.0, help="CPU baseline budget (rank 0, N=1)")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--no-firfilt", action="store_true")
+    p.add_argument("--rs-samples", type=int, default=1 << 25, help="resamp_crcf input samples per GPU")
+    p.add_argument("--no-resamp", action="store_true")
     p.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic.json"),
                    help="PMC-derived HBM bytes per launch (from a separate rocprofv3 --pmc run)")
     return p.parse_args()
@@ -154,6 +156,29 @@ def bench_firfilt(args, world, rank, stream):
     return res
 
 
+def bench_resamp(args, world, rank, stream):
+    """configs[4]: resamp_crcf r=1.037, npfb=64, m=7 on 32M samples per GPU"""
+    n = args.rs_samples
+    rate = 1.037
+    x = synth_complex(n, 4242 + rank)
+    y = torch.empty(2 * (int(n * rate) + 4096), dtype=torch.float32, device="cuda")
+    q = LQ.Resamp(rate, 7, 0.25, 60.0, 64)
+    q.set_stream(stream.cuda_stream)
+    nys = []
+
+    def step():
+        nys.append(q.execute_block_dev(x.data_ptr(), n, y.data_ptr()))
+
+    q.num_output(n)          # builds the periodic timing plan before timing
+    wall, gpu_ms = time_steps(step, args.steps, args.warmup, world, stream)
+    nout = sum(nys[args.warmup:])
+    res = {"n": n, "wall": wall, "gpu_ms": gpu_ms, "nout": nout}
+    q.destroy()
+    del x, y
+    torch.cuda.empty_cache()
+    return res
+
+
 def copy_bandwidth():
     """Measured device copy rate (read+write GB/s) as a practical HBM ceiling."""
     a = torch.empty(1 << 28, dtype=torch.float32, device="cuda")
@@ -216,6 +241,13 @@ def main():
         g_fir = allreduce_max(fir["gpu_ms"], world)
         tot_fir = allreduce_sum(fir["n"] * args.steps, world)
 
+    rs = None
+    if not args.no_resamp:
+        rs = bench_resamp(args, world, rank, stream)
+        t_rs = allreduce_max(rs["wall"], world)
+        g_rs = allreduce_max(rs["gpu_ms"], world)
+        tot_rs = allreduce_sum(rs["n"] * args.steps, world)
+
     copy_gbps = copy_bandwidth() if rank == 0 else None
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
@@ -227,11 +259,13 @@ def main():
         launch_ms = g_pfb / args.steps
         alg_bytes = 24.0 * pfb["n"]
         achieved = alg_bytes / (launch_ms * 1e-3) / 1e9
-        traffic = None
+        traffic = fir_traffic = rs_traffic = None
         if os.path.exists(args.traffic_json):
             with open(args.traffic_json) as f:
                 tj = json.load(f)
             traffic = tj.get("firpfbch2_bytes_per_launch")
+            fir_traffic = tj.get("firfilt_bytes_per_launch")
+            rs_traffic = tj.get("resamp_bytes_per_launch")
         out = {
             "metric": "Msamples/s: firfilt_crcf h=64 & firpfbch2_crcf M=1024; %HBM roofline",
             "value": tot_pfb / t_pfb / 1e6,
@@ -261,7 +295,21 @@ def main():
                                        "samples_per_gpu": fir["n"], "ms_per_step": t_fir / args.steps * 1e3,
                                        "roofline": {"bound": "hbm", "achieved": fach, "peak": HBM_PEAK_GBPS,
                                                     "unit": "GB/s", "frac": fach / HBM_PEAK_GBPS,
+                                                    "traffic": fir_traffic,
                                                     "bytes_per_unit": "16 B/sample", "launch_ms": fl_ms}}
+        if rs is not None:
+            rl_ms = g_rs / args.steps
+            rbytes = 8.0 * rs["n"] + 8.0 * rs["nout"] / args.steps
+            rach = rbytes / (rl_ms * 1e-3) / 1e9
+            out["resamp_crcf_r1037"] = {"value": tot_rs / t_rs / 1e6, "unit": "Msamples/s (input)",
+                                        "workload": "resamp_crcf r=1.037 m=7 npfb=64 (BASELINE configs[4])",
+                                        "samples_per_gpu": rs["n"], "outputs_per_step": rs["nout"] / args.steps,
+                                        "ms_per_step": t_rs / args.steps * 1e3,
+                                        "roofline": {"bound": "hbm", "achieved": rach, "peak": HBM_PEAK_GBPS,
+                                                     "unit": "GB/s", "frac": rach / HBM_PEAK_GBPS,
+                                                     "traffic": rs_traffic,
+                                                     "bytes_per_unit": "8 B/input + 8 B/output",
+                                                     "launch_ms": rl_ms}}
         print(json.dumps(out))
     if world > 1:
         dist.barrier()

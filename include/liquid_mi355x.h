@@ -147,6 +147,53 @@ void firinterp_crcf_execute_block_dev(firinterp_crcf _q, const liquid_float_comp
 void firinterp_crcf_set_stream(firinterp_crcf _q, void *_hip_stream);
 
 /* ------------------------------------------------------------------------ */
+/* firpfb (liquid.h:2392-2486): crcf                                         */
+/* ------------------------------------------------------------------------ */
+typedef struct firpfb_crcf_s *firpfb_crcf;
+firpfb_crcf firpfb_crcf_create(unsigned int _M, float *_h, unsigned int _h_len);
+firpfb_crcf firpfb_crcf_create_kaiser(unsigned int _M, unsigned int _m, float _fc, float _As);
+firpfb_crcf firpfb_crcf_recreate(firpfb_crcf _q, unsigned int _M, float *_h, unsigned int _h_len);
+void firpfb_crcf_destroy(firpfb_crcf _q);
+void firpfb_crcf_print(firpfb_crcf _q);
+void firpfb_crcf_set_scale(firpfb_crcf _q, float _g);
+void firpfb_crcf_reset(firpfb_crcf _q);
+void firpfb_crcf_push(firpfb_crcf _q, liquid_float_complex _x);
+void firpfb_crcf_execute(firpfb_crcf _q, unsigned int _i, liquid_float_complex *_y);
+/* extension: push each of _n inputs and evaluate every bank after it:
+ * _y[t*M + i] = execute(i) after push(_x[t]); host / device pointers */
+void firpfb_crcf_execute_block(firpfb_crcf _q, liquid_float_complex *_x, unsigned long long _n,
+                               liquid_float_complex *_y);
+void firpfb_crcf_execute_block_dev(firpfb_crcf _q, const liquid_float_complex *_dx,
+                                   unsigned long long _n, liquid_float_complex *_dy);
+void firpfb_crcf_set_stream(firpfb_crcf _q, void *_hip_stream);
+
+/* ------------------------------------------------------------------------ */
+/* resamp (liquid.h:2938-3015): crcf                                         */
+/* ------------------------------------------------------------------------ */
+typedef struct resamp_crcf_s *resamp_crcf;
+resamp_crcf resamp_crcf_create(float _rate, unsigned int _m, float _fc, float _As, unsigned int _npfb);
+resamp_crcf resamp_crcf_create_default(float _rate);
+void resamp_crcf_destroy(resamp_crcf _q);
+void resamp_crcf_print(resamp_crcf _q);
+void resamp_crcf_reset(resamp_crcf _q);
+unsigned int resamp_crcf_get_delay(resamp_crcf _q);
+void resamp_crcf_set_rate(resamp_crcf _q, float _rate);
+void resamp_crcf_adjust_rate(resamp_crcf _q, float _delta);
+void resamp_crcf_execute(resamp_crcf _q, liquid_float_complex _x, liquid_float_complex *_y,
+                         unsigned int *_num_written);
+void resamp_crcf_execute_block(resamp_crcf _q, liquid_float_complex *_x, unsigned int _nx,
+                               liquid_float_complex *_y, unsigned int *_ny);
+/* extension: number of outputs the next _nx inputs will produce (size _y with it) */
+unsigned long long resamp_crcf_num_output(resamp_crcf _q, unsigned long long _nx);
+/* extension: device pointers, asynchronous on the object's stream; *_ny is
+ * known (and written) before the call returns */
+void resamp_crcf_execute_block_dev(resamp_crcf _q, const liquid_float_complex *_dx,
+                                   unsigned long long _nx, liquid_float_complex *_dy,
+                                   unsigned long long *_ny);
+void resamp_crcf_set_stream(resamp_crcf _q, void *_hip_stream);
+void resamp_crcf_synchronize(resamp_crcf _q);
+
+/* ------------------------------------------------------------------------ */
 /* fftfilt (liquid.h:2192-2240): crcf                                        */
 /* ------------------------------------------------------------------------ */
 typedef struct fftfilt_crcf_s *fftfilt_crcf;

@@ -1,0 +1,244 @@
+// k_resamp.hip -- arbitrary-rate polyphase resampler (resamp_crcf) and the
+// per-sample firpfb_crcf output.
+//
+// Reference: src/filter/src/resamp.c:245-363 (execute, update_timing_state),
+// src/filter/src/firpfb.c:325-345 (bank output).  For input t the reference
+// emits, while b < npfb, outputs
+//     y = (1-mu) * y0 + mu * y1,   y_b(t) = sum_n h[b + n*npfb] x[t-n]  (n < L = 2m)
+// with (y0, y1) = (y_b(t), y_{b+1}(t)) in the INTERP state and
+// (y_{npfb-1}(t-1), y_0(t)) in the BOUNDARY state, then advances the float32
+// timing phase tau += 1/r, b = floor(tau*npfb), mu = tau*npfb - b.
+//
+// Parallel form.  The timing state at the start of every input is a pure
+// function of the previous one (it does not depend on the data), so the host
+// tabulates it once per rate (`plan`, see host/resamp.c): entry j holds
+// (tau, mu, b, state) before input j and K[j] = outputs emitted by inputs
+// < j; the sequence is eventually periodic (pre-period `pre`, period `P`
+// inputs, `Q` outputs per period).  Each lane takes R consecutive inputs,
+// reads its one entry and replays the reference's float32 recurrence
+// bit-exactly for those R inputs (contraction off), with the last L+R inputs
+// in registers.  Outputs go straight to y[K - K0].
+#include <hip/hip_runtime.h>
+
+#include "lq_device.h"
+#include "lq_kernels.h"
+
+namespace {
+
+constexpr int NT = 256;
+constexpr int RS_R = 8;
+
+struct rs_state {
+    float tau, mu;
+    int b, st; // st: 1 INTERP, 0 BOUNDARY
+};
+
+// the reference's update_timing_state (resamp.c:352-363), IEEE float32, no FMA
+__device__ __forceinline__ void rs_advance(rs_state &s, float del, float fnpfb)
+{
+#pragma clang fp contract(off)
+    s.tau = s.tau + del;
+    const float bf = s.tau * fnpfb;
+    const float fb = __builtin_floorf(bf);
+    s.b = (int)fb;
+    s.mu = bf - fb;
+}
+
+__device__ __forceinline__ void rs_lookup(const lqk_rs_plan &pl, unsigned long long g, rs_state &s,
+                                          unsigned long long &K)
+{
+    unsigned long long j = g, add = 0;
+    if (g >= pl.pre) {
+        const unsigned long long t = g - pl.pre;
+        const unsigned long long c = t / pl.P;
+        j = pl.pre + (t - c * pl.P);
+        add = c * pl.Q;
+    }
+    const lqk_rs_entry e = pl.tab[j];
+    s.tau = e.tau;
+    s.mu = e.mu;
+    s.b = e.bst >> 1;
+    s.st = e.bst & 1;
+    K = (unsigned long long)e.K + add;
+}
+
+// taps[b*L + n] = (h[b + n*npfb], h[(b+1)%npfb + n*npfb]) -- the (y0, y1) pair
+template <int L>
+__global__ __launch_bounds__(NT) void k_resamp(lqk_rs_plan pl, unsigned long long g0, unsigned long long K0,
+                                               int npfb, float del, const float2 *__restrict__ taps,
+                                               const float2 *__restrict__ hist, const float2 *__restrict__ x,
+                                               long long n, float2 *__restrict__ y)
+{
+    extern __shared__ float2 stp[];
+    for (int t = threadIdx.x; t < npfb * L; t += NT) stp[t] = taps[t];
+    __syncthreads();
+
+    const long long i0 = ((long long)blockIdx.x * NT + threadIdx.x) * RS_R;
+    if (i0 >= n) return;
+    rs_state s;
+    unsigned long long K;
+    rs_lookup(pl, g0 + (unsigned long long)i0, s, K);
+    float2 *yo = y + (K - K0);
+
+    // w[k] = x[i0 - L + k]; samples before the call come from the history
+    float2 w[L + RS_R];
+#pragma unroll
+    for (int k = 0; k < L + RS_R; ++k) {
+        const long long idx = i0 - L + k;
+        float2 v = make_float2(0.f, 0.f);
+        if (idx < 0) v = hist[L + idx];
+        else if (idx < n) v = x[idx];
+        w[k] = v;
+    }
+    const float fnpfb = (float)npfb;
+#pragma unroll
+    for (int r = 0; r < RS_R; ++r) {
+        if (i0 + r >= n) break;
+        while (s.b < npfb) {
+            if (s.st && s.b == npfb - 1) { // last filter: finish with the next input
+                s.st = 0;
+                s.b = npfb;
+                break;
+            }
+            const bool bnd = !s.st;
+            const float2 *tp = stp + (bnd ? npfb - 1 : s.b) * L;
+            float2 a0 = make_float2(0.f, 0.f), a1 = make_float2(0.f, 0.f);
+#pragma unroll
+            for (int k = 0; k < L; ++k) {
+                const float2 t = tp[k];
+                const float2 xb = w[L + r - k];
+                const float2 xa = bnd ? w[L + r - 1 - k] : xb;
+                a0.x += t.x * xa.x;
+                a0.y += t.x * xa.y;
+                a1.x += t.y * xb.x;
+                a1.y += t.y * xb.y;
+            }
+            const float c0 = 1.0f - s.mu;
+            *yo++ = make_float2(c0 * a0.x + s.mu * a1.x, c0 * a0.y + s.mu * a1.y);
+            rs_advance(s, del, fnpfb);
+            s.st = 1;
+        }
+        s.tau -= 1.0f;
+        s.b -= npfb;
+    }
+}
+
+// any L (window and taps read through the caches), one input per lane
+__global__ __launch_bounds__(NT) void k_resamp_generic(lqk_rs_plan pl, unsigned long long g0,
+                                                       unsigned long long K0, int npfb, int L, float del,
+                                                       const float2 *__restrict__ taps,
+                                                       const float2 *__restrict__ hist,
+                                                       const float2 *__restrict__ x, long long n,
+                                                       float2 *__restrict__ y)
+{
+    const long long i = (long long)blockIdx.x * NT + threadIdx.x;
+    if (i >= n) return;
+    rs_state s;
+    unsigned long long K;
+    rs_lookup(pl, g0 + (unsigned long long)i, s, K);
+    float2 *yo = y + (K - K0);
+    auto X = [&](long long idx) -> float2 { return idx < 0 ? hist[L + idx] : x[idx]; };
+    const float fnpfb = (float)npfb;
+    while (s.b < npfb) {
+        if (s.st && s.b == npfb - 1) break;
+        const bool bnd = !s.st;
+        const float2 *tp = taps + (size_t)(bnd ? npfb - 1 : s.b) * L;
+        float2 a0 = make_float2(0.f, 0.f), a1 = make_float2(0.f, 0.f);
+        for (int k = 0; k < L; ++k) {
+            const float2 t = tp[k];
+            const float2 xb = X(i - k);
+            const float2 xa = bnd ? X(i - 1 - k) : xb;
+            a0.x += t.x * xa.x;
+            a0.y += t.x * xa.y;
+            a1.x += t.y * xb.x;
+            a1.y += t.y * xb.y;
+        }
+        const float c0 = 1.0f - s.mu;
+        *yo++ = make_float2(c0 * a0.x + s.mu * a1.x, c0 * a0.y + s.mu * a1.y);
+        rs_advance(s, del, fnpfb);
+        s.st = 1;
+    }
+}
+
+// firpfb_execute(i): y = scale * sum_n hpoly[i*L + n] win[L-1-n]
+__global__ void k_firpfb_single(const float *__restrict__ hpoly, int L, int i, const float2 *__restrict__ win,
+                                float scale, float2 *y)
+{
+    __shared__ float2 part[64];
+    float2 acc = make_float2(0.f, 0.f);
+    for (int k = threadIdx.x; k < L; k += 64) {
+        const float h = hpoly[(size_t)i * L + k];
+        const float2 v = win[L - 1 - k];
+        acc.x += h * v.x;
+        acc.y += h * v.y;
+    }
+    part[threadIdx.x] = acc;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        float2 s = make_float2(0.f, 0.f);
+        for (int t = 0; t < 64; ++t) s = cadd(s, part[t]);
+        y[0] = make_float2(s.x * scale, s.y * scale);
+    }
+}
+
+template <int L>
+void launch_rs(const lqk_rs_plan &pl, unsigned long long g0, unsigned long long K0, int npfb, float del,
+               const float2 *taps, const float2 *hist, const float2 *x, long long n, float2 *y, hipStream_t st)
+{
+    const long long lanes = (n + RS_R - 1) / RS_R;
+    const unsigned nb = (unsigned)((lanes + NT - 1) / NT);
+    hipLaunchKernelGGL(k_resamp<L>, dim3(nb), dim3(NT), (size_t)npfb * L * sizeof(float2), st, pl, g0, K0, npfb,
+                       del, taps, hist, x, n, y);
+}
+
+} // namespace
+
+extern "C" void lqk_resamp(const lqk_rs_plan *pl, unsigned long long g0, unsigned long long K0,
+                           unsigned int npfb, unsigned int L, float del, const void *taps, const void *hist,
+                           const void *x, unsigned long long n, void *y, void *stream)
+{
+    if (n == 0) return;
+    hipStream_t st = (hipStream_t)stream;
+    const float2 *tp = (const float2 *)taps, *hs = (const float2 *)hist, *xi = (const float2 *)x;
+    float2 *yo = (float2 *)y;
+    const long long nn = (long long)n;
+    const bool lds_ok = (size_t)npfb * L * sizeof(float2) <= 64 * 1024;
+#define LQ_RS_CASE(LL)                                                                                     \
+    case LL:                                                                                               \
+        launch_rs<LL>(*pl, g0, K0, (int)npfb, del, tp, hs, xi, nn, yo, st);                               \
+        break;
+    if (lds_ok && L <= 32 && (L % 2) == 0) {
+        switch (L) {
+            LQ_RS_CASE(2)
+            LQ_RS_CASE(4)
+            LQ_RS_CASE(6)
+            LQ_RS_CASE(8)
+            LQ_RS_CASE(10)
+            LQ_RS_CASE(12)
+            LQ_RS_CASE(14)
+            LQ_RS_CASE(16)
+            LQ_RS_CASE(18)
+            LQ_RS_CASE(20)
+            LQ_RS_CASE(22)
+            LQ_RS_CASE(24)
+            LQ_RS_CASE(26)
+            LQ_RS_CASE(28)
+            LQ_RS_CASE(30)
+            LQ_RS_CASE(32)
+        }
+    } else {
+        const unsigned nb = (unsigned)((n + NT - 1) / NT);
+        hipLaunchKernelGGL(k_resamp_generic, dim3(nb), dim3(NT), 0, st, *pl, g0, K0, (int)npfb, (int)L, del, tp, hs,
+                           xi, nn, yo);
+    }
+#undef LQ_RS_CASE
+    LQ_CHECK_LAUNCH();
+}
+
+extern "C" void lqk_firpfb_single(const void *hpoly, unsigned int L, unsigned int i, const void *win, float scale,
+                                  void *y, void *stream)
+{
+    hipLaunchKernelGGL(k_firpfb_single, dim3(1), dim3(64), 0, (hipStream_t)stream, (const float *)hpoly, (int)L,
+                       (int)i, (const float2 *)win, scale, (float2 *)y);
+    LQ_CHECK_LAUNCH();
+}

@@ -115,6 +115,29 @@ void lqk_fftfilt_run(int real_io, unsigned int hlen, const void *H, const void *
 void lqk_fftfilt_make_H(const void *h_dev, unsigned int hlen, int is_complex, void *H, void *stream);
 unsigned int lqk_fftfilt_nfft(void);
 
+/* ---------------------------------------------------------------- resamp / firpfb
+ * Timing plan: entry j = the resampler's timing state before input j of the
+ * plan (tau, mu, b, state; bst = b*2 + (state == INTERP)) and K = outputs
+ * emitted by the plan's inputs < j.  Inputs g >= pre repeat with period P
+ * (Q outputs per period): entry(g) = entry(pre + (g-pre) % P), K += Q per period. */
+typedef struct {
+    float tau, mu;
+    int bst;
+    unsigned int K;
+} lqk_rs_entry;
+typedef struct {
+    const lqk_rs_entry *tab;   /* device */
+    unsigned long long pre, P, Q;
+} lqk_rs_plan;
+/* n inputs x (plan positions g0 .. g0+n) -> outputs y[K(g) - K0 ...];
+ * taps: npfb x L pairs (h[b + n*npfb], h[(b+1)%npfb + n*npfb]); hist = last L inputs */
+void lqk_resamp(const lqk_rs_plan *pl, unsigned long long g0, unsigned long long K0, unsigned int npfb,
+                unsigned int L, float del, const void *taps, const void *hist, const void *x,
+                unsigned long long n, void *y, void *stream);
+/* firpfb_execute(i): y = scale * sum_n hpoly[i*L + n] win[L-1-n] (win: L samples, oldest first) */
+void lqk_firpfb_single(const void *hpoly, unsigned int L, unsigned int i, const void *win, float scale,
+                       void *y, void *stream);
+
 #ifdef __cplusplus
 }
 #endif

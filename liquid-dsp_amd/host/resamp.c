@@ -1,0 +1,659 @@
+/*
+ * resamp.c -- firpfb_crcf and resamp_crcf on the MI355X.
+ *
+ * firpfb: include/liquid.h:2392-2486, src/filter/src/firpfb.c:46-345.
+ *   Bank i = h[i + n*M], n < L = floor(h_len/M); push() appends one sample,
+ *   execute(i) = scale * sum_n h[i + n*M] x[t-n].
+ * resamp: include/liquid.h:2938-3015, src/filter/src/resamp.c:79-363.
+ *   Prototype 2*m*npfb+1 Kaiser taps at fc/npfb scaled by npfb/sum(h); bank
+ *   from the first 2*m*npfb taps (L = 2m); per input the float32 timing
+ *   state machine emits (1-mu) y0 + mu y1 outputs.
+ *
+ * The resampler's timing state (tau, b, mu, INTERP/BOUNDARY) evolves
+ * independently of the data, so it is tabulated on the host -- a "plan" --
+ * and the GPU replays it: entry j = state before input j, K[j] = outputs
+ * before input j.  The float32 recurrence visits a finite set of states and
+ * is eventually periodic (r = 1.037, npfb = 64: period 1 011 163 inputs);
+ * for calls of >= RS_PERIODIC_MIN inputs the pre-period and period are found
+ * once per rate with Brent's cycle detection and the plan is reused for every
+ * later call.  Short calls (and rates whose period exceeds RS_MAX_PERIOD)
+ * get a plan covering just that call.  Every output sample is computed on
+ * the GPU (csrc/k_resamp.hip).
+ */
+#include <math.h>
+
+#include "lq_host.h"
+
+/* ================================================================== firpfb */
+
+struct firpfb_crcf_s {
+    unsigned int M, hlen, L;
+    float scale;
+    float *hpoly;                 /* M x L, hpoly[i*L + n] = h[i + n*M] */
+    void *d_hpoly;
+    void *d_win[2];               /* last L inputs, oldest first */
+    int cur;
+    liquid_float_complex *h_win;  /* host mirror for push() */
+    int host_valid, dev_valid;
+    lq_ctx ctx;
+    lq_devbuf xbuf, ybuf, one;
+};
+
+firpfb_crcf firpfb_crcf_create(unsigned int _M, float *_h, unsigned int _h_len)
+{
+    if (_M == 0) LQ_FAIL("error: firpfb_crcf_create(), number of filters must be greater than zero\n");
+    if (_h_len == 0) LQ_FAIL("error: firpfb_crcf_create(), filter length must be greater than zero\n");
+    if (_h_len < _M) LQ_FAIL("error: firpfb_crcf_create(), filter length must be at least the number of filters\n");
+    lqrt_require_device("firpfb_crcf_create");
+    firpfb_crcf q = (firpfb_crcf)lq_xmalloc(sizeof(*q));
+    q->M = _M;
+    q->hlen = _h_len;
+    q->L = _h_len / _M;
+    q->scale = 1.0f;
+    q->hpoly = (float *)lq_xmalloc((size_t)_M * q->L * sizeof(float));
+    for (unsigned int i = 0; i < _M; i++)
+        for (unsigned int n = 0; n < q->L; n++) q->hpoly[i * q->L + n] = _h[i + n * _M];
+    lq_ctx_init(&q->ctx);
+    q->d_hpoly = lqrt_malloc((size_t)_M * q->L * sizeof(float));
+    lqrt_h2d(q->d_hpoly, q->hpoly, (size_t)_M * q->L * sizeof(float), q->ctx.stream);
+    q->d_win[0] = lqrt_malloc((size_t)q->L * 8);
+    q->d_win[1] = lqrt_malloc((size_t)q->L * 8);
+    q->h_win = (liquid_float_complex *)lq_xmalloc((size_t)q->L * 8);
+    q->host_valid = q->dev_valid = 1;
+    lqrt_sync(q->ctx.stream);
+    return q;
+}
+
+firpfb_crcf firpfb_crcf_create_kaiser(unsigned int _M, unsigned int _m, float _fc, float _As)
+{
+    if (_M == 0) LQ_FAIL("error: firpfb_crcf_create_kaiser(), number of filters must be greater than zero\n");
+    if (_m == 0) LQ_FAIL("error: firpfb_crcf_create_kaiser(), filter delay must be greater than 0\n");
+    if (_fc < 0.0f || _fc > 0.5f)
+        LQ_FAIL("error: firpfb_crcf_create_kaiser(), filter cut-off frequence must be in (0,0.5)\n");
+    if (_As < 0.0f)
+        LQ_FAIL("error: firpfb_crcf_create_kaiser(), filter excess bandwidth factor must be in [0,1]\n");
+    unsigned int n = 2 * _M * _m + 1;
+    float *hf = (float *)lq_xmalloc(n * sizeof(float));
+    lq_firdes_kaiser(n, _fc / (float)_M, _As, 0.0f, hf);
+    firpfb_crcf q = firpfb_crcf_create(_M, hf, n);
+    free(hf);
+    return q;
+}
+
+void firpfb_crcf_destroy(firpfb_crcf _q)
+{
+    lqrt_sync(_q->ctx.stream);
+    lqrt_free(_q->d_hpoly);
+    lqrt_free(_q->d_win[0]);
+    lqrt_free(_q->d_win[1]);
+    lq_devbuf_free(&_q->xbuf);
+    lq_devbuf_free(&_q->ybuf);
+    lq_devbuf_free(&_q->one);
+    lq_ctx_free(&_q->ctx);
+    free(_q->hpoly);
+    free(_q->h_win);
+    free(_q);
+}
+
+/* firpfb.c:250-277: a shape change re-creates the object */
+firpfb_crcf firpfb_crcf_recreate(firpfb_crcf _q, unsigned int _M, float *_h, unsigned int _h_len)
+{
+    if (_h_len != _q->hlen || _M != _q->M) {
+        firpfb_crcf_destroy(_q);
+        return firpfb_crcf_create(_M, _h, _h_len);
+    }
+    for (unsigned int i = 0; i < _M; i++)
+        for (unsigned int n = 0; n < _q->L; n++) _q->hpoly[i * _q->L + n] = _h[i + n * _M];
+    lqrt_sync(_q->ctx.stream);
+    lqrt_h2d(_q->d_hpoly, _q->hpoly, (size_t)_M * _q->L * sizeof(float), _q->ctx.stream);
+    lqrt_sync(_q->ctx.stream);
+    return _q;
+}
+
+void firpfb_crcf_print(firpfb_crcf _q)
+{
+    printf("fir polyphase filterbank [%u] :\n", _q->M);
+    for (unsigned int i = 0; i < _q->M; i++) printf("  bank %3u: \n", i);
+}
+
+void firpfb_crcf_set_scale(firpfb_crcf _q, float _g) { _q->scale = _g; }
+
+void firpfb_crcf_reset(firpfb_crcf _q)
+{
+    lqrt_memset(_q->d_win[0], (size_t)_q->L * 8, _q->ctx.stream);
+    lqrt_memset(_q->d_win[1], (size_t)_q->L * 8, _q->ctx.stream);
+    lqrt_sync(_q->ctx.stream);
+    memset(_q->h_win, 0, (size_t)_q->L * 8);
+    _q->host_valid = _q->dev_valid = 1;
+}
+
+static void firpfb_need_host(firpfb_crcf q)
+{
+    if (q->host_valid) return;
+    lqrt_d2h(q->h_win, q->d_win[q->cur], (size_t)q->L * 8, q->ctx.stream);
+    lqrt_sync(q->ctx.stream);
+    q->host_valid = 1;
+}
+
+static void firpfb_need_dev(firpfb_crcf q)
+{
+    if (q->dev_valid) return;
+    lqrt_h2d(q->d_win[q->cur], q->h_win, (size_t)q->L * 8, q->ctx.stream);
+    q->dev_valid = 1;
+}
+
+void firpfb_crcf_push(firpfb_crcf _q, liquid_float_complex _x)
+{
+    firpfb_need_host(_q);
+    memmove(_q->h_win, _q->h_win + 1, (size_t)(_q->L - 1) * 8);
+    _q->h_win[_q->L - 1] = _x;
+    _q->dev_valid = 0;
+}
+
+void firpfb_crcf_execute(firpfb_crcf _q, unsigned int _i, liquid_float_complex *_y)
+{
+    if (_i >= _q->M)
+        LQ_FAIL("error: firpfb_execute(), filterbank index (%u) exceeds maximum (%u)\n", _i, _q->M);
+    firpfb_need_dev(_q);
+    void *dy = lq_devbuf_get(&_q->one, 16);
+    lqk_firpfb_single(_q->d_hpoly, _q->L, _i, _q->d_win[_q->cur], _q->scale, dy, _q->ctx.stream);
+    lqrt_d2h(_y, dy, 8, _q->ctx.stream);
+    lqrt_sync(_q->ctx.stream);
+}
+
+void firpfb_crcf_execute_block_dev(firpfb_crcf _q, const liquid_float_complex *_dx, unsigned long long _n,
+                                   liquid_float_complex *_dy)
+{
+    if (_n == 0) return;
+    firpfb_need_dev(_q);
+    void *wold = _q->d_win[_q->cur], *wnew = _q->d_win[_q->cur ^ 1];
+    /* bank outputs after each push: the interpolator kernel (y[t*M+i]) on
+     * the window's last L-1 samples as history */
+    lqk_firinterp(LQ_CRCF, _q->d_hpoly, _q->M, _q->L, _q->scale, (const char *)wold + 8, _dx, _n, _dy,
+                  _q->ctx.stream);
+    lqk_window_append(1, wold, _q->L, _dx, _n, wnew, _q->ctx.stream);
+    _q->cur ^= 1;
+    _q->host_valid = 0;
+}
+
+void firpfb_crcf_execute_block(firpfb_crcf _q, liquid_float_complex *_x, unsigned long long _n,
+                               liquid_float_complex *_y)
+{
+    if (_n == 0) return;
+    size_t nin = (size_t)_n * 8, nout = nin * _q->M;
+    void *dx = lq_devbuf_get(&_q->xbuf, nin);
+    void *dy = lq_devbuf_get(&_q->ybuf, nout);
+    lqrt_h2d(dx, _x, nin, _q->ctx.stream);
+    firpfb_crcf_execute_block_dev(_q, (const liquid_float_complex *)dx, _n, (liquid_float_complex *)dy);
+    lqrt_d2h(_y, dy, nout, _q->ctx.stream);
+    lqrt_sync(_q->ctx.stream);
+}
+
+void firpfb_crcf_set_stream(firpfb_crcf _q, void *_s) { lq_ctx_set_stream(&_q->ctx, _s); }
+
+/* ================================================================== resamp */
+
+#define RS_PERIODIC_MIN (1ull << 16)   /* calls at least this long use (and build) a periodic plan */
+#define RS_MAX_PERIOD (1ull << 25)     /* give up on periodic plans beyond this many inputs */
+#define RS_DIRECT_CHUNK (1ull << 24)   /* direct plans cover at most this many inputs */
+
+enum { RS_BOUNDARY = 0, RS_INTERP = 1 };
+
+typedef struct {
+    float tau, mu;
+    int b, st;
+} rs_state;
+
+typedef struct {
+    int valid, periodic;
+    rs_state origin;
+    lqk_rs_entry *tab;            /* host copy */
+    size_t nent, cap;
+    lq_devbuf d_tab;
+    unsigned long long pre, P, Q;
+} rs_plan;
+
+struct resamp_crcf_s {
+    float rate, del, fc, As;
+    unsigned int m, npfb, L;
+    void *d_taps;                 /* npfb x L float pairs (bank b, bank b+1) */
+    rs_plan pl;
+    int periodic_failed;          /* no period <= RS_MAX_PERIOD at this rate */
+    unsigned long long gpos;      /* inputs consumed since the plan origin */
+    rs_state now;                 /* timing state at gpos */
+    void *d_hist[2];              /* last L inputs */
+    int cur;
+    lq_ctx ctx;
+    lq_devbuf xbuf, ybuf;
+};
+
+static const rs_state rs_initial = {0.0f, 0.0f, 0, RS_INTERP};   /* resamp.c:181-195 */
+
+static int rs_eq(const rs_state *a, const rs_state *b)
+{
+    return memcmp(&a->tau, &b->tau, 4) == 0 && memcmp(&a->mu, &b->mu, 4) == 0 && a->b == b->b && a->st == b->st;
+}
+
+/* one input of resamp.c:245-311 with the data path removed; returns the
+ * number of outputs.  float32 arithmetic exactly as the reference (the
+ * library is compiled with -ffp-contract=off) */
+static unsigned int rs_step(rs_state *s, float del, unsigned int npfb)
+{
+    unsigned int n = 0;
+    const int np = (int)npfb;
+    while (s->b < np) {
+        if (s->st == RS_INTERP && s->b == np - 1) {
+            s->st = RS_BOUNDARY;
+            s->b = np;
+            break;
+        }
+        n++;
+        s->tau += del;                              /* resamp.c:352-363 */
+        float bf = s->tau * (float)npfb;
+        s->b = (int)floorf(bf);
+        s->mu = bf - (float)s->b;
+        s->st = RS_INTERP;
+    }
+    s->tau -= 1.0f;                                 /* resamp.c:305-307 */
+    s->b -= np;
+    return n;
+}
+
+static void rs_put(lqk_rs_entry *e, const rs_state *s, unsigned long long K)
+{
+    e->tau = s->tau;
+    e->mu = s->mu;
+    e->bst = s->b * 2 + s->st;
+    e->K = (unsigned int)K;
+}
+
+static rs_state rs_get(const lqk_rs_entry *e)
+{
+    rs_state s = {e->tau, e->mu, e->bst >> 1, e->bst & 1};
+    return s;
+}
+
+static void rs_plan_reserve(rs_plan *pl, size_t n)
+{
+    if (n > pl->cap) {
+        free(pl->tab);
+        pl->tab = (lqk_rs_entry *)lq_xmalloc(n * sizeof(lqk_rs_entry));
+        pl->cap = n;
+    }
+}
+
+/* plan entry index and K for plan position g */
+static const lqk_rs_entry *rs_plan_at(const rs_plan *pl, unsigned long long g, unsigned long long *K)
+{
+    unsigned long long j = g, add = 0;
+    if (g >= pl->pre) {
+        unsigned long long t = g - pl->pre, c = t / pl->P;
+        j = pl->pre + (t - c * pl->P);
+        add = c * pl->Q;
+    }
+    *K = (unsigned long long)pl->tab[j].K + add;
+    return &pl->tab[j];
+}
+
+static void rs_plan_upload(resamp_crcf q)
+{
+    size_t bytes = q->pl.nent * sizeof(lqk_rs_entry);
+    void *d = lq_devbuf_get(&q->pl.d_tab, bytes);
+    lqrt_h2d(d, q->pl.tab, bytes, q->ctx.stream);
+    lqrt_sync(q->ctx.stream);
+}
+
+/* Brent's cycle detection on the per-input timing state, from q->now */
+static int rs_plan_build_periodic(resamp_crcf q)
+{
+    const rs_state x0 = q->now;
+    rs_state tort = x0, hare = x0;
+    unsigned long long power = 1, lam = 1;
+    rs_step(&hare, q->del, q->npfb);
+    while (!rs_eq(&tort, &hare)) {
+        if (power == lam) {
+            if (power > RS_MAX_PERIOD) return 0;
+            tort = hare;
+            power *= 2;
+            lam = 0;
+        }
+        rs_step(&hare, q->del, q->npfb);
+        lam++;
+    }
+    /* pre-period: advance one copy lam steps, then walk both until they meet */
+    tort = x0;
+    hare = x0;
+    for (unsigned long long i = 0; i < lam; i++) rs_step(&hare, q->del, q->npfb);
+    unsigned long long mu = 0;
+    while (!rs_eq(&tort, &hare)) {
+        if (mu > RS_MAX_PERIOD) return 0;
+        rs_step(&tort, q->del, q->npfb);
+        rs_step(&hare, q->del, q->npfb);
+        mu++;
+    }
+    /* table of pre + P entries; K must fit 32 bits */
+    size_t n = (size_t)(mu + lam);
+    rs_plan_reserve(&q->pl, n);
+    rs_state s = x0;
+    unsigned long long K = 0, Kpre = 0;
+    for (size_t j = 0; j < n; j++) {
+        if (K > 0xffffffffull) return 0;
+        if (j == mu) Kpre = K;
+        rs_put(&q->pl.tab[j], &s, K);
+        K += rs_step(&s, q->del, q->npfb);
+    }
+    if (K > 0xffffffffull) return 0;
+    q->pl.nent = n;
+    q->pl.pre = mu;
+    q->pl.P = lam;
+    q->pl.Q = K - Kpre;
+    q->pl.origin = x0;
+    q->pl.periodic = 1;
+    q->pl.valid = 1;
+    q->gpos = 0;
+    return 1;
+}
+
+/* plan covering exactly the next nx inputs (nx <= RS_DIRECT_CHUNK) */
+static void rs_plan_build_direct(resamp_crcf q, unsigned long long nx)
+{
+    size_t n = (size_t)nx + 1;
+    rs_plan_reserve(&q->pl, n);
+    rs_state s = q->now;
+    unsigned long long K = 0;
+    for (size_t j = 0; j < n; j++) {
+        rs_put(&q->pl.tab[j], &s, K);
+        if (j + 1 < n) K += rs_step(&s, q->del, q->npfb);
+    }
+    if (K > 0xffffffffull) LQ_FAIL("error: resamp_crcf: too many outputs for one call\n");
+    q->pl.nent = n;
+    q->pl.pre = n;
+    q->pl.P = 1;
+    q->pl.Q = 0;
+    q->pl.origin = q->now;
+    q->pl.periodic = 0;
+    q->pl.valid = 1;
+    q->gpos = 0;
+}
+
+static void rs_check_rate(resamp_crcf q)
+{
+    if (!(q->del > 0.0f) || isinf(q->del) || isnan(q->del))
+        LQ_FAIL("error: resamp_crcf_execute(), invalid resampling rate (%f)\n", q->rate);
+}
+
+/* make the plan cover inputs [gpos, gpos + nx); returns how many of them it covers */
+static unsigned long long rs_ensure_plan(resamp_crcf q, unsigned long long nx)
+{
+    rs_check_rate(q);
+    if (q->pl.valid && q->pl.periodic) return nx;
+    if (q->pl.valid && q->gpos + nx <= q->pl.nent - 1) return nx;
+    lqrt_sync(q->ctx.stream);                /* the old table may still be in use */
+    if (q->pl.valid) {                       /* state at the end of the old plan's coverage */
+        unsigned long long K;
+        q->now = rs_get(rs_plan_at(&q->pl, q->gpos, &K));
+    }
+    q->pl.valid = 0;
+    if (!q->periodic_failed && nx >= RS_PERIODIC_MIN) {
+        if (rs_plan_build_periodic(q)) {
+            rs_plan_upload(q);
+            return nx;
+        }
+        q->periodic_failed = 1;
+    }
+    unsigned long long c = nx < RS_DIRECT_CHUNK ? nx : RS_DIRECT_CHUNK;
+    rs_plan_build_direct(q, c);
+    rs_plan_upload(q);
+    return c;
+}
+
+static unsigned long long rs_K(resamp_crcf q, unsigned long long g)
+{
+    unsigned long long K;
+    rs_plan_at(&q->pl, g, &K);
+    return K;
+}
+
+/* the plan's state at gpos becomes the object's state before a rate change */
+static void rs_sync_now(resamp_crcf q)
+{
+    if (q->pl.valid) {
+        unsigned long long K;
+        q->now = rs_get(rs_plan_at(&q->pl, q->gpos, &K));
+    }
+}
+
+resamp_crcf resamp_crcf_create(float _rate, unsigned int _m, float _fc, float _As, unsigned int _npfb)
+{
+    if (_rate <= 0) LQ_FAIL("error: resamp_crcf_create(), resampling rate must be greater than zero\n");
+    if (_m == 0) LQ_FAIL("error: resamp_crcf_create(), filter semi-length must be greater than zero\n");
+    if (_npfb == 0) LQ_FAIL("error: resamp_crcf_create(), number of filter banks must be greater than zero\n");
+    if (_fc <= 0.0f || _fc >= 0.5f) LQ_FAIL("error: resamp_crcf_create(), filter cutoff must be in (0,0.5)\n");
+    if (_As <= 0.0f)
+        LQ_FAIL("error: resamp_crcf_create(), filter stop-band suppression must be greater than zero\n");
+    lqrt_require_device("resamp_crcf_create");
+    resamp_crcf q = (resamp_crcf)lq_xmalloc(sizeof(*q));
+    q->rate = _rate;
+    q->del = 1.0f / _rate;
+    q->m = _m;
+    q->fc = _fc;
+    q->As = _As;
+    q->npfb = _npfb;
+    q->L = 2 * _m;
+    /* resamp.c:117-132: design, DC normalisation, bank from the first n-1 taps */
+    unsigned int n = 2 * _m * _npfb + 1;
+    float *hf = (float *)lq_xmalloc(n * sizeof(float));
+    lq_firdes_kaiser(n, _fc / ((float)_npfb), _As, 0.0f, hf);
+    float gain = 0.0f;
+    for (unsigned int i = 0; i < n; i++) gain += hf[i];
+    gain = (_npfb) / (gain);
+    for (unsigned int i = 0; i < n; i++) hf[i] = hf[i] * gain;
+    size_t ntap = (size_t)_npfb * q->L;
+    float *tp = (float *)lq_xmalloc(ntap * 2 * sizeof(float));
+    for (unsigned int b = 0; b < _npfb; b++)
+        for (unsigned int k = 0; k < q->L; k++) {
+            tp[2 * (b * q->L + k)] = hf[b + k * _npfb];
+            tp[2 * (b * q->L + k) + 1] = hf[(b + 1) % _npfb + k * _npfb];
+        }
+    lq_ctx_init(&q->ctx);
+    q->d_taps = lqrt_malloc(ntap * 2 * sizeof(float));
+    lqrt_h2d(q->d_taps, tp, ntap * 2 * sizeof(float), q->ctx.stream);
+    q->d_hist[0] = lqrt_malloc((size_t)q->L * 8);
+    q->d_hist[1] = lqrt_malloc((size_t)q->L * 8);
+    lqrt_sync(q->ctx.stream);
+    free(tp);
+    free(hf);
+    q->now = rs_initial;
+    q->gpos = 0;
+    return q;
+}
+
+resamp_crcf resamp_crcf_create_default(float _rate)
+{
+    if (_rate <= 0) LQ_FAIL("error: resamp_crcf_create_default(), resampling rate must be greater than zero\n");
+    return resamp_crcf_create(_rate, 7, 0.25f, 60.0f, 64);   /* resamp.c:150-169 */
+}
+
+void resamp_crcf_destroy(resamp_crcf _q)
+{
+    lqrt_sync(_q->ctx.stream);
+    lqrt_free(_q->d_taps);
+    lqrt_free(_q->d_hist[0]);
+    lqrt_free(_q->d_hist[1]);
+    lq_devbuf_free(&_q->pl.d_tab);
+    lq_devbuf_free(&_q->xbuf);
+    lq_devbuf_free(&_q->ybuf);
+    lq_ctx_free(&_q->ctx);
+    free(_q->pl.tab);
+    free(_q);
+}
+
+void resamp_crcf_print(resamp_crcf _q)
+{
+    printf("resampler [rate: %f]\n", _q->rate);
+    printf("fir polyphase filterbank [%u] :\n", _q->npfb);
+    for (unsigned int i = 0; i < _q->npfb; i++) printf("  bank %3u: \n", i);
+}
+
+void resamp_crcf_reset(resamp_crcf _q)
+{
+    lqrt_memset(_q->d_hist[0], (size_t)_q->L * 8, _q->ctx.stream);
+    lqrt_memset(_q->d_hist[1], (size_t)_q->L * 8, _q->ctx.stream);
+    lqrt_sync(_q->ctx.stream);
+    _q->now = rs_initial;
+    _q->gpos = 0;
+    /* a periodic plan that starts from the initial state stays usable */
+    if (!(_q->pl.valid && _q->pl.periodic && rs_eq(&_q->pl.origin, &rs_initial))) _q->pl.valid = 0;
+}
+
+unsigned int resamp_crcf_get_delay(resamp_crcf _q) { return _q->m; }
+
+static void rs_new_del(resamp_crcf q, float del)
+{
+    if (memcmp(&del, &q->del, 4) == 0) return;
+    lqrt_sync(q->ctx.stream);
+    rs_sync_now(q);
+    q->del = del;
+    q->pl.valid = 0;
+    q->periodic_failed = 0;
+}
+
+void resamp_crcf_set_rate(resamp_crcf _q, float _rate)
+{
+    if (_rate <= 0) LQ_FAIL("error: resamp_crcf_set_rate(), resampling rate must be greater than zero\n");
+    _q->rate = _rate;
+    rs_new_del(_q, 1.0f / _q->rate);
+}
+
+/* resamp.c:222-239, including its clipping of the rate to [-0.5, 0.5] */
+void resamp_crcf_adjust_rate(resamp_crcf _q, float _delta)
+{
+    if (_delta > 0.1f || _delta < -0.1f)
+        LQ_FAIL("error: resamp_crcf_adjust_rate(), resampling rate must be in [-0.1,0.1]\n");
+    _q->rate += _delta;
+    if (_q->rate > 0.5f) _q->rate = 0.5f;
+    if (_q->rate < -0.5f) _q->rate = -0.5f;
+    rs_new_del(_q, 1.0f / _q->rate);
+}
+
+unsigned long long resamp_crcf_num_output(resamp_crcf _q, unsigned long long _nx)
+{
+    if (_nx == 0) return 0;
+    unsigned long long done = 0, total = 0;
+    /* periodic plans answer directly; otherwise simulate on a copy of the state */
+    if (!(_q->pl.valid && _q->pl.periodic) && _nx >= RS_PERIODIC_MIN) rs_ensure_plan(_q, _nx);
+    if (_q->pl.valid && (_q->pl.periodic || _q->gpos + _nx <= _q->pl.nent - 1))
+        return rs_K(_q, _q->gpos + _nx) - rs_K(_q, _q->gpos);
+    rs_check_rate(_q);
+    rs_state s = _q->now;
+    if (_q->pl.valid) {
+        unsigned long long K;
+        s = rs_get(rs_plan_at(&_q->pl, _q->gpos, &K));
+    }
+    for (; done < _nx; done++) total += rs_step(&s, _q->del, _q->npfb);
+    return total;
+}
+
+void resamp_crcf_execute_block_dev(resamp_crcf _q, const liquid_float_complex *_dx, unsigned long long _nx,
+                                   liquid_float_complex *_dy, unsigned long long *_ny)
+{
+    unsigned long long total = 0;
+    while (_nx > 0) {
+        unsigned long long c = rs_ensure_plan(_q, _nx);
+        unsigned long long K0 = rs_K(_q, _q->gpos), K1 = rs_K(_q, _q->gpos + c);
+        lqk_rs_plan kp = {(const lqk_rs_entry *)_q->pl.d_tab.p, _q->pl.pre, _q->pl.P, _q->pl.Q};
+        void *hold = _q->d_hist[_q->cur], *hnew = _q->d_hist[_q->cur ^ 1];
+        lqk_resamp(&kp, _q->gpos, K0, _q->npfb, _q->L, _q->del, _q->d_taps, hold, _dx, c, _dy, _q->ctx.stream);
+        lqk_window_append(1, hold, _q->L, _dx, c, hnew, _q->ctx.stream);
+        _q->cur ^= 1;
+        _q->gpos += c;
+        _dx += c;
+        _dy += K1 - K0;
+        total += K1 - K0;
+        _nx -= c;
+    }
+    rs_sync_now(_q);
+    if (_ny) *_ny = total;
+}
+
+void resamp_crcf_execute_block(resamp_crcf _q, liquid_float_complex *_x, unsigned int _nx,
+                               liquid_float_complex *_y, unsigned int *_ny)
+{
+    if (_nx == 0) {
+        *_ny = 0;
+        return;
+    }
+    unsigned long long nout = resamp_crcf_num_output(_q, _nx);
+    void *dx = lq_devbuf_get(&_q->xbuf, (size_t)_nx * 8);
+    void *dy = lq_devbuf_get(&_q->ybuf, (size_t)(nout ? nout : 1) * 8);
+    lqrt_h2d(dx, _x, (size_t)_nx * 8, _q->ctx.stream);
+    unsigned long long ny = 0;
+    resamp_crcf_execute_block_dev(_q, (const liquid_float_complex *)dx, _nx, (liquid_float_complex *)dy, &ny);
+    if (ny) lqrt_d2h(_y, dy, (size_t)ny * 8, _q->ctx.stream);
+    lqrt_sync(_q->ctx.stream);
+    *_ny = (unsigned int)ny;
+}
+
+void resamp_crcf_execute(resamp_crcf _q, liquid_float_complex _x, liquid_float_complex *_y,
+                         unsigned int *_num_written)
+{
+    resamp_crcf_execute_block(_q, &_x, 1, _y, _num_written);
+}
+
+void resamp_crcf_set_stream(resamp_crcf _q, void *_s) { lq_ctx_set_stream(&_q->ctx, _s); }
+void resamp_crcf_synchronize(resamp_crcf _q) { lqrt_sync(_q->ctx.stream); }
+
+/* ----------------------------------------------------------------- test hook
+ * Host-only check of the timing plan (no GPU): builds the plan the object
+ * would use from the initial state (periodic if `periodic`, else direct) and
+ * expands it exactly as k_resamp replays it, recording for every output the
+ * bank index (-1 for a BOUNDARY output), mu and input index -- the format of
+ * the oracle's orc_resamp_schedule().  Returns the number of outputs, or -1 if
+ * no periodic plan exists within RS_MAX_PERIOD. */
+long long liquid_mi355x_resamp_schedule(float _rate, unsigned int _npfb, unsigned long long _nx, int _periodic,
+                                        int *_b, float *_mu, unsigned int *_idx, unsigned long long _cap,
+                                        unsigned long long *_pre, unsigned long long *_period)
+{
+    struct resamp_crcf_s q;
+    memset(&q, 0, sizeof(q));
+    q.rate = _rate;
+    q.del = 1.0f / _rate;
+    q.npfb = _npfb;
+    q.now = rs_initial;
+    if (_periodic) {
+        if (!rs_plan_build_periodic(&q)) {
+            free(q.pl.tab);
+            return -1;
+        }
+    } else {
+        rs_plan_build_direct(&q, _nx);
+    }
+    if (_pre) *_pre = q.pl.pre;
+    if (_period) *_period = q.pl.P;
+    unsigned long long k = 0;
+    const int np = (int)_npfb;
+    for (unsigned long long g = 0; g < _nx; g++) {
+        unsigned long long K;
+        rs_state s = rs_get(rs_plan_at(&q.pl, g, &K));
+        if (K != k) {
+            free(q.pl.tab);
+            return -2;                       /* plan's output count disagrees with the replay */
+        }
+        while (s.b < np) {
+            if (s.st == RS_INTERP && s.b == np - 1) break;
+            if (k < _cap) {
+                _b[k] = s.st == RS_INTERP ? s.b : -1;
+                _mu[k] = s.mu;
+                _idx[k] = (unsigned int)g;
+            }
+            k++;
+            s.tau += q.del;
+            float bf = s.tau * (float)_npfb;
+            s.b = (int)floorf(bf);
+            s.mu = bf - (float)s.b;
+            s.st = RS_INTERP;
+        }
+    }
+    free(q.pl.tab);
+    return (long long)k;
+}

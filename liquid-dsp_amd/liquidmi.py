@@ -147,6 +147,32 @@ def _declare(L):
         "firpfbch2_crcf_set_stream": (None, [vp, vp]),
         "firpfbch2_crcf_get_stream": (vp, [vp]),
         "firpfbch2_crcf_synchronize": (None, [vp]),
+        "firpfb_crcf_create": (vp, [u, vp, u]),
+        "firpfb_crcf_create_kaiser": (vp, [u, u, f, f]),
+        "firpfb_crcf_recreate": (vp, [vp, u, vp, u]),
+        "firpfb_crcf_destroy": (None, [vp]),
+        "firpfb_crcf_print": (None, [vp]),
+        "firpfb_crcf_set_scale": (None, [vp, f]),
+        "firpfb_crcf_reset": (None, [vp]),
+        "firpfb_crcf_push": (None, [vp, cfloat]),
+        "firpfb_crcf_execute": (None, [vp, u, vp]),
+        "firpfb_crcf_execute_block": (None, [vp, vp, ull, vp]),
+        "firpfb_crcf_execute_block_dev": (None, [vp, vp, ull, vp]),
+        "firpfb_crcf_set_stream": (None, [vp, vp]),
+        "resamp_crcf_create": (vp, [f, u, f, f, u]),
+        "resamp_crcf_create_default": (vp, [f]),
+        "resamp_crcf_destroy": (None, [vp]),
+        "resamp_crcf_print": (None, [vp]),
+        "resamp_crcf_reset": (None, [vp]),
+        "resamp_crcf_get_delay": (u, [vp]),
+        "resamp_crcf_set_rate": (None, [vp, f]),
+        "resamp_crcf_adjust_rate": (None, [vp, f]),
+        "resamp_crcf_execute": (None, [vp, cfloat, vp, vp]),
+        "resamp_crcf_execute_block": (None, [vp, vp, u, vp, vp]),
+        "resamp_crcf_num_output": (ull, [vp, ull]),
+        "resamp_crcf_execute_block_dev": (None, [vp, vp, ull, vp, vp]),
+        "resamp_crcf_set_stream": (None, [vp, vp]),
+        "resamp_crcf_synchronize": (None, [vp]),
     })
     for name, (res, args) in sig.items():
         fn = getattr(L, name)
@@ -447,3 +473,84 @@ class FirPfbch2(_Obj):
 
     def get_stream(self):
         return self._fn("_get_stream")(self.q)
+
+
+class FirPfb(_Obj):
+    prefix = "firpfb_crcf"
+
+    def __init__(self, M, h=None, m=None, fc=None, As=None):
+        self.M = M
+        if h is None:
+            self.q = self._fn("_create_kaiser")(M, m, fc, As)
+        else:
+            self._h = _coefs(h, CRCF)
+            self.q = self._fn("_create")(M, ptr(self._h), len(self._h))
+
+    def set_scale(self, s):
+        self._fn("_set_scale")(self.q, float(s))
+
+    def reset(self):
+        self._fn("_reset")(self.q)
+
+    def push(self, v):
+        v = complex(v)
+        self._fn("_push")(self.q, cfloat(v.real, v.imag))
+
+    def execute(self, i):
+        y = np.zeros(1, np.complex64)
+        self._fn("_execute")(self.q, i, ptr(y))
+        return complex(y[0])
+
+    def execute_block(self, x):
+        """push each x[t] and evaluate every bank: returns (len(x), M)"""
+        x = _samples(x, CRCF)
+        y = np.zeros(len(x) * self.M, np.complex64)
+        self._fn("_execute_block")(self.q, ptr(x), len(x), ptr(y))
+        return y.reshape(len(x), self.M)
+
+
+class Resamp(_Obj):
+    prefix = "resamp_crcf"
+
+    def __init__(self, rate, m=None, fc=None, As=None, npfb=None):
+        if m is None:
+            self.q = self._fn("_create_default")(rate)
+        else:
+            self.q = self._fn("_create")(rate, m, fc, As, npfb)
+
+    def reset(self):
+        self._fn("_reset")(self.q)
+
+    def set_rate(self, r):
+        self._fn("_set_rate")(self.q, float(r))
+
+    def adjust_rate(self, d):
+        self._fn("_adjust_rate")(self.q, float(d))
+
+    def get_delay(self):
+        return self._fn("_get_delay")(self.q)
+
+    def num_output(self, nx):
+        return int(self._fn("_num_output")(self.q, nx))
+
+    def execute(self, v):
+        v = complex(v)
+        y = np.zeros(max(1, self.num_output(1)), np.complex64)
+        nw = C.c_uint(0)
+        self._fn("_execute")(self.q, cfloat(v.real, v.imag), ptr(y), C.byref(nw))
+        return y[:nw.value].copy()
+
+    def execute_block(self, x):
+        x = _samples(x, CRCF)
+        y = np.zeros(max(1, self.num_output(len(x))), np.complex64)
+        ny = C.c_uint(0)
+        self._fn("_execute_block")(self.q, ptr(x), len(x), ptr(y), C.byref(ny))
+        return y[:ny.value]
+
+    def execute_block_dev(self, dx, nx, dy):
+        ny = C.c_ulonglong(0)
+        self._fn("_execute_block_dev")(self.q, dx, nx, dy, C.byref(ny))
+        return ny.value
+
+    def synchronize(self):
+        self._fn("_synchronize")(self.q)

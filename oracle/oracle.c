@@ -675,6 +675,22 @@ void orc_resamp_reset(orc_resamp q)          /* resamp.c:181-195 */
     q->y1 = 0;
 }
 
+void orc_resamp_set_rate(orc_resamp q, float rate)   /* resamp.c:204-217 */
+{
+    if (rate <= 0) orc_fail("resamp: bad rate");
+    q->rate = rate;
+    q->del = 1.0f / q->rate;
+}
+
+void orc_resamp_adjust_rate(orc_resamp q, float delta)   /* resamp.c:222-239 (clips to [-0.5,0.5]) */
+{
+    if (delta > 0.1f || delta < -0.1f) orc_fail("resamp: bad rate adjustment");
+    q->rate += delta;
+    if (q->rate > 0.5f) q->rate = 0.5f;
+    if (q->rate < -0.5f) q->rate = -0.5f;
+    q->del = 1.0f / q->rate;
+}
+
 static inline void orc_resamp_update_timing(orc_resamp q)   /* resamp.c:352-363 */
 {
     q->tau += q->del;

@@ -91,6 +91,8 @@ typedef struct orc_resamp_s *orc_resamp;
 orc_resamp   orc_resamp_create(float rate, unsigned int m, float fc, float As, unsigned int npfb);
 void         orc_resamp_destroy(orc_resamp q);
 void         orc_resamp_reset(orc_resamp q);
+void         orc_resamp_set_rate(orc_resamp q, float rate);
+void         orc_resamp_adjust_rate(orc_resamp q, float delta);
 void         orc_resamp_execute_block(orc_resamp q, const orc_cf *x, unsigned int nx,
                                       orc_cf *y, unsigned int *ny);
 /* the data-independent schedule: for each output k, the filter index b (or

@@ -56,12 +56,16 @@ def _declare(L):
         "orc_firpfb_destroy": (None, [vp]),
         "orc_firpfb_push": (None, [vp, vp]),
         "orc_firpfb_execute": (None, [vp, u, vp]),
+        "orc_firpfb_set_scale": (None, [vp, f]),
         "orc_firinterp_create": (vp, [i, u, vp, u]),
         "orc_firinterp_create_kaiser": (vp, [u, u, f]),
         "orc_firinterp_destroy": (None, [vp]),
         "orc_firinterp_execute_block": (None, [vp, vp, u, vp]),
         "orc_resamp_create": (vp, [f, u, f, f, u]),
         "orc_resamp_destroy": (None, [vp]),
+        "orc_resamp_reset": (None, [vp]),
+        "orc_resamp_set_rate": (None, [vp, f]),
+        "orc_resamp_adjust_rate": (None, [vp, f]),
         "orc_resamp_execute_block": (None, [vp, vp, u, vp, C.POINTER(C.c_uint)]),
         "orc_resamp_schedule": (ul, [f, u, ul, vp, vp, vp, ul]),
         "orc_fftfilt_create": (vp, [i, vp, u, u]),
@@ -213,6 +217,9 @@ class FirPfb(_Obj):
         a = _arr([v], self.typ)
         lib().orc_firpfb_push(self.q, ptr(a))
 
+    def set_scale(self, s):
+        lib().orc_firpfb_set_scale(self.q, s)
+
     def execute(self, i):
         y = _arr([0], self.typ)
         lib().orc_firpfb_execute(self.q, i, ptr(y))
@@ -243,6 +250,17 @@ class Resamp(_Obj):
     def __init__(self, rate, m=7, fc=0.25, As=60.0, npfb=64):
         self.rate = rate
         self.q = lib().orc_resamp_create(rate, m, fc, As, npfb)
+
+    def reset(self):
+        lib().orc_resamp_reset(self.q)
+
+    def set_rate(self, r):
+        self.rate = r
+        lib().orc_resamp_set_rate(self.q, r)
+
+    def adjust_rate(self, d):
+        lib().orc_resamp_adjust_rate(self.q, d)
+        self.rate = min(0.5, max(-0.5, self.rate + d))
 
     def execute_block(self, x):
         x = _arr(x, CRCF)

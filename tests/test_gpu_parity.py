@@ -306,6 +306,122 @@ def test_firpfbch_vs_oracle(typ, M, m):
 
 
 # ============================================================== drop-in programs
+# ------------------------------------------------------------------ firpfb / resamp
+def test_firpfb_known_answer():
+    # firpfb_autotest.c impulse response (rrrf data through the crcf bank, imag = 0)
+    c = KA["autotest_firpfb_impulse_response"]
+    q = LQ.FirPfb(c["M"], G.arr(c["h"]))
+    for v in G.arr(c["x"]):
+        q.push(v)
+    out = np.array([q.execute(i) for i in range(c["M"])])
+    assert np.max(np.abs(out.real - G.arr(c["y"]))) < c["tol"]
+    assert np.max(np.abs(out.imag)) == 0.0
+
+
+@pytest.mark.parametrize("M,hlen", [(8, 64), (32, 449), (64, 896), (5, 7)])
+def test_firpfb_block_and_push_vs_oracle(M, hlen):
+    r = rng(M * 3 + hlen)
+    h = r.uniform(-0.5, 0.5, hlen).astype(np.float32)
+    x = cx(r, 3000)
+    g = LQ.FirPfb(M, h)
+    o = O.FirPfb(O.CRCF, M, h)
+    g.set_scale(0.8)
+    o.set_scale(0.8)
+    ref = np.empty((len(x), M), np.complex64)
+    for t, v in enumerate(x):
+        o.push(v)
+        ref[t] = [o.execute(i) for i in range(M)]
+    y1 = g.execute_block(x[:2000])
+    for v in x[2000:2010]:              # per-sample push/execute after a block call
+        g.push(v)
+    per = np.array([g.execute(i) for i in range(M)])
+    y2 = g.execute_block(x[2010:])
+    assert G.nrm_err(y1, ref[:2000]) < NRM
+    assert G.nrm_err(per, ref[2009]) < NRM
+    assert G.nrm_err(y2, ref[2010:]) < NRM
+
+
+def _resamp_pair(rate, m=7, fc=0.25, As=60.0, npfb=64):
+    rate = float(np.float32(rate))
+    return LQ.Resamp(rate, m, fc, As, npfb), O.Resamp(rate, m, fc, As, npfb)
+
+
+@pytest.mark.parametrize("rate,m,npfb", [(1.037, 7, 64), (0.97, 7, 64), (3.7, 4, 32), (0.5, 7, 64),
+                                         (10.3, 3, 64), (0.8131, 3, 37), (2.0, 16, 64), (1.3, 20, 16)])
+def test_resamp_vs_oracle_ragged(rate, m, npfb):
+    r = rng(int(rate * 1000) + m)
+    x = cx(r, 200_000)
+    g, o = _resamp_pair(rate, m=m, npfb=npfb)
+    cuts = [0, 1, 2, 3, 100, 70_000, 70_001, 140_000, 200_000]
+    ys = []
+    for a, b in zip(cuts[:-1], cuts[1:]):
+        if b - a == 1:
+            ys.append(g.execute(x[a]))
+        else:
+            ys.append(g.execute_block(x[a:b]))
+    y = np.concatenate(ys)
+    ref = o.execute_block(x)
+    assert len(y) == len(ref)
+    assert G.nrm_err(y, ref) < NRM
+
+
+def test_resamp_long_stream_crosses_period():
+    # r = 1.037: the timing plan repeats every 1 011 163 inputs; 2.5M inputs in
+    # calls of 600k use (and wrap) the periodic plan several times
+    r = rng(37)
+    x = cx(r, 2_500_000)
+    g, o = _resamp_pair(1.037)
+    y = np.concatenate([g.execute_block(x[a:a + 600_000]) for a in range(0, len(x), 600_000)])
+    ref = o.execute_block(x)
+    assert len(y) == len(ref)
+    assert G.nrm_err(y, ref) < NRM
+
+
+def test_resamp_set_rate_adjust_rate_reset():
+    r = rng(41)
+    x = cx(r, 150_000)
+    g, o = _resamp_pair(1.037)
+    y, ref = [], []
+    y.append(g.execute_block(x[:80_000]))
+    ref.append(o.execute_block(x[:80_000]))
+    g.set_rate(0.913)
+    o.set_rate(float(np.float32(0.913)))
+    y.append(g.execute_block(x[80_000:120_000]))
+    ref.append(o.execute_block(x[80_000:120_000]))
+    g.adjust_rate(0.05)                 # the reference clips the adjusted rate to 0.5
+    o.adjust_rate(0.05)
+    y.append(g.execute_block(x[120_000:]))
+    ref.append(o.execute_block(x[120_000:]))
+    for a, b in zip(y, ref):
+        assert len(a) == len(b)
+        assert G.nrm_err(a, b) < NRM
+    g.reset()
+    o.reset()
+    o.set_rate(0.5)
+    g.set_rate(0.5)
+    a, b = g.execute_block(x[:5000]), o.execute_block(x[:5000])
+    assert len(a) == len(b) and G.nrm_err(a, b) < NRM
+
+
+def test_resamp_baseline_config5_device():
+    # BASELINE configs[4]: r = 1.037, npfb = 64, m = 7 on 32M samples, device resident
+    n = 1 << 25
+    r = rng(5)
+    x = cx(r, n)
+    g, o = _resamp_pair(1.037)
+    nout = g.num_output(n)
+    assert nout == 34_795_945
+    dx = LQ.DeviceBuffer.from_array(x)
+    dy = LQ.DeviceBuffer(nout * 8)
+    ny = g.execute_block_dev(dx.p, n, dy.p)
+    g.synchronize()
+    assert ny == nout
+    y = dy.to_array(np.complex64, nout)
+    ref = o.execute_block(x)
+    assert len(ref) == nout
+    assert G.nrm_err(y, ref) < NRM
+
+
 @pytest.mark.parametrize("src", sorted(f for f in os.listdir(os.path.join(LQ.ROOT, "examples")) if f.endswith(".c")))
 def test_examples_run_on_gpu(src, tmp_path):
     inc = os.path.join(LQ.ROOT, "include")

@@ -1,0 +1,74 @@
+"""resamp timing plan (host side, no GPU): the periodic / direct plans the
+library builds must reproduce the reference's float32 timing schedule bit for
+bit -- bank index, mu and input index of every output -- against the oracle's
+restatement of resamp.c:245-363 (orc_resamp_schedule).
+
+Covers rates with a pure cycle (1.037, 0.97), a pre-period (3.7), tiny periods
+(0.5, 1.5, 2.0), many outputs per input (10.3), non-power-of-two banks, and
+streams several periods long so the wrap-around of the plan is exercised.
+"""
+import ctypes as C
+
+import numpy as np
+import pytest
+
+import liquidmi as LM
+import oracle_lib as O
+
+
+def _lib_schedule(rate, npfb, nx, periodic):
+    L = LM.lib()
+    fn = L.liquid_mi355x_resamp_schedule
+    fn.restype = C.c_longlong
+    fn.argtypes = [C.c_float, C.c_uint, C.c_ulonglong, C.c_int, C.c_void_p, C.c_void_p, C.c_void_p,
+                   C.c_ulonglong, C.POINTER(C.c_ulonglong), C.POINTER(C.c_ulonglong)]
+    cap = int(np.ceil(nx * rate)) + 16
+    b = np.zeros(cap, np.int32)
+    mu = np.zeros(cap, np.float32)
+    idx = np.zeros(cap, np.uint32)
+    pre, per = C.c_ulonglong(0), C.c_ulonglong(0)
+    k = fn(rate, npfb, nx, periodic, LM.ptr(b), LM.ptr(mu), LM.ptr(idx), cap, C.byref(pre), C.byref(per))
+    assert k >= 0, "plan failed (%d)" % k
+    return b[:k], mu[:k], idx[:k], pre.value, per.value
+
+
+@pytest.mark.parametrize("rate,npfb,nx,pre0", [
+    (1.037, 64, 3_100_000, 0),     # config 5: period 1 011 163 inputs
+    (0.97, 64, 1_000_000, 0),
+    (3.7, 64, 2_000_000, 864_961),  # pre-period before the cycle
+    (0.5, 64, 10_000, 0),
+    (1.5, 64, 10_000, 0),
+    (2.0, 64, 10_000, 0),
+    (10.3, 64, 900_000, 0),
+    (1.037, 50, 1_500_000, 0),     # non-power-of-two bank count
+    (0.8131, 37, 400_000, None),
+])
+def test_periodic_plan_matches_oracle_schedule(rate, npfb, nx, pre0):
+    rate = float(np.float32(rate))
+    b, mu, idx, pre, per = _lib_schedule(rate, npfb, nx, 1)
+    if pre0 is not None:
+        assert pre == pre0
+    ob, omu, oidx = O.resamp_schedule(rate, npfb, nx)
+    assert len(b) == len(ob)
+    np.testing.assert_array_equal(b, ob)
+    np.testing.assert_array_equal(mu.view(np.uint32), omu.view(np.uint32))
+    np.testing.assert_array_equal(idx, oidx)
+
+
+@pytest.mark.parametrize("rate", [1.037, 0.63, 4.21])
+def test_direct_plan_matches_oracle_schedule(rate):
+    rate = float(np.float32(rate))
+    nx = 50_000
+    b, mu, idx, _, _ = _lib_schedule(rate, 64, nx, 0)
+    ob, omu, oidx = O.resamp_schedule(rate, 64, nx)
+    np.testing.assert_array_equal(b, ob)
+    np.testing.assert_array_equal(mu.view(np.uint32), omu.view(np.uint32))
+    np.testing.assert_array_equal(idx, oidx)
+
+
+def test_config5_output_count():
+    # 32M inputs at r = 1.037 -> 34 795 945 outputs (probe of the reference)
+    rate = float(np.float32(1.037))
+    b, _, _, pre, per = _lib_schedule(rate, 64, 1 << 25, 1)
+    assert (pre, per) == (0, 1_011_163)
+    assert len(b) == 34_795_945
