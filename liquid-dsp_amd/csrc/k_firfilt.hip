@@ -226,16 +226,16 @@ __global__ __launch_bounds__(NT) void k_firfilt(const typename kt<KIND>::T *__re
 }
 
 template <int KIND>
-__global__ void k_halo_copy(const typename kt<KIND>::T *x, long long n, int HP, long long ntiles,
+__global__ void k_halo_copy(const typename kt<KIND>::T *x, long long n, int HP, long long ntiles, int tile,
                             typename kt<KIND>::T *halo)
 {
     long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
     long long tot = ntiles * HP;
     if (i >= tot) return;
-    long long tile = i / HP;
-    int u = (int)(i - tile * HP);
-    if (tile == 0) return;
-    long long s = tile * TILE - HP + u;
+    long long tl = i / HP;
+    int u = (int)(i - tl * HP);
+    if (tl == 0) return;
+    long long s = tl * tile - HP + u;
     halo[i] = (s >= 0 && s < n) ? x[s] : zero<typename kt<KIND>::T>();
 }
 
@@ -337,6 +337,8 @@ __global__ __launch_bounds__(NT) void k_firinterp(const typename kt<KIND>::T *__
     }
 }
 
+int tile_of(int) { return TILE; }
+
 template <int KIND, int HC>
 void launch_firfilt(const lqk_fir_desc *d, const void *hist, const void *x, long long n, void *y,
                     const void *halo, hipStream_t st)
@@ -376,7 +378,8 @@ size_t elem_size(int kind) { return kind == 0 ? sizeof(float) : sizeof(float2); 
 
 extern "C" size_t lqk_firfilt_scratch_bytes(const lqk_fir_desc *d, unsigned long long n)
 {
-    const long long ntiles = ((long long)n + TILE - 1) / TILE;
+    const int tl = tile_of(d->kind);
+    const long long ntiles = ((long long)n + tl - 1) / tl;
     return (size_t)ntiles * d->hc * d->nchunk * elem_size(d->kind);
 }
 
@@ -389,15 +392,16 @@ extern "C" void lqk_firfilt(const lqk_fir_desc *d, const void *hist, const void 
     if (x == y) {
         // in place: save each tile's halo before any workgroup overwrites it
         const int HP = (int)(d->hc * d->nchunk);
-        const long long ntiles = ((long long)n + TILE - 1) / TILE;
+        const int tl = tile_of(d->kind);
+        const long long ntiles = ((long long)n + tl - 1) / tl;
         const long long tot = ntiles * HP;
         const unsigned nb = (unsigned)((tot + 255) / 256);
         if (d->kind == 0)
             hipLaunchKernelGGL(k_halo_copy<0>, dim3(nb), dim3(256), 0, st, (const float *)x, (long long)n, HP,
-                               ntiles, (float *)scratch);
+                               ntiles, tl, (float *)scratch);
         else
             hipLaunchKernelGGL(k_halo_copy<1>, dim3(nb), dim3(256), 0, st, (const float2 *)x, (long long)n, HP,
-                               ntiles, (float2 *)scratch);
+                               ntiles, tl, (float2 *)scratch);
         LQ_CHECK_LAUNCH();
         halo = scratch;
     }
