@@ -110,6 +110,16 @@ __device__ __forceinline__ void lds_fence()
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
+// Workgroup barrier for LDS hand-offs only: waits for this wave's LDS
+// operations, not for its global loads or stores (__syncthreads() would also
+// drain the prefetched rows and the output stores at every phase change).
+__device__ __forceinline__ void lds_barrier()
+{
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+}
+
 struct Params {
     const float2 *hist;
     const float2 *x;
@@ -122,10 +132,22 @@ struct Params {
     float2 *Y;
 };
 
-template <int L>
+__device__ unsigned long long g_pfb2_clk[2 * 1024];   // dev experiments (XMODE >= 10)
+
+// XMODE (dev experiments, 0 in the library): 1 skip the FFT phase, 2 skip the
+// row loads, 3 skip the output stores; +10 records per-workgroup clocks
+// SMODE: output path. 0: per-lane 8-byte non-temporal stores straight from the
+// FFT layout; 1: same, plain stores; 2: through the block's LDS buffer into
+// 16-byte non-temporal stores; 3: 2 with plain stores
+template <int L, int XMODE = 0, int SMODE = 2, int PF = 4, int BAR = 1>
 __global__ __launch_bounds__(NT, 1) void k_pfb2_an1024(Params P, const float *__restrict__ hsub,
                                                        const float2 *__restrict__ tw4096)
 {
+    unsigned long long clk0 = 0, rt0 = 0;
+    if (XMODE >= 10) {
+        clk0 = __builtin_amdgcn_s_memtime();
+        rt0 = __builtin_amdgcn_s_memrealtime();
+    }
     static_assert(L <= NS, "ring too small");
     __shared__ __attribute__((aligned(16))) float2 xb[NBUF * BSTR];
     __shared__ __attribute__((aligned(16))) float2 tw1[16 * 64]; // W_1024^{+t k1}
@@ -193,6 +215,7 @@ __global__ __launch_bounds__(NT, 1) void k_pfb2_an1024(Params P, const float *__
     const long long ibase = (8 * gs - NS) * M + (long long)tid - P.B0 * M2;
     const unsigned ox0 = (unsigned)(ibase * 8), oh0 = (unsigned)((HL + ibase) * 8);
     auto fetch = [&](long long c) -> float2 {
+        if (XMODE % 10 == 2) return make_float2((float)(c & 7), 0.5f);
         const unsigned k = (unsigned)(c - (8 * gs - NS)) * (unsigned)(M * 8);
         const float2 a = __builtin_bit_cast(float2, __builtin_amdgcn_raw_buffer_load_b64(rx, ox0 + k, 0, 0));
         const float2 b = __builtin_bit_cast(float2, __builtin_amdgcn_raw_buffer_load_b64(rh, oh0 + k, 0, 0));
@@ -220,7 +243,6 @@ __global__ __launch_bounds__(NT, 1) void k_pfb2_an1024(Params P, const float *__
 
     // next iteration's first PF rows are prefetched into registers while the
     // FFTs run; the rest are fetched as the rows are consumed
-    constexpr int PF = 4;
     float2 pf[PF];
 #pragma unroll
     for (int r = 0; r < PF; r++) pf[r] = fetch(8 * gs + r);
@@ -243,10 +265,21 @@ __global__ __launch_bounds__(NT, 1) void k_pfb2_an1024(Params P, const float *__
 #pragma unroll
             for (int r = 0; r < PF; r++) pf[r] = fetch(8 * (g + 1) + r);
         }
-        __syncthreads();
+        if (BAR) lds_barrier();
+        else __syncthreads();
 
         // ---- one 1024-point IFFT per wave: block b0 + wave
-        {
+        if (XMODE % 10 == 1) {
+            const long long b = b0 + wave;
+            int sb = slot0 + wave;
+            sb -= (sb >= NBUF) ? NBUF : 0;
+            float2 *B = xb + sb * BSTR;
+            if (b >= P.B0 && b < P.B0 + P.nblk) {
+                float2 *Yb = P.Y + (b - P.B0) * M;
+#pragma unroll
+                for (int r = 0; r < 16; r++) st_nt(Yb + lane + 64 * r, B[lane + 64 * r]);
+            }
+        } else {
             const long long b = b0 + wave;
             int sb = slot0 + wave;
             sb -= (sb >= NBUF) ? NBUF : 0;
@@ -286,15 +319,43 @@ __global__ __launch_bounds__(NT, 1) void k_pfb2_an1024(Params P, const float *__
                 v[r] = hi1 ? csub(p2, u) : cadd(u, p2);
             }
             // lane (k1, bq) holds Y[k1 + 16 r + 256 s], s = bitrev2(bq)
-            if (b >= P.B0 && b < P.B0 + P.nblk) {
+            if (XMODE % 10 == 3) {
+                if (v[0].x == 12345.f && v[5].y == 3.f) P.Y[0] = v[3];
+            } else if (b >= P.B0 && b < P.B0 + P.nblk) {
                 const int s = ((bq & 1) << 1) | (bq >> 1);
-                float2 *Yb = P.Y + (b - P.B0) * M + k1 + 256 * s;
+                if constexpr (SMODE < 2) {
+                    float2 *Yb = P.Y + (b - P.B0) * M + k1 + 256 * s;
 #pragma unroll
-                for (int r = 0; r < 16; r++) st_nt(Yb + 16 * r, v[r]);
+                    for (int r = 0; r < 16; r++) {
+                        if (SMODE == 0) st_nt(Yb + 16 * r, v[r]);
+                        else Yb[16 * r] = v[r];
+                    }
+                } else {
+                    // natural order in LDS, 4 pad slots per 256 (ds_write_b64
+                    // conflict-free), then whole 16-byte pairs per lane
+                    lds_fence();
+#pragma unroll
+                    for (int r = 0; r < 16; r++) B[k1 + 16 * r + 260 * s] = v[r];
+                    lds_fence();
+                    typedef float v4f __attribute__((ext_vector_type(4)));
+                    v4f *Yb = reinterpret_cast<v4f *>(P.Y + (b - P.B0) * M);
+#pragma unroll
+                    for (int q = 0; q < 8; q++) {
+                        const int o = 2 * (lane + 64 * q);
+                        const v4f val = *reinterpret_cast<const v4f *>(B + o + 4 * (o >> 8));
+                        if (SMODE == 2) __builtin_nontemporal_store(val, Yb + (o >> 1));
+                        else Yb[o >> 1] = val;
+                    }
+                }
             }
         }
         slot0 = slot0 == 0 ? NBUF - 1 : slot0 - 1; // (16(g+1)) mod 17
-        __syncthreads();
+        if (BAR) lds_barrier();
+        else __syncthreads();
+    }
+    if (XMODE >= 10 && tid == 0 && blockIdx.x < 1024) {
+        g_pfb2_clk[2 * blockIdx.x] = __builtin_amdgcn_s_memtime() - clk0;
+        g_pfb2_clk[2 * blockIdx.x + 1] = __builtin_amdgcn_s_memrealtime() - rt0;
     }
 }
 
