@@ -139,7 +139,7 @@ __device__ unsigned long long g_pfb2_clk[2 * 1024];   // dev experiments (XMODE 
 // SMODE: output path. 0: per-lane 8-byte non-temporal stores straight from the
 // FFT layout; 1: same, plain stores; 2: through the block's LDS buffer into
 // 16-byte non-temporal stores; 3: 2 with plain stores
-template <int L, int XMODE = 0, int SMODE = 2, int PF = 4, int BAR = 1>
+template <int L, int XMODE = 0, int SMODE = 2, int PF = 4, int BAR = 1, int TRES = 0>
 __global__ __launch_bounds__(NT, 1) void k_pfb2_an1024(Params P, const float *__restrict__ hsub,
                                                        const float2 *__restrict__ tw4096)
 {
@@ -180,7 +180,7 @@ __global__ __launch_bounds__(NT, 1) void k_pfb2_an1024(Params P, const float *__
     float he[L], ho[L];
     auto load_taps = [&]() {
         int oe = j * L, oo = (j ^ M2) * L;
-        asm volatile("" : "+v"(oe), "+v"(oo)); // keep the reload inside the loop
+        if (!TRES) asm volatile("" : "+v"(oe), "+v"(oo)); // keep the reload inside the loop
 #pragma unroll
         for (int n = 0; n < L; n++) {
             he[n] = hsub[oe + n];
@@ -249,7 +249,7 @@ __global__ __launch_bounds__(NT, 1) void k_pfb2_an1024(Params P, const float *__
 
     for (long long g = gs; g < ge; g++) {
         const long long b0 = 16 * g;
-        load_taps();
+        if (!TRES) load_taps();
 #pragma unroll
         for (int r = 0; r < 8; r++) {
             // row c = 8g + r -> blocks b0 + 2r + dA (first), b0 + 2r + dA + 1 (second)

@@ -14,10 +14,11 @@
 // tabulates it once per rate (`plan`, see host/resamp.c): entry j holds
 // (tau, mu, b, state) before input j and K[j] = outputs emitted by inputs
 // < j; the sequence is eventually periodic (pre-period `pre`, period `P`
-// inputs, `Q` outputs per period).  Each lane takes R consecutive inputs,
-// reads its one entry and replays the reference's float32 recurrence
-// bit-exactly for those R inputs (contraction off), with the last L+R inputs
-// in registers.  Outputs go straight to y[K - K0].
+// inputs, `Q` outputs per period).  Lanes look up the entry of their first
+// input and replay the reference's float32 recurrence bit-exactly for a few
+// inputs (contraction off).  k_resamp2 (the default) turns the replay into a
+// dense per-tile output list and evaluates it with coalesced stores;
+// k_resamp / k_resamp_generic cover shapes whose tables do not fit LDS.
 #include <hip/hip_runtime.h>
 
 #include "lq_device.h"
@@ -123,6 +124,180 @@ __global__ __launch_bounds__(NT) void k_resamp(lqk_rs_plan pl, unsigned long lon
     }
 }
 
+// Tiled form (L even, table in LDS).  A workgroup owns TIN consecutive inputs:
+//  1. the input window [i0-L-1, i0+TIN) goes to LDS twice, the second copy
+//     shifted by one sample, so every (L+1)-sample window starts 16-byte
+//     aligned in one of them;
+//  2. each lane replays the float32 timing of its RIN inputs and writes one
+//     descriptor per output (mu, input, bank) at the output's index in the
+//     tile -- the output list is now dense;
+//  3. lanes take consecutive outputs: y = sum_p c[p] x[i-L+p], p <= L, with
+//     c[p] = T.x + mu (T.y - T.x) from the pair table T2 (bank b: h_b, h_b+1
+//     on the same window; bank npfb: the BOUNDARY pair h_{npfb-1} on the
+//     window one input older and h_0), so both states are one dot product,
+//     and the stores are coalesced.  Outputs beyond CAP per tile take more
+//     rounds of 2-3.
+// plan position g = gt + d for a tile base gt (entry jt, cycles ct already
+// resolved once per tile) and a small lane offset d: 32-bit arithmetic
+__device__ __forceinline__ void rs_lookup_near(const lqk_rs_plan &pl, unsigned long long gt, unsigned long long jt,
+                                               unsigned long long ct, unsigned d, rs_state &s, unsigned long long &K)
+{
+    unsigned long long j = jt + d, c = ct;
+    if (gt >= pl.pre) {
+        const unsigned off = (unsigned)(jt - pl.pre) + d;
+        const unsigned w = off / (unsigned)pl.P;
+        j = pl.pre + (off - w * (unsigned)pl.P);
+        c += w;
+    } else if (gt + d >= pl.pre) {
+        const unsigned long long t = gt + d - pl.pre;
+        const unsigned long long w = t / pl.P;
+        j = pl.pre + (t - w * pl.P);
+        c = w;
+    }
+    const lqk_rs_entry e = pl.tab[j];
+    s.tau = e.tau;
+    s.mu = e.mu;
+    s.b = e.bst >> 1;
+    s.st = e.bst & 1;
+    K = (unsigned long long)e.K + c * pl.Q;
+}
+
+template <int L>
+__global__ __launch_bounds__(NT) void k_resamp2(lqk_rs_plan pl, unsigned long long g0, unsigned long long K0,
+                                                int npfb, float del, const float2 *__restrict__ taps2,
+                                                const float2 *__restrict__ hist, const float2 *__restrict__ x,
+                                                long long n, float2 *__restrict__ y)
+{
+    constexpr int RIN = 4;
+    constexpr int TIN = NT * RIN;
+    constexpr int LP = (L + 2 + 1) & ~1;         // pair-table stride (>= L+1, even)
+    constexpr int LPS = LP + 2;                  // LDS row stride: 16 bytes of pad spread the banks
+    constexpr int NW = LP / 2;                   // 16-byte reads per window / per tap row
+    constexpr int TS = TIN + L + 2;              // tile samples per copy (+1 for the shifted copy)
+    constexpr int CS = TS + 2;                   // copy stride (even: both copies 16-byte aligned)
+    constexpr int CAP = 1536;                    // outputs per round
+    typedef float v4f __attribute__((ext_vector_type(4)));
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    float2 *cp0 = reinterpret_cast<float2 *>(smem);
+    float2 *cp1 = cp0 + CS;
+    uint2 *desc = reinterpret_cast<uint2 *>(cp1 + CS);
+    float2 *tpl = reinterpret_cast<float2 *>(desc + CAP);
+
+    const int tid = threadIdx.x;
+    for (int t = tid; t < (npfb + 1) * LP; t += NT) tpl[(t / LP) * LPS + (t % LP)] = taps2[t];
+    const float fnpfb = (float)npfb;
+    const long long ntiles = (n + TIN - 1) / TIN;
+    constexpr int NXV = (TS + NT - 1) / NT;       // tile samples per lane
+
+    // everything a tile needs from HBM, fetched one tile ahead into registers
+    struct Pre {
+        float2 xv[NXV];
+        rs_state s;
+        unsigned long long K, Kb, Ke;
+    };
+    auto fetch = [&](long long tile, Pre &f) {
+        const long long i0 = tile * TIN;
+#pragma unroll
+        for (int u = 0; u < NXV; u++) {
+            const int t = tid + u * NT;
+            const long long sx = i0 - L - 1 + t;
+            float2 v = make_float2(0.f, 0.f);
+            if (t < TS) {
+                if (sx >= 0 && sx < n) v = x[sx];
+                else if (sx < 0 && sx >= -L) v = hist[L + sx];
+            }
+            f.xv[u] = v;
+        }
+        const unsigned long long gt = g0 + (unsigned long long)i0;
+        unsigned long long jt = gt, ct = 0;
+        if (gt >= pl.pre) {
+            const unsigned long long t = gt - pl.pre;
+            ct = t / pl.P;
+            jt = pl.pre + (t - ct * pl.P);
+        }
+        rs_state tmp;
+        rs_lookup_near(pl, gt, jt, ct, 0, tmp, f.Kb);
+        const long long ie = (i0 + TIN < n) ? i0 + TIN : n;
+        rs_lookup_near(pl, gt, jt, ct, (unsigned)(ie - i0), tmp, f.Ke);
+        rs_lookup_near(pl, gt, jt, ct, (unsigned)(tid * RIN), f.s, f.K);
+    };
+
+    long long tile = blockIdx.x;
+    if (tile >= ntiles) return;
+    Pre cur;
+    fetch(tile, cur);
+    for (; tile < ntiles; tile += gridDim.x) {
+        const long long i0 = tile * TIN;
+        __syncthreads();                              // previous tile consumed
+#pragma unroll
+        for (int u = 0; u < NXV; u++) {
+            const int t = tid + u * NT;
+            if (t < TS) {
+                cp0[t] = cur.xv[u];
+                cp1[t + 1] = cur.xv[u];
+            }
+        }
+        const unsigned long long Kb = cur.Kb;
+        const long long ntile = (long long)(cur.Ke - Kb);
+        const rs_state slane = cur.s;
+        const unsigned long long Klane = cur.K;
+        if (tile + gridDim.x < ntiles) fetch(tile + gridDim.x, cur);   // in flight during this tile
+        const long long ia = i0 + (long long)tid * RIN;   // this lane's first input
+        for (long long r0 = 0; r0 < ntile; r0 += CAP) {
+            if (r0 > 0) __syncthreads();                   // previous round consumed
+            if (ia < n) {
+                rs_state s = slane;
+                long long o = (long long)(Klane - Kb) - r0;
+#pragma unroll
+                for (int r = 0; r < RIN; r++) {
+                    if (ia + r >= n) break;
+                    const int iloc = (int)(ia + r - i0);
+                    while (s.b < npfb) {
+                        if (s.st && s.b == npfb - 1) {
+                            s.st = 0;
+                            s.b = npfb;
+                            break;
+                        }
+                        if (o >= 0 && o < CAP)
+                            desc[o] = make_uint2(__float_as_uint(s.mu),
+                                                 (unsigned)iloc | ((unsigned)(s.st ? s.b : npfb) << 12));
+                        o++;
+                        rs_advance(s, del, fnpfb);
+                        s.st = 1;
+                    }
+                    s.tau -= 1.0f;
+                    s.b -= npfb;
+                }
+            }
+            __syncthreads();
+            const int nr = (int)((ntile - r0) < CAP ? (ntile - r0) : CAP);
+            float2 *yo = y + (Kb - K0) + r0;
+            for (int o = tid; o < nr; o += NT) {
+                const uint2 d = desc[o];
+                const float mu = __uint_as_float(d.x);
+                const int iloc = (int)(d.y & 4095u);
+                const int bb = (int)(d.y >> 12);
+                const int sw = iloc + 1;                  // tile index of x[i-L]
+                const float2 *wp = (sw & 1) ? cp1 + sw + 1 : cp0 + sw;
+                const float2 *tp = tpl + bb * LPS;
+                float2 acc = make_float2(0.f, 0.f);
+#pragma unroll
+                for (int q = 0; q < NW; q++) {
+                    const v4f w = *reinterpret_cast<const v4f *>(wp + 2 * q);
+                    const v4f t = *reinterpret_cast<const v4f *>(tp + 2 * q);
+                    const float c0 = t.x + mu * (t.y - t.x);
+                    const float c1 = t.z + mu * (t.w - t.z);
+                    acc.x = fmaf(c0, w.x, acc.x);
+                    acc.y = fmaf(c0, w.y, acc.y);
+                    acc.x = fmaf(c1, w.z, acc.x);
+                    acc.y = fmaf(c1, w.w, acc.y);
+                }
+                yo[o] = acc;
+            }
+        }
+    }
+}
+
 // any L (window and taps read through the caches), one input per lane
 __global__ __launch_bounds__(NT) void k_resamp_generic(lqk_rs_plan pl, unsigned long long g0,
                                                        unsigned long long K0, int npfb, int L, float del,
@@ -183,8 +358,19 @@ __global__ void k_firpfb_single(const float *__restrict__ hpoly, int L, int i, c
 
 template <int L>
 void launch_rs(const lqk_rs_plan &pl, unsigned long long g0, unsigned long long K0, int npfb, float del,
-               const float2 *taps, const float2 *hist, const float2 *x, long long n, float2 *y, hipStream_t st)
+               const float2 *taps, const float2 *taps2, const float2 *hist, const float2 *x, long long n, float2 *y,
+               hipStream_t st)
 {
+    constexpr int LP = (L + 2 + 1) & ~1;
+    constexpr int TIN = NT * 4;
+    const size_t lds2 =
+        (size_t)2 * (TIN + L + 4) * sizeof(float2) + 1536 * 8 + (size_t)(npfb + 1) * (LP + 2) * sizeof(float2);
+    if (taps2 != nullptr && lds2 <= 64 * 1024 && pl.P < (1ull << 31) && pl.pre < (1ull << 62)) {
+        const long long ntiles = (n + TIN - 1) / TIN;
+        const unsigned nb = (unsigned)(ntiles < 1024 ? ntiles : 1024);   // persistent: ~4 per CU
+        hipLaunchKernelGGL(k_resamp2<L>, dim3(nb), dim3(NT), lds2, st, pl, g0, K0, npfb, del, taps2, hist, x, n, y);
+        return;
+    }
     const long long lanes = (n + RS_R - 1) / RS_R;
     const unsigned nb = (unsigned)((lanes + NT - 1) / NT);
     hipLaunchKernelGGL(k_resamp<L>, dim3(nb), dim3(NT), (size_t)npfb * L * sizeof(float2), st, pl, g0, K0, npfb,
@@ -194,8 +380,8 @@ void launch_rs(const lqk_rs_plan &pl, unsigned long long g0, unsigned long long 
 } // namespace
 
 extern "C" void lqk_resamp(const lqk_rs_plan *pl, unsigned long long g0, unsigned long long K0,
-                           unsigned int npfb, unsigned int L, float del, const void *taps, const void *hist,
-                           const void *x, unsigned long long n, void *y, void *stream)
+                           unsigned int npfb, unsigned int L, float del, const void *taps, const void *taps2,
+                           const void *hist, const void *x, unsigned long long n, void *y, void *stream)
 {
     if (n == 0) return;
     hipStream_t st = (hipStream_t)stream;
@@ -205,7 +391,7 @@ extern "C" void lqk_resamp(const lqk_rs_plan *pl, unsigned long long g0, unsigne
     const bool lds_ok = (size_t)npfb * L * sizeof(float2) <= 64 * 1024;
 #define LQ_RS_CASE(LL)                                                                                     \
     case LL:                                                                                               \
-        launch_rs<LL>(*pl, g0, K0, (int)npfb, del, tp, hs, xi, nn, yo, st);                               \
+        launch_rs<LL>(*pl, g0, K0, (int)npfb, del, tp, (const float2 *)taps2, hs, xi, nn, yo, st);                               \
         break;
     if (lds_ok && L <= 32 && (L % 2) == 0) {
         switch (L) {

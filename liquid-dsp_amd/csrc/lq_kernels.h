@@ -132,8 +132,10 @@ typedef struct {
 /* n inputs x (plan positions g0 .. g0+n) -> outputs y[K(g) - K0 ...];
  * taps: npfb x L pairs (h[b + n*npfb], h[(b+1)%npfb + n*npfb]); hist = last L inputs */
 void lqk_resamp(const lqk_rs_plan *pl, unsigned long long g0, unsigned long long K0, unsigned int npfb,
-                unsigned int L, float del, const void *taps, const void *hist, const void *x,
+                unsigned int L, float del, const void *taps, const void *taps2, const void *hist, const void *x,
                 unsigned long long n, void *y, void *stream);
+/* taps2: (npfb+1) x LP pairs, LP = (L+3) & ~1: row b < npfb (h_b[L-p], h_{b+1}[L-p]) for p = 1..L, row
+ * npfb the BOUNDARY pair (h_{npfb-1}[L-1-p], h_0[L-p]); zero elsewhere (NULL: untiled kernel) */
 /* firpfb_execute(i): y = scale * sum_n hpoly[i*L + n] win[L-1-n] (win: L samples, oldest first) */
 void lqk_firpfb_single(const void *hpoly, unsigned int L, unsigned int i, const void *win, float scale,
                        void *y, void *stream);

@@ -217,6 +217,7 @@ struct resamp_crcf_s {
     float rate, del, fc, As;
     unsigned int m, npfb, L;
     void *d_taps;                 /* npfb x L float pairs (bank b, bank b+1) */
+    void *d_taps2;                /* (npfb+1) x LP interpolation pairs on one window (lq_kernels.h) */
     rs_plan pl;
     int periodic_failed;          /* no period <= RS_MAX_PERIOD at this rate */
     unsigned long long gpos;      /* inputs consumed since the plan origin */
@@ -455,13 +456,30 @@ resamp_crcf resamp_crcf_create(float _rate, unsigned int _m, float _fc, float _A
             tp[2 * (b * q->L + k)] = hf[b + k * _npfb];
             tp[2 * (b * q->L + k) + 1] = hf[(b + 1) % _npfb + k * _npfb];
         }
+    /* window form: y = sum_p c[p] x[i-L+p], p <= L */
+    const unsigned int L = q->L, LP = (L + 3) & ~1u;
+    size_t ntap2 = (size_t)(_npfb + 1) * LP;
+    float *tp2 = (float *)lq_xmalloc(ntap2 * 2 * sizeof(float));
+    for (unsigned int b = 0; b < _npfb; b++)
+        for (unsigned int p = 1; p <= L; p++) {
+            tp2[2 * (b * LP + p)] = hf[b + (L - p) * _npfb];
+            tp2[2 * (b * LP + p) + 1] = (b + 1 < _npfb) ? hf[b + 1 + (L - p) * _npfb] : 0.0f;
+        }
+    for (unsigned int p = 0; p <= L; p++) {
+        tp2[2 * (_npfb * LP + p)] = p < L ? hf[_npfb - 1 + (L - 1 - p) * _npfb] : 0.0f;
+        tp2[2 * (_npfb * LP + p) + 1] = p >= 1 ? hf[(L - p) * _npfb] : 0.0f;
+    }
     lq_ctx_init(&q->ctx);
     q->d_taps = lqrt_malloc(ntap * 2 * sizeof(float));
     lqrt_h2d(q->d_taps, tp, ntap * 2 * sizeof(float), q->ctx.stream);
+    q->d_taps2 = lqrt_malloc(ntap2 * 2 * sizeof(float));
+    lqrt_h2d(q->d_taps2, tp2, ntap2 * 2 * sizeof(float), q->ctx.stream);
     q->d_hist[0] = lqrt_malloc((size_t)q->L * 8);
     q->d_hist[1] = lqrt_malloc((size_t)q->L * 8);
     lqrt_sync(q->ctx.stream);
+    lqrt_sync(q->ctx.stream);
     free(tp);
+    free(tp2);
     free(hf);
     q->now = rs_initial;
     q->gpos = 0;
@@ -478,6 +496,7 @@ void resamp_crcf_destroy(resamp_crcf _q)
 {
     lqrt_sync(_q->ctx.stream);
     lqrt_free(_q->d_taps);
+    lqrt_free(_q->d_taps2);
     lqrt_free(_q->d_hist[0]);
     lqrt_free(_q->d_hist[1]);
     lq_devbuf_free(&_q->pl.d_tab);
@@ -563,7 +582,8 @@ void resamp_crcf_execute_block_dev(resamp_crcf _q, const liquid_float_complex *_
         unsigned long long K0 = rs_K(_q, _q->gpos), K1 = rs_K(_q, _q->gpos + c);
         lqk_rs_plan kp = {(const lqk_rs_entry *)_q->pl.d_tab.p, _q->pl.pre, _q->pl.P, _q->pl.Q};
         void *hold = _q->d_hist[_q->cur], *hnew = _q->d_hist[_q->cur ^ 1];
-        lqk_resamp(&kp, _q->gpos, K0, _q->npfb, _q->L, _q->del, _q->d_taps, hold, _dx, c, _dy, _q->ctx.stream);
+        lqk_resamp(&kp, _q->gpos, K0, _q->npfb, _q->L, _q->del, _q->d_taps, _q->d_taps2, hold, _dx, c, _dy,
+                   _q->ctx.stream);
         lqk_window_append(1, hold, _q->L, _dx, c, hnew, _q->ctx.stream);
         _q->cur ^= 1;
         _q->gpos += c;
