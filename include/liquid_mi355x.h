@@ -101,6 +101,8 @@ LQMI_DOTPROD_API(dotprod_cccf, liquid_float_complex, liquid_float_complex, liqui
     void FIRFILT##_execute(FIRFILT _q, TO *_y);                                                 \
     void FIRFILT##_execute_block(FIRFILT _q, TI *_x, unsigned int _n, TO *_y);                  \
     unsigned int FIRFILT##_get_length(FIRFILT _q);                                              \
+    void FIRFILT##_freqresponse(FIRFILT _q, float _fc, liquid_float_complex *_H);               \
+    float FIRFILT##_groupdelay(FIRFILT _q, float _fc);                                          \
     /* extension: device pointers (x == y allowed), asynchronous on the object's stream */      \
     void FIRFILT##_execute_block_dev(FIRFILT _q, const TI *_dx, unsigned long long _n,          \
                                      TO *_dy);                                                  \
@@ -113,59 +115,70 @@ LQMI_FIRFILT_API(firfilt_crcf, liquid_float_complex, float, liquid_float_complex
 LQMI_FIRFILT_API(firfilt_cccf, liquid_float_complex, liquid_float_complex, liquid_float_complex)
 
 /* ------------------------------------------------------------------------ */
-/* firdecim (liquid.h:2664-2735): crcf                                       */
+/* firdecim (liquid.h:2664-2735): rrrf, crcf, cccf                           */
 /* ------------------------------------------------------------------------ */
-typedef struct firdecim_crcf_s *firdecim_crcf;
-firdecim_crcf firdecim_crcf_create(unsigned int _M, float *_h, unsigned int _h_len);
-firdecim_crcf firdecim_crcf_create_kaiser(unsigned int _M, unsigned int _m, float _As);
-void firdecim_crcf_destroy(firdecim_crcf _q);
-void firdecim_crcf_print(firdecim_crcf _q);
-void firdecim_crcf_clear(firdecim_crcf _q);
-void firdecim_crcf_execute(firdecim_crcf _q, liquid_float_complex *_x, liquid_float_complex *_y);
-void firdecim_crcf_execute_block(firdecim_crcf _q, liquid_float_complex *_x, unsigned int _n,
-                                 liquid_float_complex *_y);
-/* extension: _n = number of outputs; _dx holds _n*M samples (device) */
-void firdecim_crcf_execute_block_dev(firdecim_crcf _q, const liquid_float_complex *_dx,
-                                     unsigned long long _n, liquid_float_complex *_dy);
-void firdecim_crcf_set_stream(firdecim_crcf _q, void *_hip_stream);
+#define LQMI_FIRDECIM_API(FIRDECIM, TO, TC, TI)                                                 \
+    typedef struct FIRDECIM##_s *FIRDECIM;                                                      \
+    FIRDECIM FIRDECIM##_create(unsigned int _M, TC *_h, unsigned int _h_len);                   \
+    FIRDECIM FIRDECIM##_create_kaiser(unsigned int _M, unsigned int _m, float _As);             \
+    void FIRDECIM##_destroy(FIRDECIM _q);                                                       \
+    void FIRDECIM##_print(FIRDECIM _q);                                                         \
+    void FIRDECIM##_clear(FIRDECIM _q);                                                         \
+    void FIRDECIM##_execute(FIRDECIM _q, TI *_x, TO *_y);                                       \
+    void FIRDECIM##_execute_block(FIRDECIM _q, TI *_x, unsigned int _n, TO *_y);                \
+    /* extension: _n = number of outputs; _dx holds _n*M samples (device) */                    \
+    void FIRDECIM##_execute_block_dev(FIRDECIM _q, const TI *_dx, unsigned long long _n,        \
+                                      TO *_dy);                                                 \
+    void FIRDECIM##_set_stream(FIRDECIM _q, void *_hip_stream);
+
+LQMI_FIRDECIM_API(firdecim_rrrf, float, float, float)
+LQMI_FIRDECIM_API(firdecim_crcf, liquid_float_complex, float, liquid_float_complex)
+LQMI_FIRDECIM_API(firdecim_cccf, liquid_float_complex, liquid_float_complex, liquid_float_complex)
 
 /* ------------------------------------------------------------------------ */
-/* firinterp (liquid.h:2496-2565): crcf                                      */
+/* firinterp (liquid.h:2496-2565): rrrf, crcf, cccf                          */
 /* ------------------------------------------------------------------------ */
-typedef struct firinterp_crcf_s *firinterp_crcf;
-firinterp_crcf firinterp_crcf_create(unsigned int _M, float *_h, unsigned int _h_len);
-firinterp_crcf firinterp_crcf_create_kaiser(unsigned int _M, unsigned int _m, float _As);
-void firinterp_crcf_destroy(firinterp_crcf _q);
-void firinterp_crcf_print(firinterp_crcf _q);
-void firinterp_crcf_reset(firinterp_crcf _q);
-void firinterp_crcf_execute(firinterp_crcf _q, liquid_float_complex _x, liquid_float_complex *_y);
-void firinterp_crcf_execute_block(firinterp_crcf _q, liquid_float_complex *_x, unsigned int _n,
-                                  liquid_float_complex *_y);
-/* extension: _n inputs -> _n*M outputs, device pointers */
-void firinterp_crcf_execute_block_dev(firinterp_crcf _q, const liquid_float_complex *_dx,
-                                      unsigned long long _n, liquid_float_complex *_dy);
-void firinterp_crcf_set_stream(firinterp_crcf _q, void *_hip_stream);
+#define LQMI_FIRINTERP_API(FIRINTERP, TO, TC, TI)                                               \
+    typedef struct FIRINTERP##_s *FIRINTERP;                                                    \
+    FIRINTERP FIRINTERP##_create(unsigned int _M, TC *_h, unsigned int _h_len);                 \
+    FIRINTERP FIRINTERP##_create_kaiser(unsigned int _M, unsigned int _m, float _As);           \
+    void FIRINTERP##_destroy(FIRINTERP _q);                                                     \
+    void FIRINTERP##_print(FIRINTERP _q);                                                       \
+    void FIRINTERP##_reset(FIRINTERP _q);                                                       \
+    void FIRINTERP##_execute(FIRINTERP _q, TI _x, TO *_y);                                      \
+    void FIRINTERP##_execute_block(FIRINTERP _q, TI *_x, unsigned int _n, TO *_y);              \
+    /* extension: _n inputs -> _n*M outputs, device pointers */                                 \
+    void FIRINTERP##_execute_block_dev(FIRINTERP _q, const TI *_dx, unsigned long long _n,      \
+                                       TO *_dy);                                                \
+    void FIRINTERP##_set_stream(FIRINTERP _q, void *_hip_stream);
+
+LQMI_FIRINTERP_API(firinterp_rrrf, float, float, float)
+LQMI_FIRINTERP_API(firinterp_crcf, liquid_float_complex, float, liquid_float_complex)
+LQMI_FIRINTERP_API(firinterp_cccf, liquid_float_complex, liquid_float_complex, liquid_float_complex)
 
 /* ------------------------------------------------------------------------ */
-/* firpfb (liquid.h:2392-2486): crcf                                         */
+/* firpfb (liquid.h:2392-2486): rrrf, crcf, cccf                             */
 /* ------------------------------------------------------------------------ */
-typedef struct firpfb_crcf_s *firpfb_crcf;
-firpfb_crcf firpfb_crcf_create(unsigned int _M, float *_h, unsigned int _h_len);
-firpfb_crcf firpfb_crcf_create_kaiser(unsigned int _M, unsigned int _m, float _fc, float _As);
-firpfb_crcf firpfb_crcf_recreate(firpfb_crcf _q, unsigned int _M, float *_h, unsigned int _h_len);
-void firpfb_crcf_destroy(firpfb_crcf _q);
-void firpfb_crcf_print(firpfb_crcf _q);
-void firpfb_crcf_set_scale(firpfb_crcf _q, float _g);
-void firpfb_crcf_reset(firpfb_crcf _q);
-void firpfb_crcf_push(firpfb_crcf _q, liquid_float_complex _x);
-void firpfb_crcf_execute(firpfb_crcf _q, unsigned int _i, liquid_float_complex *_y);
-/* extension: push each of _n inputs and evaluate every bank after it:
- * _y[t*M + i] = execute(i) after push(_x[t]); host / device pointers */
-void firpfb_crcf_execute_block(firpfb_crcf _q, liquid_float_complex *_x, unsigned long long _n,
-                               liquid_float_complex *_y);
-void firpfb_crcf_execute_block_dev(firpfb_crcf _q, const liquid_float_complex *_dx,
-                                   unsigned long long _n, liquid_float_complex *_dy);
-void firpfb_crcf_set_stream(firpfb_crcf _q, void *_hip_stream);
+#define LQMI_FIRPFB_API(FIRPFB, TO, TC, TI)                                                     \
+    typedef struct FIRPFB##_s *FIRPFB;                                                          \
+    FIRPFB FIRPFB##_create(unsigned int _M, TC *_h, unsigned int _h_len);                       \
+    FIRPFB FIRPFB##_create_kaiser(unsigned int _M, unsigned int _m, float _fc, float _As);      \
+    FIRPFB FIRPFB##_recreate(FIRPFB _q, unsigned int _M, TC *_h, unsigned int _h_len);          \
+    void FIRPFB##_destroy(FIRPFB _q);                                                           \
+    void FIRPFB##_print(FIRPFB _q);                                                             \
+    void FIRPFB##_set_scale(FIRPFB _q, TC _g);                                                  \
+    void FIRPFB##_reset(FIRPFB _q);                                                             \
+    void FIRPFB##_push(FIRPFB _q, TI _x);                                                       \
+    void FIRPFB##_execute(FIRPFB _q, unsigned int _i, TO *_y);                                  \
+    /* extension: push each of _n inputs and evaluate every bank after it:                   */ \
+    /* _y[t*M + i] = execute(i) after push(_x[t]); host / device pointers                    */ \
+    void FIRPFB##_execute_block(FIRPFB _q, TI *_x, unsigned long long _n, TO *_y);              \
+    void FIRPFB##_execute_block_dev(FIRPFB _q, const TI *_dx, unsigned long long _n, TO *_dy);  \
+    void FIRPFB##_set_stream(FIRPFB _q, void *_hip_stream);
+
+LQMI_FIRPFB_API(firpfb_rrrf, float, float, float)
+LQMI_FIRPFB_API(firpfb_crcf, liquid_float_complex, float, liquid_float_complex)
+LQMI_FIRPFB_API(firpfb_cccf, liquid_float_complex, liquid_float_complex, liquid_float_complex)
 
 /* ------------------------------------------------------------------------ */
 /* resamp (liquid.h:2938-3015): crcf                                         */
@@ -194,22 +207,26 @@ void resamp_crcf_set_stream(resamp_crcf _q, void *_hip_stream);
 void resamp_crcf_synchronize(resamp_crcf _q);
 
 /* ------------------------------------------------------------------------ */
-/* fftfilt (liquid.h:2192-2240): crcf                                        */
+/* fftfilt (liquid.h:2192-2240): rrrf, crcf, cccf                            */
 /* ------------------------------------------------------------------------ */
-typedef struct fftfilt_crcf_s *fftfilt_crcf;
-fftfilt_crcf fftfilt_crcf_create(float *_h, unsigned int _h_len, unsigned int _n);
-void fftfilt_crcf_destroy(fftfilt_crcf _q);
-void fftfilt_crcf_reset(fftfilt_crcf _q);
-void fftfilt_crcf_print(fftfilt_crcf _q);
-void fftfilt_crcf_set_scale(fftfilt_crcf _q, float _scale);
-void fftfilt_crcf_execute(fftfilt_crcf _q, liquid_float_complex *_x, liquid_float_complex *_y);
-unsigned int fftfilt_crcf_get_length(fftfilt_crcf _q);
-/* extension: arbitrary-length stream (any _n), host / device pointers */
-void fftfilt_crcf_execute_block(fftfilt_crcf _q, liquid_float_complex *_x, unsigned long long _n,
-                                liquid_float_complex *_y);
-void fftfilt_crcf_execute_block_dev(fftfilt_crcf _q, const liquid_float_complex *_dx,
-                                    unsigned long long _n, liquid_float_complex *_dy);
-void fftfilt_crcf_set_stream(fftfilt_crcf _q, void *_hip_stream);
+#define LQMI_FFTFILT_API(FFTFILT, TO, TC, TI)                                                   \
+    typedef struct FFTFILT##_s *FFTFILT;                                                        \
+    FFTFILT FFTFILT##_create(TC *_h, unsigned int _h_len, unsigned int _n);                     \
+    void FFTFILT##_destroy(FFTFILT _q);                                                         \
+    void FFTFILT##_reset(FFTFILT _q);                                                           \
+    void FFTFILT##_print(FFTFILT _q);                                                           \
+    void FFTFILT##_set_scale(FFTFILT _q, TC _scale);                                            \
+    void FFTFILT##_execute(FFTFILT _q, TI *_x, TO *_y);                                         \
+    unsigned int FFTFILT##_get_length(FFTFILT _q);                                              \
+    /* extension: arbitrary-length stream (any _n), host / device pointers */                   \
+    void FFTFILT##_execute_block(FFTFILT _q, TI *_x, unsigned long long _n, TO *_y);            \
+    void FFTFILT##_execute_block_dev(FFTFILT _q, const TI *_dx, unsigned long long _n,          \
+                                     TO *_dy);                                                  \
+    void FFTFILT##_set_stream(FFTFILT _q, void *_hip_stream);
+
+LQMI_FFTFILT_API(fftfilt_rrrf, float, float, float)
+LQMI_FFTFILT_API(fftfilt_crcf, liquid_float_complex, float, liquid_float_complex)
+LQMI_FFTFILT_API(fftfilt_cccf, liquid_float_complex, liquid_float_complex, liquid_float_complex)
 
 /* ------------------------------------------------------------------------ */
 /* firpfbch (liquid.h:5667-5739): crcf                                       */

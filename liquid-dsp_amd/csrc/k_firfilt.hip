@@ -225,6 +225,25 @@ __global__ __launch_bounds__(NT) void k_firfilt(const typename kt<KIND>::T *__re
     }
 }
 
+// firpfb_execute(i): y = scale * sum_n hpoly[i*L + n] win[L-1-n] (win oldest first)
+template <int KIND>
+__global__ void k_firpfb_single(const typename kt<KIND>::TC *__restrict__ hpoly, int L, int i,
+                                const typename kt<KIND>::T *__restrict__ win, float sre, float sim,
+                                typename kt<KIND>::T *y)
+{
+    typedef typename kt<KIND>::T T;
+    __shared__ T part[64];
+    T acc = zero<T>();
+    for (int k = threadIdx.x; k < L; k += 64) mac(acc, hpoly[(size_t)i * L + k], win[L - 1 - k]);
+    part[threadIdx.x] = acc;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        T s = zero<T>();
+        for (int t = 0; t < 64; t++) s = vadd(s, part[t]);
+        y[0] = apply_scale(s, sre, sim);
+    }
+}
+
 template <int KIND>
 __global__ void k_halo_copy(const typename kt<KIND>::T *x, long long n, int HP, long long ntiles, int tile,
                             typename kt<KIND>::T *halo)
@@ -311,7 +330,7 @@ __global__ __launch_bounds__(NT) void k_firinterp(const typename kt<KIND>::T *__
                                                   const typename kt<KIND>::T *__restrict__ x,
                                                   long long n, int M, int L,
                                                   const typename kt<KIND>::TC *__restrict__ hpoly,
-                                                  float scale, typename kt<KIND>::T *__restrict__ y)
+                                                  float sre, float sim, typename kt<KIND>::T *__restrict__ y)
 {
     typedef typename kt<KIND>::T T;
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
@@ -333,7 +352,7 @@ __global__ __launch_bounds__(NT) void k_firinterp(const typename kt<KIND>::T *__
     for (int p = 0; p < M; p++) {
         T acc = zero<T>();
         for (int l = 0; l < L; l++) mac(acc, hpoly[p * L + l], w[-l]);
-        y[i * M + p] = apply_scale(acc, scale, 0.0f);
+        y[i * M + p] = apply_scale(acc, sre, sim);
     }
 }
 
@@ -477,7 +496,7 @@ extern "C" void lqk_firdecim(const lqk_fir_desc *d, unsigned int M, const void *
     LQ_CHECK_LAUNCH();
 }
 
-extern "C" void lqk_firinterp(int kind, const void *hpoly, unsigned int M, unsigned int L, float scale,
+extern "C" void lqk_firinterp(int kind, const void *hpoly, unsigned int M, unsigned int L, float sre, float sim,
                               const void *hist, const void *x, unsigned long long n, void *y, void *stream)
 {
     if (n == 0) return;
@@ -487,15 +506,36 @@ extern "C" void lqk_firinterp(int kind, const void *hpoly, unsigned int M, unsig
     switch (kind) {
     case 0:
         hipLaunchKernelGGL(k_firinterp<0>, dim3(nb), dim3(NT), lds, st, (const float *)hist, (const float *)x,
-                           (long long)n, (int)M, (int)L, (const float *)hpoly, scale, (float *)y);
+                           (long long)n, (int)M, (int)L, (const float *)hpoly, sre, sim, (float *)y);
         break;
     case 1:
         hipLaunchKernelGGL(k_firinterp<1>, dim3(nb), dim3(NT), lds, st, (const float2 *)hist, (const float2 *)x,
-                           (long long)n, (int)M, (int)L, (const float *)hpoly, scale, (float2 *)y);
+                           (long long)n, (int)M, (int)L, (const float *)hpoly, sre, sim, (float2 *)y);
         break;
     case 2:
         hipLaunchKernelGGL(k_firinterp<2>, dim3(nb), dim3(NT), lds, st, (const float2 *)hist, (const float2 *)x,
-                           (long long)n, (int)M, (int)L, (const float2 *)hpoly, scale, (float2 *)y);
+                           (long long)n, (int)M, (int)L, (const float2 *)hpoly, sre, sim, (float2 *)y);
+        break;
+    }
+    LQ_CHECK_LAUNCH();
+}
+
+extern "C" void lqk_firpfb_single(int kind, const void *hpoly, unsigned int L, unsigned int i, const void *win,
+                                  float sre, float sim, void *y, void *stream)
+{
+    hipStream_t st = (hipStream_t)stream;
+    switch (kind) {
+    case 0:
+        hipLaunchKernelGGL(k_firpfb_single<0>, dim3(1), dim3(64), 0, st, (const float *)hpoly, (int)L, (int)i,
+                           (const float *)win, sre, sim, (float *)y);
+        break;
+    case 1:
+        hipLaunchKernelGGL(k_firpfb_single<1>, dim3(1), dim3(64), 0, st, (const float *)hpoly, (int)L, (int)i,
+                           (const float2 *)win, sre, sim, (float2 *)y);
+        break;
+    case 2:
+        hipLaunchKernelGGL(k_firpfb_single<2>, dim3(1), dim3(64), 0, st, (const float2 *)hpoly, (int)L, (int)i,
+                           (const float2 *)win, sre, sim, (float2 *)y);
         break;
     }
     LQ_CHECK_LAUNCH();

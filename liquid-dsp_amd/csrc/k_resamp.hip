@@ -335,27 +335,6 @@ __global__ __launch_bounds__(NT) void k_resamp_generic(lqk_rs_plan pl, unsigned 
     }
 }
 
-// firpfb_execute(i): y = scale * sum_n hpoly[i*L + n] win[L-1-n]
-__global__ void k_firpfb_single(const float *__restrict__ hpoly, int L, int i, const float2 *__restrict__ win,
-                                float scale, float2 *y)
-{
-    __shared__ float2 part[64];
-    float2 acc = make_float2(0.f, 0.f);
-    for (int k = threadIdx.x; k < L; k += 64) {
-        const float h = hpoly[(size_t)i * L + k];
-        const float2 v = win[L - 1 - k];
-        acc.x += h * v.x;
-        acc.y += h * v.y;
-    }
-    part[threadIdx.x] = acc;
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        float2 s = make_float2(0.f, 0.f);
-        for (int t = 0; t < 64; ++t) s = cadd(s, part[t]);
-        y[0] = make_float2(s.x * scale, s.y * scale);
-    }
-}
-
 template <int L>
 void launch_rs(const lqk_rs_plan &pl, unsigned long long g0, unsigned long long K0, int npfb, float del,
                const float2 *taps, const float2 *taps2, const float2 *hist, const float2 *x, long long n, float2 *y,
@@ -421,10 +400,3 @@ extern "C" void lqk_resamp(const lqk_rs_plan *pl, unsigned long long g0, unsigne
     LQ_CHECK_LAUNCH();
 }
 
-extern "C" void lqk_firpfb_single(const void *hpoly, unsigned int L, unsigned int i, const void *win, float scale,
-                                  void *y, void *stream)
-{
-    hipLaunchKernelGGL(k_firpfb_single, dim3(1), dim3(64), 0, (hipStream_t)stream, (const float *)hpoly, (int)L,
-                       (int)i, (const float2 *)win, scale, (float2 *)y);
-    LQ_CHECK_LAUNCH();
-}

@@ -70,7 +70,7 @@ void lqk_fir_single(const lqk_fir_desc *d, const void *win, void *y, void *strea
 void lqk_firdecim(const lqk_fir_desc *d, unsigned int M, const void *hist, const void *x,
                   unsigned long long nout, void *y, void *stream);
 void lqk_firinterp(int kind, const void *hpoly /* M x L, h[p + l*M] */, unsigned int M,
-                   unsigned int L, float scale, const void *hist, const void *x,
+                   unsigned int L, float scale_re, float scale_im, const void *hist, const void *x,
                    unsigned long long n, void *y, void *stream);
 
 /* ---------------------------------------------------------------- firpfbch2 analyzer
@@ -137,8 +137,8 @@ void lqk_resamp(const lqk_rs_plan *pl, unsigned long long g0, unsigned long long
 /* taps2: (npfb+1) x LP pairs, LP = (L+3) & ~1: row b < npfb (h_b[L-p], h_{b+1}[L-p]) for p = 1..L, row
  * npfb the BOUNDARY pair (h_{npfb-1}[L-1-p], h_0[L-p]); zero elsewhere (NULL: untiled kernel) */
 /* firpfb_execute(i): y = scale * sum_n hpoly[i*L + n] win[L-1-n] (win: L samples, oldest first) */
-void lqk_firpfb_single(const void *hpoly, unsigned int L, unsigned int i, const void *win, float scale,
-                       void *y, void *stream);
+void lqk_firpfb_single(int kind, const void *hpoly, unsigned int L, unsigned int i, const void *win,
+                       float scale_re, float scale_im, void *y, void *stream);
 
 #ifdef __cplusplus
 }

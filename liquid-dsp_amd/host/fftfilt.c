@@ -1,5 +1,5 @@
 /*
- * fftfilt.c -- fftfilt_crcf (FFT fast-convolution filter).
+ * fftfilt.c -- fftfilt_{rrrf,crcf,cccf} (FFT fast-convolution filter).
  *
  * API include/liquid.h:2192-2240; semantics src/filter/src/fftfilt.c:69-266:
  * create(h, h_len, n) needs n >= h_len-1 (:78-83); execute() consumes and
@@ -9,118 +9,161 @@
  * The reference evaluates this with a 2n-point overlap-add per call; the
  * kernel (csrc/k_fftfilt.hip) uses fixed 4096-point overlap-save segments,
  * which gives the same convolution for any n and lets a long stream
- * (execute_block extension) run all segments in parallel.
+ * (execute_block extension) run all segments in parallel.  rrrf runs the
+ * real-I/O form of the kernel; crcf and cccf share the complex form (H is
+ * the transform of real or complex taps).
  */
+#include <complex.h>
+
 #include "lq_host.h"
 
-struct fftfilt_crcf_s {
+static const char *lq_ext[] = {"rrrf", "crcf", "cccf"};
+
+typedef struct {
+    int kind;
+    size_t esz, csz;
     unsigned int h_len, n;
     float *h;
     void *d_h, *d_H;
     void *d_hist[2];    /* previous h_len-1 inputs */
     int cur;
-    float scale;        /* user scale s */
+    float sre, sim;     /* user scale s */
     lq_ctx ctx;
     lq_devbuf xbuf, ybuf, cbuf;
-};
+} lq_fftf;
 
-fftfilt_crcf fftfilt_crcf_create(float *_h, unsigned int _h_len, unsigned int _n)
+static lq_fftf *lq_fftf_create(int kind, const float *h, unsigned int h_len, unsigned int n)
 {
-    if (_h_len == 0) LQ_FAIL("error: fftfilt_crcf_create(), filter length must be greater than zero\n");
-    if (_n < _h_len - 1)
-        LQ_FAIL("error: fftfilt_crcf_create(), block length must be greater than _h_len-1 (%u)\n", _h_len - 1);
-    lqrt_require_device("fftfilt_crcf_create");
-    if (_h_len - 1 > lqk_fftfilt_nfft() / 2)
-        LQ_FAIL("error: fftfilt_crcf_create(), filter length %u exceeds the GPU limit %u\n", _h_len,
+    if (h_len == 0) LQ_FAIL("error: fftfilt_%s_create(), filter length must be greater than zero\n", lq_ext[kind]);
+    if (n < h_len - 1)
+        LQ_FAIL("error: fftfilt_%s_create(), block length must be greater than _h_len-1 (%u)\n", lq_ext[kind],
+                h_len - 1);
+    lqrt_require_device("fftfilt_create");
+    if (h_len - 1 > lqk_fftfilt_nfft() / 2)
+        LQ_FAIL("error: fftfilt_%s_create(), filter length %u exceeds the GPU limit %u\n", lq_ext[kind], h_len,
                 lqk_fftfilt_nfft() / 2 + 1);
-    fftfilt_crcf q = (fftfilt_crcf)lq_xmalloc(sizeof(*q));
-    q->h_len = _h_len;
-    q->n = _n;
-    q->h = (float *)lq_xmalloc(_h_len * sizeof(float));
-    memcpy(q->h, _h, _h_len * sizeof(float));
+    lq_fftf *q = (lq_fftf *)lq_xmalloc(sizeof(*q));
+    q->kind = kind;
+    q->esz = kind == LQ_RRRF ? 4 : 8;
+    q->csz = kind == LQ_CCCF ? 8 : 4;
+    q->h_len = h_len;
+    q->n = n;
+    q->h = (float *)lq_xmalloc(h_len * q->csz);
+    memcpy(q->h, h, h_len * q->csz);
     lq_ctx_init(&q->ctx);
-    q->d_h = lqrt_malloc(_h_len * sizeof(float));
+    q->d_h = lqrt_malloc(h_len * q->csz);
     q->d_H = lqrt_malloc((size_t)lqk_fftfilt_nfft() * 8);
-    q->d_hist[0] = lqrt_malloc((size_t)(_h_len) * 8);
-    q->d_hist[1] = lqrt_malloc((size_t)(_h_len) * 8);
-    lqrt_h2d(q->d_h, q->h, _h_len * sizeof(float), q->ctx.stream);
-    lqk_fftfilt_make_H(q->d_h, _h_len, 0, q->d_H, q->ctx.stream);
+    q->d_hist[0] = lqrt_malloc((size_t)h_len * q->esz);
+    q->d_hist[1] = lqrt_malloc((size_t)h_len * q->esz);
+    lqrt_h2d(q->d_h, q->h, h_len * q->csz, q->ctx.stream);
+    lqk_fftfilt_make_H(q->d_h, h_len, kind == LQ_CCCF, q->d_H, q->ctx.stream);
     lqrt_sync(q->ctx.stream);
-    q->scale = 1.0f;
+    q->sre = 1.0f;
+    q->sim = 0.0f;
     q->cur = 0;
     return q;
 }
 
-void fftfilt_crcf_destroy(fftfilt_crcf _q)
+static void lq_fftf_destroy(lq_fftf *q)
 {
-    lqrt_sync(_q->ctx.stream);
-    lqrt_free(_q->d_h);
-    lqrt_free(_q->d_H);
-    lqrt_free(_q->d_hist[0]);
-    lqrt_free(_q->d_hist[1]);
-    lq_devbuf_free(&_q->xbuf);
-    lq_devbuf_free(&_q->ybuf);
-    lq_devbuf_free(&_q->cbuf);
-    lq_ctx_free(&_q->ctx);
-    free(_q->h);
-    free(_q);
+    lqrt_sync(q->ctx.stream);
+    lqrt_free(q->d_h);
+    lqrt_free(q->d_H);
+    lqrt_free(q->d_hist[0]);
+    lqrt_free(q->d_hist[1]);
+    lq_devbuf_free(&q->xbuf);
+    lq_devbuf_free(&q->ybuf);
+    lq_devbuf_free(&q->cbuf);
+    lq_ctx_free(&q->ctx);
+    free(q->h);
+    free(q);
 }
 
-void fftfilt_crcf_reset(fftfilt_crcf _q)
+static void lq_fftf_reset(lq_fftf *q)
 {
-    lqrt_memset(_q->d_hist[0], (size_t)_q->h_len * 8, _q->ctx.stream);
-    lqrt_memset(_q->d_hist[1], (size_t)_q->h_len * 8, _q->ctx.stream);
-    lqrt_sync(_q->ctx.stream);
+    lqrt_memset(q->d_hist[0], (size_t)q->h_len * q->esz, q->ctx.stream);
+    lqrt_memset(q->d_hist[1], (size_t)q->h_len * q->esz, q->ctx.stream);
+    lqrt_sync(q->ctx.stream);
 }
 
-void fftfilt_crcf_print(fftfilt_crcf _q)
+static void lq_fftf_print(lq_fftf *q)
 {
-    printf("fftfilt_crcf: [h_len=%u, n=%u]\n", _q->h_len, _q->n);
-    for (unsigned int i = 0; i < _q->h_len; i++) printf("  h(%3u) = %12.8f\n", i + 1, _q->h[_q->h_len - i - 1]);
-    printf("  scale = %12.8f\n", _q->scale / (float)(2 * _q->n));
+    printf("fftfilt_%s: [h_len=%u, n=%u]\n", lq_ext[q->kind], q->h_len, q->n);
+    for (unsigned int i = 0; i < q->h_len; i++) {
+        const unsigned int k = q->h_len - i - 1;
+        if (q->kind == LQ_CCCF) printf("  h(%3u) = %12.8f + j*%12.8f\n", i + 1, q->h[2 * k], q->h[2 * k + 1]);
+        else printf("  h(%3u) = %12.8f\n", i + 1, q->h[k]);
+    }
+    printf("  scale = %12.8f\n", q->sre / (float)(2 * q->n));
 }
 
-void fftfilt_crcf_set_scale(fftfilt_crcf _q, float _scale) { _q->scale = _scale; }
-
-unsigned int fftfilt_crcf_get_length(fftfilt_crcf _q) { return _q->h_len; }
-
-void fftfilt_crcf_execute_block_dev(fftfilt_crcf _q, const liquid_float_complex *_dx, unsigned long long _n,
-                                    liquid_float_complex *_dy)
+static void lq_fftf_block_dev(lq_fftf *q, const void *dx, unsigned long long n, void *dy)
 {
-    if (_n == 0) return;
-    const void *x = _dx;
-    if ((const void *)_dx == (const void *)_dy) { /* kernel segments read overlapping halos */
-        void *c = lq_devbuf_get(&_q->cbuf, (size_t)_n * 8);
-        lqrt_d2d(c, _dx, (size_t)_n * 8, _q->ctx.stream);
+    if (n == 0) return;
+    const void *x = dx;
+    if (dx == dy) { /* kernel segments read overlapping halos */
+        void *c = lq_devbuf_get(&q->cbuf, (size_t)n * q->esz);
+        lqrt_d2d(c, dx, (size_t)n * q->esz, q->ctx.stream);
         x = c;
     }
-    const unsigned int hm1 = _q->h_len - 1;
-    void *hold = _q->d_hist[_q->cur], *hnew = _q->d_hist[_q->cur ^ 1];
-    const float s = _q->scale / (float)lqk_fftfilt_nfft();
-    lqk_fftfilt_run(0, _q->h_len, _q->d_H, hold, x, _n, _dy, s, 0.0f, _q->ctx.stream);
+    const unsigned int hm1 = q->h_len - 1;
+    void *hold = q->d_hist[q->cur], *hnew = q->d_hist[q->cur ^ 1];
+    const float nf = (float)lqk_fftfilt_nfft();
+    lqk_fftfilt_run(q->kind == LQ_RRRF, q->h_len, q->d_H, hold, x, n, dy, q->sre / nf, q->sim / nf, q->ctx.stream);
     if (hm1) {
-        lqk_window_append(1, hold, hm1, x, _n, hnew, _q->ctx.stream);
-        _q->cur ^= 1;
+        lqk_window_append(q->kind != LQ_RRRF, hold, hm1, x, n, hnew, q->ctx.stream);
+        q->cur ^= 1;
     }
 }
 
-void fftfilt_crcf_execute_block(fftfilt_crcf _q, liquid_float_complex *_x, unsigned long long _n,
-                                liquid_float_complex *_y)
+static void lq_fftf_block(lq_fftf *q, const void *x, unsigned long long n, void *y)
 {
-    if (_n == 0) return;
-    size_t bytes = (size_t)_n * 8;
-    void *dx = lq_devbuf_get(&_q->xbuf, bytes);
-    void *dy = lq_devbuf_get(&_q->ybuf, bytes);
-    lqrt_h2d(dx, _x, bytes, _q->ctx.stream);
-    fftfilt_crcf_execute_block_dev(_q, (const liquid_float_complex *)dx, _n, (liquid_float_complex *)dy);
-    lqrt_d2h(_y, dy, bytes, _q->ctx.stream);
-    lqrt_sync(_q->ctx.stream);
+    if (n == 0) return;
+    size_t bytes = (size_t)n * q->esz;
+    void *dx = lq_devbuf_get(&q->xbuf, bytes);
+    void *dy = lq_devbuf_get(&q->ybuf, bytes);
+    lqrt_h2d(dx, x, bytes, q->ctx.stream);
+    lq_fftf_block_dev(q, dx, n, dy);
+    lqrt_d2h(y, dy, bytes, q->ctx.stream);
+    lqrt_sync(q->ctx.stream);
 }
 
-/* fftfilt.c:193-260: exactly n samples in and out */
-void fftfilt_crcf_execute(fftfilt_crcf _q, liquid_float_complex *_x, liquid_float_complex *_y)
-{
-    fftfilt_crcf_execute_block(_q, _x, _q->n, _y);
-}
+#define LQ_FFTFILT_FRONT(NAME, KIND, TO, TC, TI, SRE, SIM)                                          \
+    struct NAME##_s {                                                                               \
+        lq_fftf *e;                                                                                 \
+    };                                                                                              \
+    NAME NAME##_create(TC *_h, unsigned int _h_len, unsigned int _n)                                \
+    {                                                                                               \
+        NAME q = (NAME)lq_xmalloc(sizeof(*q));                                                      \
+        q->e = lq_fftf_create(KIND, (const float *)_h, _h_len, _n);                                 \
+        return q;                                                                                   \
+    }                                                                                               \
+    void NAME##_destroy(NAME _q)                                                                    \
+    {                                                                                               \
+        lq_fftf_destroy(_q->e);                                                                     \
+        free(_q);                                                                                   \
+    }                                                                                               \
+    void NAME##_reset(NAME _q) { lq_fftf_reset(_q->e); }                                            \
+    void NAME##_print(NAME _q) { lq_fftf_print(_q->e); }                                            \
+    void NAME##_set_scale(NAME _q, TC _scale)                                                       \
+    {                                                                                               \
+        _q->e->sre = SRE;                                                                           \
+        _q->e->sim = SIM;                                                                           \
+    }                                                                                               \
+    unsigned int NAME##_get_length(NAME _q) { return _q->e->h_len; }                                \
+    /* fftfilt.c:193-260: exactly n samples in and out */                                           \
+    void NAME##_execute(NAME _q, TI *_x, TO *_y) { lq_fftf_block(_q->e, _x, _q->e->n, _y); }          \
+    void NAME##_execute_block(NAME _q, TI *_x, unsigned long long _n, TO *_y)                       \
+    {                                                                                               \
+        lq_fftf_block(_q->e, _x, _n, _y);                                                           \
+    }                                                                                               \
+    void NAME##_execute_block_dev(NAME _q, const TI *_dx, unsigned long long _n, TO *_dy)           \
+    {                                                                                               \
+        lq_fftf_block_dev(_q->e, _dx, _n, _dy);                                                     \
+    }                                                                                               \
+    void NAME##_set_stream(NAME _q, void *_s) { lq_ctx_set_stream(&_q->e->ctx, _s); }
 
-void fftfilt_crcf_set_stream(fftfilt_crcf _q, void *_s) { lq_ctx_set_stream(&_q->ctx, _s); }
+LQ_FFTFILT_FRONT(fftfilt_rrrf, LQ_RRRF, float, float, float, _scale, 0.0f)
+LQ_FFTFILT_FRONT(fftfilt_crcf, LQ_CRCF, liquid_float_complex, float, liquid_float_complex, _scale, 0.0f)
+LQ_FFTFILT_FRONT(fftfilt_cccf, LQ_CCCF, liquid_float_complex, liquid_float_complex, liquid_float_complex,
+                 crealf(_scale), cimagf(_scale))

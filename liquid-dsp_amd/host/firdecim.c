@@ -1,5 +1,5 @@
 /*
- * firdecim.c / firinterp -- firdecim_crcf and firinterp_crcf.
+ * firdecim.c -- firdecim_{rrrf,crcf,cccf} and firinterp_{rrrf,crcf,cccf}.
  *
  * firdecim: include/liquid.h:2664-2735, src/filter/src/firdecim.c:47-223.
  *   y[o] = sum_{k<h} h[k] x[o*M - k]: the output is formed right after the
@@ -9,42 +9,54 @@
  * firinterp: include/liquid.h:2496-2565, src/filter/src/firinterp.c:43-215.
  *   L = ceil(h/M), h' = h zero-padded to M*L, y[i*M + p] =
  *   sum_{l<L} h'[p + l*M] x[i - l]; create needs M >= 2 and h_len >= M.
+ *
+ * One generic engine per object (sample kind rrrf / crcf / cccf chooses the
+ * kernel instantiation and element sizes); the typed front ends at the end
+ * only forward.
  */
+#include <complex.h>
+
 #include "lq_host.h"
+
+static const char *lq_ext[] = {"rrrf", "crcf", "cccf"};
 
 /* ================================================================ firdecim */
 
-struct firdecim_crcf_s {
-    unsigned int M, hlen, HP;
-    float *h;
+typedef struct {
+    int kind;
+    size_t esz, csz;
+    unsigned int M, hlen;
+    float *h;          /* host copy, hlen coefficients of csz bytes */
     lqk_fir_desc d;
     void *d_hpad;
-    void *d_hist[2]; /* last HP-1 inputs */
+    void *d_hist[2];   /* last hlen-1 inputs */
     int cur;
     lq_ctx ctx;
     lq_devbuf xbuf, ybuf;
-};
+} lq_decim;
 
-firdecim_crcf firdecim_crcf_create(unsigned int _M, float *_h, unsigned int _h_len)
+static lq_decim *lq_decim_create(int kind, unsigned int M, const float *h, unsigned int hlen)
 {
-    if (_h_len == 0) LQ_FAIL("error: decim_crcf_create(), filter length must be greater than zero\n");
-    if (_M == 0) LQ_FAIL("error: decim_crcf_create(), decimation factor must be greater than zero\n");
-    lqrt_require_device("firdecim_crcf_create");
-    firdecim_crcf q = (firdecim_crcf)lq_xmalloc(sizeof(*q));
-    q->M = _M;
-    q->hlen = _h_len;
-    q->HP = _h_len;
-    q->h = (float *)lq_xmalloc(_h_len * sizeof(float));
-    memcpy(q->h, _h, _h_len * sizeof(float));
+    if (hlen == 0) LQ_FAIL("error: decim_%s_create(), filter length must be greater than zero\n", lq_ext[kind]);
+    if (M == 0) LQ_FAIL("error: decim_%s_create(), decimation factor must be greater than zero\n", lq_ext[kind]);
+    lqrt_require_device("firdecim_create");
+    lq_decim *q = (lq_decim *)lq_xmalloc(sizeof(*q));
+    q->kind = kind;
+    q->esz = kind == LQ_RRRF ? 4 : 8;
+    q->csz = kind == LQ_CCCF ? 8 : 4;
+    q->M = M;
+    q->hlen = hlen;
+    q->h = (float *)lq_xmalloc(hlen * q->csz);
+    memcpy(q->h, h, hlen * q->csz);
     lq_ctx_init(&q->ctx);
-    q->d_hpad = lqrt_malloc(_h_len * sizeof(float));
-    lqrt_h2d(q->d_hpad, q->h, _h_len * sizeof(float), q->ctx.stream);
-    q->d_hist[0] = lqrt_malloc((size_t)_h_len * 8);
-    q->d_hist[1] = lqrt_malloc((size_t)_h_len * 8);
+    q->d_hpad = lqrt_malloc(hlen * q->csz);
+    lqrt_h2d(q->d_hpad, q->h, hlen * q->csz, q->ctx.stream);
+    q->d_hist[0] = lqrt_malloc((size_t)hlen * q->esz);
+    q->d_hist[1] = lqrt_malloc((size_t)hlen * q->esz);
     lqrt_sync(q->ctx.stream);
-    q->d.kind = LQ_CRCF;
-    q->d.hlen = _h_len;
-    q->d.hc = _h_len; /* decim kernel takes HP = hc * nchunk directly */
+    q->d.kind = kind;
+    q->d.hlen = hlen;
+    q->d.hc = hlen; /* the decimator kernel takes HP = hc * nchunk directly */
     q->d.nchunk = 1;
     q->d.hpad = q->d_hpad;
     q->d.scale_re = 1.0f;
@@ -52,182 +64,258 @@ firdecim_crcf firdecim_crcf_create(unsigned int _M, float *_h, unsigned int _h_l
     return q;
 }
 
-firdecim_crcf firdecim_crcf_create_kaiser(unsigned int _M, unsigned int _m, float _As)
+/* firdecim.c:88-122: 2Mm+1 Kaiser taps at fc = 0.5/M, first 2Mm used */
+static float *lq_decim_kaiser(const char *who, unsigned int M, unsigned int m, float As, unsigned int *n)
 {
-    if (_M < 2) LQ_FAIL("error: decim_crcf_create_kaiser(), decim factor must be greater than 1\n");
-    if (_m == 0) LQ_FAIL("error: decim_crcf_create_kaiser(), filter delay must be greater than 0\n");
-    if (_As < 0.0f) LQ_FAIL("error: decim_crcf_create_kaiser(), stop-band attenuation must be positive\n");
-    unsigned int n = 2 * _M * _m + 1;
-    float *hf = (float *)lq_xmalloc(n * sizeof(float));
-    lq_firdes_kaiser(n, 0.5f / (float)_M, _As, 0.0f, hf);
-    firdecim_crcf q = firdecim_crcf_create(_M, hf, 2 * _M * _m);
-    free(hf);
-    return q;
+    if (M < 2) LQ_FAIL("error: %s_create_kaiser(), decim factor must be greater than 1\n", who);
+    if (m == 0) LQ_FAIL("error: %s_create_kaiser(), filter delay must be greater than 0\n", who);
+    if (As < 0.0f) LQ_FAIL("error: %s_create_kaiser(), stop-band attenuation must be positive\n", who);
+    *n = 2 * M * m + 1;
+    float *hf = (float *)lq_xmalloc(*n * sizeof(float));
+    lq_firdes_kaiser(*n, 0.5f / (float)M, As, 0.0f, hf);
+    return hf;
 }
 
-void firdecim_crcf_destroy(firdecim_crcf _q)
+static void lq_decim_destroy(lq_decim *q)
 {
-    lqrt_sync(_q->ctx.stream);
-    lqrt_free(_q->d_hpad);
-    lqrt_free(_q->d_hist[0]);
-    lqrt_free(_q->d_hist[1]);
-    lq_devbuf_free(&_q->xbuf);
-    lq_devbuf_free(&_q->ybuf);
-    lq_ctx_free(&_q->ctx);
-    free(_q->h);
-    free(_q);
+    lqrt_sync(q->ctx.stream);
+    lqrt_free(q->d_hpad);
+    lqrt_free(q->d_hist[0]);
+    lqrt_free(q->d_hist[1]);
+    lq_devbuf_free(&q->xbuf);
+    lq_devbuf_free(&q->ybuf);
+    lq_ctx_free(&q->ctx);
+    free(q->h);
+    free(q);
 }
 
-void firdecim_crcf_print(firdecim_crcf _q)
+static void lq_decim_print(lq_decim *q)
 {
-    printf("FIRDECIM() [%u] :\n", _q->M);
-    for (unsigned int i = 0; i < _q->hlen; i++) printf("  h(%3u) = %12.8f\n", i + 1, _q->h[i]);
-}
-
-void firdecim_crcf_clear(firdecim_crcf _q)
-{
-    lqrt_memset(_q->d_hist[0], (size_t)_q->hlen * 8, _q->ctx.stream);
-    lqrt_memset(_q->d_hist[1], (size_t)_q->hlen * 8, _q->ctx.stream);
-    lqrt_sync(_q->ctx.stream);
-}
-
-void firdecim_crcf_execute_block_dev(firdecim_crcf _q, const liquid_float_complex *_dx, unsigned long long _n,
-                                     liquid_float_complex *_dy)
-{
-    if (_n == 0) return;
-    void *hold = _q->d_hist[_q->cur], *hnew = _q->d_hist[_q->cur ^ 1];
-    lqk_firdecim(&_q->d, _q->M, hold, _dx, _n, _dy, _q->ctx.stream);
-    if (_q->HP > 1) {
-        lqk_window_append(1, hold, _q->HP - 1, _dx, _n * _q->M, hnew, _q->ctx.stream);
-        _q->cur ^= 1;
+    printf("FIRDECIM() [%u] :\n", q->M);
+    for (unsigned int i = 0; i < q->hlen; i++) {
+        if (q->kind == LQ_CCCF) printf("  h(%3u) = %12.8f + j*%12.8f\n", i + 1, q->h[2 * i], q->h[2 * i + 1]);
+        else printf("  h(%3u) = %12.8f\n", i + 1, q->h[i]);
     }
 }
 
-void firdecim_crcf_execute_block(firdecim_crcf _q, liquid_float_complex *_x, unsigned int _n,
-                                 liquid_float_complex *_y)
+static void lq_decim_clear(lq_decim *q)
 {
-    if (_n == 0) return;
-    size_t nin = (size_t)_n * _q->M * 8, nout = (size_t)_n * 8;
-    void *dx = lq_devbuf_get(&_q->xbuf, nin);
-    void *dy = lq_devbuf_get(&_q->ybuf, nout);
-    lqrt_h2d(dx, _x, nin, _q->ctx.stream);
-    firdecim_crcf_execute_block_dev(_q, (const liquid_float_complex *)dx, _n, (liquid_float_complex *)dy);
-    lqrt_d2h(_y, dy, nout, _q->ctx.stream);
-    lqrt_sync(_q->ctx.stream);
+    lqrt_memset(q->d_hist[0], (size_t)q->hlen * q->esz, q->ctx.stream);
+    lqrt_memset(q->d_hist[1], (size_t)q->hlen * q->esz, q->ctx.stream);
+    lqrt_sync(q->ctx.stream);
 }
 
-void firdecim_crcf_execute(firdecim_crcf _q, liquid_float_complex *_x, liquid_float_complex *_y)
+static void lq_decim_block_dev(lq_decim *q, const void *dx, unsigned long long nout, void *dy)
 {
-    firdecim_crcf_execute_block(_q, _x, 1, _y);
+    if (nout == 0) return;
+    void *hold = q->d_hist[q->cur], *hnew = q->d_hist[q->cur ^ 1];
+    lqk_firdecim(&q->d, q->M, hold, dx, nout, dy, q->ctx.stream);
+    if (q->hlen > 1) {
+        lqk_window_append(q->kind != LQ_RRRF, hold, q->hlen - 1, dx, nout * q->M, hnew, q->ctx.stream);
+        q->cur ^= 1;
+    }
 }
 
-void firdecim_crcf_set_stream(firdecim_crcf _q, void *_s) { lq_ctx_set_stream(&_q->ctx, _s); }
+static void lq_decim_block(lq_decim *q, const void *x, unsigned long long nout, void *y)
+{
+    if (nout == 0) return;
+    size_t nin = (size_t)nout * q->M * q->esz, nb = (size_t)nout * q->esz;
+    void *dx = lq_devbuf_get(&q->xbuf, nin);
+    void *dy = lq_devbuf_get(&q->ybuf, nb);
+    lqrt_h2d(dx, x, nin, q->ctx.stream);
+    lq_decim_block_dev(q, dx, nout, dy);
+    lqrt_d2h(y, dy, nb, q->ctx.stream);
+    lqrt_sync(q->ctx.stream);
+}
+
+#define LQ_FIRDECIM_FRONT(NAME, KIND, TO, TC, TI)                                                   \
+    struct NAME##_s {                                                                               \
+        lq_decim *e;                                                                                \
+    };                                                                                              \
+    NAME NAME##_create(unsigned int _M, TC *_h, unsigned int _h_len)                                \
+    {                                                                                               \
+        NAME q = (NAME)lq_xmalloc(sizeof(*q));                                                      \
+        q->e = lq_decim_create(KIND, _M, (const float *)_h, _h_len);                                \
+        return q;                                                                                   \
+    }                                                                                               \
+    NAME NAME##_create_kaiser(unsigned int _M, unsigned int _m, float _As)                          \
+    {                                                                                               \
+        unsigned int n;                                                                             \
+        float *hf = lq_decim_kaiser(#NAME, _M, _m, _As, &n);                                        \
+        TC *hc = (TC *)lq_xmalloc(n * sizeof(TC));                                                  \
+        for (unsigned int i = 0; i < n; i++) hc[i] = (TC)hf[i];                                     \
+        NAME q = NAME##_create(_M, hc, n - 1);                                                      \
+        free(hf);                                                                                   \
+        free(hc);                                                                                   \
+        return q;                                                                                   \
+    }                                                                                               \
+    void NAME##_destroy(NAME _q)                                                                    \
+    {                                                                                               \
+        lq_decim_destroy(_q->e);                                                                    \
+        free(_q);                                                                                   \
+    }                                                                                               \
+    void NAME##_print(NAME _q) { lq_decim_print(_q->e); }                                           \
+    void NAME##_clear(NAME _q) { lq_decim_clear(_q->e); }                                           \
+    void NAME##_execute(NAME _q, TI *_x, TO *_y) { lq_decim_block(_q->e, _x, 1, _y); }               \
+    void NAME##_execute_block(NAME _q, TI *_x, unsigned int _n, TO *_y)                             \
+    {                                                                                               \
+        lq_decim_block(_q->e, _x, _n, _y);                                                          \
+    }                                                                                               \
+    void NAME##_execute_block_dev(NAME _q, const TI *_dx, unsigned long long _n, TO *_dy)           \
+    {                                                                                               \
+        lq_decim_block_dev(_q->e, _dx, _n, _dy);                                                    \
+    }                                                                                               \
+    void NAME##_set_stream(NAME _q, void *_s) { lq_ctx_set_stream(&_q->e->ctx, _s); }
+
+LQ_FIRDECIM_FRONT(firdecim_rrrf, LQ_RRRF, float, float, float)
+LQ_FIRDECIM_FRONT(firdecim_crcf, LQ_CRCF, liquid_float_complex, float, liquid_float_complex)
+LQ_FIRDECIM_FRONT(firdecim_cccf, LQ_CCCF, liquid_float_complex, liquid_float_complex, liquid_float_complex)
 
 /* =============================================================== firinterp */
 
-struct firinterp_crcf_s {
+typedef struct {
+    int kind;
+    size_t esz, csz;
     unsigned int M, L, hlen;
-    float *h;          /* padded prototype, M*L taps */
+    float *h;          /* padded prototype, M*L coefficients of csz bytes */
     void *d_hpoly;     /* M x L: hpoly[p*L + l] = h'[p + l*M] */
     void *d_hist[2];   /* last L-1 inputs */
     int cur;
     lq_ctx ctx;
     lq_devbuf xbuf, ybuf;
-};
+} lq_interp;
 
-firinterp_crcf firinterp_crcf_create(unsigned int _M, float *_h, unsigned int _h_len)
+static lq_interp *lq_interp_create(int kind, unsigned int M, const float *h, unsigned int hlen)
 {
-    if (_M < 2) LQ_FAIL("error: firinterp_crcf_create(), interp factor must be greater than 1\n");
-    if (_h_len < _M) LQ_FAIL("error: firinterp_crcf_create(), filter length cannot be less than interp factor\n");
-    lqrt_require_device("firinterp_crcf_create");
-    firinterp_crcf q = (firinterp_crcf)lq_xmalloc(sizeof(*q));
-    q->M = _M;
+    if (M < 2) LQ_FAIL("error: firinterp_%s_create(), interp factor must be greater than 1\n", lq_ext[kind]);
+    if (hlen < M)
+        LQ_FAIL("error: firinterp_%s_create(), filter length cannot be less than interp factor\n", lq_ext[kind]);
+    lqrt_require_device("firinterp_create");
+    lq_interp *q = (lq_interp *)lq_xmalloc(sizeof(*q));
+    q->kind = kind;
+    q->esz = kind == LQ_RRRF ? 4 : 8;
+    q->csz = kind == LQ_CCCF ? 8 : 4;
+    const size_t cf = q->csz / 4;       /* floats per coefficient */
+    q->M = M;
     q->L = 0;
-    while (_M * q->L < _h_len) q->L++;
-    q->hlen = _M * q->L;
-    q->h = (float *)lq_xmalloc(q->hlen * sizeof(float));
-    for (unsigned int i = 0; i < q->hlen; i++) q->h[i] = i < _h_len ? _h[i] : 0.0f;
-    float *hp = (float *)lq_xmalloc(q->hlen * sizeof(float));
-    for (unsigned int p = 0; p < _M; p++)
-        for (unsigned int l = 0; l < q->L; l++) hp[p * q->L + l] = q->h[p + l * _M];
+    while (M * q->L < hlen) q->L++;
+    q->hlen = M * q->L;
+    q->h = (float *)lq_xmalloc(q->hlen * q->csz);  /* tail zero (firinterp.c:68-73) */
+    memcpy(q->h, h, hlen * q->csz);
+    float *hp = (float *)lq_xmalloc(q->hlen * q->csz);
+    for (unsigned int p = 0; p < M; p++)
+        for (unsigned int l = 0; l < q->L; l++)
+            memcpy(hp + cf * (p * q->L + l), q->h + cf * (p + l * M), q->csz);
     lq_ctx_init(&q->ctx);
-    q->d_hpoly = lqrt_malloc(q->hlen * sizeof(float));
-    lqrt_h2d(q->d_hpoly, hp, q->hlen * sizeof(float), q->ctx.stream);
-    q->d_hist[0] = lqrt_malloc((size_t)q->L * 8);
-    q->d_hist[1] = lqrt_malloc((size_t)q->L * 8);
+    q->d_hpoly = lqrt_malloc(q->hlen * q->csz);
+    lqrt_h2d(q->d_hpoly, hp, q->hlen * q->csz, q->ctx.stream);
+    q->d_hist[0] = lqrt_malloc((size_t)q->L * q->esz);
+    q->d_hist[1] = lqrt_malloc((size_t)q->L * q->esz);
     lqrt_sync(q->ctx.stream);
     free(hp);
     return q;
 }
 
-firinterp_crcf firinterp_crcf_create_kaiser(unsigned int _M, unsigned int _m, float _As)
+static float *lq_interp_kaiser(const char *who, unsigned int M, unsigned int m, float As, unsigned int *n)
 {
-    if (_M < 2) LQ_FAIL("error: firinterp_crcf_create_kaiser(), interp factor must be greater than 1\n");
-    if (_m == 0) LQ_FAIL("error: firinterp_crcf_create_kaiser(), filter delay must be greater than 0\n");
-    if (_As < 0.0f) LQ_FAIL("error: firinterp_crcf_create_kaiser(), stop-band attenuation must be positive\n");
-    unsigned int n = 2 * _M * _m + 1;
-    float *hf = (float *)lq_xmalloc(n * sizeof(float));
-    lq_firdes_kaiser(n, 0.5f / (float)_M, _As, 0.0f, hf);
-    firinterp_crcf q = firinterp_crcf_create(_M, hf, 2 * _M * _m);
-    free(hf);
-    return q;
+    if (M < 2) LQ_FAIL("error: %s_create_kaiser(), interp factor must be greater than 1\n", who);
+    if (m == 0) LQ_FAIL("error: %s_create_kaiser(), filter delay must be greater than 0\n", who);
+    if (As < 0.0f) LQ_FAIL("error: %s_create_kaiser(), stop-band attenuation must be positive\n", who);
+    *n = 2 * M * m + 1;
+    float *hf = (float *)lq_xmalloc(*n * sizeof(float));
+    lq_firdes_kaiser(*n, 0.5f / (float)M, As, 0.0f, hf);
+    return hf;
 }
 
-void firinterp_crcf_destroy(firinterp_crcf _q)
+static void lq_interp_destroy(lq_interp *q)
 {
-    lqrt_sync(_q->ctx.stream);
-    lqrt_free(_q->d_hpoly);
-    lqrt_free(_q->d_hist[0]);
-    lqrt_free(_q->d_hist[1]);
-    lq_devbuf_free(&_q->xbuf);
-    lq_devbuf_free(&_q->ybuf);
-    lq_ctx_free(&_q->ctx);
-    free(_q->h);
-    free(_q);
+    lqrt_sync(q->ctx.stream);
+    lqrt_free(q->d_hpoly);
+    lqrt_free(q->d_hist[0]);
+    lqrt_free(q->d_hist[1]);
+    lq_devbuf_free(&q->xbuf);
+    lq_devbuf_free(&q->ybuf);
+    lq_ctx_free(&q->ctx);
+    free(q->h);
+    free(q);
 }
 
-void firinterp_crcf_print(firinterp_crcf _q)
+static void lq_interp_print(lq_interp *q)
 {
     printf("interp():\n");
-    printf("    M       :   %u\n", _q->M);
-    printf("    h_len   :   %u\n", _q->hlen);
+    printf("    M       :   %u\n", q->M);
+    printf("    h_len   :   %u\n", q->hlen);
 }
 
-void firinterp_crcf_reset(firinterp_crcf _q)
+static void lq_interp_reset(lq_interp *q)
 {
-    lqrt_memset(_q->d_hist[0], (size_t)_q->L * 8, _q->ctx.stream);
-    lqrt_memset(_q->d_hist[1], (size_t)_q->L * 8, _q->ctx.stream);
-    lqrt_sync(_q->ctx.stream);
+    lqrt_memset(q->d_hist[0], (size_t)q->L * q->esz, q->ctx.stream);
+    lqrt_memset(q->d_hist[1], (size_t)q->L * q->esz, q->ctx.stream);
+    lqrt_sync(q->ctx.stream);
 }
 
-void firinterp_crcf_execute_block_dev(firinterp_crcf _q, const liquid_float_complex *_dx, unsigned long long _n,
-                                      liquid_float_complex *_dy)
+static void lq_interp_block_dev(lq_interp *q, const void *dx, unsigned long long n, void *dy)
 {
-    if (_n == 0) return;
-    void *hold = _q->d_hist[_q->cur], *hnew = _q->d_hist[_q->cur ^ 1];
-    lqk_firinterp(LQ_CRCF, _q->d_hpoly, _q->M, _q->L, 1.0f, hold, _dx, _n, _dy, _q->ctx.stream);
-    if (_q->L > 1) {
-        lqk_window_append(1, hold, _q->L - 1, _dx, _n, hnew, _q->ctx.stream);
-        _q->cur ^= 1;
+    if (n == 0) return;
+    void *hold = q->d_hist[q->cur], *hnew = q->d_hist[q->cur ^ 1];
+    lqk_firinterp(q->kind, q->d_hpoly, q->M, q->L, 1.0f, 0.0f, hold, dx, n, dy, q->ctx.stream);
+    if (q->L > 1) {
+        lqk_window_append(q->kind != LQ_RRRF, hold, q->L - 1, dx, n, hnew, q->ctx.stream);
+        q->cur ^= 1;
     }
 }
 
-void firinterp_crcf_execute_block(firinterp_crcf _q, liquid_float_complex *_x, unsigned int _n,
-                                  liquid_float_complex *_y)
+static void lq_interp_block(lq_interp *q, const void *x, unsigned long long n, void *y)
 {
-    if (_n == 0) return;
-    size_t nin = (size_t)_n * 8, nout = (size_t)_n * _q->M * 8;
-    void *dx = lq_devbuf_get(&_q->xbuf, nin);
-    void *dy = lq_devbuf_get(&_q->ybuf, nout);
-    lqrt_h2d(dx, _x, nin, _q->ctx.stream);
-    firinterp_crcf_execute_block_dev(_q, (const liquid_float_complex *)dx, _n, (liquid_float_complex *)dy);
-    lqrt_d2h(_y, dy, nout, _q->ctx.stream);
-    lqrt_sync(_q->ctx.stream);
+    if (n == 0) return;
+    size_t nin = (size_t)n * q->esz, nout = (size_t)n * q->M * q->esz;
+    void *dx = lq_devbuf_get(&q->xbuf, nin);
+    void *dy = lq_devbuf_get(&q->ybuf, nout);
+    lqrt_h2d(dx, x, nin, q->ctx.stream);
+    lq_interp_block_dev(q, dx, n, dy);
+    lqrt_d2h(y, dy, nout, q->ctx.stream);
+    lqrt_sync(q->ctx.stream);
 }
 
-void firinterp_crcf_execute(firinterp_crcf _q, liquid_float_complex _x, liquid_float_complex *_y)
-{
-    firinterp_crcf_execute_block(_q, &_x, 1, _y);
-}
+#define LQ_FIRINTERP_FRONT(NAME, KIND, TO, TC, TI)                                                  \
+    struct NAME##_s {                                                                               \
+        lq_interp *e;                                                                               \
+    };                                                                                              \
+    NAME NAME##_create(unsigned int _M, TC *_h, unsigned int _h_len)                                \
+    {                                                                                               \
+        NAME q = (NAME)lq_xmalloc(sizeof(*q));                                                      \
+        q->e = lq_interp_create(KIND, _M, (const float *)_h, _h_len);                               \
+        return q;                                                                                   \
+    }                                                                                               \
+    NAME NAME##_create_kaiser(unsigned int _M, unsigned int _m, float _As)                          \
+    {                                                                                               \
+        unsigned int n;                                                                             \
+        float *hf = lq_interp_kaiser(#NAME, _M, _m, _As, &n);                                       \
+        TC *hc = (TC *)lq_xmalloc(n * sizeof(TC));                                                  \
+        for (unsigned int i = 0; i < n; i++) hc[i] = (TC)hf[i];                                     \
+        NAME q = NAME##_create(_M, hc, n - 1);                                                      \
+        free(hf);                                                                                   \
+        free(hc);                                                                                   \
+        return q;                                                                                   \
+    }                                                                                               \
+    void NAME##_destroy(NAME _q)                                                                    \
+    {                                                                                               \
+        lq_interp_destroy(_q->e);                                                                   \
+        free(_q);                                                                                   \
+    }                                                                                               \
+    void NAME##_print(NAME _q) { lq_interp_print(_q->e); }                                          \
+    void NAME##_reset(NAME _q) { lq_interp_reset(_q->e); }                                          \
+    void NAME##_execute(NAME _q, TI _x, TO *_y) { lq_interp_block(_q->e, &_x, 1, _y); }              \
+    void NAME##_execute_block(NAME _q, TI *_x, unsigned int _n, TO *_y)                             \
+    {                                                                                               \
+        lq_interp_block(_q->e, _x, _n, _y);                                                         \
+    }                                                                                               \
+    void NAME##_execute_block_dev(NAME _q, const TI *_dx, unsigned long long _n, TO *_dy)           \
+    {                                                                                               \
+        lq_interp_block_dev(_q->e, _dx, _n, _dy);                                                   \
+    }                                                                                               \
+    void NAME##_set_stream(NAME _q, void *_s) { lq_ctx_set_stream(&_q->e->ctx, _s); }
 
-void firinterp_crcf_set_stream(firinterp_crcf _q, void *_s) { lq_ctx_set_stream(&_q->ctx, _s); }
+LQ_FIRINTERP_FRONT(firinterp_rrrf, LQ_RRRF, float, float, float)
+LQ_FIRINTERP_FRONT(firinterp_crcf, LQ_CRCF, liquid_float_complex, float, liquid_float_complex)
+LQ_FIRINTERP_FRONT(firinterp_cccf, LQ_CCCF, liquid_float_complex, liquid_float_complex, liquid_float_complex)

@@ -14,6 +14,7 @@
  * execute(), is computed by a HIP kernel.
  */
 #include <complex.h>
+#include <math.h>
 
 #include "lq_host.h"
 
@@ -222,6 +223,35 @@ void lq_firfilt_execute_block(lq_firfilt *q, const void *x, unsigned long long n
 }
 
 unsigned int lq_firfilt_get_length(lq_firfilt *q) { return q->hlen; }
+
+/* firfilt.c:371-387: H = scale * sum_i hr[i] e^{j 2 pi fc i}, hr = the
+ * reference's internally reversed taps (host arithmetic, as the reference) */
+static void lq_firfilt_freqresponse(lq_firfilt *q, float fc, liquid_float_complex *H)
+{
+    float complex acc = 0.0f;
+    const unsigned int n = q->hlen;
+    for (unsigned int i = 0; i < n; i++) {
+        const unsigned int k = n - 1 - i;
+        const float complex hk = q->kind == LQ_CCCF ? q->h[2 * k] + _Complex_I * q->h[2 * k + 1] : q->h[k];
+        acc += hk * cexpf(_Complex_I * 2 * M_PI * fc * i);
+    }
+    acc *= q->d.scale_re + _Complex_I * q->d.scale_im;
+    *H = acc;
+}
+
+/* firfilt.c:393-404 and group_delay.c:34-56 (real parts of the taps) */
+static float lq_firfilt_groupdelay(lq_firfilt *q, float fc)
+{
+    const unsigned int n = q->hlen;
+    if (fc < -0.5 || fc > 0.5) LQ_FAIL("error: fir_group_delay(), _fc must be in [-0.5,0.5]\n");
+    float complex t0 = 0.0f, t1 = 0.0f;
+    for (unsigned int i = 0; i < n; i++) {
+        const float hi = q->kind == LQ_CCCF ? q->h[2 * i] : q->h[i];
+        t0 += hi * cexpf(_Complex_I * 2 * M_PI * fc * i) * i;
+        t1 += hi * cexpf(_Complex_I * 2 * M_PI * fc * i);
+    }
+    return crealf(t0 / t1);
+}
 lq_ctx *lq_firfilt_ctx(lq_firfilt *q) { return &q->ctx; }
 
 /* ----------------------------------------------------------------- typed front ends */
@@ -277,6 +307,11 @@ lq_ctx *lq_firfilt_ctx(lq_firfilt *q) { return &q->ctx; }
         lq_firfilt_execute_block(_q->f, _x, _n, _y);                                                \
     }                                                                                               \
     unsigned int NAME##_get_length(NAME _q) { return lq_firfilt_get_length(_q->f); }                \
+    void NAME##_freqresponse(NAME _q, float _fc, liquid_float_complex *_H)                          \
+    {                                                                                               \
+        lq_firfilt_freqresponse(_q->f, _fc, _H);                                                    \
+    }                                                                                               \
+    float NAME##_groupdelay(NAME _q, float _fc) { return lq_firfilt_groupdelay(_q->f, _fc); }        \
     void NAME##_execute_block_dev(NAME _q, const TI *_dx, unsigned long long _n, TO *_dy)           \
     {                                                                                               \
         lq_firfilt_execute_block_dev(_q->f, _dx, _n, _dy);                                          \

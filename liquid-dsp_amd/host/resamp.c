@@ -1,9 +1,6 @@
 /*
- * resamp.c -- firpfb_crcf and resamp_crcf on the MI355X.
+ * resamp.c -- resamp_crcf on the MI355X.
  *
- * firpfb: include/liquid.h:2392-2486, src/filter/src/firpfb.c:46-345.
- *   Bank i = h[i + n*M], n < L = floor(h_len/M); push() appends one sample,
- *   execute(i) = scale * sum_n h[i + n*M] x[t-n].
  * resamp: include/liquid.h:2938-3015, src/filter/src/resamp.c:79-363.
  *   Prototype 2*m*npfb+1 Kaiser taps at fc/npfb scaled by npfb/sum(h); bank
  *   from the first 2*m*npfb taps (L = 2m); per input the float32 timing
@@ -23,173 +20,6 @@
 #include <math.h>
 
 #include "lq_host.h"
-
-/* ================================================================== firpfb */
-
-struct firpfb_crcf_s {
-    unsigned int M, hlen, L;
-    float scale;
-    float *hpoly;                 /* M x L, hpoly[i*L + n] = h[i + n*M] */
-    void *d_hpoly;
-    void *d_win[2];               /* last L inputs, oldest first */
-    int cur;
-    liquid_float_complex *h_win;  /* host mirror for push() */
-    int host_valid, dev_valid;
-    lq_ctx ctx;
-    lq_devbuf xbuf, ybuf, one;
-};
-
-firpfb_crcf firpfb_crcf_create(unsigned int _M, float *_h, unsigned int _h_len)
-{
-    if (_M == 0) LQ_FAIL("error: firpfb_crcf_create(), number of filters must be greater than zero\n");
-    if (_h_len == 0) LQ_FAIL("error: firpfb_crcf_create(), filter length must be greater than zero\n");
-    if (_h_len < _M) LQ_FAIL("error: firpfb_crcf_create(), filter length must be at least the number of filters\n");
-    lqrt_require_device("firpfb_crcf_create");
-    firpfb_crcf q = (firpfb_crcf)lq_xmalloc(sizeof(*q));
-    q->M = _M;
-    q->hlen = _h_len;
-    q->L = _h_len / _M;
-    q->scale = 1.0f;
-    q->hpoly = (float *)lq_xmalloc((size_t)_M * q->L * sizeof(float));
-    for (unsigned int i = 0; i < _M; i++)
-        for (unsigned int n = 0; n < q->L; n++) q->hpoly[i * q->L + n] = _h[i + n * _M];
-    lq_ctx_init(&q->ctx);
-    q->d_hpoly = lqrt_malloc((size_t)_M * q->L * sizeof(float));
-    lqrt_h2d(q->d_hpoly, q->hpoly, (size_t)_M * q->L * sizeof(float), q->ctx.stream);
-    q->d_win[0] = lqrt_malloc((size_t)q->L * 8);
-    q->d_win[1] = lqrt_malloc((size_t)q->L * 8);
-    q->h_win = (liquid_float_complex *)lq_xmalloc((size_t)q->L * 8);
-    q->host_valid = q->dev_valid = 1;
-    lqrt_sync(q->ctx.stream);
-    return q;
-}
-
-firpfb_crcf firpfb_crcf_create_kaiser(unsigned int _M, unsigned int _m, float _fc, float _As)
-{
-    if (_M == 0) LQ_FAIL("error: firpfb_crcf_create_kaiser(), number of filters must be greater than zero\n");
-    if (_m == 0) LQ_FAIL("error: firpfb_crcf_create_kaiser(), filter delay must be greater than 0\n");
-    if (_fc < 0.0f || _fc > 0.5f)
-        LQ_FAIL("error: firpfb_crcf_create_kaiser(), filter cut-off frequence must be in (0,0.5)\n");
-    if (_As < 0.0f)
-        LQ_FAIL("error: firpfb_crcf_create_kaiser(), filter excess bandwidth factor must be in [0,1]\n");
-    unsigned int n = 2 * _M * _m + 1;
-    float *hf = (float *)lq_xmalloc(n * sizeof(float));
-    lq_firdes_kaiser(n, _fc / (float)_M, _As, 0.0f, hf);
-    firpfb_crcf q = firpfb_crcf_create(_M, hf, n);
-    free(hf);
-    return q;
-}
-
-void firpfb_crcf_destroy(firpfb_crcf _q)
-{
-    lqrt_sync(_q->ctx.stream);
-    lqrt_free(_q->d_hpoly);
-    lqrt_free(_q->d_win[0]);
-    lqrt_free(_q->d_win[1]);
-    lq_devbuf_free(&_q->xbuf);
-    lq_devbuf_free(&_q->ybuf);
-    lq_devbuf_free(&_q->one);
-    lq_ctx_free(&_q->ctx);
-    free(_q->hpoly);
-    free(_q->h_win);
-    free(_q);
-}
-
-/* firpfb.c:250-277: a shape change re-creates the object */
-firpfb_crcf firpfb_crcf_recreate(firpfb_crcf _q, unsigned int _M, float *_h, unsigned int _h_len)
-{
-    if (_h_len != _q->hlen || _M != _q->M) {
-        firpfb_crcf_destroy(_q);
-        return firpfb_crcf_create(_M, _h, _h_len);
-    }
-    for (unsigned int i = 0; i < _M; i++)
-        for (unsigned int n = 0; n < _q->L; n++) _q->hpoly[i * _q->L + n] = _h[i + n * _M];
-    lqrt_sync(_q->ctx.stream);
-    lqrt_h2d(_q->d_hpoly, _q->hpoly, (size_t)_M * _q->L * sizeof(float), _q->ctx.stream);
-    lqrt_sync(_q->ctx.stream);
-    return _q;
-}
-
-void firpfb_crcf_print(firpfb_crcf _q)
-{
-    printf("fir polyphase filterbank [%u] :\n", _q->M);
-    for (unsigned int i = 0; i < _q->M; i++) printf("  bank %3u: \n", i);
-}
-
-void firpfb_crcf_set_scale(firpfb_crcf _q, float _g) { _q->scale = _g; }
-
-void firpfb_crcf_reset(firpfb_crcf _q)
-{
-    lqrt_memset(_q->d_win[0], (size_t)_q->L * 8, _q->ctx.stream);
-    lqrt_memset(_q->d_win[1], (size_t)_q->L * 8, _q->ctx.stream);
-    lqrt_sync(_q->ctx.stream);
-    memset(_q->h_win, 0, (size_t)_q->L * 8);
-    _q->host_valid = _q->dev_valid = 1;
-}
-
-static void firpfb_need_host(firpfb_crcf q)
-{
-    if (q->host_valid) return;
-    lqrt_d2h(q->h_win, q->d_win[q->cur], (size_t)q->L * 8, q->ctx.stream);
-    lqrt_sync(q->ctx.stream);
-    q->host_valid = 1;
-}
-
-static void firpfb_need_dev(firpfb_crcf q)
-{
-    if (q->dev_valid) return;
-    lqrt_h2d(q->d_win[q->cur], q->h_win, (size_t)q->L * 8, q->ctx.stream);
-    q->dev_valid = 1;
-}
-
-void firpfb_crcf_push(firpfb_crcf _q, liquid_float_complex _x)
-{
-    firpfb_need_host(_q);
-    memmove(_q->h_win, _q->h_win + 1, (size_t)(_q->L - 1) * 8);
-    _q->h_win[_q->L - 1] = _x;
-    _q->dev_valid = 0;
-}
-
-void firpfb_crcf_execute(firpfb_crcf _q, unsigned int _i, liquid_float_complex *_y)
-{
-    if (_i >= _q->M)
-        LQ_FAIL("error: firpfb_execute(), filterbank index (%u) exceeds maximum (%u)\n", _i, _q->M);
-    firpfb_need_dev(_q);
-    void *dy = lq_devbuf_get(&_q->one, 16);
-    lqk_firpfb_single(_q->d_hpoly, _q->L, _i, _q->d_win[_q->cur], _q->scale, dy, _q->ctx.stream);
-    lqrt_d2h(_y, dy, 8, _q->ctx.stream);
-    lqrt_sync(_q->ctx.stream);
-}
-
-void firpfb_crcf_execute_block_dev(firpfb_crcf _q, const liquid_float_complex *_dx, unsigned long long _n,
-                                   liquid_float_complex *_dy)
-{
-    if (_n == 0) return;
-    firpfb_need_dev(_q);
-    void *wold = _q->d_win[_q->cur], *wnew = _q->d_win[_q->cur ^ 1];
-    /* bank outputs after each push: the interpolator kernel (y[t*M+i]) on
-     * the window's last L-1 samples as history */
-    lqk_firinterp(LQ_CRCF, _q->d_hpoly, _q->M, _q->L, _q->scale, (const char *)wold + 8, _dx, _n, _dy,
-                  _q->ctx.stream);
-    lqk_window_append(1, wold, _q->L, _dx, _n, wnew, _q->ctx.stream);
-    _q->cur ^= 1;
-    _q->host_valid = 0;
-}
-
-void firpfb_crcf_execute_block(firpfb_crcf _q, liquid_float_complex *_x, unsigned long long _n,
-                               liquid_float_complex *_y)
-{
-    if (_n == 0) return;
-    size_t nin = (size_t)_n * 8, nout = nin * _q->M;
-    void *dx = lq_devbuf_get(&_q->xbuf, nin);
-    void *dy = lq_devbuf_get(&_q->ybuf, nout);
-    lqrt_h2d(dx, _x, nin, _q->ctx.stream);
-    firpfb_crcf_execute_block_dev(_q, (const liquid_float_complex *)dx, _n, (liquid_float_complex *)dy);
-    lqrt_d2h(_y, dy, nout, _q->ctx.stream);
-    lqrt_sync(_q->ctx.stream);
-}
-
-void firpfb_crcf_set_stream(firpfb_crcf _q, void *_s) { lq_ctx_set_stream(&_q->ctx, _s); }
 
 /* ================================================================== resamp */
 

@@ -97,6 +97,53 @@ def _declare(L):
             "firfilt_%s_get_stream" % t: (vp, [vp]),
             "firfilt_%s_synchronize" % t: (None, [vp]),
         })
+    for t in (RRRF, CRCF, CCCF):
+        ti = f if t == RRRF else cfloat          # sample passed by value
+        tc = cfloat if t == CCCF else f          # coefficient / scale by value
+        sig.update({
+            "firfilt_%s_freqresponse" % t: (None, [vp, f, vp]),
+            "firfilt_%s_groupdelay" % t: (f, [vp, f]),
+            "firdecim_%s_create" % t: (vp, [u, vp, u]),
+            "firdecim_%s_create_kaiser" % t: (vp, [u, u, f]),
+            "firdecim_%s_destroy" % t: (None, [vp]),
+            "firdecim_%s_print" % t: (None, [vp]),
+            "firdecim_%s_clear" % t: (None, [vp]),
+            "firdecim_%s_execute" % t: (None, [vp, vp, vp]),
+            "firdecim_%s_execute_block" % t: (None, [vp, vp, u, vp]),
+            "firdecim_%s_execute_block_dev" % t: (None, [vp, vp, ull, vp]),
+            "firdecim_%s_set_stream" % t: (None, [vp, vp]),
+            "firinterp_%s_create" % t: (vp, [u, vp, u]),
+            "firinterp_%s_create_kaiser" % t: (vp, [u, u, f]),
+            "firinterp_%s_destroy" % t: (None, [vp]),
+            "firinterp_%s_print" % t: (None, [vp]),
+            "firinterp_%s_reset" % t: (None, [vp]),
+            "firinterp_%s_execute" % t: (None, [vp, ti, vp]),
+            "firinterp_%s_execute_block" % t: (None, [vp, vp, u, vp]),
+            "firinterp_%s_execute_block_dev" % t: (None, [vp, vp, ull, vp]),
+            "firinterp_%s_set_stream" % t: (None, [vp, vp]),
+            "fftfilt_%s_create" % t: (vp, [vp, u, u]),
+            "fftfilt_%s_destroy" % t: (None, [vp]),
+            "fftfilt_%s_reset" % t: (None, [vp]),
+            "fftfilt_%s_print" % t: (None, [vp]),
+            "fftfilt_%s_set_scale" % t: (None, [vp, tc]),
+            "fftfilt_%s_execute" % t: (None, [vp, vp, vp]),
+            "fftfilt_%s_get_length" % t: (u, [vp]),
+            "fftfilt_%s_execute_block" % t: (None, [vp, vp, ull, vp]),
+            "fftfilt_%s_execute_block_dev" % t: (None, [vp, vp, ull, vp]),
+            "fftfilt_%s_set_stream" % t: (None, [vp, vp]),
+            "firpfb_%s_create" % t: (vp, [u, vp, u]),
+            "firpfb_%s_create_kaiser" % t: (vp, [u, u, f, f]),
+            "firpfb_%s_recreate" % t: (vp, [vp, u, vp, u]),
+            "firpfb_%s_destroy" % t: (None, [vp]),
+            "firpfb_%s_print" % t: (None, [vp]),
+            "firpfb_%s_set_scale" % t: (None, [vp, tc]),
+            "firpfb_%s_reset" % t: (None, [vp]),
+            "firpfb_%s_push" % t: (None, [vp, ti]),
+            "firpfb_%s_execute" % t: (None, [vp, u, vp]),
+            "firpfb_%s_execute_block" % t: (None, [vp, vp, ull, vp]),
+            "firpfb_%s_execute_block_dev" % t: (None, [vp, vp, ull, vp]),
+            "firpfb_%s_set_stream" % t: (None, [vp, vp]),
+        })
     sig.update({
         "liquid_firdes_kaiser": (None, [u, f, f, f, vp]),
         "kaiser_beta_As": (f, [f]),
@@ -106,29 +153,6 @@ def _declare(L):
         "liquid_mi355x_memcpy_h2d": (None, [vp, vp, ull]),
         "liquid_mi355x_memcpy_d2h": (None, [vp, vp, ull]),
         "liquid_mi355x_device_synchronize": (None, []),
-        "firdecim_crcf_create": (vp, [u, vp, u]),
-        "firdecim_crcf_create_kaiser": (vp, [u, u, f]),
-        "firdecim_crcf_destroy": (None, [vp]),
-        "firdecim_crcf_clear": (None, [vp]),
-        "firdecim_crcf_execute": (None, [vp, vp, vp]),
-        "firdecim_crcf_execute_block": (None, [vp, vp, u, vp]),
-        "firdecim_crcf_execute_block_dev": (None, [vp, vp, ull, vp]),
-        "firinterp_crcf_create": (vp, [u, vp, u]),
-        "firinterp_crcf_create_kaiser": (vp, [u, u, f]),
-        "firinterp_crcf_destroy": (None, [vp]),
-        "firinterp_crcf_reset": (None, [vp]),
-        "firinterp_crcf_execute": (None, [vp, cfloat, vp]),
-        "firinterp_crcf_execute_block": (None, [vp, vp, u, vp]),
-        "firinterp_crcf_execute_block_dev": (None, [vp, vp, ull, vp]),
-        "fftfilt_crcf_create": (vp, [vp, u, u]),
-        "fftfilt_crcf_destroy": (None, [vp]),
-        "fftfilt_crcf_reset": (None, [vp]),
-        "fftfilt_crcf_set_scale": (None, [vp, f]),
-        "fftfilt_crcf_execute": (None, [vp, vp, vp]),
-        "fftfilt_crcf_get_length": (u, [vp]),
-        "fftfilt_crcf_execute_block": (None, [vp, vp, ull, vp]),
-        "fftfilt_crcf_execute_block_dev": (None, [vp, vp, ull, vp]),
-        "fftfilt_crcf_set_stream": (None, [vp, vp]),
         "firpfbch_crcf_create": (vp, [i, u, u, vp]),
         "firpfbch_crcf_create_kaiser": (vp, [i, u, u, f]),
         "firpfbch_crcf_destroy": (None, [vp]),
@@ -147,18 +171,6 @@ def _declare(L):
         "firpfbch2_crcf_set_stream": (None, [vp, vp]),
         "firpfbch2_crcf_get_stream": (vp, [vp]),
         "firpfbch2_crcf_synchronize": (None, [vp]),
-        "firpfb_crcf_create": (vp, [u, vp, u]),
-        "firpfb_crcf_create_kaiser": (vp, [u, u, f, f]),
-        "firpfb_crcf_recreate": (vp, [vp, u, vp, u]),
-        "firpfb_crcf_destroy": (None, [vp]),
-        "firpfb_crcf_print": (None, [vp]),
-        "firpfb_crcf_set_scale": (None, [vp, f]),
-        "firpfb_crcf_reset": (None, [vp]),
-        "firpfb_crcf_push": (None, [vp, cfloat]),
-        "firpfb_crcf_execute": (None, [vp, u, vp]),
-        "firpfb_crcf_execute_block": (None, [vp, vp, ull, vp]),
-        "firpfb_crcf_execute_block_dev": (None, [vp, vp, ull, vp]),
-        "firpfb_crcf_set_stream": (None, [vp, vp]),
         "resamp_crcf_create": (vp, [f, u, f, f, u]),
         "resamp_crcf_create_default": (vp, [f]),
         "resamp_crcf_destroy": (None, [vp]),
@@ -253,6 +265,14 @@ class _Obj:
 
 
 class FirFilt(_Obj):
+    def freqresponse(self, fc):
+        H = cfloat(0.0, 0.0)
+        self._fn("_freqresponse")(self.q, fc, C.byref(H))
+        return complex(H.re, H.im) if hasattr(H, "re") else complex(H.real, H.imag)
+
+    def groupdelay(self, fc):
+        return float(self._fn("_groupdelay")(self.q, fc))
+
     def __init__(self, t, h=None, kaiser=None):
         self.t = t
         self.prefix = "firfilt_%s" % t
@@ -333,75 +353,91 @@ def dotprod_run(t, h, x):
     return y[0]
 
 
-class FirDecim(_Obj):
-    prefix = "firdecim_crcf"
+def _by_value(v, t):
+    if t == RRRF:
+        return float(np.real(v))
+    v = complex(v)
+    return cfloat(v.real, v.imag)
 
-    def __init__(self, M, h=None, m=None, As=None):
-        self.M = M
+
+def _out_dtype(t):
+    return np.float32 if t == RRRF else np.complex64
+
+
+class FirDecim(_Obj):
+    def __init__(self, M, h=None, m=None, As=None, t=CRCF):
+        self.M, self.t = M, t
+        self.prefix = "firdecim_%s" % t
         if h is None:
             self.q = self._fn("_create_kaiser")(M, m, As)
         else:
-            self._h = _coefs(h, CRCF)
+            self._h = _coefs(h, t)
             self.q = self._fn("_create")(M, ptr(self._h), len(self._h))
 
     def execute_block(self, x):
-        x = _samples(x, CRCF)
+        x = _samples(x, self.t)
         n = len(x) // self.M
-        y = np.zeros(n, np.complex64)
+        y = np.zeros(n, _out_dtype(self.t))
         self._fn("_execute_block")(self.q, ptr(x), n, ptr(y))
         return y
 
     def execute(self, x):
-        x = _samples(x, CRCF)
-        y = np.zeros(1, np.complex64)
+        x = _samples(x, self.t)
+        y = np.zeros(1, _out_dtype(self.t))
         self._fn("_execute")(self.q, ptr(x), ptr(y))
         return y[0]
 
+    def clear(self):
+        self._fn("_clear")(self.q)
+
 
 class FirInterp(_Obj):
-    prefix = "firinterp_crcf"
-
-    def __init__(self, M, h=None, m=None, As=None):
-        self.M = M
+    def __init__(self, M, h=None, m=None, As=None, t=CRCF):
+        self.M, self.t = M, t
+        self.prefix = "firinterp_%s" % t
         if h is None:
             self.q = self._fn("_create_kaiser")(M, m, As)
         else:
-            self._h = _coefs(h, CRCF)
+            self._h = _coefs(h, t)
             self.q = self._fn("_create")(M, ptr(self._h), len(self._h))
 
     def execute_block(self, x):
-        x = _samples(x, CRCF)
-        y = np.zeros(len(x) * self.M, np.complex64)
+        x = _samples(x, self.t)
+        y = np.zeros(len(x) * self.M, _out_dtype(self.t))
         self._fn("_execute_block")(self.q, ptr(x), len(x), ptr(y))
         return y
 
     def execute(self, v):
-        v = complex(v)
-        y = np.zeros(self.M, np.complex64)
-        self._fn("_execute")(self.q, cfloat(v.real, v.imag), ptr(y))
+        y = np.zeros(self.M, _out_dtype(self.t))
+        self._fn("_execute")(self.q, _by_value(v, self.t), ptr(y))
         return y
+
+    def reset(self):
+        self._fn("_reset")(self.q)
 
 
 class FftFilt(_Obj):
-    prefix = "fftfilt_crcf"
-
-    def __init__(self, h, n):
-        self.n = n
-        self._h = _coefs(h, CRCF)
+    def __init__(self, h, n, t=CRCF):
+        self.n, self.t = n, t
+        self.prefix = "fftfilt_%s" % t
+        self._h = _coefs(h, t)
         self.q = self._fn("_create")(ptr(self._h), len(self._h), n)
 
     def set_scale(self, s):
-        self._fn("_set_scale")(self.q, float(s))
+        self._fn("_set_scale")(self.q, _by_value(s, CCCF) if self.t == CCCF else float(np.real(s)))
+
+    def reset(self):
+        self._fn("_reset")(self.q)
 
     def execute(self, x):
-        x = _samples(x, CRCF)
+        x = _samples(x, self.t)
         assert len(x) == self.n
         y = np.zeros_like(x)
         self._fn("_execute")(self.q, ptr(x), ptr(y))
         return y
 
     def execute_block(self, x):
-        x = _samples(x, CRCF)
+        x = _samples(x, self.t)
         y = np.zeros_like(x)
         self._fn("_execute_block")(self.q, ptr(x), len(x), ptr(y))
         return y
@@ -476,35 +512,33 @@ class FirPfbch2(_Obj):
 
 
 class FirPfb(_Obj):
-    prefix = "firpfb_crcf"
-
-    def __init__(self, M, h=None, m=None, fc=None, As=None):
-        self.M = M
+    def __init__(self, M, h=None, m=None, fc=None, As=None, t=CRCF):
+        self.M, self.t = M, t
+        self.prefix = "firpfb_%s" % t
         if h is None:
             self.q = self._fn("_create_kaiser")(M, m, fc, As)
         else:
-            self._h = _coefs(h, CRCF)
+            self._h = _coefs(h, t)
             self.q = self._fn("_create")(M, ptr(self._h), len(self._h))
 
     def set_scale(self, s):
-        self._fn("_set_scale")(self.q, float(s))
+        self._fn("_set_scale")(self.q, _by_value(s, CCCF) if self.t == CCCF else float(np.real(s)))
 
     def reset(self):
         self._fn("_reset")(self.q)
 
     def push(self, v):
-        v = complex(v)
-        self._fn("_push")(self.q, cfloat(v.real, v.imag))
+        self._fn("_push")(self.q, _by_value(v, self.t))
 
     def execute(self, i):
-        y = np.zeros(1, np.complex64)
+        y = np.zeros(1, _out_dtype(self.t))
         self._fn("_execute")(self.q, i, ptr(y))
-        return complex(y[0])
+        return y[0]
 
     def execute_block(self, x):
         """push each x[t] and evaluate every bank: returns (len(x), M)"""
-        x = _samples(x, CRCF)
-        y = np.zeros(len(x) * self.M, np.complex64)
+        x = _samples(x, self.t)
+        y = np.zeros(len(x) * self.M, _out_dtype(self.t))
         self._fn("_execute_block")(self.q, ptr(x), len(x), ptr(y))
         return y.reshape(len(x), self.M)
 

@@ -191,6 +191,8 @@ class FirDecim(_Obj):
 
     def __init__(self, typ, M, h=None, m=None, As=None):
         self.typ, self.M = typ, M
+        if h is None and typ != CRCF:   # firdecim.c:88-122 design, first 2Mm taps, any type
+            h = firdes_kaiser(2 * M * m + 1, 0.5 / M, As, 0.0)[:2 * M * m]
         if h is None:
             self.q = lib().orc_firdecim_create_kaiser(M, m, As)
         else:
@@ -231,6 +233,8 @@ class FirInterp(_Obj):
 
     def __init__(self, typ, M, h=None, m=None, As=None):
         self.typ, self.M = typ, M
+        if h is None and typ != CRCF:   # firinterp.c:92-120 design, first 2Mm taps, any type
+            h = firdes_kaiser(2 * M * m + 1, 0.5 / M, As, 0.0)[:2 * M * m]
         if h is None:
             self.q = lib().orc_firinterp_create_kaiser(M, m, As)
         else:

@@ -57,10 +57,8 @@ def test_firfilt_golden(case):
 
 @pytest.mark.parametrize("case", G.load("firdecim"), ids=lambda c: c["name"])
 def test_firdecim_golden(case):
-    if case["type"] != "crcf":
-        pytest.skip("firdecim rrrf/cccf are not in the GPU scope yet (SURVEY 8f rank 2)")
     h, x, y = G.arr(case["h"]), G.arr(case["x"]), G.arr(case["y"])
-    q = LQ.FirDecim(case["M"], h)
+    q = LQ.FirDecim(case["M"], h, t=case["type"])
     out = np.array([q.execute(x[i * case["M"]:(i + 1) * case["M"]]) for i in range(len(y))])
     assert np.max(np.abs(out - y)) < case["tol"]
 
@@ -75,14 +73,12 @@ def _nextpow2(x):
 
 @pytest.mark.parametrize("case", G.load("fftfilt"), ids=lambda c: c["name"])
 def test_fftfilt_golden(case):
-    if case["type"] != "crcf":
-        pytest.skip("fftfilt rrrf/cccf are not in the GPU scope yet (SURVEY 8f rank 2)")
     h, x, y = G.arr(case["h"]), G.arr(case["x"]), G.arr(case["y"])
     n = 1 << _nextpow2(len(h) - 1)
     nb = -(-len(x) // n)
-    xp = np.zeros(nb * n, np.complex64)
+    xp = np.zeros(nb * n, np.float32 if case["type"] == "rrrf" else np.complex64)
     xp[: len(x)] = x
-    q = LQ.FftFilt(h, n)
+    q = LQ.FftFilt(h, n, t=case["type"])
     out = np.concatenate([q.execute(xp[b * n:(b + 1) * n]) for b in range(nb)])
     assert np.max(np.abs(out[: len(y)] - y)) < case["tol"]
 
@@ -194,37 +190,46 @@ def test_dotprod_batch_vs_oracle(t, n):
     assert G.nrm_err(Y, ref) < NRM
 
 
+@pytest.mark.parametrize("t", ["rrrf", "crcf", "cccf"])
 @pytest.mark.parametrize("M,m", [(2, 2), (4, 3), (8, 5), (16, 4), (64, 4)])
-def test_firdecim_vs_oracle(M, m):
+def test_firdecim_vs_oracle(M, m, t):
     r = rng(M)
-    x = cx(r, M * 5000)
-    g = LQ.FirDecim(M, m=m, As=60.0)
-    o = O.FirDecim(O.CRCF, M, m=m, As=60.0)
+    x = samples(r, t, M * 5000)
+    if t == "cccf":   # complex taps
+        h = coefs(r, t, 2 * M * m)
+        g, o = LQ.FirDecim(M, h, t=t), O.FirDecim(O.CCCF, M, h)
+    else:
+        g, o = LQ.FirDecim(M, m=m, As=60.0, t=t), O.FirDecim(TYPES[t], M, m=m, As=60.0)
     y = np.concatenate([g.execute_block(x[: M * 1234]), g.execute_block(x[M * 1234:])])
     assert G.nrm_err(y, o.execute_block(x)) < NRM
 
 
+@pytest.mark.parametrize("t", ["rrrf", "crcf", "cccf"])
 @pytest.mark.parametrize("M,m", [(2, 3), (4, 3), (8, 5), (32, 2)])
-def test_firinterp_vs_oracle(M, m):
+def test_firinterp_vs_oracle(M, m, t):
     r = rng(M + 1)
-    x = cx(r, 5000)
-    g = LQ.FirInterp(M, m=m, As=60.0)
-    o = O.FirInterp(O.CRCF, M, m=m, As=60.0)
-    y = np.concatenate([g.execute_block(x[:777]), g.execute_block(x[777:])])
+    x = samples(r, t, 5000)
+    if t == "cccf":
+        h = coefs(r, t, 2 * M * m - 3)     # ragged length: zero-padded to M*L
+        g, o = LQ.FirInterp(M, h, t=t), O.FirInterp(O.CCCF, M, h)
+    else:
+        g, o = LQ.FirInterp(M, m=m, As=60.0, t=t), O.FirInterp(TYPES[t], M, m=m, As=60.0)
+    y = np.concatenate([g.execute_block(x[:777])] + [g.execute(v) for v in x[777:780]] + [g.execute_block(x[780:])])
     assert G.nrm_err(y, o.execute_block(x)) < NRM
 
 
+@pytest.mark.parametrize("t", ["rrrf", "crcf", "cccf"])
 @pytest.mark.parametrize("hlen,n", [(4, 4), (23, 32), (512, 2048), (2049, 2048)])
-def test_fftfilt_vs_oracle(hlen, n):
+def test_fftfilt_vs_oracle(hlen, n, t):
     r = rng(hlen)
-    h = r.uniform(-0.5, 0.5, hlen).astype(np.float32)
+    h = coefs(r, t, hlen)
     nb = 40 if n <= 32 else 12
-    x = cx(r, n * nb)
-    g, o = LQ.FftFilt(h, n), O.FftFilt(O.CRCF, h, n)
-    g.set_scale(1.5)
-    o.set_scale(1.5)
+    x = samples(r, t, n * nb)
+    g, o = LQ.FftFilt(h, n, t=t), O.FftFilt(TYPES[t], h, n)
+    s = (1.5 - 0.25j) if t == "cccf" else 1.5
+    g.set_scale(s)            # linear: the oracle runs at unit scale and the reference is scaled after
     y = np.concatenate([g.execute(x[b * n:(b + 1) * n]) for b in range(nb)])
-    assert G.nrm_err(y, o.execute_stream(x)) < NRM
+    assert G.nrm_err(y, s * o.execute_stream(x)) < NRM
 
 
 def test_fftfilt_long_stream_block_extension():
@@ -318,19 +323,21 @@ def test_firpfb_known_answer():
     assert np.max(np.abs(out.imag)) == 0.0
 
 
+@pytest.mark.parametrize("t", ["rrrf", "crcf", "cccf"])
 @pytest.mark.parametrize("M,hlen", [(8, 64), (32, 449), (64, 896), (5, 7)])
-def test_firpfb_block_and_push_vs_oracle(M, hlen):
+def test_firpfb_block_and_push_vs_oracle(M, hlen, t):
     r = rng(M * 3 + hlen)
-    h = r.uniform(-0.5, 0.5, hlen).astype(np.float32)
-    x = cx(r, 3000)
-    g = LQ.FirPfb(M, h)
-    o = O.FirPfb(O.CRCF, M, h)
-    g.set_scale(0.8)
-    o.set_scale(0.8)
-    ref = np.empty((len(x), M), np.complex64)
-    for t, v in enumerate(x):
+    h = coefs(r, t, hlen)
+    x = samples(r, t, 3000)
+    g = LQ.FirPfb(M, h, t=t)
+    o = O.FirPfb(TYPES[t], M, h)
+    s = (0.8 + 0.1j) if t == "cccf" else 0.8
+    g.set_scale(s)            # linear: the oracle runs at unit scale and the reference is scaled after
+    ref = np.empty((len(x), M), np.float32 if t == "rrrf" else np.complex64)
+    for k, v in enumerate(x):
         o.push(v)
-        ref[t] = [o.execute(i) for i in range(M)]
+        ref[k] = [o.execute(i) for i in range(M)]
+    ref = ref * s
     y1 = g.execute_block(x[:2000])
     for v in x[2000:2010]:              # per-sample push/execute after a block call
         g.push(v)
@@ -339,6 +346,24 @@ def test_firpfb_block_and_push_vs_oracle(M, hlen):
     assert G.nrm_err(y1, ref[:2000]) < NRM
     assert G.nrm_err(per, ref[2009]) < NRM
     assert G.nrm_err(y2, ref[2010:]) < NRM
+
+
+def test_firfilt_freqresponse_groupdelay():
+    # firfilt.c:371-404 restated in float64: H = s * sum_i h[n-1-i] e^{j2pi fc i}
+    r = rng(3)
+    for t in ("rrrf", "crcf", "cccf"):
+        h = coefs(r, t, 37)
+        g = LQ.FirFilt(t, h)
+        s = (0.9 + 0.2j) if t == "cccf" else 0.9
+        g.set_scale(s)
+        i = np.arange(len(h))
+        for fc in (-0.31, 0.0, 0.125, 0.4):
+            H = s * np.sum(h[::-1].astype(np.complex128) * np.exp(2j * np.pi * fc * i))
+            assert abs(g.freqresponse(fc) - H) <= 1e-5 * max(1.0, abs(H))
+            hr = np.real(h).astype(np.float64)
+            e = np.exp(2j * np.pi * fc * i)
+            gd = np.real(np.sum(hr * e * i) / np.sum(hr * e))
+            assert abs(g.groupdelay(fc) - gd) <= 1e-3 * max(1.0, abs(gd))
 
 
 def _resamp_pair(rate, m=7, fc=0.25, As=60.0, npfb=64):

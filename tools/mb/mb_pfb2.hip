@@ -17,15 +17,15 @@ void lq_check(hipError_t e, const char *what, const char *file, int line)
 static float2 *g_tw = nullptr;
 extern "C" const float *lqrt_twiddles(void) { return (const float *)g_tw; }
 
-template <int X, int SM = 2, int PF = 4, int BAR = 1>
+template <int X, int SM = 2, int PF = 4, int BAR = 1, int TRES = 0>
 static void run(const char *name, Params P, const float *hsub, unsigned nwg, int iters)
 {
     hipEvent_t e0, e1;
     LQ_CHECK(hipEventCreate(&e0));
     LQ_CHECK(hipEventCreate(&e1));
-    hipLaunchKernelGGL((k_pfb2_an1024<8, X, SM, PF, BAR>), dim3(nwg), dim3(NT), 0, 0, P, hsub, g_tw);
+    hipLaunchKernelGGL((k_pfb2_an1024<8, X, SM, PF, BAR, TRES>), dim3(nwg), dim3(NT), 0, 0, P, hsub, g_tw);
     LQ_CHECK(hipEventRecord(e0));
-    for (int i = 0; i < iters; i++) hipLaunchKernelGGL((k_pfb2_an1024<8, X, SM, PF, BAR>), dim3(nwg), dim3(NT), 0, 0, P, hsub, g_tw);
+    for (int i = 0; i < iters; i++) hipLaunchKernelGGL((k_pfb2_an1024<8, X, SM, PF, BAR, TRES>), dim3(nwg), dim3(NT), 0, 0, P, hsub, g_tw);
     LQ_CHECK(hipEventRecord(e1));
     LQ_CHECK(hipEventSynchronize(e1));
     float ms;
@@ -87,14 +87,10 @@ int main()
     P.gend = ngroups;
     const int it = 10;
     for (int rep = 0; rep < 2; rep++) {
-        run<0, 0, 4, 0>("old: smode0 PF4 syncthreads", P, hsub, nwg, it);
-        run<0, 2, 4, 0>("smode2 PF4 syncthreads", P, hsub, nwg, it);
-        run<0, 2, 6, 0>("smode2 PF6 syncthreads", P, hsub, nwg, it);
-        run<0, 2, 4, 1>("smode2 PF4 ldsbar", P, hsub, nwg, it);
-        run<0, 2, 6, 1>("smode2 PF6 ldsbar", P, hsub, nwg, it);
-        run<0, 2, 8, 1>("smode2 PF8 ldsbar", P, hsub, nwg, it);
-        run<0, 0, 4, 1>("smode0 PF4 ldsbar", P, hsub, nwg, it);
-        run<10, 2, 6, 1>("smode2 PF6 ldsbar (clock)", P, hsub, nwg, it);
+        run<0, 2, 4, 1, 0>("PF4 taps reloaded", P, hsub, nwg, it);
+        run<0, 2, 4, 1, 1>("PF4 taps resident", P, hsub, nwg, it);
+        run<0, 2, 2, 1, 1>("PF2 taps resident", P, hsub, nwg, it);
+        run<0, 2, 2, 1, 0>("PF2 taps reloaded", P, hsub, nwg, it);
     }
     return 0;
 }
