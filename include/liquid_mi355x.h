@@ -59,6 +59,19 @@ LIQUID_DEFINE_COMPLEX(float, liquid_float_complex);
 /* ------------------------------------------------------------------------ */
 float kaiser_beta_As(float _As);
 void liquid_firdes_kaiser(unsigned int _n, float _fc, float _As, float _mu, float *_h);
+/* liquid.h:1580 */
+void liquid_firdes_rrcos(unsigned int _k, unsigned int _m, float _beta, float _dt, float *_h);
+/* liquid.h:4445 */
+float hamming(unsigned int _n, unsigned int _N);
+
+/* ------------------------------------------------------------------------ */
+/* random helpers (liquid.h:6301-6315): test-signal generation on the host   */
+/* ------------------------------------------------------------------------ */
+float randf(void);
+float randnf(void);
+void awgn(float *_x, float _nstd);
+void crandnf(liquid_float_complex *_y);
+void cawgn(liquid_float_complex *_x, float _nstd);
 
 /* ------------------------------------------------------------------------ */
 /* dotprod (liquid.h:503-560): rrrf, crcf, cccf                              */

@@ -76,3 +76,12 @@ def test_examples_compile_and_link(src, tmp_path):
     subprocess.check_call(["gcc", "-std=gnu99", "-O2", "-Wall", "-I", inc, os.path.join(ROOT, "examples", src),
                            "-L", libdir, "-lliquid_mi355x", "-Wl,-rpath," + libdir, "-lm", "-o", str(out)])
     assert out.exists()
+
+
+@pytest.mark.skipif(not os.path.isdir("/root/reference/examples"), reason="reference sources not present")
+def test_reference_examples_compile_unchanged():
+    """liquid-dsp's own examples for this path compile and link, unchanged,
+    against include/liquid.h + libliquid_mi355x (tools/build_ref_examples.sh)."""
+    subprocess.check_call(["bash", os.path.join(ROOT, "tools", "build_ref_examples.sh")])
+    built = os.listdir(os.path.join(ROOT, "build", "ref_examples"))
+    assert len(built) == 12

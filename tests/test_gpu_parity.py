@@ -457,3 +457,17 @@ def test_examples_run_on_gpu(src, tmp_path):
     res = subprocess.run([str(out)], capture_output=True, text=True, timeout=120)
     print(res.stdout, res.stderr)
     assert res.returncode == 0
+
+
+REF_EX = os.path.join(LQ.ROOT, "build", "ref_examples")
+
+
+@pytest.mark.skipif(not os.path.isdir(REF_EX), reason="reference examples not built (tools/build_ref_examples.sh)")
+@pytest.mark.parametrize("exe", sorted(os.listdir(REF_EX)) if os.path.isdir(REF_EX) else [])
+def test_reference_examples_run(exe, tmp_path):
+    """liquid-dsp's own example programs, compiled unchanged against the
+    drop-in header, run to completion on the GPU (they write .m files)."""
+    res = subprocess.run([os.path.join(REF_EX, exe)], capture_output=True, text=True, timeout=120, cwd=tmp_path)
+    print(res.stdout[-2000:], res.stderr[-2000:])
+    assert res.returncode == 0
+    assert "error" not in res.stderr.lower()
