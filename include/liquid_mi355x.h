@@ -59,8 +59,65 @@ LIQUID_DEFINE_COMPLEX(float, liquid_float_complex);
 /* ------------------------------------------------------------------------ */
 float kaiser_beta_As(float _As);
 void liquid_firdes_kaiser(unsigned int _n, float _fc, float _As, float _mu, float *_h);
-/* liquid.h:1580 */
+/* liquid.h:1413-1435: prototype filter types */
+typedef enum {
+    LIQUID_FIRFILT_UNKNOWN = 0,
+    LIQUID_FIRFILT_KAISER,
+    LIQUID_FIRFILT_PM,
+    LIQUID_FIRFILT_RCOS,
+    LIQUID_FIRFILT_FEXP,
+    LIQUID_FIRFILT_FSECH,
+    LIQUID_FIRFILT_FARCSECH,
+    LIQUID_FIRFILT_ARKAISER,
+    LIQUID_FIRFILT_RKAISER,
+    LIQUID_FIRFILT_RRC,
+    LIQUID_FIRFILT_hM3,
+    LIQUID_FIRFILT_GMSKTX,
+    LIQUID_FIRFILT_GMSKRX,
+    LIQUID_FIRFILT_RFEXP,
+    LIQUID_FIRFILT_RFSECH,
+    LIQUID_FIRFILT_RFARCSECH,
+} liquid_firfilt_type;
+/* liquid.h:1444-1471 */
+void liquid_firdes_prototype(liquid_firfilt_type _type, unsigned int _k, unsigned int _m, float _beta, float _dt,
+                             float *_h);
+int liquid_getopt_str2firfilt(const char *_str);
+unsigned int estimate_req_filter_len(float _df, float _As);
+float estimate_req_filter_As(float _df, unsigned int _N);
+float estimate_req_filter_df(float _As, unsigned int _N);
+/* liquid.h:1481-1512: Parks-McClellan (this build designs band-pass filters) */
+typedef enum {
+    LIQUID_FIRDESPM_BANDPASS = 0,
+    LIQUID_FIRDESPM_DIFFERENTIATOR,
+    LIQUID_FIRDESPM_HILBERT
+} liquid_firdespm_btype;
+typedef enum {
+    LIQUID_FIRDESPM_FLATWEIGHT = 0,
+    LIQUID_FIRDESPM_EXPWEIGHT,
+    LIQUID_FIRDESPM_LINWEIGHT,
+} liquid_firdespm_wtype;
+void firdespm_run(unsigned int _h_len, unsigned int _num_bands, float *_bands, float *_des, float *_weights,
+                  liquid_firdespm_wtype *_wtype, liquid_firdespm_btype _btype, float *_h);
+/* liquid.h:1573-1605 */
+void liquid_firdes_rcos(unsigned int _k, unsigned int _m, float _beta, float _dt, float *_h);
 void liquid_firdes_rrcos(unsigned int _k, unsigned int _m, float _beta, float _dt, float *_h);
+void liquid_firdes_rkaiser(unsigned int _k, unsigned int _m, float _beta, float _dt, float *_h);
+void liquid_firdes_arkaiser(unsigned int _k, unsigned int _m, float _beta, float _dt, float *_h);
+float rkaiser_approximate_rho(unsigned int _m, float _beta);
+void liquid_firdes_hM3(unsigned int _k, unsigned int _m, float _beta, float _dt, float *_h);
+void liquid_firdes_gmsktx(unsigned int _k, unsigned int _m, float _beta, float _dt, float *_h);
+void liquid_firdes_gmskrx(unsigned int _k, unsigned int _m, float _beta, float _dt, float *_h);
+void liquid_firdes_fexp(unsigned int _k, unsigned int _m, float _beta, float _dt, float *_h);
+void liquid_firdes_rfexp(unsigned int _k, unsigned int _m, float _beta, float _dt, float *_h);
+void liquid_firdes_fsech(unsigned int _k, unsigned int _m, float _beta, float _dt, float *_h);
+void liquid_firdes_rfsech(unsigned int _k, unsigned int _m, float _beta, float _dt, float *_h);
+void liquid_firdes_farcsech(unsigned int _k, unsigned int _m, float _beta, float _dt, float *_h);
+void liquid_firdes_rfarcsech(unsigned int _k, unsigned int _m, float _beta, float _dt, float *_h);
+/* liquid.h:1635-1668 */
+float liquid_filter_autocorr(float *_h, unsigned int _h_len, int _lag);
+void liquid_filter_isi(float *_h, unsigned int _k, unsigned int _m, float *_rms, float *_max);
+/* liquid.h:4396 */
+float liquid_Qf(float _z);
 /* liquid.h:4445 */
 float hamming(unsigned int _n, unsigned int _N);
 
@@ -105,6 +162,7 @@ LQMI_DOTPROD_API(dotprod_cccf, liquid_float_complex, liquid_float_complex, liqui
     FIRFILT FIRFILT##_create(TC *_h, unsigned int _n);                                          \
     FIRFILT FIRFILT##_create_kaiser(unsigned int _n, float _fc, float _As, float _mu);          \
     FIRFILT FIRFILT##_create_rect(unsigned int _n);                                             \
+    FIRFILT FIRFILT##_create_rnyquist(int _type, unsigned int _k, unsigned int _m, float _beta, float _mu);\
     FIRFILT FIRFILT##_recreate(FIRFILT _q, TC *_h, unsigned int _n);                            \
     void FIRFILT##_destroy(FIRFILT _q);                                                         \
     void FIRFILT##_reset(FIRFILT _q);                                                           \
@@ -134,6 +192,7 @@ LQMI_FIRFILT_API(firfilt_cccf, liquid_float_complex, liquid_float_complex, liqui
     typedef struct FIRDECIM##_s *FIRDECIM;                                                      \
     FIRDECIM FIRDECIM##_create(unsigned int _M, TC *_h, unsigned int _h_len);                   \
     FIRDECIM FIRDECIM##_create_kaiser(unsigned int _M, unsigned int _m, float _As);             \
+    FIRDECIM FIRDECIM##_create_prototype(int _type, unsigned int _M, unsigned int _m, float _beta, float _dt);\
     void FIRDECIM##_destroy(FIRDECIM _q);                                                       \
     void FIRDECIM##_print(FIRDECIM _q);                                                         \
     void FIRDECIM##_clear(FIRDECIM _q);                                                         \
@@ -155,6 +214,7 @@ LQMI_FIRDECIM_API(firdecim_cccf, liquid_float_complex, liquid_float_complex, liq
     typedef struct FIRINTERP##_s *FIRINTERP;                                                    \
     FIRINTERP FIRINTERP##_create(unsigned int _M, TC *_h, unsigned int _h_len);                 \
     FIRINTERP FIRINTERP##_create_kaiser(unsigned int _M, unsigned int _m, float _As);           \
+    FIRINTERP FIRINTERP##_create_prototype(int _type, unsigned int _M, unsigned int _m, float _beta, float _dt);\
     void FIRINTERP##_destroy(FIRINTERP _q);                                                     \
     void FIRINTERP##_print(FIRINTERP _q);                                                       \
     void FIRINTERP##_reset(FIRINTERP _q);                                                       \
@@ -176,6 +236,8 @@ LQMI_FIRINTERP_API(firinterp_cccf, liquid_float_complex, liquid_float_complex, l
     typedef struct FIRPFB##_s *FIRPFB;                                                          \
     FIRPFB FIRPFB##_create(unsigned int _M, TC *_h, unsigned int _h_len);                       \
     FIRPFB FIRPFB##_create_kaiser(unsigned int _M, unsigned int _m, float _fc, float _As);      \
+    FIRPFB FIRPFB##_create_rnyquist(int _type, unsigned int _M, unsigned int _k, unsigned int _m, float _beta);\
+    FIRPFB FIRPFB##_create_drnyquist(int _type, unsigned int _M, unsigned int _k, unsigned int _m, float _beta);\
     FIRPFB FIRPFB##_recreate(FIRPFB _q, unsigned int _M, TC *_h, unsigned int _h_len);          \
     void FIRPFB##_destroy(FIRPFB _q);                                                           \
     void FIRPFB##_print(FIRPFB _q);                                                             \
@@ -194,30 +256,32 @@ LQMI_FIRPFB_API(firpfb_crcf, liquid_float_complex, float, liquid_float_complex)
 LQMI_FIRPFB_API(firpfb_cccf, liquid_float_complex, liquid_float_complex, liquid_float_complex)
 
 /* ------------------------------------------------------------------------ */
-/* resamp (liquid.h:2938-3015): crcf                                         */
+/* resamp (liquid.h:2938-3015): rrrf, crcf, cccf                            */
 /* ------------------------------------------------------------------------ */
-typedef struct resamp_crcf_s *resamp_crcf;
-resamp_crcf resamp_crcf_create(float _rate, unsigned int _m, float _fc, float _As, unsigned int _npfb);
-resamp_crcf resamp_crcf_create_default(float _rate);
-void resamp_crcf_destroy(resamp_crcf _q);
-void resamp_crcf_print(resamp_crcf _q);
-void resamp_crcf_reset(resamp_crcf _q);
-unsigned int resamp_crcf_get_delay(resamp_crcf _q);
-void resamp_crcf_set_rate(resamp_crcf _q, float _rate);
-void resamp_crcf_adjust_rate(resamp_crcf _q, float _delta);
-void resamp_crcf_execute(resamp_crcf _q, liquid_float_complex _x, liquid_float_complex *_y,
-                         unsigned int *_num_written);
-void resamp_crcf_execute_block(resamp_crcf _q, liquid_float_complex *_x, unsigned int _nx,
-                               liquid_float_complex *_y, unsigned int *_ny);
-/* extension: number of outputs the next _nx inputs will produce (size _y with it) */
-unsigned long long resamp_crcf_num_output(resamp_crcf _q, unsigned long long _nx);
-/* extension: device pointers, asynchronous on the object's stream; *_ny is
- * known (and written) before the call returns */
-void resamp_crcf_execute_block_dev(resamp_crcf _q, const liquid_float_complex *_dx,
-                                   unsigned long long _nx, liquid_float_complex *_dy,
-                                   unsigned long long *_ny);
-void resamp_crcf_set_stream(resamp_crcf _q, void *_hip_stream);
-void resamp_crcf_synchronize(resamp_crcf _q);
+#define LQMI_RESAMP_API(RESAMP, T)                                                                  \
+    typedef struct RESAMP##_s *RESAMP;                                                              \
+    RESAMP RESAMP##_create(float _rate, unsigned int _m, float _fc, float _As, unsigned int _npfb);  \
+    RESAMP RESAMP##_create_default(float _rate);                                                    \
+    void RESAMP##_destroy(RESAMP _q);                                                               \
+    void RESAMP##_print(RESAMP _q);                                                                 \
+    void RESAMP##_reset(RESAMP _q);                                                                 \
+    unsigned int RESAMP##_get_delay(RESAMP _q);                                                     \
+    void RESAMP##_set_rate(RESAMP _q, float _rate);                                                 \
+    void RESAMP##_adjust_rate(RESAMP _q, float _delta);                                             \
+    void RESAMP##_execute(RESAMP _q, T _x, T *_y, unsigned int *_num_written);                      \
+    void RESAMP##_execute_block(RESAMP _q, T *_x, unsigned int _nx, T *_y, unsigned int *_ny);      \
+    /* extension: number of outputs the next _nx inputs will produce (size _y with it) */          \
+    unsigned long long RESAMP##_num_output(RESAMP _q, unsigned long long _nx);                      \
+    /* extension: device pointers, asynchronous on the object's stream; *_ny is                     \
+     * known (and written) before the call returns */                                               \
+    void RESAMP##_execute_block_dev(RESAMP _q, const T *_dx, unsigned long long _nx, T *_dy,         \
+                                    unsigned long long *_ny);                                       \
+    void RESAMP##_set_stream(RESAMP _q, void *_hip_stream);                                         \
+    void RESAMP##_synchronize(RESAMP _q);
+
+LQMI_RESAMP_API(resamp_rrrf, float)
+LQMI_RESAMP_API(resamp_crcf, liquid_float_complex)
+LQMI_RESAMP_API(resamp_cccf, liquid_float_complex)
 
 /* ------------------------------------------------------------------------ */
 /* fftfilt (liquid.h:2192-2240): rrrf, crcf, cccf                            */
@@ -242,24 +306,30 @@ LQMI_FFTFILT_API(fftfilt_crcf, liquid_float_complex, float, liquid_float_complex
 LQMI_FFTFILT_API(fftfilt_cccf, liquid_float_complex, liquid_float_complex, liquid_float_complex)
 
 /* ------------------------------------------------------------------------ */
-/* firpfbch (liquid.h:5667-5739): crcf                                       */
+/* firpfbch (liquid.h:5667-5739): crcf, cccf                                 */
 /* ------------------------------------------------------------------------ */
-typedef struct firpfbch_crcf_s *firpfbch_crcf;
-firpfbch_crcf firpfbch_crcf_create(int _type, unsigned int _M, unsigned int _p, float *_h);
-firpfbch_crcf firpfbch_crcf_create_kaiser(int _type, unsigned int _M, unsigned int _m, float _As);
-void firpfbch_crcf_destroy(firpfbch_crcf _q);
-void firpfbch_crcf_reset(firpfbch_crcf _q);
-void firpfbch_crcf_print(firpfbch_crcf _q);
-void firpfbch_crcf_synthesizer_execute(firpfbch_crcf _q, liquid_float_complex *_x,
-                                       liquid_float_complex *_y);
-void firpfbch_crcf_analyzer_execute(firpfbch_crcf _q, liquid_float_complex *_x,
-                                    liquid_float_complex *_y);
-/* extension: _nblocks consecutive calls (M in, M out each), host / device pointers */
-void firpfbch_crcf_execute_block(firpfbch_crcf _q, liquid_float_complex *_x,
-                                 unsigned long long _nblocks, liquid_float_complex *_y);
-void firpfbch_crcf_execute_block_dev(firpfbch_crcf _q, const liquid_float_complex *_dx,
-                                     unsigned long long _nblocks, liquid_float_complex *_dy);
-void firpfbch_crcf_set_stream(firpfbch_crcf _q, void *_hip_stream);
+#define LQMI_FIRPFBCH_API(FIRPFBCH, TC)                                                             \
+    typedef struct FIRPFBCH##_s *FIRPFBCH;                                                          \
+    FIRPFBCH FIRPFBCH##_create(int _type, unsigned int _M, unsigned int _p, TC *_h);                \
+    FIRPFBCH FIRPFBCH##_create_kaiser(int _type, unsigned int _M, unsigned int _m, float _As);      \
+    FIRPFBCH FIRPFBCH##_create_rnyquist(int _type, unsigned int _M, unsigned int _m, float _beta,   \
+                                        int _ftype);                                                \
+    void FIRPFBCH##_destroy(FIRPFBCH _q);                                                           \
+    void FIRPFBCH##_reset(FIRPFBCH _q);                                                             \
+    void FIRPFBCH##_print(FIRPFBCH _q);                                                             \
+    void FIRPFBCH##_synthesizer_execute(FIRPFBCH _q, liquid_float_complex *_x,                      \
+                                        liquid_float_complex *_y);                                  \
+    void FIRPFBCH##_analyzer_execute(FIRPFBCH _q, liquid_float_complex *_x,                         \
+                                     liquid_float_complex *_y);                                     \
+    /* extension: _nblocks consecutive M-sample blocks (analyzer or synthesizer) */                 \
+    void FIRPFBCH##_execute_block(FIRPFBCH _q, liquid_float_complex *_x, unsigned long long _nblocks, \
+                                  liquid_float_complex *_y);                                        \
+    void FIRPFBCH##_execute_block_dev(FIRPFBCH _q, const liquid_float_complex *_dx,                 \
+                                      unsigned long long _nblocks, liquid_float_complex *_dy);      \
+    void FIRPFBCH##_set_stream(FIRPFBCH _q, void *_hip_stream);
+
+LQMI_FIRPFBCH_API(firpfbch_crcf, float)
+LQMI_FIRPFBCH_API(firpfbch_cccf, liquid_float_complex)
 
 /* ------------------------------------------------------------------------ */
 /* firpfbch2 (liquid.h:5754-5799): crcf                                      */

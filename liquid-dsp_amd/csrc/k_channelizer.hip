@@ -198,7 +198,18 @@ __global__ void k_pfb2_syn_out(int M, int m, const float *__restrict__ hsub, con
 }
 
 // ------------------------------------------------------------------ firpfbch analyzer (X build)
-__global__ void k_pfb_an_X(int M, int p, const float *__restrict__ hsub, const float2 *__restrict__ hist,
+// tap x sample: real taps (crcf) or complex taps (cccf, no conjugation, as dotprod_cccf)
+__device__ __forceinline__ float2 pfb_mac(float h, float2 v, float2 a)
+{
+    return make_float2(fmaf(h, v.x, a.x), fmaf(h, v.y, a.y));
+}
+__device__ __forceinline__ float2 pfb_mac(float2 h, float2 v, float2 a)
+{
+    return make_float2(fmaf(h.x, v.x, fmaf(-h.y, v.y, a.x)), fmaf(h.x, v.y, fmaf(h.y, v.x, a.y)));
+}
+
+template <typename TC>
+__global__ void k_pfb_an_X(int M, int p, const TC *__restrict__ hsub, const float2 *__restrict__ hist,
                            const float2 *__restrict__ x, long long nblocks, float2 *__restrict__ X)
 {
     const long long e = (long long)blockIdx.x * blockDim.x + threadIdx.x;
@@ -210,15 +221,14 @@ __global__ void k_pfb_an_X(int M, int p, const float *__restrict__ hsub, const f
     float2 acc = make_float2(0.f, 0.f);
     for (int n = 0; n < p; n++) {
         const float2 v = ext_load(hist, HL, x, (b - n) * M + j);
-        const float h = hsub[i * p + n];
-        acc.x = fmaf(h, v.x, acc.x);
-        acc.y = fmaf(h, v.y, acc.y);
+        acc = pfb_mac(hsub[i * p + n], v, acc);
     }
     X[e] = acc;
 }
 
 // firpfbch synthesizer output: Z = [p-1 history z | nblocks new z]
-__global__ void k_pfb_syn_out(int M, int p, const float *__restrict__ hsub, const float2 *__restrict__ Z,
+template <typename TC>
+__global__ void k_pfb_syn_out(int M, int p, const TC *__restrict__ hsub, const float2 *__restrict__ Z,
                               long long nblocks, float2 *__restrict__ y)
 {
     const long long e = (long long)blockIdx.x * blockDim.x + threadIdx.x;
@@ -228,10 +238,7 @@ __global__ void k_pfb_syn_out(int M, int p, const float *__restrict__ hsub, cons
     const long long zb = (p - 1) + b;
     float2 acc = make_float2(0.f, 0.f);
     for (int n = 0; n < p; n++) {
-        const float h = hsub[i * p + n];
-        const float2 z = Z[(zb - n) * M + i];
-        acc.x = fmaf(h, z.x, acc.x);
-        acc.y = fmaf(h, z.y, acc.y);
+        acc = pfb_mac(hsub[i * p + n], Z[(zb - n) * M + i], acc);
     }
     y[e] = acc;
 }
@@ -356,22 +363,26 @@ extern "C" void lqk_firpfbch2_synthesizer(unsigned int M, unsigned int m, const 
                             st));
 }
 
-extern "C" void lqk_firpfbch_analyzer(unsigned int M, unsigned int p, const void *hsub, const void *hist,
+extern "C" void lqk_firpfbch_analyzer(int ctaps, unsigned int M, unsigned int p, const void *hsub, const void *hist,
                                       const void *x, unsigned long long nblocks, void *Y, void *stream)
 {
     if (nblocks == 0) return;
     hipStream_t st = (hipStream_t)stream;
     const long long tot = (long long)nblocks * M;
+    const dim3 grid((unsigned)((tot + 255) / 256));
     // X is formed in Y then transformed in place
-    hipLaunchKernelGGL(k_pfb_an_X, dim3((unsigned)((tot + 255) / 256)), dim3(256), 0, st, (int)M, (int)p,
-                       (const float *)hsub, (const float2 *)hist, (const float2 *)x, (long long)nblocks,
-                       (float2 *)Y);
+    if (ctaps)
+        hipLaunchKernelGGL(k_pfb_an_X<float2>, grid, dim3(256), 0, st, (int)M, (int)p, (const float2 *)hsub,
+                           (const float2 *)hist, (const float2 *)x, (long long)nblocks, (float2 *)Y);
+    else
+        hipLaunchKernelGGL(k_pfb_an_X<float>, grid, dim3(256), 0, st, (int)M, (int)p, (const float *)hsub,
+                           (const float2 *)hist, (const float2 *)x, (long long)nblocks, (float2 *)Y);
     LQ_CHECK_LAUNCH();
     fft_batch_scaled(M, +1, Y, Y, (long long)nblocks, 1.f, 1.f, 0, 0, st);
 }
 
 // state: the previous p-1 z vectors; zscratch: (p-1 + nblocks)*M
-extern "C" void lqk_firpfbch_synthesizer(unsigned int M, unsigned int p, const void *hsub, void *state,
+extern "C" void lqk_firpfbch_synthesizer(int ctaps, unsigned int M, unsigned int p, const void *hsub, void *state,
                                          void *zscratch, const void *X, unsigned long long nblocks, void *y,
                                          void *stream)
 {
@@ -382,8 +393,13 @@ extern "C" void lqk_firpfbch_synthesizer(unsigned int M, unsigned int p, const v
     if (HB > 0) LQ_CHECK(hipMemcpyAsync(Z, state, HB * M * sizeof(float2), hipMemcpyDeviceToDevice, st));
     fft_batch_scaled(M, -1, X, Z + HB * M, (long long)nblocks, 1.f, 1.f, 0, 0, st);
     const long long tot = (long long)nblocks * M;
-    hipLaunchKernelGGL(k_pfb_syn_out, dim3((unsigned)((tot + 255) / 256)), dim3(256), 0, st, (int)M, (int)p,
-                       (const float *)hsub, (const float2 *)Z, (long long)nblocks, (float2 *)y);
+    const dim3 grid((unsigned)((tot + 255) / 256));
+    if (ctaps)
+        hipLaunchKernelGGL(k_pfb_syn_out<float2>, grid, dim3(256), 0, st, (int)M, (int)p, (const float2 *)hsub,
+                           (const float2 *)Z, (long long)nblocks, (float2 *)y);
+    else
+        hipLaunchKernelGGL(k_pfb_syn_out<float>, grid, dim3(256), 0, st, (int)M, (int)p, (const float *)hsub,
+                           (const float2 *)Z, (long long)nblocks, (float2 *)y);
     LQ_CHECK_LAUNCH();
     if (HB > 0)
         LQ_CHECK(hipMemcpyAsync(state, Z + (long long)nblocks * M, HB * M * sizeof(float2),

@@ -34,6 +34,19 @@ struct rs_state {
     int b, st; // st: 1 INTERP, 0 BOUNDARY
 };
 
+// sample-type helpers: real (rrrf) or complex (crcf, cccf) samples, real taps
+// (resamp.c:117-132 designs real taps for every type)
+__device__ __forceinline__ float2 rs_axpy(float a, float2 x, float2 y)
+{
+    return make_float2(fmaf(a, x.x, y.x), fmaf(a, x.y, y.y));
+}
+__device__ __forceinline__ float rs_axpy(float a, float x, float y) { return fmaf(a, x, y); }
+__device__ __forceinline__ float2 rs_mix(float c0, float2 a, float mu, float2 b)
+{
+    return make_float2(c0 * a.x + mu * b.x, c0 * a.y + mu * b.y);
+}
+__device__ __forceinline__ float rs_mix(float c0, float a, float mu, float b) { return c0 * a + mu * b; }
+
 // the reference's update_timing_state (resamp.c:352-363), IEEE float32, no FMA
 __device__ __forceinline__ void rs_advance(rs_state &s, float del, float fnpfb)
 {
@@ -55,7 +68,7 @@ __device__ __forceinline__ void rs_lookup(const lqk_rs_plan &pl, unsigned long l
         j = pl.pre + (t - c * pl.P);
         add = c * pl.Q;
     }
-    const lqk_rs_entry e = pl.tab[j];
+    const lqk_rs_entry e = pl.tab[(j & 3) * pl.qs + (j >> 2)];
     s.tau = e.tau;
     s.mu = e.mu;
     s.b = e.bst >> 1;
@@ -64,11 +77,11 @@ __device__ __forceinline__ void rs_lookup(const lqk_rs_plan &pl, unsigned long l
 }
 
 // taps[b*L + n] = (h[b + n*npfb], h[(b+1)%npfb + n*npfb]) -- the (y0, y1) pair
-template <int L>
+template <int L, typename S>
 __global__ __launch_bounds__(NT) void k_resamp(lqk_rs_plan pl, unsigned long long g0, unsigned long long K0,
                                                int npfb, float del, const float2 *__restrict__ taps,
-                                               const float2 *__restrict__ hist, const float2 *__restrict__ x,
-                                               long long n, float2 *__restrict__ y)
+                                               const S *__restrict__ hist, const S *__restrict__ x,
+                                               long long n, S *__restrict__ y)
 {
     extern __shared__ float2 stp[];
     for (int t = threadIdx.x; t < npfb * L; t += NT) stp[t] = taps[t];
@@ -79,14 +92,14 @@ __global__ __launch_bounds__(NT) void k_resamp(lqk_rs_plan pl, unsigned long lon
     rs_state s;
     unsigned long long K;
     rs_lookup(pl, g0 + (unsigned long long)i0, s, K);
-    float2 *yo = y + (K - K0);
+    S *yo = y + (K - K0);
 
     // w[k] = x[i0 - L + k]; samples before the call come from the history
-    float2 w[L + RS_R];
+    S w[L + RS_R];
 #pragma unroll
     for (int k = 0; k < L + RS_R; ++k) {
         const long long idx = i0 - L + k;
-        float2 v = make_float2(0.f, 0.f);
+        S v{};
         if (idx < 0) v = hist[L + idx];
         else if (idx < n) v = x[idx];
         w[k] = v;
@@ -103,19 +116,16 @@ __global__ __launch_bounds__(NT) void k_resamp(lqk_rs_plan pl, unsigned long lon
             }
             const bool bnd = !s.st;
             const float2 *tp = stp + (bnd ? npfb - 1 : s.b) * L;
-            float2 a0 = make_float2(0.f, 0.f), a1 = make_float2(0.f, 0.f);
+            S a0{}, a1{};
 #pragma unroll
             for (int k = 0; k < L; ++k) {
                 const float2 t = tp[k];
-                const float2 xb = w[L + r - k];
-                const float2 xa = bnd ? w[L + r - 1 - k] : xb;
-                a0.x += t.x * xa.x;
-                a0.y += t.x * xa.y;
-                a1.x += t.y * xb.x;
-                a1.y += t.y * xb.y;
+                const S xb = w[L + r - k];
+                const S xa = bnd ? w[L + r - 1 - k] : xb;
+                a0 = rs_axpy(t.x, xa, a0);
+                a1 = rs_axpy(t.y, xb, a1);
             }
-            const float c0 = 1.0f - s.mu;
-            *yo++ = make_float2(c0 * a0.x + s.mu * a1.x, c0 * a0.y + s.mu * a1.y);
+            *yo++ = rs_mix(1.0f - s.mu, a0, s.mu, a1);
             rs_advance(s, del, fnpfb);
             s.st = 1;
         }
@@ -154,7 +164,7 @@ __device__ __forceinline__ void rs_lookup_near(const lqk_rs_plan &pl, unsigned l
         j = pl.pre + (t - w * pl.P);
         c = w;
     }
-    const lqk_rs_entry e = pl.tab[j];
+    const lqk_rs_entry e = pl.tab[(j & 3) * pl.qs + (j >> 2)];
     s.tau = e.tau;
     s.mu = e.mu;
     s.b = e.bst >> 1;
@@ -162,11 +172,11 @@ __device__ __forceinline__ void rs_lookup_near(const lqk_rs_plan &pl, unsigned l
     K = (unsigned long long)e.K + c * pl.Q;
 }
 
-template <int L>
+template <int L, typename S>
 __global__ __launch_bounds__(NT) void k_resamp2(lqk_rs_plan pl, unsigned long long g0, unsigned long long K0,
                                                 int npfb, float del, const float2 *__restrict__ taps2,
-                                                const float2 *__restrict__ hist, const float2 *__restrict__ x,
-                                                long long n, float2 *__restrict__ y)
+                                                const S *__restrict__ hist, const S *__restrict__ x,
+                                                long long n, S *__restrict__ y)
 {
     constexpr int RIN = 4;
     constexpr int TIN = NT * RIN;
@@ -178,8 +188,8 @@ __global__ __launch_bounds__(NT) void k_resamp2(lqk_rs_plan pl, unsigned long lo
     constexpr int CAP = 1536;                    // outputs per round
     typedef float v4f __attribute__((ext_vector_type(4)));
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-    float2 *cp0 = reinterpret_cast<float2 *>(smem);
-    float2 *cp1 = cp0 + CS;
+    S *cp0 = reinterpret_cast<S *>(smem);
+    S *cp1 = cp0 + CS;
     uint2 *desc = reinterpret_cast<uint2 *>(cp1 + CS);
     float2 *tpl = reinterpret_cast<float2 *>(desc + CAP);
 
@@ -191,7 +201,7 @@ __global__ __launch_bounds__(NT) void k_resamp2(lqk_rs_plan pl, unsigned long lo
 
     // everything a tile needs from HBM, fetched one tile ahead into registers
     struct Pre {
-        float2 xv[NXV];
+        S xv[NXV];
         rs_state s;
         unsigned long long K, Kb, Ke;
     };
@@ -201,7 +211,7 @@ __global__ __launch_bounds__(NT) void k_resamp2(lqk_rs_plan pl, unsigned long lo
         for (int u = 0; u < NXV; u++) {
             const int t = tid + u * NT;
             const long long sx = i0 - L - 1 + t;
-            float2 v = make_float2(0.f, 0.f);
+            S v{};
             if (t < TS) {
                 if (sx >= 0 && sx < n) v = x[sx];
                 else if (sx < 0 && sx >= -L) v = hist[L + sx];
@@ -271,26 +281,30 @@ __global__ __launch_bounds__(NT) void k_resamp2(lqk_rs_plan pl, unsigned long lo
             }
             __syncthreads();
             const int nr = (int)((ntile - r0) < CAP ? (ntile - r0) : CAP);
-            float2 *yo = y + (Kb - K0) + r0;
+            S *yo = y + (Kb - K0) + r0;
             for (int o = tid; o < nr; o += NT) {
                 const uint2 d = desc[o];
                 const float mu = __uint_as_float(d.x);
                 const int iloc = (int)(d.y & 4095u);
                 const int bb = (int)(d.y >> 12);
                 const int sw = iloc + 1;                  // tile index of x[i-L]
-                const float2 *wp = (sw & 1) ? cp1 + sw + 1 : cp0 + sw;
+                const S *wp = (sw & 1) ? cp1 + sw + 1 : cp0 + sw;
                 const float2 *tp = tpl + bb * LPS;
-                float2 acc = make_float2(0.f, 0.f);
+                S acc{};
 #pragma unroll
                 for (int q = 0; q < NW; q++) {
-                    const v4f w = *reinterpret_cast<const v4f *>(wp + 2 * q);
                     const v4f t = *reinterpret_cast<const v4f *>(tp + 2 * q);
                     const float c0 = t.x + mu * (t.y - t.x);
                     const float c1 = t.z + mu * (t.w - t.z);
-                    acc.x = fmaf(c0, w.x, acc.x);
-                    acc.y = fmaf(c0, w.y, acc.y);
-                    acc.x = fmaf(c1, w.z, acc.x);
-                    acc.y = fmaf(c1, w.w, acc.y);
+                    if constexpr (sizeof(S) == 8) {    // two complex samples: one 16-byte read
+                        const v4f w = *reinterpret_cast<const v4f *>(wp + 2 * q);
+                        acc = rs_axpy(c0, make_float2(w.x, w.y), acc);
+                        acc = rs_axpy(c1, make_float2(w.z, w.w), acc);
+                    } else {                           // two real samples: one 8-byte read
+                        const float2 w = *reinterpret_cast<const float2 *>(wp + 2 * q);
+                        acc = rs_axpy(c0, w.x, acc);
+                        acc = rs_axpy(c1, w.y, acc);
+                    }
                 }
                 yo[o] = acc;
             }
@@ -299,79 +313,76 @@ __global__ __launch_bounds__(NT) void k_resamp2(lqk_rs_plan pl, unsigned long lo
 }
 
 // any L (window and taps read through the caches), one input per lane
+template <typename S>
 __global__ __launch_bounds__(NT) void k_resamp_generic(lqk_rs_plan pl, unsigned long long g0,
                                                        unsigned long long K0, int npfb, int L, float del,
                                                        const float2 *__restrict__ taps,
-                                                       const float2 *__restrict__ hist,
-                                                       const float2 *__restrict__ x, long long n,
-                                                       float2 *__restrict__ y)
+                                                       const S *__restrict__ hist,
+                                                       const S *__restrict__ x, long long n,
+                                                       S *__restrict__ y)
 {
     const long long i = (long long)blockIdx.x * NT + threadIdx.x;
     if (i >= n) return;
     rs_state s;
     unsigned long long K;
     rs_lookup(pl, g0 + (unsigned long long)i, s, K);
-    float2 *yo = y + (K - K0);
-    auto X = [&](long long idx) -> float2 { return idx < 0 ? hist[L + idx] : x[idx]; };
+    S *yo = y + (K - K0);
+    auto X = [&](long long idx) -> S { return idx < 0 ? hist[L + idx] : x[idx]; };
     const float fnpfb = (float)npfb;
     while (s.b < npfb) {
         if (s.st && s.b == npfb - 1) break;
         const bool bnd = !s.st;
         const float2 *tp = taps + (size_t)(bnd ? npfb - 1 : s.b) * L;
-        float2 a0 = make_float2(0.f, 0.f), a1 = make_float2(0.f, 0.f);
+        S a0{}, a1{};
         for (int k = 0; k < L; ++k) {
             const float2 t = tp[k];
-            const float2 xb = X(i - k);
-            const float2 xa = bnd ? X(i - 1 - k) : xb;
-            a0.x += t.x * xa.x;
-            a0.y += t.x * xa.y;
-            a1.x += t.y * xb.x;
-            a1.y += t.y * xb.y;
+            const S xb = X(i - k);
+            const S xa = bnd ? X(i - 1 - k) : xb;
+            a0 = rs_axpy(t.x, xa, a0);
+            a1 = rs_axpy(t.y, xb, a1);
         }
-        const float c0 = 1.0f - s.mu;
-        *yo++ = make_float2(c0 * a0.x + s.mu * a1.x, c0 * a0.y + s.mu * a1.y);
+        *yo++ = rs_mix(1.0f - s.mu, a0, s.mu, a1);
         rs_advance(s, del, fnpfb);
         s.st = 1;
     }
 }
 
-template <int L>
+template <int L, typename S>
 void launch_rs(const lqk_rs_plan &pl, unsigned long long g0, unsigned long long K0, int npfb, float del,
-               const float2 *taps, const float2 *taps2, const float2 *hist, const float2 *x, long long n, float2 *y,
+               const float2 *taps, const float2 *taps2, const S *hist, const S *x, long long n, S *y,
                hipStream_t st)
 {
     constexpr int LP = (L + 2 + 1) & ~1;
     constexpr int TIN = NT * 4;
     const size_t lds2 =
-        (size_t)2 * (TIN + L + 4) * sizeof(float2) + 1536 * 8 + (size_t)(npfb + 1) * (LP + 2) * sizeof(float2);
+        (size_t)2 * (TIN + L + 4) * sizeof(S) + 1536 * 8 + (size_t)(npfb + 1) * (LP + 2) * sizeof(float2);
     if (taps2 != nullptr && lds2 <= 64 * 1024 && pl.P < (1ull << 31) && pl.pre < (1ull << 62)) {
         const long long ntiles = (n + TIN - 1) / TIN;
         const unsigned nb = (unsigned)(ntiles < 1024 ? ntiles : 1024);   // persistent: ~4 per CU
-        hipLaunchKernelGGL(k_resamp2<L>, dim3(nb), dim3(NT), lds2, st, pl, g0, K0, npfb, del, taps2, hist, x, n, y);
+        hipLaunchKernelGGL((k_resamp2<L, S>), dim3(nb), dim3(NT), lds2, st, pl, g0, K0, npfb, del, taps2, hist, x,
+                           n, y);
         return;
     }
     const long long lanes = (n + RS_R - 1) / RS_R;
     const unsigned nb = (unsigned)((lanes + NT - 1) / NT);
-    hipLaunchKernelGGL(k_resamp<L>, dim3(nb), dim3(NT), (size_t)npfb * L * sizeof(float2), st, pl, g0, K0, npfb,
-                       del, taps, hist, x, n, y);
+    hipLaunchKernelGGL((k_resamp<L, S>), dim3(nb), dim3(NT), (size_t)npfb * L * sizeof(float2), st, pl, g0, K0,
+                       npfb, del, taps, hist, x, n, y);
 }
 
-} // namespace
-
-extern "C" void lqk_resamp(const lqk_rs_plan *pl, unsigned long long g0, unsigned long long K0,
-                           unsigned int npfb, unsigned int L, float del, const void *taps, const void *taps2,
-                           const void *hist, const void *x, unsigned long long n, void *y, void *stream)
+template <typename S>
+void run_rs(const lqk_rs_plan *pl, unsigned long long g0, unsigned long long K0, unsigned int npfb, unsigned int L,
+            float del, const void *taps, const void *taps2, const void *hist, const void *x, unsigned long long n,
+            void *y, hipStream_t st)
 {
-    if (n == 0) return;
-    hipStream_t st = (hipStream_t)stream;
-    const float2 *tp = (const float2 *)taps, *hs = (const float2 *)hist, *xi = (const float2 *)x;
-    float2 *yo = (float2 *)y;
+    const float2 *tp = (const float2 *)taps;
+    const S *hs = (const S *)hist, *xi = (const S *)x;
+    S *yo = (S *)y;
     const long long nn = (long long)n;
     const bool lds_ok = (size_t)npfb * L * sizeof(float2) <= 64 * 1024;
 #define LQ_RS_CASE(LL)                                                                                     \
     case LL:                                                                                               \
-        launch_rs<LL>(*pl, g0, K0, (int)npfb, del, tp, (const float2 *)taps2, hs, xi, nn, yo, st);                               \
-        break;
+        launch_rs<LL, S>(*pl, g0, K0, (int)npfb, del, tp, (const float2 *)taps2, hs, xi, nn, yo, st);     \
+        return;
     if (lds_ok && L <= 32 && (L % 2) == 0) {
         switch (L) {
             LQ_RS_CASE(2)
@@ -391,12 +402,22 @@ extern "C" void lqk_resamp(const lqk_rs_plan *pl, unsigned long long g0, unsigne
             LQ_RS_CASE(30)
             LQ_RS_CASE(32)
         }
-    } else {
-        const unsigned nb = (unsigned)((n + NT - 1) / NT);
-        hipLaunchKernelGGL(k_resamp_generic, dim3(nb), dim3(NT), 0, st, *pl, g0, K0, (int)npfb, (int)L, del, tp, hs,
-                           xi, nn, yo);
     }
 #undef LQ_RS_CASE
-    LQ_CHECK_LAUNCH();
+    const unsigned nb = (unsigned)((n + NT - 1) / NT);
+    hipLaunchKernelGGL((k_resamp_generic<S>), dim3(nb), dim3(NT), 0, st, *pl, g0, K0, (int)npfb, (int)L, del, tp,
+                       hs, xi, nn, yo);
 }
 
+} // namespace
+
+extern "C" void lqk_resamp(int real_io, const lqk_rs_plan *pl, unsigned long long g0, unsigned long long K0,
+                           unsigned int npfb, unsigned int L, float del, const void *taps, const void *taps2,
+                           const void *hist, const void *x, unsigned long long n, void *y, void *stream)
+{
+    if (n == 0) return;
+    hipStream_t st = (hipStream_t)stream;
+    if (real_io) run_rs<float>(pl, g0, K0, npfb, L, del, taps, taps2, hist, x, n, y, st);
+    else run_rs<float2>(pl, g0, K0, npfb, L, del, taps, taps2, hist, x, n, y, st);
+    LQ_CHECK_LAUNCH();
+}

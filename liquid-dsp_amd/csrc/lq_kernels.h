@@ -96,10 +96,11 @@ void lqk_firpfbch2_synthesizer(unsigned int M, unsigned int m, const void *hsub_
 
 /* ---------------------------------------------------------------- firpfbch (critically sampled)
  * analyzer: block b consumes x[bM .. bM+M); window i receives x[bM + M-1-i]
- * X[M-1-i] = sum_n h[i + n*M] win_i, Y = FFT_forward(X).  hsub[i*p + n] = h[i+n*M] */
-void lqk_firpfbch_analyzer(unsigned int M, unsigned int p, const void *hsub, const void *hist,
+ * X[M-1-i] = sum_n h[i + n*M] win_i, Y = FFT_forward(X).  hsub[i*p + n] = h[i+n*M];
+ * ctaps: hsub holds complex taps (cccf), else real (crcf) */
+void lqk_firpfbch_analyzer(int ctaps, unsigned int M, unsigned int p, const void *hsub, const void *hist,
                            const void *x, unsigned long long nblocks, void *Y, void *stream);
-void lqk_firpfbch_synthesizer(unsigned int M, unsigned int p, const void *hsub, void *state,
+void lqk_firpfbch_synthesizer(int ctaps, unsigned int M, unsigned int p, const void *hsub, void *state,
                               void *zscratch, const void *X, unsigned long long nblocks, void *y,
                               void *stream);
 
@@ -126,12 +127,14 @@ typedef struct {
     unsigned int K;
 } lqk_rs_entry;
 typedef struct {
-    const lqk_rs_entry *tab;   /* device */
+    const lqk_rs_entry *tab;   /* device, entry j at tab[(j & 3) * qs + (j >> 2)] */
     unsigned long long pre, P, Q;
+    unsigned long long qs;     /* quarter-table stride */
 } lqk_rs_plan;
 /* n inputs x (plan positions g0 .. g0+n) -> outputs y[K(g) - K0 ...];
- * taps: npfb x L pairs (h[b + n*npfb], h[(b+1)%npfb + n*npfb]); hist = last L inputs */
-void lqk_resamp(const lqk_rs_plan *pl, unsigned long long g0, unsigned long long K0, unsigned int npfb,
+ * taps: npfb x L pairs (h[b + n*npfb], h[(b+1)%npfb + n*npfb]); hist = last L inputs.
+ * real_io: float samples (rrrf), else interleaved complex (crcf, cccf: the taps are real for every type) */
+void lqk_resamp(int real_io, const lqk_rs_plan *pl, unsigned long long g0, unsigned long long K0, unsigned int npfb,
                 unsigned int L, float del, const void *taps, const void *taps2, const void *hist, const void *x,
                 unsigned long long n, void *y, void *stream);
 /* taps2: (npfb+1) x LP pairs, LP = (L+3) & ~1: row b < npfb (h_b[L-p], h_{b+1}[L-p]) for p = 1..L, row

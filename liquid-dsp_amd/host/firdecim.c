@@ -149,6 +149,25 @@ static void lq_decim_block(lq_decim *q, const void *x, unsigned long long nout, 
         free(hc);                                                                                   \
         return q;                                                                                   \
     }                                                                                               \
+    /* firdecim.c:126-160: 2Mm+1 taps from liquid_firdes_prototype */                               \
+    NAME NAME##_create_prototype(int _type, unsigned int _M, unsigned int _m, float _beta, float _dt) \
+    {                                                                                               \
+        if (_M < 2) LQ_FAIL("error: " #NAME "_create_prototype(), decimation factor must be greater than 1\n"); \
+        if (_m == 0) LQ_FAIL("error: " #NAME "_create_prototype(), filter delay must be greater than 0\n"); \
+        if (_beta < 0.0f || _beta > 1.0f)                                                           \
+            LQ_FAIL("error: " #NAME "_create_prototype(), filter excess bandwidth factor must be in [0,1]\n"); \
+        if (_dt < -1.0f || _dt > 1.0f)                                                              \
+            LQ_FAIL("error: " #NAME "_create_prototype(), filter fractional sample delay must be in [-1,1]\n"); \
+        const unsigned int n = 2 * _M * _m + 1;                                                     \
+        float *hf = (float *)lq_xmalloc(n * sizeof(float));                                         \
+        TC *hc = (TC *)lq_xmalloc(n * sizeof(TC));                                                  \
+        liquid_firdes_prototype((liquid_firfilt_type)_type, _M, _m, _beta, _dt, hf);                \
+        for (unsigned int i = 0; i < n; i++) hc[i] = (TC)hf[i];                                     \
+        NAME q = NAME##_create(_M, hc, n);                                                          \
+        free(hf);                                                                                   \
+        free(hc);                                                                                   \
+        return q;                                                                                   \
+    }                                                                                               \
     void NAME##_destroy(NAME _q)                                                                    \
     {                                                                                               \
         lq_decim_destroy(_q->e);                                                                    \
@@ -156,7 +175,7 @@ static void lq_decim_block(lq_decim *q, const void *x, unsigned long long nout, 
     }                                                                                               \
     void NAME##_print(NAME _q) { lq_decim_print(_q->e); }                                           \
     void NAME##_clear(NAME _q) { lq_decim_clear(_q->e); }                                           \
-    void NAME##_execute(NAME _q, TI *_x, TO *_y) { lq_decim_block(_q->e, _x, 1, _y); }               \
+    void NAME##_execute(NAME _q, TI *_x, TO *_y) { lq_decim_block(_q->e, _x, 1, _y); }              \
     void NAME##_execute_block(NAME _q, TI *_x, unsigned int _n, TO *_y)                             \
     {                                                                                               \
         lq_decim_block(_q->e, _x, _n, _y);                                                          \
@@ -298,6 +317,25 @@ static void lq_interp_block(lq_interp *q, const void *x, unsigned long long n, v
         free(hc);                                                                                   \
         return q;                                                                                   \
     }                                                                                               \
+    /* firinterp.c:124-158: 2Mm+1 taps from liquid_firdes_prototype */                              \
+    NAME NAME##_create_prototype(int _type, unsigned int _M, unsigned int _m, float _beta, float _dt) \
+    {                                                                                               \
+        if (_M < 2) LQ_FAIL("error: " #NAME "_create_prototype(), interp factor must be greater than 1\n"); \
+        if (_m == 0) LQ_FAIL("error: " #NAME "_create_prototype(), filter delay must be greater than 0\n"); \
+        if (_beta < 0.0f || _beta > 1.0f)                                                           \
+            LQ_FAIL("error: " #NAME "_create_prototype(), filter excess bandwidth factor must be in [0,1]\n"); \
+        if (_dt < -1.0f || _dt > 1.0f)                                                              \
+            LQ_FAIL("error: " #NAME "_create_prototype(), filter fractional sample delay must be in [-1,1]\n"); \
+        const unsigned int n = 2 * _M * _m + 1;                                                     \
+        float *hf = (float *)lq_xmalloc(n * sizeof(float));                                         \
+        TC *hc = (TC *)lq_xmalloc(n * sizeof(TC));                                                  \
+        liquid_firdes_prototype((liquid_firfilt_type)_type, _M, _m, _beta, _dt, hf);                \
+        for (unsigned int i = 0; i < n; i++) hc[i] = (TC)hf[i];                                     \
+        NAME q = NAME##_create(_M, hc, n);                                                          \
+        free(hf);                                                                                   \
+        free(hc);                                                                                   \
+        return q;                                                                                   \
+    }                                                                                               \
     void NAME##_destroy(NAME _q)                                                                    \
     {                                                                                               \
         lq_interp_destroy(_q->e);                                                                   \
@@ -305,7 +343,7 @@ static void lq_interp_block(lq_interp *q, const void *x, unsigned long long n, v
     }                                                                                               \
     void NAME##_print(NAME _q) { lq_interp_print(_q->e); }                                          \
     void NAME##_reset(NAME _q) { lq_interp_reset(_q->e); }                                          \
-    void NAME##_execute(NAME _q, TI _x, TO *_y) { lq_interp_block(_q->e, &_x, 1, _y); }              \
+    void NAME##_execute(NAME _q, TI _x, TO *_y) { lq_interp_block(_q->e, &_x, 1, _y); }             \
     void NAME##_execute_block(NAME _q, TI *_x, unsigned int _n, TO *_y)                             \
     {                                                                                               \
         lq_interp_block(_q->e, _x, _n, _y);                                                         \

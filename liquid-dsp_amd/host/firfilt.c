@@ -287,6 +287,23 @@ lq_ctx *lq_firfilt_ctx(lq_firfilt *q) { return &q->ctx; }
         free(hc);                                                                                   \
         return q;                                                                                   \
     }                                                                                               \
+    /* firfilt.c:140-171: 2km+1 taps from liquid_firdes_prototype */                                \
+    NAME NAME##_create_rnyquist(int _type, unsigned int _k, unsigned int _m, float _beta, float _mu)\
+    {                                                                                               \
+        if (_k < 2) LQ_FAIL("error: " #NAME "_create_rnyquist(), filter samples/symbol must be greater than 1\n");\
+        if (_m == 0) LQ_FAIL("error: " #NAME "_create_rnyquist(), filter delay must be greater than 0\n");\
+        if (_beta < 0.0f || _beta > 1.0f)                                                           \
+            LQ_FAIL("error: " #NAME "_create_rnyquist(), filter excess bandwidth factor must be in [0,1]\n");\
+        const unsigned int n = 2 * _k * _m + 1;                                                     \
+        float *hf = (float *)lq_xmalloc(n * sizeof(float));                                         \
+        TC *hc = (TC *)lq_xmalloc(n * sizeof(TC));                                                  \
+        liquid_firdes_prototype((liquid_firfilt_type)_type, _k, _m, _beta, _mu, hf);                \
+        for (unsigned int i = 0; i < n; i++) hc[i] = (TC)hf[i];                                     \
+        NAME q = NAME##_create(hc, n);                                                              \
+        free(hf);                                                                                   \
+        free(hc);                                                                                   \
+        return q;                                                                                   \
+    }                                                                                               \
     NAME NAME##_recreate(NAME _q, TC *_h, unsigned int _n)                                          \
     {                                                                                               \
         _q->f = lq_firfilt_recreate(_q->f, (const float *)_h, _n);                                  \

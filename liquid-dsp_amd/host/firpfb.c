@@ -11,6 +11,8 @@
  */
 #include <complex.h>
 
+#include <math.h>
+
 #include "lq_host.h"
 
 static const char *lq_ext[] = {"rrrf", "crcf", "cccf"};
@@ -76,6 +78,32 @@ static float *lq_pfb_kaiser(const char *who, unsigned int M, unsigned int m, flo
     float *hf = (float *)lq_xmalloc(*n * sizeof(float));
     lq_firdes_kaiser(*n, fc / (float)M, As, 0.0f, hf);
     return hf;
+}
+
+/* firpfb.c:146-240: prototype of 2*M*k*m+1 taps at M*k samples/symbol; the
+ * derivative bank is the central difference (circular at the ends) scaled so
+ * that max |h dh| = 0.06 */
+static float *lq_pfb_rnyquist(const char *who, const char *fn, int deriv, int type, unsigned int M, unsigned int k,
+                              unsigned int m, float beta, unsigned int *n)
+{
+    if (M == 0) LQ_FAIL("error: %s%s(), number of filters must be greater than zero\n", who, fn);
+    if (k < 2) LQ_FAIL("error: %s%s(), filter samples/symbol must be greater than 1\n", who, fn);
+    if (m == 0) LQ_FAIL("error: %s%s(), filter delay must be greater than 0\n", who, fn);
+    if (beta < 0.0f || beta > 1.0f) LQ_FAIL("error: %s%s(), filter excess bandwidth factor must be in [0,1]\n", who, fn);
+    const unsigned int N = 2 * M * k * m + 1;
+    *n = N;
+    float *H = (float *)lq_xmalloc(N * sizeof(float));
+    liquid_firdes_prototype((liquid_firfilt_type)type, M * k, m, beta, 0, H);
+    if (!deriv) return H;
+    float *dH = (float *)lq_xmalloc(N * sizeof(float));
+    float mx = 0.0f;
+    for (unsigned int i = 0; i < N; i++) {
+        dH[i] = H[i == N - 1 ? 0 : i + 1] - H[i == 0 ? N - 1 : i - 1];
+        if (fabsf(H[i] * dH[i]) > mx) mx = fabsf(H[i] * dH[i]);
+    }
+    for (unsigned int i = 0; i < N; i++) dH[i] = dH[i] * 0.06f / mx;
+    free(H);
+    return dH;
 }
 
 static void lq_pfb_destroy(lq_pfb *q)
@@ -189,6 +217,29 @@ static void lq_pfb_block(lq_pfb *q, const void *x, unsigned long long n, void *y
     {                                                                                               \
         unsigned int n;                                                                             \
         float *hf = lq_pfb_kaiser(#NAME, _M, _m, _fc, _As, &n);                                     \
+        TC *hc = (TC *)lq_xmalloc(n * sizeof(TC));                                                  \
+        for (unsigned int i = 0; i < n; i++) hc[i] = (TC)hf[i];                                     \
+        NAME q = NAME##_create(_M, hc, n);                                                          \
+        free(hf);                                                                                   \
+        free(hc);                                                                                   \
+        return q;                                                                                   \
+    }                                                                                               \
+    /* firpfb.c:146-180 (d = 0) and :188-240 (d = 1: derivative bank) */                            \
+    NAME NAME##_create_rnyquist(int _type, unsigned int _M, unsigned int _k, unsigned int _m, float _beta)\
+    {                                                                                               \
+        unsigned int n;                                                                             \
+        float *hf = lq_pfb_rnyquist(#NAME, "_create_rnyquist", 0, _type, _M, _k, _m, _beta, &n);    \
+        TC *hc = (TC *)lq_xmalloc(n * sizeof(TC));                                                  \
+        for (unsigned int i = 0; i < n; i++) hc[i] = (TC)hf[i];                                     \
+        NAME q = NAME##_create(_M, hc, n);                                                          \
+        free(hf);                                                                                   \
+        free(hc);                                                                                   \
+        return q;                                                                                   \
+    }                                                                                               \
+    NAME NAME##_create_drnyquist(int _type, unsigned int _M, unsigned int _k, unsigned int _m, float _beta)\
+    {                                                                                               \
+        unsigned int n;                                                                             \
+        float *hf = lq_pfb_rnyquist(#NAME, "_create_drnyquist", 1, _type, _M, _k, _m, _beta, &n);   \
         TC *hc = (TC *)lq_xmalloc(n * sizeof(TC));                                                  \
         for (unsigned int i = 0; i < n; i++) hc[i] = (TC)hf[i];                                     \
         NAME q = NAME##_create(_M, hc, n);                                                          \

@@ -1,20 +1,29 @@
 /*
- * firpfbch.c -- firpfbch_crcf (critically sampled polyphase channelizer).
+ * firpfbch.c -- firpfbch_{crcf,cccf} (critically sampled polyphase channelizer).
  *
  * API include/liquid.h:5667-5739; semantics src/multichannel/src/firpfbch.c:
- *  create        :73-142  type, M > 0 channels, p > 0 taps per branch,
- *                         h has M*p taps; branch i uses h[i + n*M]
- *  create_kaiser :150-184 2*M*m+1 Kaiser taps at fc = 0.5/M, p = 2m
- *  analyzer      :346-409 M inputs -> M channels, forward FFT (analyzer type)
- *  synthesizer   :314-336 M channels -> M outputs, backward FFT
+ *  create          :73-142  type, M > 0 channels, p > 0 taps per branch,
+ *                           h has M*p taps; branch i uses h[i + n*M]
+ *  create_kaiser   :150-184 2*M*m+1 Kaiser taps at fc = 0.5/M, p = 2m
+ *  create_rnyquist :193-256 root-Nyquist prototype (arkaiser, rkaiser, rrc,
+ *                           hM3) of 2*M*m+1 taps; the analyzer keeps the
+ *                           time-reversed first 2*M*m (matched filter)
+ *  analyzer        :346-409 M inputs -> M channels, forward FFT (analyzer type)
+ *  synthesizer     :314-336 M channels -> M outputs, backward FFT
  * The transform direction follows the object's type, as in the reference
- * (the plan is created once per object, firpfbch.c:132-135).
+ * (the plan is created once per object, firpfbch.c:132-135).  crcf has real
+ * taps, cccf complex ones (multiplied without conjugation, dotprod_cccf).
  */
+#include <complex.h>
+
 #include "lq_host.h"
 
-struct firpfbch_crcf_s {
-    int type;
+static const char *lq_ext[] = {"rrrf", "crcf", "cccf"};
+
+typedef struct {
+    int kind, type;
     unsigned int M, p;
+    size_t csz;        /* bytes per coefficient */
     float *h;
     void *d_hsub;      /* M x p: hsub[i*p + n] = h[i + n*M] */
     void *d_hist[2];   /* analyzer: last (p-1)*M inputs */
@@ -22,28 +31,33 @@ struct firpfbch_crcf_s {
     void *d_zstate;    /* synthesizer: last p-1 IFFT vectors */
     lq_ctx ctx;
     lq_devbuf xbuf, ybuf, zbuf;
-};
+} lq_pfbch;
 
-firpfbch_crcf firpfbch_crcf_create(int _type, unsigned int _M, unsigned int _p, float *_h)
+static lq_pfbch *lq_pfbch_create(int kind, int type, unsigned int M, unsigned int p, const float *h)
 {
-    if (_type != LIQUID_ANALYZER && _type != LIQUID_SYNTHESIZER)
-        LQ_FAIL("error: firpfbch_crcf_create(), invalid type %d\n", _type);
-    if (_M == 0) LQ_FAIL("error: firpfbch_crcf_create(), number of channels must be greater than 0\n");
-    if (_p == 0) LQ_FAIL("error: firpfbch_crcf_create(), invalid filter size (must be greater than 0)\n");
-    lqrt_require_device("firpfbch_crcf_create");
-    firpfbch_crcf q = (firpfbch_crcf)lq_xmalloc(sizeof(*q));
-    q->type = _type;
-    q->M = _M;
-    q->p = _p;
-    q->h = (float *)lq_xmalloc((size_t)_M * _p * sizeof(float));
-    memcpy(q->h, _h, (size_t)_M * _p * sizeof(float));
-    float *hsub = (float *)lq_xmalloc((size_t)_M * _p * sizeof(float));
-    for (unsigned int i = 0; i < _M; i++)
-        for (unsigned int n = 0; n < _p; n++) hsub[i * _p + n] = _h[i + n * _M];
+    const char *e = lq_ext[kind];
+    if (type != LIQUID_ANALYZER && type != LIQUID_SYNTHESIZER)
+        LQ_FAIL("error: firpfbch_%s_create(), invalid type %d\n", e, type);
+    if (M == 0) LQ_FAIL("error: firpfbch_%s_create(), number of channels must be greater than 0\n", e);
+    if (p == 0) LQ_FAIL("error: firpfbch_%s_create(), invalid filter size (must be greater than 0)\n", e);
+    lqrt_require_device("firpfbch_create");
+    lq_pfbch *q = (lq_pfbch *)lq_xmalloc(sizeof(*q));
+    q->kind = kind;
+    q->type = type;
+    q->M = M;
+    q->p = p;
+    q->csz = kind == LQ_CCCF ? 8 : 4;
+    const size_t nh = (size_t)M * p, cw = q->csz / 4;
+    q->h = (float *)lq_xmalloc(nh * q->csz);
+    memcpy(q->h, h, nh * q->csz);
+    float *hsub = (float *)lq_xmalloc(nh * q->csz);
+    for (unsigned int i = 0; i < M; i++)
+        for (unsigned int n = 0; n < p; n++)
+            for (size_t c = 0; c < cw; c++) hsub[(i * p + n) * cw + c] = h[(i + (size_t)n * M) * cw + c];
     lq_ctx_init(&q->ctx);
-    q->d_hsub = lqrt_malloc((size_t)_M * _p * sizeof(float));
-    lqrt_h2d(q->d_hsub, hsub, (size_t)_M * _p * sizeof(float), q->ctx.stream);
-    size_t hb = (size_t)(_p - 1) * _M * 8;
+    q->d_hsub = lqrt_malloc(nh * q->csz);
+    lqrt_h2d(q->d_hsub, hsub, nh * q->csz, q->ctx.stream);
+    size_t hb = (size_t)(p - 1) * M * 8;
     q->d_hist[0] = lqrt_malloc(hb);
     q->d_hist[1] = lqrt_malloc(hb);
     q->d_zstate = lqrt_malloc(hb);
@@ -52,87 +66,168 @@ firpfbch_crcf firpfbch_crcf_create(int _type, unsigned int _M, unsigned int _p, 
     return q;
 }
 
-firpfbch_crcf firpfbch_crcf_create_kaiser(int _type, unsigned int _M, unsigned int _m, float _As)
+/* real prototype h (n taps, n >= M*p) -> typed coefficients, first M*p taps */
+static lq_pfbch *lq_pfbch_create_real(int kind, int type, unsigned int M, unsigned int p, const float *h)
 {
-    if (_M == 0) LQ_FAIL("error: firpfbch_crcf_create_kaiser(), number of channels must be greater than 0\n");
-    if (_m == 0) LQ_FAIL("error: firpfbch_crcf_create_kaiser(), invalid filter size (must be greater than 0)\n");
-    _As = _As < 0 ? -_As : _As;
-    unsigned int n = 2 * _M * _m + 1;
+    const size_t nh = (size_t)M * p;
+    if (kind != LQ_CCCF) return lq_pfbch_create(kind, type, M, p, h);
+    float *hc = (float *)lq_xmalloc(nh * 8);
+    for (size_t i = 0; i < nh; i++) {
+        hc[2 * i] = h[i];
+        hc[2 * i + 1] = 0.0f;
+    }
+    lq_pfbch *q = lq_pfbch_create(kind, type, M, p, hc);
+    free(hc);
+    return q;
+}
+
+static lq_pfbch *lq_pfbch_create_kaiser(int kind, int type, unsigned int M, unsigned int m, float As)
+{
+    if (M == 0) LQ_FAIL("error: firpfbch_%s_create_kaiser(), number of channels must be greater than 0\n", lq_ext[kind]);
+    if (m == 0) LQ_FAIL("error: firpfbch_%s_create_kaiser(), invalid filter size (must be greater than 0)\n", lq_ext[kind]);
+    As = As < 0 ? -As : As;
+    unsigned int n = 2 * M * m + 1;
     float *h = (float *)lq_xmalloc(n * sizeof(float));
-    lq_firdes_kaiser(n, 0.5f / (float)_M, _As, 0.0f, h);
-    firpfbch_crcf q = firpfbch_crcf_create(_type, _M, 2 * _m, h);
+    lq_firdes_kaiser(n, 0.5f / (float)M, As, 0.0f, h);
+    lq_pfbch *q = lq_pfbch_create_real(kind, type, M, 2 * m, h);
     free(h);
     return q;
 }
 
-void firpfbch_crcf_destroy(firpfbch_crcf _q)
+static lq_pfbch *lq_pfbch_create_rnyquist(int kind, int type, unsigned int M, unsigned int m, float beta, int ftype)
 {
-    lqrt_sync(_q->ctx.stream);
-    lqrt_free(_q->d_hsub);
-    lqrt_free(_q->d_hist[0]);
-    lqrt_free(_q->d_hist[1]);
-    lqrt_free(_q->d_zstate);
-    lq_devbuf_free(&_q->xbuf);
-    lq_devbuf_free(&_q->ybuf);
-    lq_devbuf_free(&_q->zbuf);
-    lq_ctx_free(&_q->ctx);
-    free(_q->h);
-    free(_q);
+    const char *e = lq_ext[kind];
+    if (type != LIQUID_ANALYZER && type != LIQUID_SYNTHESIZER)
+        LQ_FAIL("error: firpfbch_%s_create_rnyquist(), invalid type %d\n", e, type);
+    if (M == 0) LQ_FAIL("error: firpfbch_%s_create_rnyquist(), number of channels must be greater than 0\n", e);
+    if (m == 0) LQ_FAIL("error: firpfbch_%s_create_rnyquist(), invalid filter size (must be greater than 0)\n", e);
+    const unsigned int n = 2 * M * m + 1, g = 2 * M * m;
+    float *h = (float *)lq_xmalloc(n * sizeof(float));
+    switch (ftype) {
+    case LIQUID_FIRFILT_ARKAISER: liquid_firdes_arkaiser(M, m, beta, 0.0f, h); break;
+    case LIQUID_FIRFILT_RKAISER: liquid_firdes_rkaiser(M, m, beta, 0.0f, h); break;
+    case LIQUID_FIRFILT_RRC: liquid_firdes_rrcos(M, m, beta, 0.0f, h); break;
+    case LIQUID_FIRFILT_hM3: liquid_firdes_hM3(M, m, beta, 0.0f, h); break;
+    default: LQ_FAIL("error: firpfbch_%s_create_rnyquist(), unknown/invalid prototype (%d)\n", e, ftype);
+    }
+    float *gc = (float *)lq_xmalloc(g * sizeof(float));
+    for (unsigned int i = 0; i < g; i++) gc[i] = type == LIQUID_SYNTHESIZER ? h[i] : h[g - i - 1];
+    lq_pfbch *q = lq_pfbch_create_real(kind, type, M, 2 * m, gc);
+    free(h);
+    free(gc);
+    return q;
 }
 
-void firpfbch_crcf_reset(firpfbch_crcf _q)
+static void lq_pfbch_destroy(lq_pfbch *q)
 {
-    size_t hb = (size_t)(_q->p - 1) * _q->M * 8;
-    lqrt_memset(_q->d_hist[0], hb, _q->ctx.stream);
-    lqrt_memset(_q->d_hist[1], hb, _q->ctx.stream);
-    lqrt_memset(_q->d_zstate, hb, _q->ctx.stream);
-    lqrt_sync(_q->ctx.stream);
+    lqrt_sync(q->ctx.stream);
+    lqrt_free(q->d_hsub);
+    lqrt_free(q->d_hist[0]);
+    lqrt_free(q->d_hist[1]);
+    lqrt_free(q->d_zstate);
+    lq_devbuf_free(&q->xbuf);
+    lq_devbuf_free(&q->ybuf);
+    lq_devbuf_free(&q->zbuf);
+    lq_ctx_free(&q->ctx);
+    free(q->h);
+    free(q);
 }
 
-void firpfbch_crcf_print(firpfbch_crcf _q)
+static void lq_pfbch_reset(lq_pfbch *q)
 {
-    printf("firpfbch (%s) [%u channels]:\n", _q->type == LIQUID_ANALYZER ? "analyzer" : "synthesizer", _q->M);
-    for (unsigned int i = 0; i < _q->M * _q->p; i++)
-        printf("  h[%3u] = %12.8f + %12.8f*j\n", i, _q->h[i], 0.0f);
+    size_t hb = (size_t)(q->p - 1) * q->M * 8;
+    lqrt_memset(q->d_hist[0], hb, q->ctx.stream);
+    lqrt_memset(q->d_hist[1], hb, q->ctx.stream);
+    lqrt_memset(q->d_zstate, hb, q->ctx.stream);
+    lqrt_sync(q->ctx.stream);
 }
 
-void firpfbch_crcf_execute_block_dev(firpfbch_crcf _q, const liquid_float_complex *_dx,
-                                     unsigned long long _nblocks, liquid_float_complex *_dy)
+static void lq_pfbch_print(lq_pfbch *q)
 {
-    if (_nblocks == 0) return;
-    if (_q->type == LIQUID_ANALYZER) {
-        void *hold = _q->d_hist[_q->cur], *hnew = _q->d_hist[_q->cur ^ 1];
-        const unsigned int HL = (_q->p - 1) * _q->M;
-        if (HL) lqk_window_append(1, hold, HL, _dx, _nblocks * _q->M, hnew, _q->ctx.stream);
-        lqk_firpfbch_analyzer(_q->M, _q->p, _q->d_hsub, hold, _dx, _nblocks, _dy, _q->ctx.stream);
-        if (HL) _q->cur ^= 1;
-    } else {
-        void *z = lq_devbuf_get(&_q->zbuf, (size_t)(_q->p - 1 + _nblocks) * _q->M * 8);
-        lqk_firpfbch_synthesizer(_q->M, _q->p, _q->d_hsub, _q->d_zstate, z, _dx, _nblocks, _dy, _q->ctx.stream);
+    printf("firpfbch (%s) [%u channels]:\n", q->type == LIQUID_ANALYZER ? "analyzer" : "synthesizer", q->M);
+    for (unsigned int i = 0; i < q->M * q->p; i++) {
+        const float re = q->kind == LQ_CCCF ? q->h[2 * i] : q->h[i];
+        const float im = q->kind == LQ_CCCF ? q->h[2 * i + 1] : 0.0f;
+        printf("  h[%3u] = %12.8f + %12.8f*j\n", i, re, im);
     }
 }
 
-void firpfbch_crcf_execute_block(firpfbch_crcf _q, liquid_float_complex *_x, unsigned long long _nblocks,
-                                 liquid_float_complex *_y)
+static void lq_pfbch_block_dev(lq_pfbch *q, const void *dx, unsigned long long nblocks, void *dy)
 {
-    if (_nblocks == 0) return;
-    size_t bytes = (size_t)_nblocks * _q->M * 8;
-    void *dx = lq_devbuf_get(&_q->xbuf, bytes);
-    void *dy = lq_devbuf_get(&_q->ybuf, bytes);
-    lqrt_h2d(dx, _x, bytes, _q->ctx.stream);
-    firpfbch_crcf_execute_block_dev(_q, (const liquid_float_complex *)dx, _nblocks, (liquid_float_complex *)dy);
-    lqrt_d2h(_y, dy, bytes, _q->ctx.stream);
-    lqrt_sync(_q->ctx.stream);
+    if (nblocks == 0) return;
+    const int ctaps = q->kind == LQ_CCCF;
+    if (q->type == LIQUID_ANALYZER) {
+        void *hold = q->d_hist[q->cur], *hnew = q->d_hist[q->cur ^ 1];
+        const unsigned int HL = (q->p - 1) * q->M;
+        if (HL) lqk_window_append(1, hold, HL, dx, nblocks * q->M, hnew, q->ctx.stream);
+        lqk_firpfbch_analyzer(ctaps, q->M, q->p, q->d_hsub, hold, dx, nblocks, dy, q->ctx.stream);
+        if (HL) q->cur ^= 1;
+    } else {
+        void *z = lq_devbuf_get(&q->zbuf, (size_t)(q->p - 1 + nblocks) * q->M * 8);
+        lqk_firpfbch_synthesizer(ctaps, q->M, q->p, q->d_hsub, q->d_zstate, z, dx, nblocks, dy, q->ctx.stream);
+    }
 }
 
-void firpfbch_crcf_analyzer_execute(firpfbch_crcf _q, liquid_float_complex *_x, liquid_float_complex *_y)
+static void lq_pfbch_block(lq_pfbch *q, const void *x, unsigned long long nblocks, void *y)
 {
-    firpfbch_crcf_execute_block(_q, _x, 1, _y);
+    if (nblocks == 0) return;
+    size_t bytes = (size_t)nblocks * q->M * 8;
+    void *dx = lq_devbuf_get(&q->xbuf, bytes);
+    void *dy = lq_devbuf_get(&q->ybuf, bytes);
+    lqrt_h2d(dx, x, bytes, q->ctx.stream);
+    lq_pfbch_block_dev(q, dx, nblocks, dy);
+    lqrt_d2h(y, dy, bytes, q->ctx.stream);
+    lqrt_sync(q->ctx.stream);
 }
 
-void firpfbch_crcf_synthesizer_execute(firpfbch_crcf _q, liquid_float_complex *_x, liquid_float_complex *_y)
-{
-    firpfbch_crcf_execute_block(_q, _x, 1, _y);
-}
+#define LQ_FIRPFBCH_FRONT(NAME, KIND, TC)                                                           \
+    struct NAME##_s {                                                                               \
+        lq_pfbch *e;                                                                                \
+    };                                                                                              \
+    static NAME NAME##_wrap(lq_pfbch *e)                                                            \
+    {                                                                                               \
+        NAME q = (NAME)lq_xmalloc(sizeof(*q));                                                      \
+        q->e = e;                                                                                   \
+        return q;                                                                                   \
+    }                                                                                               \
+    NAME NAME##_create(int _type, unsigned int _M, unsigned int _p, TC *_h)                         \
+    {                                                                                               \
+        return NAME##_wrap(lq_pfbch_create(KIND, _type, _M, _p, (const float *)_h));                \
+    }                                                                                               \
+    NAME NAME##_create_kaiser(int _type, unsigned int _M, unsigned int _m, float _As)               \
+    {                                                                                               \
+        return NAME##_wrap(lq_pfbch_create_kaiser(KIND, _type, _M, _m, _As));                       \
+    }                                                                                               \
+    NAME NAME##_create_rnyquist(int _type, unsigned int _M, unsigned int _m, float _beta, int _ftype) \
+    {                                                                                               \
+        return NAME##_wrap(lq_pfbch_create_rnyquist(KIND, _type, _M, _m, _beta, _ftype));           \
+    }                                                                                               \
+    void NAME##_destroy(NAME _q)                                                                    \
+    {                                                                                               \
+        lq_pfbch_destroy(_q->e);                                                                    \
+        free(_q);                                                                                   \
+    }                                                                                               \
+    void NAME##_reset(NAME _q) { lq_pfbch_reset(_q->e); }                                           \
+    void NAME##_print(NAME _q) { lq_pfbch_print(_q->e); }                                           \
+    void NAME##_execute_block_dev(NAME _q, const liquid_float_complex *_dx, unsigned long long _nblocks, \
+                                  liquid_float_complex *_dy)                                        \
+    {                                                                                               \
+        lq_pfbch_block_dev(_q->e, _dx, _nblocks, _dy);                                              \
+    }                                                                                               \
+    void NAME##_execute_block(NAME _q, liquid_float_complex *_x, unsigned long long _nblocks,       \
+                              liquid_float_complex *_y)                                             \
+    {                                                                                               \
+        lq_pfbch_block(_q->e, _x, _nblocks, _y);                                                    \
+    }                                                                                               \
+    void NAME##_analyzer_execute(NAME _q, liquid_float_complex *_x, liquid_float_complex *_y)       \
+    {                                                                                               \
+        lq_pfbch_block(_q->e, _x, 1, _y);                                                           \
+    }                                                                                               \
+    void NAME##_synthesizer_execute(NAME _q, liquid_float_complex *_x, liquid_float_complex *_y)    \
+    {                                                                                               \
+        lq_pfbch_block(_q->e, _x, 1, _y);                                                           \
+    }                                                                                               \
+    void NAME##_set_stream(NAME _q, void *_s) { lq_ctx_set_stream(&_q->e->ctx, _s); }
 
-void firpfbch_crcf_set_stream(firpfbch_crcf _q, void *_s) { lq_ctx_set_stream(&_q->ctx, _s); }
+LQ_FIRPFBCH_FRONT(firpfbch_crcf, LQ_CRCF, float)
+LQ_FIRPFBCH_FRONT(firpfbch_cccf, LQ_CCCF, liquid_float_complex)

@@ -1,5 +1,5 @@
 /*
- * resamp.c -- resamp_crcf on the MI355X.
+ * resamp.c -- resamp_{rrrf,crcf,cccf} on the MI355X.
  *
  * resamp: include/liquid.h:2938-3015, src/filter/src/resamp.c:79-363.
  *   Prototype 2*m*npfb+1 Kaiser taps at fc/npfb scaled by npfb/sum(h); bank
@@ -15,7 +15,9 @@
  * once per rate with Brent's cycle detection and the plan is reused for every
  * later call.  Short calls (and rates whose period exceeds RS_MAX_PERIOD)
  * get a plan covering just that call.  Every output sample is computed on
- * the GPU (csrc/k_resamp.hip).
+ * the GPU (csrc/k_resamp.hip).  The taps are real for every type
+ * (resamp.c:117-132 designs them with liquid_firdes_kaiser), so cccf runs the
+ * crcf kernel and rrrf its real-sample instantiation.
  */
 #include <math.h>
 
@@ -40,10 +42,12 @@ typedef struct {
     lqk_rs_entry *tab;            /* host copy */
     size_t nent, cap;
     lq_devbuf d_tab;
-    unsigned long long pre, P, Q;
+    unsigned long long pre, P, Q, qs;
 } rs_plan;
 
-struct resamp_crcf_s {
+typedef struct {
+    int kind;
+    size_t esz;                   /* bytes per sample */
     float rate, del, fc, As;
     unsigned int m, npfb, L;
     void *d_taps;                 /* npfb x L float pairs (bank b, bank b+1) */
@@ -56,7 +60,9 @@ struct resamp_crcf_s {
     int cur;
     lq_ctx ctx;
     lq_devbuf xbuf, ybuf;
-};
+} lq_rs;
+
+static const char *lq_ext[] = {"rrrf", "crcf", "cccf"};
 
 static const rs_state rs_initial = {0.0f, 0.0f, 0, RS_INTERP};   /* resamp.c:181-195 */
 
@@ -126,16 +132,24 @@ static const lqk_rs_entry *rs_plan_at(const rs_plan *pl, unsigned long long g, u
     return &pl->tab[j];
 }
 
-static void rs_plan_upload(resamp_crcf q)
+static void rs_plan_upload(lq_rs *q)
 {
-    size_t bytes = q->pl.nent * sizeof(lqk_rs_entry);
+    /* device layout: four quarter tables by j mod 4, so lanes looking up
+     * positions 4 apart read consecutive entries (lqk_rs_plan.qs) */
+    const size_t n = q->pl.nent, qs = (n + 3) / 4;
+    size_t bytes = 4 * qs * sizeof(lqk_rs_entry);
+    lqk_rs_entry *perm = (lqk_rs_entry *)lq_xmalloc(bytes);
+    memset(perm, 0, bytes);
+    for (size_t j = 0; j < n; j++) perm[(j & 3) * qs + (j >> 2)] = q->pl.tab[j];
     void *d = lq_devbuf_get(&q->pl.d_tab, bytes);
-    lqrt_h2d(d, q->pl.tab, bytes, q->ctx.stream);
+    lqrt_h2d(d, perm, bytes, q->ctx.stream);
     lqrt_sync(q->ctx.stream);
+    free(perm);
+    q->pl.qs = qs;
 }
 
 /* Brent's cycle detection on the per-input timing state, from q->now */
-static int rs_plan_build_periodic(resamp_crcf q)
+static int rs_plan_build_periodic(lq_rs *q)
 {
     const rs_state x0 = q->now;
     rs_state tort = x0, hare = x0;
@@ -186,7 +200,7 @@ static int rs_plan_build_periodic(resamp_crcf q)
 }
 
 /* plan covering exactly the next nx inputs (nx <= RS_DIRECT_CHUNK) */
-static void rs_plan_build_direct(resamp_crcf q, unsigned long long nx)
+static void rs_plan_build_direct(lq_rs *q, unsigned long long nx)
 {
     size_t n = (size_t)nx + 1;
     rs_plan_reserve(&q->pl, n);
@@ -196,7 +210,7 @@ static void rs_plan_build_direct(resamp_crcf q, unsigned long long nx)
         rs_put(&q->pl.tab[j], &s, K);
         if (j + 1 < n) K += rs_step(&s, q->del, q->npfb);
     }
-    if (K > 0xffffffffull) LQ_FAIL("error: resamp_crcf: too many outputs for one call\n");
+    if (K > 0xffffffffull) LQ_FAIL("error: resamp_%s: too many outputs for one call\n", lq_ext[q->kind]);
     q->pl.nent = n;
     q->pl.pre = n;
     q->pl.P = 1;
@@ -207,14 +221,14 @@ static void rs_plan_build_direct(resamp_crcf q, unsigned long long nx)
     q->gpos = 0;
 }
 
-static void rs_check_rate(resamp_crcf q)
+static void rs_check_rate(lq_rs *q)
 {
     if (!(q->del > 0.0f) || isinf(q->del) || isnan(q->del))
-        LQ_FAIL("error: resamp_crcf_execute(), invalid resampling rate (%f)\n", q->rate);
+        LQ_FAIL("error: resamp_%s_execute(), invalid resampling rate (%f)\n", lq_ext[q->kind], q->rate);
 }
 
 /* make the plan cover inputs [gpos, gpos + nx); returns how many of them it covers */
-static unsigned long long rs_ensure_plan(resamp_crcf q, unsigned long long nx)
+static unsigned long long rs_ensure_plan(lq_rs *q, unsigned long long nx)
 {
     rs_check_rate(q);
     if (q->pl.valid && q->pl.periodic) return nx;
@@ -238,7 +252,7 @@ static unsigned long long rs_ensure_plan(resamp_crcf q, unsigned long long nx)
     return c;
 }
 
-static unsigned long long rs_K(resamp_crcf q, unsigned long long g)
+static unsigned long long rs_K(lq_rs *q, unsigned long long g)
 {
     unsigned long long K;
     rs_plan_at(&q->pl, g, &K);
@@ -246,7 +260,7 @@ static unsigned long long rs_K(resamp_crcf q, unsigned long long g)
 }
 
 /* the plan's state at gpos becomes the object's state before a rate change */
-static void rs_sync_now(resamp_crcf q)
+static void rs_sync_now(lq_rs *q)
 {
     if (q->pl.valid) {
         unsigned long long K;
@@ -254,16 +268,18 @@ static void rs_sync_now(resamp_crcf q)
     }
 }
 
-resamp_crcf resamp_crcf_create(float _rate, unsigned int _m, float _fc, float _As, unsigned int _npfb)
+static lq_rs *lq_rs_create(int kind, float _rate, unsigned int _m, float _fc, float _As, unsigned int _npfb)
 {
-    if (_rate <= 0) LQ_FAIL("error: resamp_crcf_create(), resampling rate must be greater than zero\n");
-    if (_m == 0) LQ_FAIL("error: resamp_crcf_create(), filter semi-length must be greater than zero\n");
-    if (_npfb == 0) LQ_FAIL("error: resamp_crcf_create(), number of filter banks must be greater than zero\n");
-    if (_fc <= 0.0f || _fc >= 0.5f) LQ_FAIL("error: resamp_crcf_create(), filter cutoff must be in (0,0.5)\n");
+    if (_rate <= 0) LQ_FAIL("error: resamp_%s_create(), resampling rate must be greater than zero\n", lq_ext[kind]);
+    if (_m == 0) LQ_FAIL("error: resamp_%s_create(), filter semi-length must be greater than zero\n", lq_ext[kind]);
+    if (_npfb == 0) LQ_FAIL("error: resamp_%s_create(), number of filter banks must be greater than zero\n", lq_ext[kind]);
+    if (_fc <= 0.0f || _fc >= 0.5f) LQ_FAIL("error: resamp_%s_create(), filter cutoff must be in (0,0.5)\n", lq_ext[kind]);
     if (_As <= 0.0f)
-        LQ_FAIL("error: resamp_crcf_create(), filter stop-band suppression must be greater than zero\n");
-    lqrt_require_device("resamp_crcf_create");
-    resamp_crcf q = (resamp_crcf)lq_xmalloc(sizeof(*q));
+        LQ_FAIL("error: resamp_%s_create(), filter stop-band suppression must be greater than zero\n", lq_ext[kind]);
+    lqrt_require_device("resamp_create");
+    lq_rs *q = (lq_rs *)lq_xmalloc(sizeof(*q));
+    q->kind = kind;
+    q->esz = kind == LQ_RRRF ? 4 : 8;
     q->rate = _rate;
     q->del = 1.0f / _rate;
     q->m = _m;
@@ -304,8 +320,8 @@ resamp_crcf resamp_crcf_create(float _rate, unsigned int _m, float _fc, float _A
     lqrt_h2d(q->d_taps, tp, ntap * 2 * sizeof(float), q->ctx.stream);
     q->d_taps2 = lqrt_malloc(ntap2 * 2 * sizeof(float));
     lqrt_h2d(q->d_taps2, tp2, ntap2 * 2 * sizeof(float), q->ctx.stream);
-    q->d_hist[0] = lqrt_malloc((size_t)q->L * 8);
-    q->d_hist[1] = lqrt_malloc((size_t)q->L * 8);
+    q->d_hist[0] = lqrt_malloc((size_t)q->L * q->esz);
+    q->d_hist[1] = lqrt_malloc((size_t)q->L * q->esz);
     lqrt_sync(q->ctx.stream);
     lqrt_sync(q->ctx.stream);
     free(tp);
@@ -316,13 +332,7 @@ resamp_crcf resamp_crcf_create(float _rate, unsigned int _m, float _fc, float _A
     return q;
 }
 
-resamp_crcf resamp_crcf_create_default(float _rate)
-{
-    if (_rate <= 0) LQ_FAIL("error: resamp_crcf_create_default(), resampling rate must be greater than zero\n");
-    return resamp_crcf_create(_rate, 7, 0.25f, 60.0f, 64);   /* resamp.c:150-169 */
-}
-
-void resamp_crcf_destroy(resamp_crcf _q)
+static void lq_rs_destroy(lq_rs *_q)
 {
     lqrt_sync(_q->ctx.stream);
     lqrt_free(_q->d_taps);
@@ -337,17 +347,17 @@ void resamp_crcf_destroy(resamp_crcf _q)
     free(_q);
 }
 
-void resamp_crcf_print(resamp_crcf _q)
+static void lq_rs_print(lq_rs *_q)
 {
     printf("resampler [rate: %f]\n", _q->rate);
     printf("fir polyphase filterbank [%u] :\n", _q->npfb);
     for (unsigned int i = 0; i < _q->npfb; i++) printf("  bank %3u: \n", i);
 }
 
-void resamp_crcf_reset(resamp_crcf _q)
+static void lq_rs_reset(lq_rs *_q)
 {
-    lqrt_memset(_q->d_hist[0], (size_t)_q->L * 8, _q->ctx.stream);
-    lqrt_memset(_q->d_hist[1], (size_t)_q->L * 8, _q->ctx.stream);
+    lqrt_memset(_q->d_hist[0], (size_t)_q->L * _q->esz, _q->ctx.stream);
+    lqrt_memset(_q->d_hist[1], (size_t)_q->L * _q->esz, _q->ctx.stream);
     lqrt_sync(_q->ctx.stream);
     _q->now = rs_initial;
     _q->gpos = 0;
@@ -355,9 +365,8 @@ void resamp_crcf_reset(resamp_crcf _q)
     if (!(_q->pl.valid && _q->pl.periodic && rs_eq(&_q->pl.origin, &rs_initial))) _q->pl.valid = 0;
 }
 
-unsigned int resamp_crcf_get_delay(resamp_crcf _q) { return _q->m; }
 
-static void rs_new_del(resamp_crcf q, float del)
+static void rs_new_del(lq_rs *q, float del)
 {
     if (memcmp(&del, &q->del, 4) == 0) return;
     lqrt_sync(q->ctx.stream);
@@ -367,25 +376,25 @@ static void rs_new_del(resamp_crcf q, float del)
     q->periodic_failed = 0;
 }
 
-void resamp_crcf_set_rate(resamp_crcf _q, float _rate)
+static void lq_rs_set_rate(lq_rs *_q, float _rate)
 {
-    if (_rate <= 0) LQ_FAIL("error: resamp_crcf_set_rate(), resampling rate must be greater than zero\n");
+    if (_rate <= 0) LQ_FAIL("error: resamp_%s_set_rate(), resampling rate must be greater than zero\n", lq_ext[_q->kind]);
     _q->rate = _rate;
     rs_new_del(_q, 1.0f / _q->rate);
 }
 
 /* resamp.c:222-239, including its clipping of the rate to [-0.5, 0.5] */
-void resamp_crcf_adjust_rate(resamp_crcf _q, float _delta)
+static void lq_rs_adjust_rate(lq_rs *_q, float _delta)
 {
     if (_delta > 0.1f || _delta < -0.1f)
-        LQ_FAIL("error: resamp_crcf_adjust_rate(), resampling rate must be in [-0.1,0.1]\n");
+        LQ_FAIL("error: resamp_%s_adjust_rate(), resampling rate must be in [-0.1,0.1]\n", lq_ext[_q->kind]);
     _q->rate += _delta;
     if (_q->rate > 0.5f) _q->rate = 0.5f;
     if (_q->rate < -0.5f) _q->rate = -0.5f;
     rs_new_del(_q, 1.0f / _q->rate);
 }
 
-unsigned long long resamp_crcf_num_output(resamp_crcf _q, unsigned long long _nx)
+static unsigned long long lq_rs_num_output(lq_rs *_q, unsigned long long _nx)
 {
     if (_nx == 0) return 0;
     unsigned long long done = 0, total = 0;
@@ -403,22 +412,24 @@ unsigned long long resamp_crcf_num_output(resamp_crcf _q, unsigned long long _nx
     return total;
 }
 
-void resamp_crcf_execute_block_dev(resamp_crcf _q, const liquid_float_complex *_dx, unsigned long long _nx,
-                                   liquid_float_complex *_dy, unsigned long long *_ny)
+static void lq_rs_block_dev(lq_rs *_q, const void *_dxv, unsigned long long _nx, void *_dyv,
+                            unsigned long long *_ny)
 {
+    const char *_dx = (const char *)_dxv;
+    char *_dy = (char *)_dyv;
     unsigned long long total = 0;
     while (_nx > 0) {
         unsigned long long c = rs_ensure_plan(_q, _nx);
         unsigned long long K0 = rs_K(_q, _q->gpos), K1 = rs_K(_q, _q->gpos + c);
-        lqk_rs_plan kp = {(const lqk_rs_entry *)_q->pl.d_tab.p, _q->pl.pre, _q->pl.P, _q->pl.Q};
+        lqk_rs_plan kp = {(const lqk_rs_entry *)_q->pl.d_tab.p, _q->pl.pre, _q->pl.P, _q->pl.Q, _q->pl.qs};
         void *hold = _q->d_hist[_q->cur], *hnew = _q->d_hist[_q->cur ^ 1];
-        lqk_resamp(&kp, _q->gpos, K0, _q->npfb, _q->L, _q->del, _q->d_taps, _q->d_taps2, hold, _dx, c, _dy,
+        lqk_resamp(_q->kind == LQ_RRRF, &kp, _q->gpos, K0, _q->npfb, _q->L, _q->del, _q->d_taps, _q->d_taps2, hold, _dx, c, _dy,
                    _q->ctx.stream);
-        lqk_window_append(1, hold, _q->L, _dx, c, hnew, _q->ctx.stream);
+        lqk_window_append(_q->kind != LQ_RRRF, hold, _q->L, _dx, c, hnew, _q->ctx.stream);
         _q->cur ^= 1;
         _q->gpos += c;
-        _dx += c;
-        _dy += K1 - K0;
+        _dx += c * _q->esz;
+        _dy += (K1 - K0) * _q->esz;
         total += K1 - K0;
         _nx -= c;
     }
@@ -426,32 +437,74 @@ void resamp_crcf_execute_block_dev(resamp_crcf _q, const liquid_float_complex *_
     if (_ny) *_ny = total;
 }
 
-void resamp_crcf_execute_block(resamp_crcf _q, liquid_float_complex *_x, unsigned int _nx,
-                               liquid_float_complex *_y, unsigned int *_ny)
+static void lq_rs_block(lq_rs *_q, const void *_x, unsigned int _nx, void *_y, unsigned int *_ny)
 {
     if (_nx == 0) {
         *_ny = 0;
         return;
     }
-    unsigned long long nout = resamp_crcf_num_output(_q, _nx);
-    void *dx = lq_devbuf_get(&_q->xbuf, (size_t)_nx * 8);
-    void *dy = lq_devbuf_get(&_q->ybuf, (size_t)(nout ? nout : 1) * 8);
-    lqrt_h2d(dx, _x, (size_t)_nx * 8, _q->ctx.stream);
+    unsigned long long nout = lq_rs_num_output(_q, _nx);
+    void *dx = lq_devbuf_get(&_q->xbuf, (size_t)_nx * _q->esz);
+    void *dy = lq_devbuf_get(&_q->ybuf, (size_t)(nout ? nout : 1) * _q->esz);
+    lqrt_h2d(dx, _x, (size_t)_nx * _q->esz, _q->ctx.stream);
     unsigned long long ny = 0;
-    resamp_crcf_execute_block_dev(_q, (const liquid_float_complex *)dx, _nx, (liquid_float_complex *)dy, &ny);
-    if (ny) lqrt_d2h(_y, dy, (size_t)ny * 8, _q->ctx.stream);
+    lq_rs_block_dev(_q, dx, _nx, dy, &ny);
+    if (ny) lqrt_d2h(_y, dy, (size_t)ny * _q->esz, _q->ctx.stream);
     lqrt_sync(_q->ctx.stream);
     *_ny = (unsigned int)ny;
 }
 
-void resamp_crcf_execute(resamp_crcf _q, liquid_float_complex _x, liquid_float_complex *_y,
-                         unsigned int *_num_written)
-{
-    resamp_crcf_execute_block(_q, &_x, 1, _y, _num_written);
-}
+#define LQ_RESAMP_FRONT(NAME, KIND, T)                                                                  \
+    struct NAME##_s {                                                                               \
+        lq_rs *e;                                                                                   \
+    };                                                                                              \
+    NAME NAME##_create(float _rate, unsigned int _m, float _fc, float _As, unsigned int _npfb)      \
+    {                                                                                               \
+        lq_rs *e = lq_rs_create(KIND, _rate, _m, _fc, _As, _npfb);                                  \
+        NAME q = (NAME)lq_xmalloc(sizeof(*q));                                                      \
+        q->e = e;                                                                                   \
+        return q;                                                                                   \
+    }                                                                                               \
+    /* resamp.c:150-169: m = 7, fc = 0.25, As = 60, npfb = 64 */                                    \
+    NAME NAME##_create_default(float _rate)                                                         \
+    {                                                                                               \
+        if (_rate <= 0)                                                                             \
+            LQ_FAIL("error: " #NAME "_create_default(), resampling rate must be greater than zero\n"); \
+        return NAME##_create(_rate, 7, 0.25f, 60.0f, 64);                                           \
+    }                                                                                               \
+    void NAME##_destroy(NAME _q)                                                                    \
+    {                                                                                               \
+        lq_rs_destroy(_q->e);                                                                       \
+        free(_q);                                                                                   \
+    }                                                                                               \
+    void NAME##_print(NAME _q) { lq_rs_print(_q->e); }                                              \
+    void NAME##_reset(NAME _q) { lq_rs_reset(_q->e); }                                              \
+    unsigned int NAME##_get_delay(NAME _q) { return _q->e->m; }                                     \
+    void NAME##_set_rate(NAME _q, float _rate) { lq_rs_set_rate(_q->e, _rate); }                     \
+    void NAME##_adjust_rate(NAME _q, float _delta) { lq_rs_adjust_rate(_q->e, _delta); }             \
+    unsigned long long NAME##_num_output(NAME _q, unsigned long long _nx)                           \
+    {                                                                                               \
+        return lq_rs_num_output(_q->e, _nx);                                                        \
+    }                                                                                               \
+    void NAME##_execute_block_dev(NAME _q, const T *_dx, unsigned long long _nx, T *_dy,            \
+                                  unsigned long long *_ny)                                          \
+    {                                                                                               \
+        lq_rs_block_dev(_q->e, _dx, _nx, _dy, _ny);                                                 \
+    }                                                                                               \
+    void NAME##_execute_block(NAME _q, T *_x, unsigned int _nx, T *_y, unsigned int *_ny)           \
+    {                                                                                               \
+        lq_rs_block(_q->e, _x, _nx, _y, _ny);                                                       \
+    }                                                                                               \
+    void NAME##_execute(NAME _q, T _x, T *_y, unsigned int *_num_written)                           \
+    {                                                                                               \
+        lq_rs_block(_q->e, &_x, 1, _y, _num_written);                                               \
+    }                                                                                               \
+    void NAME##_set_stream(NAME _q, void *_s) { lq_ctx_set_stream(&_q->e->ctx, _s); }               \
+    void NAME##_synchronize(NAME _q) { lqrt_sync(_q->e->ctx.stream); }
 
-void resamp_crcf_set_stream(resamp_crcf _q, void *_s) { lq_ctx_set_stream(&_q->ctx, _s); }
-void resamp_crcf_synchronize(resamp_crcf _q) { lqrt_sync(_q->ctx.stream); }
+LQ_RESAMP_FRONT(resamp_rrrf, LQ_RRRF, float)
+LQ_RESAMP_FRONT(resamp_crcf, LQ_CRCF, liquid_float_complex)
+LQ_RESAMP_FRONT(resamp_cccf, LQ_CCCF, liquid_float_complex)
 
 /* ----------------------------------------------------------------- test hook
  * Host-only check of the timing plan (no GPU): builds the plan the object
@@ -464,7 +517,7 @@ long long liquid_mi355x_resamp_schedule(float _rate, unsigned int _npfb, unsigne
                                         int *_b, float *_mu, unsigned int *_idx, unsigned long long _cap,
                                         unsigned long long *_pre, unsigned long long *_period)
 {
-    struct resamp_crcf_s q;
+    lq_rs q;
     memset(&q, 0, sizeof(q));
     q.rate = _rate;
     q.del = 1.0f / _rate;

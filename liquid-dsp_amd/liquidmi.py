@@ -62,6 +62,8 @@ def header_functions():
 
 
 vp, u, f, i, ull = C.c_void_p, C.c_uint, C.c_float, C.c_int, C.c_ulonglong
+FIRDES_DESIGNS = ("rcos", "rrcos", "rkaiser", "arkaiser", "hM3", "gmsktx", "gmskrx", "fexp", "rfexp", "fsech",
+                  "rfsech", "farcsech", "rfarcsech")
 
 
 def _declare(L):
@@ -121,6 +123,20 @@ def _declare(L):
             "firinterp_%s_execute_block" % t: (None, [vp, vp, u, vp]),
             "firinterp_%s_execute_block_dev" % t: (None, [vp, vp, ull, vp]),
             "firinterp_%s_set_stream" % t: (None, [vp, vp]),
+            "resamp_%s_create" % t: (vp, [f, u, f, f, u]),
+            "resamp_%s_create_default" % t: (vp, [f]),
+            "resamp_%s_destroy" % t: (None, [vp]),
+            "resamp_%s_print" % t: (None, [vp]),
+            "resamp_%s_reset" % t: (None, [vp]),
+            "resamp_%s_get_delay" % t: (u, [vp]),
+            "resamp_%s_set_rate" % t: (None, [vp, f]),
+            "resamp_%s_adjust_rate" % t: (None, [vp, f]),
+            "resamp_%s_execute" % t: (None, [vp, ti, vp, vp]),
+            "resamp_%s_execute_block" % t: (None, [vp, vp, u, vp, vp]),
+            "resamp_%s_num_output" % t: (ull, [vp, ull]),
+            "resamp_%s_execute_block_dev" % t: (None, [vp, vp, ull, vp, vp]),
+            "resamp_%s_set_stream" % t: (None, [vp, vp]),
+            "resamp_%s_synchronize" % t: (None, [vp]),
             "fftfilt_%s_create" % t: (vp, [vp, u, u]),
             "fftfilt_%s_destroy" % t: (None, [vp]),
             "fftfilt_%s_reset" % t: (None, [vp]),
@@ -143,7 +159,28 @@ def _declare(L):
             "firpfb_%s_execute_block" % t: (None, [vp, vp, ull, vp]),
             "firpfb_%s_execute_block_dev" % t: (None, [vp, vp, ull, vp]),
             "firpfb_%s_set_stream" % t: (None, [vp, vp]),
+            "firpfb_%s_create_rnyquist" % t: (vp, [i, u, u, u, f]),
+            "firpfb_%s_create_drnyquist" % t: (vp, [i, u, u, u, f]),
+            "firfilt_%s_create_rnyquist" % t: (vp, [i, u, u, f, f]),
+            "firdecim_%s_create_prototype" % t: (vp, [i, u, u, f, f]),
+            "firinterp_%s_create_prototype" % t: (vp, [i, u, u, f, f]),
         })
+    for t in (CRCF, CCCF):
+        sig.update({
+            "firpfbch_%s_create" % t: (vp, [i, u, u, vp]),
+            "firpfbch_%s_create_kaiser" % t: (vp, [i, u, u, f]),
+            "firpfbch_%s_create_rnyquist" % t: (vp, [i, u, u, f, i]),
+            "firpfbch_%s_destroy" % t: (None, [vp]),
+            "firpfbch_%s_reset" % t: (None, [vp]),
+            "firpfbch_%s_print" % t: (None, [vp]),
+            "firpfbch_%s_analyzer_execute" % t: (None, [vp, vp, vp]),
+            "firpfbch_%s_synthesizer_execute" % t: (None, [vp, vp, vp]),
+            "firpfbch_%s_execute_block" % t: (None, [vp, vp, ull, vp]),
+            "firpfbch_%s_execute_block_dev" % t: (None, [vp, vp, ull, vp]),
+            "firpfbch_%s_set_stream" % t: (None, [vp, vp]),
+        })
+    for d in FIRDES_DESIGNS:
+        sig["liquid_firdes_" + d] = (None, [u, u, f, f, vp])
     sig.update({
         "liquid_firdes_kaiser": (None, [u, f, f, f, vp]),
         "kaiser_beta_As": (f, [f]),
@@ -153,14 +190,16 @@ def _declare(L):
         "liquid_mi355x_memcpy_h2d": (None, [vp, vp, ull]),
         "liquid_mi355x_memcpy_d2h": (None, [vp, vp, ull]),
         "liquid_mi355x_device_synchronize": (None, []),
-        "firpfbch_crcf_create": (vp, [i, u, u, vp]),
-        "firpfbch_crcf_create_kaiser": (vp, [i, u, u, f]),
-        "firpfbch_crcf_destroy": (None, [vp]),
-        "firpfbch_crcf_reset": (None, [vp]),
-        "firpfbch_crcf_analyzer_execute": (None, [vp, vp, vp]),
-        "firpfbch_crcf_synthesizer_execute": (None, [vp, vp, vp]),
-        "firpfbch_crcf_execute_block": (None, [vp, vp, ull, vp]),
-        "firpfbch_crcf_execute_block_dev": (None, [vp, vp, ull, vp]),
+        "liquid_firdes_prototype": (None, [i, u, u, f, f, vp]),
+        "liquid_getopt_str2firfilt": (i, [C.c_char_p]),
+        "estimate_req_filter_len": (u, [f, f]),
+        "estimate_req_filter_As": (f, [f, u]),
+        "estimate_req_filter_df": (f, [f, u]),
+        "rkaiser_approximate_rho": (f, [u, f]),
+        "firdespm_run": (None, [u, u, vp, vp, vp, vp, i, vp]),
+        "liquid_filter_autocorr": (f, [vp, u, i]),
+        "liquid_filter_isi": (None, [vp, u, u, vp, vp]),
+        "liquid_Qf": (f, [f]),
         "firpfbch2_crcf_create": (vp, [i, u, u, vp]),
         "firpfbch2_crcf_create_kaiser": (vp, [i, u, u, f]),
         "firpfbch2_crcf_destroy": (None, [vp]),
@@ -171,20 +210,6 @@ def _declare(L):
         "firpfbch2_crcf_set_stream": (None, [vp, vp]),
         "firpfbch2_crcf_get_stream": (vp, [vp]),
         "firpfbch2_crcf_synchronize": (None, [vp]),
-        "resamp_crcf_create": (vp, [f, u, f, f, u]),
-        "resamp_crcf_create_default": (vp, [f]),
-        "resamp_crcf_destroy": (None, [vp]),
-        "resamp_crcf_print": (None, [vp]),
-        "resamp_crcf_reset": (None, [vp]),
-        "resamp_crcf_get_delay": (u, [vp]),
-        "resamp_crcf_set_rate": (None, [vp, f]),
-        "resamp_crcf_adjust_rate": (None, [vp, f]),
-        "resamp_crcf_execute": (None, [vp, cfloat, vp, vp]),
-        "resamp_crcf_execute_block": (None, [vp, vp, u, vp, vp]),
-        "resamp_crcf_num_output": (ull, [vp, ull]),
-        "resamp_crcf_execute_block_dev": (None, [vp, vp, ull, vp, vp]),
-        "resamp_crcf_set_stream": (None, [vp, vp]),
-        "resamp_crcf_synchronize": (None, [vp]),
     })
     for name, (res, args) in sig.items():
         fn = getattr(L, name)
@@ -194,6 +219,46 @@ def _declare(L):
 
 def ptr(a):
     return a.ctypes.data_as(C.c_void_p)
+
+
+# ------------------------------------------------------------------ filter design (liquid.h:1413-1668)
+FIRFILT_TYPES = ["kaiser", "pm", "rcos", "fexp", "fsech", "farcsech", "arkaiser", "rkaiser", "rrc", "hM3",
+                 "gmsktx", "gmskrx", "rfexp", "rfsech", "rfarcsech"]
+LIQUID_FIRFILT = {n: k + 1 for k, n in enumerate(FIRFILT_TYPES)}
+
+
+def firdes_prototype(ftype, k, m, beta, dt=0.0):
+    """liquid_firdes_prototype: 2km+1 taps (ftype: name or LIQUID_FIRFILT_* code)."""
+    code = LIQUID_FIRFILT[ftype] if isinstance(ftype, str) else int(ftype)
+    h = np.zeros(2 * k * m + 1, np.float32)
+    lib().liquid_firdes_prototype(code, k, m, beta, dt, ptr(h))
+    return h
+
+
+def firdes(design, k, m, beta, dt=0.0):
+    """liquid_firdes_<design>(k, m, beta, dt): e.g. design = "rkaiser", "rcos", "gmskrx"."""
+    h = np.zeros(2 * k * m + 1, np.float32)
+    getattr(lib(), "liquid_firdes_" + design)(k, m, beta, dt, ptr(h))
+    return h
+
+
+def firdespm(n, bands, des, weights=None, wtype=None):
+    """firdespm_run, band-pass designs."""
+    bands = np.ascontiguousarray(bands, np.float32)
+    des = np.ascontiguousarray(des, np.float32)
+    w = None if weights is None else np.ascontiguousarray(weights, np.float32)
+    wt = None if wtype is None else np.ascontiguousarray(wtype, np.int32)
+    h = np.zeros(n, np.float32)
+    lib().firdespm_run(n, len(des), ptr(bands), ptr(des), None if w is None else ptr(w),
+                       None if wt is None else ptr(wt), 0, ptr(h))
+    return h
+
+
+def filter_isi(h, k, m):
+    h = np.ascontiguousarray(h, np.float32)
+    rms, mx = C.c_float(), C.c_float()
+    lib().liquid_filter_isi(ptr(h), k, m, C.byref(rms), C.byref(mx))
+    return rms.value, mx.value
 
 
 def _samples(x, t):
@@ -263,8 +328,23 @@ class _Obj:
     def set_stream(self, s):
         self._fn("_set_stream")(self.q, s)
 
+    @classmethod
+    def construct(cls, ctor, args, t=CRCF, **attrs):
+        """Object from another constructor of the family, e.g.
+        FirFilt.construct("_create_rnyquist", (type, k, m, beta, mu), t=CRCF)."""
+        o = cls.__new__(cls)
+        o.t = t
+        o.prefix = cls.family % t
+        o.__dict__.update(attrs)
+        o.q = getattr(lib(), o.prefix + ctor)(*args)
+        if not o.q:
+            raise RuntimeError(o.prefix + ctor + " failed")
+        return o
+
 
 class FirFilt(_Obj):
+    family = "firfilt_%s"
+
     def freqresponse(self, fc):
         H = cfloat(0.0, 0.0)
         self._fn("_freqresponse")(self.q, fc, C.byref(H))
@@ -365,6 +445,8 @@ def _out_dtype(t):
 
 
 class FirDecim(_Obj):
+    family = "firdecim_%s"
+
     def __init__(self, M, h=None, m=None, As=None, t=CRCF):
         self.M, self.t = M, t
         self.prefix = "firdecim_%s" % t
@@ -392,6 +474,8 @@ class FirDecim(_Obj):
 
 
 class FirInterp(_Obj):
+    family = "firinterp_%s"
+
     def __init__(self, M, h=None, m=None, As=None, t=CRCF):
         self.M, self.t = M, t
         self.prefix = "firinterp_%s" % t
@@ -417,6 +501,8 @@ class FirInterp(_Obj):
 
 
 class FftFilt(_Obj):
+    family = "fftfilt_%s"
+
     def __init__(self, h, n, t=CRCF):
         self.n, self.t = n, t
         self.prefix = "fftfilt_%s" % t
@@ -447,14 +533,17 @@ class FftFilt(_Obj):
 
 
 class FirPfbch(_Obj):
-    prefix = "firpfbch_crcf"
+    family = "firpfbch_%s"
 
-    def __init__(self, typ, M, p=None, h=None, m=None, As=None):
-        self.typ, self.M = typ, M
-        if h is None:
+    def __init__(self, typ, M, p=None, h=None, m=None, As=None, t=CRCF, rnyquist=None):
+        self.typ, self.M, self.t = typ, M, t
+        self.prefix = self.family % t
+        if rnyquist is not None:               # (m, beta, ftype)
+            self.q = self._fn("_create_rnyquist")(typ, M, rnyquist[0], rnyquist[1], rnyquist[2])
+        elif h is None:
             self.q = self._fn("_create_kaiser")(typ, M, m, As)
         else:
-            self._h = _coefs(h, CRCF)
+            self._h = _coefs(h, t)
             self.q = self._fn("_create")(typ, M, p, ptr(self._h))
 
     def execute(self, x):
@@ -512,6 +601,8 @@ class FirPfbch2(_Obj):
 
 
 class FirPfb(_Obj):
+    family = "firpfb_%s"
+
     def __init__(self, M, h=None, m=None, fc=None, As=None, t=CRCF):
         self.M, self.t = M, t
         self.prefix = "firpfb_%s" % t
@@ -544,9 +635,11 @@ class FirPfb(_Obj):
 
 
 class Resamp(_Obj):
-    prefix = "resamp_crcf"
+    family = "resamp_%s"
 
-    def __init__(self, rate, m=None, fc=None, As=None, npfb=None):
+    def __init__(self, rate, m=None, fc=None, As=None, npfb=None, t=CRCF):
+        self.t = t
+        self.prefix = "resamp_%s" % t
         if m is None:
             self.q = self._fn("_create_default")(rate)
         else:
@@ -568,15 +661,14 @@ class Resamp(_Obj):
         return int(self._fn("_num_output")(self.q, nx))
 
     def execute(self, v):
-        v = complex(v)
-        y = np.zeros(max(1, self.num_output(1)), np.complex64)
+        y = np.zeros(max(1, self.num_output(1)), _out_dtype(self.t))
         nw = C.c_uint(0)
-        self._fn("_execute")(self.q, cfloat(v.real, v.imag), ptr(y), C.byref(nw))
+        self._fn("_execute")(self.q, _by_value(v, self.t), ptr(y), C.byref(nw))
         return y[:nw.value].copy()
 
     def execute_block(self, x):
-        x = _samples(x, CRCF)
-        y = np.zeros(max(1, self.num_output(len(x))), np.complex64)
+        x = _samples(x, self.t)
+        y = np.zeros(max(1, self.num_output(len(x))), _out_dtype(self.t))
         ny = C.c_uint(0)
         self._fn("_execute_block")(self.q, ptr(x), len(x), ptr(y), C.byref(ny))
         return y[:ny.value]

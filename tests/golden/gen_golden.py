@@ -20,6 +20,9 @@ arrays, plus the tolerances the reference's runners apply):
       dotprod  src/dotprod/tests/dotprod_{rrrf,crcf,cccf}_autotest.c
       firinterp src/filter/tests/firinterp_autotest.c:29-150
       firpfb   src/filter/tests/firpfb_autotest.c:26-73
+  * firdes   : rcos / rrcos coefficient arrays (src/filter/tests/firdes_autotest.c:25-95,
+               tol 1e-5) and Parks-McClellan designs with their band specs
+               (src/filter/tests/firdespm_autotest.c:26-140, tol 1e-4)
 
 Usage:  python tests/golden/gen_golden.py [/root/reference]
 """
@@ -192,8 +195,31 @@ def gen_known_answers():
     return ka
 
 
+def gen_firdes():
+    out = {}
+    b = parse_function_bodies(read("src/filter/tests/firdes_autotest.c"))
+    for fname, kind in (("autotest_liquid_firdes_rcos", "rcos"), ("autotest_liquid_firdes_rrcos", "rrcos")):
+        body = b[fname]
+        arr = parse_arrays(body)
+        sc = {k: float(v) for k, v in re.findall(r"\b(beta|offset)\s*=\s*(" + NUM + r")f?", body)}
+        k, m = (int(v) for v in re.search(r"unsigned int k\s*=\s*(\d+),\s*m\s*=\s*(\d+)", body).groups())
+        out[fname] = {"design": kind, "k": k, "m": m, "beta": sc["beta"], "dt": sc["offset"],
+                      "h": list(arr["h0"]), "tol": 1e-5,
+                      "source": "src/filter/tests/firdes_autotest.c"}
+    b = parse_function_bodies(read("src/filter/tests/firdespm_autotest.c"))
+    for fname, body in b.items():
+        arr = parse_arrays(body)
+        n = int(re.search(r"unsigned int n\s*=\s*(\d+)", body).group(1))
+        out[fname] = {"design": "firdespm", "n": n, "bands": list(arr["bands"]),
+                      "des": list(arr["des"]), "weights": list(arr["weights"]),
+                      "h": list(arr["h0"]), "tol": 1e-4,
+                      "source": "src/filter/tests/firdespm_autotest.c"}
+    return out
+
+
 def main():
     fixtures = {
+        "firdes": gen_firdes(),
         "firfilt": gen_filter_data("firfilt"),
         "firdecim": gen_filter_data("firdecim"),
         "fftfilt": gen_filter_data("fftfilt"),

@@ -348,6 +348,103 @@ def test_firpfb_block_and_push_vs_oracle(M, hlen, t):
     assert G.nrm_err(y2, ref[2010:]) < NRM
 
 
+# ------------------------------------------------------------ prototype constructors
+# *_create_rnyquist / *_create_prototype design taps on the host
+# (liquid_firdes_prototype, pinned in tests/test_firdes.py) and hand them to
+# the ordinary constructors: check the wiring against the oracle objects built
+# from the same taps.
+@pytest.mark.parametrize("t", ["rrrf", "crcf", "cccf"])
+@pytest.mark.parametrize("ftype,k,m,beta,mu", [("rkaiser", 2, 7, 0.3, 0.0), ("rrc", 4, 3, 0.5, 0.25),
+                                                ("gmsktx", 3, 4, 0.3, -0.5)])
+def test_firfilt_create_rnyquist(t, ftype, k, m, beta, mu):
+    r = rng(k * 11 + m)
+    x = samples(r, t, 5000)
+    code = LQ.LIQUID_FIRFILT[ftype]
+    g = LQ.FirFilt.construct("_create_rnyquist", (code, k, m, beta, mu), t=t)
+    h = LQ.firdes_prototype(ftype, k, m, beta, mu)
+    o = O.FirFilt(TYPES[t], h.astype(np.complex64) if t == "cccf" else h)
+    assert G.nrm_err(g.execute_block(x), o.execute_block(x)) < NRM
+
+
+@pytest.mark.parametrize("t", ["rrrf", "crcf", "cccf"])
+@pytest.mark.parametrize("ftype,M,m,beta,dt", [("arkaiser", 4, 5, 0.35, 0.0), ("kaiser", 3, 4, 0.3, 0.5),
+                                                ("rcos", 8, 2, 0.25, 0.0)])
+def test_firdecim_firinterp_create_prototype(t, ftype, M, m, beta, dt):
+    r = rng(M * 5 + m)
+    code = LQ.LIQUID_FIRFILT[ftype]
+    h = LQ.firdes_prototype(ftype, M, m, beta, dt)
+    hc = h.astype(np.complex64) if t == "cccf" else h
+    x = samples(r, t, 400 * M)
+    gd = LQ.FirDecim.construct("_create_prototype", (code, M, m, beta, dt), t=t, M=M)
+    od = O.FirDecim(TYPES[t], M, hc)
+    assert G.nrm_err(gd.execute_block(x), od.execute_block(x)) < NRM
+    xi = samples(r, t, 700)
+    gi = LQ.FirInterp.construct("_create_prototype", (code, M, m, beta, dt), t=t, M=M)
+    oi = O.FirInterp(TYPES[t], M, hc)
+    assert G.nrm_err(gi.execute_block(xi), oi.execute_block(xi)) < NRM
+
+
+@pytest.mark.parametrize("t", ["rrrf", "crcf", "cccf"])
+@pytest.mark.parametrize("deriv", [0, 1])
+def test_firpfb_create_rnyquist_drnyquist(t, deriv):
+    # firpfb.c:146-240: prototype at M*k samples/symbol; derivative bank = central
+    # difference (circular ends) scaled to max|h dh| = 0.06
+    M, k, m, beta = 16, 2, 5, 0.35
+    code = LQ.LIQUID_FIRFILT["rkaiser"]
+    H = LQ.firdes_prototype("rkaiser", M * k, m, beta).astype(np.float64)
+    if deriv:
+        dH = np.roll(H, -1) - np.roll(H, 1)
+        H = dH * 0.06 / np.max(np.abs(H * dH))
+    H = H.astype(np.float32)
+    ctor = "_create_drnyquist" if deriv else "_create_rnyquist"
+    g = LQ.FirPfb.construct(ctor, (code, M, k, m, beta), t=t, M=M)
+    o = O.FirPfb(TYPES[t], M, H.astype(np.complex64) if t == "cccf" else H)
+    r = rng(77 + deriv)
+    x = samples(r, t, 600)
+    ref = np.empty((len(x), M), np.float32 if t == "rrrf" else np.complex64)
+    for j, v in enumerate(x):
+        o.push(v)
+        ref[j] = [o.execute(i) for i in range(M)]
+    assert G.nrm_err(g.execute_block(x), ref) < 2 * NRM
+
+
+@pytest.mark.parametrize("typ", [LQ.LIQUID_ANALYZER, LQ.LIQUID_SYNTHESIZER])
+@pytest.mark.parametrize("M,p", [(8, 4), (64, 6), (6, 3)])
+def test_firpfbch_cccf_complex_taps(typ, M, p):
+    # the channelizer is linear in its taps over the complex numbers:
+    # A(hr + j hi) = A(hr) + j A(hi), so two real-tap oracle runs pin cccf
+    r = rng(M * p + typ)
+    h = cx(r, M * p)
+    nb = 20
+    x = cx(r, nb * M)
+    g = LQ.FirPfbch(typ, M, p=p, h=h, t="cccf")
+    o_re = O.FirPfbch(typ, M, p=p, h=h.real.copy())
+    o_im = O.FirPfbch(typ, M, p=p, h=h.imag.copy())
+    y = np.concatenate([g.execute(x[:M]), g.execute_block(x[M:])])
+    ref = np.concatenate([o_re.execute(x[b * M:(b + 1) * M]).astype(np.complex128)
+                          + 1j * o_im.execute(x[b * M:(b + 1) * M]) for b in range(nb)])
+    assert G.nrm_err(y, ref) < NRM
+
+
+@pytest.mark.parametrize("t", ["crcf", "cccf"])
+@pytest.mark.parametrize("typ", [LQ.LIQUID_ANALYZER, LQ.LIQUID_SYNTHESIZER])
+@pytest.mark.parametrize("ftype", ["arkaiser", "rkaiser", "rrc", "hM3"])
+def test_firpfbch_create_rnyquist(t, typ, ftype):
+    # firpfbch.c:193-256: analyzer taps are the time-reversed first 2Mm (matched filter)
+    M, m, beta = 16, 3, 0.4
+    h = LQ.firdes_prototype(ftype, M, m, beta)
+    g_len = 2 * M * m
+    gc = h[:g_len] if typ == LQ.LIQUID_SYNTHESIZER else h[:g_len][::-1]
+    g = LQ.FirPfbch(typ, M, t=t, rnyquist=(m, beta, LQ.LIQUID_FIRFILT[ftype]))
+    o = O.FirPfbch(typ, M, p=2 * m, h=np.ascontiguousarray(gc))
+    r = rng(5 + typ)
+    nb = 24
+    x = cx(r, nb * M)
+    y = g.execute_block(x)
+    ref = np.concatenate([o.execute(x[b * M:(b + 1) * M]) for b in range(nb)])
+    assert G.nrm_err(y, ref) < NRM
+
+
 def test_firfilt_freqresponse_groupdelay():
     # firfilt.c:371-404 restated in float64: H = s * sum_i h[n-1-i] e^{j2pi fc i}
     r = rng(3)
@@ -426,6 +523,31 @@ def test_resamp_set_rate_adjust_rate_reset():
     g.set_rate(0.5)
     a, b = g.execute_block(x[:5000]), o.execute_block(x[:5000])
     assert len(a) == len(b) and G.nrm_err(a, b) < NRM
+
+
+@pytest.mark.parametrize("t", [LQ.RRRF, LQ.CCCF])
+@pytest.mark.parametrize("rate,m,npfb", [(1.037, 7, 64), (0.8131, 3, 37), (1.3, 20, 16)])
+def test_resamp_types_vs_oracle(t, rate, m, npfb):
+    # resamp.c:117-132 designs real taps for every type: cccf filters exactly as
+    # crcf, and rrrf as crcf on a real signal (imaginary part zero)
+    r = rng(int(rate * 100) + m + (7 if t == LQ.RRRF else 0))
+    rate = float(np.float32(rate))
+    x = cx(r, 150_000)
+    if t == LQ.RRRF:
+        x = np.ascontiguousarray(x.real)
+    g = LQ.Resamp(rate, m, 0.25, 60.0, npfb, t=t)
+    o = O.Resamp(rate, m, 0.25, 60.0, npfb)
+    cuts = [0, 1, 2, 5000, 80_000, 80_001, 150_000]
+    ys = []
+    for a, b in zip(cuts[:-1], cuts[1:]):
+        ys.append(g.execute(x[a]) if b - a == 1 else g.execute_block(x[a:b]))
+    y = np.concatenate(ys)
+    ref = o.execute_block(x.astype(np.complex64))
+    assert len(y) == len(ref)
+    if t == LQ.RRRF:
+        assert y.dtype == np.float32
+        ref = ref.real
+    assert G.nrm_err(y, ref) < NRM
 
 
 def test_resamp_baseline_config5_device():

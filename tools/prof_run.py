@@ -13,10 +13,10 @@ import liquidmi as LQ  # noqa: E402
 
 p = argparse.ArgumentParser()
 p.add_argument("--iters", type=int, default=3)
-p.add_argument("--what", default="both", choices=["both", "pfb2", "fir"])
+p.add_argument("--what", default="both", choices=["both", "all", "pfb2", "fir", "resamp"])
 a = p.parse_args()
 s = torch.cuda.Stream()
-if a.what in ("both", "pfb2"):
+if a.what in ("both", "all", "pfb2"):
     n = 1 << 27
     x = torch.rand(2 * n, device="cuda") - 0.5
     y = torch.empty(4 * n, device="cuda")
@@ -27,7 +27,7 @@ if a.what in ("both", "pfb2"):
     q.synchronize()
     q.destroy()
     del x, y
-if a.what in ("both", "fir"):
+if a.what in ("both", "all", "fir"):
     n = 1 << 28
     x = torch.rand(2 * n, device="cuda") - 0.5
     y = torch.empty(2 * n, device="cuda")
@@ -37,5 +37,16 @@ if a.what in ("both", "fir"):
         f.execute_block_dev(x.data_ptr(), n, y.data_ptr())
     f.synchronize()
     f.destroy()
+if a.what in ("all", "resamp"):
+    n = 1 << 25
+    x = torch.rand(2 * n, device="cuda") - 0.5
+    y = torch.empty(2 * (int(n * 1.037) + 4096), device="cuda")
+    r = LQ.Resamp(1.037, 7, 0.25, 60.0, 64)
+    r.set_stream(s.cuda_stream)
+    r.num_output(n)
+    for _ in range(a.iters):
+        r.execute_block_dev(x.data_ptr(), n, y.data_ptr())
+    r.synchronize()
+    r.destroy()
 torch.cuda.synchronize()
 print("done")

@@ -9,7 +9,7 @@ OUT=gpurun_out/$TAG; rm -rf $OUT; mkdir -p $OUT
 python -c "import __graft_entry__ as g; g.build()" > $OUT/build.log 2>&1 || exit 1
 timeout -k 10 600 rocprofv3 --kernel-trace --stats -d $OUT/trace -o run --output-format csv -- python3 bench.py --steps 10 --warmup 2 --no-cpu-baseline > $OUT/bench_under_rocprof.log 2>&1 || { tail -20 $OUT/bench_under_rocprof.log; exit 1; }
 for C in FETCH_SIZE WRITE_SIZE; do
-  timeout -k 10 300 rocprofv3 --pmc $C --output-format csv -d $OUT/$C -o run -- python3 tools/prof_run.py --what both --iters 2 > $OUT/$C.log 2>&1 || { tail -5 $OUT/$C.log; exit 1; }
+  timeout -k 10 300 rocprofv3 --pmc $C --output-format csv -d $OUT/$C -o run -- python3 tools/prof_run.py --what all --iters 2 > $OUT/$C.log 2>&1 || { tail -5 $OUT/$C.log; exit 1; }
 done
 python3 - $OUT <<'PY'
 import csv, glob, json, os, sys, collections
@@ -21,7 +21,7 @@ for c in ("FETCH_SIZE", "WRITE_SIZE"):
     for r in csv.DictReader(open(f)):
         agg[r["Kernel_Name"]].append(float(r["Counter_Value"]))
     for k, v in agg.items():
-        key = "firpfbch2" if "pfb2" in k else ("firfilt" if "firfilt" in k else None)
+        key = "firpfbch2" if "pfb2" in k else ("firfilt" if "firfilt" in k else ("resamp" if "k_resamp" in k else None))
         if key:
             res.setdefault(key, {})[c] = sum(v) / len(v)
 traffic = {}
@@ -34,8 +34,11 @@ for key, d in res.items():
                     "raw_FETCH_SIZE_KB": d.get("FETCH_SIZE"), "raw_WRITE_SIZE_KB": d.get("WRITE_SIZE")}
 json.dump({"firpfbch2_bytes_per_launch": traffic.get("firpfbch2", {}).get("total_bytes"),
            "firfilt_bytes_per_launch": traffic.get("firfilt", {}).get("total_bytes"),
+           "resamp_bytes_per_launch": traffic.get("resamp", {}).get("total_bytes"),
            "detail": traffic,
-           "launch_shapes": {"firpfbch2": "M=1024 m=4, 2^27 input samples", "firfilt": "h=64, 2^28 samples"},
+           "launch_shapes": {"firpfbch2": "M=1024 m=4, 2^27 input samples", "firfilt": "h=64, 2^28 samples",
+                             "resamp": "r=1.037 m=7 npfb=64, 2^25 input samples (8-byte loads: the x2 FETCH "
+                                       "correction is calibrated for 16-byte streams only)"},
            "method": "rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE in separate passes over tools/prof_run.py; "
                      "FETCH_SIZE doubled per the gfx950 correction"},
           open(os.path.join(out, "traffic.json"), "w"), indent=1)
