@@ -284,6 +284,85 @@ LQMI_RESAMP_API(resamp_crcf, liquid_float_complex)
 LQMI_RESAMP_API(resamp_cccf, liquid_float_complex)
 
 /* ------------------------------------------------------------------------ */
+/* resamp2 (liquid.h:2840-2925), msresamp2 (:3027-3090), msresamp (:3094-3140) */
+/* ------------------------------------------------------------------------ */
+/* liquid.h:3022-3025 */
+typedef enum {
+    LIQUID_RESAMP_INTERP = 0,
+    LIQUID_RESAMP_DECIM,
+} liquid_resamp_type;
+
+/* extension: mode argument of resamp2_*_execute_block[_dev] */
+enum {
+    LQMI_RESAMP2_FILTER = 0,       /* n calls: x[n] -> y0[n] (low band), y1[n] (high band) */
+    LQMI_RESAMP2_ANALYZER,         /* x[2n] -> y0[2n] */
+    LQMI_RESAMP2_SYNTHESIZER,      /* x[2n] -> y0[2n] */
+    LQMI_RESAMP2_DECIM,            /* x[2n] -> y0[n] */
+    LQMI_RESAMP2_INTERP,           /* x[n]  -> y0[2n] */
+};
+
+#define LQMI_RESAMP2_API(RESAMP2, T)                                                                \
+    typedef struct RESAMP2##_s *RESAMP2;                                                            \
+    RESAMP2 RESAMP2##_create(unsigned int _m, float _f0, float _As);                                \
+    RESAMP2 RESAMP2##_recreate(RESAMP2 _q, unsigned int _m, float _f0, float _As);                  \
+    void RESAMP2##_destroy(RESAMP2 _q);                                                             \
+    void RESAMP2##_print(RESAMP2 _q);                                                               \
+    void RESAMP2##_clear(RESAMP2 _q);                                                               \
+    unsigned int RESAMP2##_get_delay(RESAMP2 _q);                                                   \
+    void RESAMP2##_filter_execute(RESAMP2 _q, T _x, T *_y0, T *_y1);                                \
+    void RESAMP2##_analyzer_execute(RESAMP2 _q, T *_x, T *_y);                                      \
+    void RESAMP2##_synthesizer_execute(RESAMP2 _q, T *_x, T *_y);                                   \
+    void RESAMP2##_decim_execute(RESAMP2 _q, T *_x, T *_y);                                         \
+    void RESAMP2##_interp_execute(RESAMP2 _q, T _x, T *_y);                                         \
+    /* extension: _n consecutive calls of one mode (LQMI_RESAMP2_*); _y1 only for FILTER */         \
+    void RESAMP2##_execute_block(RESAMP2 _q, int _mode, T *_x, unsigned long long _n, T *_y0, T *_y1); \
+    void RESAMP2##_execute_block_dev(RESAMP2 _q, int _mode, const T *_dx, unsigned long long _n,    \
+                                     T *_dy0, T *_dy1);                                             \
+    void RESAMP2##_set_stream(RESAMP2 _q, void *_hip_stream);                                       \
+    void RESAMP2##_synchronize(RESAMP2 _q);
+
+LQMI_RESAMP2_API(resamp2_rrrf, float)
+LQMI_RESAMP2_API(resamp2_crcf, liquid_float_complex)
+LQMI_RESAMP2_API(resamp2_cccf, liquid_float_complex)
+
+#define LQMI_MSRESAMP2_API(MSRESAMP2, T)                                                            \
+    typedef struct MSRESAMP2##_s *MSRESAMP2;                                                        \
+    MSRESAMP2 MSRESAMP2##_create(int _type, unsigned int _num_stages, float _fc, float _f0, float _As); \
+    void MSRESAMP2##_destroy(MSRESAMP2 _q);                                                         \
+    void MSRESAMP2##_print(MSRESAMP2 _q);                                                           \
+    void MSRESAMP2##_reset(MSRESAMP2 _q);                                                           \
+    float MSRESAMP2##_get_delay(MSRESAMP2 _q);                                                      \
+    void MSRESAMP2##_execute(MSRESAMP2 _q, T *_x, T *_y);                                           \
+    /* extension: _n consecutive calls (interp: 1 in, 2^s out; decim: 2^s in, 1 out) */            \
+    void MSRESAMP2##_execute_block(MSRESAMP2 _q, T *_x, unsigned long long _n, T *_y);              \
+    void MSRESAMP2##_execute_block_dev(MSRESAMP2 _q, const T *_dx, unsigned long long _n, T *_dy);  \
+    void MSRESAMP2##_set_stream(MSRESAMP2 _q, void *_hip_stream);                                   \
+    void MSRESAMP2##_synchronize(MSRESAMP2 _q);
+
+LQMI_MSRESAMP2_API(msresamp2_rrrf, float)
+LQMI_MSRESAMP2_API(msresamp2_crcf, liquid_float_complex)
+LQMI_MSRESAMP2_API(msresamp2_cccf, liquid_float_complex)
+
+#define LQMI_MSRESAMP_API(MSRESAMP, T)                                                              \
+    typedef struct MSRESAMP##_s *MSRESAMP;                                                          \
+    MSRESAMP MSRESAMP##_create(float _r, float _As);                                                \
+    void MSRESAMP##_destroy(MSRESAMP _q);                                                           \
+    void MSRESAMP##_print(MSRESAMP _q);                                                             \
+    void MSRESAMP##_reset(MSRESAMP _q);                                                             \
+    float MSRESAMP##_get_delay(MSRESAMP _q);                                                        \
+    void MSRESAMP##_execute(MSRESAMP _q, T *_x, unsigned int _nx, T *_y, unsigned int *_ny);        \
+    /* extension: outputs the next _nx inputs produce; device-pointer form */                       \
+    unsigned long long MSRESAMP##_num_output(MSRESAMP _q, unsigned long long _nx);                  \
+    void MSRESAMP##_execute_block_dev(MSRESAMP _q, const T *_dx, unsigned long long _nx, T *_dy,    \
+                                      unsigned long long *_ny);                                     \
+    void MSRESAMP##_set_stream(MSRESAMP _q, void *_hip_stream);                                     \
+    void MSRESAMP##_synchronize(MSRESAMP _q);
+
+LQMI_MSRESAMP_API(msresamp_rrrf, float)
+LQMI_MSRESAMP_API(msresamp_crcf, liquid_float_complex)
+LQMI_MSRESAMP_API(msresamp_cccf, liquid_float_complex)
+
+/* ------------------------------------------------------------------------ */
 /* fftfilt (liquid.h:2192-2240): rrrf, crcf, cccf                            */
 /* ------------------------------------------------------------------------ */
 #define LQMI_FFTFILT_API(FFTFILT, TO, TC, TI)                                                   \

@@ -1,0 +1,170 @@
+// k_resamp2.hip -- half-band resampler (resamp2, src/filter/src/resamp2.c)
+// as one data-parallel kernel per block of calls.
+//
+// The reference keeps two windows w0, w1 of 2m samples; every mode pushes
+// samples into them and reads either the "delay" tap (window index m-1, i.e.
+// the sample pushed m pushes ago) or the odd-tap dot product
+// sum_j h1[j] w[j] (h1[j] = h[4m-1-2j]).  Here each window is the virtual
+// sequence E_p = hist_p (2m samples) ++ this block's pushes, so the output of
+// call i is a pure function of E_0, E_1 -- one lane per call, no state.
+//   filter : call i pushes x[i] into window p_i = (t0+i)&1
+//   decim  : w1 <- x[2i], w0 <- x[2i+1]            (analyzer: halved)
+//   interp : w0 <- x[i],  w1 <- x[i]
+//   synth  : w0 <- X[2i]+X[2i+1], w1 <- X[2i]-X[2i+1]
+#include <hip/hip_runtime.h>
+
+#include "lq_device.h"
+#include "lq_kernels.h"
+
+namespace {
+
+constexpr int NT = 256;
+
+__device__ __forceinline__ float2 r2_mac(float h, float2 v, float2 a)
+{
+    return make_float2(fmaf(h, v.x, a.x), fmaf(h, v.y, a.y));
+}
+__device__ __forceinline__ float r2_mac(float h, float v, float a) { return fmaf(h, v, a); }
+__device__ __forceinline__ float2 r2_mac(float2 h, float2 v, float2 a)
+{
+    return make_float2(fmaf(h.x, v.x, fmaf(-h.y, v.y, a.x)), fmaf(h.x, v.y, fmaf(h.y, v.x, a.y)));
+}
+__device__ __forceinline__ float r2_scale(float s, float v) { return s * v; }
+__device__ __forceinline__ float2 r2_scale(float s, float2 v) { return make_float2(s * v.x, s * v.y); }
+__device__ __forceinline__ float r2_add(float a, float b) { return a + b; }
+__device__ __forceinline__ float2 r2_add(float2 a, float2 b) { return make_float2(a.x + b.x, a.y + b.y); }
+__device__ __forceinline__ float r2_sub(float a, float b) { return a - b; }
+__device__ __forceinline__ float2 r2_sub(float2 a, float2 b) { return make_float2(a.x - b.x, a.y - b.y); }
+
+struct R2Args {
+    int mode;          // LQK_R2_*
+    int m;             // semi-length: windows of 2m
+    int t0;            // filter mode: toggle before the first call
+    long long n;       // calls in this block
+    float scale;       // power-of-two output scale (msresamp2 decimator's 1/M), exact
+};
+
+// E_p[k]: k < 2m from the history, else the (k-2m)-th push of this block
+template <typename S>
+__device__ __forceinline__ S r2_E(const R2Args &a, int p, long long k, const S *__restrict__ h0,
+                                  const S *__restrict__ h1, const S *__restrict__ x)
+{
+    const int W = 2 * a.m;
+    if (k < W) return p ? h1[k] : h0[k];
+    const long long c = k - W;
+    switch (a.mode) {
+    case LQK_R2_FILTER: return x[2 * c + ((p + a.t0) & 1)];
+    case LQK_R2_DECIM: return p ? x[2 * c] : x[2 * c + 1];
+    case LQK_R2_ANALYZER: return r2_scale(0.5f, p ? x[2 * c] : x[2 * c + 1]);
+    case LQK_R2_INTERP: return x[c];
+    default: {   // synthesizer
+        const S u = x[2 * c], v = x[2 * c + 1];
+        return p ? r2_sub(u, v) : r2_add(u, v);
+    }
+    }
+}
+
+template <typename S, typename C>
+__device__ __forceinline__ S r2_dot(const R2Args &a, const C *__restrict__ th, int p, long long k0,
+                                    const S *__restrict__ h0, const S *__restrict__ h1, const S *__restrict__ x)
+{
+    S acc{};
+    for (int j = 0; j < 2 * a.m; j++) acc = r2_mac(th[j], r2_E(a, p, k0 + j, h0, h1, x), acc);
+    return acc;
+}
+
+template <typename S, typename C>
+__global__ __launch_bounds__(NT) void k_resamp2(R2Args a, const C *__restrict__ taps, const S *__restrict__ hist0,
+                                                const S *__restrict__ hist1, const S *__restrict__ x,
+                                                S *__restrict__ y0, S *__restrict__ y1)
+{
+    extern __shared__ __attribute__((aligned(16))) unsigned char r2_smem[];
+    C *th = reinterpret_cast<C *>(r2_smem);
+    for (int j = threadIdx.x; j < 2 * a.m; j += NT) th[j] = taps[j];
+    __syncthreads();
+    const long long i = (long long)blockIdx.x * NT + threadIdx.x;
+    if (i >= a.n) return;
+    const long long W = 2 * a.m;
+    switch (a.mode) {
+    case LQK_R2_FILTER: {
+        const int p = (a.t0 + (int)(i & 1)) & 1;
+        const int sp = (p + a.t0) & 1;                 // block inputs of window p are x[2c + sp]
+        const long long cp = (i + 1 - sp) >> 1;        // pushes into p before call i
+        const long long cq = i - cp;
+        const S yi = r2_E(a, p, W + cp - a.m, hist0, hist1, x);
+        const S yq = r2_dot(a, th, 1 - p, cq, hist0, hist1, x);
+        y0[i] = r2_scale(0.5f, r2_add(yi, yq));
+        y1[i] = r2_scale(0.5f, r2_sub(yi, yq));
+        break;
+    }
+    case LQK_R2_DECIM:
+    case LQK_R2_ANALYZER: {
+        const S yq = r2_dot(a, th, 1, i + 1, hist0, hist1, x);
+        const S yd = r2_E(a, 0, W + i - a.m, hist0, hist1, x);
+        if (a.mode == LQK_R2_DECIM) {
+            y0[i] = r2_scale(a.scale, r2_add(yd, yq));
+        } else {
+            y0[2 * i] = r2_add(yq, yd);
+            y0[2 * i + 1] = r2_sub(yq, yd);
+        }
+        break;
+    }
+    default: {   // interp, synthesizer: delay branch first, then the dot product
+        y0[2 * i] = r2_E(a, 0, W + i - a.m, hist0, hist1, x);
+        y0[2 * i + 1] = r2_dot(a, th, 1, i + 1, hist0, hist1, x);
+    }
+    }
+}
+
+// new history: hist_p[k] = E_p[pushes_p + k], k < 2m
+template <typename S>
+__global__ __launch_bounds__(NT) void k_resamp2_hist(R2Args a, long long push0, long long push1,
+                                                     const S *__restrict__ hist0, const S *__restrict__ hist1,
+                                                     const S *__restrict__ x, S *__restrict__ out0,
+                                                     S *__restrict__ out1)
+{
+    const int k = blockIdx.x * NT + threadIdx.x;
+    const int W = 2 * a.m;
+    if (k >= 2 * W) return;
+    const int p = k >= W;
+    const int kk = p ? k - W : k;
+    const S v = r2_E(a, p, (p ? push1 : push0) + kk, hist0, hist1, x);
+    (p ? out1 : out0)[kk] = v;
+}
+
+template <typename S, typename C>
+void run_r2(const R2Args &a, const void *taps, const void *h0, const void *h1, void *n0, void *n1, const void *x,
+            void *y0, void *y1, hipStream_t st)
+{
+    long long p0, p1;
+    switch (a.mode) {
+    case LQK_R2_FILTER:
+        p1 = (a.n + (a.t0 ? 1 : 0)) / 2;   // calls whose window is w1
+        p0 = a.n - p1;
+        break;
+    default: p0 = p1 = a.n;
+    }
+    const unsigned grid = (unsigned)((a.n + NT - 1) / NT);
+    hipLaunchKernelGGL((k_resamp2<S, C>), dim3(grid), dim3(NT), (size_t)2 * a.m * sizeof(C), st, a,
+                       (const C *)taps, (const S *)h0, (const S *)h1, (const S *)x, (S *)y0, (S *)y1);
+    LQ_CHECK_LAUNCH();
+    hipLaunchKernelGGL((k_resamp2_hist<S>), dim3((unsigned)((4 * a.m + NT - 1) / NT)), dim3(NT), 0, st, a, p0, p1,
+                       (const S *)h0, (const S *)h1, (const S *)x, (S *)n0, (S *)n1);
+    LQ_CHECK_LAUNCH();
+}
+
+} // namespace
+
+extern "C" void lqk_resamp2(int kind, int mode, unsigned int m, int t0, float scale, const void *taps,
+                            const void *hist0, const void *hist1, void *hist0_new, void *hist1_new, const void *x,
+                            unsigned long long n, void *y0, void *y1, void *stream)
+{
+    if (n == 0) return;
+    R2Args a{mode, (int)m, t0 & 1, (long long)n, scale};
+    hipStream_t st = (hipStream_t)stream;
+    switch (kind) {
+    case 0: run_r2<float, float>(a, taps, hist0, hist1, hist0_new, hist1_new, x, y0, y1, st); break;
+    case 1: run_r2<float2, float>(a, taps, hist0, hist1, hist0_new, hist1_new, x, y0, y1, st); break;
+    default: run_r2<float2, float2>(a, taps, hist0, hist1, hist0_new, hist1_new, x, y0, y1, st); break;
+    }
+}

@@ -143,6 +143,18 @@ void lqk_resamp(int real_io, const lqk_rs_plan *pl, unsigned long long g0, unsig
 void lqk_firpfb_single(int kind, const void *hpoly, unsigned int L, unsigned int i, const void *win,
                        float scale_re, float scale_im, void *y, void *stream);
 
+/* ---------------------------------------------------------------- resamp2 (half-band)
+ * n calls of one resamp2 mode (src/filter/src/resamp2.c:273-356).  hist0/hist1 =
+ * the two 2m-sample windows (oldest first); the updated windows go to
+ * hist0_new/hist1_new (must not alias).  taps: the 2m odd taps h1[j] = h[4m-1-2j]
+ * (float for kind 0/1, float2 for kind 2).  Outputs: filter y0[i], y1[i];
+ * decim y0[i] (times scale, a power of two); analyzer/interp/synthesizer
+ * y0[2i], y0[2i+1].  t0: filter-mode toggle before the first call. */
+enum { LQK_R2_FILTER = 0, LQK_R2_ANALYZER, LQK_R2_SYNTHESIZER, LQK_R2_DECIM, LQK_R2_INTERP };
+void lqk_resamp2(int kind, int mode, unsigned int m, int t0, float scale, const void *taps, const void *hist0,
+                 const void *hist1, void *hist0_new, void *hist1_new, const void *x, unsigned long long n,
+                 void *y0, void *y1, void *stream);
+
 #ifdef __cplusplus
 }
 #endif

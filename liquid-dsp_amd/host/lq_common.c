@@ -94,7 +94,7 @@ float lq_kaiser_beta_As(float As)
 
 float kaiser_beta_As(float _As) { return lq_kaiser_beta_As(_As); }
 
-static float lq_sincf(float x)
+float lq_sincf(float x)
 {
     if (fabsf(x) < 0.01f) return cosf(M_PI * x / 2.0f) * cosf(M_PI * x / 4.0f) * cosf(M_PI * x / 8.0f);
     return sinf(M_PI * x) / (M_PI * x);
@@ -131,7 +131,7 @@ static float lq_besseli0f(float z)
     return y;
 }
 
-static float lq_kaiser_window(unsigned int n, unsigned int N, float beta, float mu)
+float lq_kaiser_window(unsigned int n, unsigned int N, float beta, float mu)
 {
     float t = (float)n - (float)(N - 1) / 2 + mu;
     float r = 2.0f * t / (float)N;

@@ -53,6 +53,8 @@ int lq_is_pow2(unsigned int x);
 /* host-side design routines (create time only; src/filter/src/firdes.c) */
 float lq_kaiser_beta_As(float As);
 void lq_firdes_kaiser(unsigned int n, float fc, float As, float mu, float *h);
+float lq_sincf(float x);                                                   /* math.c:128-139 */
+float lq_kaiser_window(unsigned int n, unsigned int N, float beta, float mu); /* math.c:289-312 */
 
 /* generic firfilt engine used by the three typed front ends */
 typedef struct lq_firfilt_s lq_firfilt;
@@ -68,6 +70,15 @@ void lq_firfilt_execute_block(lq_firfilt *q, const void *x, unsigned long long n
 void lq_firfilt_execute_block_dev(lq_firfilt *q, const void *dx, unsigned long long n, void *dy);
 unsigned int lq_firfilt_get_length(lq_firfilt *q);
 lq_ctx *lq_firfilt_ctx(lq_firfilt *q);
+
+/* arbitrary-rate resampler engine (host/resamp.c), used by msresamp */
+typedef struct lq_rs_s lq_rs;
+lq_rs *lq_rs_create(int kind, float rate, unsigned int m, float fc, float As, unsigned int npfb);
+void lq_rs_destroy(lq_rs *q);
+void lq_rs_reset(lq_rs *q);
+unsigned long long lq_rs_num_output(lq_rs *q, unsigned long long nx);
+void lq_rs_block_dev(lq_rs *q, const void *dx, unsigned long long nx, void *dy, unsigned long long *ny);
+lq_ctx *lq_rs_ctx(lq_rs *q);
 
 /* generic dotprod engine */
 typedef struct lq_dotprod_s lq_dotprod;

@@ -45,7 +45,7 @@ typedef struct {
     unsigned long long pre, P, Q, qs;
 } rs_plan;
 
-typedef struct {
+struct lq_rs_s {
     int kind;
     size_t esz;                   /* bytes per sample */
     float rate, del, fc, As;
@@ -60,7 +60,7 @@ typedef struct {
     int cur;
     lq_ctx ctx;
     lq_devbuf xbuf, ybuf;
-} lq_rs;
+};
 
 static const char *lq_ext[] = {"rrrf", "crcf", "cccf"};
 
@@ -268,7 +268,7 @@ static void rs_sync_now(lq_rs *q)
     }
 }
 
-static lq_rs *lq_rs_create(int kind, float _rate, unsigned int _m, float _fc, float _As, unsigned int _npfb)
+lq_rs *lq_rs_create(int kind, float _rate, unsigned int _m, float _fc, float _As, unsigned int _npfb)
 {
     if (_rate <= 0) LQ_FAIL("error: resamp_%s_create(), resampling rate must be greater than zero\n", lq_ext[kind]);
     if (_m == 0) LQ_FAIL("error: resamp_%s_create(), filter semi-length must be greater than zero\n", lq_ext[kind]);
@@ -332,7 +332,7 @@ static lq_rs *lq_rs_create(int kind, float _rate, unsigned int _m, float _fc, fl
     return q;
 }
 
-static void lq_rs_destroy(lq_rs *_q)
+void lq_rs_destroy(lq_rs *_q)
 {
     lqrt_sync(_q->ctx.stream);
     lqrt_free(_q->d_taps);
@@ -354,7 +354,7 @@ static void lq_rs_print(lq_rs *_q)
     for (unsigned int i = 0; i < _q->npfb; i++) printf("  bank %3u: \n", i);
 }
 
-static void lq_rs_reset(lq_rs *_q)
+void lq_rs_reset(lq_rs *_q)
 {
     lqrt_memset(_q->d_hist[0], (size_t)_q->L * _q->esz, _q->ctx.stream);
     lqrt_memset(_q->d_hist[1], (size_t)_q->L * _q->esz, _q->ctx.stream);
@@ -394,7 +394,7 @@ static void lq_rs_adjust_rate(lq_rs *_q, float _delta)
     rs_new_del(_q, 1.0f / _q->rate);
 }
 
-static unsigned long long lq_rs_num_output(lq_rs *_q, unsigned long long _nx)
+unsigned long long lq_rs_num_output(lq_rs *_q, unsigned long long _nx)
 {
     if (_nx == 0) return 0;
     unsigned long long done = 0, total = 0;
@@ -412,7 +412,7 @@ static unsigned long long lq_rs_num_output(lq_rs *_q, unsigned long long _nx)
     return total;
 }
 
-static void lq_rs_block_dev(lq_rs *_q, const void *_dxv, unsigned long long _nx, void *_dyv,
+void lq_rs_block_dev(lq_rs *_q, const void *_dxv, unsigned long long _nx, void *_dyv,
                             unsigned long long *_ny)
 {
     const char *_dx = (const char *)_dxv;
@@ -453,6 +453,8 @@ static void lq_rs_block(lq_rs *_q, const void *_x, unsigned int _nx, void *_y, u
     lqrt_sync(_q->ctx.stream);
     *_ny = (unsigned int)ny;
 }
+
+lq_ctx *lq_rs_ctx(lq_rs *q) { return &q->ctx; }
 
 #define LQ_RESAMP_FRONT(NAME, KIND, T)                                                                  \
     struct NAME##_s {                                                                               \

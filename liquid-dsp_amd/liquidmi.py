@@ -165,6 +165,45 @@ def _declare(L):
             "firdecim_%s_create_prototype" % t: (vp, [i, u, u, f, f]),
             "firinterp_%s_create_prototype" % t: (vp, [i, u, u, f, f]),
         })
+    for t in (RRRF, CRCF, CCCF):
+        ti = f if t == RRRF else cfloat
+        sig.update({
+            "resamp2_%s_create" % t: (vp, [u, f, f]),
+            "resamp2_%s_recreate" % t: (vp, [vp, u, f, f]),
+            "resamp2_%s_destroy" % t: (None, [vp]),
+            "resamp2_%s_print" % t: (None, [vp]),
+            "resamp2_%s_clear" % t: (None, [vp]),
+            "resamp2_%s_get_delay" % t: (u, [vp]),
+            "resamp2_%s_filter_execute" % t: (None, [vp, ti, vp, vp]),
+            "resamp2_%s_analyzer_execute" % t: (None, [vp, vp, vp]),
+            "resamp2_%s_synthesizer_execute" % t: (None, [vp, vp, vp]),
+            "resamp2_%s_decim_execute" % t: (None, [vp, vp, vp]),
+            "resamp2_%s_interp_execute" % t: (None, [vp, ti, vp]),
+            "resamp2_%s_execute_block" % t: (None, [vp, i, vp, ull, vp, vp]),
+            "resamp2_%s_execute_block_dev" % t: (None, [vp, i, vp, ull, vp, vp]),
+            "resamp2_%s_set_stream" % t: (None, [vp, vp]),
+            "resamp2_%s_synchronize" % t: (None, [vp]),
+            "msresamp2_%s_create" % t: (vp, [i, u, f, f, f]),
+            "msresamp2_%s_destroy" % t: (None, [vp]),
+            "msresamp2_%s_print" % t: (None, [vp]),
+            "msresamp2_%s_reset" % t: (None, [vp]),
+            "msresamp2_%s_get_delay" % t: (f, [vp]),
+            "msresamp2_%s_execute" % t: (None, [vp, vp, vp]),
+            "msresamp2_%s_execute_block" % t: (None, [vp, vp, ull, vp]),
+            "msresamp2_%s_execute_block_dev" % t: (None, [vp, vp, ull, vp]),
+            "msresamp2_%s_set_stream" % t: (None, [vp, vp]),
+            "msresamp2_%s_synchronize" % t: (None, [vp]),
+            "msresamp_%s_create" % t: (vp, [f, f]),
+            "msresamp_%s_destroy" % t: (None, [vp]),
+            "msresamp_%s_print" % t: (None, [vp]),
+            "msresamp_%s_reset" % t: (None, [vp]),
+            "msresamp_%s_get_delay" % t: (f, [vp]),
+            "msresamp_%s_execute" % t: (None, [vp, vp, u, vp, vp]),
+            "msresamp_%s_num_output" % t: (ull, [vp, ull]),
+            "msresamp_%s_execute_block_dev" % t: (None, [vp, vp, ull, vp, vp]),
+            "msresamp_%s_set_stream" % t: (None, [vp, vp]),
+            "msresamp_%s_synchronize" % t: (None, [vp]),
+        })
     for t in (CRCF, CCCF):
         sig.update({
             "firpfbch_%s_create" % t: (vp, [i, u, u, vp]),
@@ -677,6 +716,112 @@ class Resamp(_Obj):
         ny = C.c_ulonglong(0)
         self._fn("_execute_block_dev")(self.q, dx, nx, dy, C.byref(ny))
         return ny.value
+
+    def synchronize(self):
+        self._fn("_synchronize")(self.q)
+
+
+# ------------------------------------------------------------------ half-band / multi-stage resamplers
+RESAMP2_FILTER, RESAMP2_ANALYZER, RESAMP2_SYNTHESIZER, RESAMP2_DECIM, RESAMP2_INTERP = range(5)
+LIQUID_RESAMP_INTERP, LIQUID_RESAMP_DECIM = 0, 1
+
+
+class Resamp2(_Obj):
+    family = "resamp2_%s"
+    NIN = {0: 1, 1: 2, 2: 2, 3: 2, 4: 1}
+    NOUT = {0: 1, 1: 2, 2: 2, 3: 1, 4: 2}
+
+    def __init__(self, m, f0, As, t=CRCF):
+        self.t = t
+        self.prefix = self.family % t
+        self.q = self._fn("_create")(m, f0, As)
+
+    def clear(self):
+        self._fn("_clear")(self.q)
+
+    def get_delay(self):
+        return self._fn("_get_delay")(self.q)
+
+    def run(self, mode, x):
+        """n consecutive calls of one mode (execute_block extension)."""
+        x = _samples(x, self.t)
+        n = len(x) // self.NIN[mode]
+        y0 = np.zeros(n * self.NOUT[mode], _out_dtype(self.t))
+        y1 = np.zeros(n, _out_dtype(self.t))
+        self._fn("_execute_block")(self.q, mode, ptr(x), n, ptr(y0), ptr(y1))
+        return (y0, y1) if mode == RESAMP2_FILTER else y0
+
+    def call(self, mode, x):
+        """one call of the original per-call API"""
+        if mode == RESAMP2_FILTER:
+            y0, y1 = np.zeros(1, _out_dtype(self.t)), np.zeros(1, _out_dtype(self.t))
+            self._fn("_filter_execute")(self.q, _by_value(x, self.t), ptr(y0), ptr(y1))
+            return y0[0], y1[0]
+        if mode == RESAMP2_INTERP:
+            y = np.zeros(2, _out_dtype(self.t))
+            self._fn("_interp_execute")(self.q, _by_value(x, self.t), ptr(y))
+            return y
+        x = _samples(x, self.t)
+        y = np.zeros(self.NOUT[mode], _out_dtype(self.t))
+        fn = {RESAMP2_ANALYZER: "_analyzer_execute", RESAMP2_SYNTHESIZER: "_synthesizer_execute",
+              RESAMP2_DECIM: "_decim_execute"}[mode]
+        self._fn(fn)(self.q, ptr(x), ptr(y))
+        return y
+
+
+class MsResamp2(_Obj):
+    family = "msresamp2_%s"
+
+    def __init__(self, typ, ns, fc, f0, As, t=CRCF):
+        self.t, self.typ, self.M = t, typ, 1 << ns
+        self.prefix = self.family % t
+        self.q = self._fn("_create")(typ, ns, fc, f0, As)
+
+    def execute_block(self, x):
+        x = _samples(x, self.t)
+        n = len(x) if self.typ == LIQUID_RESAMP_INTERP else len(x) // self.M
+        y = np.zeros(n * self.M if self.typ == LIQUID_RESAMP_INTERP else n, _out_dtype(self.t))
+        self._fn("_execute_block")(self.q, ptr(x), n, ptr(y))
+        return y
+
+    def execute(self, x):
+        x = _samples(x, self.t)
+        y = np.zeros(self.M if self.typ == LIQUID_RESAMP_INTERP else 1, _out_dtype(self.t))
+        self._fn("_execute")(self.q, ptr(x), ptr(y))
+        return y
+
+    def get_delay(self):
+        return self._fn("_get_delay")(self.q)
+
+
+class MsResamp(_Obj):
+    family = "msresamp_%s"
+
+    def __init__(self, rate, As, t=CRCF):
+        self.t = t
+        self.prefix = self.family % t
+        self.q = self._fn("_create")(rate, As)
+
+    def reset(self):
+        self._fn("_reset")(self.q)
+
+    def num_output(self, nx):
+        return int(self._fn("_num_output")(self.q, nx))
+
+    def execute(self, x):
+        x = _samples(x, self.t)
+        y = np.zeros(max(1, self.num_output(len(x))), _out_dtype(self.t))
+        ny = C.c_uint(0)
+        self._fn("_execute")(self.q, ptr(x), len(x), ptr(y), C.byref(ny))
+        return y[:ny.value]
+
+    def execute_block_dev(self, dx, nx, dy):
+        ny = C.c_ulonglong(0)
+        self._fn("_execute_block_dev")(self.q, dx, nx, dy, C.byref(ny))
+        return ny.value
+
+    def get_delay(self):
+        return self._fn("_get_delay")(self.q)
 
     def synchronize(self):
         self._fn("_synchronize")(self.q)

@@ -1054,3 +1054,287 @@ void orc_firpfbch2_execute_block(orc_firpfbch2 q, const orc_cf *x, unsigned int 
     for (unsigned int b = 0; b < nblocks; b++)
         orc_firpfbch2_execute(q, x + (size_t)b * in, y + (size_t)b * out);
 }
+
+
+/* ========================================================================= */
+/* resamp2: src/filter/src/resamp2.c:46-360                                  */
+/* h[i] = sinc(t/2) kaiser(i) mod(t), t = i - 2m, i < 4m+1; the dot product  */
+/* uses the odd taps h1[j] = h[4m-1-2j] against a window of 2m samples; the  */
+/* delay branch reads index m-1 of the other window (:273-356).              */
+/* ========================================================================= */
+struct orc_resamp2_s {
+    int ctaps;
+    unsigned int m;
+    orc_cf *h1;
+    orc_window w0, w1;
+    unsigned int toggle;
+};
+
+orc_resamp2 orc_resamp2_create(int ctaps, unsigned int m, float f0, float As)
+{
+    if (m < 2) orc_fail("resamp2: m must be at least 2");
+    if (f0 < -0.5f || f0 > 0.5f) orc_fail("resamp2: f0 out of range");
+    orc_resamp2 q = (orc_resamp2)orc_calloc(1, sizeof(*q));
+    q->ctaps = ctaps;
+    q->m = m;
+    const unsigned int hl = 4 * m + 1;
+    orc_cf *h = (orc_cf *)orc_calloc(hl, sizeof(orc_cf));
+    const float beta = orc_kaiser_beta_As(As);
+    for (unsigned int i = 0; i < hl; i++) {
+        const float t = (float)i - (float)(hl - 1) / 2.0f;
+        const float a = orc_sincf(t / 2.0f) * orc_kaiser(i, hl, beta, 0);
+        const float c = cosf(2.0f * M_PI * t * f0);
+        h[i] = ctaps ? CMPLXF(a * c, a * sinf(2.0f * M_PI * t * f0)) : CMPLXF(a * c, 0.0f);
+    }
+    q->h1 = (orc_cf *)orc_calloc(2 * m, sizeof(orc_cf));
+    unsigned int j = 0;
+    for (unsigned int i = 1; i < hl; i += 2) q->h1[j++] = h[hl - i - 1];
+    free(h);
+    orc_window_init(&q->w0, 2 * m);
+    orc_window_init(&q->w1, 2 * m);
+    return q;
+}
+
+void orc_resamp2_destroy(orc_resamp2 q)
+{
+    free(q->h1);
+    free(q->w0.v);
+    free(q->w1.v);
+    free(q);
+}
+
+void orc_resamp2_clear(orc_resamp2 q)
+{
+    orc_window_clear(&q->w0);
+    orc_window_clear(&q->w1);
+    q->toggle = 0;
+}
+
+static inline orc_cf orc_r2_dot(orc_resamp2 q, const orc_window *w) { return orc_dot(q->ctaps, q->h1, orc_window_read(w), 2 * q->m); }
+static inline orc_cf orc_r2_delay(orc_resamp2 q, const orc_window *w) { return orc_window_read(w)[q->m - 1]; }
+
+void orc_resamp2_filter_execute(orc_resamp2 q, orc_cf x, orc_cf *y0, orc_cf *y1)
+{
+    orc_cf yi, yq;
+    if (q->toggle == 0) {
+        orc_window_push(&q->w0, x);
+        yi = orc_r2_delay(q, &q->w0);
+        yq = orc_r2_dot(q, &q->w1);
+    } else {
+        orc_window_push(&q->w1, x);
+        yi = orc_r2_delay(q, &q->w1);
+        yq = orc_r2_dot(q, &q->w0);
+    }
+    q->toggle = 1 - q->toggle;
+    *y0 = CMPLXF(0.5f * (crealf(yi) + crealf(yq)), 0.5f * (cimagf(yi) + cimagf(yq)));
+    *y1 = CMPLXF(0.5f * (crealf(yi) - crealf(yq)), 0.5f * (cimagf(yi) - cimagf(yq)));
+}
+
+void orc_resamp2_analyzer_execute(orc_resamp2 q, const orc_cf *x, orc_cf *y)
+{
+    orc_window_push(&q->w1, CMPLXF(0.5f * crealf(x[0]), 0.5f * cimagf(x[0])));
+    const orc_cf y1 = orc_r2_dot(q, &q->w1);
+    orc_window_push(&q->w0, CMPLXF(0.5f * crealf(x[1]), 0.5f * cimagf(x[1])));
+    const orc_cf y0 = orc_r2_delay(q, &q->w0);
+    y[0] = y1 + y0;
+    y[1] = y1 - y0;
+}
+
+void orc_resamp2_synthesizer_execute(orc_resamp2 q, const orc_cf *x, orc_cf *y)
+{
+    orc_window_push(&q->w0, x[0] + x[1]);
+    y[0] = orc_r2_delay(q, &q->w0);
+    orc_window_push(&q->w1, x[0] - x[1]);
+    y[1] = orc_r2_dot(q, &q->w1);
+}
+
+void orc_resamp2_decim_execute(orc_resamp2 q, const orc_cf *x, orc_cf *y)
+{
+    orc_window_push(&q->w1, x[0]);
+    const orc_cf y1 = orc_r2_dot(q, &q->w1);
+    orc_window_push(&q->w0, x[1]);
+    *y = orc_r2_delay(q, &q->w0) + y1;
+}
+
+void orc_resamp2_interp_execute(orc_resamp2 q, orc_cf x, orc_cf *y)
+{
+    orc_window_push(&q->w0, x);
+    y[0] = orc_r2_delay(q, &q->w0);
+    orc_window_push(&q->w1, x);
+    y[1] = orc_r2_dot(q, &q->w1);
+}
+
+/* ========================================================================= */
+/* msresamp2: src/filter/src/msresamp2.c:66-354                              */
+/* ========================================================================= */
+struct orc_msresamp2_s {
+    int type;
+    unsigned int ns, M;
+    float zeta;
+    orc_resamp2 *st;
+    orc_cf *b0, *b1;
+};
+
+/* estimate_req_filter_len (Kaiser), src/filter/src/firdes.c:52-75, 163-176 */
+static unsigned int orc_req_len(float df, float As) { return (unsigned int)((As - 7.95f) / (14.26f * df)); }
+
+orc_msresamp2 orc_msresamp2_create(int ctaps, int type, unsigned int ns, float fc, float f0, float As)
+{
+    if (ns > 16) orc_fail("msresamp2: too many stages");
+    if (fc <= 0.0f || fc >= 0.5f) orc_fail("msresamp2: bad cutoff");
+    if (fc > 0.45f) fc = 0.45f;
+    f0 = 0.0f;                                  /* :109-113: non-zero center frequency unsupported */
+    orc_msresamp2 q = (orc_msresamp2)orc_calloc(1, sizeof(*q));
+    q->type = type == 0 ? 0 : 1;
+    q->ns = ns;
+    q->M = 1u << ns;
+    q->zeta = 1.0f / (float)q->M;
+    q->b0 = (orc_cf *)orc_calloc(q->M, sizeof(orc_cf));
+    q->b1 = (orc_cf *)orc_calloc(q->M, sizeof(orc_cf));
+    q->st = (orc_resamp2 *)orc_calloc(ns ? ns : 1, sizeof(orc_resamp2));
+    for (unsigned int i = 0; i < ns; i++) {     /* :137-150 */
+        f0 = 0.5f * f0;
+        fc = 0.5f * fc;
+        const float ft = (0.5f - fc) / 2.0f;
+        const unsigned int hl = orc_req_len(ft, As);
+        unsigned int m = (unsigned int)ceilf((float)(hl - 1) / 4.0f);
+        q->st[i] = orc_resamp2_create(ctaps, m < 3 ? 3 : m, f0, As);
+    }
+    return q;
+}
+
+void orc_msresamp2_destroy(orc_msresamp2 q)
+{
+    for (unsigned int i = 0; i < q->ns; i++) orc_resamp2_destroy(q->st[i]);
+    free(q->st);
+    free(q->b0);
+    free(q->b1);
+    free(q);
+}
+
+void orc_msresamp2_reset(orc_msresamp2 q)
+{
+    for (unsigned int i = 0; i < q->ns; i++) orc_resamp2_clear(q->st[i]);
+}
+
+void orc_msresamp2_execute(orc_msresamp2 q, const orc_cf *x, orc_cf *y)
+{
+    if (q->ns == 0) {
+        y[0] = x[0];
+        return;
+    }
+    if (q->type == 0) {                         /* :289-318: stages run in reverse order */
+        orc_cf *in = q->b0, *out = q->b1;
+        in[0] = x[0];
+        for (unsigned int s = 0; s < q->ns; s++) {
+            const unsigned int k = 1u << s;
+            if (s == q->ns - 1) out = y;
+            for (unsigned int i = 0; i < k; i++) orc_resamp2_interp_execute(q->st[q->ns - s - 1], in[i], &out[2 * i]);
+            orc_cf *t = in;
+            in = out;
+            out = t;
+        }
+    } else {                                    /* :321-354 */
+        const orc_cf *in = x;
+        orc_cf *out = q->b1, *spare = q->b0;
+        for (unsigned int s = 0; s < q->ns; s++) {
+            const unsigned int k = 1u << (q->ns - s - 1);
+            for (unsigned int i = 0; i < k; i++) orc_resamp2_decim_execute(q->st[s], &in[2 * i], &out[i]);
+            in = out;
+            orc_cf *t = out;
+            out = spare;
+            spare = t;
+        }
+        y[0] = CMPLXF(crealf(in[0]) * q->zeta, cimagf(in[0]) * q->zeta);
+    }
+}
+
+/* ========================================================================= */
+/* msresamp: src/filter/src/msresamp.c:68-349 -- halfband cascade + resamp  */
+/* (m = 7, fc = 0.4, npfb = 64); interp: resamp first, decim: halfbands first */
+/* ========================================================================= */
+struct orc_msresamp_s {
+    int type;                                   /* 0 interp (rate > 1), 1 decim */
+    unsigned int ns, M, bi;
+    orc_msresamp2 hb;
+    orc_resamp rs;
+    orc_cf *buf;
+};
+
+orc_msresamp orc_msresamp_create(float rate, float As)
+{
+    if (rate <= 0.0f) orc_fail("msresamp: rate must be > 0");
+    orc_msresamp q = (orc_msresamp)orc_calloc(1, sizeof(*q));
+    q->type = rate > 1.0f ? 0 : 1;
+    float ra = rate;
+    if (q->type == 0)
+        while (ra > 2.0f) {
+            q->ns++;
+            ra *= 0.5f;
+        }
+    else
+        while (ra < 0.5f) {
+            q->ns++;
+            ra *= 2.0f;
+        }
+    q->M = 1u << q->ns;
+    q->buf = (orc_cf *)orc_calloc(4 + q->M, sizeof(orc_cf));
+    q->hb = orc_msresamp2_create(0, q->type, q->ns, 0.4f, 0.0f, As);
+    q->rs = orc_resamp_create(ra, 7, 0.4f, As, 64);
+    return q;
+}
+
+void orc_msresamp_destroy(orc_msresamp q)
+{
+    orc_msresamp2_destroy(q->hb);
+    orc_resamp_destroy(q->rs);
+    free(q->buf);
+    free(q);
+}
+
+void orc_msresamp_reset(orc_msresamp q)
+{
+    orc_msresamp2_reset(q->hb);
+    orc_resamp_reset(q->rs);
+    q->bi = 0;
+}
+
+void orc_msresamp_execute(orc_msresamp q, const orc_cf *x, unsigned int nx, orc_cf *y, unsigned int *ny)
+{
+    unsigned int n = 0, nw;
+    for (unsigned int i = 0; i < nx; i++) {
+        if (q->type == 0) {
+            orc_resamp_execute_block(q->rs, &x[i], 1, q->buf, &nw);
+            for (unsigned int k = 0; k < nw; k++) {
+                orc_msresamp2_execute(q->hb, &q->buf[k], &y[n]);
+                n += q->M;
+            }
+        } else {
+            q->buf[q->bi++] = x[i];
+            if (q->bi == q->M) {
+                orc_cf h;
+                orc_msresamp2_execute(q->hb, q->buf, &h);
+                orc_resamp_execute_block(q->rs, &h, 1, &y[n], &nw);
+                n += nw;
+                q->bi = 0;
+            }
+        }
+    }
+    *ny = n;
+}
+
+/* n consecutive calls of one resamp2 mode on arrays (test convenience):
+ * mode 0 filter (x[n] -> y0[n], y1[n]), 1 analyzer, 2 synthesizer (x[2n] ->
+ * y0[2n]), 3 decim (x[2n] -> y0[n]), 4 interp (x[n] -> y0[2n]) */
+void orc_resamp2_run(orc_resamp2 q, int mode, const orc_cf *x, unsigned int n, orc_cf *y0, orc_cf *y1)
+{
+    for (unsigned int i = 0; i < n; i++) {
+        switch (mode) {
+        case 0: orc_resamp2_filter_execute(q, x[i], &y0[i], &y1[i]); break;
+        case 1: orc_resamp2_analyzer_execute(q, &x[2 * i], &y0[2 * i]); break;
+        case 2: orc_resamp2_synthesizer_execute(q, &x[2 * i], &y0[2 * i]); break;
+        case 3: orc_resamp2_decim_execute(q, &x[2 * i], &y0[i]); break;
+        default: orc_resamp2_interp_execute(q, x[i], &y0[2 * i]); break;
+        }
+    }
+}

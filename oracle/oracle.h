@@ -129,4 +129,32 @@ void          orc_firpfbch2_execute_block(orc_firpfbch2 q, const orc_cf *x, unsi
 /* prototype used by create_kaiser (firpfbch2.c:135-172): 2*M*m+1 taps */
 void          orc_firpfbch2_prototype(int type, unsigned int M, unsigned int m, float As, float *h);
 
+/* resamp2 (src/filter/src/resamp2.c:46-360): half-band filter/resampler.
+ * ctaps: complex taps (cccf: exp(j 2 pi t f0) modulation), else real (cos). */
+typedef struct orc_resamp2_s *orc_resamp2;
+orc_resamp2   orc_resamp2_create(int ctaps, unsigned int m, float f0, float As);
+void          orc_resamp2_destroy(orc_resamp2 q);
+void          orc_resamp2_clear(orc_resamp2 q);
+void          orc_resamp2_filter_execute(orc_resamp2 q, orc_cf x, orc_cf *y0, orc_cf *y1);
+void          orc_resamp2_analyzer_execute(orc_resamp2 q, const orc_cf *x, orc_cf *y);
+void          orc_resamp2_synthesizer_execute(orc_resamp2 q, const orc_cf *x, orc_cf *y);
+void          orc_resamp2_decim_execute(orc_resamp2 q, const orc_cf *x, orc_cf *y);
+void          orc_resamp2_interp_execute(orc_resamp2 q, orc_cf x, orc_cf *y);
+void          orc_resamp2_run(orc_resamp2 q, int mode, const orc_cf *x, unsigned int n, orc_cf *y0, orc_cf *y1);
+
+/* msresamp2 (src/filter/src/msresamp2.c:66-354): type 0 interp, 1 decim */
+typedef struct orc_msresamp2_s *orc_msresamp2;
+orc_msresamp2 orc_msresamp2_create(int ctaps, int type, unsigned int num_stages, float fc, float f0, float As);
+void          orc_msresamp2_destroy(orc_msresamp2 q);
+void          orc_msresamp2_reset(orc_msresamp2 q);
+/* interp: 1 in, 2^s out; decim: 2^s in, 1 out */
+void          orc_msresamp2_execute(orc_msresamp2 q, const orc_cf *x, orc_cf *y);
+
+/* msresamp (src/filter/src/msresamp.c:68-349) */
+typedef struct orc_msresamp_s *orc_msresamp;
+orc_msresamp  orc_msresamp_create(float rate, float As);
+void          orc_msresamp_destroy(orc_msresamp q);
+void          orc_msresamp_reset(orc_msresamp q);
+void          orc_msresamp_execute(orc_msresamp q, const orc_cf *x, unsigned int nx, orc_cf *y, unsigned int *ny);
+
 #endif

@@ -35,3 +35,75 @@ def nrm_err(y, ref):
     den = np.max(np.abs(ref)) if ref.size else 1.0
     return float(np.max(np.abs(y.astype(np.complex128) - ref.astype(np.complex128))) / (den if den > 0 else 1.0)) \
         if ref.size else 0.0
+
+
+# ------------------------------------------------------------ reference property tests
+# (shared by the oracle and GPU suites: the same checks the reference's autotests make)
+def liquid_kaiser(n, N, beta, mu=0.0):
+    """kaiser(), src/math/src/math.c:289-312 (float64)."""
+    from scipy.special import i0
+    t = n - (N - 1) / 2.0 + mu
+    r = 2.0 * t / N
+    return i0(beta * np.sqrt(np.clip(1 - r * r, 0.0, None))) / i0(beta)
+
+
+def resamp2_analysis_case():
+    """src/filter/tests/resamp2_crcf_autotest.c:27-58: two tones through the
+    analyzer; returns (x, check(y0, y1) -> max error, tol)."""
+    m, n, f0, f1 = 5, 37, 0.0739, -0.1387
+    i = np.arange(2 * n + 2 * m + 1)
+    x = np.where(i < 2 * n, np.exp(1j * f0 * i) + np.exp(1j * (np.pi + f1) * i), 0).astype(np.complex64)
+
+    def check(y0, y1):
+        k = np.arange(m, n - m)
+        d0 = y0[k + m] - np.exp(1j * 2 * f0 * (k + 0.5))
+        d1 = y1[k + m] - np.exp(1j * 2 * f1 * (k + 0.5))
+        return \
+            max(np.max(np.abs(d0.real)), np.max(np.abs(d0.imag)), np.max(np.abs(d1.real)),
+                np.max(np.abs(d1.imag))), 1e-3
+    return m, n, x[:2 * n], check
+
+
+def resamp2_synthesis_case():
+    """src/filter/tests/resamp2_crcf_autotest.c:81-113"""
+    m, n, f0, f1 = 5, 37, 0.0739, -0.1387
+    i = np.arange(n)
+    x = np.empty(2 * n, np.complex64)
+    x[0::2] = np.exp(1j * f0 * i)
+    x[1::2] = np.exp(1j * f1 * i)
+
+    def check(y):
+        k = np.arange(m, n - 2 * m)
+        ref = np.exp(1j * 0.5 * f0 * k) + np.exp(1j * (np.pi + 0.5 * f1) * k)
+        d = y[k + 2 * m] - ref
+        return max(np.max(np.abs(d.real)), np.max(np.abs(d.imag))), 3e-3
+    return m, n, x, check
+
+
+def msresamp_spectral_case():
+    """src/filter/tests/msresamp_crcf_autotest.c:25-100: Kaiser-windowed tone at
+    0.2 r; returns (r, As, x, check(y) -> list of failed conditions)."""
+    m, r, As, n, fx = 13, 0.127115323, 60.0, 1200, 0.0254230646
+    nx = n + m
+    i = np.arange(nx)
+    w = np.where(i < n, liquid_kaiser(i, n, 10.0), 0.0)
+    x = (np.exp(1j * 2 * np.pi * fx * i) * w).astype(np.complex64)
+    wsum = float(np.sum(w))
+
+    def check(y):
+        ny = len(y)
+        fy = fx / r
+        nfft = 1 << int(np.ceil(np.log2(ny)))
+        Y = np.fft.fftshift(np.fft.fft(np.concatenate([y, np.zeros(nfft - ny)])))
+        Y = Y / (r * wsum)
+        f = np.arange(nfft) / nfft - 0.5
+        mag = 20 * np.log10(np.abs(Y) + 1e-30)
+        k = int(np.argmax(mag))
+        side = np.max(mag[np.abs(f - fy) > 0.07])
+        bad = []
+        if abs(ny / nx - r) > 0.01: bad.append("rate %g" % (ny / nx))
+        if abs(mag[k]) > 0.25: bad.append("peak %g dB" % mag[k])
+        if abs(f[k] - fy) > 0.01: bad.append("peak freq %g" % f[k])
+        if side >= -As: bad.append("sidelobe %g dB" % side)
+        return bad
+    return r, As, x, check

@@ -61,6 +61,18 @@ def _declare(L):
         "orc_firinterp_create_kaiser": (vp, [u, u, f]),
         "orc_firinterp_destroy": (None, [vp]),
         "orc_firinterp_execute_block": (None, [vp, vp, u, vp]),
+        "orc_resamp2_create": (vp, [i, u, f, f]),
+        "orc_resamp2_destroy": (None, [vp]),
+        "orc_resamp2_clear": (None, [vp]),
+        "orc_resamp2_run": (None, [vp, i, vp, u, vp, vp]),
+        "orc_msresamp2_create": (vp, [i, i, u, f, f, f]),
+        "orc_msresamp2_destroy": (None, [vp]),
+        "orc_msresamp2_reset": (None, [vp]),
+        "orc_msresamp2_execute": (None, [vp, vp, vp]),
+        "orc_msresamp_create": (vp, [f, f]),
+        "orc_msresamp_destroy": (None, [vp]),
+        "orc_msresamp_reset": (None, [vp]),
+        "orc_msresamp_execute": (None, [vp, vp, u, vp, C.POINTER(C.c_uint)]),
         "orc_resamp_create": (vp, [f, u, f, f, u]),
         "orc_resamp_destroy": (None, [vp]),
         "orc_resamp_reset": (None, [vp]),
@@ -273,6 +285,66 @@ class Resamp(_Obj):
         ny = C.c_uint(0)
         lib().orc_resamp_execute_block(self.q, ptr(x), len(x), ptr(y), C.byref(ny))
         return y[: ny.value]
+
+
+class Resamp2(_Obj):
+    """resamp2 (resamp2.c:46-360); ctaps: complex taps (cccf)."""
+    _destroy = "orc_resamp2_destroy"
+    NIN = {0: 1, 1: 2, 2: 2, 3: 2, 4: 1}
+    NOUT = {0: 1, 1: 2, 2: 2, 3: 1, 4: 2}
+
+    def __init__(self, m, f0, As, ctaps=False):
+        self.q = lib().orc_resamp2_create(int(ctaps), m, f0, As)
+
+    def clear(self):
+        lib().orc_resamp2_clear(self.q)
+
+    def run(self, mode, x):
+        x = _arr(x, CRCF)
+        n = len(x) // self.NIN[mode]
+        y0 = np.zeros(n * self.NOUT[mode], np.complex64)
+        y1 = np.zeros(n, np.complex64)
+        lib().orc_resamp2_run(self.q, mode, ptr(x), n, ptr(y0), ptr(y1))
+        return (y0, y1) if mode == 0 else y0
+
+
+class MsResamp2(_Obj):
+    _destroy = "orc_msresamp2_destroy"
+
+    def __init__(self, typ, ns, fc, f0, As, ctaps=False):
+        self.typ, self.M = typ, 1 << ns
+        self.q = lib().orc_msresamp2_create(int(ctaps), typ, ns, fc, f0, As)
+
+    def execute_block(self, x):
+        x = _arr(x, CRCF)
+        if self.typ == 0:
+            y = np.zeros(len(x) * self.M, np.complex64)
+            for i in range(len(x)):
+                lib().orc_msresamp2_execute(self.q, ptr(x[i:i + 1]), ptr(y[i * self.M:]))
+        else:
+            n = len(x) // self.M
+            y = np.zeros(n, np.complex64)
+            for i in range(n):
+                lib().orc_msresamp2_execute(self.q, ptr(x[i * self.M:(i + 1) * self.M]), ptr(y[i:]))
+        return y
+
+
+class MsResamp(_Obj):
+    _destroy = "orc_msresamp_destroy"
+
+    def __init__(self, rate, As):
+        self.rate = rate
+        self.q = lib().orc_msresamp_create(rate, As)
+
+    def reset(self):
+        lib().orc_msresamp_reset(self.q)
+
+    def execute(self, x):
+        x = _arr(x, CRCF)
+        y = np.zeros(int(np.ceil(len(x) * self.rate)) + 64, np.complex64)
+        ny = C.c_uint(0)
+        lib().orc_msresamp_execute(self.q, ptr(x), len(x), ptr(y), C.byref(ny))
+        return y[:ny.value]
 
 
 def resamp_schedule(rate, npfb, nx):

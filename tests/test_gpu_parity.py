@@ -593,3 +593,141 @@ def test_reference_examples_run(exe, tmp_path):
     print(res.stdout[-2000:], res.stderr[-2000:])
     assert res.returncode == 0
     assert "error" not in res.stderr.lower()
+
+
+# ------------------------------------------------------------ resamp2 / msresamp2 / msresamp
+def _as_oracle_in(x):
+    return x.astype(np.complex64)
+
+
+def _cmp_typed(y, ref, t):
+    if t == "rrrf":
+        assert y.dtype == np.float32
+        ref = ref.real
+    assert G.nrm_err(y, ref) < NRM
+
+
+@pytest.mark.parametrize("t", ["rrrf", "crcf", "cccf"])
+@pytest.mark.parametrize("mode", [0, 1, 2, 3, 4])
+@pytest.mark.parametrize("m,f0", [(5, 0.0), (12, 0.13), (2, -0.2)])
+def test_resamp2_modes_vs_oracle(t, mode, m, f0):
+    r = rng(m * 10 + mode)
+    nin = LQ.Resamp2.NIN[mode]
+    ncalls = 2000
+    x = samples(r, t, ncalls * nin)
+    g = LQ.Resamp2(m, f0, 60.0, t=t)
+    o = O.Resamp2(m, f0, 60.0, ctaps=(t == "cccf"))
+    # ragged: single per-call API calls, then blocks of odd sizes (toggle parity)
+    cuts = [0, 1, 2, 3, 700, 701, 1500, ncalls]
+    ys0, ys1 = [], []
+    for a, b in zip(cuts[:-1], cuts[1:]):
+        xa = x[a * nin:b * nin]
+        if b - a == 1:
+            res = g.call(mode, xa[0] if nin == 1 else xa)
+            if mode == 0:
+                ys0.append(np.array([res[0]]))
+                ys1.append(np.array([res[1]]))
+            else:
+                ys0.append(res)
+        else:
+            res = g.run(mode, xa)
+            if mode == 0:
+                ys0.append(res[0])
+                ys1.append(res[1])
+            else:
+                ys0.append(res)
+    ref = o.run(mode, _as_oracle_in(x))
+    if mode == 0:
+        _cmp_typed(np.concatenate(ys0), ref[0], t)
+        _cmp_typed(np.concatenate(ys1), ref[1], t)
+    else:
+        _cmp_typed(np.concatenate(ys0), ref, t)
+
+
+def test_resamp2_mixed_modes_share_windows():
+    # the reference's modes push into the same two windows; switching modes on
+    # one object continues from that shared state
+    r = rng(99)
+    g = LQ.Resamp2(6, 0.0, 60.0)
+    o = O.Resamp2(6, 0.0, 60.0)
+    for mode, n in [(0, 37), (3, 50), (4, 21), (1, 40), (0, 3), (2, 64), (0, 11)]:
+        x = cx(r, n * LQ.Resamp2.NIN[mode])
+        a, b = g.run(mode, x), o.run(mode, x)
+        if mode == 0:
+            assert G.nrm_err(a[0], b[0]) < NRM and G.nrm_err(a[1], b[1]) < NRM
+        else:
+            assert G.nrm_err(a, b) < NRM
+    g.clear()
+    o.clear()
+    x = cx(r, 64)
+    assert G.nrm_err(g.run(3, x), o.run(3, x)) < NRM
+
+
+def test_resamp2_reference_analysis_synthesis_gpu():
+    m, n, x, check = G.resamp2_analysis_case()
+    g = LQ.Resamp2(m, 0.0, 60.0)
+    y = np.concatenate([g.call(LQ.RESAMP2_ANALYZER, x[2 * i:2 * i + 2]) for i in range(n)])
+    err, tol = check(y[0::2], y[1::2])
+    assert err < tol
+    m, n, x, check = G.resamp2_synthesis_case()
+    y = LQ.Resamp2(m, 0.0, 60.0).run(LQ.RESAMP2_SYNTHESIZER, x)
+    err, tol = check(y)
+    assert err < tol
+
+
+@pytest.mark.parametrize("t", ["rrrf", "crcf", "cccf"])
+@pytest.mark.parametrize("typ", [0, 1])
+@pytest.mark.parametrize("ns", [0, 1, 3])
+def test_msresamp2_vs_oracle(t, typ, ns):
+    r = rng(ns * 7 + typ)
+    M = 1 << ns
+    ncalls = 300
+    x = samples(r, t, ncalls * (1 if typ == 0 else M))
+    g = LQ.MsResamp2(typ, ns, 0.4, 0.0, 60.0, t=t)
+    o = O.MsResamp2(typ, ns, 0.4, 0.0, 60.0)
+    step = 1 if typ == 0 else M
+    y = np.concatenate([g.execute(x[:step]), g.execute_block(x[step:100 * step]), g.execute_block(x[100 * step:])])
+    _cmp_typed(y, o.execute_block(_as_oracle_in(x)), t)
+
+
+@pytest.mark.parametrize("t", ["rrrf", "crcf", "cccf"])
+@pytest.mark.parametrize("rate", [0.127115323, 0.3, 0.77, 1.0, 1.7, 3.3, 10.5])
+def test_msresamp_vs_oracle(t, rate):
+    r = rng(int(rate * 1000))
+    rate = float(np.float32(rate))
+    x = samples(r, t, 20_000)
+    g = LQ.MsResamp(rate, 60.0, t=t)
+    o = O.MsResamp(rate, 60.0)
+    cuts = [0, 1, 2, 3, 5, 333, 4000, 4001, 20_000]
+    y = np.concatenate([g.execute(x[a:b]) for a, b in zip(cuts[:-1], cuts[1:])])
+    ref = o.execute(_as_oracle_in(x))
+    assert len(y) == len(ref)
+    _cmp_typed(y, ref, t)
+    assert abs(g.get_delay() - LQ.MsResamp(rate, 60.0, t=t).get_delay()) == 0
+
+
+def test_msresamp_reference_spectral_gpu():
+    r, As, x, check = G.msresamp_spectral_case()
+    g = LQ.MsResamp(r, As)
+    y = np.concatenate([g.execute(x[i:i + 1]) for i in range(len(x))])
+    assert check(y) == []
+
+
+def test_msresamp_device_long_stream():
+    # 4M samples device-resident through a 1/8.3 decimating chain
+    n = 1 << 22
+    r = rng(123)
+    x = cx(r, n)
+    rate = float(np.float32(1 / 8.3))
+    g = LQ.MsResamp(rate, 60.0)
+    o = O.MsResamp(rate, 60.0)
+    nout = g.num_output(n)
+    dx = LQ.DeviceBuffer.from_array(x)
+    dy = LQ.DeviceBuffer(max(1, nout) * 8)
+    ny = g.execute_block_dev(dx.p, n, dy.p)
+    g.synchronize()
+    assert ny == nout
+    y = dy.to_array(np.complex64, ny)
+    ref = o.execute(x)
+    assert len(ref) == ny
+    assert G.nrm_err(y, ref) < NRM

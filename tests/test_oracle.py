@@ -290,3 +290,54 @@ def test_resamp_spectral():
     amp = np.abs(t)
     assert abs(np.mean(amp) - 1.0) < 0.01
     assert abs(len(y) / n - 0.9) < 0.01
+
+
+# ------------------------------------------------------------ resamp2 / msresamp (reference autotests)
+def test_resamp2_analysis_reference():
+    m, n, x, check = G.resamp2_analysis_case()
+    q = O.Resamp2(m, 0.0, 60.0)
+    y = q.run(1, x)
+    err, tol = check(y[0::2], y[1::2])
+    assert err < tol
+
+
+def test_resamp2_synthesis_reference():
+    m, n, x, check = G.resamp2_synthesis_case()
+    y = O.Resamp2(m, 0.0, 60.0).run(2, x)
+    err, tol = check(y)
+    assert err < tol
+
+
+def test_resamp2_modes_closed_form():
+    # every mode is a convolution with the half-band h (resamp2.c:62-99):
+    # interp y[2n] = x[n-m], y[2n+1] = sum_l h[2l+1] x[n-l]; the filter mode's
+    # low band is 0.5 (x[i-2m] + sum_l h[2l+1] x[i-1-2l])
+    m, As = 4, 60.0
+    hl = 4 * m + 1
+    t = np.arange(hl) - 2 * m
+    from scipy.special import i0
+    beta = 0.1102 * (As - 8.7)
+    h = np.sinc(t / 2.0) * G.liquid_kaiser(np.arange(hl), hl, beta)
+    r = _rng(8)
+    x = _cx(r, 300).astype(np.complex128)
+    q = O.Resamp2(m, 0.0, As)
+    y = q.run(4, x.astype(np.complex64))
+    xp = np.concatenate([np.zeros(2 * m), x])
+    ref = np.empty(600, complex)
+    for k in range(300):
+        ref[2 * k] = xp[2 * m + k - m]
+        ref[2 * k + 1] = sum(h[2 * l + 1] * xp[2 * m + k - l] for l in range(2 * m))
+    assert np.max(np.abs(y - ref)) < 1e-5 * np.max(np.abs(ref))
+    q2 = O.Resamp2(m, 0.0, As)
+    y0, y1 = q2.run(0, x.astype(np.complex64))
+    xp = np.concatenate([np.zeros(4 * m), x])
+    lo = np.array([0.5 * (xp[4 * m + i - 2 * m] + sum(h[2 * l + 1] * xp[4 * m + i - 1 - 2 * l] for l in range(2 * m)))
+                   for i in range(300)])
+    assert np.max(np.abs(y0 - lo)) < 1e-5 * np.max(np.abs(lo))
+
+
+def test_msresamp_spectral_reference():
+    r, As, x, check = G.msresamp_spectral_case()
+    q = O.MsResamp(r, As)
+    y = np.concatenate([q.execute(x[i:i + 1]) for i in range(len(x))])
+    assert check(y) == []
