@@ -118,8 +118,14 @@ float liquid_filter_autocorr(float *_h, unsigned int _h_len, int _lag);
 void liquid_filter_isi(float *_h, unsigned int _k, unsigned int _m, float *_rms, float *_max);
 /* liquid.h:4396 */
 float liquid_Qf(float _z);
-/* liquid.h:4445 */
+/* windows, liquid.h:4425-4465 */
+float kaiser(unsigned int _n, unsigned int _N, float _beta, float _mu);
 float hamming(unsigned int _n, unsigned int _N);
+float hann(unsigned int _n, unsigned int _N);
+float blackmanharris(unsigned int _n, unsigned int _N);
+float liquid_rcostaper_windowf(unsigned int _n, unsigned int _t, unsigned int _N);
+float liquid_kbd(unsigned int _n, unsigned int _N, float _beta);
+void liquid_kbd_window(unsigned int _n, float _beta, float *_w);
 
 /* ------------------------------------------------------------------------ */
 /* random helpers (liquid.h:6301-6315): test-signal generation on the host   */
@@ -282,6 +288,67 @@ LQMI_FIRPFB_API(firpfb_cccf, liquid_float_complex, liquid_float_complex, liquid_
 LQMI_RESAMP_API(resamp_rrrf, float)
 LQMI_RESAMP_API(resamp_crcf, liquid_float_complex)
 LQMI_RESAMP_API(resamp_cccf, liquid_float_complex)
+
+/* ------------------------------------------------------------------------ */
+/* fft (liquid.h:1113-1216): plans bind host arrays; the transform runs on   */
+/* the GPU.  liquid_nextpow2: liquid.h (math), src/math/src/math.c:143       */
+/* ------------------------------------------------------------------------ */
+typedef enum {
+    LIQUID_FFT_UNKNOWN = 0,
+    LIQUID_FFT_FORWARD = +1,
+    LIQUID_FFT_BACKWARD = -1,
+    LIQUID_FFT_REDFT00 = 10,
+    LIQUID_FFT_REDFT10 = 11,
+    LIQUID_FFT_REDFT01 = 12,
+    LIQUID_FFT_REDFT11 = 13,
+    LIQUID_FFT_RODFT00 = 20,
+    LIQUID_FFT_RODFT10 = 21,
+    LIQUID_FFT_RODFT01 = 22,
+    LIQUID_FFT_RODFT11 = 23,
+    LIQUID_FFT_MDCT = 30,
+    LIQUID_FFT_IMDCT = 31,
+} liquid_fft_type;
+typedef struct fftplan_s *fftplan;
+fftplan fft_create_plan(unsigned int _n, liquid_float_complex *_x, liquid_float_complex *_y, int _dir, int _flags);
+fftplan fft_create_plan_r2r_1d(unsigned int _n, float *_x, float *_y, int _type, int _flags);
+void fft_destroy_plan(fftplan _p);
+void fft_print_plan(fftplan _p);
+void fft_execute(fftplan _p);
+void fft_run(unsigned int _n, liquid_float_complex *_x, liquid_float_complex *_y, int _dir, int _flags);
+void fft_r2r_1d_run(unsigned int _n, float *_x, float *_y, int _type, int _flags);
+void fft_shift(liquid_float_complex *_x, unsigned int _n);
+unsigned int liquid_nextpow2(unsigned int _x);
+/* extension: _batch transforms of the plan's size/direction (contiguous);
+ * host arrays or device pointers (asynchronous on the plan's stream) */
+void fft_execute_batch(fftplan _p, const void *_x, void *_y, unsigned long long _batch);
+void fft_execute_batch_dev(fftplan _p, const void *_dx, void *_dy, unsigned long long _batch);
+void fft_set_stream(fftplan _p, void *_hip_stream);
+
+/* ------------------------------------------------------------------------ */
+/* spgram (liquid.h:1220-1290): spgramcf (complex in), spgramf (real in)     */
+/* ------------------------------------------------------------------------ */
+#define LQMI_SPGRAM_API(SPGRAM, TI)                                                                 \
+    typedef struct SPGRAM##_s *SPGRAM;                                                              \
+    SPGRAM SPGRAM##_create(unsigned int _nfft, float *_window, unsigned int _window_len);          \
+    SPGRAM SPGRAM##_create_kaiser(unsigned int _nfft, unsigned int _window_len, float _beta);      \
+    SPGRAM SPGRAM##_create_default(unsigned int _nfft);                                             \
+    void SPGRAM##_destroy(SPGRAM _q);                                                               \
+    void SPGRAM##_reset(SPGRAM _q);                                                                 \
+    void SPGRAM##_push(SPGRAM _q, TI _x);                                                           \
+    void SPGRAM##_write(SPGRAM _q, TI *_x, unsigned int _n);                                        \
+    void SPGRAM##_execute(SPGRAM _q, liquid_float_complex *_X);                                     \
+    void SPGRAM##_execute_psd(SPGRAM _q, float *_X);                                                \
+    void SPGRAM##_accumulate_psd(SPGRAM _q, TI *_x, float _alpha, unsigned int _n);                 \
+    void SPGRAM##_write_accumulation(SPGRAM _q, float *_x);                                         \
+    void SPGRAM##_estimate_psd(SPGRAM _q, TI *_x, unsigned int _n, float *_psd);                    \
+    /* extensions: device-resident input (and psd output), asynchronous */                          \
+    void SPGRAM##_accumulate_psd_dev(SPGRAM _q, const TI *_dx, float _alpha, unsigned long long _n); \
+    void SPGRAM##_estimate_psd_dev(SPGRAM _q, const TI *_dx, unsigned long long _n, float *_dpsd);  \
+    void SPGRAM##_set_stream(SPGRAM _q, void *_hip_stream);                                         \
+    void SPGRAM##_synchronize(SPGRAM _q);
+
+LQMI_SPGRAM_API(spgramcf, liquid_float_complex)
+LQMI_SPGRAM_API(spgramf, float)
 
 /* ------------------------------------------------------------------------ */
 /* resamp2 (liquid.h:2840-2925), msresamp2 (:3027-3090), msresamp (:3094-3140) */

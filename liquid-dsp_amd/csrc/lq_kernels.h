@@ -143,6 +143,31 @@ void lqk_resamp(int real_io, const lqk_rs_plan *pl, unsigned long long g0, unsig
 void lqk_firpfb_single(int kind, const void *hpoly, unsigned int L, unsigned int i, const void *win,
                        float scale_re, float scale_im, void *y, void *stream);
 
+/* ---------------------------------------------------------------- FFT of any size (csrc/k_fft.hip)
+ * batch transforms of n points (complex, contiguous), dir +1 forward / -1
+ * backward, unnormalised; x may alias y.  work: lqk_fft_work_bytes(n, batch)
+ * bytes of device scratch (NULL when 0). */
+size_t lqk_fft_work_bytes(unsigned int n, unsigned long long batch);
+void lqk_fft_any(unsigned int n, int dir, const void *x, void *y, unsigned long long batch, void *work,
+                 void *stream);
+/* real-to-real (fft_r2r_1d.c): type codes as liquid_fft_type (10-13 DCT, 20-23 DST); x must not alias y */
+enum {
+    LQK_R2R_REDFT00 = 10, LQK_R2R_REDFT10 = 11, LQK_R2R_REDFT01 = 12, LQK_R2R_REDFT11 = 13,
+    LQK_R2R_RODFT00 = 20, LQK_R2R_RODFT10 = 21, LQK_R2R_RODFT01 = 22, LQK_R2R_RODFT11 = 23,
+};
+void lqk_fft_r2r(int type, unsigned int n, const void *x, void *y, unsigned long long batch, void *stream);
+
+/* ---------------------------------------------------------------- spgram (csrc/k_spgram.hip)
+ * gather: out[t][i] = ext[ends[t]+1+i] w[i] (i < W, zero to nfft), ext = hist(W) ++ x;
+ * accumulate: psd = (1-a) psd + a |X_t|^2 in t order; sum: acc[shift(k)] += sum_t |X_t[k]|^2;
+ * db: mode 0 10log10(|X|^2+1e-16) shifted, 1 10log10(v) shifted, 2 10log10(v/T) */
+void lqk_spgram_gather(int real_in, const void *hist, unsigned int W, const void *x, const long long *ends,
+                       unsigned long long T, const float *w, unsigned int nfft, void *out, void *stream);
+void lqk_spgram_accumulate(const void *X, unsigned long long T, unsigned int nfft, float alpha, float *psd,
+                           void *stream);
+void lqk_spgram_sum(const void *X, unsigned long long T, unsigned int nfft, float *acc, void *stream);
+void lqk_spgram_db(int mode, const void *X, const float *v, unsigned int nfft, float T, float *out, void *stream);
+
 /* ---------------------------------------------------------------- resamp2 (half-band)
  * n calls of one resamp2 mode (src/filter/src/resamp2.c:273-356).  hist0/hist1 =
  * the two 2m-sample windows (oldest first); the updated windows go to

@@ -78,3 +78,63 @@ void cawgn(liquid_float_complex *_x, float _nstd)
     crandnf(&y);
     *_x += y * _nstd * 0.707106781186547f;
 }
+
+/* ------------------------------------------------------------------ windows
+ * src/math/src/math.c:198-360 */
+float kaiser(unsigned int _n, unsigned int _N, float _beta, float _mu)
+{
+    if (_n > _N) LQ_FAIL("error: kaiser(), sample index must not exceed window length\n");
+    if (_beta < 0) LQ_FAIL("error: kaiser(), beta must be greater than or equal to zero\n");
+    if (_mu < -0.5 || _mu > 0.5) LQ_FAIL("error: kaiser(), fractional sample offset must be in [-0.5,0.5]\n");
+    return lq_kaiser_window(_n, _N, _beta, _mu);
+}
+
+float hann(unsigned int _n, unsigned int _N) { return 0.5f - 0.5f * cosf((2 * M_PI * (float)_n) / ((float)(_N - 1))); }
+
+float blackmanharris(unsigned int _n, unsigned int _N)
+{
+    const float t = 2 * M_PI * (float)_n / ((float)(_N - 1));
+    return 0.35875f - 0.48829f * cosf(t) + 0.14128f * cosf(2 * t) - 0.01168f * cosf(3 * t);
+}
+
+float liquid_rcostaper_windowf(unsigned int _n, unsigned int _t, unsigned int _N)
+{
+    if (_n > _N) LQ_FAIL("error: liquid_rcostaper_windowf(), sample index must not exceed window length\n");
+    if (_t > _N / 2) LQ_FAIL("error: liquid_rcostaper_windowf(), taper length cannot exceed half window length\n");
+    if (_n > _N - _t - 1) _n = _N - _n - 1;   /* symmetric taper */
+    return (_n < _t) ? 0.5f - 0.5f * cosf(M_PI * ((float)_n + 0.5f) / (float)_t) : 1.0f;
+}
+
+/* Kaiser-Bessel derived window: cumulative sums of a Kaiser window of M+1 */
+float liquid_kbd(unsigned int _n, unsigned int _N, float _beta)
+{
+    if (_n >= _N) LQ_FAIL("error: liquid_kbd(), index exceeds maximum\n");
+    if (_N == 0) LQ_FAIL("error: liquid_kbd(), window length must be greater than zero\n");
+    if (_N % 2) LQ_FAIL("error: liquid_kbd(), window length must be odd\n");
+    const unsigned int M = _N / 2;
+    if (_n >= M) return liquid_kbd(_N - _n - 1, _N, _beta);
+    float w0 = 0.0f, w1 = 0.0f;
+    for (unsigned int i = 0; i <= M; i++) {
+        const float w = kaiser(i, M + 1, _beta, 0.0f);
+        w1 += w;
+        if (i <= _n) w0 += w;
+    }
+    return sqrtf(w0 / w1);
+}
+
+void liquid_kbd_window(unsigned int _n, float _beta, float *_w)
+{
+    if (_n == 0) LQ_FAIL("error: liquid_kbd_window(), window length must be greater than zero\n");
+    if (_n % 2) LQ_FAIL("error: liquid_kbd_window(), window length must be odd\n");
+    if (_beta < 0.0f) LQ_FAIL("error: liquid_kbd_window(), _beta must be positive\n");
+    const unsigned int M = _n / 2;
+    float *wk = (float *)lq_xmalloc((M + 1) * sizeof(float));
+    float sum = 0.0f, acc = 0.0f;
+    for (unsigned int i = 0; i <= M; i++) sum += (wk[i] = kaiser(i, M + 1, _beta, 0.0f));
+    for (unsigned int i = 0; i < M; i++) {
+        acc += wk[i];
+        _w[i] = sqrtf(acc / sum);
+    }
+    for (unsigned int i = 0; i < M; i++) _w[_n - i - 1] = _w[i];
+    free(wk);
+}

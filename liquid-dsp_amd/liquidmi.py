@@ -204,6 +204,25 @@ def _declare(L):
             "msresamp_%s_set_stream" % t: (None, [vp, vp]),
             "msresamp_%s_synchronize" % t: (None, [vp]),
         })
+    for t, ti in (("spgramcf", cfloat), ("spgramf", f)):
+        sig.update({
+            t + "_create": (vp, [u, vp, u]),
+            t + "_create_kaiser": (vp, [u, u, f]),
+            t + "_create_default": (vp, [u]),
+            t + "_destroy": (None, [vp]),
+            t + "_reset": (None, [vp]),
+            t + "_push": (None, [vp, ti]),
+            t + "_write": (None, [vp, vp, u]),
+            t + "_execute": (None, [vp, vp]),
+            t + "_execute_psd": (None, [vp, vp]),
+            t + "_accumulate_psd": (None, [vp, vp, f, u]),
+            t + "_write_accumulation": (None, [vp, vp]),
+            t + "_estimate_psd": (None, [vp, vp, u, vp]),
+            t + "_accumulate_psd_dev": (None, [vp, vp, f, ull]),
+            t + "_estimate_psd_dev": (None, [vp, vp, ull, vp]),
+            t + "_set_stream": (None, [vp, vp]),
+            t + "_synchronize": (None, [vp]),
+        })
     for t in (CRCF, CCCF):
         sig.update({
             "firpfbch_%s_create" % t: (vp, [i, u, u, vp]),
@@ -229,6 +248,24 @@ def _declare(L):
         "liquid_mi355x_memcpy_h2d": (None, [vp, vp, ull]),
         "liquid_mi355x_memcpy_d2h": (None, [vp, vp, ull]),
         "liquid_mi355x_device_synchronize": (None, []),
+        "kaiser": (f, [u, u, f, f]),
+        "hann": (f, [u, u]),
+        "blackmanharris": (f, [u, u]),
+        "liquid_rcostaper_windowf": (f, [u, u, u]),
+        "liquid_kbd": (f, [u, u, f]),
+        "liquid_kbd_window": (None, [u, f, vp]),
+        "fft_create_plan": (vp, [u, vp, vp, i, i]),
+        "fft_create_plan_r2r_1d": (vp, [u, vp, vp, i, i]),
+        "fft_destroy_plan": (None, [vp]),
+        "fft_print_plan": (None, [vp]),
+        "fft_execute": (None, [vp]),
+        "fft_run": (None, [u, vp, vp, i, i]),
+        "fft_r2r_1d_run": (None, [u, vp, vp, i, i]),
+        "fft_shift": (None, [vp, u]),
+        "liquid_nextpow2": (u, [u]),
+        "fft_execute_batch": (None, [vp, vp, vp, ull]),
+        "fft_execute_batch_dev": (None, [vp, vp, vp, ull]),
+        "fft_set_stream": (None, [vp, vp]),
         "liquid_firdes_prototype": (None, [i, u, u, f, f, vp]),
         "liquid_getopt_str2firfilt": (i, [C.c_char_p]),
         "estimate_req_filter_len": (u, [f, f]),
@@ -825,3 +862,90 @@ class MsResamp(_Obj):
 
     def synchronize(self):
         self._fn("_synchronize")(self.q)
+
+
+# ------------------------------------------------------------------ FFT plan API (liquid.h:1113-1216)
+def fft_run(x, direction=+1):
+    x = np.ascontiguousarray(x, np.complex64)
+    y = np.zeros_like(x)
+    lib().fft_run(len(x), ptr(x), ptr(y), direction, 0)
+    return y
+
+
+def fft_r2r(x, typ):
+    x = np.ascontiguousarray(x, np.float32)
+    y = np.zeros_like(x)
+    lib().fft_r2r_1d_run(len(x), ptr(x), ptr(y), typ, 0)
+    return y
+
+
+def fft_batch(X, direction=+1):
+    """fft_execute_batch over the rows of X (host arrays)."""
+    X = np.ascontiguousarray(X, np.complex64)
+    b, n = X.shape
+    Y = np.zeros_like(X)
+    p = lib().fft_create_plan(n, None, None, direction, 0)
+    try:
+        lib().fft_execute_batch(p, ptr(X), ptr(Y), b)
+    finally:
+        lib().fft_destroy_plan(p)
+    return Y
+
+
+def fft_shift(x):
+    x = np.array(x, np.complex64)
+    lib().fft_shift(ptr(x), len(x))
+    return x
+
+
+
+# ------------------------------------------------------------------ spectral periodogram (liquid.h:1220-1290)
+class Spgram(_Obj):
+    def __init__(self, nfft, window=None, real_in=False, default=False, kaiser=None):
+        self.nfft, self.real_in = nfft, real_in
+        self.prefix = "spgramf" if real_in else "spgramcf"
+        if default:
+            self.q = self._fn("_create_default")(nfft)
+        elif kaiser is not None:               # (window_len, beta)
+            self.q = self._fn("_create_kaiser")(nfft, kaiser[0], kaiser[1])
+        else:
+            self._w = np.ascontiguousarray(window, np.float32)
+            self.q = self._fn("_create")(nfft, ptr(self._w), len(self._w))
+
+    def _x(self, x):
+        return np.ascontiguousarray(x, np.float32 if self.real_in else np.complex64)
+
+    def reset(self):
+        self._fn("_reset")(self.q)
+
+    def push(self, v):
+        self._fn("_push")(self.q, float(np.real(v)) if self.real_in else _by_value(v, CRCF))
+
+    def write(self, x):
+        x = self._x(x)
+        self._fn("_write")(self.q, ptr(x), len(x))
+
+    def execute(self):
+        X = np.zeros(self.nfft, np.complex64)
+        self._fn("_execute")(self.q, ptr(X))
+        return X
+
+    def execute_psd(self):
+        X = np.zeros(self.nfft, np.float32)
+        self._fn("_execute_psd")(self.q, ptr(X))
+        return X
+
+    def accumulate_psd(self, x, alpha):
+        x = self._x(x)
+        self._fn("_accumulate_psd")(self.q, ptr(x), alpha, len(x))
+
+    def write_accumulation(self):
+        X = np.zeros(self.nfft, np.float32)
+        self._fn("_write_accumulation")(self.q, ptr(X))
+        return X
+
+    def estimate_psd(self, x):
+        x = self._x(x)
+        X = np.zeros(self.nfft, np.float32)
+        self._fn("_estimate_psd")(self.q, ptr(x), len(x), ptr(X))
+        return X

@@ -1338,3 +1338,118 @@ void orc_resamp2_run(orc_resamp2 q, int mode, const orc_cf *x, unsigned int n, o
         }
     }
 }
+
+/* ========================================================================= */
+/* spgram: src/fft/src/spgram.c:41-286 (complex or real input)              */
+/* ========================================================================= */
+struct orc_spgram_s {
+    int real_in;
+    unsigned int nfft, W, sc, nt;
+    float *w, *psd;
+    orc_window buf;
+    orc_cf *x, *X;
+};
+
+orc_spgram orc_spgram_create(int real_in, unsigned int nfft, const float *window, unsigned int W)
+{
+    if (nfft < 2 || W > nfft || W == 0) orc_fail("spgram: bad sizes");
+    orc_spgram q = (orc_spgram)orc_calloc(1, sizeof(*q));
+    q->real_in = real_in;
+    q->nfft = nfft;
+    q->W = W;
+    q->w = (float *)orc_calloc(W, sizeof(float));
+    q->psd = (float *)orc_calloc(nfft, sizeof(float));
+    q->x = (orc_cf *)orc_calloc(nfft, sizeof(orc_cf));
+    q->X = (orc_cf *)orc_calloc(nfft, sizeof(orc_cf));
+    float g = 0.0f;
+    for (unsigned int i = 0; i < W; i++) g += window[i] * window[i];
+    g = (float)1.41421356237309504880 / (sqrtf(g / W) * sqrtf((float)nfft));   /* M_SQRT2 */
+    for (unsigned int i = 0; i < W; i++) q->w[i] = g * window[i];
+    orc_window_init(&q->buf, W);
+    orc_spgram_reset(q);
+    return q;
+}
+
+void orc_spgram_destroy(orc_spgram q)
+{
+    free(q->w);
+    free(q->psd);
+    free(q->x);
+    free(q->X);
+    free(q->buf.v);
+    free(q);
+}
+
+void orc_spgram_reset(orc_spgram q)
+{
+    orc_window_clear(&q->buf);
+    memset(q->x, 0, q->nfft * sizeof(orc_cf));
+    q->nt = 0;
+    q->sc = 0;
+    for (unsigned int i = 0; i < q->nfft; i++) q->psd[i] = 1;
+}
+
+static orc_cf orc_spg_in(orc_spgram q, const void *x, unsigned int i)
+{
+    return q->real_in ? CMPLXF(((const float *)x)[i], 0.0f) : ((const orc_cf *)x)[i];
+}
+
+void orc_spgram_write(orc_spgram q, const void *x, unsigned int n)
+{
+    for (unsigned int i = 0; i < n; i++) orc_window_push(&q->buf, orc_spg_in(q, x, i));
+}
+
+void orc_spgram_execute(orc_spgram q, orc_cf *X)
+{
+    const orc_cf *r = orc_window_read(&q->buf);
+    for (unsigned int i = 0; i < q->W; i++) q->x[i] = CMPLXF(crealf(r[i]) * q->w[i], cimagf(r[i]) * q->w[i]);
+    orc_fft(q->nfft, q->x, q->X, +1);
+    if (X) memcpy(X, q->X, q->nfft * sizeof(orc_cf));
+}
+
+static float orc_pwr(orc_cf v) { return crealf(v) * crealf(v) + cimagf(v) * cimagf(v); }
+
+void orc_spgram_execute_psd(orc_spgram q, float *X)
+{
+    orc_spgram_execute(q, NULL);
+    for (unsigned int i = 0; i < q->nfft; i++) X[(i + q->nfft / 2) % q->nfft] = 10 * log10f(orc_pwr(q->X[i]) + 1e-16f);
+}
+
+void orc_spgram_accumulate_psd(orc_spgram q, const void *x, float alpha, unsigned int n)
+{
+    for (unsigned int i = 0; i < n; i++) {
+        orc_window_push(&q->buf, orc_spg_in(q, x, i));
+        q->sc++;
+        if (q->sc == q->W / 2) {
+            if (q->nt == 0) alpha = 1.0f;   /* stays 1 for the rest of this call, as spgram.c:214-216 */
+            orc_spgram_execute(q, NULL);
+            for (unsigned int k = 0; k < q->nfft; k++) q->psd[k] = (1.0f - alpha) * q->psd[k] + alpha * orc_pwr(q->X[k]);
+            q->sc = 0;
+            q->nt++;
+        }
+    }
+}
+
+void orc_spgram_write_accumulation(orc_spgram q, float *x)
+{
+    for (unsigned int i = 0; i < q->nfft; i++) x[(i + q->nfft / 2) % q->nfft] = 10 * log10f(q->psd[i]);
+}
+
+void orc_spgram_estimate_psd(orc_spgram q, const void *x, unsigned int n, float *psd)
+{
+    if (n == 0) return;
+    orc_spgram_reset(q);
+    unsigned int delay = q->nfft / 4;
+    if (delay == 0) delay = 1;
+    for (unsigned int i = 0; i < q->nfft; i++) psd[i] = 0.0f;
+    unsigned int nt = 0;
+    for (unsigned int i = 0; i < n; i++) {
+        orc_window_push(&q->buf, orc_spg_in(q, x, i));
+        if (((i + 1) % delay) == 0 || i == n - 1) {
+            orc_spgram_execute(q, NULL);
+            for (unsigned int k = 0; k < q->nfft; k++) psd[(k + q->nfft / 2) % q->nfft] += orc_pwr(q->X[k]);
+            nt++;
+        }
+    }
+    for (unsigned int i = 0; i < q->nfft; i++) psd[i] = 10 * log10f(psd[i] / (float)nt);
+}

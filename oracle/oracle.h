@@ -157,4 +157,16 @@ void          orc_msresamp_destroy(orc_msresamp q);
 void          orc_msresamp_reset(orc_msresamp q);
 void          orc_msresamp_execute(orc_msresamp q, const orc_cf *x, unsigned int nx, orc_cf *y, unsigned int *ny);
 
+/* spgram (src/fft/src/spgram.c:41-286): real_in selects spgramf */
+typedef struct orc_spgram_s *orc_spgram;
+orc_spgram orc_spgram_create(int real_in, unsigned int nfft, const float *window, unsigned int W);
+void       orc_spgram_destroy(orc_spgram q);
+void       orc_spgram_reset(orc_spgram q);
+void       orc_spgram_write(orc_spgram q, const void *x, unsigned int n);
+void       orc_spgram_execute(orc_spgram q, orc_cf *X);
+void       orc_spgram_execute_psd(orc_spgram q, float *X);
+void       orc_spgram_accumulate_psd(orc_spgram q, const void *x, float alpha, unsigned int n);
+void       orc_spgram_write_accumulation(orc_spgram q, float *x);
+void       orc_spgram_estimate_psd(orc_spgram q, const void *x, unsigned int n, float *psd);
+
 #endif

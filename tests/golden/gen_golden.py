@@ -20,6 +20,7 @@ arrays, plus the tolerances the reference's runners apply):
       dotprod  src/dotprod/tests/dotprod_{rrrf,crcf,cccf}_autotest.c
       firinterp src/filter/tests/firinterp_autotest.c:29-150
       firpfb   src/filter/tests/firpfb_autotest.c:26-73
+  * fft_r2r  : src/fft/tests/data/fft_r2rdata_{8,27,32}.c (DCT/DST I-IV, tol 1e-4)
   * firdes   : rcos / rrcos coefficient arrays (src/filter/tests/firdes_autotest.c:25-95,
                tol 1e-5) and Parks-McClellan designs with their band specs
                (src/filter/tests/firdespm_autotest.c:26-140, tol 1e-4)
@@ -195,6 +196,23 @@ def gen_known_answers():
     return ka
 
 
+def gen_fft_r2r():
+    """src/fft/tests/data/fft_r2rdata_{8,27,32}.c (runner fft_r2r_autotest.c:27-48, tol 1e-4)"""
+    out = []
+    codes = {"REDFT00": 10, "REDFT10": 11, "REDFT01": 12, "REDFT11": 13,
+             "RODFT00": 20, "RODFT10": 21, "RODFT01": 22, "RODFT11": 23}
+    for n in (8, 27, 32):
+        arr = parse_arrays(read("src/fft/tests/data/fft_r2rdata_%d.c" % n))
+        x = arr["fftdata_r2r_x%d" % n]
+        for name, code in codes.items():
+            key = "fftdata_r2r_%s_y%d" % (name, n)
+            if key in arr:
+                out.append({"name": "%s_n%d" % (name, n), "n": n, "type": code, "x": list(x),
+                            "y": list(arr[key]), "tol": 1e-4,
+                            "source": "src/fft/tests/data/fft_r2rdata_%d.c" % n})
+    return out
+
+
 def gen_firdes():
     out = {}
     b = parse_function_bodies(read("src/filter/tests/firdes_autotest.c"))
@@ -220,6 +238,7 @@ def gen_firdes():
 def main():
     fixtures = {
         "firdes": gen_firdes(),
+        "fft_r2r": gen_fft_r2r(),
         "firfilt": gen_filter_data("firfilt"),
         "firdecim": gen_filter_data("firdecim"),
         "fftfilt": gen_filter_data("fftfilt"),

@@ -61,6 +61,15 @@ def _declare(L):
         "orc_firinterp_create_kaiser": (vp, [u, u, f]),
         "orc_firinterp_destroy": (None, [vp]),
         "orc_firinterp_execute_block": (None, [vp, vp, u, vp]),
+        "orc_spgram_create": (vp, [i, u, vp, u]),
+        "orc_spgram_destroy": (None, [vp]),
+        "orc_spgram_reset": (None, [vp]),
+        "orc_spgram_write": (None, [vp, vp, u]),
+        "orc_spgram_execute": (None, [vp, vp]),
+        "orc_spgram_execute_psd": (None, [vp, vp]),
+        "orc_spgram_accumulate_psd": (None, [vp, vp, f, u]),
+        "orc_spgram_write_accumulation": (None, [vp, vp]),
+        "orc_spgram_estimate_psd": (None, [vp, vp, u, vp]),
         "orc_resamp2_create": (vp, [i, u, f, f]),
         "orc_resamp2_destroy": (None, [vp]),
         "orc_resamp2_clear": (None, [vp]),
@@ -429,3 +438,45 @@ class FirPfbch2(_Obj):
         y = np.zeros(nb * out, np.complex64)
         lib().orc_firpfbch2_execute_block(self.q, ptr(x), nb, ptr(y))
         return y
+
+
+class Spgram(_Obj):
+    """spgram.c:41-286; real_in: spgramf"""
+    _destroy = "orc_spgram_destroy"
+
+    def __init__(self, nfft, window, real_in=False):
+        self.nfft, self.real_in = nfft, real_in
+        w = np.ascontiguousarray(window, np.float32)
+        self.q = lib().orc_spgram_create(int(real_in), nfft, ptr(w), len(w))
+
+    def _x(self, x):
+        return np.ascontiguousarray(x, np.float32 if self.real_in else np.complex64)
+
+    def write(self, x):
+        x = self._x(x)
+        lib().orc_spgram_write(self.q, ptr(x), len(x))
+
+    def execute(self):
+        X = np.zeros(self.nfft, np.complex64)
+        lib().orc_spgram_execute(self.q, ptr(X))
+        return X
+
+    def execute_psd(self):
+        X = np.zeros(self.nfft, np.float32)
+        lib().orc_spgram_execute_psd(self.q, ptr(X))
+        return X
+
+    def accumulate_psd(self, x, alpha):
+        x = self._x(x)
+        lib().orc_spgram_accumulate_psd(self.q, ptr(x), alpha, len(x))
+
+    def write_accumulation(self):
+        X = np.zeros(self.nfft, np.float32)
+        lib().orc_spgram_write_accumulation(self.q, ptr(X))
+        return X
+
+    def estimate_psd(self, x):
+        x = self._x(x)
+        X = np.zeros(self.nfft, np.float32)
+        lib().orc_spgram_estimate_psd(self.q, ptr(x), len(x), ptr(X))
+        return X

@@ -84,4 +84,4 @@ def test_reference_examples_compile_unchanged():
     against include/liquid.h + libliquid_mi355x (tools/build_ref_examples.sh)."""
     subprocess.check_call(["bash", os.path.join(ROOT, "tools", "build_ref_examples.sh")])
     built = os.listdir(os.path.join(ROOT, "build", "ref_examples"))
-    assert len(built) == 12
+    assert len(built) == 25

@@ -731,3 +731,133 @@ def test_msresamp_device_long_stream():
     ref = o.execute(x)
     assert len(ref) == ny
     assert G.nrm_err(y, ref) < NRM
+
+
+# ------------------------------------------------------------ FFT plan API
+FFTG = G.load("fft")
+R2RG = G.load("fft_r2r")
+
+
+@pytest.mark.parametrize("case", FFTG, ids=lambda c: "n%d" % c["n"])
+def test_fft_run_golden(case):
+    # fft_runtest.c:30-67: forward against the data, backward recovers n x
+    x, y = G.arr(case["x"]), G.arr(case["y"])
+    Y = LQ.fft_run(x, +1)
+    assert np.max(np.abs(Y - y)) < case["tol"]
+    z = LQ.fft_run(Y, -1) / len(x)
+    assert np.max(np.abs(z - x)) < case["tol"]
+    assert G.nrm_err(Y, O.fft(x, +1)) < NRM
+
+
+@pytest.mark.parametrize("case", R2RG, ids=lambda c: c["name"])
+def test_fft_r2r_golden(case):
+    y = LQ.fft_r2r(G.arr(case["x"]).real.astype(np.float32), case["type"])
+    assert np.max(np.abs(y - np.asarray(case["y"]))) < case["tol"]
+
+
+@pytest.mark.parametrize("n", [4096, 8192, 65536, 1 << 20, 1000, 4099, 12345, 100003, 17, 3 * 4096])
+@pytest.mark.parametrize("direction", [+1, -1])
+def test_fft_sizes_vs_float64(n, direction):
+    r = rng(n)
+    batch = 3 if n <= 100003 else 1
+    X = (r.standard_normal((batch, n)) + 1j * r.standard_normal((batch, n))).astype(np.complex64)
+    Y = LQ.fft_batch(X, direction)
+    ref = np.fft.fft(X.astype(np.complex128), axis=1) if direction > 0 else \
+        np.fft.ifft(X.astype(np.complex128), axis=1) * n
+    for b in range(batch):
+        assert G.nrm_err(Y[b], ref[b]) < NRM
+
+
+@pytest.mark.parametrize("typ", [10, 11, 12, 13, 20, 21, 22, 23])
+def test_fft_r2r_large_vs_formula(typ):
+    import test_oracle as TO
+    r = rng(typ)
+    x = r.standard_normal(1000).astype(np.float32)
+    assert G.nrm_err(LQ.fft_r2r(x, typ), TO.r2r_np(typ, x)) < NRM
+
+
+def test_fft_plan_binds_arrays_and_device_batch():
+    # fft_create_plan binds x/y; fft_execute reads x at call time
+    n = 256
+    x = np.zeros(n, np.complex64)
+    y = np.zeros(n, np.complex64)
+    L = LQ.lib()
+    p = L.fft_create_plan(n, LQ.ptr(x), LQ.ptr(y), LQ.LIQUID_FFT_FORWARD if hasattr(LQ, "LIQUID_FFT_FORWARD") else 1, 0)
+    r = rng(4)
+    for _ in range(3):
+        x[:] = cx(r, n)
+        L.fft_execute(p)
+        assert G.nrm_err(y, np.fft.fft(x.astype(np.complex128))) < NRM
+    L.fft_destroy_plan(p)
+    # device-resident batch
+    X = cx(r, 64 * 1024).reshape(64, 1024)
+    dX = LQ.DeviceBuffer.from_array(X)
+    q = L.fft_create_plan(1024, None, None, -1, 0)
+    L.fft_execute_batch_dev(q, dX.p, dX.p, 64)
+    LQ.lib().liquid_mi355x_device_synchronize()
+    L.fft_destroy_plan(q)
+    Y = dX.to_array(np.complex64, 64 * 1024).reshape(64, 1024)
+    assert G.nrm_err(Y, np.fft.ifft(X.astype(np.complex128), axis=1) * 1024) < NRM
+
+
+# ------------------------------------------------------------ spgram
+def _db_close(a, b):
+    # dB outputs compared in linear power, normwise (NRM)
+    return G.nrm_err(10 ** (np.asarray(a, np.float64) / 10), 10 ** (np.asarray(b, np.float64) / 10)) < NRM
+
+
+def _kaiser_window(W, beta):
+    return np.array([LQ.lib().kaiser(i, W, beta, 0.0) for i in range(W)], np.float32)
+
+
+@pytest.mark.parametrize("real_in", [False, True])
+@pytest.mark.parametrize("nfft,W", [(64, 48), (256, 128), (1000, 1000), (2, 1)])
+def test_spgram_vs_oracle(real_in, nfft, W):
+    r = rng(nfft + W + real_in)
+    win = _kaiser_window(W, 8.0)
+    g = LQ.Spgram(nfft, win, real_in=real_in)
+    o = O.Spgram(nfft, win, real_in=real_in)
+    sig = (lambda n: r.standard_normal(n).astype(np.float32)) if real_in else (lambda n: cx(r, n))
+    # write / push then execute
+    x = sig(W + 7)
+    g.write(x[:-3])
+    for v in x[-3:]:
+        g.push(v)
+    o.write(x)
+    assert G.nrm_err(g.execute(), o.execute()) < NRM
+    assert _db_close(g.execute_psd(), o.execute_psd())
+    # accumulate in ragged calls (the first call's alpha = 1 rule included)
+    for n, a in [(5, 0.2), (3 * W + 1, 0.2), (1, 0.05), (7 * W + 3, 0.05), (0, 0.3), (W // 2 + 2, 0.3)]:
+        xs = sig(n)
+        g.accumulate_psd(xs, a)
+        o.accumulate_psd(xs, a)
+    assert _db_close(g.write_accumulation(), o.write_accumulation())
+    # estimate: resets, then averages every nfft/4 and at the end
+    xs = sig(10 * nfft + 3)
+    assert _db_close(g.estimate_psd(xs), o.estimate_psd(xs))
+    assert G.nrm_err(g.execute(), o.execute()) < NRM        # window continues after estimate
+
+
+def test_spgram_default_and_kaiser_constructors():
+    r = rng(12)
+    x = cx(r, 5000)
+    g = LQ.Spgram(512, default=True)
+    o = O.Spgram(512, _kaiser_window(256, 10.0))
+    assert _db_close(g.estimate_psd(x), o.estimate_psd(x))
+    g2 = LQ.Spgram(300, kaiser=(200, 6.0))
+    o2 = O.Spgram(300, _kaiser_window(200, 6.0))
+    assert _db_close(g2.estimate_psd(x), o2.estimate_psd(x))
+
+
+def test_spgram_device_estimate_long():
+    n, nfft = 1 << 22, 1024
+    r = rng(77)
+    x = cx(r, n)
+    win = _kaiser_window(nfft // 2, 10.0)
+    g = LQ.Spgram(nfft, win)
+    o = O.Spgram(nfft, win)
+    dx = LQ.DeviceBuffer.from_array(x)
+    dp = LQ.DeviceBuffer(nfft * 4)
+    LQ.lib().spgramcf_estimate_psd_dev(g.q, dx.p, n, dp.p)
+    LQ.lib().spgramcf_synchronize(g.q)
+    assert _db_close(dp.to_array(np.float32, nfft), o.estimate_psd(x))

@@ -341,3 +341,38 @@ def test_msresamp_spectral_reference():
     q = O.MsResamp(r, As)
     y = np.concatenate([q.execute(x[i:i + 1]) for i in range(len(x))])
     assert check(y) == []
+
+
+# ------------------------------------------------------------ real-to-real transforms
+R2R = G.load("fft_r2r")
+
+
+def r2r_np(typ, x):
+    """fft_r2r_1d.c:95-250 in float64 (un-normalised, factor 2)."""
+    x = np.asarray(x, np.float64)
+    n = len(x)
+    i = np.arange(n)[:, None]
+    k = np.arange(n)[None, :]
+    if typ == 10:
+        y = 0.5 * (x[0] + np.where(np.arange(n) % 2, -x[-1], x[-1]))
+        y = y + (np.cos(np.pi * k[:, 1:n - 1] * i / (n - 1)) @ x[1:n - 1])
+    elif typ == 11:
+        y = np.cos(np.pi * (k + 0.5) * i / n) @ x
+    elif typ == 12:
+        y = 0.5 * x[0] + np.cos(np.pi * (i + 0.5) * k[:, 1:] / n) @ x[1:]
+    elif typ == 13:
+        y = np.cos(np.pi * (k + 0.5) * (i + 0.5) / n) @ x
+    elif typ == 20:
+        y = np.sin(np.pi * (k + 1) * (i + 1) / (n + 1)) @ x
+    elif typ == 21:
+        y = np.sin(np.pi * (k + 0.5) * (i + 1) / n) @ x
+    elif typ == 22:
+        y = np.where(np.arange(n) % 2, -0.5, 0.5) * x[-1] + np.sin(np.pi * (k[:, :n - 1] + 1) * (i + 0.5) / n) @ x[:n - 1]
+    else:
+        y = np.sin(np.pi * (k + 0.5) * (i + 0.5) / n) @ x
+    return 2.0 * np.ravel(y)
+
+
+@pytest.mark.parametrize("case", R2R, ids=lambda c: c["name"])
+def test_r2r_formula_golden(case):
+    assert np.max(np.abs(r2r_np(case["type"], case["x"]) - np.asarray(case["y"]))) < case["tol"]

@@ -13,7 +13,9 @@ OUT=build/ref_examples
 mkdir -p "$OUT"
 LIBDIR=$PWD/liquid-dsp_amd/lib
 EXAMPLES="dotprod_cccf dotprod_rrrf fftfilt_crcf firdecim_crcf firfilt_cccf firfilt_crcf firfilt_rrrf
-          firinterp_crcf firpfbch2_crcf firpfbch_crcf firpfbch_crcf_analysis firpfbch_crcf_synthesis"
+          firinterp_crcf firpfbch2_crcf firpfbch_crcf firpfbch_crcf_analysis firpfbch_crcf_synthesis
+          resamp_crcf resamp2_crcf resamp2_crcf_decim resamp2_crcf_filter resamp2_crcf_interp
+          msresamp_crcf msresamp2_crcf fft firdes_kaiser firdespm nyquist_filter spgramcf spgramf"
 for e in $EXAMPLES; do
   gcc -std=gnu99 -O2 -w -I include "$REF/examples/${e}_example.c" -L "$LIBDIR" -lliquid_mi355x \
       -Wl,-rpath,"$LIBDIR" -Wl,-rpath,'$ORIGIN/../../liquid-dsp_amd/lib' -lm -o "$OUT/${e}_example"
