@@ -47,8 +47,8 @@ HBM_PEAK_GBPS = 8000.0
 def parse():
     p = argparse.ArgumentParser()
     p.add_argument("--gpus", type=int, default=1)
-    p.add_argument("--steps", type=int, default=20)
-    p.add_argument("--warmup", type=int, default=3)
+    p.add_argument("--steps", type=int, default=50)
+    p.add_argument("--warmup", type=int, default=20)
     p.add_argument("--samples", type=int, default=1 << 27, help="firpfbch2 input samples per GPU")
     p.add_argument("--fir-samples", type=int, default=1 << 28, help="firfilt samples per GPU")
     p.add_argument("--cpu-seconds", type=float, default=10.0, help="CPU baseline budget (rank 0, N=1)")

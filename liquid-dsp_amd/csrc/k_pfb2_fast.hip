@@ -221,7 +221,7 @@ __global__ __launch_bounds__(NT, 1) void k_pfb2_an1024(Params P, const float *__
         const float2 b = __builtin_bit_cast(float2, __builtin_amdgcn_raw_buffer_load_b64(rh, oh0 + k, 0, 0));
         return make_float2(a.x + b.x, a.y + b.y);
     };
-    const float inv = 1.0f / (float)M; // output scale 1/M: exact for M = 2^10
+    // taps arrive scaled by 1/M (firpfbch2.c:277-278's output scale, exact for M = 2^10)
     auto dot = [&](int newest, const float (&h)[L]) -> float2 {
         float2 acc = make_float2(0.f, 0.f);
 #pragma unroll
@@ -230,7 +230,7 @@ __global__ __launch_bounds__(NT, 1) void k_pfb2_an1024(Params P, const float *__
             acc.x = fmaf(h[n], v.x, acc.x);
             acc.y = fmaf(h[n], v.y, acc.y);
         }
-        return make_float2(acc.x * inv, acc.y * inv);
+        return acc;
     };
 
     // warm-up: rows 8gs-8 .. 8gs-1 fill the ring; the last gives the hi-bin

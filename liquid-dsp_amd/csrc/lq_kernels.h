@@ -83,7 +83,8 @@ void lqk_firpfbch2_analyzer(unsigned int M, unsigned int m, const void *hsub, co
                             void *stream);
 /* M = 1024 (m = 2 or 4) register/LDS-streaming fast path; returns 0 if the
  * shape is not covered (caller then uses lqk_firpfbch2_analyzer).  B0 = global
- * index of the first block (only its parity matters). */
+ * index of the first block (only its parity matters).  hsub here is the tap
+ * table already multiplied by 1/M (the kernel applies no output scale). */
 int lqk_firpfbch2_analyzer_fast(unsigned int M, unsigned int m, const void *hsub, const void *hist,
                                 const void *x, unsigned long long nblocks, long long B0, void *Y,
                                 void *stream);

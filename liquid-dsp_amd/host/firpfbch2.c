@@ -20,6 +20,7 @@ struct firpfbch2_crcf_s {
     unsigned int M, m, HL;
     float *h;          /* 2*M*m prototype taps */
     void *d_hsub;      /* M x 2m: hsub[i*2m + n] = h[i + n*M] */
+    void *d_hsub_s;    /* analyzer: hsub / M (exact for M = 2^k), the fast path's form */
     void *d_hist[2];   /* analyzer: last HL inputs */
     int cur;
     void *d_zstate;    /* synthesizer: last 4m-1 IFFT vectors */
@@ -56,6 +57,12 @@ firpfbch2_crcf firpfbch2_crcf_create(int _type, unsigned int _M, unsigned int _m
     q->d_hsub = lqrt_malloc((size_t)_M * L * sizeof(float));
     lqrt_h2d(q->d_hsub, hsub, (size_t)_M * L * sizeof(float), q->ctx.stream);
     if (_type == LIQUID_ANALYZER) {
+        /* the output scale 1/M folded into the taps: a power of two, so every
+         * product and partial sum scales exactly and the results are unchanged */
+        const float inv = 1.0f / (float)_M;
+        for (size_t i = 0; i < (size_t)_M * L; i++) hsub[i] *= inv;
+        q->d_hsub_s = lqrt_malloc((size_t)_M * L * sizeof(float));
+        lqrt_h2d(q->d_hsub_s, hsub, (size_t)_M * L * sizeof(float), q->ctx.stream);
         q->d_hist[0] = lqrt_malloc((size_t)q->HL * 8);
         q->d_hist[1] = lqrt_malloc((size_t)q->HL * 8);
     } else {
@@ -87,6 +94,7 @@ void firpfbch2_crcf_destroy(firpfbch2_crcf _q)
 {
     lqrt_sync(_q->ctx.stream);
     lqrt_free(_q->d_hsub);
+    lqrt_free(_q->d_hsub_s);
     lqrt_free(_q->d_hist[0]);
     lqrt_free(_q->d_hist[1]);
     lqrt_free(_q->d_zstate);
@@ -124,7 +132,7 @@ void firpfbch2_crcf_execute_block_dev(firpfbch2_crcf _q, const liquid_float_comp
     if (_nblocks == 0) return;
     if (_q->type == LIQUID_ANALYZER) {
         void *hold = _q->d_hist[_q->cur], *hnew = _q->d_hist[_q->cur ^ 1];
-        if (!lqk_firpfbch2_analyzer_fast(_q->M, _q->m, _q->d_hsub, hold, _dx, _nblocks, _q->flag, _dy,
+        if (!lqk_firpfbch2_analyzer_fast(_q->M, _q->m, _q->d_hsub_s, hold, _dx, _nblocks, _q->flag, _dy,
                                          _q->ctx.stream))
             lqk_firpfbch2_analyzer(_q->M, _q->m, _q->d_hsub, hold, _dx, _nblocks, _q->flag, _dy, _q->ctx.stream);
         lqk_window_append(1, hold, _q->HL, _dx, _nblocks * (_q->M / 2), hnew, _q->ctx.stream);

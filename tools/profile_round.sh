@@ -7,7 +7,7 @@ TAG=${1:-prof}
 export TMPDIR=/tmp
 OUT=gpurun_out/$TAG; rm -rf $OUT; mkdir -p $OUT
 python -c "import __graft_entry__ as g; g.build()" > $OUT/build.log 2>&1 || exit 1
-timeout -k 10 600 rocprofv3 --kernel-trace --stats -d $OUT/trace -o run --output-format csv -- python3 bench.py --steps 10 --warmup 2 --no-cpu-baseline > $OUT/bench_under_rocprof.log 2>&1 || { tail -20 $OUT/bench_under_rocprof.log; exit 1; }
+timeout -k 10 600 rocprofv3 --kernel-trace --stats -d $OUT/trace -o run --output-format csv -- python3 bench.py --steps 50 --warmup 20 --no-cpu-baseline > $OUT/bench_under_rocprof.log 2>&1 || { tail -20 $OUT/bench_under_rocprof.log; exit 1; }
 for C in FETCH_SIZE WRITE_SIZE; do
   timeout -k 10 300 rocprofv3 --pmc $C --output-format csv -d $OUT/$C -o run -- python3 tools/prof_run.py --what all --iters 2 > $OUT/$C.log 2>&1 || { tail -5 $OUT/$C.log; exit 1; }
 done
@@ -45,4 +45,26 @@ json.dump({"firpfbch2_bytes_per_launch": traffic.get("firpfbch2", {}).get("total
 print(json.dumps(traffic))
 PY
 find $OUT/trace -name "*kernel_stats.csv" -exec cp {} $OUT/kernel_stats.csv \;
+# the bench's timed window: the last 50 dispatches of each hot kernel (the
+# 20 warm-up dispatches before them are in kernel_stats.csv's average)
+python3 - $OUT <<'PY'
+import csv, glob, json, os, sys, collections
+out = sys.argv[1]
+f = glob.glob(os.path.join(out, "trace", "**", "*kernel_trace.csv"), recursive=True)[0]
+d = collections.defaultdict(list)
+for r in csv.DictReader(open(f)):
+    d[r["Kernel_Name"]].append((int(r["Start_Timestamp"]), int(r["End_Timestamp"])))
+res = {}
+for k, v in d.items():
+    key = "firpfbch2" if "pfb2" in k else ("firfilt" if "k_firfilt<" in k else ("resamp" if "k_resamp" in k else None))
+    if not key or len(v) < 50:
+        continue
+    v.sort()
+    last = [e - s for s, e in v[-50:]]
+    res[key] = {"kernel": k[:120], "dispatches": len(v), "timed_window_avg_us": sum(last) / len(last) / 1e3,
+                "timed_window_min_us": min(last) / 1e3, "timed_window_max_us": max(last) / 1e3,
+                "all_avg_us": sum(e - s for s, e in v) / len(v) / 1e3}
+json.dump(res, open(os.path.join(out, "timed_window.json"), "w"), indent=1)
+print(json.dumps(res, indent=1))
+PY
 head -5 $OUT/kernel_stats.csv | cut -c1-200
