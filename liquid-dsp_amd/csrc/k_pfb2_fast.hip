@@ -14,8 +14,10 @@
 //    SIMD) owns all 1024 columns, one per lane, with the column's even- and
 //    odd-block taps and an 8-deep register ring.  Rows stream through the
 //    ring, so every input sample is read from HBM once per workgroup
-//    segment.  Eight rows per iteration complete sixteen blocks; the next
-//    eight rows are prefetched into registers while the FFTs run.
+//    segment.  Eight rows per iteration complete sixteen blocks; six of the
+//    next eight rows are prefetched into registers while the FFTs run (the
+//    tap selection is per lane, outside the loop, so the row loop and the
+//    quad butterflies carry no per-lane selects: 122 VGPRs, no spills).
 //  * X of each block goes to an LDS ring (17 block buffers, 148 KB); after a
 //    barrier each wave runs one 1024-point IFFT in registers: 16-point DFT over the
 //    lane's 16 bins (j = lane + 64k), twiddle, LDS transpose (row stride 68
@@ -139,7 +141,7 @@ __device__ unsigned long long g_pfb2_clk[2 * 1024];   // dev experiments (XMODE 
 // SMODE: output path. 0: per-lane 8-byte non-temporal stores straight from the
 // FFT layout; 1: same, plain stores; 2: through the block's LDS buffer into
 // 16-byte non-temporal stores; 3: 2 with plain stores
-template <int L, int XMODE = 0, int SMODE = 2, int PF = 4, int BAR = 1, int TRES = 0>
+template <int L, int XMODE = 0, int SMODE = 2, int PF = 6, int BAR = 1, int TRES = 0>
 __global__ __launch_bounds__(NT, 1) void k_pfb2_an1024(Params P, const float *__restrict__ hsub,
                                                        const float2 *__restrict__ tw4096)
 {
@@ -176,19 +178,19 @@ __global__ __launch_bounds__(NT, 1) void k_pfb2_an1024(Params P, const float *__
     const int j = lo ? (M2 - 1 - tid) : (3 * M2 - 1 - tid);
     // taps are re-read (L1/L2 hits) at each dot phase instead of being held
     // in registers across the FFT phase; hsub is pre-scaled by 1/M on the host
-    const float *hpe = hsub + j * L, *hpo = hsub + (j ^ M2) * L;
-    float he[L], ho[L];
+    // ta: taps of the first block a row feeds (lo: even taps of block 2c; hi:
+    // odd taps of block 2c+1), tb: the second (lo: odd, 2c+1; hi: even, 2c+2).
+    // Chosen once per lane, so the row loop has no per-lane tap selects.
+    float ta[L], tb[L];
     auto load_taps = [&]() {
-        int oe = j * L, oo = (j ^ M2) * L;
-        if (!TRES) asm volatile("" : "+v"(oe), "+v"(oo)); // keep the reload inside the loop
+        int oa = (lo ? j : (j ^ M2)) * L, ob = (lo ? (j ^ M2) : j) * L;
+        if (!TRES) asm volatile("" : "+v"(oa), "+v"(ob)); // keep the reload inside the loop
 #pragma unroll
         for (int n = 0; n < L; n++) {
-            he[n] = hsub[oe + n];
-            ho[n] = hsub[oo + n];
+            ta[n] = hsub[oa + n];
+            tb[n] = hsub[ob + n];
         }
     };
-    (void)hpe;
-    (void)hpo;
     load_taps();
     // first / second block fed by row c: lo: (2c, E), (2c+1, O); hi: (2c+1, O), (2c+2, E)
     const int dA = lo ? 0 : 1;
@@ -238,7 +240,7 @@ __global__ __launch_bounds__(NT, 1) void k_pfb2_an1024(Params P, const float *__
 #pragma unroll
     for (int s = 0; s < NS; s++) w[s] = fetch(8 * gs - NS + s);
     int slot0 = (int)((16 * gs) % NBUF); // buffer of block 16g (advances by 16 mod 17 = -1)
-    if (!lo) xb[slot0 * BSTR + j] = dot(NS - 1, he);
+    if (!lo) xb[slot0 * BSTR + j] = dot(NS - 1, tb);
     __syncthreads(); // twiddle tables ready
 
     // next iteration's first PF rows are prefetched into registers while the
@@ -258,8 +260,8 @@ __global__ __launch_bounds__(NT, 1) void k_pfb2_an1024(Params P, const float *__
             s1 -= (s1 >= NBUF) ? NBUF : 0;
             int s2 = s1 + 1;
             s2 -= (s2 >= NBUF) ? NBUF : 0;
-            xb[s1 * BSTR + j] = dot(r, lo ? he : ho);
-            xb[s2 * BSTR + j] = dot(r, lo ? ho : he);
+            xb[s1 * BSTR + j] = dot(r, ta);
+            xb[s2 * BSTR + j] = dot(r, tb);
         }
         if (g + 1 < ge) {
 #pragma unroll
@@ -309,14 +311,16 @@ __global__ __launch_bounds__(NT, 1) void k_pfb2_an1024(Params P, const float *__
             }
             // 4-point DFT over bq across the lane quad (radix-2 x 2):
             // stage 1 pairs bq, bq^2; twiddle W4^{+1} on bq=3; stage 2 pairs bq, bq^1
-            const bool hi2 = (bq & 2) != 0, hi1 = (bq & 1) != 0;
+            // butterflies as p + sign * own (one fma per component instead of
+            // both sum and difference plus a select)
+            const float sg2 = (bq & 2) ? -1.0f : 1.0f, sg1 = (bq & 1) ? -1.0f : 1.0f;
 #pragma unroll
             for (int r = 0; r < 16; r++) {
-                float2 p = quad_xor<2>(v[r]);
-                float2 u = hi2 ? csub(p, v[r]) : cadd(v[r], p);
+                const float2 p = quad_xor<2>(v[r]);
+                float2 u = make_float2(fmaf(sg2, v[r].x, p.x), fmaf(sg2, v[r].y, p.y));
                 if (bq == 3) u = cmul_pj(u);
-                float2 p2 = quad_xor<1>(u);
-                v[r] = hi1 ? csub(p2, u) : cadd(u, p2);
+                const float2 p2 = quad_xor<1>(u);
+                v[r] = make_float2(fmaf(sg1, u.x, p2.x), fmaf(sg1, u.y, p2.y));
             }
             // lane (k1, bq) holds Y[k1 + 16 r + 256 s], s = bitrev2(bq)
             if (XMODE % 10 == 3) {

@@ -106,57 +106,11 @@ int main()
     P.gpw = (int)gpw;
     P.gend = ngroups;
     const int it = 10;
-    // v2: 8-block groups, two workgroups per CU
-    Params P2 = P;
-    const long long ng8 = nb / 8;
-    for (int target : {512}) {
-        long long gpw8 = (ng8 + target - 1) / target;
-        if (gpw8 < 2) gpw8 = 2;
-        const unsigned nwg8 = (unsigned)((ng8 + gpw8 - 1) / gpw8);
-        P2.gs0 = 0;
-        P2.gpw = (int)gpw8;
-        P2.gend = ng8;
-        for (int rep = 0; rep < 2; rep++) {
-            run_v2<2>("v2 PF2", P2, hsub, nwg8, it);
-            run_v2<1>("v2 PF1", P2, hsub, nwg8, it);
-            run_v2<0>("v2 PF0", P2, hsub, nwg8, it);
-        }
-    }
-    for (int rep = 0; rep < 2; rep++) run<10, 2, 4, 1, 0>("library v1 (synthetic taps)", P, hsub, nwg, it);
-    {   // Kaiser prototype taps (firpfbch2_crcf_create_kaiser-like), scaled by 1/M
-        const int L = 8, nh = 2 * M * 4 + 1;
-        const double beta = 0.1102 * (60.0 - 8.7), fc = 1.0 / M;
-        std::vector<float> hk(M * L);
-        for (int i = 0; i < M; i++)
-            for (int q = 0; q < L; q++) {
-                const int k = i + q * M;
-                const double t = k - (nh - 1) / 2.0, r = 2.0 * t / nh;
-                const double sinc = t == 0 ? 1.0 : sin(M_PI * 2 * fc * t) / (M_PI * 2 * fc * t);
-                hk[i * L + q] = (float)(sinc * std::cyl_bessel_i(0.0, beta * sqrt(1 - r * r)) /
-                                        std::cyl_bessel_i(0.0, beta) / M);
-            }
-        LQ_CHECK(hipMemcpy(hsub, hk.data(), M * L * 4, hipMemcpyHostToDevice));
-        for (int rep = 0; rep < 3; rep++) run<10, 2, 4, 1, 0>("library v1 (Kaiser taps)", P, hsub, nwg, it);
-        LQ_CHECK(hipMemcpy(hsub, hh.data(), M * 8 * 4, hipMemcpyHostToDevice));
-        for (int rep = 0; rep < 2; rep++) run<10, 2, 4, 1, 0>("library v1 (synthetic taps)", P, hsub, nwg, it);
-    }
-    // correctness: v1 and v2 agree
-    {
-        std::vector<float2> y1(nb * M), y2(nb * M);
-        hipLaunchKernelGGL((k_pfb2_an1024<8, 0, 2, 4, 1, 0>), dim3(nwg), dim3(NT), 0, 0, P, hsub, g_tw);
-        LQ_CHECK(hipMemcpy(y1.data(), y, nb * M * 8, hipMemcpyDeviceToHost));
-        LQ_CHECK(hipMemset(y, 0, nb * M * 8));
-        long long gpw8 = (ng8 + 511) / 512;
-        P2.gpw = (int)gpw8;
-        hipLaunchKernelGGL((k_pfb2_an1024_v2<8, 0>), dim3((unsigned)((ng8 + gpw8 - 1) / gpw8)), dim3(NT2), 0, 0, P2,
-                           hsub, g_tw);
-        LQ_CHECK(hipMemcpy(y2.data(), y, nb * M * 8, hipMemcpyDeviceToHost));
-        double md = 0, mx = 0;
-        for (long long i = 0; i < nb * M; i++) {
-            md = fmax(md, fabs(y1[i].x - y2[i].x) + fabs(y1[i].y - y2[i].y));
-            mx = fmax(mx, fabs(y1[i].x) + fabs(y1[i].y));
-        }
-        printf("v1 vs v2: max |diff| %.3e (max |y| %.3e)\n", md, mx);
+    for (int rep = 0; rep < 2; rep++) run<10, 2, 4, 1, 0>("warm", P, hsub, nwg, it);
+    for (int rep = 0; rep < 2; rep++) {
+        run<10, 2, 4, 1, 0>("PF4", P, hsub, nwg, it);
+        run<10, 2, 6, 1, 0>("PF6", P, hsub, nwg, it);
+        run<10, 2, 8, 1, 0>("PF8", P, hsub, nwg, it);
     }
     return 0;
 }
