@@ -56,6 +56,9 @@ def parse():
     p.add_argument("--no-firfilt", action="store_true")
     p.add_argument("--rs-samples", type=int, default=1 << 25, help="resamp_crcf input samples per GPU")
     p.add_argument("--no-resamp", action="store_true")
+    p.add_argument("--dp-vectors", type=int, default=1 << 20, help="dotprod_cccf vectors per GPU per n")
+    p.add_argument("--ff-samples", type=int, default=1 << 26, help="fftfilt_crcf samples per GPU")
+    p.add_argument("--no-extra", action="store_true", help="skip the dotprod / fftfilt legs")
     p.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic.json"),
                    help="PMC-derived HBM bytes per launch (from a separate rocprofv3 --pmc run)")
     return p.parse_args()
@@ -156,6 +159,51 @@ def bench_firfilt(args, world, rank, stream):
     return res
 
 
+def bench_dotprod(args, world, rank, stream):
+    """configs[1]: dotprod_cccf n in {16,64,256,1024}, 2^20 vectors per GPU"""
+    out = {}
+    nvec = args.dp_vectors
+    g = torch.Generator()
+    g.manual_seed(11)
+    for n in (16, 64, 256, 1024):
+        X = synth_complex(n * nvec, 99 + n + rank)
+        Y = torch.empty(2 * nvec, dtype=torch.float32, device="cuda")
+        h = ((torch.rand(n, generator=g) - 0.5) + 1j * (torch.rand(n, generator=g) - 0.5)).numpy()
+        q = LQ.DotProd("cccf", h)
+        q.set_stream(stream.cuda_stream)
+
+        def step():
+            q.execute_batch_dev(X.data_ptr(), nvec, Y.data_ptr())
+
+        wall, gpu_ms = time_steps(step, args.steps, args.warmup, world, stream)
+        out[n] = {"wall": wall, "gpu_ms": gpu_ms}
+        q.destroy()
+        del X, Y
+        torch.cuda.empty_cache()
+    return {"nvec": nvec, "runs": out}
+
+
+def bench_fftfilt(args, world, rank, stream):
+    """configs[2]: fftfilt_crcf h=512 on 2^26 samples per GPU"""
+    n = args.ff_samples
+    x = synth_complex(n, 31337 + rank)
+    y = torch.empty(2 * n, dtype=torch.float32, device="cuda")
+    g = torch.Generator()
+    g.manual_seed(17)
+    h = (torch.rand(512, generator=g) - 0.5).numpy()
+    q = LQ.FftFilt(h, 2048)
+    q.set_stream(stream.cuda_stream)
+
+    def step():
+        q.execute_block_dev(x.data_ptr(), n, y.data_ptr())
+
+    wall, gpu_ms = time_steps(step, args.steps, args.warmup, world, stream)
+    q.destroy()
+    del x, y
+    torch.cuda.empty_cache()
+    return {"n": n, "wall": wall, "gpu_ms": gpu_ms}
+
+
 def bench_resamp(args, world, rank, stream):
     """configs[4]: resamp_crcf r=1.037, npfb=64, m=7 on 32M samples per GPU"""
     n = args.rs_samples
@@ -248,6 +296,13 @@ def main():
         g_rs = allreduce_max(rs["gpu_ms"], world)
         tot_rs = allreduce_sum(rs["n"] * args.steps, world)
 
+    dp = ff = None
+    if not args.no_extra:
+        dp = bench_dotprod(args, world, rank, stream)
+        ff = bench_fftfilt(args, world, rank, stream)
+        dp_t = {n: (allreduce_max(r["wall"], world), allreduce_max(r["gpu_ms"], world)) for n, r in dp["runs"].items()}
+        ff_t = (allreduce_max(ff["wall"], world), allreduce_max(ff["gpu_ms"], world))
+
     copy_gbps = copy_bandwidth() if rank == 0 else None
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
@@ -310,6 +365,22 @@ def main():
                                                      "traffic": rs_traffic,
                                                      "bytes_per_unit": "8 B/input + 8 B/output",
                                                      "launch_ms": rl_ms}}
+        if dp is not None:
+            legs = {}
+            for n, (tw, tg) in dp_t.items():
+                ms = tg / args.steps
+                legs["n%d" % n] = {"value": world * dp["nvec"] * args.steps / tw / 1e6, "unit": "M dot products/s",
+                                   "launch_ms": ms, "achieved_GBps": (8.0 * n + 8.0) * dp["nvec"] / (ms * 1e-3) / 1e9,
+                                   "frac": (8.0 * n + 8.0) * dp["nvec"] / (ms * 1e-3) / 1e9 / HBM_PEAK_GBPS}
+            out["dotprod_cccf"] = {"workload": "dotprod_cccf batched, %d vectors/GPU (BASELINE configs[1])"
+                                   % dp["nvec"], "bytes_per_unit": "8n+8 B/vector", "legs": legs}
+            ms = ff_t[1] / args.steps
+            out["fftfilt_crcf_h512"] = {"value": world * ff["n"] * args.steps / ff_t[0] / 1e6, "unit": "Msamples/s",
+                                        "workload": "fftfilt_crcf h=512 overlap-save, %d samples/GPU "
+                                                    "(BASELINE configs[2])" % ff["n"],
+                                        "launch_ms": ms, "achieved_GBps": 16.0 * ff["n"] / (ms * 1e-3) / 1e9,
+                                        "frac": 16.0 * ff["n"] / (ms * 1e-3) / 1e9 / HBM_PEAK_GBPS,
+                                        "bytes_per_unit": "16 B/sample"}
         print(json.dumps(out))
     if world > 1:
         dist.barrier()

@@ -1,4 +1,6 @@
 // k_fftfilt.hip -- FFT fast convolution for fftfilt_{crcf,rrrf,cccf}.
+// Default kernel: k_fftfilt_r16 (register radix-16 transforms, persistent
+// grid); k_fftfilt (LDS Stockham) is the earlier form, kept for comparison.
 //
 // Reference: src/filter/src/fftfilt.c:193-260 runs overlap-ADD with a 2n-point
 // transform per n-sample call; its output is the causal linear convolution
@@ -14,12 +16,21 @@
 #include "lq_kernels.h"
 
 #include <cstdio>
+#include <type_traits>
 #include <cstdlib>
 
 namespace {
 
 constexpr int NT = 256;
 constexpr int NFFT = 4096;
+// k_fftfilt_r16 configuration (tools/mb/mb_fftfilt.hip, h=512, 2^26 samples):
+// the two register transforms need ~250 VGPRs, so 2 waves/SIMD without
+// spills (0.29 ms) beats 4 waves/SIMD with spills (0.73 ms); the filter
+// spectrum is read from L2 per segment (holding it in registers: no gain)
+#ifndef FF_HREG
+#define FF_HREG false
+#define FF_WPE 2
+#endif
 
 // kind 0: real input/output (rrrf), otherwise complex
 template <bool REAL>
@@ -65,6 +76,72 @@ __global__ __launch_bounds__(NT) void k_fftfilt(int hm1, const float2 *__restric
     }
 }
 
+__device__ __forceinline__ float2 to_c2(float a) { return make_float2(a, 0.f); }
+__device__ __forceinline__ float2 to_c2(float2 a) { return a; }
+
+// Register form (default): 256 threads, thread t holds segment samples
+// t + 256 n; forward 4096-point FFT (fft4096_r16), x H, inverse, all with the
+// data in registers and two LDS transposes per transform (35 KB LDS -> four
+// workgroups per CU); loads and stores are coalesced across t.
+template <bool REAL, bool HREG, int WPE>
+__global__ __launch_bounds__(NT, WPE) void k_fftfilt_r16(int hm1, const float2 *__restrict__ H,
+                                                    const void *__restrict__ hist, const void *__restrict__ xin,
+                                                    long long n, void *__restrict__ yout, float sre, float sim,
+                                                    const float2 *__restrict__ tw)
+{
+    __shared__ __attribute__((aligned(16))) float2 lds[FFT4096_LDS];
+    const int L = NFFT - hm1;
+    const int t = threadIdx.x;
+    const long long nseg = (n + L - 1) / L;
+    // persistent: the filter spectrum stays in registers across segments
+    float2 hv[HREG ? 16 : 1];
+    if (HREG) {
+#pragma unroll
+        for (int k = 0; k < 16; k++) hv[k] = H[t + 256 * k];
+    }
+    using S = typename std::conditional<REAL, float, float2>::type;
+    for (long long seg = blockIdx.x; seg < nseg; seg += gridDim.x) {
+    const long long s0 = seg * L;
+    // segment sample i = t + 256 q is stream sample s0 - hm1 + i; 32-bit
+    // indices relative to the segment start (the history only feeds seg 0)
+    const long long rem = n - (s0 - hm1);              // segment samples that exist
+    const int lim = rem < NFFT ? (int)rem : NFFT;
+    float2 v[16];
+    if (seg == 0) {
+#pragma unroll
+        for (int q = 0; q < 16; q++) {
+            const int i = t + 256 * q, s = i - hm1;
+            S a{};
+            if (s < 0) a = ((const S *)hist)[hm1 + s];
+            else if (i < lim) a = ((const S *)xin)[s];
+            v[q] = to_c2(a);
+        }
+    } else {
+        const S *xs = (const S *)xin + (s0 - hm1);
+#pragma unroll
+        for (int q = 0; q < 16; q++) {
+            const int i = t + 256 * q;
+            S a{};
+            if (i < lim) a = xs[i];
+            v[q] = to_c2(a);
+        }
+    }
+    fft4096_r16<+1>(v, lds, tw, t);
+#pragma unroll
+    for (int k = 0; k < 16; k++) v[k] = cmul(v[k], HREG ? hv[k & (HREG ? 15 : 0)] : H[t + 256 * k]);
+    fft4096_r16<-1>(v, lds, tw, t);
+    S *ys = (S *)yout + (s0 - hm1);                    // output o = s0 + i - hm1 for i >= hm1
+#pragma unroll
+    for (int q = 0; q < 16; q++) {
+        const int i = t + 256 * q;
+        if (i < hm1 || i >= lim) continue;
+        const float2 r = v[q];
+        if constexpr (REAL) ys[i] = r.x * sre;
+        else ys[i] = make_float2(r.x * sre - r.y * sim, r.x * sim + r.y * sre);
+    }
+    }
+}
+
 } // namespace
 
 extern "C" void lqk_fftfilt_run(int real_io, unsigned int hlen, const void *H, const void *hist, const void *x,
@@ -81,12 +158,13 @@ extern "C" void lqk_fftfilt_run(int real_io, unsigned int hlen, const void *H, c
     const int L = NFFT - hm1;
     const long long nseg = ((long long)n + L - 1) / L;
     const float2 *tw = (const float2 *)lqrt_twiddles();
+    const unsigned grid = (unsigned)(nseg < 1024 ? nseg : 1024);   // persistent: 4 workgroups per CU
     if (real_io)
-        hipLaunchKernelGGL(k_fftfilt<true>, dim3((unsigned)nseg), dim3(NT), 0, st, hm1, (const float2 *)H, hist, x,
-                           (long long)n, y, scale_re, scale_im, tw);
+        hipLaunchKernelGGL((k_fftfilt_r16<true, FF_HREG, FF_WPE>), dim3(grid), dim3(NT), 0, st, hm1, (const float2 *)H, hist,
+                           x, (long long)n, y, scale_re, scale_im, tw);
     else
-        hipLaunchKernelGGL(k_fftfilt<false>, dim3((unsigned)nseg), dim3(NT), 0, st, hm1, (const float2 *)H, hist, x,
-                           (long long)n, y, scale_re, scale_im, tw);
+        hipLaunchKernelGGL((k_fftfilt_r16<false, FF_HREG, FF_WPE>), dim3(grid), dim3(NT), 0, st, hm1, (const float2 *)H, hist,
+                           x, (long long)n, y, scale_re, scale_im, tw);
     LQ_CHECK_LAUNCH();
 }
 

@@ -115,3 +115,104 @@ __device__ float2 *lds_fft(float2 *a, float2 *b, const float2 *__restrict__ tw, 
     }
     return src;
 }
+
+// ---------------------------------------------------------------- register radix-16
+// 16-point DFT in registers, natural order in and out; DIR +1 forward
+// (exp(-j 2 pi nk/16)), -1 backward.  Radix 4 x 4 with the W16 twiddles
+// between the two passes.
+template <int DIR>
+__device__ __forceinline__ void dft16(float2 (&v)[16])
+{
+    constexpr float C[16] = {1.0f,         0.92387953f,  0.70710678f,  0.38268343f,  0.0f,        -0.38268343f,
+                             -0.70710678f, -0.92387953f, -1.0f,        -0.92387953f, -0.70710678f, -0.38268343f,
+                             0.0f,         0.38268343f,  0.70710678f,  0.92387953f};
+    constexpr float S[16] = {0.0f,  0.38268343f,  0.70710678f,  0.92387953f,  1.0f,         0.92387953f,
+                             0.70710678f,  0.38268343f,  0.0f,  -0.38268343f, -0.70710678f, -0.92387953f,
+                             -1.0f, -0.92387953f, -0.70710678f, -0.38268343f};
+    float2 t[16];
+#pragma unroll
+    for (int q = 0; q < 4; q++) {
+        float2 a0 = v[q], a1 = v[4 + q], a2 = v[8 + q], a3 = v[12 + q];
+        dft4(a0, a1, a2, a3, DIR);
+        t[q] = a0;
+        if (q == 0) {
+            t[4] = a1;
+            t[8] = a2;
+            t[12] = a3;
+        } else {   // W16^{DIR q k0}
+            t[4 + q] = cmul(a1, make_float2(C[(1 * q) & 15], -DIR * S[(1 * q) & 15]));
+            t[8 + q] = cmul(a2, make_float2(C[(2 * q) & 15], -DIR * S[(2 * q) & 15]));
+            t[12 + q] = cmul(a3, make_float2(C[(3 * q) & 15], -DIR * S[(3 * q) & 15]));
+        }
+    }
+#pragma unroll
+    for (int k0 = 0; k0 < 4; k0++) {
+        float2 b0 = t[4 * k0 + 0], b1 = t[4 * k0 + 1], b2 = t[4 * k0 + 2], b3 = t[4 * k0 + 3];
+        dft4(b0, b1, b2, b3, DIR);
+        v[k0] = b0;
+        v[k0 + 4] = b1;
+        v[k0 + 8] = b2;
+        v[k0 + 12] = b3;
+    }
+}
+
+// 4096-point FFT by a 256-thread block, three register radix-16 passes and two
+// LDS transposes (lds: FFT4096_LDS float2).  In: thread t holds x[t + 256 n]
+// in v[n]; out: X[t + 256 k] in v[k].  tw: W_4096^e = exp(-2 pi i e/4096).
+// Every thread of the block calls it (it synchronises).
+//   pass 1: DFT16 over n (stride 256), twiddle W_4096^{t k2}
+//   pass 2: thread (k2 = u>>4, m0 = u&15) DFT16 over m1 of B[m0 + 16 m1][k2],
+//           twiddle W_256^{m0 j1}
+//   pass 3: thread (k2 = v&15, j1 = v>>4) DFT16 over m0 -> X[k2 + 16 j1 + 256 j0]
+#define FFT4096_LDS (16 * 272)
+// v[k] *= W_4096^{DIR e k}, k = 1..15, from two table reads (W^e, W^{4e}):
+// W^{e k} = W^{e (k & 3)} W^{e (k & 12)}, each factor at most two products
+// from a table value (keeps the cached-table traffic at 2 loads per pass)
+template <int DIR>
+__device__ __forceinline__ void twiddle16(float2 (&v)[16], const float2 *__restrict__ tw, int e)
+{
+    float2 w1 = tw[e & 4095], w4 = tw[(4 * e) & 4095];
+    if (DIR < 0) {
+        w1.y = -w1.y;
+        w4.y = -w4.y;
+    }
+    const float2 w2 = cmul(w1, w1), w3 = cmul(w2, w1);
+    const float2 w8 = cmul(w4, w4), w12 = cmul(w8, w4);
+    v[1] = cmul(v[1], w1);
+    v[2] = cmul(v[2], w2);
+    v[3] = cmul(v[3], w3);
+    v[4] = cmul(v[4], w4);
+    v[8] = cmul(v[8], w8);
+    v[12] = cmul(v[12], w12);
+    v[5] = cmul(v[5], cmul(w1, w4));
+    v[6] = cmul(v[6], cmul(w2, w4));
+    v[7] = cmul(v[7], cmul(w3, w4));
+    v[9] = cmul(v[9], cmul(w1, w8));
+    v[10] = cmul(v[10], cmul(w2, w8));
+    v[11] = cmul(v[11], cmul(w3, w8));
+    v[13] = cmul(v[13], cmul(w1, w12));
+    v[14] = cmul(v[14], cmul(w2, w12));
+    v[15] = cmul(v[15], cmul(w3, w12));
+}
+template <int DIR>
+__device__ __forceinline__ void fft4096_r16(float2 (&v)[16], float2 *lds, const float2 *__restrict__ tw, int t)
+{
+    dft16<DIR>(v);
+    twiddle16<DIR>(v, tw, t);   // W_4096^{t k}
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < 16; k++) lds[k * 272 + t] = v[k];   // row pad 16: conflict-free reads below
+    __syncthreads();
+    const int m0 = t & 15, k2 = t >> 4;
+#pragma unroll
+    for (int m = 0; m < 16; m++) v[m] = lds[k2 * 272 + m0 + 16 * m];
+    dft16<DIR>(v);
+    twiddle16<DIR>(v, tw, 16 * m0);   // W_256^{m0 j} = W_4096^{16 m0 j}
+    __syncthreads();
+#pragma unroll
+    for (int j = 0; j < 16; j++) lds[(k2 + 16 * j) * 17 + m0] = v[j];
+    __syncthreads();
+#pragma unroll
+    for (int m = 0; m < 16; m++) v[m] = lds[t * 17 + m];
+    dft16<DIR>(v);
+}
