@@ -48,15 +48,15 @@ static void run(const char *name, Params P, const float *hsub, unsigned nwg, int
     fflush(stdout);
 }
 
-template <int PF>
+template <int PF, int WPE = 4>
 static void run_v2(const char *name, Params P, const float *hsub, unsigned nwg, int iters)
 {
     hipEvent_t e0, e1;
     LQ_CHECK(hipEventCreate(&e0));
     LQ_CHECK(hipEventCreate(&e1));
-    hipLaunchKernelGGL((k_pfb2_an1024_v2<8, PF>), dim3(nwg), dim3(NT2), 0, 0, P, hsub, g_tw);
+    hipLaunchKernelGGL((k_pfb2_an1024_v2<8, PF, WPE>), dim3(nwg), dim3(NT2), 0, 0, P, hsub, g_tw);
     LQ_CHECK(hipEventRecord(e0));
-    for (int i = 0; i < iters; i++) hipLaunchKernelGGL((k_pfb2_an1024_v2<8, PF>), dim3(nwg), dim3(NT2), 0, 0, P, hsub, g_tw);
+    for (int i = 0; i < iters; i++) hipLaunchKernelGGL((k_pfb2_an1024_v2<8, PF, WPE>), dim3(nwg), dim3(NT2), 0, 0, P, hsub, g_tw);
     LQ_CHECK(hipEventRecord(e1));
     LQ_CHECK(hipEventSynchronize(e1));
     float ms;
@@ -106,11 +106,20 @@ int main()
     P.gpw = (int)gpw;
     P.gend = ngroups;
     const int it = 10;
-    for (int rep = 0; rep < 2; rep++) run<10, 2, 4, 1, 0>("warm", P, hsub, nwg, it);
+    for (int rep = 0; rep < 2; rep++) run<10, 2, 6, 1, 0>("warm", P, hsub, nwg, it);
+    Params P2 = P;
+    const long long ng8 = nb / 8;
     for (int rep = 0; rep < 2; rep++) {
-        run<10, 2, 4, 1, 0>("PF4", P, hsub, nwg, it);
-        run<10, 2, 6, 1, 0>("PF6", P, hsub, nwg, it);
-        run<10, 2, 8, 1, 0>("PF8", P, hsub, nwg, it);
+        run<10, 2, 6, 1, 0>("library", P, hsub, nwg, it);
+        for (int target : {256, 512}) {
+            long long gpw8 = (ng8 + target - 1) / target;
+            const unsigned nwg8 = (unsigned)((ng8 + gpw8 - 1) / gpw8);
+            P2.gs0 = 0;
+            P2.gpw = (int)gpw8;
+            P2.gend = ng8;
+            run_v2<4, 2>("v2 8 waves/CU PF4", P2, hsub, nwg8, it);
+            run_v2<2, 2>("v2 8 waves/CU PF2", P2, hsub, nwg8, it);
+        }
     }
     return 0;
 }

@@ -73,8 +73,8 @@ __device__ __forceinline__ void fft1024_store(float2 *B, long long b, const Para
 // is free.  Iterations are unrolled in pairs so the 8-row register ring is
 // indexed with constants.
 constexpr int NT2 = 512;
-template <int L, int PF = 4>
-__global__ __launch_bounds__(NT2, 4) void k_pfb2_an1024_v2(Params P, const float *__restrict__ hsub,
+template <int L, int PF = 4, int WPE = 4>
+__global__ __launch_bounds__(NT2, WPE) void k_pfb2_an1024_v2(Params P, const float *__restrict__ hsub,
                                                             const float2 *__restrict__ tw4096)
 {
     static_assert(L <= NS && PF <= 4, "ring / prefetch");
