@@ -21,6 +21,7 @@
 //  firpfbch synthesizer firpfbch.c:314-336: z_b = IFFT(X_b),
 //        y_b[i] = sum_{n<p} h[i+nM] z_{b-n}[i]
 #include "lq_device.h"
+#include "lq_fft1024.h"
 #include "lq_kernels.h"
 
 #include <cmath>
@@ -243,6 +244,157 @@ __global__ void k_pfb_syn_out(int M, int p, const TC *__restrict__ hsub, const f
     y[e] = acc;
 }
 
+// ---------------------------------------------------------------- run kernels
+// One lane per (column, run of RUN consecutive blocks): the column's taps stay
+// in registers and a P-deep shift register of the column's history slides
+// along the run, so each input is loaded ~(RUN + P - 1)/RUN times instead of
+// P times and each tap once per run (the per-element kernels above re-load
+// both for every output).
+constexpr int RUN = 64;
+
+// firpfbch analyzer X (firpfbch.c:346-409): X[b][j] = sum_n h[i*P + n] x[(b-n)M + j], i = M-1-j
+template <int P, typename TC>
+__global__ __launch_bounds__(256) void k_pfb_an_X_run(int M, const TC *__restrict__ hsub,
+                                                      const float2 *__restrict__ hist, const float2 *__restrict__ x,
+                                                      long long nblocks, float2 *__restrict__ X)
+{
+    const long long e = (long long)blockIdx.x * 256 + threadIdx.x;
+    const int j = (int)(e % M);
+    const long long b0 = (e / M) * RUN;
+    if (b0 >= nblocks) return;
+    const int i = M - 1 - j, HL = (P - 1) * M;
+    TC h[P];
+#pragma unroll
+    for (int n = 0; n < P; n++) h[n] = hsub[i * P + n];
+    float2 w[P];   // w[n] = x[(b - n) M + j]
+#pragma unroll
+    for (int n = 1; n < P; n++) w[n] = ext_load(hist, HL, x, (b0 - n) * M + j);
+    const long long be = b0 + RUN < nblocks ? b0 + RUN : nblocks;
+    for (long long b = b0; b < be; b++) {
+        w[0] = x[b * M + j];
+        float2 acc = make_float2(0.f, 0.f);
+#pragma unroll
+        for (int n = 0; n < P; n++) acc = pfb_mac(h[n], w[n], acc);
+        X[b * M + j] = acc;
+#pragma unroll
+        for (int n = P - 1; n > 0; n--) w[n] = w[n - 1];
+    }
+}
+
+// firpfbch synthesizer output (firpfbch.c:314-336): y[b][i] = sum_n h[i*P + n] Z[(P-1+b-n) M + i]
+template <int P, typename TC>
+__global__ __launch_bounds__(256) void k_pfb_syn_out_run(int M, const TC *__restrict__ hsub,
+                                                         const float2 *__restrict__ Z, long long nblocks,
+                                                         float2 *__restrict__ y)
+{
+    const long long e = (long long)blockIdx.x * 256 + threadIdx.x;
+    const int i = (int)(e % M);
+    const long long b0 = (e / M) * RUN;
+    if (b0 >= nblocks) return;
+    TC h[P];
+#pragma unroll
+    for (int n = 0; n < P; n++) h[n] = hsub[i * P + n];
+    float2 w[P];   // w[n] = Z[(P-1+b-n) M + i]
+#pragma unroll
+    for (int n = 1; n < P; n++) w[n] = Z[(P - 1 + b0 - n) * M + i];
+    const long long be = b0 + RUN < nblocks ? b0 + RUN : nblocks;
+    for (long long b = b0; b < be; b++) {
+        w[0] = Z[(P - 1 + b) * M + i];
+        float2 acc = make_float2(0.f, 0.f);
+#pragma unroll
+        for (int n = 0; n < P; n++) acc = pfb_mac(h[n], w[n], acc);
+        y[b * M + i] = acc;
+#pragma unroll
+        for (int n = P - 1; n > 0; n--) w[n] = w[n - 1];
+    }
+}
+
+// firpfbch2 synthesizer output (firpfbch2.c:287-335): block b (parity f) uses
+// column c = i + f M/2: y = sum_n h0[n] z_{b-2n}[c] + h1[n] z_{b-1-2n}[c].
+// The lane keeps 2L-deep histories of both of its columns.
+template <int L>
+__global__ __launch_bounds__(256) void k_pfb2_syn_out_run(int M, const float *__restrict__ hsub,
+                                                          const float2 *__restrict__ Z, long long nblocks, int p0,
+                                                          float2 *__restrict__ y)
+{
+    const int M2 = M / 2, HB = 2 * L - 1;
+    const long long e = (long long)blockIdx.x * 256 + threadIdx.x;
+    const int i = (int)(e % M2);
+    const long long b0 = (e / M2) * RUN;
+    if (b0 >= nblocks) return;
+    float h0[L], h1[L];
+#pragma unroll
+    for (int n = 0; n < L; n++) {
+        h0[n] = hsub[i * L + n];
+        h1[n] = hsub[(i + M2) * L + n];
+    }
+    float2 wa[2 * L], wb[2 * L];   // columns i and i + M/2; w[k] = z_{b-k}
+#pragma unroll
+    for (int k = 1; k < 2 * L; k++) {
+        wa[k] = Z[(HB + b0 - k) * M + i];
+        wb[k] = Z[(HB + b0 - k) * M + i + M2];
+    }
+    const long long be = b0 + RUN < nblocks ? b0 + RUN : nblocks;
+    for (long long b = b0; b < be; b++) {
+        wa[0] = Z[(HB + b) * M + i];
+        wb[0] = Z[(HB + b) * M + i + M2];
+        const bool f = ((p0 + b) & 1) != 0;
+        float2 acc0 = make_float2(0.f, 0.f), acc1 = make_float2(0.f, 0.f);
+#pragma unroll
+        for (int n = 0; n < L; n++) {
+            const float2 z0 = f ? wb[2 * n] : wa[2 * n];
+            const float2 z1 = f ? wb[2 * n + 1] : wa[2 * n + 1];
+            acc0.x = fmaf(h0[n], z0.x, acc0.x);
+            acc0.y = fmaf(h0[n], z0.y, acc0.y);
+            acc1.x = fmaf(h1[n], z1.x, acc1.x);
+            acc1.y = fmaf(h1[n], z1.y, acc1.y);
+        }
+        y[b * M2 + i] = cadd(acc0, acc1);
+#pragma unroll
+        for (int k = 2 * L - 1; k > 0; k--) {
+            wa[k] = wa[k - 1];
+            wb[k] = wb[k - 1];
+        }
+    }
+}
+
+// dispatch helpers: compile-time ring depths for the common shapes, else the
+// per-element kernels
+template <typename TC>
+bool launch_an_X_run(int M, int p, const void *hsub, const void *hist, const void *x, long long nb, void *X,
+                     hipStream_t st)
+{
+    const long long threads = (long long)M * ((nb + RUN - 1) / RUN);
+    const dim3 g((unsigned)((threads + 255) / 256));
+#define LQ_AX(PP)                                                                                                 \
+    case PP:                                                                                                      \
+        hipLaunchKernelGGL((k_pfb_an_X_run<PP, TC>), g, dim3(256), 0, st, M, (const TC *)hsub,                   \
+                           (const float2 *)hist, (const float2 *)x, nb, (float2 *)X);                             \
+        return true;
+    switch (p) {
+        LQ_AX(1) LQ_AX(2) LQ_AX(4) LQ_AX(6) LQ_AX(8) LQ_AX(10) LQ_AX(12) LQ_AX(14) LQ_AX(16)
+    }
+#undef LQ_AX
+    return false;
+}
+
+template <typename TC>
+bool launch_syn_run(int M, int p, const void *hsub, const void *Z, long long nb, void *y, hipStream_t st)
+{
+    const long long threads = (long long)M * ((nb + RUN - 1) / RUN);
+    const dim3 g((unsigned)((threads + 255) / 256));
+#define LQ_SY(PP)                                                                                                 \
+    case PP:                                                                                                      \
+        hipLaunchKernelGGL((k_pfb_syn_out_run<PP, TC>), g, dim3(256), 0, st, M, (const TC *)hsub,                \
+                           (const float2 *)Z, nb, (float2 *)y);                                                   \
+        return true;
+    switch (p) {
+        LQ_SY(1) LQ_SY(2) LQ_SY(4) LQ_SY(6) LQ_SY(8) LQ_SY(10) LQ_SY(12) LQ_SY(14) LQ_SY(16)
+    }
+#undef LQ_SY
+    return false;
+}
+
 template <int M>
 void launch_pfb2_an(int m, const void *hsub, const void *hist, const void *x, long long nblocks, int p0, void *Y,
                     hipStream_t st)
@@ -253,6 +405,66 @@ void launch_pfb2_an(int m, const void *hsub, const void *hist, const void *x, lo
                        (const float2 *)hist, (const float2 *)x, nblocks, p0, (float2 *)Y,
                        (const float2 *)lqrt_twiddles());
     LQ_CHECK_LAUNCH();
+}
+
+// batched 1024-point transforms, one wave each (lq_fft1024.h); 4 waves per workgroup
+template <int DIR>
+__global__ __launch_bounds__(256) void k_fft1024_batch(const float2 *__restrict__ x, float2 *__restrict__ y,
+                                                        long long batch, float s1, float s2, int use_s1,
+                                                        int use_s2, const float2 *__restrict__ tw4096)
+{
+    __shared__ __attribute__((aligned(16))) float2 buf[4 * 1088];
+    __shared__ __attribute__((aligned(16))) float2 tw1[1024];
+    __shared__ __attribute__((aligned(16))) float2 tw2[64];
+    f1k_tables<DIR>(tw1, tw2, tw4096);
+    __syncthreads();
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    float2 *B = buf + wave * 1088;
+    for (long long b = (long long)blockIdx.x * 4 + wave; b < batch; b += (long long)gridDim.x * 4) {
+        float2 v[16];
+        const float2 *xb = x + b * 1024;
+#pragma unroll
+        for (int k = 0; k < 16; k++) v[k] = xb[lane + 64 * k];
+        fft1024_wave<DIR>(v, B, tw1, tw2, lane);
+        typedef float v4f __attribute__((ext_vector_type(4)));
+        v4f *yb = reinterpret_cast<v4f *>(y + b * 1024);
+#pragma unroll
+        for (int q = 0; q < 8; q++) {
+            const int o = 2 * (lane + 64 * q);
+            v4f val = *reinterpret_cast<const v4f *>(B + o + 4 * (o >> 8));
+            if (use_s1) val = val * s1;
+            if (use_s2) val = val * s2;
+            yb[o >> 1] = val;
+        }
+        f1k_wave_fence();   // B is reused by the next transform of this wave
+    }
+}
+
+// batched 4096-point transforms, one 256-thread workgroup each (fft4096_r16);
+// the register transform needs ~2 waves/SIMD worth of VGPRs
+template <int DIR>
+__global__ __launch_bounds__(256, 2) void k_fft4096_batch(const float2 *__restrict__ x, float2 *__restrict__ y,
+                                                           long long batch, float s1, float s2, int use_s1,
+                                                           int use_s2, const float2 *__restrict__ tw4096)
+{
+    __shared__ __attribute__((aligned(16))) float2 lds[FFT4096_LDS];
+    const int t = threadIdx.x;
+    for (long long b = blockIdx.x; b < batch; b += gridDim.x) {
+        float2 v[16];
+        const float2 *xb = x + b * 4096;
+#pragma unroll
+        for (int k = 0; k < 16; k++) v[k] = xb[t + 256 * k];
+        fft4096_r16<DIR>(v, lds, tw4096, t);
+        float2 *yb = y + b * 4096;
+#pragma unroll
+        for (int k = 0; k < 16; k++) {
+            float2 w = v[k];
+            if (use_s1) w = cscale(w, s1);
+            if (use_s2) w = cscale(w, s2);
+            yb[t + 256 * k] = w;
+        }
+        __syncthreads();   // lds is reused by the next transform
+    }
 }
 
 template <int N>
@@ -282,9 +494,30 @@ void fft_batch_scaled(unsigned n, int dir, const void *x, void *y, long long bat
     case 128: launch_fft_batch<128>(x, y, batch, dir, s1, s2, u1, u2, st); return;
     case 256: launch_fft_batch<256>(x, y, batch, dir, s1, s2, u1, u2, st); return;
     case 512: launch_fft_batch<512>(x, y, batch, dir, s1, s2, u1, u2, st); return;
-    case 1024: launch_fft_batch<1024>(x, y, batch, dir, s1, s2, u1, u2, st); return;
+    case 1024: {
+        const long long g = (batch + 3) / 4;
+        const unsigned grid = (unsigned)(g < 4096 ? g : 4096);
+        if (dir > 0)
+            hipLaunchKernelGGL(k_fft1024_batch<+1>, dim3(grid), dim3(256), 0, st, (const float2 *)x, (float2 *)y,
+                               batch, s1, s2, u1, u2, (const float2 *)lqrt_twiddles());
+        else
+            hipLaunchKernelGGL(k_fft1024_batch<-1>, dim3(grid), dim3(256), 0, st, (const float2 *)x, (float2 *)y,
+                               batch, s1, s2, u1, u2, (const float2 *)lqrt_twiddles());
+        LQ_CHECK_LAUNCH();
+        return;
+    }
     case 2048: launch_fft_batch<2048>(x, y, batch, dir, s1, s2, u1, u2, st); return;
-    case 4096: launch_fft_batch<4096>(x, y, batch, dir, s1, s2, u1, u2, st); return;
+    case 4096: {
+        const unsigned grid = (unsigned)(batch < 2048 ? batch : 2048);
+        if (dir > 0)
+            hipLaunchKernelGGL(k_fft4096_batch<+1>, dim3(grid), dim3(256), 0, st, (const float2 *)x, (float2 *)y,
+                               batch, s1, s2, u1, u2, (const float2 *)lqrt_twiddles());
+        else
+            hipLaunchKernelGGL(k_fft4096_batch<-1>, dim3(grid), dim3(256), 0, st, (const float2 *)x, (float2 *)y,
+                               batch, s1, s2, u1, u2, (const float2 *)lqrt_twiddles());
+        LQ_CHECK_LAUNCH();
+        return;
+    }
     default:
         break;
     }
@@ -355,8 +588,20 @@ extern "C" void lqk_firpfbch2_synthesizer(unsigned int M, unsigned int m, const 
     LQ_CHECK(hipMemcpyAsync(Z, state, HB * M * sizeof(float2), hipMemcpyDeviceToDevice, st));
     fft_batch_scaled(M, -1, X, Z + HB * M, (long long)nblocks, 1.0f / (float)M, (float)(M / 2), 1, 1, st);
     const long long tot = (long long)nblocks * (M / 2);
-    hipLaunchKernelGGL(k_pfb2_syn_out, dim3((unsigned)((tot + 255) / 256)), dim3(256), 0, st, (int)M, (int)m,
-                       (const float *)hsub, (const float2 *)Z, (long long)nblocks, p0, (float2 *)Y);
+    const long long runs = (long long)(M / 2) * (((long long)nblocks + RUN - 1) / RUN);
+    const dim3 gr((unsigned)((runs + 255) / 256));
+    if (m == 4)
+        hipLaunchKernelGGL(k_pfb2_syn_out_run<8>, gr, dim3(256), 0, st, (int)M, (const float *)hsub,
+                           (const float2 *)Z, (long long)nblocks, p0, (float2 *)Y);
+    else if (m == 2)
+        hipLaunchKernelGGL(k_pfb2_syn_out_run<4>, gr, dim3(256), 0, st, (int)M, (const float *)hsub,
+                           (const float2 *)Z, (long long)nblocks, p0, (float2 *)Y);
+    else if (m == 3)
+        hipLaunchKernelGGL(k_pfb2_syn_out_run<6>, gr, dim3(256), 0, st, (int)M, (const float *)hsub,
+                           (const float2 *)Z, (long long)nblocks, p0, (float2 *)Y);
+    else
+        hipLaunchKernelGGL(k_pfb2_syn_out, dim3((unsigned)((tot + 255) / 256)), dim3(256), 0, st, (int)M, (int)m,
+                           (const float *)hsub, (const float2 *)Z, (long long)nblocks, p0, (float2 *)Y);
     LQ_CHECK_LAUNCH();
     // keep the newest HB z vectors as the state for the next call
     LQ_CHECK(hipMemcpyAsync(state, Z + (long long)nblocks * M, HB * M * sizeof(float2), hipMemcpyDeviceToDevice,
@@ -371,10 +616,12 @@ extern "C" void lqk_firpfbch_analyzer(int ctaps, unsigned int M, unsigned int p,
     const long long tot = (long long)nblocks * M;
     const dim3 grid((unsigned)((tot + 255) / 256));
     // X is formed in Y then transformed in place
-    if (ctaps)
+    const bool run = ctaps ? launch_an_X_run<float2>((int)M, (int)p, hsub, hist, x, (long long)nblocks, Y, st)
+                           : launch_an_X_run<float>((int)M, (int)p, hsub, hist, x, (long long)nblocks, Y, st);
+    if (!run && ctaps)
         hipLaunchKernelGGL(k_pfb_an_X<float2>, grid, dim3(256), 0, st, (int)M, (int)p, (const float2 *)hsub,
                            (const float2 *)hist, (const float2 *)x, (long long)nblocks, (float2 *)Y);
-    else
+    else if (!run)
         hipLaunchKernelGGL(k_pfb_an_X<float>, grid, dim3(256), 0, st, (int)M, (int)p, (const float *)hsub,
                            (const float2 *)hist, (const float2 *)x, (long long)nblocks, (float2 *)Y);
     LQ_CHECK_LAUNCH();
@@ -394,10 +641,12 @@ extern "C" void lqk_firpfbch_synthesizer(int ctaps, unsigned int M, unsigned int
     fft_batch_scaled(M, -1, X, Z + HB * M, (long long)nblocks, 1.f, 1.f, 0, 0, st);
     const long long tot = (long long)nblocks * M;
     const dim3 grid((unsigned)((tot + 255) / 256));
-    if (ctaps)
+    const bool run = ctaps ? launch_syn_run<float2>((int)M, (int)p, hsub, Z, (long long)nblocks, y, st)
+                           : launch_syn_run<float>((int)M, (int)p, hsub, Z, (long long)nblocks, y, st);
+    if (!run && ctaps)
         hipLaunchKernelGGL(k_pfb_syn_out<float2>, grid, dim3(256), 0, st, (int)M, (int)p, (const float2 *)hsub,
                            (const float2 *)Z, (long long)nblocks, (float2 *)y);
-    else
+    else if (!run)
         hipLaunchKernelGGL(k_pfb_syn_out<float>, grid, dim3(256), 0, st, (int)M, (int)p, (const float *)hsub,
                            (const float2 *)Z, (long long)nblocks, (float2 *)y);
     LQ_CHECK_LAUNCH();
