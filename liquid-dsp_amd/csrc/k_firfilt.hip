@@ -323,6 +323,96 @@ __global__ __launch_bounds__(NT) void k_firdecim(const typename kt<KIND>::T *__r
     y[o] = acc;
 }
 
+// Phase-layout decimator.  With the filter padded to QC*M taps and split
+// k = q*M + r, output o is
+//     y[o] = sum_r sum_q hq[r*QC + q] x[(o - q)*M - r],   hq[r*QC + q] = h[q*M + r],
+// i.e. M short filters, filter r running over input phase (-r mod M) at the
+// output rate.  The workgroup stages its input tile in LDS de-interleaved by
+// phase, P[ph][j] = tile[j*M + ph], one padded row per phase; lane t produces
+// R consecutive outputs, sliding a QCT+R-1 register window along each phase
+// row with the taps wave-uniform (scalar loads), so a phase costs QCT+R-1 LDS
+// reads for QCT*R multiply-adds.  Row element j sits at j + (j >> 5): lanes R
+// elements apart then spread over all banks.
+// Tile: outputs [o0, o0+TO), TO = NT*R; tile sample u = input s0 + u with
+// s0 = o0*M - QC*M + 1, u = j*M + ph for j < TO + QC - 1.
+__host__ __device__ __forceinline__ int dph_pitch(int J) { return J + (J >> 5) + 1; }
+__device__ __forceinline__ int dph_col(int j) { return j + (j >> 5); }
+
+template <int KIND, int QCT, int R, int NT_>
+__global__ __launch_bounds__(NT_) void k_firdecim_ph(const typename kt<KIND>::T *__restrict__ hist, int hl1,
+                                                     const typename kt<KIND>::T *__restrict__ x, long long nout,
+                                                     int M, int QC, typename kt<KIND>::T *__restrict__ y,
+                                                     const typename kt<KIND>::TC *__restrict__ hq)
+{
+    typedef typename kt<KIND>::T T;
+    typedef typename kt<KIND>::TC TC;
+    constexpr int TO = NT_ * R;
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    T *P = reinterpret_cast<T *>(smem);
+    const int J = TO + QC - 1;
+    const int pitch = dph_pitch(J);
+    const long long o0 = (long long)blockIdx.x * TO;
+    const long long nin = nout * M;
+    // stage: aligned start s0 - 1 (o0*M and QC*M are multiples of 4), tile
+    // sample u = v - 1
+    const long long sa = o0 * M - (long long)QC * M;
+    const int S = J * M + 1;
+    constexpr int VW = 16 / (int)sizeof(T);
+    const bool vec_ok = (reinterpret_cast<uintptr_t>(x) & 15) == 0;
+    for (int v0 = threadIdx.x * VW; v0 < S; v0 += NT_ * VW) {
+        const long long s = sa + v0;
+        T e[VW];
+        if (vec_ok && s >= 0 && s + VW <= nin) {
+            load16<T>(x + s, e);
+        } else {
+#pragma unroll
+            for (int i = 0; i < VW; i++) {
+                const long long si = s + i;
+                T val = zero<T>();
+                if (si < 0) {
+                    if (si >= -(long long)hl1) val = hist[hl1 + si];
+                } else if (si < nin) {
+                    val = x[si];
+                }
+                e[i] = val;
+            }
+        }
+#pragma unroll
+        for (int i = 0; i < VW; i++) {
+            const int u = v0 + i - 1;
+            if (u >= 0 && u < S - 1) {
+                const int j = u / M, ph = u - j * M;
+                P[ph * pitch + dph_col(j)] = e[i];
+            }
+        }
+    }
+    __syncthreads();
+    T acc[R];
+#pragma unroll
+    for (int rr = 0; rr < R; rr++) acc[rr] = zero<T>();
+    const int tb = threadIdx.x * R;
+    for (int ph = 0; ph < M; ph++) {
+        const T *row = P + ph * pitch;
+        const TC *hr = hq + (M - 1 - ph) * QC;
+        for (int c = 0; c < QC; c += QCT) {
+            const int base = tb + QC - c - QCT; // window start of this tap chunk
+            T w[QCT + R - 1];
+#pragma unroll
+            for (int i = 0; i < QCT + R - 1; i++) w[i] = row[dph_col(base + i)];
+#pragma unroll
+            for (int q = 0; q < QCT; q++) {
+                const TC h = hr[c + q];
+#pragma unroll
+                for (int rr = 0; rr < R; rr++) mac(acc[rr], h, w[QCT - 1 + rr - q]);
+            }
+        }
+    }
+    const long long o = o0 + tb;
+#pragma unroll
+    for (int rr = 0; rr < R; rr++)
+        if (o + rr < nout) y[o + rr] = acc[rr];
+}
+
 // ------------------------------------------------------------------ firinterp
 // one input sample per lane -> M outputs; hpoly[p*L + l] = h'[p + l*M]
 template <int KIND>
@@ -494,6 +584,71 @@ extern "C" void lqk_firdecim(const lqk_fir_desc *d, unsigned int M, const void *
         break;
     }
     LQ_CHECK_LAUNCH();
+}
+
+namespace {
+template <int KIND, int QCT, int R, int NT_>
+void launch_decim_ph(unsigned M, unsigned QC, const void *hq, unsigned hl1, const void *hist, const void *x,
+                     long long nout, void *y, size_t lds, hipStream_t st)
+{
+    typedef typename kt<KIND>::T T;
+    typedef typename kt<KIND>::TC TC;
+    const long long TO = (long long)NT_ * R;
+    const unsigned nb = (unsigned)((nout + TO - 1) / TO);
+    hipLaunchKernelGGL((k_firdecim_ph<KIND, QCT, R, NT_>), dim3(nb), dim3(NT_), lds, st, (const T *)hist,
+                       (int)hl1, (const T *)x, nout, (int)M, (int)QC, (T *)y, (const TC *)hq);
+    LQ_CHECK_LAUNCH();
+}
+
+template <int KIND, int QCT>
+int decim_ph_shape(unsigned M, unsigned QC, const void *hq, unsigned hl1, const void *hist, const void *x,
+                   long long nout, void *y, hipStream_t st)
+{
+    const size_t es = elem_size(KIND);
+    const size_t lds_a = (size_t)M * dph_pitch(256 * 2 + (int)QC - 1) * es;
+    const size_t lds_b = (size_t)M * dph_pitch(64 + (int)QC - 1) * es;
+    if (lds_a <= 64 * 1024) launch_decim_ph<KIND, QCT, 2, 256>(M, QC, hq, hl1, hist, x, nout, y, lds_a, st);
+    else if (lds_b <= 160 * 1024) launch_decim_ph<KIND, QCT, 1, 64>(M, QC, hq, hl1, hist, x, nout, y, lds_b, st);
+    else return -1;
+    return 0;
+}
+
+template <int KIND>
+int decim_ph_qct(unsigned M, unsigned QC, const void *hq, unsigned hl1, const void *hist, const void *x,
+                 long long nout, void *y, hipStream_t st)
+{
+    switch (QC) {
+    case 4: return decim_ph_shape<KIND, 4>(M, QC, hq, hl1, hist, x, nout, y, st);
+    case 8: return decim_ph_shape<KIND, 8>(M, QC, hq, hl1, hist, x, nout, y, st);
+    case 16: return decim_ph_shape<KIND, 16>(M, QC, hq, hl1, hist, x, nout, y, st);
+    case 32: return decim_ph_shape<KIND, 32>(M, QC, hq, hl1, hist, x, nout, y, st);
+    default:
+        if (QC % 16) return -1;
+        return decim_ph_shape<KIND, 16>(M, QC, hq, hl1, hist, x, nout, y, st);
+    }
+}
+} // namespace
+
+extern "C" unsigned lqk_firdecim_ph_qc(unsigned M, unsigned hlen)
+{
+    const unsigned q0 = (hlen + M - 1) / M;
+    if (q0 <= 4) return 4;
+    if (q0 <= 8) return 8;
+    if (q0 <= 16) return 16;
+    if (q0 <= 32) return 32;
+    return (q0 + 15) / 16 * 16;
+}
+
+extern "C" int lqk_firdecim_ph(int kind, unsigned int M, unsigned int QC, const void *hq, unsigned int hl1,
+                               const void *hist, const void *x, unsigned long long nout, void *y, void *stream)
+{
+    if (nout == 0) return 0;
+    hipStream_t st = (hipStream_t)stream;
+    switch (kind) {
+    case 0: return decim_ph_qct<0>(M, QC, hq, hl1, hist, x, (long long)nout, y, st);
+    case 1: return decim_ph_qct<1>(M, QC, hq, hl1, hist, x, (long long)nout, y, st);
+    default: return decim_ph_qct<2>(M, QC, hq, hl1, hist, x, (long long)nout, y, st);
+    }
 }
 
 extern "C" void lqk_firinterp(int kind, const void *hpoly, unsigned int M, unsigned int L, float sre, float sim,

@@ -69,6 +69,13 @@ void lqk_fir_single(const lqk_fir_desc *d, const void *win, void *y, void *strea
  * interp: y[i*M + p] = scale * sum_{l<L} h[p + l*M] ext[i - l]  (i < n) */
 void lqk_firdecim(const lqk_fir_desc *d, unsigned int M, const void *hist, const void *x,
                   unsigned long long nout, void *y, void *stream);
+/* phase-layout decimator: hq = M x QC phase-major padded taps,
+ * hq[r*QC + q] = h[q*M + r] (0 past hlen), QC = lqk_firdecim_ph_qc(M, hlen);
+ * hist = the previous hl1 = hlen-1 inputs.  Returns -1 (nothing launched)
+ * when the tile does not fit in LDS. */
+unsigned lqk_firdecim_ph_qc(unsigned M, unsigned hlen);
+int lqk_firdecim_ph(int kind, unsigned int M, unsigned int QC, const void *hq, unsigned int hl1,
+                    const void *hist, const void *x, unsigned long long nout, void *y, void *stream);
 void lqk_firinterp(int kind, const void *hpoly /* M x L, h[p + l*M] */, unsigned int M,
                    unsigned int L, float scale_re, float scale_im, const void *hist, const void *x,
                    unsigned long long n, void *y, void *stream);

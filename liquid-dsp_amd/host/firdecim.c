@@ -29,6 +29,8 @@ typedef struct {
     float *h;          /* host copy, hlen coefficients of csz bytes */
     lqk_fir_desc d;
     void *d_hpad;
+    void *d_hq;        /* M x QC phase-major taps for the phase-layout kernel */
+    unsigned int QC;
     void *d_hist[2];   /* last hlen-1 inputs */
     int cur;
     lq_ctx ctx;
@@ -51,9 +53,19 @@ static lq_decim *lq_decim_create(int kind, unsigned int M, const float *h, unsig
     lq_ctx_init(&q->ctx);
     q->d_hpad = lqrt_malloc(hlen * q->csz);
     lqrt_h2d(q->d_hpad, q->h, hlen * q->csz, q->ctx.stream);
+    /* k = qM + r -> hq[r*QC + q] (zero past hlen) */
+    q->QC = lqk_firdecim_ph_qc(M, hlen);
+    const size_t nq = (size_t)M * q->QC, cf = q->csz / sizeof(float);
+    float *hq = (float *)lq_xmalloc(nq * q->csz);
+    memset(hq, 0, nq * q->csz);
+    for (unsigned int k = 0; k < hlen; k++)
+        memcpy(hq + ((size_t)(k % M) * q->QC + k / M) * cf, q->h + (size_t)k * cf, q->csz);
+    q->d_hq = lqrt_malloc(nq * q->csz);
+    lqrt_h2d(q->d_hq, hq, nq * q->csz, q->ctx.stream);
     q->d_hist[0] = lqrt_malloc((size_t)hlen * q->esz);
     q->d_hist[1] = lqrt_malloc((size_t)hlen * q->esz);
     lqrt_sync(q->ctx.stream);
+    free(hq);
     q->d.kind = kind;
     q->d.hlen = hlen;
     q->d.hc = hlen; /* the decimator kernel takes HP = hc * nchunk directly */
@@ -80,6 +92,7 @@ static void lq_decim_destroy(lq_decim *q)
 {
     lqrt_sync(q->ctx.stream);
     lqrt_free(q->d_hpad);
+    lqrt_free(q->d_hq);
     lqrt_free(q->d_hist[0]);
     lqrt_free(q->d_hist[1]);
     lq_devbuf_free(&q->xbuf);
@@ -109,7 +122,8 @@ static void lq_decim_block_dev(lq_decim *q, const void *dx, unsigned long long n
 {
     if (nout == 0) return;
     void *hold = q->d_hist[q->cur], *hnew = q->d_hist[q->cur ^ 1];
-    lqk_firdecim(&q->d, q->M, hold, dx, nout, dy, q->ctx.stream);
+    if (lqk_firdecim_ph(q->kind, q->M, q->QC, q->d_hq, q->hlen - 1, hold, dx, nout, dy, q->ctx.stream) != 0)
+        lqk_firdecim(&q->d, q->M, hold, dx, nout, dy, q->ctx.stream);
     if (q->hlen > 1) {
         lqk_window_append(q->kind != LQ_RRRF, hold, q->hlen - 1, dx, nout * q->M, hnew, q->ctx.stream);
         q->cur ^= 1;

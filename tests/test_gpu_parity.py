@@ -205,6 +205,41 @@ def test_firdecim_vs_oracle(M, m, t):
 
 
 @pytest.mark.parametrize("t", ["rrrf", "crcf", "cccf"])
+@pytest.mark.parametrize("M,hlen", [(1, 7), (3, 29), (2, 80), (5, 333), (7, 8), (200, 801), (8, 2)])
+def test_firdecim_ragged_vs_oracle(M, hlen, t):
+    """arbitrary taps (hlen not a multiple of M, long filters split in tap
+    chunks, one-tap-per-phase filters, decimation factors whose tile exceeds
+    the fast kernel's LDS shape) over block sizes that are not tile multiples"""
+    r = rng(M * 7 + hlen)
+    x = samples(r, t, M * 3001)
+    h = coefs(r, t, hlen)
+    g, o = LQ.FirDecim(M, h, t=t), O.FirDecim(TYPES[t], M, h)
+    cuts = [0, 1, 517, 2048 + 3, 3001]
+    y = np.concatenate([g.execute_block(x[M * a: M * b]) for a, b in zip(cuts[:-1], cuts[1:])])
+    assert G.nrm_err(y, o.execute_block(x)) < NRM
+
+
+@pytest.mark.parametrize("t", ["rrrf", "crcf"])
+def test_firdecim_device_path_unaligned(t):
+    """device pointers that are not 16-byte aligned (the staging loop's
+    vector loads must not be taken)"""
+    M, r = 4, rng(77)
+    x = samples(r, t, M * 70001 + 1)
+    h = coefs(r, t, 37)
+    esz = 4 if t == "rrrf" else 8
+    g = LQ.FirDecim(M, h, t=t)
+    fn = getattr(LQ.lib(), "firdecim_%s_execute_block_dev" % t)
+    bx = LQ.DeviceBuffer.from_array(x)
+    by = LQ.DeviceBuffer((70000 + 1) * esz)
+    fn(g.q, bx.p + esz, 30001, by.p + esz)
+    fn(g.q, bx.p + esz + 30001 * M * esz, 39999, by.p + esz + 30001 * esz)
+    LQ.lib().liquid_mi355x_device_synchronize()
+    y = by.to_array(np.float32 if t == "rrrf" else np.complex64, 70001)[1:]
+    ref = O.FirDecim(TYPES[t], M, h).execute_block(x[1:])[:70000]
+    assert G.nrm_err(y, ref) < NRM
+
+
+@pytest.mark.parametrize("t", ["rrrf", "crcf", "cccf"])
 @pytest.mark.parametrize("M,m", [(2, 3), (4, 3), (8, 5), (32, 2)])
 def test_firinterp_vs_oracle(M, m, t):
     r = rng(M + 1)
