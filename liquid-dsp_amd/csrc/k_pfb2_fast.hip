@@ -14,16 +14,22 @@
 //    SIMD) owns all 1024 columns, one per lane, with the column's even- and
 //    odd-block taps and an 8-deep register ring.  Rows stream through the
 //    ring, so every input sample is read from HBM once per workgroup
-//    segment.  Eight rows per iteration complete sixteen blocks; six of the
-//    next eight rows are prefetched into registers while the FFTs run (the
-//    tap selection is per lane, outside the loop, so the row loop and the
-//    quad butterflies carry no per-lane selects: 122 VGPRs, no spills).
+//    segment.  Eight rows per iteration complete sixteen blocks; all eight
+//    rows of the next iteration are prefetched into registers while the FFTs
+//    run (the tap selection is per lane, outside the loop, so the row loop
+//    carries no per-lane selects: 108 VGPRs, no spills).
 //  * X of each block goes to an LDS ring (17 block buffers, 148 KB); after a
-//    barrier each wave runs one 1024-point IFFT in registers: 16-point DFT over the
-//    lane's 16 bins (j = lane + 64k), twiddle, LDS transpose (row stride 68
-//    keeps ds_read_b64 conflict-free), 16-point DFT, twiddle, and a 4-point
-//    DFT across lane quads with DPP-level shuffles.  1/M is folded into the
-//    coefficients (exact for M = 2^10).
+//    barrier each wave runs one 1024-point IFFT in registers, 1024 = 16x16x4:
+//    16-point DFT over the lane's 16 bins (j = lane + 64k), twiddle, LDS
+//    transpose (row stride 68 keeps ds_read_b64 conflict-free), 16-point DFT,
+//    twiddle, LDS transpose, four 4-point DFTs.  Every complex operation is a
+//    packed v_pk_{add,mul,fma}_f32 with op_sel/neg modifiers (one instruction
+//    per add or +-j rotation, two per multiply): 380 VALU instructions per
+//    transform instead of ~650 for the scalar + DPP-quad form (FM = 0, kept
+//    for tools/mb/mb_pfb2.hip; 0.74-0.79 -> 0.70-0.71 ms per 2^27 samples).
+//    The last transpose leaves each lane two adjacent bins, so the outputs
+//    leave as 16-byte non-temporal stores, 1 KB contiguous per instruction.
+//    1/M is folded into the coefficients (exact for M = 2^10).
 //  * Blocks are grouped four at a time in global block numbering (even block
 //    = offset 0, odd = M/2), so calls of any length and start parity share one
 //    kernel; blocks outside the call are computed but not stored.
@@ -85,6 +91,93 @@ __device__ __forceinline__ void dft16_bwd(float2 (&v)[16])
     }
 }
 
+// ---- packed complex arithmetic (v_pk_*_f32 on (re, im) register pairs) ----
+// One VOP3P instruction per complex add / +-j rotation, two per complex
+// multiply; op_sel / neg modifiers do the component swaps the compiler
+// otherwise spends v_mov / v_xor on.
+typedef float v2f __attribute__((ext_vector_type(2)));
+
+__device__ __forceinline__ v2f pk(float2 a) { return v2f{a.x, a.y}; }
+__device__ __forceinline__ float2 unpk(v2f a) { return make_float2(a.x, a.y); }
+// b + j d = (b.x - d.y, b.y + d.x)
+__device__ __forceinline__ v2f pk_addpj(v2f b, v2f d)
+{
+    v2f r;
+    asm("v_pk_add_f32 %0, %1, %2 op_sel:[0,1] op_sel_hi:[1,0] neg_lo:[0,1]" : "=v"(r) : "v"(b), "v"(d));
+    return r;
+}
+// b - j d = (b.x + d.y, b.y - d.x)
+__device__ __forceinline__ v2f pk_subpj(v2f b, v2f d)
+{
+    v2f r;
+    asm("v_pk_add_f32 %0, %1, %2 op_sel:[0,1] op_sel_hi:[1,0] neg_hi:[0,1]" : "=v"(r) : "v"(b), "v"(d));
+    return r;
+}
+// a * w (complex), w in VGPRs: t = a.x * w; r = (t.x - a.y w.y, t.y + a.y w.x)
+__device__ __forceinline__ v2f pk_cmul(v2f a, v2f w)
+{
+    v2f t, r;
+    asm("v_pk_mul_f32 %0, %1, %2 op_sel_hi:[0,1]" : "=v"(t) : "v"(a), "v"(w));
+    asm("v_pk_fma_f32 %0, %1, %2, %3 op_sel:[1,1,0] op_sel_hi:[1,0,1] neg_lo:[0,1,0]"
+        : "=v"(r)
+        : "v"(a), "v"(w), "v"(t));
+    return r;
+}
+// a * w for a compile-time constant w (held in an SGPR pair)
+__device__ __forceinline__ v2f pk_cmulk(v2f a, v2f w)
+{
+    v2f t, r;
+    asm("v_pk_mul_f32 %0, %1, %2 op_sel_hi:[0,1]" : "=v"(t) : "v"(a), "s"(w));
+    asm("v_pk_fma_f32 %0, %1, %2, %3 op_sel:[1,1,0] op_sel_hi:[1,0,1] neg_lo:[0,1,0]"
+        : "=v"(r)
+        : "v"(a), "s"(w), "v"(t));
+    return r;
+}
+// backward radix-4 butterfly: (v0..v3) <- sum_q v_q e^{+2 pi i q s / 4}
+__device__ __forceinline__ void pk_dft4b(v2f &v0, v2f &v1, v2f &v2, v2f &v3)
+{
+    const v2f a = v0 + v2, b = v0 - v2, c = v1 + v3, d = v1 - v3;
+    v0 = a + c;
+    v2 = a - c;
+    v1 = pk_addpj(b, d);
+    v3 = pk_subpj(b, d);
+}
+// 16-point backward DFT, natural order in / out, all packed: 8 radix-4
+// butterflies (64 instructions) and 8 constant twiddles (16); W16^4 = j is
+// folded into the second butterfly of its column.
+__device__ __forceinline__ void pk_dft16b(v2f (&v)[16])
+{
+    v2f t[16];
+#pragma unroll
+    for (int q = 0; q < 4; q++) {
+        v2f a0 = v[q], a1 = v[4 + q], a2 = v[8 + q], a3 = v[12 + q];
+        pk_dft4b(a0, a1, a2, a3);
+        t[q] = a0;
+        t[4 + q] = q == 0 ? a1 : pk_cmulk(a1, v2f{C16[q], S16[q]});
+        t[8 + q] = (q == 0 || q == 2) ? a2 : pk_cmulk(a2, v2f{C16[2 * q], S16[2 * q]});
+        t[12 + q] = q == 0 ? a3 : pk_cmulk(a3, v2f{C16[(3 * q) & 15], S16[(3 * q) & 15]});
+    }
+#pragma unroll
+    for (int k0 = 0; k0 < 4; k0++) {
+        v2f b0 = t[k0 * 4 + 0], b1 = t[k0 * 4 + 1], b2 = t[k0 * 4 + 2], b3 = t[k0 * 4 + 3];
+        if (k0 == 2) {
+            // b2 still lacks its W16^4 = j factor: b0 +- j b2
+            const v2f a = pk_addpj(b0, b2), b = pk_subpj(b0, b2), c = b1 + b3, d = b1 - b3;
+            // columns: out0 = a + c, out2 = a - c, out1 = b + j d, out3 = b - j d
+            b0 = a + c;
+            b2 = a - c;
+            b1 = pk_addpj(b, d);
+            b3 = pk_subpj(b, d);
+        } else {
+            pk_dft4b(b0, b1, b2, b3);
+        }
+        v[k0 + 0] = b0;
+        v[k0 + 4] = b1;
+        v[k0 + 8] = b2;
+        v[k0 + 12] = b3;
+    }
+}
+
 // exchange with the partner lane inside a quad through DPP (a VALU operand
 // modifier, no LDS crossbar): quad_perm [1,0,3,2] for xor 1, [2,3,0,1] for xor 2
 template <int X>
@@ -95,8 +188,6 @@ __device__ __forceinline__ float2 quad_xor(float2 v)
     const int b = __builtin_amdgcn_mov_dpp(__float_as_int(v.y), ctrl, 0xF, 0xF, false);
     return make_float2(__int_as_float(a), __int_as_float(b));
 }
-
-typedef float v2f __attribute__((ext_vector_type(2)));
 
 // streaming (non-temporal) store of one complex sample: output is written once
 __device__ __forceinline__ void st_nt(float2 *p, float2 v)
@@ -141,7 +232,7 @@ __device__ unsigned long long g_pfb2_clk[2 * 1024];   // dev experiments (XMODE 
 // SMODE: output path. 0: per-lane 8-byte non-temporal stores straight from the
 // FFT layout; 1: same, plain stores; 2: through the block's LDS buffer into
 // 16-byte non-temporal stores; 3: 2 with plain stores
-template <int L, int XMODE = 0, int SMODE = 2, int PF = 6, int BAR = 1, int TRES = 0>
+template <int L, int XMODE = 0, int SMODE = 2, int PF = 8, int BAR = 1, int TRES = 0, int FM = 1>
 __global__ __launch_bounds__(NT, 1) void k_pfb2_an1024(Params P, const float *__restrict__ hsub,
                                                        const float2 *__restrict__ tw4096)
 {
@@ -280,6 +371,70 @@ __global__ __launch_bounds__(NT, 1) void k_pfb2_an1024(Params P, const float *__
                 float2 *Yb = P.Y + (b - P.B0) * M;
 #pragma unroll
                 for (int r = 0; r < 16; r++) st_nt(Yb + lane + 64 * r, B[lane + 64 * r]);
+            }
+        } else if constexpr (FM == 1) {
+            // 1024 = 16 x 16 x 4, every radix in registers with packed math:
+            // DFT16 over k (j = lane + 64k), twiddle, transpose, DFT16 over a
+            // (l = 4a + bq), twiddle, transpose, 4 x DFT4 over bq; the last
+            // transpose leaves each lane two adjacent bins, so the outputs
+            // leave as 16-byte stores covering 1 KB per wave instruction.
+            const long long b = b0 + wave;
+            int sb = slot0 + wave;
+            sb -= (sb >= NBUF) ? NBUF : 0;
+            float2 *B = xb + sb * BSTR;
+            v2f v[16];
+#pragma unroll
+            for (int k = 0; k < 16; k++) v[k] = pk(B[lane + 64 * k]);
+            pk_dft16b(v);
+#pragma unroll
+            for (int k1 = 1; k1 < 16; k1++) {
+                if ((k1 & 3) == 0) __builtin_amdgcn_sched_barrier(0);
+                v[k1] = pk_cmul(v[k1], pk(tw1[k1 * 64 + lane]));
+            }
+            lds_fence();
+#pragma unroll
+            for (int k1 = 0; k1 < 16; k1++) B[k1 * TSTR + lane] = unpk(v[k1]);
+            lds_fence();
+            const int k1 = lane >> 2, bq = lane & 3;
+#pragma unroll
+            for (int a = 0; a < 16; a++) v[a] = pk(B[k1 * TSTR + 4 * a + bq]);
+            pk_dft16b(v);
+#pragma unroll
+            for (int r = 1; r < 16; r++) {
+                if ((r & 3) == 0) __builtin_amdgcn_sched_barrier(0);
+                v[r] = pk_cmul(v[r], pk(tw2[r * 4 + bq]));
+            }
+            if (XMODE % 10 == 3) {
+                if (v[0].x == 12345.f && v[5].y == 3.f) P.Y[0] = unpk(v[3]);
+            } else if (b >= P.B0 && b < P.B0 + P.nblk) {
+                // C[k1][bq][r] at k1 + 16 r + 260 bq: the b64 writes of each
+                // 16-lane group hit 16 distinct bank pairs, the b128 reads below
+                // are conflict-free (MI355X_MICROARCH.md LDS table)
+                lds_fence();
+#pragma unroll
+                for (int r = 0; r < 16; r++) B[k1 + 16 * r + 260 * bq] = unpk(v[r]);
+                lds_fence();
+                typedef float v4f __attribute__((ext_vector_type(4)));
+                // lane (t2, p2): bins k1 = 2 p2 + {0, 1}, r = t2 + 8u
+                const int t2 = lane >> 3, p2 = lane & 7;
+                v4f *Yb = reinterpret_cast<v4f *>(P.Y + (b - P.B0) * M + 2 * p2 + 16 * t2);
+#pragma unroll
+                for (int u = 0; u < 2; u++) {
+                    v4f c[4];
+#pragma unroll
+                    for (int q = 0; q < 4; q++)
+                        c[q] = *reinterpret_cast<const v4f *>(B + 2 * p2 + 16 * (t2 + 8 * u) + 260 * q);
+                    v2f e0[4] = {c[0].xy, c[1].xy, c[2].xy, c[3].xy};
+                    v2f e1[4] = {c[0].zw, c[1].zw, c[2].zw, c[3].zw};
+                    pk_dft4b(e0[0], e0[1], e0[2], e0[3]);
+                    pk_dft4b(e1[0], e1[1], e1[2], e1[3]);
+                    // Y[k1 + 16 r + 256 s]
+#pragma unroll
+                    for (int sidx = 0; sidx < 4; sidx++) {
+                        const v4f val = {e0[sidx].x, e0[sidx].y, e1[sidx].x, e1[sidx].y};
+                        __builtin_nontemporal_store(val, Yb + (128 * u + 256 * sidx) / 2);
+                    }
+                }
             }
         } else {
             const long long b = b0 + wave;

@@ -18,15 +18,15 @@ void lq_check(hipError_t e, const char *what, const char *file, int line)
 static float2 *g_tw = nullptr;
 extern "C" const float *lqrt_twiddles(void) { return (const float *)g_tw; }
 
-template <int X, int SM = 2, int PF = 4, int BAR = 1, int TRES = 0>
+template <int X, int SM = 2, int PF = 4, int BAR = 1, int TRES = 0, int FM = 1>
 static void run(const char *name, Params P, const float *hsub, unsigned nwg, int iters)
 {
     hipEvent_t e0, e1;
     LQ_CHECK(hipEventCreate(&e0));
     LQ_CHECK(hipEventCreate(&e1));
-    hipLaunchKernelGGL((k_pfb2_an1024<8, X, SM, PF, BAR, TRES>), dim3(nwg), dim3(NT), 0, 0, P, hsub, g_tw);
+    hipLaunchKernelGGL((k_pfb2_an1024<8, X, SM, PF, BAR, TRES, FM>), dim3(nwg), dim3(NT), 0, 0, P, hsub, g_tw);
     LQ_CHECK(hipEventRecord(e0));
-    for (int i = 0; i < iters; i++) hipLaunchKernelGGL((k_pfb2_an1024<8, X, SM, PF, BAR, TRES>), dim3(nwg), dim3(NT), 0, 0, P, hsub, g_tw);
+    for (int i = 0; i < iters; i++) hipLaunchKernelGGL((k_pfb2_an1024<8, X, SM, PF, BAR, TRES, FM>), dim3(nwg), dim3(NT), 0, 0, P, hsub, g_tw);
     LQ_CHECK(hipEventRecord(e1));
     LQ_CHECK(hipEventSynchronize(e1));
     float ms;
@@ -106,20 +106,27 @@ int main()
     P.gpw = (int)gpw;
     P.gend = ngroups;
     const int it = 10;
-    for (int rep = 0; rep < 2; rep++) run<10, 2, 6, 1, 0>("warm", P, hsub, nwg, it);
-    Params P2 = P;
-    const long long ng8 = nb / 8;
-    for (int rep = 0; rep < 2; rep++) {
-        run<10, 2, 6, 1, 0>("library", P, hsub, nwg, it);
-        for (int target : {256, 512}) {
-            long long gpw8 = (ng8 + target - 1) / target;
-            const unsigned nwg8 = (unsigned)((ng8 + gpw8 - 1) / gpw8);
-            P2.gs0 = 0;
-            P2.gpw = (int)gpw8;
-            P2.gend = ng8;
-            run_v2<4, 2>("v2 8 waves/CU PF4", P2, hsub, nwg8, it);
-            run_v2<2, 2>("v2 8 waves/CU PF2", P2, hsub, nwg8, it);
-        }
+    for (int rep = 0; rep < 2; rep++) run<10, 2, 6, 1, 0, 1>("warm", P, hsub, nwg, it);
+    // outputs of the two transform modes must agree
+    std::vector<float2> ya(nb * M), yb(nb * M);
+    run<0, 2, 6, 1, 0, 0>("FM0 (dpp quad)", P, hsub, nwg, 1);
+    LQ_CHECK(hipMemcpy(ya.data(), y, nb * M * 8, hipMemcpyDeviceToHost));
+    LQ_CHECK(hipMemset(y, 0, nb * M * 8));
+    run<0, 2, 6, 1, 0, 1>("FM1 (packed 16x16x4)", P, hsub, nwg, 1);
+    LQ_CHECK(hipMemcpy(yb.data(), y, nb * M * 8, hipMemcpyDeviceToHost));
+    double md = 0, mx = 0;
+    for (long long i = 0; i < nb * M; i++) {
+        md = fmax(md, fmax(fabs(ya[i].x - yb[i].x), fabs(ya[i].y - yb[i].y)));
+        mx = fmax(mx, fmax(fabs(ya[i].x), fabs(ya[i].y)));
+    }
+    printf("FM0 vs FM1: max|d| %.3e  max|y| %.3e  rel %.3e\n", md, mx, md / mx);
+    for (int rep = 0; rep < 3; rep++) {
+        run<10, 2, 6, 1, 0, 0>("FM0 dpp quad", P, hsub, nwg, it);
+        run<10, 2, 6, 1, 0, 1>("FM1 packed", P, hsub, nwg, it);
+        run<11, 2, 6, 1, 0, 1>("FM1 no transforms", P, hsub, nwg, it);
+        run<10, 2, 8, 1, 0, 1>("FM1 PF8", P, hsub, nwg, it);
+        run<10, 2, 4, 1, 0, 1>("FM1 PF4", P, hsub, nwg, it);
+        run<10, 2, 6, 1, 1, 1>("FM1 taps resident", P, hsub, nwg, it);
     }
     return 0;
 }
