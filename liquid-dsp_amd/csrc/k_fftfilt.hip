@@ -24,11 +24,12 @@ namespace {
 constexpr int NT = 256;
 constexpr int NFFT = 4096;
 // k_fftfilt_r16 configuration (tools/mb/mb_fftfilt.hip, h=512, 2^26 samples):
-// the two register transforms need ~250 VGPRs, so 2 waves/SIMD without
-// spills (0.29 ms) beats 4 waves/SIMD with spills (0.73 ms); the filter
-// spectrum is read from L2 per segment (holding it in registers: no gain)
+// with the packed transforms (lq_device.h) the kernel needs ~185 VGPRs (+32
+// for the filter spectrum held in registers), so 2 waves/SIMD without spills;
+// spectrum in registers, 2048 persistent workgroups: 0.283 ms (spectrum from
+// L2 per segment: 0.36 ms; the scalar-complex transforms: 0.30 ms)
 #ifndef FF_HREG
-#define FF_HREG false
+#define FF_HREG true
 #define FF_WPE 2
 #endif
 
@@ -81,8 +82,9 @@ __device__ __forceinline__ float2 to_c2(float2 a) { return a; }
 
 // Register form (default): 256 threads, thread t holds segment samples
 // t + 256 n; forward 4096-point FFT (fft4096_r16), x H, inverse, all with the
-// data in registers and two LDS transposes per transform (35 KB LDS -> four
-// workgroups per CU); loads and stores are coalesced across t.
+// data in registers and two LDS transposes per transform (35 KB LDS; the
+// register budget allows two workgroups per CU); loads and stores are
+// coalesced across t.
 template <bool REAL, bool HREG, int WPE>
 __global__ __launch_bounds__(NT, WPE) void k_fftfilt_r16(int hm1, const float2 *__restrict__ H,
                                                     const void *__restrict__ hist, const void *__restrict__ xin,
@@ -128,7 +130,7 @@ __global__ __launch_bounds__(NT, WPE) void k_fftfilt_r16(int hm1, const float2 *
     }
     fft4096_r16<+1>(v, lds, tw, t);
 #pragma unroll
-    for (int k = 0; k < 16; k++) v[k] = cmul(v[k], HREG ? hv[k & (HREG ? 15 : 0)] : H[t + 256 * k]);
+    for (int k = 0; k < 16; k++) v[k] = unpk(pk_cmul(pk(v[k]), pk(HREG ? hv[k & (HREG ? 15 : 0)] : H[t + 256 * k])));
     fft4096_r16<-1>(v, lds, tw, t);
     S *ys = (S *)yout + (s0 - hm1);                    // output o = s0 + i - hm1 for i >= hm1
 #pragma unroll
@@ -158,7 +160,7 @@ extern "C" void lqk_fftfilt_run(int real_io, unsigned int hlen, const void *H, c
     const int L = NFFT - hm1;
     const long long nseg = ((long long)n + L - 1) / L;
     const float2 *tw = (const float2 *)lqrt_twiddles();
-    const unsigned grid = (unsigned)(nseg < 1024 ? nseg : 1024);   // persistent: 4 workgroups per CU
+    const unsigned grid = (unsigned)(nseg < 2048 ? nseg : 2048);   // persistent, two resident per CU
     if (real_io)
         hipLaunchKernelGGL((k_fftfilt_r16<true, FF_HREG, FF_WPE>), dim3(grid), dim3(NT), 0, st, hm1, (const float2 *)H, hist,
                            x, (long long)n, y, scale_re, scale_im, tw);

@@ -91,93 +91,6 @@ __device__ __forceinline__ void dft16_bwd(float2 (&v)[16])
     }
 }
 
-// ---- packed complex arithmetic (v_pk_*_f32 on (re, im) register pairs) ----
-// One VOP3P instruction per complex add / +-j rotation, two per complex
-// multiply; op_sel / neg modifiers do the component swaps the compiler
-// otherwise spends v_mov / v_xor on.
-typedef float v2f __attribute__((ext_vector_type(2)));
-
-__device__ __forceinline__ v2f pk(float2 a) { return v2f{a.x, a.y}; }
-__device__ __forceinline__ float2 unpk(v2f a) { return make_float2(a.x, a.y); }
-// b + j d = (b.x - d.y, b.y + d.x)
-__device__ __forceinline__ v2f pk_addpj(v2f b, v2f d)
-{
-    v2f r;
-    asm("v_pk_add_f32 %0, %1, %2 op_sel:[0,1] op_sel_hi:[1,0] neg_lo:[0,1]" : "=v"(r) : "v"(b), "v"(d));
-    return r;
-}
-// b - j d = (b.x + d.y, b.y - d.x)
-__device__ __forceinline__ v2f pk_subpj(v2f b, v2f d)
-{
-    v2f r;
-    asm("v_pk_add_f32 %0, %1, %2 op_sel:[0,1] op_sel_hi:[1,0] neg_hi:[0,1]" : "=v"(r) : "v"(b), "v"(d));
-    return r;
-}
-// a * w (complex), w in VGPRs: t = a.x * w; r = (t.x - a.y w.y, t.y + a.y w.x)
-__device__ __forceinline__ v2f pk_cmul(v2f a, v2f w)
-{
-    v2f t, r;
-    asm("v_pk_mul_f32 %0, %1, %2 op_sel_hi:[0,1]" : "=v"(t) : "v"(a), "v"(w));
-    asm("v_pk_fma_f32 %0, %1, %2, %3 op_sel:[1,1,0] op_sel_hi:[1,0,1] neg_lo:[0,1,0]"
-        : "=v"(r)
-        : "v"(a), "v"(w), "v"(t));
-    return r;
-}
-// a * w for a compile-time constant w (held in an SGPR pair)
-__device__ __forceinline__ v2f pk_cmulk(v2f a, v2f w)
-{
-    v2f t, r;
-    asm("v_pk_mul_f32 %0, %1, %2 op_sel_hi:[0,1]" : "=v"(t) : "v"(a), "s"(w));
-    asm("v_pk_fma_f32 %0, %1, %2, %3 op_sel:[1,1,0] op_sel_hi:[1,0,1] neg_lo:[0,1,0]"
-        : "=v"(r)
-        : "v"(a), "s"(w), "v"(t));
-    return r;
-}
-// backward radix-4 butterfly: (v0..v3) <- sum_q v_q e^{+2 pi i q s / 4}
-__device__ __forceinline__ void pk_dft4b(v2f &v0, v2f &v1, v2f &v2, v2f &v3)
-{
-    const v2f a = v0 + v2, b = v0 - v2, c = v1 + v3, d = v1 - v3;
-    v0 = a + c;
-    v2 = a - c;
-    v1 = pk_addpj(b, d);
-    v3 = pk_subpj(b, d);
-}
-// 16-point backward DFT, natural order in / out, all packed: 8 radix-4
-// butterflies (64 instructions) and 8 constant twiddles (16); W16^4 = j is
-// folded into the second butterfly of its column.
-__device__ __forceinline__ void pk_dft16b(v2f (&v)[16])
-{
-    v2f t[16];
-#pragma unroll
-    for (int q = 0; q < 4; q++) {
-        v2f a0 = v[q], a1 = v[4 + q], a2 = v[8 + q], a3 = v[12 + q];
-        pk_dft4b(a0, a1, a2, a3);
-        t[q] = a0;
-        t[4 + q] = q == 0 ? a1 : pk_cmulk(a1, v2f{C16[q], S16[q]});
-        t[8 + q] = (q == 0 || q == 2) ? a2 : pk_cmulk(a2, v2f{C16[2 * q], S16[2 * q]});
-        t[12 + q] = q == 0 ? a3 : pk_cmulk(a3, v2f{C16[(3 * q) & 15], S16[(3 * q) & 15]});
-    }
-#pragma unroll
-    for (int k0 = 0; k0 < 4; k0++) {
-        v2f b0 = t[k0 * 4 + 0], b1 = t[k0 * 4 + 1], b2 = t[k0 * 4 + 2], b3 = t[k0 * 4 + 3];
-        if (k0 == 2) {
-            // b2 still lacks its W16^4 = j factor: b0 +- j b2
-            const v2f a = pk_addpj(b0, b2), b = pk_subpj(b0, b2), c = b1 + b3, d = b1 - b3;
-            // columns: out0 = a + c, out2 = a - c, out1 = b + j d, out3 = b - j d
-            b0 = a + c;
-            b2 = a - c;
-            b1 = pk_addpj(b, d);
-            b3 = pk_subpj(b, d);
-        } else {
-            pk_dft4b(b0, b1, b2, b3);
-        }
-        v[k0 + 0] = b0;
-        v[k0 + 4] = b1;
-        v[k0 + 8] = b2;
-        v[k0 + 12] = b3;
-    }
-}
-
 // exchange with the partner lane inside a quad through DPP (a VALU operand
 // modifier, no LDS crossbar): quad_perm [1,0,3,2] for xor 1, [2,3,0,1] for xor 2
 template <int X>
@@ -385,7 +298,7 @@ __global__ __launch_bounds__(NT, 1) void k_pfb2_an1024(Params P, const float *__
             v2f v[16];
 #pragma unroll
             for (int k = 0; k < 16; k++) v[k] = pk(B[lane + 64 * k]);
-            pk_dft16b(v);
+            pk_dft16<-1>(v);
 #pragma unroll
             for (int k1 = 1; k1 < 16; k1++) {
                 if ((k1 & 3) == 0) __builtin_amdgcn_sched_barrier(0);
@@ -398,7 +311,7 @@ __global__ __launch_bounds__(NT, 1) void k_pfb2_an1024(Params P, const float *__
             const int k1 = lane >> 2, bq = lane & 3;
 #pragma unroll
             for (int a = 0; a < 16; a++) v[a] = pk(B[k1 * TSTR + 4 * a + bq]);
-            pk_dft16b(v);
+            pk_dft16<-1>(v);
 #pragma unroll
             for (int r = 1; r < 16; r++) {
                 if ((r & 3) == 0) __builtin_amdgcn_sched_barrier(0);
@@ -426,8 +339,8 @@ __global__ __launch_bounds__(NT, 1) void k_pfb2_an1024(Params P, const float *__
                         c[q] = *reinterpret_cast<const v4f *>(B + 2 * p2 + 16 * (t2 + 8 * u) + 260 * q);
                     v2f e0[4] = {c[0].xy, c[1].xy, c[2].xy, c[3].xy};
                     v2f e1[4] = {c[0].zw, c[1].zw, c[2].zw, c[3].zw};
-                    pk_dft4b(e0[0], e0[1], e0[2], e0[3]);
-                    pk_dft4b(e1[0], e1[1], e1[2], e1[3]);
+                    pk_dft4<-1>(e0[0], e0[1], e0[2], e0[3]);
+                    pk_dft4<-1>(e1[0], e1[1], e1[2], e1[3]);
                     // Y[k1 + 16 r + 256 s]
 #pragma unroll
                     for (int sidx = 0; sidx < 4; sidx++) {

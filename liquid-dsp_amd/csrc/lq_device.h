@@ -22,6 +22,102 @@ __device__ __forceinline__ float2 cscale(float2 a, float s) { return make_float2
 __device__ __forceinline__ float2 cmul_mj(float2 a) { return make_float2(a.y, -a.x); }
 __device__ __forceinline__ float2 cmul_pj(float2 a) { return make_float2(-a.y, a.x); }
 
+// ---- packed complex arithmetic: (re, im) in a VGPR pair, v_pk_*_f32 with
+// op_sel / neg modifiers doing the component swaps (one instruction per
+// complex add or +-j rotation, two per complex multiply; the compiler's own
+// float2 code spends extra v_mov / v_xor on the swaps)
+typedef float v2f __attribute__((ext_vector_type(2)));
+
+__device__ __forceinline__ v2f pk(float2 a) { return v2f{a.x, a.y}; }
+__device__ __forceinline__ float2 unpk(v2f a) { return make_float2(a.x, a.y); }
+// b + j d = (b.x - d.y, b.y + d.x)
+__device__ __forceinline__ v2f pk_addpj(v2f b, v2f d)
+{
+    v2f r;
+    asm("v_pk_add_f32 %0, %1, %2 op_sel:[0,1] op_sel_hi:[1,0] neg_lo:[0,1]" : "=v"(r) : "v"(b), "v"(d));
+    return r;
+}
+// b - j d = (b.x + d.y, b.y - d.x)
+__device__ __forceinline__ v2f pk_subpj(v2f b, v2f d)
+{
+    v2f r;
+    asm("v_pk_add_f32 %0, %1, %2 op_sel:[0,1] op_sel_hi:[1,0] neg_hi:[0,1]" : "=v"(r) : "v"(b), "v"(d));
+    return r;
+}
+// a * w, w in VGPRs: t = a.x * w; r = (t.x - a.y w.y, t.y + a.y w.x)
+__device__ __forceinline__ v2f pk_cmul(v2f a, v2f w)
+{
+    v2f t, r;
+    asm("v_pk_mul_f32 %0, %1, %2 op_sel_hi:[0,1]" : "=v"(t) : "v"(a), "v"(w));
+    asm("v_pk_fma_f32 %0, %1, %2, %3 op_sel:[1,1,0] op_sel_hi:[1,0,1] neg_lo:[0,1,0]"
+        : "=v"(r)
+        : "v"(a), "v"(w), "v"(t));
+    return r;
+}
+// a * w for a compile-time constant w (held in an SGPR pair)
+__device__ __forceinline__ v2f pk_cmulk(v2f a, v2f w)
+{
+    v2f t, r;
+    asm("v_pk_mul_f32 %0, %1, %2 op_sel_hi:[0,1]" : "=v"(t) : "v"(a), "s"(w));
+    asm("v_pk_fma_f32 %0, %1, %2, %3 op_sel:[1,1,0] op_sel_hi:[1,0,1] neg_lo:[0,1,0]"
+        : "=v"(r)
+        : "v"(a), "s"(w), "v"(t));
+    return r;
+}
+// radix-4 butterfly, DIR +1 forward (exp(-j 2 pi qs/4)), -1 backward
+template <int DIR>
+__device__ __forceinline__ void pk_dft4(v2f &v0, v2f &v1, v2f &v2, v2f &v3)
+{
+    const v2f a = v0 + v2, b = v0 - v2, c = v1 + v3, d = v1 - v3;
+    v0 = a + c;
+    v2 = a - c;
+    v1 = DIR > 0 ? pk_subpj(b, d) : pk_addpj(b, d);
+    v3 = DIR > 0 ? pk_addpj(b, d) : pk_subpj(b, d);
+}
+// 16-point DFT, natural order in / out, radix 4 x 4: 8 butterflies (64
+// packed instructions) and 8 constant twiddles (16); W16^{+-4} = +-j is folded
+// into the butterfly of its column.
+template <int DIR>
+__device__ __forceinline__ void pk_dft16(v2f (&v)[16])
+{
+    constexpr float C[16] = {1.0f,         0.92387953f,  0.70710678f,  0.38268343f,  0.0f,        -0.38268343f,
+                             -0.70710678f, -0.92387953f, -1.0f,        -0.92387953f, -0.70710678f, -0.38268343f,
+                             0.0f,         0.38268343f,  0.70710678f,  0.92387953f};
+    constexpr float S[16] = {0.0f,  0.38268343f,  0.70710678f,  0.92387953f,  1.0f,         0.92387953f,
+                             0.70710678f,  0.38268343f,  0.0f,  -0.38268343f, -0.70710678f, -0.92387953f,
+                             -1.0f, -0.92387953f, -0.70710678f, -0.38268343f};
+    v2f t[16];
+#pragma unroll
+    for (int q = 0; q < 4; q++) {
+        v2f a0 = v[q], a1 = v[4 + q], a2 = v[8 + q], a3 = v[12 + q];
+        pk_dft4<DIR>(a0, a1, a2, a3);
+        t[q] = a0;
+        t[4 + q] = q == 0 ? a1 : pk_cmulk(a1, v2f{C[q], -DIR * S[q]});
+        t[8 + q] = (q == 0 || q == 2) ? a2 : pk_cmulk(a2, v2f{C[2 * q], -DIR * S[2 * q]});
+        t[12 + q] = q == 0 ? a3 : pk_cmulk(a3, v2f{C[(3 * q) & 15], -DIR * S[(3 * q) & 15]});
+    }
+#pragma unroll
+    for (int k0 = 0; k0 < 4; k0++) {
+        v2f b0 = t[4 * k0 + 0], b1 = t[4 * k0 + 1], b2 = t[4 * k0 + 2], b3 = t[4 * k0 + 3];
+        if (k0 == 2) {
+            // b2 still lacks its W16^{-4 DIR} = -DIR j factor
+            const v2f a = DIR > 0 ? pk_subpj(b0, b2) : pk_addpj(b0, b2);
+            const v2f b = DIR > 0 ? pk_addpj(b0, b2) : pk_subpj(b0, b2);
+            const v2f c = b1 + b3, d = b1 - b3;
+            b0 = a + c;
+            b2 = a - c;
+            b1 = DIR > 0 ? pk_subpj(b, d) : pk_addpj(b, d);
+            b3 = DIR > 0 ? pk_addpj(b, d) : pk_subpj(b, d);
+        } else {
+            pk_dft4<DIR>(b0, b1, b2, b3);
+        }
+        v[k0] = b0;
+        v[k0 + 4] = b1;
+        v[k0 + 8] = b2;
+        v[k0 + 12] = b3;
+    }
+}
+
 // twiddle W_n^e for direction dir (+1: exp(-2 pi i e/n), -1: conjugate) from the
 // 4096-entry table; n must divide 4096 and e < n.
 __device__ __forceinline__ float2 twiddle(const float2 *__restrict__ tw, int e_4096, int dir)
@@ -118,42 +214,16 @@ __device__ float2 *lds_fft(float2 *a, float2 *b, const float2 *__restrict__ tw, 
 
 // ---------------------------------------------------------------- register radix-16
 // 16-point DFT in registers, natural order in and out; DIR +1 forward
-// (exp(-j 2 pi nk/16)), -1 backward.  Radix 4 x 4 with the W16 twiddles
-// between the two passes.
+// (exp(-j 2 pi nk/16)), -1 backward (packed form above).
 template <int DIR>
 __device__ __forceinline__ void dft16(float2 (&v)[16])
 {
-    constexpr float C[16] = {1.0f,         0.92387953f,  0.70710678f,  0.38268343f,  0.0f,        -0.38268343f,
-                             -0.70710678f, -0.92387953f, -1.0f,        -0.92387953f, -0.70710678f, -0.38268343f,
-                             0.0f,         0.38268343f,  0.70710678f,  0.92387953f};
-    constexpr float S[16] = {0.0f,  0.38268343f,  0.70710678f,  0.92387953f,  1.0f,         0.92387953f,
-                             0.70710678f,  0.38268343f,  0.0f,  -0.38268343f, -0.70710678f, -0.92387953f,
-                             -1.0f, -0.92387953f, -0.70710678f, -0.38268343f};
-    float2 t[16];
+    v2f p[16];
 #pragma unroll
-    for (int q = 0; q < 4; q++) {
-        float2 a0 = v[q], a1 = v[4 + q], a2 = v[8 + q], a3 = v[12 + q];
-        dft4(a0, a1, a2, a3, DIR);
-        t[q] = a0;
-        if (q == 0) {
-            t[4] = a1;
-            t[8] = a2;
-            t[12] = a3;
-        } else {   // W16^{DIR q k0}
-            t[4 + q] = cmul(a1, make_float2(C[(1 * q) & 15], -DIR * S[(1 * q) & 15]));
-            t[8 + q] = cmul(a2, make_float2(C[(2 * q) & 15], -DIR * S[(2 * q) & 15]));
-            t[12 + q] = cmul(a3, make_float2(C[(3 * q) & 15], -DIR * S[(3 * q) & 15]));
-        }
-    }
+    for (int k = 0; k < 16; k++) p[k] = pk(v[k]);
+    pk_dft16<DIR>(p);
 #pragma unroll
-    for (int k0 = 0; k0 < 4; k0++) {
-        float2 b0 = t[4 * k0 + 0], b1 = t[4 * k0 + 1], b2 = t[4 * k0 + 2], b3 = t[4 * k0 + 3];
-        dft4(b0, b1, b2, b3, DIR);
-        v[k0] = b0;
-        v[k0 + 4] = b1;
-        v[k0 + 8] = b2;
-        v[k0 + 12] = b3;
-    }
+    for (int k = 0; k < 16; k++) v[k] = unpk(p[k]);
 }
 
 // 4096-point FFT by a 256-thread block, three register radix-16 passes and two
@@ -171,28 +241,22 @@ __device__ __forceinline__ void dft16(float2 (&v)[16])
 template <int DIR>
 __device__ __forceinline__ void twiddle16(float2 (&v)[16], const float2 *__restrict__ tw, int e)
 {
-    float2 w1 = tw[e & 4095], w4 = tw[(4 * e) & 4095];
+    float2 a1 = tw[e & 4095], a4 = tw[(4 * e) & 4095];
     if (DIR < 0) {
-        w1.y = -w1.y;
-        w4.y = -w4.y;
+        a1.y = -a1.y;
+        a4.y = -a4.y;
     }
-    const float2 w2 = cmul(w1, w1), w3 = cmul(w2, w1);
-    const float2 w8 = cmul(w4, w4), w12 = cmul(w8, w4);
-    v[1] = cmul(v[1], w1);
-    v[2] = cmul(v[2], w2);
-    v[3] = cmul(v[3], w3);
-    v[4] = cmul(v[4], w4);
-    v[8] = cmul(v[8], w8);
-    v[12] = cmul(v[12], w12);
-    v[5] = cmul(v[5], cmul(w1, w4));
-    v[6] = cmul(v[6], cmul(w2, w4));
-    v[7] = cmul(v[7], cmul(w3, w4));
-    v[9] = cmul(v[9], cmul(w1, w8));
-    v[10] = cmul(v[10], cmul(w2, w8));
-    v[11] = cmul(v[11], cmul(w3, w8));
-    v[13] = cmul(v[13], cmul(w1, w12));
-    v[14] = cmul(v[14], cmul(w2, w12));
-    v[15] = cmul(v[15], cmul(w3, w12));
+    const v2f w1 = pk(a1), w4 = pk(a4);
+    const v2f w2 = pk_cmul(w1, w1), w3 = pk_cmul(w2, w1);
+    const v2f w8 = pk_cmul(w4, w4), w12 = pk_cmul(w8, w4);
+    const v2f lo[3] = {w1, w2, w3}, hi[3] = {w4, w8, w12};
+#pragma unroll
+    for (int k = 1; k < 16; k++) {
+        const int l = k & 3, h = k >> 2;
+        v2f w = l ? lo[l - 1] : hi[h - 1];
+        if (l && h) w = pk_cmul(lo[l - 1], hi[h - 1]);
+        v[k] = unpk(pk_cmul(pk(v[k]), w));
+    }
 }
 template <int DIR>
 __device__ __forceinline__ void fft4096_r16(float2 (&v)[16], float2 *lds, const float2 *__restrict__ tw, int t)

@@ -9,15 +9,6 @@
 
 #include "lq_device.h"
 
-template <int X>
-__device__ __forceinline__ float2 f1k_quad_xor(float2 v)
-{
-    constexpr int ctrl = X == 1 ? 0xB1 : 0x4E;
-    const int a = __builtin_amdgcn_mov_dpp(__float_as_int(v.x), ctrl, 0xF, 0xF, false);
-    const int b = __builtin_amdgcn_mov_dpp(__float_as_int(v.y), ctrl, 0xF, 0xF, false);
-    return make_float2(__int_as_float(a), __int_as_float(b));
-}
-
 __device__ __forceinline__ void f1k_wave_fence()
 {
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
@@ -42,37 +33,56 @@ __device__ __forceinline__ void f1k_tables(float2 *tw1, float2 *tw2, const float
 }
 
 // v[k] = x[lane + 64 k] in; natural-order result left in B[k + 4 (k >> 8)]
-// (B: 1088 float2 per wave).
+// (B: 1088 float2 per wave).  1024 = 16 x 16 x 4 with packed arithmetic
+// (lq_device.h): DFT16, twiddle, transpose, DFT16, twiddle, transpose, four
+// DFT4 per lane; the same transform as the firpfbch2 fast path.
 template <int DIR>
 __device__ __forceinline__ void fft1024_wave(float2 (&v)[16], float2 *B, const float2 *tw1, const float2 *tw2,
                                              int lane)
 {
-    dft16<DIR>(v);
+    v2f p[16];
 #pragma unroll
-    for (int k1 = 1; k1 < 16; k1++) v[k1] = cmul(v[k1], tw1[k1 * 64 + lane]);
+    for (int k = 0; k < 16; k++) p[k] = pk(v[k]);
+    pk_dft16<DIR>(p);
+#pragma unroll
+    for (int k1 = 1; k1 < 16; k1++) p[k1] = pk_cmul(p[k1], pk(tw1[k1 * 64 + lane]));
     f1k_wave_fence();
 #pragma unroll
-    for (int k1 = 0; k1 < 16; k1++) B[k1 * 68 + lane] = v[k1];
+    for (int k1 = 0; k1 < 16; k1++) B[k1 * 68 + lane] = unpk(p[k1]);
     f1k_wave_fence();
     const int k1 = lane >> 2, bq = lane & 3;
 #pragma unroll
-    for (int a = 0; a < 16; a++) v[a] = B[k1 * 68 + 4 * a + bq];
-    dft16<DIR>(v);
+    for (int a = 0; a < 16; a++) p[a] = pk(B[k1 * 68 + 4 * a + bq]);
+    pk_dft16<DIR>(p);
 #pragma unroll
-    for (int r = 1; r < 16; r++) v[r] = cmul(v[r], tw2[r * 4 + bq]);
-    const float sg2 = (bq & 2) ? -1.0f : 1.0f, sg1 = (bq & 1) ? -1.0f : 1.0f;
-#pragma unroll
-    for (int r = 0; r < 16; r++) {
-        const float2 p = f1k_quad_xor<2>(v[r]);
-        float2 u = make_float2(fmaf(sg2, v[r].x, p.x), fmaf(sg2, v[r].y, p.y));
-        if (bq == 3) u = DIR > 0 ? cmul_mj(u) : cmul_pj(u);
-        const float2 p2 = f1k_quad_xor<1>(u);
-        v[r] = make_float2(fmaf(sg1, u.x, p2.x), fmaf(sg1, u.y, p2.y));
-    }
-    // lane (k1, bq) holds Y[k1 + 16 r + 256 s], s = bitrev2(bq)
-    const int s = ((bq & 1) << 1) | (bq >> 1);
+    for (int r = 1; r < 16; r++) p[r] = pk_cmul(p[r], pk(tw2[r * 4 + bq]));
+    // C[k1][bq][r] at k1 + 16 r + 260 bq (conflict-free b64 writes, b128 reads)
     f1k_wave_fence();
 #pragma unroll
-    for (int r = 0; r < 16; r++) B[k1 + 16 * r + 260 * s] = v[r];
+    for (int r = 0; r < 16; r++) B[k1 + 16 * r + 260 * bq] = unpk(p[r]);
+    f1k_wave_fence();
+    typedef float v4f __attribute__((ext_vector_type(4)));
+    // lane (t2, p2): bins k1 = 2 p2 + {0, 1}, r = t2 + 8u
+    const int t2 = lane >> 3, p2 = lane & 7;
+    v4f c[2][4];
+#pragma unroll
+    for (int u = 0; u < 2; u++)
+#pragma unroll
+        for (int q = 0; q < 4; q++)
+            c[u][q] = *reinterpret_cast<const v4f *>(B + 2 * p2 + 16 * (t2 + 8 * u) + 260 * q);
+    f1k_wave_fence();
+#pragma unroll
+    for (int u = 0; u < 2; u++) {
+        v2f e0[4] = {c[u][0].xy, c[u][1].xy, c[u][2].xy, c[u][3].xy};
+        v2f e1[4] = {c[u][0].zw, c[u][1].zw, c[u][2].zw, c[u][3].zw};
+        pk_dft4<DIR>(e0[0], e0[1], e0[2], e0[3]);
+        pk_dft4<DIR>(e1[0], e1[1], e1[2], e1[3]);
+        // Y[K], K = 2 p2 + 16 (t2 + 8u) + 256 s, at K + 4 s
+#pragma unroll
+        for (int sidx = 0; sidx < 4; sidx++) {
+            const v4f val = {e0[sidx].x, e0[sidx].y, e1[sidx].x, e1[sidx].y};
+            *reinterpret_cast<v4f *>(B + 2 * p2 + 16 * (t2 + 8 * u) + 260 * sidx) = val;
+        }
+    }
     f1k_wave_fence();
 }
