@@ -496,6 +496,10 @@ extern "C" void lqk_firfilt(const lqk_fir_desc *d, const void *hist, const void 
                             void *y, void *scratch, void *stream)
 {
     if (n == 0) return;
+    // LQ_FIRFILT_NO_MFMA=1 keeps crcf h<=64 on the VALU kernel (comparisons)
+    static int no_mx = -1;
+    if (no_mx < 0) no_mx = getenv("LQ_FIRFILT_NO_MFMA") != nullptr;
+    if (!no_mx && lqk_firfilt_mx(d, hist, x, n, y, stream)) return;
     hipStream_t st = (hipStream_t)stream;
     const void *halo = nullptr;
     if (x == y) {

@@ -1,0 +1,267 @@
+// k_firfilt_mx.hip -- firfilt_crcf for filters of 33..64 taps on the matrix
+// cores (the BASELINE config-1 shape, h = 64).
+//
+// Reference: src/filter/src/firfilt.c:322-359 (execute / execute_block),
+// y[t] = scale * sum_{k<h} h[k] x[t-k].  The VALU kernel (k_firfilt.hip)
+// spends 64 v_pk_fma_f32 per output and co-limits with HBM; here the
+// convolution runs as a banded-Toeplitz GEMM on v_mfma_f32_32x32x16_bf16:
+//
+//   C[i][n] = sum_{j<96} H[i][j] B[j][n],  H[i][j] = h[i + 64 - j] (0 outside
+//   0..63),  B[j][n] = x_comp(n)[s_seg(n) - 64 + j]
+//
+// i = output within a 32-sample segment, n = (segment, re/im) column, so one
+// 32x32 tile is 16 segments x 2 components = 512 complex outputs, six K = 16
+// steps.  float32 accuracy is kept by splitting both operands into three
+// bf16 terms (x = x1 + x2 + x3, each the round-to-nearest bf16 of the
+// remaining residual, exact to 2^-24 relative; products of bf16 terms are
+// exact in the fp32 accumulator) and summing the six products whose order is
+// at most 2^-16: x1h1, x1h2, x2h1, x1h3, x2h2, x3h1.  The dropped terms and
+// the representation error are below 3 * 2^-24 |x||h| per tap -- the size of
+// float32 rounding; tests hold the output to the same 1e-5 normwise bound as
+// every other kernel (tests/test_gpu_parity.py).
+//
+// Workgroup: 4 waves, persistent over a contiguous run of 2048-output chunks.
+// Each iteration: the 8 samples a lane prefetched are split into six bf16
+// planes (3 terms x re/im) of the chunk's 2112-sample span in LDS (16 bytes of
+// pad per 32 samples: the B-operand reads of the 16 segments of a tile land
+// on 16 distinct bank groups; the 64-sample halo comes from a small buffer the
+// previous iteration's tail lanes filled), the loads of the chunk after next
+// are issued (two chunks, 32 KB per workgroup, stay in flight), then each wave
+// runs 36 MFMAs for its 512 outputs, stages the accumulator through LDS and
+// writes 16-byte stores.  The taps' A fragments (3 terms x 6 K steps, 72
+// VGPRs) are built once per workgroup from the padded fp32 taps.
+#include "lq_device.h"
+#include "lq_kernels.h"
+
+#include <cstdint>
+#include <cstdio>
+#include <cstdlib>
+
+namespace {
+
+typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+typedef float v4f __attribute__((ext_vector_type(4)));
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+
+constexpr int NT = 256;           // 4 waves
+constexpr int CH = 2048;          // outputs per chunk (4 tiles of 512)
+constexpr int SPAN = CH + 64;     // samples a chunk's tiles read (64-sample halo)
+constexpr int PLB = SPAN * 2 + 16 * (SPAN / 32);   // bytes per plane (5280)
+constexpr int HPB = 64 * 2 + 16 * 2;               // bytes per plane of a halo buffer
+constexpr int SSTR = 68;          // floats per staged segment (32 x re/im + pad)
+constexpr int LDS_BYTES = 6 * PLB + 2 * 6 * HPB + 4 * 16 * SSTR * 4;   // 51008: three workgroups per CU
+
+__device__ __forceinline__ int poff(int pos) { return 2 * pos + 16 * (pos >> 5); }
+
+// three-term bf16 split of a pair of floats
+__device__ __forceinline__ void split3(v2f a, bf16x2 &t1, bf16x2 &t2, bf16x2 &t3)
+{
+    t1 = __builtin_convertvector(a, bf16x2);
+    const v2f r1 = a - __builtin_convertvector(t1, v2f);
+    t2 = __builtin_convertvector(r1, bf16x2);
+    const v2f r2 = r1 - __builtin_convertvector(t2, v2f);
+    t3 = __builtin_convertvector(r2, bf16x2);
+}
+
+// write 8 consecutive complex samples (ring position pos, a multiple of 8)
+// into the six planes: plane (p, c) = term p of component c.  v[q] holds
+// samples 2q and 2q+1 as (re, im, re, im).
+__device__ __forceinline__ void put8(unsigned char *planes, int pstride, int pos, const v4f (&v)[4])
+{
+    bf16x2 t[3][2][4];
+#pragma unroll
+    for (int q = 0; q < 4; q++) {
+        split3(v2f{v[q].x, v[q].z}, t[0][0][q], t[1][0][q], t[2][0][q]);
+        split3(v2f{v[q].y, v[q].w}, t[0][1][q], t[1][1][q], t[2][1][q]);
+    }
+    const int o = poff(pos);
+#pragma unroll
+    for (int p = 0; p < 3; p++)
+#pragma unroll
+        for (int c = 0; c < 2; c++) {
+            const u32x4 w = {__builtin_bit_cast(unsigned, t[p][c][0]), __builtin_bit_cast(unsigned, t[p][c][1]),
+                             __builtin_bit_cast(unsigned, t[p][c][2]), __builtin_bit_cast(unsigned, t[p][c][3])};
+            *reinterpret_cast<u32x4 *>(planes + (2 * p + c) * pstride + o) = w;
+        }
+}
+
+// 8 complex samples of the stream starting at s (a multiple of 8); ext[t<0]
+// comes from the 64-sample history win, samples at or past n are zero
+__device__ __forceinline__ v2f sample_at(const v2f *__restrict__ win, const v2f *__restrict__ x, long long n,
+                                         long long t)
+{
+    return t < 0 ? win[64 + t] : (t < n ? x[t] : v2f{0.f, 0.f});
+}
+template <bool NTL>
+__device__ __forceinline__ void load8(const v2f *__restrict__ win, const v2f *__restrict__ x, long long n,
+                                      long long s, v4f (&v)[4])
+{
+    if (s >= 0 && s + 8 <= n) {
+        const v4f *p = reinterpret_cast<const v4f *>(x + s);
+#pragma unroll
+        for (int q = 0; q < 4; q++) v[q] = NTL ? __builtin_nontemporal_load(p + q) : p[q];
+    } else {
+#pragma unroll
+        for (int q = 0; q < 4; q++) {
+            const v2f e0 = sample_at(win, x, n, s + 2 * q), e1 = sample_at(win, x, n, s + 2 * q + 1);
+            v[q] = v4f{e0.x, e0.y, e1.x, e1.y};
+        }
+    }
+}
+
+template <int VAR>
+__global__ __launch_bounds__(NT, 3) void k_firfilt_mx(const v2f *__restrict__ win, const v2f *__restrict__ x,
+                                                     long long n, v2f *__restrict__ y,
+                                                     const float *__restrict__ hpad, float sre, float sim,
+                                                     long long nch, long long cpw)
+{
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    unsigned char *planes = smem;
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int r32 = lane & 31, hh = lane >> 5;
+    unsigned char *halo = smem + 6 * PLB;   // two halo buffers (chunk tails), 6 planes each
+    float *stage = reinterpret_cast<float *>(smem + 6 * PLB + 2 * 6 * HPB) + wave * 16 * SSTR;
+
+    const long long c0 = (long long)blockIdx.x * cpw;
+    long long c1 = c0 + cpw;
+    if (c1 > nch) c1 = nch;
+    if (c0 >= c1) return;
+
+    // A fragments: lane (row i = r32, k half hh) holds H[i][16s + 8hh + e]
+    bf16x8 A[3][6];
+#pragma unroll
+    for (int s = 0; s < 6; s++) {
+        bf16x2 t[3][4];
+#pragma unroll
+        for (int q = 0; q < 4; q++) {
+            float hv[2];
+#pragma unroll
+            for (int u = 0; u < 2; u++) {
+                const int k = r32 + 64 - (16 * s + 8 * hh + 2 * q + u);
+                hv[u] = (k >= 0 && k < 64) ? hpad[k] : 0.f;
+            }
+            split3(v2f{hv[0], hv[1]}, t[0][q], t[1][q], t[2][q]);
+        }
+#pragma unroll
+        for (int p = 0; p < 3; p++)
+            A[p][s] = bf16x8{t[p][0].x, t[p][0].y, t[p][1].x, t[p][1].y, t[p][2].x, t[p][2].y, t[p][3].x, t[p][3].y};
+    }
+
+    // plane position p of chunk c = stream sample CH c - 64 + p; positions
+    // 0..63 (the previous chunk's tail) come from halo buffer (c - 1) & 1,
+    // filled by the lanes holding that tail one iteration earlier (from
+    // memory for the first chunk)
+    if (tid < 8) {
+        v4f v[4];
+        load8<(VAR & 1) != 0>(win, x, n, CH * c0 - 64 + 8 * tid, v);
+        put8(halo + ((c0 - 1) & 1) * 6 * HPB, HPB, 8 * tid, v);
+    }
+    // two chunks in flight per workgroup: register sets xa / xb alternate
+    // (the loop is unrolled by two so neither set is ever copied, which would
+    // wait on its loads early)
+    v4f xa[4], xb[4];
+    load8<(VAR & 1) != 0>(win, x, n, CH * c0 + 8 * tid, xa);
+    if (c0 + 1 < c1) load8<(VAR & 1) != 0>(win, x, n, CH * (c0 + 1) + 8 * tid, xb);
+
+    // B operand: lane column n = r32 -> segment sg = n & 15, component n >> 4
+    const int sg = r32 & 15, comp = r32 >> 4;
+    auto step = [&](long long c, v4f (&xv)[4]) {
+        __syncthreads();   // the previous chunk's MFMA reads are done
+        if (tid < 8) {
+            const unsigned char *hs = halo + ((c - 1) & 1) * 6 * HPB + poff(8 * tid);
+#pragma unroll
+            for (int p = 0; p < 6; p++)
+                *reinterpret_cast<u32x4 *>(planes + p * PLB + poff(8 * tid)) =
+                    *reinterpret_cast<const u32x4 *>(hs + p * HPB);
+        }
+        put8(planes, PLB, 64 + 8 * tid, xv);
+        if (tid >= NT - 8) put8(halo + (c & 1) * 6 * HPB, HPB, 8 * (tid - (NT - 8)), xv);
+        if (c + 2 < c1) load8<(VAR & 1) != 0>(win, x, n, CH * (c + 2) + 8 * tid, xv);
+        __syncthreads();
+
+        f32x16 C = {};
+#pragma unroll
+        for (int s = 0; s < 6; s++) {
+            const int pos = 512 * wave + 32 * sg + 16 * s + 8 * hh;
+            const unsigned char *bp = planes + comp * PLB + poff(pos);
+            const bf16x8 b0 = *reinterpret_cast<const bf16x8 *>(bp);
+            const bf16x8 b1 = *reinterpret_cast<const bf16x8 *>(bp + 2 * PLB);
+            const bf16x8 b2 = *reinterpret_cast<const bf16x8 *>(bp + 4 * PLB);
+            // terms of order 2^-16 first, then 2^-8, then the leading product
+            C = __builtin_amdgcn_mfma_f32_32x32x16_bf16(A[0][s], b2, C, 0, 0, 0);
+            C = __builtin_amdgcn_mfma_f32_32x32x16_bf16(A[1][s], b1, C, 0, 0, 0);
+            C = __builtin_amdgcn_mfma_f32_32x32x16_bf16(A[2][s], b0, C, 0, 0, 0);
+            C = __builtin_amdgcn_mfma_f32_32x32x16_bf16(A[0][s], b1, C, 0, 0, 0);
+            C = __builtin_amdgcn_mfma_f32_32x32x16_bf16(A[1][s], b0, C, 0, 0, 0);
+            C = __builtin_amdgcn_mfma_f32_32x32x16_bf16(A[0][s], b0, C, 0, 0, 0);
+        }
+
+        // accumulator (col r32, row (r&3) + 8(r>>2) + 4hh) -> stage[sg][i][comp]
+#pragma unroll
+        for (int r = 0; r < 16; r++) stage[sg * SSTR + 2 * ((r & 3) + 8 * (r >> 2) + 4 * hh) + comp] = C[r];
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        const long long o0 = CH * c + 512 * wave;
+#pragma unroll
+        for (int q = 0; q < 4; q++) {
+            const int o = 2 * (lane + 64 * q);
+            const v4f a = *reinterpret_cast<const v4f *>(stage + (o >> 5) * SSTR + 2 * (o & 31));
+            const v4f r = {a.x * sre - a.y * sim, a.x * sim + a.y * sre, a.z * sre - a.w * sim,
+                           a.z * sim + a.w * sre};
+            const long long ty = o0 + o;
+            if (ty + 2 <= n) {
+                if (VAR & 2) __builtin_nontemporal_store(r, reinterpret_cast<v4f *>(y + ty));
+                else *reinterpret_cast<v4f *>(y + ty) = r;
+            } else if (ty < n) {
+                y[ty] = v2f{r.x, r.y};
+            }
+        }
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    };
+    for (long long c = c0; c < c1; c += 2) {
+        step(c, xa);
+        if (c + 1 < c1) step(c + 1, xb);
+    }
+}
+
+} // namespace
+
+// Returns 1 if the call was handled on the matrix cores: crcf, 33..64 taps
+// (HP = 64, one chunk), not in place, 16-byte aligned x and y.
+extern "C" int lqk_firfilt_mx(const lqk_fir_desc *d, const void *hist, const void *x, unsigned long long n,
+                              void *y, void *stream)
+{
+    if (d->kind != 1 || d->hc != 64 || d->nchunk != 1 || x == y) return 0;
+    if (((uintptr_t)x & 15) || ((uintptr_t)y & 15)) return 0;
+    if (n == 0) return 1;
+    const long long nch = ((long long)n + CH - 1) / CH;
+    const long long nwg = nch < 768 ? nch : 768;   // three resident per CU
+    const long long cpw = (nch + nwg - 1) / nwg;
+    // LQ_MX_VARIANT (dev): bit 0 non-temporal loads, bit 1 non-temporal stores;
+    // default 2: plain loads (non-temporal loads cost 15 %: 0.887 vs 1.019 ms
+    // per 2^28 samples), non-temporal stores
+    static int var = -1;
+    if (var < 0) {
+        const char *e = getenv("LQ_MX_VARIANT");
+        var = e ? (atoi(e) & 3) : 2;
+    }
+    const dim3 grid((unsigned)((nch + cpw - 1) / cpw));
+    const hipStream_t st = (hipStream_t)stream;
+#define LQ_MX_LAUNCH(V)                                                                                  \
+    hipLaunchKernelGGL(k_firfilt_mx<V>, grid, dim3(NT), LDS_BYTES, st, (const v2f *)hist, (const v2f *)x, \
+                       (long long)n, (v2f *)y, (const float *)d->hpad, d->scale_re, d->scale_im, nch, cpw)
+    switch (var) {
+    case 0: LQ_MX_LAUNCH(0); break;
+    case 1: LQ_MX_LAUNCH(1); break;
+    case 2: LQ_MX_LAUNCH(2); break;
+    default: LQ_MX_LAUNCH(3); break;
+    }
+#undef LQ_MX_LAUNCH
+    LQ_CHECK_LAUNCH();
+    return 1;
+}

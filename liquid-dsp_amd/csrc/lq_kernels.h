@@ -53,6 +53,10 @@ typedef struct {
 
 void lqk_firfilt(const lqk_fir_desc *d, const void *hist, const void *x, unsigned long long n,
                  void *y, void *scratch, void *stream);
+/* crcf with 33..64 taps on the matrix cores (k_firfilt_mx.hip); returns 0
+ * when the call does not qualify (then lqk_firfilt runs the VALU kernel) */
+int lqk_firfilt_mx(const lqk_fir_desc *d, const void *hist, const void *x, unsigned long long n, void *y,
+                   void *stream);
 /* bytes of scratch lqk_firfilt needs for an in-place call of n samples */
 size_t lqk_firfilt_scratch_bytes(const lqk_fir_desc *d, unsigned long long n);
 

@@ -37,6 +37,47 @@ __global__ __launch_bounds__(256) void k_mix(const f4 *__restrict__ a, f4 *__res
     }
 }
 
+// per-workgroup contiguous segments (the persistent kernels' assignment):
+// workgroup w copies elements [w*per, (w+1)*per) in 256-lane steps
+template <int K, bool NTS>
+__global__ __launch_bounds__(256) void k_seg(const f4 *__restrict__ a, f4 *__restrict__ b, long long n4, long long per)
+{
+    const long long e0 = (long long)blockIdx.x * per;
+    long long e1 = e0 + per;
+    if (e1 > n4) e1 = n4;
+    for (long long i = e0 + threadIdx.x; i < e1; i += 256) {
+        f4 v = a[i];
+#pragma unroll
+        for (int k = 0; k < K; k++) {
+            f4 w = v * (float)(k + 1);
+            if (NTS) __builtin_nontemporal_store(w, b + (long long)k * n4 + i);
+            else b[(long long)k * n4 + i] = w;
+        }
+    }
+}
+
+template <int K, bool NTS>
+void run_seg(const char *name, const f4 *a, f4 *b, long long n4, int grid)
+{
+    hipEvent_t e0, e1;
+    CK(hipEventCreate(&e0));
+    CK(hipEventCreate(&e1));
+    const long long per = (n4 + grid - 1) / grid;
+    hipLaunchKernelGGL((k_seg<K, NTS>), dim3(grid), dim3(256), 0, 0, a, b, n4, per);
+    CK(hipEventRecord(e0));
+    const int it = 20;
+    for (int i = 0; i < it; i++) hipLaunchKernelGGL((k_seg<K, NTS>), dim3(grid), dim3(256), 0, 0, a, b, n4, per);
+    CK(hipEventRecord(e1));
+    CK(hipEventSynchronize(e1));
+    float ms;
+    CK(hipEventElapsedTime(&ms, e0, e1));
+    ms /= it;
+    const double rd = 16.0 * n4, wr = 16.0 * n4 * K;
+    printf("%-34s grid %6d  %8.3f ms  read %6.0f GB/s  write %6.0f GB/s  total %6.0f GB/s\n", name, grid, ms,
+           rd / ms / 1e6, wr / ms / 1e6, (rd + wr) / ms / 1e6);
+    fflush(stdout);
+}
+
 template <int K, bool NTS>
 void run(const char *name, const f4 *a, f4 *b, long long n4, int grid)
 {
@@ -66,14 +107,15 @@ int main()
     CK(hipMalloc(&b, 2 * n4 * 16));
     CK(hipMemset(a, 1, n4 * 16));
     CK(hipMemset(b, 0, 2 * n4 * 16));
-    for (int grid : {1024, 2048, 4096, 16384}) {
-        run<0, false>("read only", a, b, n4, grid);
-        run<-1, false>("write only (1x)", a, b, n4, grid);
-        run<-1, true>("write only nt (1x)", a, b, n4, grid);
-        run<1, false>("copy 1:1", a, b, n4, grid);
-        run<1, true>("copy 1:1 nt", a, b, n4, grid);
-        run<2, false>("read 1 : write 2", a, b, n4, grid);
-        run<2, true>("read 1 : write 2 nt", a, b, n4, grid);
+    for (int grid : {1024, 2048, 4096}) {
+        run<1, true>("copy 1:1 nt (grid-stride)", a, b, n4, grid);
+        run_seg<1, true>("copy 1:1 nt (per-WG segment)", a, b, n4, grid);
+        run<2, true>("read 1 : write 2 nt (grid-stride)", a, b, n4, grid);
+        run_seg<2, true>("read 1 : write 2 nt (per-WG seg)", a, b, n4, grid);
+    }
+    for (int grid : {256, 512}) {
+        run_seg<1, true>("copy 1:1 nt (per-WG segment)", a, b, n4, grid);
+        run_seg<2, true>("read 1 : write 2 nt (per-WG seg)", a, b, n4, grid);
     }
     return 0;
 }
