@@ -56,7 +56,7 @@ for r in csv.DictReader(open(f)):
     d[r["Kernel_Name"]].append((int(r["Start_Timestamp"]), int(r["End_Timestamp"])))
 res = {}
 for k, v in d.items():
-    key = "firpfbch2" if "pfb2" in k else ("firfilt" if "k_firfilt<" in k else ("resamp" if "k_resamp" in k else None))
+    key = "firpfbch2" if "pfb2" in k else ("firfilt" if ("k_firfilt<" in k or "k_firfilt_mx" in k) else ("resamp" if "k_resamp" in k else None))
     if not key or len(v) < 50:
         continue
     v.sort()
