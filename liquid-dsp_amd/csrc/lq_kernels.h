@@ -175,9 +175,17 @@ void lqk_fft_r2r(int type, unsigned int n, const void *x, void *y, unsigned long
  * db: mode 0 10log10(|X|^2+1e-16) shifted, 1 10log10(v) shifted, 2 10log10(v/T) */
 void lqk_spgram_gather(int real_in, const void *hist, unsigned int W, const void *x, const long long *ends,
                        unsigned long long T, const float *w, unsigned int nfft, void *out, void *stream);
+/* per-bin reductions over T transforms; work: lqk_spgram_work_bytes(T, nfft) bytes of device scratch */
+size_t lqk_spgram_work_bytes(unsigned long long T, unsigned int nfft);
 void lqk_spgram_accumulate(const void *X, unsigned long long T, unsigned int nfft, float alpha, float *psd,
-                           void *stream);
-void lqk_spgram_sum(const void *X, unsigned long long T, unsigned int nfft, float *acc, void *stream);
+                           void *work, void *stream);
+void lqk_spgram_sum(const void *X, unsigned long long T, unsigned int nfft, float *acc, void *work, void *stream);
+/* nfft = 1024 (W <= 1024): windows gathered from (hist | x), transformed and reduced in one pass;
+ * transform t ends at e0 + t*hop (the last at elast); accum: dst = psd (exponential average),
+ * else dst = acc (sum, fft-shifted); work: lqk_spgram_work_bytes(T, 1024) bytes */
+void lqk_spgram_fused1024(int real_in, const void *hist, unsigned int W, const void *x, long long e0,
+                          long long hop, unsigned long long T, long long elast, const float *w, int accum,
+                          float alpha, float *dst, void *work, void *stream);
 void lqk_spgram_db(int mode, const void *X, const float *v, unsigned int nfft, float T, float *out, void *stream);
 
 /* ---------------------------------------------------------------- resamp2 (half-band)

@@ -34,7 +34,7 @@ typedef struct {
     size_t npend, cappend;
     fftplan plan;
     lq_ctx ctx;
-    lq_devbuf xbuf, Xbuf, ends, acc, out;
+    lq_devbuf xbuf, Xbuf, ends, acc, out, work;
 } lq_spg;
 
 static lq_spg *lq_spg_create(int real_in, unsigned int nfft, const float *window, unsigned int W, const char *who)
@@ -91,6 +91,7 @@ static void lq_spg_destroy(lq_spg *q)
     lq_devbuf_free(&q->ends);
     lq_devbuf_free(&q->acc);
     lq_devbuf_free(&q->out);
+    lq_devbuf_free(&q->work);
     lq_ctx_free(&q->ctx);
     free(q->pend);
     free(q->w);
@@ -181,7 +182,8 @@ static void lq_spg_execute_psd(lq_spg *q, float *out)
 
 static void lq_spg_each_accum(lq_spg *q, const void *X, unsigned long long T, void *arg)
 {
-    lqk_spgram_accumulate(X, T, q->nfft, *(float *)arg, q->d_psd, q->ctx.stream);
+    void *w = lq_devbuf_get(&q->work, lqk_spgram_work_bytes(T, q->nfft));
+    lqk_spgram_accumulate(X, T, q->nfft, *(float *)arg, q->d_psd, w, q->ctx.stream);
 }
 
 static void lq_spg_accumulate_dev(lq_spg *q, const void *dx, unsigned long long n, float alpha)
@@ -195,6 +197,18 @@ static void lq_spg_accumulate_dev(lq_spg *q, const void *dx, unsigned long long 
     if (H > 0) {   /* transform after the input that brings sample_counter to W/2 */
         const long long first = (long long)(H - q->sample_counter) - 1;
         if (first < (long long)n) T = (unsigned long long)(((long long)n - 1 - first) / H + 1);
+        if (q->nfft == 1024) {   /* fused path: ends are first + t H, no table */
+            if (T > 0) {
+                float a = q->num_transforms == 0 ? 1.0f : alpha;
+                void *w = lq_devbuf_get(&q->work, lqk_spgram_work_bytes(T, q->nfft));
+                lqk_spgram_fused1024(q->real_in, q->d_hist[q->cur], q->W, dx, first, (long long)H, T,
+                                     first + (long long)((T - 1) * H), q->d_w, 1, a, q->d_psd, w, q->ctx.stream);
+                q->num_transforms += (unsigned int)T;
+            }
+            q->sample_counter = (unsigned int)((q->sample_counter + n) % H);
+            lq_spg_append_dev(q, dx, n);
+            return;
+        }
         ends = (long long *)lq_xmalloc((T ? T : 1) * sizeof(long long));
         for (unsigned long long t = 0; t < T; t++) ends[t] = first + (long long)(t * H);
         q->sample_counter = (unsigned int)((q->sample_counter + n) % H);
@@ -226,7 +240,8 @@ static void lq_spg_write_accumulation(lq_spg *q, float *out)
 
 static void lq_spg_each_sum(lq_spg *q, const void *X, unsigned long long T, void *arg)
 {
-    lqk_spgram_sum(X, T, q->nfft, (float *)arg, q->ctx.stream);
+    void *w = lq_devbuf_get(&q->work, lqk_spgram_work_bytes(T, q->nfft));
+    lqk_spgram_sum(X, T, q->nfft, (float *)arg, w, q->ctx.stream);
 }
 
 static void lq_spg_estimate_dev(lq_spg *q, const void *dx, unsigned long long n, float *dpsd)
@@ -236,12 +251,20 @@ static void lq_spg_estimate_dev(lq_spg *q, const void *dx, unsigned long long n,
     unsigned int delay = q->nfft / 4;
     if (delay == 0) delay = 1;
     unsigned long long T = n / delay + ((n % delay) ? 1 : 0);
+    float *acc = (float *)lq_devbuf_get(&q->acc, q->nfft * sizeof(float));
+    lqrt_memset(acc, q->nfft * sizeof(float), q->ctx.stream);
+    if (q->nfft == 1024) {   /* fused path: ends are delay-1 + t delay, the last one n-1 */
+        void *w = lq_devbuf_get(&q->work, lqk_spgram_work_bytes(T, q->nfft));
+        lqk_spgram_fused1024(q->real_in, q->d_hist[q->cur], q->W, dx, (long long)delay - 1, (long long)delay, T,
+                             (long long)n - 1, q->d_w, 0, 0.0f, acc, w, q->ctx.stream);
+        lqk_spgram_db(2, NULL, acc, q->nfft, (float)T, dpsd, q->ctx.stream);
+        lq_spg_append_dev(q, dx, n);
+        return;
+    }
     long long *ends = (long long *)lq_xmalloc(T * sizeof(long long));
     unsigned long long t = 0;
     for (unsigned long long i = delay - 1; i < n; i += delay) ends[t++] = (long long)i;
     if (t < T) ends[t++] = (long long)n - 1;
-    float *acc = (float *)lq_devbuf_get(&q->acc, q->nfft * sizeof(float));
-    lqrt_memset(acc, q->nfft * sizeof(float), q->ctx.stream);
     lq_spg_transforms(q, dx, ends, t, lq_spg_each_sum, acc);
     lqk_spgram_db(2, NULL, acc, q->nfft, (float)t, dpsd, q->ctx.stream);
     free(ends);

@@ -888,7 +888,7 @@ def _kaiser_window(W, beta):
 
 
 @pytest.mark.parametrize("real_in", [False, True])
-@pytest.mark.parametrize("nfft,W", [(64, 48), (256, 128), (1000, 1000), (2, 1)])
+@pytest.mark.parametrize("nfft,W", [(64, 48), (256, 128), (1000, 1000), (2, 1), (1024, 512), (1024, 1024), (1024, 301)])
 def test_spgram_vs_oracle(real_in, nfft, W):
     r = rng(nfft + W + real_in)
     win = _kaiser_window(W, 8.0)
