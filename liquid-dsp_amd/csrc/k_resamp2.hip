@@ -116,6 +116,61 @@ __global__ __launch_bounds__(NT) void k_resamp2(R2Args a, const C *__restrict__ 
     }
 }
 
+// Tiled form for the modes whose call i reads the dot window E_1[i+1 ..
+// i+2m] and the delay sample E_0[2m + i - m] (decim, analyzer, interp,
+// synthesizer): a workgroup stages the E_1 / E_0 spans of its C = NT*R calls
+// in LDS once (each element gathered from history or x a single time instead
+// of once per tap), then each lane evaluates R consecutive calls from a
+// register window of R + 2m - 1 samples.
+template <typename S, typename C, int R>
+__global__ __launch_bounds__(NT) void k_resamp2_tiled(R2Args a, const C *__restrict__ taps,
+                                                      const S *__restrict__ hist0, const S *__restrict__ hist1,
+                                                      const S *__restrict__ x, S *__restrict__ y0)
+{
+    constexpr int CT = NT * R;                    // calls per tile
+    extern __shared__ __attribute__((aligned(16))) unsigned char r2_smem[];
+    const int m = a.m, W = 2 * m;
+    C *th = reinterpret_cast<C *>(r2_smem);
+    S *e1 = reinterpret_cast<S *>(r2_smem + ((2 * W * sizeof(C) + 15) & ~15));   // E_1[i0+1 ...], CT + W - 1
+    S *e0 = e1 + CT + W;                                                       // E_0[W + i0 - m ...], CT
+    const long long i0 = (long long)blockIdx.x * CT;
+    for (int j = threadIdx.x; j < W; j += NT) th[j] = taps[j];
+    for (int u = threadIdx.x; u < CT + W - 1; u += NT) {
+        const long long k = i0 + 1 + u;
+        if (k - W < a.n) e1[u] = r2_E(a, 1, k, hist0, hist1, x);   // push k-W exists
+    }
+    for (int u = threadIdx.x; u < CT; u += NT) {
+        if (i0 + u < a.n) e0[u] = r2_E(a, 0, W + i0 + u - m, hist0, hist1, x);
+    }
+    __syncthreads();
+    const int l0 = threadIdx.x * R;
+    if (i0 + l0 >= a.n) return;
+    S acc[R];
+#pragma unroll
+    for (int r = 0; r < R; r++) acc[r] = S{};
+    for (int j = 0; j < W; j++) {
+        const C h = th[j];
+#pragma unroll
+        for (int r = 0; r < R; r++) acc[r] = r2_mac(h, e1[l0 + r + j], acc[r]);
+    }
+#pragma unroll
+    for (int r = 0; r < R; r++) {
+        const long long i = i0 + l0 + r;
+        if (i >= a.n) break;
+        const S yq = acc[r], yd = e0[l0 + r];
+        switch (a.mode) {
+        case LQK_R2_DECIM: y0[i] = r2_scale(a.scale, r2_add(yd, yq)); break;
+        case LQK_R2_ANALYZER:
+            y0[2 * i] = r2_add(yq, yd);
+            y0[2 * i + 1] = r2_sub(yq, yd);
+            break;
+        default:   // interp, synthesizer
+            y0[2 * i] = yd;
+            y0[2 * i + 1] = yq;
+        }
+    }
+}
+
 // new history: hist_p[k] = E_p[pushes_p + k], k < 2m
 template <typename S>
 __global__ __launch_bounds__(NT) void k_resamp2_hist(R2Args a, long long push0, long long push1,
@@ -144,9 +199,17 @@ void run_r2(const R2Args &a, const void *taps, const void *h0, const void *h1, v
         break;
     default: p0 = p1 = a.n;
     }
-    const unsigned grid = (unsigned)((a.n + NT - 1) / NT);
-    hipLaunchKernelGGL((k_resamp2<S, C>), dim3(grid), dim3(NT), (size_t)2 * a.m * sizeof(C), st, a,
-                       (const C *)taps, (const S *)h0, (const S *)h1, (const S *)x, (S *)y0, (S *)y1);
+    if (a.mode == LQK_R2_FILTER) {
+        const unsigned grid = (unsigned)((a.n + NT - 1) / NT);
+        hipLaunchKernelGGL((k_resamp2<S, C>), dim3(grid), dim3(NT), (size_t)2 * a.m * sizeof(C), st, a,
+                           (const C *)taps, (const S *)h0, (const S *)h1, (const S *)x, (S *)y0, (S *)y1);
+    } else {
+        constexpr int R = 4, CT = NT * R;
+        const size_t lds = ((2 * 2 * a.m * sizeof(C) + 15) & ~(size_t)15) + (size_t)(2 * CT + 2 * a.m) * sizeof(S);
+        const unsigned grid = (unsigned)((a.n + CT - 1) / CT);
+        hipLaunchKernelGGL((k_resamp2_tiled<S, C, R>), dim3(grid), dim3(NT), lds, st, a, (const C *)taps,
+                           (const S *)h0, (const S *)h1, (const S *)x, (S *)y0);
+    }
     LQ_CHECK_LAUNCH();
     hipLaunchKernelGGL((k_resamp2_hist<S>), dim3((unsigned)((4 * a.m + NT - 1) / NT)), dim3(NT), 0, st, a, p0, p1,
                        (const S *)h0, (const S *)h1, (const S *)x, (S *)n0, (S *)n1);
