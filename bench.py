@@ -351,7 +351,11 @@ def main():
                                        "roofline": {"bound": "hbm", "achieved": fach, "peak": HBM_PEAK_GBPS,
                                                     "unit": "GB/s", "frac": fach / HBM_PEAK_GBPS,
                                                     "traffic": fir_traffic,
-                                                    "bytes_per_unit": "16 B/sample", "launch_ms": fl_ms}}
+                                                    "bytes_per_unit": "16 B/sample", "launch_ms": fl_ms},
+                                       "arith": ("f32-accurate: taps and samples split into three bf16 terms, "
+                                                 "six exact products accumulated in f32 on "
+                                                 "v_mfma_f32_32x32x16_bf16 (k_firfilt_mx); "
+                                                 "LQ_FIRFILT_NO_MFMA=1 selects the f32 VALU kernel")}
         if rs is not None:
             rl_ms = g_rs / args.steps
             rbytes = 8.0 * rs["n"] + 8.0 * rs["nout"] / args.steps
