@@ -24,6 +24,8 @@
 #include "lq_device.h"
 #include "lq_kernels.h"
 
+#include <cstdlib>
+
 namespace {
 
 constexpr int NT = 256;
@@ -194,7 +196,15 @@ __global__ __launch_bounds__(NT) void k_resamp2(lqk_rs_plan pl, unsigned long lo
     float2 *tpl = reinterpret_cast<float2 *>(desc + CAP);
 
     const int tid = threadIdx.x;
-    for (int t = tid; t < (npfb + 1) * LP; t += NT) tpl[(t / LP) * LPS + (t % LP)] = taps2[t];
+    // pair p = 2q + e of a row goes to floats 4q + e (h_b) and 4q + 2 + e (h_b+1),
+    // so a 16-byte read gives (h_b[2q], h_b[2q+1], h_b+1[2q], h_b+1[2q+1])
+    for (int t = tid; t < (npfb + 1) * LP; t += NT) {
+        const int b = t / LP, p = t % LP;
+        float *row = reinterpret_cast<float *>(tpl + b * LPS);
+        const float2 v = taps2[t];
+        row[4 * (p >> 1) + (p & 1)] = v.x;
+        row[4 * (p >> 1) + 2 + (p & 1)] = v.y;
+    }
     const float fnpfb = (float)npfb;
     const long long ntiles = (n + TIN - 1) / TIN;
     constexpr int NXV = (TS + NT - 1) / NT;       // tile samples per lane
@@ -294,13 +304,19 @@ __global__ __launch_bounds__(NT) void k_resamp2(lqk_rs_plan pl, unsigned long lo
 #pragma unroll
                 for (int q = 0; q < NW; q++) {
                     const v4f t = *reinterpret_cast<const v4f *>(tp + 2 * q);
-                    const float c0 = t.x + mu * (t.y - t.x);
-                    const float c1 = t.z + mu * (t.w - t.z);
                     if constexpr (sizeof(S) == 8) {    // two complex samples: one 16-byte read
+                        // packed: (c0, c1) = (t.x, t.z) + mu ((t.y, t.w) - (t.x, t.z)), then
+                        // acc += c0 w0 + c1 w1 as two v_pk_fma_f32 on (re, im)
+                        const v2f lo = {t.x, t.y}, hi = {t.z, t.w};
+                        const v2f c = lo + v2f{mu, mu} * (hi - lo);
                         const v4f w = *reinterpret_cast<const v4f *>(wp + 2 * q);
-                        acc = rs_axpy(c0, make_float2(w.x, w.y), acc);
-                        acc = rs_axpy(c1, make_float2(w.z, w.w), acc);
+                        v2f a2 = {acc.x, acc.y};
+                        a2 = v2f{c.x, c.x} * v2f{w.x, w.y} + a2;
+                        a2 = v2f{c.y, c.y} * v2f{w.z, w.w} + a2;
+                        acc = make_float2(a2.x, a2.y);
                     } else {                           // two real samples: one 8-byte read
+                        const float c0 = t.x + mu * (t.z - t.x);
+                        const float c1 = t.y + mu * (t.w - t.y);
                         const float2 w = *reinterpret_cast<const float2 *>(wp + 2 * q);
                         acc = rs_axpy(c0, w.x, acc);
                         acc = rs_axpy(c1, w.y, acc);
