@@ -25,7 +25,9 @@ stream the kernel runs on; peak 8000 GB/s (MI355X HBM3E spec).
 
 cpu_baseline: the CPU oracle (oracle/oracle.c, a restatement of the
 reference firpfbch2.c analyzer; "port") on one host core, rank 0 at N=1
-only, over a bounded sample of the same workload (>= ~10 s of CPU work).
+only, over a bounded sample of the same workload (>= ~10 s of CPU work);
+the secondary legs carry their own oracle rates (firfilt, resamp, fftfilt,
+dotprod n=64; ~2.5 s each).
 """
 import argparse
 import json
@@ -270,6 +272,52 @@ def cpu_baseline(seconds):
                       "(%.1f s, 1 thread)" % (done // chunk, el)}
 
 
+def cpu_baselines_secondary(seconds):
+    """Oracle rates for the secondary legs (configs[0], [1], [2], [4]) on one
+    host core, each over a bounded sample of about `seconds` of CPU work."""
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    import numpy as np
+
+    import oracle_lib as O
+    rng = np.random.default_rng(10)
+
+    def cx(n):
+        return (rng.uniform(-0.5, 0.5, n) + 1j * rng.uniform(-0.5, 0.5, n)).astype(np.complex64)
+
+    def timed(fn, units_per_call, what, unit):
+        done, t0 = 0, time.perf_counter()
+        while True:
+            fn()
+            done += units_per_call
+            el = time.perf_counter() - t0
+            if el >= seconds:
+                break
+        return {"value": done / el / 1e6, "unit": unit, "cores": 1, "kind": "port",
+                "sample": "%s, %d units (%.1f s, 1 thread)" % (what, done, el)}
+
+    out = {}
+    h64 = rng.uniform(-0.5, 0.5, 64).astype(np.float32)
+    ff = O.FirFilt(O.CRCF, h64)
+    x = cx(1 << 18)
+    out["firfilt_crcf_h64"] = timed(lambda: ff.execute_block(x), len(x),
+                                    "oracle firfilt_crcf h=64 execute_block on 2^18-sample blocks", "Msamples/s")
+    rs = O.Resamp(1.037, 7, 0.25, 60.0, 64)
+    out["resamp_crcf_r1037"] = timed(lambda: rs.execute_block(x), len(x),
+                                     "oracle resamp_crcf r=1.037 m=7 npfb=64 on 2^18-sample blocks",
+                                     "Msamples/s (input)")
+    h512 = rng.uniform(-0.5, 0.5, 512).astype(np.float32)
+    fq = O.FftFilt(O.CRCF, h512, 2048)
+    xb = cx(2048)
+    out["fftfilt_crcf_h512"] = timed(lambda: fq.execute(xb), 2048,
+                                     "oracle fftfilt_crcf h=512 (n=2048, nfft=4096) execute per block",
+                                     "Msamples/s")
+    hd = cx(64)
+    X = cx(64 * (1 << 14))
+    out["dotprod_cccf_n64"] = timed(lambda: O.dotprod_batch(O.CCCF, hd, X), 1 << 14,
+                                    "oracle dotprod_cccf n=64 over batches of 2^14 vectors", "M dot products/s")
+    return out
+
+
 def main():
     args = parse()
     world, rank, local = setup_dist()
@@ -304,9 +352,10 @@ def main():
         ff_t = (allreduce_max(ff["wall"], world), allreduce_max(ff["gpu_ms"], world))
 
     copy_gbps = copy_bandwidth() if rank == 0 else None
-    cpu = None
+    cpu = cpu2 = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         cpu = cpu_baseline(args.cpu_seconds)
+        cpu2 = cpu_baselines_secondary(args.cpu_seconds / 4)
 
     if rank == 0:
         # dominant kernel: firpfbch2 analyzer, one launch per step (+ a tiny
@@ -385,6 +434,11 @@ def main():
                                         "launch_ms": ms, "achieved_GBps": 16.0 * ff["n"] / (ms * 1e-3) / 1e9,
                                         "frac": 16.0 * ff["n"] / (ms * 1e-3) / 1e9 / HBM_PEAK_GBPS,
                                         "bytes_per_unit": "16 B/sample"}
+        if cpu2:
+            for leg, c in cpu2.items():
+                key = "dotprod_cccf" if leg == "dotprod_cccf_n64" else leg
+                if key in out:
+                    out[key]["cpu_baseline"] = c
         print(json.dumps(out))
     if world > 1:
         dist.barrier()
