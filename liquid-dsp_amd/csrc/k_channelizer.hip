@@ -612,6 +612,7 @@ extern "C" void lqk_firpfbch_analyzer(int ctaps, unsigned int M, unsigned int p,
                                       const void *x, unsigned long long nblocks, void *Y, void *stream)
 {
     if (nblocks == 0) return;
+    if (lqk_firpfbch_analyzer_fast(ctaps, M, p, hsub, hist, x, nblocks, Y, stream)) return;
     hipStream_t st = (hipStream_t)stream;
     const long long tot = (long long)nblocks * M;
     const dim3 grid((unsigned)((tot + 255) / 256));

@@ -431,6 +431,147 @@ __global__ __launch_bounds__(NT, 1) void k_pfb2_an1024(Params P, const float *__
     }
 }
 
+// ---------------------------------------------------------------- firpfbch analyzer
+// Critically sampled analyzer (firpfbch_crcf, M = 1024, real taps), the same
+// structure for the reference's firpfbch.c:346-409: row b = x[bM .. bM+M),
+// X_b[j] = sum_{n<P} h[(M-1-j) P + n] row_{b-n}[j], Y_b = FFT_forward(X_b).
+// Every row completes one block, so an iteration streams 16 rows into 16
+// block buffers (no half-block carried over) and 16 waves transform them.
+
+// forward (DIR +1) / backward tables: tw1[k1*64 + t] = W_1024^{DIR t k1},
+// tw2[r*4 + b] = W_64^{DIR b r}
+template <int DIR>
+__device__ __forceinline__ void fft1k_tables(float2 *tw1, float2 *tw2, const float2 *__restrict__ tw4096, int tid)
+{
+    const int k1 = tid >> 6, t = tid & 63;
+    const float2 w = tw4096[(4 * t * k1) & 4095];
+    tw1[tid] = make_float2(w.x, DIR > 0 ? w.y : -w.y);
+    if (tid < 64) {
+        const int r = tid >> 2, b = tid & 3;
+        const float2 u = tw4096[(64 * b * r) & 4095];
+        tw2[tid] = make_float2(u.x, DIR > 0 ? u.y : -u.y);
+    }
+}
+
+// one 1024-point transform of B (one wave, packed 16 x 16 x 4; B is the
+// block's own LDS buffer, used as transpose scratch) stored to Yb with
+// 16-byte non-temporal stores
+template <int DIR>
+__device__ __forceinline__ void fft1k_wave_store(float2 *B, const float2 *tw1, const float2 *tw2, int lane, float2 *Yb)
+{
+    v2f v[16];
+#pragma unroll
+    for (int k = 0; k < 16; k++) v[k] = pk(B[lane + 64 * k]);
+    pk_dft16<DIR>(v);
+#pragma unroll
+    for (int k1 = 1; k1 < 16; k1++) v[k1] = pk_cmul(v[k1], pk(tw1[k1 * 64 + lane]));
+    lds_fence();
+#pragma unroll
+    for (int k1 = 0; k1 < 16; k1++) B[k1 * TSTR + lane] = unpk(v[k1]);
+    lds_fence();
+    const int k1 = lane >> 2, bq = lane & 3;
+#pragma unroll
+    for (int a = 0; a < 16; a++) v[a] = pk(B[k1 * TSTR + 4 * a + bq]);
+    pk_dft16<DIR>(v);
+#pragma unroll
+    for (int r = 1; r < 16; r++) v[r] = pk_cmul(v[r], pk(tw2[r * 4 + bq]));
+    lds_fence();
+#pragma unroll
+    for (int r = 0; r < 16; r++) B[k1 + 16 * r + 260 * bq] = unpk(v[r]);
+    lds_fence();
+    typedef float v4f __attribute__((ext_vector_type(4)));
+    const int t2 = lane >> 3, p2 = lane & 7;
+    v4f *Yv = reinterpret_cast<v4f *>(Yb + 2 * p2 + 16 * t2);
+#pragma unroll
+    for (int u = 0; u < 2; u++) {
+        v4f c[4];
+#pragma unroll
+        for (int q = 0; q < 4; q++) c[q] = *reinterpret_cast<const v4f *>(B + 2 * p2 + 16 * (t2 + 8 * u) + 260 * q);
+        v2f e0[4] = {c[0].xy, c[1].xy, c[2].xy, c[3].xy};
+        v2f e1[4] = {c[0].zw, c[1].zw, c[2].zw, c[3].zw};
+        pk_dft4<DIR>(e0[0], e0[1], e0[2], e0[3]);
+        pk_dft4<DIR>(e1[0], e1[1], e1[2], e1[3]);
+#pragma unroll
+        for (int sidx = 0; sidx < 4; sidx++) {
+            const v4f val = {e0[sidx].x, e0[sidx].y, e1[sidx].x, e1[sidx].y};
+            __builtin_nontemporal_store(val, Yv + (128 * u + 256 * sidx) / 2);
+        }
+    }
+}
+
+template <int P, int PF>
+__global__ __launch_bounds__(NT, 1) void k_pfb_an1024(const float2 *hist, const float2 *x, long long nblk, int gpw,
+                                                      const float *__restrict__ hsub,
+                                                      const float2 *__restrict__ tw4096, float2 *Y)
+{
+    static_assert(P <= 8, "ring of 8 rows");
+    __shared__ __attribute__((aligned(16))) float2 xb[16 * BSTR];
+    __shared__ __attribute__((aligned(16))) float2 tw1[16 * 64];
+    __shared__ __attribute__((aligned(16))) float2 tw2[16 * 4];
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    fft1k_tables<+1>(tw1, tw2, tw4096, tid);
+    // column tid: X[j] with i = M-1-j taps h[i P + n]
+    float hv[P];
+    {
+        int o = (M - 1 - tid) * P;
+        asm volatile("" : "+v"(o));
+#pragma unroll
+        for (int n = 0; n < P; n++) hv[n] = hsub[o + n];
+    }
+    const long long ngroups = (nblk + 15) / 16;
+    const long long gs = (long long)blockIdx.x * gpw;
+    long long ge = gs + gpw;
+    if (ge > ngroups) ge = ngroups;
+    const long long HL = (long long)(P - 1) * M;
+    // rows through two range-checked buffer descriptors: x (nblk rows) and
+    // the history (P-1 rows before x); out-of-range loads return 0
+    const __amdgpu_buffer_rsrc_t rx =
+        __builtin_amdgcn_make_buffer_rsrc((void *)x, (short)0, (int)(nblk * M * 8), 0x00020000);
+    const __amdgpu_buffer_rsrc_t rh =
+        __builtin_amdgcn_make_buffer_rsrc((void *)hist, (short)0, (int)(HL * 8), 0x00020000);
+    const long long R0 = 16 * gs - 8;   // first row this workgroup touches
+    const long long ib = R0 * M + tid;
+    const unsigned ox0 = (unsigned)(ib * 8), oh0 = (unsigned)((HL + ib) * 8);
+    auto fetch = [&](long long c) -> float2 {
+        const unsigned k = (unsigned)(c - R0) * (unsigned)(M * 8);
+        const float2 a = __builtin_bit_cast(float2, __builtin_amdgcn_raw_buffer_load_b64(rx, ox0 + k, 0, 0));
+        const float2 b = __builtin_bit_cast(float2, __builtin_amdgcn_raw_buffer_load_b64(rh, oh0 + k, 0, 0));
+        return make_float2(a.x + b.x, a.y + b.y);
+    };
+    // row c lives in ring slot c & 7
+    float2 w[8];
+#pragma unroll
+    for (int s = 1; s < 8; s++) w[(8 - s) & 7] = fetch(16 * gs - s);
+    w[0] = make_float2(0.f, 0.f);
+    float2 pf[PF];
+#pragma unroll
+    for (int r = 0; r < PF; r++) pf[r] = fetch(16 * gs + r);
+    __syncthreads();   // twiddle tables ready
+
+    for (long long g = gs; g < ge; g++) {
+#pragma unroll
+        for (int r = 0; r < 16; r++) {
+            w[r & 7] = r < PF ? pf[r] : fetch(16 * g + r);
+            float2 acc = make_float2(0.f, 0.f);
+#pragma unroll
+            for (int n = 0; n < P; n++) {
+                const float2 v = w[(r - n) & 7];
+                acc.x = fmaf(hv[n], v.x, acc.x);
+                acc.y = fmaf(hv[n], v.y, acc.y);
+            }
+            xb[r * BSTR + tid] = acc;   // X[j], j = the lane's column
+        }
+        if (g + 1 < ge) {
+#pragma unroll
+            for (int r = 0; r < PF; r++) pf[r] = fetch(16 * (g + 1) + r);
+        }
+        lds_barrier();
+        const long long b = 16 * g + wave;
+        if (b < nblk) fft1k_wave_store<+1>(xb + wave * BSTR, tw1, tw2, lane, Y + b * M);
+        lds_barrier();
+    }
+}
+
 } // namespace
 
 // Returns 1 if handled by the fast path.  Launches cover at most 2^18 blocks
@@ -470,6 +611,39 @@ extern "C" int lqk_firpfbch2_analyzer_fast(unsigned int Mch, unsigned int m, con
             hipLaunchKernelGGL(k_pfb2_an1024<8>, dim3((unsigned)nwg), dim3(NT), 0, st, P, (const float *)hsub, tw);
         else
             hipLaunchKernelGGL(k_pfb2_an1024<4>, dim3((unsigned)nwg), dim3(NT), 0, st, P, (const float *)hsub, tw);
+        LQ_CHECK_LAUNCH();
+    }
+    return 1;
+}
+
+// firpfbch_crcf analyzer, M = 1024, P = 8 or 4 real-tap branches: returns 1
+// if handled.  Launches cover at most 2^17 blocks (2^27 samples) so buffer
+// offsets fit 31 bits; later chunks take their history from the input.
+extern "C" int lqk_firpfbch_analyzer_fast(int ctaps, unsigned int Mch, unsigned int p, const void *hsub,
+                                          const void *hist, const void *x, unsigned long long nblocks, void *Y,
+                                          void *stream)
+{
+    if (ctaps || Mch != (unsigned)M || !(p == 8 || p == 4)) return 0;
+    if (((uintptr_t)x & 7) || ((uintptr_t)hist & 7) || ((uintptr_t)Y & 15)) return 0;
+    if (nblocks == 0) return 1;
+    hipStream_t st = (hipStream_t)stream;
+    const float2 *tw = (const float2 *)lqrt_twiddles();
+    const long long HL = (long long)(p - 1) * M;
+    const long long CH = 1LL << 17;
+    for (long long ob = 0; ob < (long long)nblocks; ob += CH) {
+        const long long nb = ((long long)nblocks - ob) < CH ? ((long long)nblocks - ob) : CH;
+        const float2 *xs = (const float2 *)x + ob * M;
+        const float2 *hs = ob == 0 ? (const float2 *)hist : xs - HL;
+        const long long ngroups = (nb + 15) / 16;
+        long long gpw = (ngroups + 255) / 256;
+        if (gpw < 2) gpw = 2;
+        const unsigned nwg = (unsigned)((ngroups + gpw - 1) / gpw);
+        if (p == 8)
+            hipLaunchKernelGGL((k_pfb_an1024<8, 12>), dim3(nwg), dim3(NT), 0, st, hs, xs, nb, (int)gpw,
+                               (const float *)hsub, tw, (float2 *)Y + ob * M);
+        else
+            hipLaunchKernelGGL((k_pfb_an1024<4, 16>), dim3(nwg), dim3(NT), 0, st, hs, xs, nb, (int)gpw,
+                               (const float *)hsub, tw, (float2 *)Y + ob * M);
         LQ_CHECK_LAUNCH();
     }
     return 1;

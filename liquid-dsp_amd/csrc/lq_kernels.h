@@ -96,6 +96,9 @@ void lqk_firpfbch2_analyzer(unsigned int M, unsigned int m, const void *hsub, co
  * shape is not covered (caller then uses lqk_firpfbch2_analyzer).  B0 = global
  * index of the first block (only its parity matters).  hsub here is the tap
  * table already multiplied by 1/M (the kernel applies no output scale). */
+/* firpfbch_crcf analyzer M = 1024, p in {4, 8}, real taps (k_pfb2_fast.hip); 0 = not handled */
+int lqk_firpfbch_analyzer_fast(int ctaps, unsigned int M, unsigned int p, const void *hsub, const void *hist,
+                               const void *x, unsigned long long nblocks, void *Y, void *stream);
 int lqk_firpfbch2_analyzer_fast(unsigned int M, unsigned int m, const void *hsub, const void *hist,
                                 const void *x, unsigned long long nblocks, long long B0, void *Y,
                                 void *stream);
