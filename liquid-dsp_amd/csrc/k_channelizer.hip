@@ -635,6 +635,7 @@ extern "C" void lqk_firpfbch_synthesizer(int ctaps, unsigned int M, unsigned int
                                          void *stream)
 {
     if (nblocks == 0) return;
+    if (lqk_firpfbch_synthesizer_fast(ctaps, M, p, hsub, state, X, nblocks, y, stream)) return;
     hipStream_t st = (hipStream_t)stream;
     const long long HB = (long long)p - 1;
     float2 *Z = (float2 *)zscratch;

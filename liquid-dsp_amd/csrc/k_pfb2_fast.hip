@@ -34,6 +34,7 @@
 //    = offset 0, odd = M/2), so calls of any length and start parity share one
 //    kernel; blocks outside the call are computed but not stored.
 #include "lq_device.h"
+#include "lq_fft1024.h"
 #include "lq_kernels.h"
 
 #include <cstdint>
@@ -572,6 +573,90 @@ __global__ __launch_bounds__(NT, 1) void k_pfb_an1024(const float2 *hist, const 
     }
 }
 
+// ---------------------------------------------------------------- firpfbch synthesizer
+// firpfbch.c:314-336 mirrored: Z_b = IFFT(X_b) (unnormalised), y_b[i] =
+// sum_{n<P} h[i P + n] Z_{b-n}[i].  Per iteration the 16 waves transform 16
+// blocks of X (prefetched into registers one iteration ahead) into LDS; then
+// lane i pulls column i of the 16 results through a register ring of the
+// last 8 Z values and writes y_b[i] (64 consecutive samples per wave
+// instruction).  A workgroup rebuilds its first blocks' history by
+// transforming the 7 X blocks before its range (or reads the object's state).
+template <int P>
+__global__ __launch_bounds__(NT, 1) void k_pfb_syn1024(const float2 *__restrict__ X, long long nblk, int gpw,
+                                                       const float *__restrict__ hsub,
+                                                       const float2 *__restrict__ state,
+                                                       const float2 *__restrict__ tw4096, float2 *y)
+{
+    static_assert(P <= 8, "ring of 8");
+    __shared__ __attribute__((aligned(16))) float2 zb[16 * BSTR];
+    __shared__ __attribute__((aligned(16))) float2 tw1[16 * 64];
+    __shared__ __attribute__((aligned(16))) float2 tw2[16 * 4];
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    fft1k_tables<-1>(tw1, tw2, tw4096, tid);
+    float hv[P];
+    {
+        int o = tid * P;
+        asm volatile("" : "+v"(o));
+#pragma unroll
+        for (int n = 0; n < P; n++) hv[n] = hsub[o + n];
+    }
+    const long long ngroups = (nblk + 15) / 16;
+    const long long gs = (long long)blockIdx.x * gpw;
+    long long ge = gs + gpw;
+    if (ge > ngroups) ge = ngroups;
+    const long long b0 = 16 * gs;
+    const int zi = tid + 4 * (tid >> 8);   // natural-order bin tid in a transform buffer
+
+    auto load_block = [&](long long b, float2 (&v)[16]) {
+        const float2 *Xb = X + b * M + lane;
+#pragma unroll
+        for (int k = 0; k < 16; k++) v[k] = Xb[64 * k];
+    };
+    __syncthreads();   // twiddle tables ready
+    // history: Z_{b0-1} .. Z_{b0-P+1}
+    if (wave < P - 1 && b0 - (P - 1) + wave >= 0) {
+        float2 v[16];
+        load_block(b0 - (P - 1) + wave, v);
+        fft1024_wave<-1>(v, zb + wave * BSTR, tw1, tw2, lane);
+    }
+    __syncthreads();
+    float2 zr[8];
+#pragma unroll
+    for (int s = 0; s < 8; s++) zr[s] = make_float2(0.f, 0.f);
+#pragma unroll
+    for (int s = 1; s < P; s++) {
+        const long long c = b0 - s;   // buffer (P-1) - s
+        zr[c & 7] = c < 0 ? state[(P - 1 + c) * M + tid] : zb[(P - 1 - s) * BSTR + zi];
+    }
+    float2 xv[16];
+    if (b0 + wave < nblk) load_block(b0 + wave, xv);
+    __syncthreads();   // history buffers consumed
+
+    for (long long g = gs; g < ge; g++) {
+        const long long b = 16 * g + wave;
+        float2 v[16];
+#pragma unroll
+        for (int k = 0; k < 16; k++) v[k] = xv[k];
+        if (g + 1 < ge && b + 16 < nblk) load_block(b + 16, xv);
+        if (b < nblk) fft1024_wave<-1>(v, zb + wave * BSTR, tw1, tw2, lane);
+        lds_barrier();
+#pragma unroll
+        for (int r = 0; r < 16; r++) {
+            const long long bb = 16 * g + r;
+            zr[(16 * g + r) & 7] = zb[r * BSTR + zi];
+            float2 acc = make_float2(0.f, 0.f);
+#pragma unroll
+            for (int n = 0; n < P; n++) {
+                const float2 z = zr[(16 * g + r - n) & 7];
+                acc.x = fmaf(hv[n], z.x, acc.x);
+                acc.y = fmaf(hv[n], z.y, acc.y);
+            }
+            if (bb < nblk) y[bb * M + tid] = acc;
+        }
+        lds_barrier();
+    }
+}
+
 } // namespace
 
 // Returns 1 if handled by the fast path.  Launches cover at most 2^18 blocks
@@ -646,5 +731,31 @@ extern "C" int lqk_firpfbch_analyzer_fast(int ctaps, unsigned int Mch, unsigned 
                                (const float *)hsub, tw, (float2 *)Y + ob * M);
         LQ_CHECK_LAUNCH();
     }
+    return 1;
+}
+
+// firpfbch_crcf synthesizer, M = 1024, P = 8 or 4 real-tap branches, calls of
+// at least P-1 blocks: returns 1 if handled (y written, state advanced).
+extern "C" int lqk_firpfbch_synthesizer_fast(int ctaps, unsigned int Mch, unsigned int p, const void *hsub,
+                                             void *state, const void *X, unsigned long long nblocks, void *y,
+                                             void *stream)
+{
+    if (ctaps || Mch != (unsigned)M || !(p == 8 || p == 4) || nblocks < p - 1) return 0;
+    if (((uintptr_t)X & 7) || ((uintptr_t)y & 7)) return 0;
+    hipStream_t st = (hipStream_t)stream;
+    const float2 *tw = (const float2 *)lqrt_twiddles();
+    const long long ngroups = ((long long)nblocks + 15) / 16;
+    long long gpw = (ngroups + 255) / 256;
+    if (gpw < 2) gpw = 2;
+    const unsigned nwg = (unsigned)((ngroups + gpw - 1) / gpw);
+    if (p == 8)
+        hipLaunchKernelGGL((k_pfb_syn1024<8>), dim3(nwg), dim3(NT), 0, st, (const float2 *)X, (long long)nblocks,
+                           (int)gpw, (const float *)hsub, (const float2 *)state, tw, (float2 *)y);
+    else
+        hipLaunchKernelGGL((k_pfb_syn1024<4>), dim3(nwg), dim3(NT), 0, st, (const float2 *)X, (long long)nblocks,
+                           (int)gpw, (const float *)hsub, (const float2 *)state, tw, (float2 *)y);
+    LQ_CHECK_LAUNCH();
+    // new state: Z of the last p-1 blocks (after the kernel has read the old one)
+    lqk_fft_batch(M, -1, (const float2 *)X + (nblocks - (p - 1)) * M, state, p - 1, stream);
     return 1;
 }

@@ -99,6 +99,9 @@ void lqk_firpfbch2_analyzer(unsigned int M, unsigned int m, const void *hsub, co
 /* firpfbch_crcf analyzer M = 1024, p in {4, 8}, real taps (k_pfb2_fast.hip); 0 = not handled */
 int lqk_firpfbch_analyzer_fast(int ctaps, unsigned int M, unsigned int p, const void *hsub, const void *hist,
                                const void *x, unsigned long long nblocks, void *Y, void *stream);
+/* firpfbch_crcf synthesizer M = 1024, p in {4, 8}, real taps, nblocks >= p-1; 0 = not handled */
+int lqk_firpfbch_synthesizer_fast(int ctaps, unsigned int M, unsigned int p, const void *hsub, void *state,
+                                  const void *X, unsigned long long nblocks, void *y, void *stream);
 int lqk_firpfbch2_analyzer_fast(unsigned int M, unsigned int m, const void *hsub, const void *hist,
                                 const void *x, unsigned long long nblocks, long long B0, void *Y,
                                 void *stream);

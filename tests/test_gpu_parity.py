@@ -486,6 +486,22 @@ def test_firpfb_create_rnyquist_drnyquist(t, deriv):
 
 
 @pytest.mark.parametrize("typ", [LQ.LIQUID_ANALYZER, LQ.LIQUID_SYNTHESIZER])
+@pytest.mark.parametrize("m", [4, 2])
+def test_firpfbch_m1024_fast_path_many_workgroups(typ, m):
+    # M = 1024 fast kernels (k_pfb_an1024 / k_pfb_syn1024): 700 blocks spread
+    # over ~22 workgroups, so every workgroup but the first rebuilds its
+    # history from the input; a ragged second call continues the stream
+    M, nb = 1024, 700
+    r = rng(40 + m + typ)
+    x = cx(r, (nb + 9) * M)
+    g = LQ.FirPfbch(typ, M, m=m, As=60.0)
+    o = O.FirPfbch(typ, M, m=m, As=60.0)
+    y = np.concatenate([g.execute_block(x[: nb * M]), g.execute_block(x[nb * M:])])
+    ref = np.concatenate([o.execute(x[b * M:(b + 1) * M]) for b in range(nb + 9)])
+    assert G.nrm_err(y, ref) < NRM
+
+
+@pytest.mark.parametrize("typ", [LQ.LIQUID_ANALYZER, LQ.LIQUID_SYNTHESIZER])
 @pytest.mark.parametrize("M,p", [(8, 4), (64, 6), (6, 3)])
 def test_firpfbch_cccf_complex_taps(typ, M, p):
     # the channelizer is linear in its taps over the complex numbers:
