@@ -544,6 +544,12 @@ extern "C" void lqk_fft_batch(unsigned int n, int dir, const void *x, void *y, u
     fft_batch_scaled(n, dir, x, y, (long long)batch, 1.f, 1.f, 0, 0, (hipStream_t)stream);
 }
 
+extern "C" void lqk_fft_batch_scaled(unsigned int n, int dir, const void *x, void *y, unsigned long long batch,
+                                     float s1, float s2, void *stream)
+{
+    fft_batch_scaled(n, dir, x, y, (long long)batch, s1, s2, 1, 1, (hipStream_t)stream);
+}
+
 extern "C" void lqk_firpfbch2_analyzer(unsigned int M, unsigned int m, const void *hsub, const void *hist,
                                        const void *x, unsigned long long nblocks, int p0, void *Y, void *stream)
 {
@@ -582,6 +588,7 @@ extern "C" void lqk_firpfbch2_synthesizer(unsigned int M, unsigned int m, const 
                                           void *Y, void *stream)
 {
     if (nblocks == 0) return;
+    if (lqk_firpfbch2_synthesizer_fast(M, m, hsub, state, X, nblocks, p0, Y, stream)) return;
     hipStream_t st = (hipStream_t)stream;
     const long long HB = 4 * (long long)m - 1;
     float2 *Z = (float2 *)zscratch;

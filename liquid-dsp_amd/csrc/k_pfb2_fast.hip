@@ -657,6 +657,122 @@ __global__ __launch_bounds__(NT, 1) void k_pfb_syn1024(const float2 *__restrict_
     }
 }
 
+// ---------------------------------------------------------------- firpfbch2 synthesizer
+// firpfbch2.c:287-335 with M = 1024: z_b = IFFT(X_b) / M * (M/2) (= 0.5
+// IFFT, exact), block b of parity f = (p0 + b) & 1 outputs, for i < M/2,
+//   y_b[i] = sum_{n<L} h[i L + n] z_{b-2n}[c] + h[(i + M/2) L + n] z_{b-1-2n}[c],
+// c = i + f M/2: every term comes from the one column c, so lane c owns it
+// (a 16-deep register ring of z_b[c]) and writes y for the blocks whose
+// parity matches its half.  16 inverse transforms per iteration as in the
+// firpfbch synthesizer; history from the 15 X blocks before the range.
+template <int L>
+__global__ __launch_bounds__(NT, 1) void k_pfb2_syn1024(const float2 *__restrict__ X, long long nblk, int p0,
+                                                        int gpw, const float *__restrict__ hsub,
+                                                        const float2 *__restrict__ state,
+                                                        const float2 *__restrict__ tw4096, float2 *y)
+{
+    static_assert(2 * L <= 16, "ring of 16");
+    constexpr int HB = 2 * L - 1;
+    __shared__ __attribute__((aligned(16))) float2 zb[16 * BSTR];
+    __shared__ __attribute__((aligned(16))) float2 tw1[16 * 64];
+    __shared__ __attribute__((aligned(16))) float2 tw2[16 * 4];
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    fft1k_tables<-1>(tw1, tw2, tw4096, tid);
+    const int c = tid, f = c >= M2 ? 1 : 0, i = c - f * M2;
+    // taps are re-read (L1 hits) in each column phase instead of being held
+    // across the transforms (register budget)
+    float h0[L], h1[L];
+    auto load_taps = [&]() {
+        int o0 = i * L, o1 = (i + M2) * L;
+        asm volatile("" : "+v"(o0), "+v"(o1));
+#pragma unroll
+        for (int n = 0; n < L; n++) {
+            h0[n] = hsub[o0 + n];
+            h1[n] = hsub[o1 + n];
+        }
+    };
+    const long long ngroups = (nblk + 15) / 16;
+    const long long gs = (long long)blockIdx.x * gpw;
+    long long ge = gs + gpw;
+    if (ge > ngroups) ge = ngroups;
+    const long long b0 = 16 * gs;
+    const int zi = c + 4 * (c >> 8);
+    auto load_block = [&](long long b, float2 (&v)[16]) {
+        const float2 *Xb = X + b * M + lane;
+#pragma unroll
+        for (int k = 0; k < 16; k++) v[k] = Xb[64 * k];
+    };
+    // the next block's first PFX values are prefetched during the column phase
+    constexpr int PFX = 8;
+    // 0.5 IFFT of one block into B (natural order, padded)
+    auto zform = [&](float2 (&v)[16], float2 *B) {
+        fft1024_wave<-1>(v, B, tw1, tw2, lane);
+#pragma unroll
+        for (int k = 0; k < 16; k++) {
+            const int o = lane + 64 * k;
+            float2 *p = B + o + 4 * (o >> 8);
+            *p = make_float2(p->x * (1.0f / M) * (float)M2, p->y * (1.0f / M) * (float)M2);
+        }
+        f1k_wave_fence();
+    };
+    __syncthreads();   // twiddle tables ready
+    // history z_{b0-15} .. z_{b0-1}: wave w < 15 forms z_{b0-15+w}
+    if (wave < HB && b0 - HB + wave >= 0) {
+        float2 v[16];
+        load_block(b0 - HB + wave, v);
+        zform(v, zb + wave * BSTR);
+    }
+    __syncthreads();
+    float2 zr[16];
+#pragma unroll
+    for (int s = 0; s < 16; s++) zr[s] = make_float2(0.f, 0.f);
+#pragma unroll
+    for (int s = 1; s <= HB; s++) {
+        const long long cb = b0 - s;   // buffer HB - s
+        zr[cb & 15] = cb < 0 ? state[(HB + cb) * M + c] : zb[(HB - s) * BSTR + zi];
+    }
+    float2 xv[PFX];
+    if (b0 + wave < nblk) {
+#pragma unroll
+        for (int q = 0; q < PFX; q++) xv[q] = X[(b0 + wave) * M + lane + 64 * q];
+    }
+    __syncthreads();   // history buffers consumed
+
+    for (long long g = gs; g < ge; g++) {
+        const long long b = 16 * g + wave;
+        if (b < nblk) {
+            float2 v[16];
+#pragma unroll
+            for (int q = 0; q < 16; q++) v[q] = q < PFX ? xv[q] : X[b * M + lane + 64 * q];
+            zform(v, zb + wave * BSTR);
+        }
+        lds_barrier();
+        load_taps();
+        if (g + 1 < ge && b + 16 < nblk) {
+#pragma unroll
+            for (int q = 0; q < PFX; q++) xv[q] = X[(b + 16) * M + lane + 64 * q];
+        }
+#pragma unroll
+        for (int r = 0; r < 16; r++) {
+            const long long bb = 16 * g + r;
+            zr[r] = zb[r * BSTR + zi];   // slot bb & 15 = r
+            if (((p0 + bb) & 1) == f && bb < nblk) {
+                float2 acc0 = make_float2(0.f, 0.f), acc1 = make_float2(0.f, 0.f);
+#pragma unroll
+                for (int n = 0; n < L; n++) {
+                    const float2 z0 = zr[(r - 2 * n) & 15], z1 = zr[(r - 1 - 2 * n) & 15];
+                    acc0.x = fmaf(h0[n], z0.x, acc0.x);
+                    acc0.y = fmaf(h0[n], z0.y, acc0.y);
+                    acc1.x = fmaf(h1[n], z1.x, acc1.x);
+                    acc1.y = fmaf(h1[n], z1.y, acc1.y);
+                }
+                y[bb * M2 + i] = make_float2(acc0.x + acc1.x, acc0.y + acc1.y);
+            }
+        }
+        lds_barrier();
+    }
+}
+
 } // namespace
 
 // Returns 1 if handled by the fast path.  Launches cover at most 2^18 blocks
@@ -757,5 +873,33 @@ extern "C" int lqk_firpfbch_synthesizer_fast(int ctaps, unsigned int Mch, unsign
     LQ_CHECK_LAUNCH();
     // new state: Z of the last p-1 blocks (after the kernel has read the old one)
     lqk_fft_batch(M, -1, (const float2 *)X + (nblocks - (p - 1)) * M, state, p - 1, stream);
+    return 1;
+}
+
+// firpfbch2_crcf synthesizer, M = 1024, m = 4 or 2, calls of at least 4m-1
+// blocks: returns 1 if handled (Y written, state advanced).
+extern "C" int lqk_firpfbch2_synthesizer_fast(unsigned int Mch, unsigned int m, const void *hsub, void *state,
+                                              const void *X, unsigned long long nblocks, int p0, void *Y,
+                                              void *stream)
+{
+    const unsigned HB = 4 * m - 1;
+    if (Mch != (unsigned)M || !(m == 4 || m == 2) || nblocks < HB) return 0;
+    if (((uintptr_t)X & 7) || ((uintptr_t)Y & 7)) return 0;
+    hipStream_t st = (hipStream_t)stream;
+    const float2 *tw = (const float2 *)lqrt_twiddles();
+    const long long ngroups = ((long long)nblocks + 15) / 16;
+    long long gpw = (ngroups + 255) / 256;
+    if (gpw < 2) gpw = 2;
+    const unsigned nwg = (unsigned)((ngroups + gpw - 1) / gpw);
+    if (m == 4)
+        hipLaunchKernelGGL((k_pfb2_syn1024<8>), dim3(nwg), dim3(NT), 0, st, (const float2 *)X, (long long)nblocks,
+                           p0 & 1, (int)gpw, (const float *)hsub, (const float2 *)state, tw, (float2 *)Y);
+    else
+        hipLaunchKernelGGL((k_pfb2_syn1024<4>), dim3(nwg), dim3(NT), 0, st, (const float2 *)X, (long long)nblocks,
+                           p0 & 1, (int)gpw, (const float *)hsub, (const float2 *)state, tw, (float2 *)Y);
+    LQ_CHECK_LAUNCH();
+    // new state: z of the last 4m-1 blocks, formed as the reference does (IFFT, x 1/M, x M/2)
+    lqk_fft_batch_scaled(M, -1, (const float2 *)X + (nblocks - HB) * M, state, HB, 1.0f / (float)M,
+                         (float)(M / 2), stream);
     return 1;
 }

@@ -102,6 +102,12 @@ int lqk_firpfbch_analyzer_fast(int ctaps, unsigned int M, unsigned int p, const 
 /* firpfbch_crcf synthesizer M = 1024, p in {4, 8}, real taps, nblocks >= p-1; 0 = not handled */
 int lqk_firpfbch_synthesizer_fast(int ctaps, unsigned int M, unsigned int p, const void *hsub, void *state,
                                   const void *X, unsigned long long nblocks, void *y, void *stream);
+/* firpfbch2_crcf synthesizer M = 1024, m in {2, 4}, nblocks >= 4m-1; 0 = not handled */
+int lqk_firpfbch2_synthesizer_fast(unsigned int M, unsigned int m, const void *hsub, void *state, const void *X,
+                                   unsigned long long nblocks, int p0, void *Y, void *stream);
+/* batched transforms with the two sequential output scales of fft_batch_scaled (k_channelizer.hip) */
+void lqk_fft_batch_scaled(unsigned int n, int dir, const void *x, void *y, unsigned long long batch, float s1,
+                          float s2, void *stream);
 int lqk_firpfbch2_analyzer_fast(unsigned int M, unsigned int m, const void *hsub, const void *hist,
                                 const void *x, unsigned long long nblocks, long long B0, void *Y,
                                 void *stream);

@@ -374,6 +374,21 @@ def test_firpfbch2_synthesizer_vs_oracle(M, m):
     assert G.nrm_err(y, o.execute_block(X)) < NRM
 
 
+@pytest.mark.parametrize("m", [4, 2])
+def test_firpfbch2_synthesizer_m1024_many_workgroups(m):
+    # k_pfb2_syn1024: 701 blocks over ~22 workgroups (history rebuilt from the
+    # input), odd first call so the second call starts on the other parity,
+    # then a short call below 4m-1 blocks (general path, shared state)
+    M, nb = 1024, 701
+    r = rng(60 + m)
+    X = cx(r, (nb + 20 + 3) * M)
+    g = LQ.FirPfbch2(LQ.LIQUID_SYNTHESIZER, M, m, 60.0)
+    o = O.FirPfbch2(O.SYNTHESIZER, M, m, 60.0)
+    y = np.concatenate([g.execute_block(X[: nb * M]), g.execute_block(X[nb * M:(nb + 20) * M]),
+                        g.execute_block(X[(nb + 20) * M:])])
+    assert G.nrm_err(y, o.execute_block(X)) < NRM
+
+
 @pytest.mark.parametrize("typ", [LQ.LIQUID_ANALYZER, LQ.LIQUID_SYNTHESIZER])
 @pytest.mark.parametrize("M,m", [(4, 2), (16, 3), (1024, 2), (6, 2)])
 def test_firpfbch_vs_oracle(typ, M, m):
