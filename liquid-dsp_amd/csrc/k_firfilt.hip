@@ -14,6 +14,8 @@
 #include "lq_device.h"
 #include "lq_kernels.h"
 
+#include <cstdint>
+
 namespace {
 
 constexpr int NT = 256;      // threads per workgroup
@@ -446,6 +448,75 @@ __global__ __launch_bounds__(NT) void k_firinterp(const typename kt<KIND>::T *__
     }
 }
 
+// firinterp crcf/rrrf (real taps), L <= LT taps per phase, M phases: a tile of
+// NT inputs in LDS, the phase taps in LDS (read as broadcasts), each lane
+// keeps its input's window in registers and forms all M outputs, which go
+// back through LDS so that the wave's 64*M outputs leave as contiguous 16-byte
+// stores.  Window samples older than the object's L-1 history are zero.
+template <int KIND, int LT>
+__global__ __launch_bounds__(NT) void k_firinterp_t(const typename kt<KIND>::T *__restrict__ hist,
+                                                    const typename kt<KIND>::T *__restrict__ x, long long n,
+                                                    int M, int L, const float *__restrict__ hpoly, float sre,
+                                                    float sim, typename kt<KIND>::T *__restrict__ y)
+{
+    typedef typename kt<KIND>::T T;
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    float *tp = reinterpret_cast<float *>(smem);                         // M x LT taps, zero padded
+    T *tile = reinterpret_cast<T *>(smem + ((M * LT * 4 + 15) & ~15));  // NT + LT - 1 samples
+    T *stage = tile + ((NT + LT - 1 + 3) & ~3);                            // NT * M outputs
+    const long long i0 = (long long)blockIdx.x * NT;
+    for (int e = threadIdx.x; e < M * LT; e += NT) {
+        const int p = e / LT, l = e - p * LT;
+        tp[e] = l < L ? hpoly[p * L + l] : 0.0f;
+    }
+    for (int u = threadIdx.x; u < NT + LT - 1; u += NT) {
+        const long long s = i0 - (LT - 1) + u;
+        T v = zero<T>();
+        if (s >= 0) {
+            if (s < n) v = x[s];
+        } else if (s >= -(long long)(L - 1)) {
+            v = hist[L - 1 + s];
+        }
+        tile[u] = v;
+    }
+    __syncthreads();
+    T w[LT];   // w[l] = x[i - l]
+#pragma unroll
+    for (int l = 0; l < LT; l++) w[l] = tile[threadIdx.x + LT - 1 - l];
+    T *st = stage + (threadIdx.x >> 6) * 64 * M;   // this wave's outputs, natural order
+    const int lane = threadIdx.x & 63;
+    for (int p = 0; p < M; p++) {
+        const float *hp = tp + p * LT;
+        T acc = zero<T>();
+#pragma unroll
+        for (int l = 0; l < LT; l += 4) {
+            const float4 h4 = *reinterpret_cast<const float4 *>(hp + l);
+            mac(acc, h4.x, w[l]);
+            if (l + 1 < LT) mac(acc, h4.y, w[l + 1]);
+            if (l + 2 < LT) mac(acc, h4.z, w[l + 2]);
+            if (l + 3 < LT) mac(acc, h4.w, w[l + 3]);
+        }
+        st[lane * M + p] = apply_scale(acc, sre, sim);
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    // the wave's outputs y[(iw) M .. (iw + 64) M), iw = its first input
+    const long long iw = i0 + (threadIdx.x & ~63);
+    if (iw >= n) return;
+    const long long nin = (n - iw) < 64 ? (n - iw) : 64;
+    const int nout = (int)(nin * M);
+    constexpr int VE = vec16<T>::N;
+    T *yw = y + iw * M;
+    for (int e = lane * VE; e < nout; e += 64 * VE) {
+        if (e + VE <= nout) {
+            *reinterpret_cast<float4 *>(yw + e) = *reinterpret_cast<const float4 *>(st + e);
+        } else {
+            for (int k = 0; k < VE && e + k < nout; k++) yw[e + k] = st[e + k];
+        }
+    }
+}
+
 int tile_of(int) { return TILE; }
 
 template <int KIND, int HC>
@@ -661,6 +732,34 @@ extern "C" void lqk_firinterp(int kind, const void *hpoly, unsigned int M, unsig
     if (n == 0) return;
     hipStream_t st = (hipStream_t)stream;
     const unsigned nb = (unsigned)((n + NT - 1) / NT);
+    // real taps, L <= 32, 16-byte aligned output: the register-window kernel
+    if (kind != 2 && L <= 32 && M <= 64 && ((uintptr_t)y & 15) == 0) {
+        const int LT = L <= 8 ? 8 : L <= 12 ? 12 : L <= 16 ? 16 : L <= 20 ? 20 : L <= 24 ? 24 : 32;
+        const size_t es = elem_size(kind);
+        const size_t lds2 = (((size_t)M * LT * 4 + 15) & ~(size_t)15) + (((size_t)NT + LT - 1 + 3) & ~(size_t)3) * es +
+                            (size_t)NT * M * es;
+        if (lds2 <= 64 * 1024) {
+#define LQ_FI(K, LTV)                                                                                             \
+    hipLaunchKernelGGL((k_firinterp_t<K, LTV>), dim3(nb), dim3(NT), lds2, st, (const typename kt<K>::T *)hist,     \
+                       (const typename kt<K>::T *)x, (long long)n, (int)M, (int)L, (const float *)hpoly, sre, sim, \
+                       (typename kt<K>::T *)y)
+#define LQ_FI_L(K)                                                                                                \
+    switch (LT) {                                                                                                 \
+    case 8: LQ_FI(K, 8); break;                                                                                   \
+    case 12: LQ_FI(K, 12); break;                                                                                 \
+    case 16: LQ_FI(K, 16); break;                                                                                 \
+    case 20: LQ_FI(K, 20); break;                                                                                 \
+    case 24: LQ_FI(K, 24); break;                                                                                 \
+    default: LQ_FI(K, 32); break;                                                                                 \
+    }
+            if (kind == 0) { LQ_FI_L(0) }
+            else { LQ_FI_L(1) }
+#undef LQ_FI_L
+#undef LQ_FI
+            LQ_CHECK_LAUNCH();
+            return;
+        }
+    }
     const size_t lds = (size_t)(NT + L) * elem_size(kind);
     switch (kind) {
     case 0:
