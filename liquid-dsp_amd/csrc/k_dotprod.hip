@@ -148,8 +148,13 @@ void launch(const void *h, unsigned n, const void *X, long long stride, long lon
     const bool vec_ok = (n % VEC == 0) && ((stride * esz) % 16 == 0) && (((uintptr_t)X & 15) == 0) &&
                         (((uintptr_t)h & 15) == 0);
     const long long work = vec_ok ? n / VEC : n; // elements a group walks
+    // at most 8 (n <= 128 complex) or 16 lanes per vector: each lane keeps
+    // several 16-byte loads in flight and the shuffle reduction stays short
+    // (dotprod_cccf 2^20 vectors: n=64 0.61-0.69 -> 0.82, n=256 0.76 -> 0.83
+    // of the 8 TB/s spec; 64 lanes per vector before)
+    const int gmax = work <= 64 ? 8 : 16;
     int G = 1, lg = 0;
-    while (G < 64 && (long long)G * 2 <= work) {
+    while (G < gmax && (long long)G * 2 <= work) {
         G <<= 1;
         lg++;
     }
