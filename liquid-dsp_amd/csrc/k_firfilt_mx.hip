@@ -35,7 +35,6 @@
 
 #include <cstdint>
 #include <cstdio>
-#include <cstdlib>
 
 namespace {
 
@@ -51,7 +50,10 @@ constexpr int SPAN = CH + 64;     // samples a chunk's tiles read (64-sample hal
 constexpr int PLB = SPAN * 2 + 16 * (SPAN / 32);   // bytes per plane (5280)
 constexpr int HPB = 64 * 2 + 16 * 2;               // bytes per plane of a halo buffer
 constexpr int SSTR = 68;          // floats per staged segment (32 x re/im + pad)
-constexpr int LDS_BYTES = 6 * PLB + 2 * 6 * HPB + 4 * 16 * SSTR * 4;   // 51008: three workgroups per CU
+// crcf: one staged accumulator per wave (51008 B: three workgroups per CU);
+// cccf: two (the real- and imaginary-tap products; 68416 B: two per CU)
+template <bool CC>
+constexpr int lds_bytes_mx() { return 6 * PLB + 2 * 6 * HPB + (CC ? 2 : 1) * 4 * 16 * SSTR * 4; }
 
 __device__ __forceinline__ int poff(int pos) { return 2 * pos + 16 * (pos >> 5); }
 
@@ -94,14 +96,13 @@ __device__ __forceinline__ v2f sample_at(const v2f *__restrict__ win, const v2f 
 {
     return t < 0 ? win[64 + t] : (t < n ? x[t] : v2f{0.f, 0.f});
 }
-template <bool NTL>
 __device__ __forceinline__ void load8(const v2f *__restrict__ win, const v2f *__restrict__ x, long long n,
                                       long long s, v4f (&v)[4])
 {
     if (s >= 0 && s + 8 <= n) {
         const v4f *p = reinterpret_cast<const v4f *>(x + s);
 #pragma unroll
-        for (int q = 0; q < 4; q++) v[q] = NTL ? __builtin_nontemporal_load(p + q) : p[q];
+        for (int q = 0; q < 4; q++) v[q] = p[q];   // plain loads: non-temporal ones cost 15 %
     } else {
 #pragma unroll
         for (int q = 0; q < 4; q++) {
@@ -111,18 +112,22 @@ __device__ __forceinline__ void load8(const v2f *__restrict__ win, const v2f *__
     }
 }
 
-template <int VAR>
-__global__ __launch_bounds__(NT, 3) void k_firfilt_mx(const v2f *__restrict__ win, const v2f *__restrict__ x,
-                                                     long long n, v2f *__restrict__ y,
-                                                     const float *__restrict__ hpad, float sre, float sim,
-                                                     long long nch, long long cpw)
+// CC: complex taps (cccf).  Then H = Hr + j Hi and the tile keeps two
+// accumulators, C1 = Hr [Xr | Xi] and C2 = Hi [Xr | Xi]; y = (C1.re - C2.im,
+// C1.im + C2.re) is formed when the staged accumulators are read back.
+template <bool CC>
+__global__ __launch_bounds__(NT, CC ? 2 : 3) void k_firfilt_mx(const v2f *__restrict__ win,
+                                                              const v2f *__restrict__ x, long long n,
+                                                              v2f *__restrict__ y, const float *__restrict__ hpad,
+                                                              float sre, float sim, long long nch, long long cpw)
 {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     unsigned char *planes = smem;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int r32 = lane & 31, hh = lane >> 5;
     unsigned char *halo = smem + 6 * PLB;   // two halo buffers (chunk tails), 6 planes each
-    float *stage = reinterpret_cast<float *>(smem + 6 * PLB + 2 * 6 * HPB) + wave * 16 * SSTR;
+    constexpr int NA = CC ? 2 : 1;   // tap matrices
+    float *stage = reinterpret_cast<float *>(smem + 6 * PLB + 2 * 6 * HPB) + wave * NA * 16 * SSTR;
 
     const long long c0 = (long long)blockIdx.x * cpw;
     long long c1 = c0 + cpw;
@@ -130,24 +135,28 @@ __global__ __launch_bounds__(NT, 3) void k_firfilt_mx(const v2f *__restrict__ wi
     if (c0 >= c1) return;
 
     // A fragments: lane (row i = r32, k half hh) holds H[i][16s + 8hh + e]
-    bf16x8 A[3][6];
+    // (cccf: hpad holds (re, im) pairs; matrix a takes component a)
+    bf16x8 A[NA][3][6];
 #pragma unroll
-    for (int s = 0; s < 6; s++) {
-        bf16x2 t[3][4];
+    for (int a = 0; a < NA; a++)
 #pragma unroll
-        for (int q = 0; q < 4; q++) {
-            float hv[2];
+        for (int s = 0; s < 6; s++) {
+            bf16x2 t[3][4];
 #pragma unroll
-            for (int u = 0; u < 2; u++) {
-                const int k = r32 + 64 - (16 * s + 8 * hh + 2 * q + u);
-                hv[u] = (k >= 0 && k < 64) ? hpad[k] : 0.f;
+            for (int q = 0; q < 4; q++) {
+                float hv[2];
+#pragma unroll
+                for (int u = 0; u < 2; u++) {
+                    const int k = r32 + 64 - (16 * s + 8 * hh + 2 * q + u);
+                    hv[u] = (k >= 0 && k < 64) ? hpad[CC ? 2 * k + a : k] : 0.f;
+                }
+                split3(v2f{hv[0], hv[1]}, t[0][q], t[1][q], t[2][q]);
             }
-            split3(v2f{hv[0], hv[1]}, t[0][q], t[1][q], t[2][q]);
-        }
 #pragma unroll
-        for (int p = 0; p < 3; p++)
-            A[p][s] = bf16x8{t[p][0].x, t[p][0].y, t[p][1].x, t[p][1].y, t[p][2].x, t[p][2].y, t[p][3].x, t[p][3].y};
-    }
+            for (int p = 0; p < 3; p++)
+                A[a][p][s] =
+                    bf16x8{t[p][0].x, t[p][0].y, t[p][1].x, t[p][1].y, t[p][2].x, t[p][2].y, t[p][3].x, t[p][3].y};
+        }
 
     // plane position p of chunk c = stream sample CH c - 64 + p; positions
     // 0..63 (the previous chunk's tail) come from halo buffer (c - 1) & 1,
@@ -155,15 +164,15 @@ __global__ __launch_bounds__(NT, 3) void k_firfilt_mx(const v2f *__restrict__ wi
     // memory for the first chunk)
     if (tid < 8) {
         v4f v[4];
-        load8<(VAR & 1) != 0>(win, x, n, CH * c0 - 64 + 8 * tid, v);
+        load8(win, x, n, CH * c0 - 64 + 8 * tid, v);
         put8(halo + ((c0 - 1) & 1) * 6 * HPB, HPB, 8 * tid, v);
     }
     // two chunks in flight per workgroup: register sets xa / xb alternate
     // (the loop is unrolled by two so neither set is ever copied, which would
     // wait on its loads early)
     v4f xa[4], xb[4];
-    load8<(VAR & 1) != 0>(win, x, n, CH * c0 + 8 * tid, xa);
-    if (c0 + 1 < c1) load8<(VAR & 1) != 0>(win, x, n, CH * (c0 + 1) + 8 * tid, xb);
+    load8(win, x, n, CH * c0 + 8 * tid, xa);
+    if (c0 + 1 < c1) load8(win, x, n, CH * (c0 + 1) + 8 * tid, xb);
 
     // B operand: lane column n = r32 -> segment sg = n & 15, component n >> 4
     const int sg = r32 & 15, comp = r32 >> 4;
@@ -178,10 +187,12 @@ __global__ __launch_bounds__(NT, 3) void k_firfilt_mx(const v2f *__restrict__ wi
         }
         put8(planes, PLB, 64 + 8 * tid, xv);
         if (tid >= NT - 8) put8(halo + (c & 1) * 6 * HPB, HPB, 8 * (tid - (NT - 8)), xv);
-        if (c + 2 < c1) load8<(VAR & 1) != 0>(win, x, n, CH * (c + 2) + 8 * tid, xv);
+        if (c + 2 < c1) load8(win, x, n, CH * (c + 2) + 8 * tid, xv);
         __syncthreads();
 
-        f32x16 C = {};
+        f32x16 C[NA];
+#pragma unroll
+        for (int a = 0; a < NA; a++) C[a] = f32x16{};
 #pragma unroll
         for (int s = 0; s < 6; s++) {
             const int pos = 512 * wave + 32 * sg + 16 * s + 8 * hh;
@@ -190,17 +201,23 @@ __global__ __launch_bounds__(NT, 3) void k_firfilt_mx(const v2f *__restrict__ wi
             const bf16x8 b1 = *reinterpret_cast<const bf16x8 *>(bp + 2 * PLB);
             const bf16x8 b2 = *reinterpret_cast<const bf16x8 *>(bp + 4 * PLB);
             // terms of order 2^-16 first, then 2^-8, then the leading product
-            C = __builtin_amdgcn_mfma_f32_32x32x16_bf16(A[0][s], b2, C, 0, 0, 0);
-            C = __builtin_amdgcn_mfma_f32_32x32x16_bf16(A[1][s], b1, C, 0, 0, 0);
-            C = __builtin_amdgcn_mfma_f32_32x32x16_bf16(A[2][s], b0, C, 0, 0, 0);
-            C = __builtin_amdgcn_mfma_f32_32x32x16_bf16(A[0][s], b1, C, 0, 0, 0);
-            C = __builtin_amdgcn_mfma_f32_32x32x16_bf16(A[1][s], b0, C, 0, 0, 0);
-            C = __builtin_amdgcn_mfma_f32_32x32x16_bf16(A[0][s], b0, C, 0, 0, 0);
+#pragma unroll
+            for (int a = 0; a < NA; a++) {
+                C[a] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(A[a][0][s], b2, C[a], 0, 0, 0);
+                C[a] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(A[a][1][s], b1, C[a], 0, 0, 0);
+                C[a] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(A[a][2][s], b0, C[a], 0, 0, 0);
+                C[a] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(A[a][0][s], b1, C[a], 0, 0, 0);
+                C[a] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(A[a][1][s], b0, C[a], 0, 0, 0);
+                C[a] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(A[a][0][s], b0, C[a], 0, 0, 0);
+            }
         }
 
-        // accumulator (col r32, row (r&3) + 8(r>>2) + 4hh) -> stage[sg][i][comp]
+        // accumulator (col r32, row (r&3) + 8(r>>2) + 4hh) -> stage[a][sg][i][comp]
 #pragma unroll
-        for (int r = 0; r < 16; r++) stage[sg * SSTR + 2 * ((r & 3) + 8 * (r >> 2) + 4 * hh) + comp] = C[r];
+        for (int a = 0; a < NA; a++)
+#pragma unroll
+            for (int r = 0; r < 16; r++)
+                stage[a * 16 * SSTR + sg * SSTR + 2 * ((r & 3) + 8 * (r >> 2) + 4 * hh) + comp] = C[a][r];
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
         __builtin_amdgcn_wave_barrier();
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
@@ -208,13 +225,16 @@ __global__ __launch_bounds__(NT, 3) void k_firfilt_mx(const v2f *__restrict__ wi
 #pragma unroll
         for (int q = 0; q < 4; q++) {
             const int o = 2 * (lane + 64 * q);
-            const v4f a = *reinterpret_cast<const v4f *>(stage + (o >> 5) * SSTR + 2 * (o & 31));
+            v4f a = *reinterpret_cast<const v4f *>(stage + (o >> 5) * SSTR + 2 * (o & 31));
+            if constexpr (CC) {
+                const v4f b = *reinterpret_cast<const v4f *>(stage + 16 * SSTR + (o >> 5) * SSTR + 2 * (o & 31));
+                a = v4f{a.x - b.y, a.y + b.x, a.z - b.w, a.w + b.z};
+            }
             const v4f r = {a.x * sre - a.y * sim, a.x * sim + a.y * sre, a.z * sre - a.w * sim,
                            a.z * sim + a.w * sre};
             const long long ty = o0 + o;
             if (ty + 2 <= n) {
-                if (VAR & 2) __builtin_nontemporal_store(r, reinterpret_cast<v4f *>(y + ty));
-                else *reinterpret_cast<v4f *>(y + ty) = r;
+                __builtin_nontemporal_store(r, reinterpret_cast<v4f *>(y + ty));
             } else if (ty < n) {
                 y[ty] = v2f{r.x, r.y};
             }
@@ -231,37 +251,29 @@ __global__ __launch_bounds__(NT, 3) void k_firfilt_mx(const v2f *__restrict__ wi
 
 } // namespace
 
-// Returns 1 if the call was handled on the matrix cores: crcf, 33..64 taps
-// (HP = 64, one chunk), not in place, 16-byte aligned x and y.
+// Returns 1 if the call was handled on the matrix cores: crcf or cccf, 33..64
+// taps (HP = 64, one chunk), not in place, 16-byte aligned x and y.
 extern "C" int lqk_firfilt_mx(const lqk_fir_desc *d, const void *hist, const void *x, unsigned long long n,
                               void *y, void *stream)
 {
-    if (d->kind != 1 || d->hc != 64 || d->nchunk != 1 || x == y) return 0;
+    if ((d->kind != 1 && d->kind != 2) || d->hc != 64 || d->nchunk != 1 || x == y) return 0;
     if (((uintptr_t)x & 15) || ((uintptr_t)y & 15)) return 0;
     if (n == 0) return 1;
+    const bool cc = d->kind == 2;
     const long long nch = ((long long)n + CH - 1) / CH;
-    const long long nwg = nch < 768 ? nch : 768;   // three resident per CU
+    const long long wgs = cc ? 512 : 768;   // resident workgroups (two / three per CU)
+    const long long nwg = nch < wgs ? nch : wgs;
     const long long cpw = (nch + nwg - 1) / nwg;
-    // LQ_MX_VARIANT (dev): bit 0 non-temporal loads, bit 1 non-temporal stores;
-    // default 2: plain loads (non-temporal loads cost 15 %: 0.887 vs 1.019 ms
-    // per 2^28 samples), non-temporal stores
-    static int var = -1;
-    if (var < 0) {
-        const char *e = getenv("LQ_MX_VARIANT");
-        var = e ? (atoi(e) & 3) : 2;
-    }
     const dim3 grid((unsigned)((nch + cpw - 1) / cpw));
     const hipStream_t st = (hipStream_t)stream;
-#define LQ_MX_LAUNCH(V)                                                                                  \
-    hipLaunchKernelGGL(k_firfilt_mx<V>, grid, dim3(NT), LDS_BYTES, st, (const v2f *)hist, (const v2f *)x, \
-                       (long long)n, (v2f *)y, (const float *)d->hpad, d->scale_re, d->scale_im, nch, cpw)
-    switch (var) {
-    case 0: LQ_MX_LAUNCH(0); break;
-    case 1: LQ_MX_LAUNCH(1); break;
-    case 2: LQ_MX_LAUNCH(2); break;
-    default: LQ_MX_LAUNCH(3); break;
-    }
-#undef LQ_MX_LAUNCH
+    if (cc)
+        hipLaunchKernelGGL(k_firfilt_mx<true>, grid, dim3(NT), lds_bytes_mx<true>(), st, (const v2f *)hist,
+                           (const v2f *)x, (long long)n, (v2f *)y, (const float *)d->hpad, d->scale_re, d->scale_im,
+                           nch, cpw);
+    else
+        hipLaunchKernelGGL(k_firfilt_mx<false>, grid, dim3(NT), lds_bytes_mx<false>(), st, (const v2f *)hist,
+                           (const v2f *)x, (long long)n, (v2f *)y, (const float *)d->hpad, d->scale_re, d->scale_im,
+                           nch, cpw);
     LQ_CHECK_LAUNCH();
     return 1;
 }

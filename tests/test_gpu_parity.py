@@ -173,30 +173,32 @@ def test_firfilt_device_path_in_place():
     assert G.nrm_err(y, ref) < NRM
 
 
+@pytest.mark.parametrize("t", ["crcf", "cccf"])
 @pytest.mark.parametrize("hlen", [33, 45, 64])
-def test_firfilt_crcf_matrix_core_path_long_stream(hlen):
+def test_firfilt_crcf_matrix_core_path_long_stream(t, hlen):
     # crcf h in 33..64, device pointers, not in place: the MFMA kernel
     # (k_firfilt_mx.hip).  Several 2048-output chunks per workgroup, a ragged
     # tail, a second call continuing the stream, and a complex scale.  Held to
     # the oracle at the usual bound and to a float64 convolution at 2e-6 (the
     # three-term bf16 split is float32-accurate, not bf16-accurate).
     r = rng(100 + hlen)
-    h = r.uniform(-0.5, 0.5, hlen).astype(np.float32)
+    h = coefs(r, t, hlen)
     n1, n2 = (3 << 20) + 12345, 777
     x = cx(r, n1 + n2)
-    g = LQ.FirFilt("crcf", h)
-    g.set_scale(0.7)
+    g = LQ.FirFilt(t, h)
+    s = (0.7 - 0.2j) if t == "cccf" else 0.7
+    g.set_scale(s)
     bx = LQ.DeviceBuffer.from_array(x)
     by = LQ.DeviceBuffer(x.nbytes)
     g.execute_block_dev(bx.p, n1, by.p)
     g.execute_block_dev(bx.p + n1 * 8, n2, by.p + n1 * 8)
     g.synchronize()
     y = by.to_array(np.complex64, len(x))
-    o = O.FirFilt(O.CRCF, h)
-    o.set_scale(0.7)
+    o = O.FirFilt(TYPES[t], h)
+    o.set_scale(s)
     ref = o.execute_block(x)
     assert G.nrm_err(y, ref) < NRM
-    ref64 = 0.7 * np.convolve(x.astype(np.complex128), h.astype(np.float64))[: len(x)]
+    ref64 = s * np.convolve(x.astype(np.complex128), h.astype(np.complex128))[: len(x)]
     assert G.nrm_err(y, ref64) < 2e-6
 
 
