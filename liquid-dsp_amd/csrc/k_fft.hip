@@ -2,8 +2,8 @@
 // (include/liquid.h:1122-1216, src/fft/src/fft_common.c) and spgram.
 //
 //   n = 2^k <= 4096      : register/LDS Stockham kernel (lqk_fft_batch)
-//   n = 2^k  > 4096      : four-step n = n1 n2 -- transpose, n2 FFTs of n1,
-//                          twiddle-transpose, n1 FFTs of n2, transpose
+//   n = 2^k  > 4096      : two passes n = N1 N2 -- column transforms with the
+//                          twiddle, then row transforms written transposed
 //   other n <= 16        : direct DFT (lqk_fft_batch)
 //   other n              : Bluestein chirp-z over a power-of-two M >= 2n-1
 //                          (the chirp's FFT is computed once per plan)
@@ -18,7 +18,6 @@
 namespace {
 
 constexpr int NT = 256;
-constexpr int TT = 32;   // transpose tile
 
 __device__ __forceinline__ float2 tw_exp(long long num, long long den, int dir)
 {
@@ -28,50 +27,93 @@ __device__ __forceinline__ float2 tw_exp(long long num, long long den, int dir)
     return make_float2((float)c, (float)s);
 }
 
-// out[c*R + r] = in[r*C + c] (* W_N^(r*c) when N > 0), per transform z
-__global__ __launch_bounds__(TT * 8) void k_transpose(const float2 *__restrict__ in, float2 *__restrict__ out, int R,
-                                                      int C, long long N, int dir)
+// power-of-two n > 4096 in two passes (n = N1 N2, x as N1 rows of N2):
+//   A: the N2 columns' N1-point transforms, G columns per workgroup (G N1 =
+//      4096 samples in LDS, rows of G consecutive samples loaded), times
+//      W_n^(j2 k1), written back in place to `work`;
+//   B: the N1 rows' N2-point transforms, G rows per workgroup, written
+//      transposed: y[k1 + N1 k2] (G consecutive outputs per k2).
+// 32 bytes of HBM traffic per point instead of the six passes of a
+// transpose-based four-step.  x may alias y.
+template <int N1>
+__global__ __launch_bounds__(NT) void k_fft2p_cols(const float2 *__restrict__ x, float2 *__restrict__ work, long long n,
+                                                   int N2, int dir, const float2 *__restrict__ tw)
 {
-    __shared__ float2 t[TT][TT + 1];
-    const long long off = (long long)blockIdx.z * R * C;
-    const int c0 = blockIdx.x * TT, r0 = blockIdx.y * TT;
-    for (int k = threadIdx.y; k < TT; k += 8) {
-        const int r = r0 + k, c = c0 + threadIdx.x;
-        if (r < R && c < C) {
-            float2 v = in[off + (long long)r * C + c];
-            if (N > 0) v = cmul(v, tw_exp((long long)r * c, N, dir));
-            t[k][threadIdx.x] = v;
-        }
+    constexpr int G = 4096 / N1;
+    __shared__ __attribute__((aligned(16))) float2 a[4096];
+    __shared__ __attribute__((aligned(16))) float2 b[4096];
+    const long long off = (long long)blockIdx.z * n;
+    const int j20 = blockIdx.x * G;
+    for (int e = threadIdx.x; e < 4096; e += NT) {
+        const int j1 = e / G, g = e - j1 * G;
+        a[g * N1 + j1] = x[off + (long long)N2 * j1 + j20 + g];
     }
     __syncthreads();
-    for (int k = threadIdx.y; k < TT; k += 8) {
-        const int c = c0 + k, r = r0 + threadIdx.x;
-        if (r < R && c < C) out[off + (long long)c * R + r] = t[threadIdx.x][k];
+    const float2 *F = lds_fft<N1, G, NT>(a, b, tw, dir);
+    for (int e = threadIdx.x; e < 4096; e += NT) {
+        const int k1 = e / G, g = e - k1 * G;
+        const float2 v = cmul(F[g * N1 + k1], tw_exp((long long)(j20 + g) * k1, n, dir));
+        work[off + (long long)N2 * k1 + j20 + g] = v;
     }
 }
 
-void transpose(const void *in, void *out, int R, int C, long long batch, long long N, int dir, hipStream_t st)
+template <int N2>
+__global__ __launch_bounds__(NT) void k_fft2p_rows(const float2 *__restrict__ work, float2 *__restrict__ y, long long n,
+                                                   int N1, int dir, const float2 *__restrict__ tw)
 {
-    const dim3 grid((C + TT - 1) / TT, (R + TT - 1) / TT, (unsigned)batch);
-    hipLaunchKernelGGL(k_transpose, grid, dim3(TT, 8), 0, st, (const float2 *)in, (float2 *)out, R, C, N, dir);
+    constexpr int G = 4096 / N2;
+    __shared__ __attribute__((aligned(16))) float2 a[4096];
+    __shared__ __attribute__((aligned(16))) float2 b[4096];
+    const long long off = (long long)blockIdx.z * n;
+    const int k10 = blockIdx.x * G;
+    for (int e = threadIdx.x; e < 4096; e += NT) a[e] = work[off + (long long)N2 * k10 + e];
+    __syncthreads();
+    const float2 *F = lds_fft<N2, G, NT>(a, b, tw, dir);
+    for (int e = threadIdx.x; e < 4096; e += NT) {
+        const int k2 = e / G, g = e - k2 * G;
+        y[off + k10 + g + (long long)N1 * k2] = F[g * N2 + k2];
+    }
+}
+
+template <int N>
+void launch_cols(const void *x, void *work, long long n, int N2, int dir, long long batch, hipStream_t st)
+{
+    const dim3 g((unsigned)(N2 / (4096 / N)), 1, (unsigned)batch);
+    hipLaunchKernelGGL(k_fft2p_cols<N>, g, dim3(NT), 0, st, (const float2 *)x, (float2 *)work, n, N2, dir,
+                       (const float2 *)lqrt_twiddles());
+    LQ_CHECK_LAUNCH();
+}
+template <int N>
+void launch_rows(const void *work, void *y, long long n, int N1, int dir, long long batch, hipStream_t st)
+{
+    const dim3 g((unsigned)(N1 / (4096 / N)), 1, (unsigned)batch);
+    hipLaunchKernelGGL(k_fft2p_rows<N>, g, dim3(NT), 0, st, (const float2 *)work, (float2 *)y, n, N1, dir,
+                       (const float2 *)lqrt_twiddles());
     LQ_CHECK_LAUNCH();
 }
 
-// power-of-two n > 4096: four-step through `work` (n * batch samples); x may alias y
 void fft_four_step(unsigned n, int dir, const void *x, void *y, long long batch, void *work, hipStream_t st)
 {
     unsigned lg = 0;
     while ((1u << lg) < n) lg++;
-    const int n1 = 1 << ((lg + 1) / 2), n2 = (int)(n / (unsigned)n1);
-    // x as n1 rows x n2 cols -> A: n2 rows of n1
-    transpose(x, work, n1, n2, batch, 0, dir, st);
-    lqk_fft_batch((unsigned)n1, dir, work, work, (unsigned long long)batch * n2, st);
-    // B[j2][k1] * W_n^(j2 k1) -> C: n1 rows of n2
-    transpose(work, y, n2, n1, batch, (long long)n, dir, st);
-    lqk_fft_batch((unsigned)n2, dir, y, y, (unsigned long long)batch * n1, st);
-    // D[k1][k2] -> y[k2*n1 + k1]
-    transpose(y, work, n1, n2, batch, 0, dir, st);
-    LQ_CHECK(hipMemcpyAsync(y, work, (size_t)n * batch * sizeof(float2), hipMemcpyDeviceToDevice, st));
+    const int N1 = 1 << (lg / 2), N2 = (int)(n / (unsigned)N1);   // N1 <= N2 <= 4096 for n <= 2^24
+    switch (N1) {
+    case 64: launch_cols<64>(x, work, n, N2, dir, batch, st); break;
+    case 128: launch_cols<128>(x, work, n, N2, dir, batch, st); break;
+    case 256: launch_cols<256>(x, work, n, N2, dir, batch, st); break;
+    case 512: launch_cols<512>(x, work, n, N2, dir, batch, st); break;
+    case 1024: launch_cols<1024>(x, work, n, N2, dir, batch, st); break;
+    case 2048: launch_cols<2048>(x, work, n, N2, dir, batch, st); break;
+    default: launch_cols<4096>(x, work, n, N2, dir, batch, st); break;
+    }
+    switch (N2) {
+    case 128: launch_rows<128>(work, y, n, N1, dir, batch, st); break;
+    case 256: launch_rows<256>(work, y, n, N1, dir, batch, st); break;
+    case 512: launch_rows<512>(work, y, n, N1, dir, batch, st); break;
+    case 1024: launch_rows<1024>(work, y, n, N1, dir, batch, st); break;
+    case 2048: launch_rows<2048>(work, y, n, N1, dir, batch, st); break;
+    default: launch_rows<4096>(work, y, n, N1, dir, batch, st); break;
+    }
 }
 
 void fft_pow2(unsigned n, int dir, const void *x, void *y, long long batch, void *work, hipStream_t st)
