@@ -249,16 +249,178 @@ __global__ __launch_bounds__(NT, CC ? 2 : 3) void k_firfilt_mx(const v2f *__rest
     }
 }
 
+// ---------------------------------------------------------------- rrrf
+// Real samples: the 32 columns of a tile are 32 segments, so a wave's tile is
+// 1024 outputs and a chunk 4096; three bf16 planes.
+constexpr int CHR = 4096;
+constexpr int SPANR = CHR + 64;
+constexpr int PLBR = SPANR * 2 + 16 * (SPANR / 32);   // 10400
+constexpr int SSTRR = 36;                              // floats per staged segment (32 + pad)
+constexpr int LDS_BYTES_R = 3 * PLBR + 2 * 3 * HPB + 4 * 32 * SSTRR * 4;
+
+__device__ __forceinline__ float rsample_at(const float *__restrict__ win, const float *__restrict__ x, long long n,
+                                            long long t)
+{
+    return t < 0 ? win[64 + t] : (t < n ? x[t] : 0.f);
+}
+// 16 real samples from s (a multiple of 8)
+__device__ __forceinline__ void load16r(const float *__restrict__ win, const float *__restrict__ x, long long n,
+                                        long long s, v4f (&v)[4])
+{
+    if (s >= 0 && s + 16 <= n) {
+        const v4f *p = reinterpret_cast<const v4f *>(x + s);
+#pragma unroll
+        for (int q = 0; q < 4; q++) v[q] = p[q];
+    } else {
+#pragma unroll
+        for (int q = 0; q < 4; q++)
+            v[q] = v4f{rsample_at(win, x, n, s + 4 * q), rsample_at(win, x, n, s + 4 * q + 1),
+                       rsample_at(win, x, n, s + 4 * q + 2), rsample_at(win, x, n, s + 4 * q + 3)};
+    }
+}
+// 8 real samples (v4f pair) into the three planes at pos (a multiple of 8)
+__device__ __forceinline__ void put8r(unsigned char *planes, int pstride, int pos, v4f a, v4f b)
+{
+    bf16x2 t[3][4];
+    split3(v2f{a.x, a.y}, t[0][0], t[1][0], t[2][0]);
+    split3(v2f{a.z, a.w}, t[0][1], t[1][1], t[2][1]);
+    split3(v2f{b.x, b.y}, t[0][2], t[1][2], t[2][2]);
+    split3(v2f{b.z, b.w}, t[0][3], t[1][3], t[2][3]);
+    const int o = poff(pos);
+#pragma unroll
+    for (int p = 0; p < 3; p++) {
+        const u32x4 w = {__builtin_bit_cast(unsigned, t[p][0]), __builtin_bit_cast(unsigned, t[p][1]),
+                         __builtin_bit_cast(unsigned, t[p][2]), __builtin_bit_cast(unsigned, t[p][3])};
+        *reinterpret_cast<u32x4 *>(planes + p * pstride + o) = w;
+    }
+}
+
+__global__ __launch_bounds__(NT, 3) void k_firfilt_mx_r(const float *__restrict__ win, const float *__restrict__ x,
+                                                       long long n, float *__restrict__ y,
+                                                       const float *__restrict__ hpad, float sre, long long nch,
+                                                       long long cpw)
+{
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    unsigned char *planes = smem;
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int r32 = lane & 31, hh = lane >> 5;
+    unsigned char *halo = smem + 3 * PLBR;
+    float *stage = reinterpret_cast<float *>(smem + 3 * PLBR + 2 * 3 * HPB) + wave * 32 * SSTRR;
+    const long long c0 = (long long)blockIdx.x * cpw;
+    long long c1 = c0 + cpw;
+    if (c1 > nch) c1 = nch;
+    if (c0 >= c1) return;
+
+    bf16x8 A[3][6];
+#pragma unroll
+    for (int s = 0; s < 6; s++) {
+        bf16x2 t[3][4];
+#pragma unroll
+        for (int q = 0; q < 4; q++) {
+            float hv[2];
+#pragma unroll
+            for (int u = 0; u < 2; u++) {
+                const int k = r32 + 64 - (16 * s + 8 * hh + 2 * q + u);
+                hv[u] = (k >= 0 && k < 64) ? hpad[k] : 0.f;
+            }
+            split3(v2f{hv[0], hv[1]}, t[0][q], t[1][q], t[2][q]);
+        }
+#pragma unroll
+        for (int p = 0; p < 3; p++)
+            A[p][s] = bf16x8{t[p][0].x, t[p][0].y, t[p][1].x, t[p][1].y, t[p][2].x, t[p][2].y, t[p][3].x, t[p][3].y};
+    }
+    // halo of the first chunk: 64 samples by threads 0..3 (16 each)
+    if (tid < 4) {
+        v4f v[4];
+        load16r(win, x, n, CHR * c0 - 64 + 16 * tid, v);
+        unsigned char *hb = halo + ((c0 - 1) & 1) * 3 * HPB;
+        put8r(hb, HPB, 16 * tid, v[0], v[1]);
+        put8r(hb, HPB, 16 * tid + 8, v[2], v[3]);
+    }
+    v4f xa[4], xb[4];
+    load16r(win, x, n, CHR * c0 + 16 * tid, xa);
+    if (c0 + 1 < c1) load16r(win, x, n, CHR * (c0 + 1) + 16 * tid, xb);
+    const int sg = r32;   // B column = segment
+    auto step = [&](long long c, v4f (&xv)[4]) {
+        __syncthreads();
+        if (tid < 8) {
+            const unsigned char *hs = halo + ((c - 1) & 1) * 3 * HPB + poff(8 * tid);
+#pragma unroll
+            for (int p = 0; p < 3; p++)
+                *reinterpret_cast<u32x4 *>(planes + p * PLBR + poff(8 * tid)) =
+                    *reinterpret_cast<const u32x4 *>(hs + p * HPB);
+        }
+        put8r(planes, PLBR, 64 + 16 * tid, xv[0], xv[1]);
+        put8r(planes, PLBR, 64 + 16 * tid + 8, xv[2], xv[3]);
+        if (tid >= NT - 4) {
+            unsigned char *hb = halo + (c & 1) * 3 * HPB;
+            put8r(hb, HPB, 16 * (tid - (NT - 4)), xv[0], xv[1]);
+            put8r(hb, HPB, 16 * (tid - (NT - 4)) + 8, xv[2], xv[3]);
+        }
+        if (c + 2 < c1) load16r(win, x, n, CHR * (c + 2) + 16 * tid, xv);
+        __syncthreads();
+        f32x16 C = {};
+#pragma unroll
+        for (int s = 0; s < 6; s++) {
+            const int pos = 1024 * wave + 32 * sg + 16 * s + 8 * hh;
+            const unsigned char *bp = planes + poff(pos);
+            const bf16x8 b0 = *reinterpret_cast<const bf16x8 *>(bp);
+            const bf16x8 b1 = *reinterpret_cast<const bf16x8 *>(bp + PLBR);
+            const bf16x8 b2 = *reinterpret_cast<const bf16x8 *>(bp + 2 * PLBR);
+            C = __builtin_amdgcn_mfma_f32_32x32x16_bf16(A[0][s], b2, C, 0, 0, 0);
+            C = __builtin_amdgcn_mfma_f32_32x32x16_bf16(A[1][s], b1, C, 0, 0, 0);
+            C = __builtin_amdgcn_mfma_f32_32x32x16_bf16(A[2][s], b0, C, 0, 0, 0);
+            C = __builtin_amdgcn_mfma_f32_32x32x16_bf16(A[0][s], b1, C, 0, 0, 0);
+            C = __builtin_amdgcn_mfma_f32_32x32x16_bf16(A[1][s], b0, C, 0, 0, 0);
+            C = __builtin_amdgcn_mfma_f32_32x32x16_bf16(A[0][s], b0, C, 0, 0, 0);
+        }
+#pragma unroll
+        for (int r = 0; r < 16; r++) stage[sg * SSTRR + (r & 3) + 8 * (r >> 2) + 4 * hh] = C[r];
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        const long long o0 = CHR * c + 1024 * wave;
+#pragma unroll
+        for (int q = 0; q < 4; q++) {
+            const int o = 4 * (lane + 64 * q);
+            const v4f a = *reinterpret_cast<const v4f *>(stage + (o >> 5) * SSTRR + (o & 31)) * sre;
+            const long long ty = o0 + o;
+            if (ty + 4 <= n) {
+                __builtin_nontemporal_store(a, reinterpret_cast<v4f *>(y + ty));
+            } else {
+                for (int e = 0; e < 4 && ty + e < n; e++) y[ty + e] = a[e];
+            }
+        }
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    };
+    for (long long c = c0; c < c1; c += 2) {
+        step(c, xa);
+        if (c + 1 < c1) step(c + 1, xb);
+    }
+}
+
 } // namespace
 
-// Returns 1 if the call was handled on the matrix cores: crcf or cccf, 33..64
-// taps (HP = 64, one chunk), not in place, 16-byte aligned x and y.
+// Returns 1 if the call was handled on the matrix cores: rrrf, crcf or cccf,
+// 33..64 taps (HP = 64, one chunk), not in place, 16-byte aligned x and y.
 extern "C" int lqk_firfilt_mx(const lqk_fir_desc *d, const void *hist, const void *x, unsigned long long n,
                               void *y, void *stream)
 {
-    if ((d->kind != 1 && d->kind != 2) || d->hc != 64 || d->nchunk != 1 || x == y) return 0;
+    if (d->hc != 64 || d->nchunk != 1 || x == y) return 0;
     if (((uintptr_t)x & 15) || ((uintptr_t)y & 15)) return 0;
     if (n == 0) return 1;
+    if (d->kind == 0) {   // rrrf: 4096-output chunks, three workgroups per CU
+        const long long nch = ((long long)n + CHR - 1) / CHR;
+        const long long nwg = nch < 768 ? nch : 768;
+        const long long cpw = (nch + nwg - 1) / nwg;
+        hipLaunchKernelGGL(k_firfilt_mx_r, dim3((unsigned)((nch + cpw - 1) / cpw)), dim3(NT), LDS_BYTES_R,
+                           (hipStream_t)stream, (const float *)hist, (const float *)x, (long long)n, (float *)y,
+                           (const float *)d->hpad, d->scale_re, nch, cpw);
+        LQ_CHECK_LAUNCH();
+        return 1;
+    }
     const bool cc = d->kind == 2;
     const long long nch = ((long long)n + CH - 1) / CH;
     const long long wgs = cc ? 512 : 768;   // resident workgroups (two / three per CU)

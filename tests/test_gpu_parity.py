@@ -173,7 +173,7 @@ def test_firfilt_device_path_in_place():
     assert G.nrm_err(y, ref) < NRM
 
 
-@pytest.mark.parametrize("t", ["crcf", "cccf"])
+@pytest.mark.parametrize("t", ["rrrf", "crcf", "cccf"])
 @pytest.mark.parametrize("hlen", [33, 45, 64])
 def test_firfilt_crcf_matrix_core_path_long_stream(t, hlen):
     # crcf h in 33..64, device pointers, not in place: the MFMA kernel
@@ -184,21 +184,24 @@ def test_firfilt_crcf_matrix_core_path_long_stream(t, hlen):
     r = rng(100 + hlen)
     h = coefs(r, t, hlen)
     n1, n2 = (3 << 20) + 12345, 777
-    x = cx(r, n1 + n2)
+    x = samples(r, t, n1 + n2)
+    esz = x.itemsize
     g = LQ.FirFilt(t, h)
     s = (0.7 - 0.2j) if t == "cccf" else 0.7
     g.set_scale(s)
     bx = LQ.DeviceBuffer.from_array(x)
     by = LQ.DeviceBuffer(x.nbytes)
     g.execute_block_dev(bx.p, n1, by.p)
-    g.execute_block_dev(bx.p + n1 * 8, n2, by.p + n1 * 8)
+    g.execute_block_dev(bx.p + n1 * esz, n2, by.p + n1 * esz)   # second call 4- or 8-byte aligned: VALU kernel
     g.synchronize()
-    y = by.to_array(np.complex64, len(x))
+    y = by.to_array(x.dtype, len(x))
     o = O.FirFilt(TYPES[t], h)
     o.set_scale(s)
     ref = o.execute_block(x)
     assert G.nrm_err(y, ref) < NRM
     ref64 = s * np.convolve(x.astype(np.complex128), h.astype(np.complex128))[: len(x)]
+    if t == "rrrf":
+        ref64 = ref64.real
     assert G.nrm_err(y, ref64) < 2e-6
 
 
