@@ -184,6 +184,9 @@ __global__ __launch_bounds__(NT) void k_resamp2(lqk_rs_plan pl, unsigned long lo
     constexpr int TIN = NT * RIN;
     constexpr int LP = (L + 2 + 1) & ~1;         // pair-table stride (>= L+1, even)
     constexpr int LPS = LP + 2;                  // LDS row stride: 16 bytes of pad spread the banks
+    // rows 16 apart would share bank groups (consecutive outputs step the bank
+    // by ~npfb/r): shift every 16-row block by 4 more 16-byte slots
+    auto rowoff = [](int b) { return b * LPS + 8 * (b >> 4); };
     constexpr int NW = LP / 2;                   // 16-byte reads per window / per tap row
     constexpr int TS = TIN + L + 2;              // tile samples per copy (+1 for the shifted copy)
     constexpr int CS = TS + 2;                   // copy stride (even: both copies 16-byte aligned)
@@ -200,7 +203,7 @@ __global__ __launch_bounds__(NT) void k_resamp2(lqk_rs_plan pl, unsigned long lo
     // so a 16-byte read gives (h_b[2q], h_b[2q+1], h_b+1[2q], h_b+1[2q+1])
     for (int t = tid; t < (npfb + 1) * LP; t += NT) {
         const int b = t / LP, p = t % LP;
-        float *row = reinterpret_cast<float *>(tpl + b * LPS);
+        float *row = reinterpret_cast<float *>(tpl + rowoff(b));
         const float2 v = taps2[t];
         row[4 * (p >> 1) + (p & 1)] = v.x;
         row[4 * (p >> 1) + 2 + (p & 1)] = v.y;
@@ -299,7 +302,7 @@ __global__ __launch_bounds__(NT) void k_resamp2(lqk_rs_plan pl, unsigned long lo
                 const int bb = (int)(d.y >> 12);
                 const int sw = iloc + 1;                  // tile index of x[i-L]
                 const S *wp = (sw & 1) ? cp1 + sw + 1 : cp0 + sw;
-                const float2 *tp = tpl + bb * LPS;
+                const float2 *tp = tpl + rowoff(bb);
                 S acc{};
 #pragma unroll
                 for (int q = 0; q < NW; q++) {
@@ -371,7 +374,7 @@ void launch_rs(const lqk_rs_plan &pl, unsigned long long g0, unsigned long long 
     constexpr int LP = (L + 2 + 1) & ~1;
     constexpr int TIN = NT * 4;
     const size_t lds2 =
-        (size_t)2 * (TIN + L + 4) * sizeof(S) + 1536 * 8 + (size_t)(npfb + 1) * (LP + 2) * sizeof(float2);
+        (size_t)2 * (TIN + L + 4) * sizeof(S) + 1536 * 8 + ((size_t)(npfb + 1) * (LP + 2) + 8 * (npfb / 16 + 1)) * sizeof(float2);
     if (taps2 != nullptr && lds2 <= 64 * 1024 && pl.P < (1ull << 31) && pl.pre < (1ull << 62)) {
         const long long ntiles = (n + TIN - 1) / TIN;
         const unsigned nb = (unsigned)(ntiles < 1024 ? ntiles : 1024);   // persistent: ~4 per CU
