@@ -24,13 +24,15 @@ namespace {
 constexpr int NT = 256;
 constexpr int NFFT = 4096;
 // k_fftfilt_r16 configuration (tools/mb/mb_fftfilt.hip, h=512, 2^26 samples):
-// with the packed transforms (lq_device.h) the kernel needs ~185 VGPRs (+32
-// for the filter spectrum held in registers), so 2 waves/SIMD without spills;
-// spectrum in registers, 2048 persistent workgroups: 0.283 ms (spectrum from
-// L2 per segment: 0.36 ms; the scalar-complex transforms: 0.30 ms)
+// with the packed transforms (lq_device.h) and buffer-descriptor loads /
+// stores (no per-sample branches or 64-bit addresses) the kernel needs 128
+// VGPRs including the filter spectrum held in registers, so four waves per
+// SIMD; 4096 persistent workgroups: 0.253 ms (float2 pointer loads with
+// branches and ~220 VGPRs: 0.283 ms; a second, history, load for every
+// segment instead of the first only: 0.367 ms)
 #ifndef FF_HREG
 #define FF_HREG true
-#define FF_WPE 2
+#define FF_WPE 4
 #endif
 
 // kind 0: real input/output (rrrf), otherwise complex
@@ -82,9 +84,8 @@ __device__ __forceinline__ float2 to_c2(float2 a) { return a; }
 
 // Register form (default): 256 threads, thread t holds segment samples
 // t + 256 n; forward 4096-point FFT (fft4096_r16), x H, inverse, all with the
-// data in registers and two LDS transposes per transform (35 KB LDS; the
-// register budget allows two workgroups per CU); loads and stores are
-// coalesced across t.
+// data in registers and two LDS transposes per transform (35 KB LDS, four
+// workgroups per CU); loads and stores are coalesced across t.
 template <bool REAL, bool HREG, int WPE>
 __global__ __launch_bounds__(NT, WPE) void k_fftfilt_r16(int hm1, const float2 *__restrict__ H,
                                                     const void *__restrict__ hist, const void *__restrict__ xin,
@@ -102,44 +103,60 @@ __global__ __launch_bounds__(NT, WPE) void k_fftfilt_r16(int hm1, const float2 *
         for (int k = 0; k < 16; k++) hv[k] = H[t + 256 * k];
     }
     using S = typename std::conditional<REAL, float, float2>::type;
+    constexpr int ES = (int)sizeof(S);
+    // range-checked buffer descriptors replace the per-sample branches (and
+    // their 64-bit addresses): x (n samples), the history (hm1 samples just
+    // before x) and y; an out-of-range load returns 0 and an out-of-range
+    // store is dropped.  Byte offsets are 32-bit: the host keeps each launch
+    // below 2^28 samples.
+    const __amdgpu_buffer_rsrc_t rx = __builtin_amdgcn_make_buffer_rsrc((void *)xin, (short)0, (int)(n * ES), 0x00020000);
+    const __amdgpu_buffer_rsrc_t rh = __builtin_amdgcn_make_buffer_rsrc((void *)hist, (short)0, hm1 * ES, 0x00020000);
+    const __amdgpu_buffer_rsrc_t ry = __builtin_amdgcn_make_buffer_rsrc(yout, (short)0, (int)(n * ES), 0x00020000);
     for (long long seg = blockIdx.x; seg < nseg; seg += gridDim.x) {
-    const long long s0 = seg * L;
-    // segment sample i = t + 256 q is stream sample s0 - hm1 + i; 32-bit
-    // indices relative to the segment start (the history only feeds seg 0)
-    const long long rem = n - (s0 - hm1);              // segment samples that exist
-    const int lim = rem < NFFT ? (int)rem : NFFT;
+    // segment sample i = t + 256 q is stream sample s0 - hm1 + i
+    const int sb = (int)(seg * L) - hm1;   // stream index of segment sample 0
     float2 v[16];
-    if (seg == 0) {
+    if (seg == 0) {   // the only segment that reaches into the history
 #pragma unroll
         for (int q = 0; q < 16; q++) {
-            const int i = t + 256 * q, s = i - hm1;
-            S a{};
-            if (s < 0) a = ((const S *)hist)[hm1 + s];
-            else if (i < lim) a = ((const S *)xin)[s];
-            v[q] = to_c2(a);
+            const int si = sb + t + 256 * q;
+            const unsigned ox = (unsigned)si * ES, oh = (unsigned)(si + hm1) * ES;
+            if constexpr (REAL) {
+                const float a = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rx, ox, 0, 0)) +
+                                __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rh, oh, 0, 0));
+                v[q] = make_float2(a, 0.f);
+            } else {
+                const float2 a = __builtin_bit_cast(float2, __builtin_amdgcn_raw_buffer_load_b64(rx, ox, 0, 0));
+                const float2 b = __builtin_bit_cast(float2, __builtin_amdgcn_raw_buffer_load_b64(rh, oh, 0, 0));
+                v[q] = make_float2(a.x + b.x, a.y + b.y);
+            }
         }
     } else {
-        const S *xs = (const S *)xin + (s0 - hm1);
 #pragma unroll
         for (int q = 0; q < 16; q++) {
-            const int i = t + 256 * q;
-            S a{};
-            if (i < lim) a = xs[i];
-            v[q] = to_c2(a);
+            const unsigned ox = (unsigned)(sb + t + 256 * q) * ES;
+            if constexpr (REAL)
+                v[q] = make_float2(__builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rx, ox, 0, 0)), 0.f);
+            else
+                v[q] = __builtin_bit_cast(float2, __builtin_amdgcn_raw_buffer_load_b64(rx, ox, 0, 0));
         }
     }
     fft4096_r16<+1>(v, lds, tw, t);
 #pragma unroll
     for (int k = 0; k < 16; k++) v[k] = unpk(pk_cmul(pk(v[k]), pk(HREG ? hv[k & (HREG ? 15 : 0)] : H[t + 256 * k])));
     fft4096_r16<-1>(v, lds, tw, t);
-    S *ys = (S *)yout + (s0 - hm1);                    // output o = s0 + i - hm1 for i >= hm1
 #pragma unroll
     for (int q = 0; q < 16; q++) {
         const int i = t + 256 * q;
-        if (i < hm1 || i >= lim) continue;
+        const unsigned oy = i < hm1 ? 0xFFFFFFF0u : (unsigned)(sb + i) * ES;   // first hm1 outputs: discarded
         const float2 r = v[q];
-        if constexpr (REAL) ys[i] = r.x * sre;
-        else ys[i] = make_float2(r.x * sre - r.y * sim, r.x * sim + r.y * sre);
+        if constexpr (REAL) {
+            __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, r.x * sre), ry, oy, 0, 0);
+        } else {
+            const float2 o = make_float2(r.x * sre - r.y * sim, r.x * sim + r.y * sre);
+            typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
+            __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2, o), ry, oy, 0, 0);
+        }
     }
     }
 }
@@ -158,16 +175,26 @@ extern "C" void lqk_fftfilt_run(int real_io, unsigned int hlen, const void *H, c
     hipStream_t st = (hipStream_t)stream;
     const int hm1 = (int)hlen - 1;
     const int L = NFFT - hm1;
-    const long long nseg = ((long long)n + L - 1) / L;
     const float2 *tw = (const float2 *)lqrt_twiddles();
-    const unsigned grid = (unsigned)(nseg < 2048 ? nseg : 2048);   // persistent, two resident per CU
-    if (real_io)
-        hipLaunchKernelGGL((k_fftfilt_r16<true, FF_HREG, FF_WPE>), dim3(grid), dim3(NT), 0, st, hm1, (const float2 *)H, hist,
-                           x, (long long)n, y, scale_re, scale_im, tw);
-    else
-        hipLaunchKernelGGL((k_fftfilt_r16<false, FF_HREG, FF_WPE>), dim3(grid), dim3(NT), 0, st, hm1, (const float2 *)H, hist,
-                           x, (long long)n, y, scale_re, scale_im, tw);
-    LQ_CHECK_LAUNCH();
+    const size_t es = real_io ? 4 : 8;
+    // launches of at most 2^27 samples (32-bit buffer offsets); later chunks
+    // take their history straight from the preceding input
+    const unsigned long long CHN = 1ull << 27;
+    for (unsigned long long c0 = 0; c0 < n; c0 += CHN) {
+        const unsigned long long nc = (n - c0) < CHN ? (n - c0) : CHN;
+        const char *xc = (const char *)x + c0 * es;
+        const void *hc = c0 == 0 ? hist : (const void *)(xc - (size_t)hm1 * es);
+        void *yc = (char *)y + c0 * es;
+        const long long nsegc = ((long long)nc + L - 1) / L;
+        const unsigned grid = (unsigned)(nsegc < 4096 ? nsegc : 4096);   // persistent, four resident per CU
+        if (real_io)
+            hipLaunchKernelGGL((k_fftfilt_r16<true, FF_HREG, FF_WPE>), dim3(grid), dim3(NT), 0, st, hm1,
+                               (const float2 *)H, hc, (const void *)xc, (long long)nc, yc, scale_re, scale_im, tw);
+        else
+            hipLaunchKernelGGL((k_fftfilt_r16<false, FF_HREG, FF_WPE>), dim3(grid), dim3(NT), 0, st, hm1,
+                               (const float2 *)H, hc, (const void *)xc, (long long)nc, yc, scale_re, scale_im, tw);
+        LQ_CHECK_LAUNCH();
+    }
 }
 
 extern "C" unsigned int lqk_fftfilt_nfft(void) { return NFFT; }

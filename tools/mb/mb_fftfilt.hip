@@ -63,19 +63,19 @@ int main()
         timeit("LDS Stockham (one seg / WG)", [&] {
             hipLaunchKernelGGL(k_fftfilt<false>, dim3((unsigned)nseg), dim3(NT), 0, 0, hm1, H, hist, x, n, y, sc, 0.f, g_tw);
         }, n);
-        for (unsigned grid : {512u, 768u, 1024u, 2048u, (unsigned)nseg}) {
+        for (unsigned grid : {1024u, 2048u, 4096u}) {
             char nm[64];
             snprintf(nm, sizeof nm, "r16 Hreg wpe2 grid %u", grid);
             timeit(nm, [&] {
                 hipLaunchKernelGGL((k_fftfilt_r16<false, true, 2>), dim3(grid), dim3(NT), 0, 0, hm1, H, hist, x, n, y, sc, 0.f, g_tw);
             }, n);
-            snprintf(nm, sizeof nm, "r16 Hglb wpe2 grid %u", grid);
+            snprintf(nm, sizeof nm, "r16 Hreg wpe4 grid %u", grid);
             timeit(nm, [&] {
-                hipLaunchKernelGGL((k_fftfilt_r16<false, false, 2>), dim3(grid), dim3(NT), 0, 0, hm1, H, hist, x, n, y, sc, 0.f, g_tw);
+                hipLaunchKernelGGL((k_fftfilt_r16<false, true, 4>), dim3(grid), dim3(NT), 0, 0, hm1, H, hist, x, n, y, sc, 0.f, g_tw);
             }, n);
-            snprintf(nm, sizeof nm, "r16 Hglb wpe3 grid %u", grid);
+            snprintf(nm, sizeof nm, "r16 Hglb wpe4 grid %u", grid);
             timeit(nm, [&] {
-                hipLaunchKernelGGL((k_fftfilt_r16<false, false, 3>), dim3(grid), dim3(NT), 0, 0, hm1, H, hist, x, n, y, sc, 0.f, g_tw);
+                hipLaunchKernelGGL((k_fftfilt_r16<false, false, 4>), dim3(grid), dim3(NT), 0, 0, hm1, H, hist, x, n, y, sc, 0.f, g_tw);
             }, n);
         }
     }
