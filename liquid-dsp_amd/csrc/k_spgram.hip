@@ -117,7 +117,7 @@ __global__ __launch_bounds__(NT) void k_spg_fold(const float *__restrict__ part,
 // ends at e0 + t*hop (the last one at elast).  Writes part[chunk][k] for
 // k_spg_fold, exactly as k_spg_part does.
 template <typename S>
-__global__ __launch_bounds__(NT) void k_spg_fused1024(const S *__restrict__ hist, int W, const S *__restrict__ x,
+__global__ __launch_bounds__(NT, 3) void k_spg_fused1024(const S *__restrict__ hist, int W, const S *__restrict__ x,
                                                       long long e0, long long hop, long long T, long long elast,
                                                       const float *__restrict__ w, int accum, float alpha,
                                                       const float2 *__restrict__ tw4096, float *__restrict__ part)
@@ -143,21 +143,42 @@ __global__ __launch_bounds__(NT) void k_spg_fused1024(const S *__restrict__ hist
     }
     // window samples of transform t (unweighted); the next transform's are
     // loaded while this one is transformed
+    // x through a range-checked buffer descriptor (32-bit offsets, no
+    // per-sample branches: the register budget of the prefetch); the history
+    // only feeds the first transforms of a call
+    constexpr int ES = (int)sizeof(S);
+    const __amdgpu_buffer_rsrc_t rx =
+        __builtin_amdgcn_make_buffer_rsrc((void *)x, (short)0, (int)((elast + 1) * ES), 0x00020000);
+    const __amdgpu_buffer_rsrc_t rh = __builtin_amdgcn_make_buffer_rsrc((void *)hist, (short)0, W * ES, 0x00020000);
     auto gather = [&](long long t, float2 (&u)[16]) {
         const long long j0 = ((t == T - 1) ? elast : e0 + t * hop) + 1;   // ext index of window sample 0
         if (j0 >= W) {   // all from x (every transform but the first few of a call)
-            const S *xp = x + (j0 - W);
+            const int b = (int)(j0 - W);
 #pragma unroll
             for (int r = 0; r < 16; r++) {
                 const int i = lane + 64 * r;
-                u[r] = i < W ? as_c(xp[i]) : make_float2(0.f, 0.f);
+                const unsigned o = i < W ? (unsigned)(b + i) * ES : 0xFFFFFFF0u;
+                if constexpr (ES == 8)
+                    u[r] = __builtin_bit_cast(float2, __builtin_amdgcn_raw_buffer_load_b64(rx, o, 0, 0));
+                else
+                    u[r] = make_float2(__builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rx, o, 0, 0)), 0.f);
             }
-        } else {
+        } else {   // sample j < W from the history, else x[j - W]: one of the two loads is in range
+            const int b = (int)j0;
 #pragma unroll
             for (int r = 0; r < 16; r++) {
-                const int i = lane + 64 * r;
-                const long long j = j0 + i;
-                u[r] = i < W ? as_c(j < W ? hist[j] : x[j - W]) : make_float2(0.f, 0.f);
+                const int i = lane + 64 * r, j = b + i;
+                const unsigned oh = i < W ? (unsigned)j * ES : 0xFFFFFFF0u;
+                const unsigned ox = i < W ? (unsigned)(j - W) * ES : 0xFFFFFFF0u;
+                if constexpr (ES == 8) {
+                    const float2 a = __builtin_bit_cast(float2, __builtin_amdgcn_raw_buffer_load_b64(rh, oh, 0, 0));
+                    const float2 c = __builtin_bit_cast(float2, __builtin_amdgcn_raw_buffer_load_b64(rx, ox, 0, 0));
+                    u[r] = make_float2(a.x + c.x, a.y + c.y);
+                } else {
+                    u[r] = make_float2(__builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rh, oh, 0, 0)) +
+                                           __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rx, ox, 0, 0)),
+                                       0.f);
+                }
             }
         }
     };

@@ -197,7 +197,7 @@ static void lq_spg_accumulate_dev(lq_spg *q, const void *dx, unsigned long long 
     if (H > 0) {   /* transform after the input that brings sample_counter to W/2 */
         const long long first = (long long)(H - q->sample_counter) - 1;
         if (first < (long long)n) T = (unsigned long long)(((long long)n - 1 - first) / H + 1);
-        if (q->nfft == 1024) {   /* fused path: ends are first + t H, no table */
+        if (q->nfft == 1024 && n < (1ull << 27)) {   /* fused path: ends are first + t H, no table */
             if (T > 0) {
                 float a = q->num_transforms == 0 ? 1.0f : alpha;
                 void *w = lq_devbuf_get(&q->work, lqk_spgram_work_bytes(T, q->nfft));
@@ -253,7 +253,7 @@ static void lq_spg_estimate_dev(lq_spg *q, const void *dx, unsigned long long n,
     unsigned long long T = n / delay + ((n % delay) ? 1 : 0);
     float *acc = (float *)lq_devbuf_get(&q->acc, q->nfft * sizeof(float));
     lqrt_memset(acc, q->nfft * sizeof(float), q->ctx.stream);
-    if (q->nfft == 1024) {   /* fused path: ends are delay-1 + t delay, the last one n-1 */
+    if (q->nfft == 1024 && n < (1ull << 27)) {   /* fused path: ends are delay-1 + t delay, the last one n-1 */
         void *w = lq_devbuf_get(&q->work, lqk_spgram_work_bytes(T, q->nfft));
         lqk_spgram_fused1024(q->real_in, q->d_hist[q->cur], q->W, dx, (long long)delay - 1, (long long)delay, T,
                              (long long)n - 1, q->d_w, 0, 0.0f, acc, w, q->ctx.stream);
