@@ -974,3 +974,38 @@ def test_spgram_device_estimate_long():
     LQ.lib().spgramcf_estimate_psd_dev(g.q, dx.p, n, dp.p)
     LQ.lib().spgramcf_synchronize(g.q)
     assert _db_close(dp.to_array(np.float32, nfft), o.estimate_psd(x))
+
+
+# ------------------------------------------------ launch-chunk boundaries
+# The fast kernels split very long calls into launches of 2^17 / 2^18 blocks
+# (firpfbch / firpfbch2) or 2^27 samples (fftfilt) so that 32-bit buffer
+# offsets suffice; a call that crosses such a boundary must equal the same
+# stream fed in two calls split elsewhere.  Channelizer blocks do not depend
+# on where calls or launches start: bit-exact.  fftfilt segments restart at
+# call boundaries: equal to float32 rounding.
+@pytest.mark.parametrize("which", ["firpfbch2", "firpfbch"])
+def test_channelizer_launch_chunk_boundary(which):
+    r = rng(91)
+    if which == "firpfbch2":
+        M, per, nb, cut = 1024, 512, (1 << 18) + 77, 100003
+        make = lambda: LQ.FirPfbch2(LQ.LIQUID_ANALYZER, M, 4, 60.0)   # noqa: E731
+    else:
+        M, per, nb, cut = 1024, 1024, (1 << 17) + 33, 70001
+        make = lambda: LQ.FirPfbch(LQ.LIQUID_ANALYZER, M, m=4, As=60.0)   # noqa: E731
+    x = cx(r, nb * per)
+    y1 = make().execute_block(x)
+    q = make()
+    y2 = np.concatenate([q.execute_block(x[: cut * per]), q.execute_block(x[cut * per:])])
+    assert y1.shape == y2.shape
+    assert np.array_equal(y1, y2)
+
+
+def test_fftfilt_launch_chunk_boundary():
+    r = rng(92)
+    h = r.uniform(-0.5, 0.5, 512).astype(np.float32)
+    n, cut = (1 << 27) + 4097, (1 << 26) + 3
+    x = cx(r, n)
+    y1 = LQ.FftFilt(h, 2048).execute_block(x)
+    q = LQ.FftFilt(h, 2048)
+    y2 = np.concatenate([q.execute_block(x[:cut]), q.execute_block(x[cut:])])
+    assert G.nrm_err(y1, y2) < 1e-6
