@@ -14,20 +14,35 @@ The second headline workload, firfilt_crcf h=64 (configs[0] shape, 2^28
 samples per GPU so the 4 GB working set is far above the 256 MB Infinity
 Cache), is timed the same way and reported under "firfilt_crcf_h64".
 
-Multi-GPU: one process per GPU (torch.distributed.run); streams are
-independent, so per-GPU work is fixed (weak scaling) and the only
-collectives are RCCL all-reduces of the counters (max time, sample counts).
+Multi-GPU: one process per GPU.  `--gpus N` without a launcher starts N
+child ranks itself (fresh interpreters, started before this process makes
+any GPU call); under torch.distributed.run the env's RANK / WORLD_SIZE are
+used.  Each rank binds its own GPU; the only collectives are RCCL
+all-reduces of counters (max time, sample counts, checksums).  `value`:
+independent 128M-sample streams, one per GPU (weak scaling).  Leg
+"firpfbch2_sharded_stream": ONE 128M-sample stream split across the ranks
+by liquid-dsp_amd/lqshard.py (even-block shard starts, a 16-block warm-up
+halo recomputed per shard, no data exchange; strong scaling), with an
+order-independent checksum of the owned outputs that must not change with N.
 
 roofline: algorithmic bytes of the dominant kernel per launch (24 B per
 input sample for the analyzer: 8 B read + 16 B written; 16 B per sample for
 firfilt) / its average launch duration measured with HIP events on the
 stream the kernel runs on; peak 8000 GB/s (MI355X HBM3E spec).
 
-cpu_baseline: the CPU oracle (oracle/oracle.c, a restatement of the
-reference firpfbch2.c analyzer; "port") on one host core, rank 0 at N=1
-only, over a bounded sample of the same workload (>= ~10 s of CPU work);
-the secondary legs carry their own oracle rates (firfilt, resamp, fftfilt,
-dotprod n=64; ~2.5 s each).
+cpu_baseline: the CPU oracle (oracle/oracle.c, a plain-C port of the
+reference firpfbch2.c analyzer, "kind": "port"; the reference itself cannot
+be built in this image) timed on the host cores, rank 0 at
+N=1 only: `value` = the aggregate of C processes each running its own
+independent stream (C = the box's CPU share, stated in `cores`), beside the
+one-core figure; bounded samples (~10 s + ~5 s).  The secondary legs carry
+their own one-core oracle rates (firfilt, resamp, fftfilt, dotprod n=64).
+
+per_call: the reference's own per-call benchmark bodies
+(src/*/bench/*_benchmark.c: push/execute one sample, one firpfbch2 block,
+one dot product per call) compiled unchanged against this library by
+tools/build_ref_benches.sh and timed in wall clock -- the latency of the
+unbatched liquid.h API, one GPU round trip per call.
 """
 import argparse
 import json
@@ -61,18 +76,61 @@ def parse():
     p.add_argument("--dp-vectors", type=int, default=1 << 20, help="dotprod_cccf vectors per GPU per n")
     p.add_argument("--ff-samples", type=int, default=1 << 26, help="fftfilt_crcf samples per GPU")
     p.add_argument("--no-extra", action="store_true", help="skip the dotprod / fftfilt legs")
+    p.add_argument("--shard-samples", type=int, default=1 << 27,
+                   help="length of the ONE firpfbch2 stream split across ranks (sharded leg)")
+    p.add_argument("--no-shard", action="store_true", help="skip the single-stream sharded leg")
+    p.add_argument("--no-percall", action="store_true", help="skip the per-call latency leg")
+    p.add_argument("--cpu-procs", type=int, default=0,
+                   help="processes for the aggregate CPU baseline (0: the host CPU share, at most 16)")
     p.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic.json"),
                    help="PMC-derived HBM bytes per launch (from a separate rocprofv3 --pmc run)")
     return p.parse_args()
 
 
+def launch_ranks(n):
+    """Start n ranks of this script as child processes (one per GPU) and
+    return the worst exit code.  Runs before this process touches the GPU
+    (no HIP call, no torch.cuda initialisation), so nothing is re-executed
+    from a process holding a device context."""
+    import socket
+    import subprocess
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:], env=env))
+    rc = 0
+    for p in procs:
+        c = p.wait()
+        if c != 0 and rc == 0:
+            rc = c
+            for q in procs:
+                if q.poll() is None:
+                    q.terminate()
+    return rc
+
+
+DEV_COLLECTIVES = True   # counters reduced over RCCL (device tensors) unless ranks share a GPU
+
+
 def setup_dist():
+    global DEV_COLLECTIVES
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    torch.cuda.set_device(local)
+    ndev = torch.cuda.device_count()
+    if ndev == 0:
+        sys.exit("bench.py: no GPU visible (the library has no CPU path)")
+    torch.cuda.set_device(local % ndev)
     if world > 1:
-        dist.init_process_group(backend="nccl", init_method="env://")
+        # RCCL needs one GPU per rank; ranks sharing a GPU (a 1-GPU rehearsal
+        # of --gpus N) reduce their counters over gloo instead
+        DEV_COLLECTIVES = world <= ndev
+        dist.init_process_group(backend="nccl" if DEV_COLLECTIVES else "gloo", init_method="env://")
     return world, rank, local
 
 
@@ -82,18 +140,23 @@ def barrier(world):
     torch.cuda.synchronize()
 
 
-def allreduce_max(v, world):
-    t = torch.tensor([v], dtype=torch.float64, device="cuda")
+def _reduce(v, world, op, dtype=torch.float64):
+    t = torch.tensor([v], dtype=dtype, device="cuda" if DEV_COLLECTIVES else "cpu")
     if world > 1:
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-    return float(t.item())
+        dist.all_reduce(t, op=op)
+    return t.item()
+
+
+def allreduce_max(v, world):
+    return float(_reduce(v, world, dist.ReduceOp.MAX))
 
 
 def allreduce_sum(v, world):
-    t = torch.tensor([v], dtype=torch.float64, device="cuda")
-    if world > 1:
-        dist.all_reduce(t, op=dist.ReduceOp.SUM)
-    return float(t.item())
+    return float(_reduce(v, world, dist.ReduceOp.SUM))
+
+
+def allreduce_sum_i64(v, world):
+    return int(_reduce(int(v), world, dist.ReduceOp.SUM, torch.int64))
 
 
 def synth_complex(n, seed):
@@ -101,6 +164,25 @@ def synth_complex(n, seed):
     g.manual_seed(seed)
     x = torch.rand(2 * n, generator=g, device="cuda", dtype=torch.float32) - 0.5
     return x
+
+
+def synth_indexed(a, b, chunk=1 << 24):
+    """Complex samples a..b-1 of ONE synthetic stream, as interleaved float32:
+    a counter-based hash of the global float index, so any shard of the stream
+    is generated identically on any rank, U[-0.5, 0.5) in steps of 2^-24."""
+    out = torch.empty(2 * (b - a), dtype=torch.float32, device="cuda")
+    for c0 in range(2 * a, 2 * b, chunk):
+        c1 = min(2 * b, c0 + chunk)
+        h = torch.arange(c0, c1, dtype=torch.int64, device="cuda")
+        h = (h * 0x9E3779B1) & 0xFFFFFFFF
+        h ^= h >> 15
+        h = (h * 0x85EBCA77) & 0xFFFFFFFF
+        h ^= h >> 13
+        h = (h * 0xC2B2AE3D) & 0xFFFFFFFF
+        h ^= h >> 16
+        out[c0 - 2 * a:c1 - 2 * a] = (h >> 8).to(torch.float32) * (1.0 / (1 << 24)) - 0.5
+        del h
+    return out
 
 
 def time_steps(run_step, steps, warmup, world, stream):
@@ -136,6 +218,42 @@ def bench_firpfbch2(args, world, rank, stream):
     res = {"n": n, "nblocks": nblocks, "wall": wall, "gpu_ms": gpu_ms}
     q.destroy()
     del x, y
+    torch.cuda.empty_cache()
+    return res
+
+
+def bench_firpfbch2_sharded(args, world, rank, stream):
+    """ONE firpfbch2 analyzer stream of args.shard_samples samples split across
+    the ranks: rank r owns blocks [start, start+count) of
+    lqshard.firpfbch2_plan and runs its own object over [start-warm, start+count)
+    -- a 16-block warm-up recomputed from its own slice of the stream, block
+    parity preserved, no data exchange.  Checksum: sum of the int32 bit
+    patterns of the owned outputs of a fresh object (exact, order-independent),
+    identical for every N iff the sharded outputs equal the single-stream ones."""
+    import lqshard
+    M, m = 1024, 4
+    nb_total = args.shard_samples // (M // 2)
+    sh = lqshard.firpfbch2_plan(nb_total, world, M, m)[rank]
+    nb = sh.warm + sh.count
+    x = synth_indexed(sh.first * (M // 2), (sh.start + sh.count) * (M // 2))
+    y = torch.empty(2 * max(nb, 1) * M, dtype=torch.float32, device="cuda")
+    q = LQ.FirPfbch2(LQ.LIQUID_ANALYZER, M, m, 60.0)
+    q.set_stream(stream.cuda_stream)
+
+    def step():
+        if nb:
+            q.execute_block_dev(x.data_ptr(), nb, y.data_ptr())
+
+    wall, gpu_ms = time_steps(step, args.steps, args.warmup, world, stream)
+    q.reset()                      # checksum pass from the stream's initial state
+    step()
+    stream.synchronize()
+    own = y[2 * sh.warm * M:2 * nb * M]
+    csum = int(own.view(torch.int32).sum(dtype=torch.int64).item()) if sh.count else 0
+    res = {"wall": wall, "gpu_ms": gpu_ms, "owned": sh.count * (M // 2), "halo_blocks": sh.warm,
+           "total": nb_total * (M // 2), "checksum": csum}
+    q.destroy()
+    del x, y, own
     torch.cuda.empty_cache()
     return res
 
@@ -249,8 +367,45 @@ def copy_bandwidth():
     return gbps
 
 
-def cpu_baseline(seconds):
-    """Oracle firpfbch2 analyzer (M=1024, m=4) on one core, bounded sample."""
+def _cpu_pfb2_worker(seconds, seed, start_evt, out_q):
+    """One independent firpfbch2 stream on one core (oracle port), for the
+    aggregate CPU baseline."""
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    import numpy as np
+
+    import oracle_lib as O
+    q = O.FirPfbch2(O.ANALYZER, 1024, 4, 60.0)
+    rng = np.random.default_rng(seed)
+    chunk = 1 << 18
+    x = (rng.uniform(-0.5, 0.5, chunk) + 1j * rng.uniform(-0.5, 0.5, chunk)).astype(np.complex64)
+    start_evt.wait()
+    done, t0 = 0, time.perf_counter()
+    while True:
+        q.execute_block(x)
+        done += chunk
+        el = time.perf_counter() - t0
+        if el >= seconds:
+            break
+    out_q.put((done, el))
+
+
+def cpu_share():
+    try:
+        n = len(os.sched_getaffinity(0))
+    except AttributeError:
+        n = os.cpu_count() or 1
+    for var in ("OMP_NUM_THREADS", "MAX_JOBS"):
+        v = os.environ.get(var)
+        if v and v.isdigit():
+            n = min(n, int(v))
+    return max(1, min(n, 16))
+
+
+def cpu_baseline(seconds, procs):
+    """Oracle firpfbch2 analyzer (M=1024, m=4): one core, then `procs`
+    processes on independent streams (the reference is single-threaded; its
+    multi-core figure is N streams in N processes)."""
+    import multiprocessing as mp
     sys.path.insert(0, os.path.join(ROOT, "tests"))
     import numpy as np
 
@@ -267,9 +422,53 @@ def cpu_baseline(seconds):
         el = time.perf_counter() - t0
         if el >= seconds:
             break
-    return {"value": done / el / 1e6, "unit": "Msamples/s", "cores": 1, "kind": "port",
-            "sample": "oracle firpfbch2_crcf analyzer M=1024 m=4 As=60 on %d x 2^20 complex samples "
-                      "(%.1f s, 1 thread)" % (done // chunk, el)}
+    single = {"value": done / el / 1e6, "unit": "Msamples/s", "cores": 1,
+              "sample": "%d x 2^20 complex samples, %.1f s, 1 thread" % (done // chunk, el)}
+    ctx = mp.get_context("spawn")
+    evt, out_q = ctx.Event(), ctx.Queue()
+    agg_s = seconds / 2
+    ps = [ctx.Process(target=_cpu_pfb2_worker, args=(agg_s, 100 + i, evt, out_q)) for i in range(procs)]
+    for p in ps:
+        p.start()
+    time.sleep(1.0)               # let every worker import and allocate before the start signal
+    evt.set()
+    res = [out_q.get(timeout=120 + 4 * agg_s) for _ in ps]
+    for p in ps:
+        p.join(timeout=30)
+    agg = sum(d for d, _ in res) / max(e for _, e in res) / 1e6
+    return {"value": agg, "unit": "Msamples/s", "cores": procs, "kind": "port",
+            "what": "oracle/oracle.c: plain-C port of the reference firpfbch2_crcf analyzer "
+                    "(src/multichannel/src/firpfbch2.c:244-282), M=1024 m=4 As=60; the reference itself "
+                    "is not buildable in this image (DESIGN.md (c))",
+            "sample": "%d processes x one independent stream each, %.1f s, 2^18-sample blocks" % (procs, agg_s),
+            "single_core": single,
+            "reference_measured_in_survey": {"1_core": 22.9, "8_cores_8_streams": 135.0, "unit": "Msamples/s",
+                                             "source": "BASELINE.md section 2"}}
+
+
+def percall_baseline():
+    """The reference's own per-call benchmark bodies linked against this
+    library (tools/build_ref_benches.sh -> build/ref_bench/percall), wall
+    clock; None when the harness was not built."""
+    import subprocess
+    exe = os.path.join(ROOT, "build", "ref_bench", "percall")
+    if not os.path.exists(exe):
+        return None
+    names = ["firfilt_crcf_64", "dotprod_crcf_64", "dotprod_cccf_64", "firpfbch2_crcf_a1024",
+             "firpfbch_crcf_a1024", "resamp_crcf_m8", "firdecim_crcf_m8_h32", "firinterp_crcf_m8_h32",
+             "fftfilt_crcf_64", "windowcf_push_n64"]
+    try:
+        out = subprocess.run([exe, "--runtime", "0.25"] + names, capture_output=True, text=True, timeout=240)
+    except subprocess.TimeoutExpired:
+        return {"error": "timeout"}
+    res = {}
+    for line in out.stdout.splitlines():
+        if line.startswith("{"):
+            d = json.loads(line)
+            res[d.pop("name")] = d
+    if out.returncode != 0:
+        res["error"] = "exit %d: %s" % (out.returncode, out.stderr[-300:])
+    return res
 
 
 def cpu_baselines_secondary(seconds):
@@ -320,6 +519,8 @@ def cpu_baselines_secondary(seconds):
 
 def main():
     args = parse()
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        sys.exit(launch_ranks(args.gpus))
     world, rank, local = setup_dist()
     # a dedicated (non-null) stream: the library's objects launch on it and
     # the HIP events below are recorded on it
@@ -329,6 +530,14 @@ def main():
     t_pfb = allreduce_max(pfb["wall"], world)
     g_pfb = allreduce_max(pfb["gpu_ms"], world)
     tot_pfb = allreduce_sum(pfb["n"] * args.steps, world)
+
+    shd = None
+    if not args.no_shard:
+        shd = bench_firpfbch2_sharded(args, world, rank, stream)
+        t_shd = allreduce_max(shd["wall"], world)
+        g_shd = allreduce_max(shd["gpu_ms"], world)
+        owned_shd = allreduce_sum(shd["owned"], world)
+        csum_shd = allreduce_sum_i64(shd["checksum"], world)
 
     fir = None
     if not args.no_firfilt:
@@ -352,9 +561,12 @@ def main():
         ff_t = (allreduce_max(ff["wall"], world), allreduce_max(ff["gpu_ms"], world))
 
     copy_gbps = copy_bandwidth() if rank == 0 else None
+    percall = None
+    if rank == 0 and world == 1 and not args.no_percall:
+        percall = percall_baseline()
     cpu = cpu2 = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        cpu = cpu_baseline(args.cpu_seconds)
+        cpu = cpu_baseline(args.cpu_seconds, args.cpu_procs or cpu_share())
         cpu2 = cpu_baselines_secondary(args.cpu_seconds / 4)
 
     if rank == 0:
@@ -392,6 +604,18 @@ def main():
                          "launch_ms": launch_ms, "measured_copy_GBps": copy_gbps},
             "cpu_baseline": cpu,
         }
+        if shd is not None:
+            out["firpfbch2_sharded_stream"] = {
+                "value": owned_shd * args.steps / t_shd / 1e6, "unit": "Msamples/s", "scaling": "strong",
+                "workload": "ONE firpfbch2_crcf analyzer stream (M=1024 m=4) of %d samples split over %d rank(s)"
+                            % (shd["total"], world),
+                "plan": "liquid-dsp_amd/lqshard.py firpfbch2_plan: even-block shard starts, %d-block warm-up "
+                        "halo recomputed per shard, no data-path collective" % shd["halo_blocks"],
+                "ms_per_step": t_shd / args.steps * 1e3, "launch_ms": g_shd / args.steps,
+                "owned_samples": int(owned_shd),
+                "output_checksum": csum_shd,
+                "checksum_def": "sum of the int32 bit patterns of every owned output (fresh object, one pass); "
+                                "equal for every N iff the shards reproduce the single-stream outputs"}
         if fir is not None:
             fl_ms = g_fir / args.steps
             fach = 16.0 * fir["n"] / (fl_ms * 1e-3) / 1e9
@@ -434,6 +658,10 @@ def main():
                                         "launch_ms": ms, "achieved_GBps": 16.0 * ff["n"] / (ms * 1e-3) / 1e9,
                                         "frac": 16.0 * ff["n"] / (ms * 1e-3) / 1e9 / HBM_PEAK_GBPS,
                                         "bytes_per_unit": "16 B/sample"}
+        if percall is not None:
+            out["per_call"] = {"what": "the reference's per-call benchmark loops (src/*/bench/*_benchmark.c) "
+                                       "linked against this library; wall clock; one GPU round trip per call",
+                               "runs": percall}
         if cpu2:
             for leg, c in cpu2.items():
                 key = "dotprod_cccf" if leg == "dotprod_cccf_n64" else leg

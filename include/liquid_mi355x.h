@@ -137,6 +137,28 @@ void crandnf(liquid_float_complex *_y);
 void cawgn(liquid_float_complex *_x, float _nstd);
 
 /* ------------------------------------------------------------------------ */
+/* window buffers (liquid.h:296-349): the last _n samples, contiguous,       */
+/* oldest first.  A host container by contract (read() hands the caller a    */
+/* host pointer); the streaming objects below keep their own history on the */
+/* device and do not use it.                                                 */
+/* ------------------------------------------------------------------------ */
+#define LQMI_WINDOW_API(WINDOW, T)                                                              \
+    typedef struct WINDOW##_s *WINDOW;                                                          \
+    WINDOW WINDOW##_create(unsigned int _n);                                                    \
+    WINDOW WINDOW##_recreate(WINDOW _q, unsigned int _n);                                       \
+    void WINDOW##_destroy(WINDOW _q);                                                           \
+    void WINDOW##_print(WINDOW _q);                                                             \
+    void WINDOW##_debug_print(WINDOW _q);                                                       \
+    void WINDOW##_clear(WINDOW _q);                                                             \
+    void WINDOW##_read(WINDOW _q, T **_v);                                                      \
+    void WINDOW##_index(WINDOW _q, unsigned int _i, T *_v);                                     \
+    void WINDOW##_push(WINDOW _q, T _v);                                                        \
+    void WINDOW##_write(WINDOW _q, T *_v, unsigned int _n);
+
+LQMI_WINDOW_API(windowf, float)
+LQMI_WINDOW_API(windowcf, liquid_float_complex)
+
+/* ------------------------------------------------------------------------ */
 /* dotprod (liquid.h:503-560): rrrf, crcf, cccf                              */
 /* ------------------------------------------------------------------------ */
 #define LQMI_DOTPROD_API(DOTPROD, TO, TC, TI)                                                   \

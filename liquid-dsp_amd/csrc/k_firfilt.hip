@@ -134,7 +134,7 @@ __global__ __launch_bounds__(NT) void k_firfilt(const typename kt<KIND>::T *__re
                                                 typename kt<KIND>::T *y,
                                                 const typename kt<KIND>::TC *__restrict__ hpad,
                                                 int nchunk, float sre, float sim,
-                                                const typename kt<KIND>::T *__restrict__ halo)
+                                                const typename kt<KIND>::T *__restrict__ halo, int hexact)
 {
     typedef typename kt<KIND>::T T;
     typedef typename kt<KIND>::TC TC;
@@ -145,6 +145,11 @@ __global__ __launch_bounds__(NT) void k_firfilt(const typename kt<KIND>::T *__re
     const long long t0 = (long long)blockIdx.x * TILE;
     const int S = TILE + HP;
 
+    // hexact = hlen when the taps are zero padded (hlen < HP): a padded zero
+    // tap times an Inf / NaN sample would put NaN into outputs the reference
+    // (firfilt.c:322-338, hlen taps) keeps finite, so a tile holding a
+    // non-finite sample runs the exact loop over the true taps instead
+    bool bad = false;
     for (int e = threadIdx.x; e < S / VE; e += NT) {
         const int u = e * VE;
         const long long s = t0 - HP + u;
@@ -159,15 +164,25 @@ __global__ __launch_bounds__(NT) void k_firfilt(const typename kt<KIND>::T *__re
 #pragma unroll
             for (int i = 0; i < VE; i++) o[i] = (s + i < n) ? x[s + i] : zero<T>();
         }
-        *reinterpret_cast<float4 *>(smem + lds_off<T>(u)) = pack16(o);
+        const float4 pv = pack16(o);
+        if (hexact) bad |= !(isfinite(pv.x) && isfinite(pv.y) && isfinite(pv.z) && isfinite(pv.w));
+        *reinterpret_cast<float4 *>(smem + lds_off<T>(u)) = pv;
     }
-    __syncthreads();
+    const bool exact = hexact ? __syncthreads_or(bad) : (__syncthreads(), false);
 
     T acc[R];
 #pragma unroll
     for (int r = 0; r < R; r++) acc[r] = zero<T>();
 
-    for (int c = 0; c < nchunk; c++) {
+    if (exact) {
+        for (int r = 0; r < R; r++) {
+            const int u = HP + R * threadIdx.x + r;
+            T a = zero<T>();
+            for (int k = 0; k < hexact; k++) mac(a, hpad[k], *reinterpret_cast<const T *>(smem + lds_off<T>(u - k)));
+            acc[r] = a;
+        }
+    }
+    for (int c = 0; c < (exact ? 0 : nchunk); c++) {
         const TC *hc = hpad + c * HC;
         // window sample a' (0 <= a' < HC+R) of this chunk is tile sample
         // u = R*tid + HP - c*HC - HC + a'  (a row start when a' % 16 == 0)
@@ -534,7 +549,7 @@ void launch_firfilt(const lqk_fir_desc *d, const void *hist, const void *x, long
     }
     hipLaunchKernelGGL((k_firfilt<KIND, HC>), dim3((unsigned)ntiles), dim3(NT), lds, st, (const T *)hist,
                        (const T *)x, n, (T *)y, (const TC *)d->hpad, (int)d->nchunk, d->scale_re,
-                       d->scale_im, (const T *)halo);
+                       d->scale_im, (const T *)halo, (int)d->hlen < HP ? (int)d->hlen : 0);
     LQ_CHECK_LAUNCH();
 }
 

@@ -30,6 +30,17 @@
 // runs 36 MFMAs for its 512 outputs, stages the accumulator through LDS and
 // writes 16-byte stores.  The taps' A fragments (3 terms x 6 K steps, 72
 // VGPRs) are built once per workgroup from the padded fp32 taps.
+//
+// Range guard.  The split is float32-accurate only for finite values whose
+// bf16 terms stay normal, and the band's zero entries multiply every sample
+// of the 96-sample span (0 * Inf = NaN would reach outputs the reference
+// keeps finite).  So each lane classifies the samples it stages (finite,
+// zero or |x| in [2^-50, 2^50]); a chunk whose span (its 2048 samples plus
+// the 64-sample halo) holds any other value is computed by the exact float32
+// dot product over the true taps instead (k < hlen, as firfilt.c:322-338),
+// from global memory -- the outputs the reference would produce, Inf / NaN
+// propagation included.  Filters whose taps fail the same test never come
+// here (lqk_fir_desc.mx_ok, checked at create time).
 #include "lq_device.h"
 #include "lq_kernels.h"
 
@@ -56,6 +67,19 @@ template <bool CC>
 constexpr int lds_bytes_mx() { return 6 * PLB + 2 * 6 * HPB + (CC ? 2 : 1) * 4 * 16 * SSTR * 4; }
 
 __device__ __forceinline__ int poff(int pos) { return 2 * pos + 16 * (pos >> 5); }
+
+// 1 if v is outside the split's safe class: NaN, +-Inf, or a nonzero |v|
+// outside [2^-50, 2^50] (integer compare on the magnitude bits; NaN and Inf
+// patterns sit above 2^50's)
+__device__ __forceinline__ unsigned unsafe_bits(float v)
+{
+    const unsigned a = __float_as_uint(v) & 0x7fffffffu;
+    return (unsigned)(a - 0x26800000u) > (0x58800000u - 0x26800000u) ? (a != 0u) : 0u;
+}
+__device__ __forceinline__ unsigned unsafe4(v4f v)
+{
+    return unsafe_bits(v.x) | unsafe_bits(v.y) | unsafe_bits(v.z) | unsafe_bits(v.w);
+}
 
 // three-term bf16 split of a pair of floats
 __device__ __forceinline__ void split3(v2f a, bf16x2 &t1, bf16x2 &t2, bf16x2 &t3)
@@ -112,6 +136,32 @@ __device__ __forceinline__ void load8(const v2f *__restrict__ win, const v2f *__
     }
 }
 
+// Exact float32 outputs t0 .. t0+cnt-1 (the range guard's path): the
+// reference's dot product over the true taps, firfilt.c:322-338, then the
+// scale.  Out of line, so the matrix path's register allocation is unchanged.
+template <bool CC>
+__device__ __attribute__((noinline)) void exact_chunk_c(const v2f *__restrict__ win, const v2f *__restrict__ x,
+                                                         long long n, v2f *__restrict__ y,
+                                                         const float *__restrict__ hpad, int hlen, long long t0,
+                                                         int cnt, float sre, float sim)
+{
+    for (int e = 0; e < cnt; e++) {
+        const long long t = t0 + e;
+        if (t >= n) break;
+        v2f acc = {0.f, 0.f};
+        for (int k = 0; k < hlen; k++) {
+            const v2f v = sample_at(win, x, n, t - k);
+            if constexpr (CC) {
+                const float hr = hpad[2 * k], hi = hpad[2 * k + 1];
+                acc = v2f{fmaf(-hi, v.y, fmaf(hr, v.x, acc.x)), fmaf(hi, v.x, fmaf(hr, v.y, acc.y))};
+            } else {
+                acc = v2f{fmaf(hpad[k], v.x, acc.x), fmaf(hpad[k], v.y, acc.y)};
+            }
+        }
+        y[t] = v2f{acc.x * sre - acc.y * sim, acc.x * sim + acc.y * sre};
+    }
+}
+
 // CC: complex taps (cccf).  Then H = Hr + j Hi and the tile keeps two
 // accumulators, C1 = Hr [Xr | Xi] and C2 = Hi [Xr | Xi]; y = (C1.re - C2.im,
 // C1.im + C2.re) is formed when the staged accumulators are read back.
@@ -119,9 +169,13 @@ template <bool CC>
 __global__ __launch_bounds__(NT, CC ? 2 : 3) void k_firfilt_mx(const v2f *__restrict__ win,
                                                               const v2f *__restrict__ x, long long n,
                                                               v2f *__restrict__ y, const float *__restrict__ hpad,
-                                                              float sre, float sim, long long nch, long long cpw)
+                                                              float sre, float sim, long long nch, long long cpw,
+                                                              int hlen)
 {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    // per chunk c % 3: bit 0 any unsafe sample, bit 1 one in the tail (the next chunk's halo);
+    // kept after the dynamic region so its base stays 16-byte aligned
+    unsigned *sbad = reinterpret_cast<unsigned *>(smem + lds_bytes_mx<CC>());
     unsigned char *planes = smem;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int r32 = lane & 31, hh = lane >> 5;
@@ -162,10 +216,13 @@ __global__ __launch_bounds__(NT, CC ? 2 : 3) void k_firfilt_mx(const v2f *__rest
     // 0..63 (the previous chunk's tail) come from halo buffer (c - 1) & 1,
     // filled by the lanes holding that tail one iteration earlier (from
     // memory for the first chunk)
+    if (tid < 3) sbad[tid] = 0u;
+    __syncthreads();
     if (tid < 8) {
         v4f v[4];
         load8(win, x, n, CH * c0 - 64 + 8 * tid, v);
         put8(halo + ((c0 - 1) & 1) * 6 * HPB, HPB, 8 * tid, v);
+        if (unsafe4(v[0]) | unsafe4(v[1]) | unsafe4(v[2]) | unsafe4(v[3])) atomicOr(&sbad[(c0 + 2) % 3], 2u);
     }
     // two chunks in flight per workgroup: register sets xa / xb alternate
     // (the loop is unrolled by two so neither set is ever copied, which would
@@ -187,8 +244,16 @@ __global__ __launch_bounds__(NT, CC ? 2 : 3) void k_firfilt_mx(const v2f *__rest
         }
         put8(planes, PLB, 64 + 8 * tid, xv);
         if (tid >= NT - 8) put8(halo + (c & 1) * 6 * HPB, HPB, 8 * (tid - (NT - 8)), xv);
+        const int cs = (int)(c % 3);
+        if (unsafe4(xv[0]) | unsafe4(xv[1]) | unsafe4(xv[2]) | unsafe4(xv[3]))
+            atomicOr(&sbad[cs], tid >= NT - 8 ? 3u : 1u);
+        if (tid == 0) sbad[(cs + 1) % 3] = 0u;   // chunk c+1's slot (last read in step c-2)
         if (c + 2 < c1) load8(win, x, n, CH * (c + 2) + 8 * tid, xv);
         __syncthreads();
+        if ((sbad[cs] & 1u) | (sbad[(cs + 2) % 3] & 2u)) {
+            exact_chunk_c<CC>(win, x, n, y, hpad, hlen, CH * c + 8 * tid, 8, sre, sim);
+            return;
+        }
 
         f32x16 C[NA];
 #pragma unroll
@@ -295,12 +360,27 @@ __device__ __forceinline__ void put8r(unsigned char *planes, int pstride, int po
     }
 }
 
+__device__ __attribute__((noinline)) void exact_chunk_r(const float *__restrict__ win, const float *__restrict__ x,
+                                                        long long n, float *__restrict__ y,
+                                                        const float *__restrict__ hpad, int hlen, long long t0,
+                                                        int cnt, float sre)
+{
+    for (int e = 0; e < cnt; e++) {
+        const long long t = t0 + e;
+        if (t >= n) break;
+        float acc = 0.f;
+        for (int k = 0; k < hlen; k++) acc = fmaf(hpad[k], rsample_at(win, x, n, t - k), acc);
+        y[t] = acc * sre;
+    }
+}
+
 __global__ __launch_bounds__(NT, 3) void k_firfilt_mx_r(const float *__restrict__ win, const float *__restrict__ x,
                                                        long long n, float *__restrict__ y,
                                                        const float *__restrict__ hpad, float sre, long long nch,
-                                                       long long cpw)
+                                                       long long cpw, int hlen)
 {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    unsigned *sbad = reinterpret_cast<unsigned *>(smem + LDS_BYTES_R);   // as k_firfilt_mx
     unsigned char *planes = smem;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int r32 = lane & 31, hh = lane >> 5;
@@ -330,12 +410,15 @@ __global__ __launch_bounds__(NT, 3) void k_firfilt_mx_r(const float *__restrict_
             A[p][s] = bf16x8{t[p][0].x, t[p][0].y, t[p][1].x, t[p][1].y, t[p][2].x, t[p][2].y, t[p][3].x, t[p][3].y};
     }
     // halo of the first chunk: 64 samples by threads 0..3 (16 each)
+    if (tid < 3) sbad[tid] = 0u;
+    __syncthreads();
     if (tid < 4) {
         v4f v[4];
         load16r(win, x, n, CHR * c0 - 64 + 16 * tid, v);
         unsigned char *hb = halo + ((c0 - 1) & 1) * 3 * HPB;
         put8r(hb, HPB, 16 * tid, v[0], v[1]);
         put8r(hb, HPB, 16 * tid + 8, v[2], v[3]);
+        if (unsafe4(v[0]) | unsafe4(v[1]) | unsafe4(v[2]) | unsafe4(v[3])) atomicOr(&sbad[(c0 + 2) % 3], 2u);
     }
     v4f xa[4], xb[4];
     load16r(win, x, n, CHR * c0 + 16 * tid, xa);
@@ -357,8 +440,16 @@ __global__ __launch_bounds__(NT, 3) void k_firfilt_mx_r(const float *__restrict_
             put8r(hb, HPB, 16 * (tid - (NT - 4)), xv[0], xv[1]);
             put8r(hb, HPB, 16 * (tid - (NT - 4)) + 8, xv[2], xv[3]);
         }
+        const int cs = (int)(c % 3);
+        if (unsafe4(xv[0]) | unsafe4(xv[1]) | unsafe4(xv[2]) | unsafe4(xv[3]))
+            atomicOr(&sbad[cs], tid >= NT - 4 ? 3u : 1u);
+        if (tid == 0) sbad[(cs + 1) % 3] = 0u;
         if (c + 2 < c1) load16r(win, x, n, CHR * (c + 2) + 16 * tid, xv);
         __syncthreads();
+        if ((sbad[cs] & 1u) | (sbad[(cs + 2) % 3] & 2u)) {
+            exact_chunk_r(win, x, n, y, hpad, hlen, CHR * c + 16 * tid, 16, sre);
+            return;
+        }
         f32x16 C = {};
 #pragma unroll
         for (int s = 0; s < 6; s++) {
@@ -408,16 +499,16 @@ __global__ __launch_bounds__(NT, 3) void k_firfilt_mx_r(const float *__restrict_
 extern "C" int lqk_firfilt_mx(const lqk_fir_desc *d, const void *hist, const void *x, unsigned long long n,
                               void *y, void *stream)
 {
-    if (d->hc != 64 || d->nchunk != 1 || x == y) return 0;
+    if (d->hc != 64 || d->nchunk != 1 || x == y || !d->mx_ok) return 0;
     if (((uintptr_t)x & 15) || ((uintptr_t)y & 15)) return 0;
     if (n == 0) return 1;
     if (d->kind == 0) {   // rrrf: 4096-output chunks, three workgroups per CU
         const long long nch = ((long long)n + CHR - 1) / CHR;
         const long long nwg = nch < 768 ? nch : 768;
         const long long cpw = (nch + nwg - 1) / nwg;
-        hipLaunchKernelGGL(k_firfilt_mx_r, dim3((unsigned)((nch + cpw - 1) / cpw)), dim3(NT), LDS_BYTES_R,
+        hipLaunchKernelGGL(k_firfilt_mx_r, dim3((unsigned)((nch + cpw - 1) / cpw)), dim3(NT), LDS_BYTES_R + 16,
                            (hipStream_t)stream, (const float *)hist, (const float *)x, (long long)n, (float *)y,
-                           (const float *)d->hpad, d->scale_re, nch, cpw);
+                           (const float *)d->hpad, d->scale_re, nch, cpw, (int)d->hlen);
         LQ_CHECK_LAUNCH();
         return 1;
     }
@@ -429,13 +520,13 @@ extern "C" int lqk_firfilt_mx(const lqk_fir_desc *d, const void *hist, const voi
     const dim3 grid((unsigned)((nch + cpw - 1) / cpw));
     const hipStream_t st = (hipStream_t)stream;
     if (cc)
-        hipLaunchKernelGGL(k_firfilt_mx<true>, grid, dim3(NT), lds_bytes_mx<true>(), st, (const v2f *)hist,
+        hipLaunchKernelGGL(k_firfilt_mx<true>, grid, dim3(NT), lds_bytes_mx<true>() + 16, st, (const v2f *)hist,
                            (const v2f *)x, (long long)n, (v2f *)y, (const float *)d->hpad, d->scale_re, d->scale_im,
-                           nch, cpw);
+                           nch, cpw, (int)d->hlen);
     else
-        hipLaunchKernelGGL(k_firfilt_mx<false>, grid, dim3(NT), lds_bytes_mx<false>(), st, (const v2f *)hist,
+        hipLaunchKernelGGL(k_firfilt_mx<false>, grid, dim3(NT), lds_bytes_mx<false>() + 16, st, (const v2f *)hist,
                            (const v2f *)x, (long long)n, (v2f *)y, (const float *)d->hpad, d->scale_re, d->scale_im,
-                           nch, cpw);
+                           nch, cpw, (int)d->hlen);
     LQ_CHECK_LAUNCH();
     return 1;
 }

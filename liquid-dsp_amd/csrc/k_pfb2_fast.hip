@@ -783,7 +783,8 @@ extern "C" int lqk_firpfbch2_analyzer_fast(unsigned int Mch, unsigned int m, con
                                            void *stream)
 {
     if (Mch != (unsigned)M || !(m == 4 || m == 2)) return 0;
-    if (((uintptr_t)x & 7) || ((uintptr_t)hist & 7)) return 0;
+    // x / hist: 8-byte sample loads; Y: 16-byte (two-bin) non-temporal stores
+    if (((uintptr_t)x & 7) || ((uintptr_t)hist & 7) || ((uintptr_t)Y & 15)) return 0;
     if (nblocks == 0) return 1;
     hipStream_t st = (hipStream_t)stream;
     const float2 *tw = (const float2 *)lqrt_twiddles();

@@ -49,6 +49,8 @@ typedef struct {
     unsigned int nchunk;     /* padded length = hc*nchunk */
     const void *hpad;        /* device coefficients (float or float2) */
     float scale_re, scale_im;
+    int mx_ok;               /* taps finite, nonzero |h| in [2^-50, 2^50]: the matrix-core kernel's
+                              * three-term bf16 split is float32-accurate (k_firfilt_mx.hip) */
 } lqk_fir_desc;
 
 void lqk_firfilt(const lqk_fir_desc *d, const void *hist, const void *x, unsigned long long n,

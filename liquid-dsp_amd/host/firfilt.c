@@ -78,6 +78,16 @@ static void lq_firfilt_upload_coefs(lq_firfilt *q)
     lqrt_sync(q->ctx.stream);
     free(pad);
     q->d.hpad = q->d_hpad;
+    /* the matrix-core kernel splits taps into three bf16 terms; outside
+     * [2^-50, 2^50] (or non-finite) the split would lose float32 accuracy or
+     * the reference's Inf/NaN propagation, so such filters stay on the VALU
+     * kernel */
+    const unsigned int nv = q->hlen * (unsigned int)(q->csz / sizeof(float));
+    q->d.mx_ok = 1;
+    for (unsigned int i = 0; i < nv; i++) {
+        const float a = fabsf(q->h[i]);
+        if (!(a <= 0x1p50f) || (a != 0.0f && a < 0x1p-50f)) q->d.mx_ok = 0;
+    }
 }
 
 lq_firfilt *lq_firfilt_create(int kind, const float *h, unsigned int n, const char *who)

@@ -1,0 +1,99 @@
+"""Edge cases of the firfilt kernels against the oracle (`-m gpu`).
+
+The matrix-core kernel (k_firfilt_mx.hip, 33..64 taps) computes with a
+three-term bf16 split; the VALU kernel pads taps with zeros to 16/32/64*k.
+Neither may change what the reference computes (firfilt.c:322-338, a plain
+float32 dot product over the true taps): these tests sweep the input scale
+from 2^-120 to 2^120 and inject +Inf / -Inf / NaN samples, and require
+  * the same finite / +Inf / -Inf / NaN pattern as the oracle, sample for
+    sample (so a bad sample reaches exactly the outputs t..t+h-1 it reaches
+    in the reference, none before it), and
+  * normwise 1e-5 on the finite outputs (the suite's parity bound).
+"""
+import numpy as np
+import pytest
+
+import liquidmi as LQ
+import oracle_lib as O
+
+pytestmark = pytest.mark.gpu
+
+TYPES = {"rrrf": O.RRRF, "crcf": O.CRCF, "cccf": O.CCCF}
+NRM = 1e-5
+
+
+def _data(t, n, h_len, seed, scale):
+    r = np.random.default_rng(seed)
+    if t == "rrrf":
+        x = (r.uniform(-0.5, 0.5, n) * scale).astype(np.float32)
+    else:
+        x = ((r.uniform(-0.5, 0.5, n) + 1j * r.uniform(-0.5, 0.5, n)) * scale).astype(np.complex64)
+    if t == "cccf":
+        h = (r.uniform(-0.5, 0.5, h_len) + 1j * r.uniform(-0.5, 0.5, h_len)).astype(np.complex64)
+    else:
+        h = r.uniform(-0.5, 0.5, h_len).astype(np.float32)
+    return h, x
+
+
+def _pattern(a):
+    a = np.asarray(a)
+    parts = [a.real, a.imag] if np.iscomplexobj(a) else [a]
+    return np.stack([np.where(np.isnan(p), 3, np.where(np.isposinf(p), 1, np.where(np.isneginf(p), 2, 0)))
+                     for p in parts])
+
+
+def _check(got, ref):
+    assert np.array_equal(_pattern(got), _pattern(ref)), "non-finite pattern differs from the oracle"
+    fin = np.isfinite(ref)
+    if fin.any():
+        d = np.max(np.abs(got[fin].astype(np.complex128) - ref[fin].astype(np.complex128)))
+        assert d <= NRM * np.max(np.abs(ref[fin])) or d == 0.0
+
+
+def _run(t, h, x, dev):
+    g = LQ.FirFilt(t, h)
+    if not dev:
+        return g.execute_block(x)
+    bx = LQ.DeviceBuffer.from_array(x)
+    by = LQ.DeviceBuffer(x.nbytes)
+    g.execute_block_dev(bx.p, len(x), by.p)
+    g.synchronize()
+    return by.to_array(x.dtype, len(x))
+
+
+@pytest.mark.parametrize("t", ["rrrf", "crcf", "cccf"])
+@pytest.mark.parametrize("h_len", [64, 45, 20, 100])
+@pytest.mark.parametrize("e", [-120, -60, -40, 40, 60, 120])
+def test_firfilt_input_scale_sweep(t, h_len, e):
+    h, x = _data(t, 50001, h_len, 7 + h_len, 2.0 ** e)
+    ref = O.FirFilt(TYPES[t], h).execute_block(x)
+    _check(_run(t, h, x, dev=True), ref)
+
+
+@pytest.mark.parametrize("t", ["rrrf", "crcf", "cccf"])
+@pytest.mark.parametrize("h_len", [64, 45, 20, 100])
+def test_firfilt_nonfinite_samples(t, h_len):
+    h, x = _data(t, 70001, h_len, 11 + h_len, 1.0)
+    # isolated +Inf, -Inf and NaN, one in the first chunk's halo region, one
+    # on a 2048/4096-sample chunk seam, one deep inside; plus a second call
+    x[5] = np.inf
+    x[4096 - 1] = -np.inf
+    x[33333] = np.nan
+    if t != "rrrf":
+        x[50000] = complex(1.0, np.inf)
+    ref = O.FirFilt(TYPES[t], h).execute_block(x)
+    _check(_run(t, h, x, dev=True), ref)
+    _check(_run(t, h, x, dev=False), ref)
+    # outputs strictly before the first bad sample stay finite
+    assert np.all(np.isfinite(_run(t, h, x, dev=True)[:5]))
+
+
+def test_firfilt_extreme_taps_stay_exact():
+    # taps outside [2^-50, 2^50] keep the filter off the matrix cores
+    r = np.random.default_rng(3)
+    h = r.uniform(-0.5, 0.5, 64).astype(np.float32)
+    h[7] = 2.0 ** -70
+    h[9] = np.float32(2.0 ** 60)
+    x = ((r.uniform(-0.5, 0.5, 30000) + 1j * r.uniform(-0.5, 0.5, 30000)) * 2.0 ** -20).astype(np.complex64)
+    ref = O.FirFilt(O.CRCF, h).execute_block(x)
+    _check(_run("crcf", h, x, dev=True), ref)
