@@ -68,6 +68,16 @@ __device__ __forceinline__ float2 apply_scale(float2 a, float sre, float sim)
     return make_float2(a.x * sre - a.y * sim, a.x * sim + a.y * sre);
 }
 __device__ __forceinline__ float2 apply_scale_real(float2 a, float s) { return make_float2(a.x * s, a.y * s); }
+// output scale as the reference applies it (firfilt.c:337, firpfb.c:343,
+// `*y *= scale`): a real scale (rrrf / crcf) multiplies each component, a
+// complex one (cccf) is a complex product -- they differ for Inf samples
+template <int KIND, typename T>
+__device__ __forceinline__ T oscale(T a, float sre, float sim)
+{
+    if constexpr (KIND == 2) return apply_scale(a, sre, sim);
+    else if constexpr (sizeof(T) == 8) return apply_scale_real(a, sre);
+    else return a * sre;
+}
 
 __device__ __forceinline__ float vadd(float a, float b) { return a + b; }
 __device__ __forceinline__ float2 vadd(float2 a, float2 b) { return make_float2(a.x + b.x, a.y + b.y); }
@@ -223,7 +233,7 @@ __global__ __launch_bounds__(NT) void k_firfilt(const typename kt<KIND>::T *__re
     for (int i = 0; i < R / VE; i++) {
         T o[VE];
 #pragma unroll
-        for (int k = 0; k < VE; k++) o[k] = apply_scale(acc[i * VE + k], sre, sim);
+        for (int k = 0; k < VE; k++) o[k] = oscale<KIND>(acc[i * VE + k], sre, sim);
         *reinterpret_cast<float4 *>(smem + lds_off<T>(R * threadIdx.x + i * VE)) = pack16(o);
     }
     __syncthreads();
@@ -257,7 +267,7 @@ __global__ void k_firpfb_single(const typename kt<KIND>::TC *__restrict__ hpoly,
     if (threadIdx.x == 0) {
         T s = zero<T>();
         for (int t = 0; t < 64; t++) s = vadd(s, part[t]);
-        y[0] = apply_scale(s, sre, sim);
+        y[0] = oscale<KIND>(s, sre, sim);
     }
 }
 
@@ -301,7 +311,7 @@ __global__ void k_fir_single(const typename kt<KIND>::TC *__restrict__ hpad, int
     if (threadIdx.x == 0) {
         T s = zero<T>();
         for (int i = 0; i < 64; i++) s = vadd(s, part[i]);
-        y[0] = apply_scale(s, sre, sim);
+        y[0] = oscale<KIND>(s, sre, sim);
     }
 }
 
@@ -459,7 +469,7 @@ __global__ __launch_bounds__(NT) void k_firinterp(const typename kt<KIND>::T *__
     for (int p = 0; p < M; p++) {
         T acc = zero<T>();
         for (int l = 0; l < L; l++) mac(acc, hpoly[p * L + l], w[-l]);
-        y[i * M + p] = apply_scale(acc, sre, sim);
+        y[i * M + p] = oscale<KIND>(acc, sre, sim);
     }
 }
 
@@ -511,7 +521,7 @@ __global__ __launch_bounds__(NT) void k_firinterp_t(const typename kt<KIND>::T *
             if (l + 2 < LT) mac(acc, h4.z, w[l + 2]);
             if (l + 3 < LT) mac(acc, h4.w, w[l + 3]);
         }
-        st[lane * M + p] = apply_scale(acc, sre, sim);
+        st[lane * M + p] = oscale<KIND>(acc, sre, sim);
     }
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();

@@ -158,8 +158,19 @@ __device__ __attribute__((noinline)) void exact_chunk_c(const v2f *__restrict__ 
                 acc = v2f{fmaf(hpad[k], v.x, acc.x), fmaf(hpad[k], v.y, acc.y)};
             }
         }
-        y[t] = v2f{acc.x * sre - acc.y * sim, acc.x * sim + acc.y * sre};
+        // crcf: real scale per component (firfilt.c:337); cccf: complex product
+        y[t] = CC ? v2f{acc.x * sre - acc.y * sim, acc.x * sim + acc.y * sre} : v2f{acc.x * sre, acc.y * sre};
     }
+}
+
+// 8 complex samples from byte offset off of the range-checked descriptor
+// over x (zeros past the end): no branch, so the loads of the chunk after
+// next stay in flight while this chunk runs (a branchy load merged its
+// results through register copies, which made every prefetch wait at once)
+__device__ __forceinline__ void load8b(__amdgpu_buffer_rsrc_t rx, unsigned off, v4f (&v)[4])
+{
+#pragma unroll
+    for (int q = 0; q < 4; q++) v[q] = __builtin_amdgcn_raw_buffer_load_b128(rx, off + 16 * q, 0, 0);
 }
 
 // CC: complex taps (cccf).  Then H = Hr + j Hi and the tile keeps two
@@ -226,10 +237,21 @@ __global__ __launch_bounds__(NT, CC ? 2 : 3) void k_firfilt_mx(const v2f *__rest
     }
     // two chunks in flight per workgroup: register sets xa / xb alternate
     // (the loop is unrolled by two so neither set is ever copied, which would
-    // wait on its loads early)
+    // wait on its loads early).  The loop body is branch-free in its memory
+    // operations -- range-checked buffer loads and stores, a step past the
+    // workgroup's last chunk (odd chunk counts) lands out of range -- so the
+    // compiler's vmcnt waits only for the rows a step consumes and the
+    // previous chunks' stores stay in flight.  The host keeps n * 8 bytes
+    // below 2^31 per launch and cpw even (chunk c1 then lies past n).
+    const __amdgpu_buffer_rsrc_t rx = __builtin_amdgcn_make_buffer_rsrc((void *)x, (short)0, (int)(n * 8), 0x00020000);
+    const __amdgpu_buffer_rsrc_t ry = __builtin_amdgcn_make_buffer_rsrc((void *)y, (short)0, (int)(n * 8), 0x00020000);
+    const unsigned OOB = 0xfffff000u;   // an offset past any launch's range
     v4f xa[4], xb[4];
-    load8(win, x, n, CH * c0 + 8 * tid, xa);
-    if (c0 + 1 < c1) load8(win, x, n, CH * (c0 + 1) + 8 * tid, xb);
+    load8b(rx, (unsigned)(CH * c0 + 8 * tid) * 8u, xa);
+    load8b(rx, c0 + 1 < c1 ? (unsigned)(CH * (c0 + 1) + 8 * tid) * 8u : OOB, xb);
+    // chunks of this workgroup that need the exact path (bit c - c0), done after the loop
+    unsigned *bad_mask = sbad + 4;
+    if (tid < 16) bad_mask[tid] = 0u;
 
     // B operand: lane column n = r32 -> segment sg = n & 15, component n >> 4
     const int sg = r32 & 15, comp = r32 >> 4;
@@ -248,11 +270,11 @@ __global__ __launch_bounds__(NT, CC ? 2 : 3) void k_firfilt_mx(const v2f *__rest
         if (unsafe4(xv[0]) | unsafe4(xv[1]) | unsafe4(xv[2]) | unsafe4(xv[3]))
             atomicOr(&sbad[cs], tid >= NT - 8 ? 3u : 1u);
         if (tid == 0) sbad[(cs + 1) % 3] = 0u;   // chunk c+1's slot (last read in step c-2)
-        if (c + 2 < c1) load8(win, x, n, CH * (c + 2) + 8 * tid, xv);
+        load8b(rx, c + 2 < c1 ? (unsigned)(CH * (c + 2) + 8 * tid) * 8u : OOB, xv);
         __syncthreads();
-        if ((sbad[cs] & 1u) | (sbad[(cs + 2) % 3] & 2u)) {
-            exact_chunk_c<CC>(win, x, n, y, hpad, hlen, CH * c + 8 * tid, 8, sre, sim);
-            return;
+        if (tid == 0 && ((sbad[cs] & 1u) | (sbad[(cs + 2) % 3] & 2u)) && c < c1) {
+            const int k = (int)(c - c0);
+            bad_mask[k >> 5] |= 1u << (k & 31);
         }
 
         f32x16 C[NA];
@@ -286,7 +308,9 @@ __global__ __launch_bounds__(NT, CC ? 2 : 3) void k_firfilt_mx(const v2f *__rest
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
         __builtin_amdgcn_wave_barrier();
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-        const long long o0 = CH * c + 512 * wave;
+        // 16-byte pairs; a pair straddling n (odd n) keeps its in-range half
+        // (the range check is per dword)
+        const unsigned o0 = (unsigned)(CH * c + 512 * wave) * 8u;
 #pragma unroll
         for (int q = 0; q < 4; q++) {
             const int o = 2 * (lane + 64 * q);
@@ -295,14 +319,10 @@ __global__ __launch_bounds__(NT, CC ? 2 : 3) void k_firfilt_mx(const v2f *__rest
                 const v4f b = *reinterpret_cast<const v4f *>(stage + 16 * SSTR + (o >> 5) * SSTR + 2 * (o & 31));
                 a = v4f{a.x - b.y, a.y + b.x, a.z - b.w, a.w + b.z};
             }
-            const v4f r = {a.x * sre - a.y * sim, a.x * sim + a.y * sre, a.z * sre - a.w * sim,
-                           a.z * sim + a.w * sre};
-            const long long ty = o0 + o;
-            if (ty + 2 <= n) {
-                __builtin_nontemporal_store(r, reinterpret_cast<v4f *>(y + ty));
-            } else if (ty < n) {
-                y[ty] = v2f{r.x, r.y};
-            }
+            const v4f r = CC ? v4f{a.x * sre - a.y * sim, a.x * sim + a.y * sre, a.z * sre - a.w * sim,
+                                   a.z * sim + a.w * sre}
+                             : a * sre;   // crcf: real scale per component (firfilt.c:337)
+            __builtin_amdgcn_raw_buffer_store_b128(r, ry, c < c1 ? o0 + 8u * o : OOB, 0, 2);
         }
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
         __builtin_amdgcn_wave_barrier();
@@ -310,7 +330,23 @@ __global__ __launch_bounds__(NT, CC ? 2 : 3) void k_firfilt_mx(const v2f *__rest
     };
     for (long long c = c0; c < c1; c += 2) {
         step(c, xa);
-        if (c + 1 < c1) step(c + 1, xb);
+        step(c + 1, xb);
+    }
+    // the range guard's chunks: the exact float32 outputs overwrite what the
+    // matrix path stored for them.  Only workgroup-scope ordering is needed
+    // (the same workgroup wrote them); no fence at all in the common case (a
+    // device-scope fence here writes back L2 in every workgroup: +12 %)
+    __syncthreads();
+    unsigned anybad = 0;
+#pragma unroll
+    for (int i = 0; i < 16; i++) anybad |= bad_mask[i];
+    if (anybad) {
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+        __syncthreads();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+        for (int k = 0; k < (int)(c1 - c0); k++)
+            if (bad_mask[k >> 5] & (1u << (k & 31)))
+                exact_chunk_c<CC>(win, x, n, y, hpad, hlen, CH * (c0 + k) + 8 * tid, 8, sre, sim);
     }
 }
 
@@ -374,6 +410,12 @@ __device__ __attribute__((noinline)) void exact_chunk_r(const float *__restrict_
     }
 }
 
+__device__ __forceinline__ void load16rb(__amdgpu_buffer_rsrc_t rx, unsigned off, v4f (&v)[4])
+{
+#pragma unroll
+    for (int q = 0; q < 4; q++) v[q] = __builtin_amdgcn_raw_buffer_load_b128(rx, off + 16 * q, 0, 0);
+}
+
 __global__ __launch_bounds__(NT, 3) void k_firfilt_mx_r(const float *__restrict__ win, const float *__restrict__ x,
                                                        long long n, float *__restrict__ y,
                                                        const float *__restrict__ hpad, float sre, long long nch,
@@ -420,9 +462,15 @@ __global__ __launch_bounds__(NT, 3) void k_firfilt_mx_r(const float *__restrict_
         put8r(hb, HPB, 16 * tid + 8, v[2], v[3]);
         if (unsafe4(v[0]) | unsafe4(v[1]) | unsafe4(v[2]) | unsafe4(v[3])) atomicOr(&sbad[(c0 + 2) % 3], 2u);
     }
+    // branch-free memory operations in the loop, as k_firfilt_mx
+    const __amdgpu_buffer_rsrc_t rx = __builtin_amdgcn_make_buffer_rsrc((void *)x, (short)0, (int)(n * 4), 0x00020000);
+    const __amdgpu_buffer_rsrc_t ry = __builtin_amdgcn_make_buffer_rsrc((void *)y, (short)0, (int)(n * 4), 0x00020000);
+    const unsigned OOB = 0xfffff000u;
     v4f xa[4], xb[4];
-    load16r(win, x, n, CHR * c0 + 16 * tid, xa);
-    if (c0 + 1 < c1) load16r(win, x, n, CHR * (c0 + 1) + 16 * tid, xb);
+    load16rb(rx, (unsigned)(CHR * c0 + 16 * tid) * 4u, xa);
+    load16rb(rx, c0 + 1 < c1 ? (unsigned)(CHR * (c0 + 1) + 16 * tid) * 4u : OOB, xb);
+    unsigned *bad_mask = sbad + 4;
+    if (tid < 16) bad_mask[tid] = 0u;
     const int sg = r32;   // B column = segment
     auto step = [&](long long c, v4f (&xv)[4]) {
         __syncthreads();
@@ -444,11 +492,11 @@ __global__ __launch_bounds__(NT, 3) void k_firfilt_mx_r(const float *__restrict_
         if (unsafe4(xv[0]) | unsafe4(xv[1]) | unsafe4(xv[2]) | unsafe4(xv[3]))
             atomicOr(&sbad[cs], tid >= NT - 4 ? 3u : 1u);
         if (tid == 0) sbad[(cs + 1) % 3] = 0u;
-        if (c + 2 < c1) load16r(win, x, n, CHR * (c + 2) + 16 * tid, xv);
+        load16rb(rx, c + 2 < c1 ? (unsigned)(CHR * (c + 2) + 16 * tid) * 4u : OOB, xv);
         __syncthreads();
-        if ((sbad[cs] & 1u) | (sbad[(cs + 2) % 3] & 2u)) {
-            exact_chunk_r(win, x, n, y, hpad, hlen, CHR * c + 16 * tid, 16, sre);
-            return;
+        if (tid == 0 && ((sbad[cs] & 1u) | (sbad[(cs + 2) % 3] & 2u)) && c < c1) {
+            const int k = (int)(c - c0);
+            bad_mask[k >> 5] |= 1u << (k & 31);
         }
         f32x16 C = {};
 #pragma unroll
@@ -470,17 +518,12 @@ __global__ __launch_bounds__(NT, 3) void k_firfilt_mx_r(const float *__restrict_
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
         __builtin_amdgcn_wave_barrier();
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-        const long long o0 = CHR * c + 1024 * wave;
+        const unsigned o0 = (unsigned)(CHR * c + 1024 * wave) * 4u;
 #pragma unroll
         for (int q = 0; q < 4; q++) {
             const int o = 4 * (lane + 64 * q);
             const v4f a = *reinterpret_cast<const v4f *>(stage + (o >> 5) * SSTRR + (o & 31)) * sre;
-            const long long ty = o0 + o;
-            if (ty + 4 <= n) {
-                __builtin_nontemporal_store(a, reinterpret_cast<v4f *>(y + ty));
-            } else {
-                for (int e = 0; e < 4 && ty + e < n; e++) y[ty + e] = a[e];
-            }
+            __builtin_amdgcn_raw_buffer_store_b128(a, ry, c < c1 ? o0 + 4u * o : OOB, 0, 2);
         }
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
         __builtin_amdgcn_wave_barrier();
@@ -488,7 +531,19 @@ __global__ __launch_bounds__(NT, 3) void k_firfilt_mx_r(const float *__restrict_
     };
     for (long long c = c0; c < c1; c += 2) {
         step(c, xa);
-        if (c + 1 < c1) step(c + 1, xb);
+        step(c + 1, xb);
+    }
+    __syncthreads();
+    unsigned anybad = 0;
+#pragma unroll
+    for (int i = 0; i < 16; i++) anybad |= bad_mask[i];
+    if (anybad) {
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+        __syncthreads();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+        for (int k = 0; k < (int)(c1 - c0); k++)
+            if (bad_mask[k >> 5] & (1u << (k & 31)))
+                exact_chunk_r(win, x, n, y, hpad, hlen, CHR * (c0 + k) + 16 * tid, 16, sre);
     }
 }
 
@@ -496,37 +551,73 @@ __global__ __launch_bounds__(NT, 3) void k_firfilt_mx_r(const float *__restrict_
 
 // Returns 1 if the call was handled on the matrix cores: rrrf, crcf or cccf,
 // 33..64 taps (HP = 64, one chunk), not in place, 16-byte aligned x and y.
+// Chunks per workgroup: each workgroup streams a contiguous segment of cpw
+// chunks and all of them run at once, so the segment length is the stride
+// between concurrent accesses.  An even cpw put those strides on a power-of-
+// two multiple of the chunk size and the segments onto the same HBM channels:
+// cpw 172 ran 12-15 % slower than 171 or 173 (2^28 samples, tools/mb/
+// mb_firmx_sweep.hip).  So cpw is odd; an odd count leaves each workgroup one
+// step past its last chunk, which the loop's range checks turn into no-ops.
+// At most 511: the per-workgroup guard mask holds 512 chunks (16 words after
+// the three guard slots: the kernels' dynamic LDS carries 80 extra bytes).
+static long long odd_cpw(long long nch, long long nwg)
+{
+    const long long cpw = ((nch + nwg - 1) / nwg) | 1;
+    if (cpw > 511) {
+        fprintf(stderr, "error: firfilt: %lld chunks per workgroup exceed the guard mask\n", cpw);
+        exit(1);
+    }
+    return cpw;
+}
+
+// Launches cover at most 2^28 complex / 2^29 real samples (2 GiB) so the
+// range-checked load offsets fit 32 bits; a later launch takes its 64-sample
+// history straight from the preceding input.
+static void launch_mx(const lqk_fir_desc *d, const void *hist, const void *x, long long n, void *y,
+                      hipStream_t st)
+{
+    if (d->kind == 0) {   // rrrf: 4096-output chunks, three workgroups per CU
+        const long long nch = (n + CHR - 1) / CHR;
+        const long long nwg = nch < 768 ? nch : 768;
+        const long long cpw = odd_cpw(nch, nwg);
+        hipLaunchKernelGGL(k_firfilt_mx_r, dim3((unsigned)((nch + cpw - 1) / cpw)), dim3(NT), LDS_BYTES_R + 80, st,
+                           (const float *)hist, (const float *)x, n, (float *)y, (const float *)d->hpad, d->scale_re,
+                           nch, cpw, (int)d->hlen);
+        LQ_CHECK_LAUNCH();
+        return;
+    }
+    const bool cc = d->kind == 2;
+    const long long nch = (n + CH - 1) / CH;
+    const long long wgs = cc ? 512 : 768;   // resident workgroups (two / three per CU)
+    const long long nwg = nch < wgs ? nch : wgs;
+    const long long cpw = odd_cpw(nch, nwg);
+    const dim3 grid((unsigned)((nch + cpw - 1) / cpw));
+    if (cc)
+        hipLaunchKernelGGL(k_firfilt_mx<true>, grid, dim3(NT), lds_bytes_mx<true>() + 80, st, (const v2f *)hist,
+                           (const v2f *)x, n, (v2f *)y, (const float *)d->hpad, d->scale_re, d->scale_im, nch, cpw,
+                           (int)d->hlen);
+    else
+        hipLaunchKernelGGL(k_firfilt_mx<false>, grid, dim3(NT), lds_bytes_mx<false>() + 80, st, (const v2f *)hist,
+                           (const v2f *)x, n, (v2f *)y, (const float *)d->hpad, d->scale_re, d->scale_im, nch, cpw,
+                           (int)d->hlen);
+    LQ_CHECK_LAUNCH();
+}
+
+// Returns 1 if the call was handled on the matrix cores: rrrf, crcf or cccf,
+// 33..64 taps (HP = 64, one chunk), taps in the split's safe range, not in
+// place, 16-byte aligned x and y.
 extern "C" int lqk_firfilt_mx(const lqk_fir_desc *d, const void *hist, const void *x, unsigned long long n,
                               void *y, void *stream)
 {
     if (d->hc != 64 || d->nchunk != 1 || x == y || !d->mx_ok) return 0;
     if (((uintptr_t)x & 15) || ((uintptr_t)y & 15)) return 0;
     if (n == 0) return 1;
-    if (d->kind == 0) {   // rrrf: 4096-output chunks, three workgroups per CU
-        const long long nch = ((long long)n + CHR - 1) / CHR;
-        const long long nwg = nch < 768 ? nch : 768;
-        const long long cpw = (nch + nwg - 1) / nwg;
-        hipLaunchKernelGGL(k_firfilt_mx_r, dim3((unsigned)((nch + cpw - 1) / cpw)), dim3(NT), LDS_BYTES_R + 16,
-                           (hipStream_t)stream, (const float *)hist, (const float *)x, (long long)n, (float *)y,
-                           (const float *)d->hpad, d->scale_re, nch, cpw, (int)d->hlen);
-        LQ_CHECK_LAUNCH();
-        return 1;
+    const size_t es = d->kind == 0 ? 4 : 8;
+    const long long LCH = d->kind == 0 ? (1LL << 29) : (1LL << 28);
+    for (long long o = 0; o < (long long)n; o += LCH) {
+        const long long nn = ((long long)n - o) < LCH ? ((long long)n - o) : LCH;
+        const char *xo = (const char *)x + o * es;
+        launch_mx(d, o == 0 ? hist : (const void *)(xo - 64 * es), xo, nn, (char *)y + o * es, (hipStream_t)stream);
     }
-    const bool cc = d->kind == 2;
-    const long long nch = ((long long)n + CH - 1) / CH;
-    const long long wgs = cc ? 512 : 768;   // resident workgroups (two / three per CU)
-    const long long nwg = nch < wgs ? nch : wgs;
-    const long long cpw = (nch + nwg - 1) / nwg;
-    const dim3 grid((unsigned)((nch + cpw - 1) / cpw));
-    const hipStream_t st = (hipStream_t)stream;
-    if (cc)
-        hipLaunchKernelGGL(k_firfilt_mx<true>, grid, dim3(NT), lds_bytes_mx<true>() + 16, st, (const v2f *)hist,
-                           (const v2f *)x, (long long)n, (v2f *)y, (const float *)d->hpad, d->scale_re, d->scale_im,
-                           nch, cpw, (int)d->hlen);
-    else
-        hipLaunchKernelGGL(k_firfilt_mx<false>, grid, dim3(NT), lds_bytes_mx<false>() + 16, st, (const v2f *)hist,
-                           (const v2f *)x, (long long)n, (v2f *)y, (const float *)d->hpad, d->scale_re, d->scale_im,
-                           nch, cpw, (int)d->hlen);
-    LQ_CHECK_LAUNCH();
     return 1;
 }

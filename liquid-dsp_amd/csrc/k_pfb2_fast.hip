@@ -51,65 +51,6 @@ constexpr int NBUF = 17;   // LDS block buffers (writes b0..b0+16, FFT reads b0.
 constexpr int BSTR = 1088; // floats2 per block buffer (16 x 68 transpose)
 constexpr int TSTR = 68;
 
-// cos/sin(2 pi e / 16), e = 0..15
-__device__ constexpr float C16[16] = {1.0f,         0.92387953f,  0.70710678f,  0.38268343f,
-                                      0.0f,         -0.38268343f, -0.70710678f, -0.92387953f,
-                                      -1.0f,        -0.92387953f, -0.70710678f, -0.38268343f,
-                                      0.0f,         0.38268343f,  0.70710678f,  0.92387953f};
-__device__ constexpr float S16[16] = {0.0f,         0.38268343f,  0.70710678f,  0.92387953f,
-                                      1.0f,         0.92387953f,  0.70710678f,  0.38268343f,
-                                      0.0f,         -0.38268343f, -0.70710678f, -0.92387953f,
-                                      -1.0f,        -0.92387953f, -0.70710678f, -0.38268343f};
-
-// 16-point backward DFT (e^{+j2pi nk/16}) in registers, natural order in/out.
-__device__ __forceinline__ void dft16_bwd(float2 (&v)[16])
-{
-    float2 t[16];
-#pragma unroll
-    for (int q = 0; q < 4; q++) {
-        float2 a0 = v[q], a1 = v[4 + q], a2 = v[8 + q], a3 = v[12 + q];
-        dft4(a0, a1, a2, a3, -1);
-        // twiddle W16^{+q k0}
-        t[0 * 4 + q] = a0;
-        if (q == 0) {
-            t[1 * 4 + q] = a1;
-            t[2 * 4 + q] = a2;
-            t[3 * 4 + q] = a3;
-        } else {
-            t[1 * 4 + q] = cmul(a1, make_float2(C16[(1 * q) & 15], S16[(1 * q) & 15]));
-            t[2 * 4 + q] = cmul(a2, make_float2(C16[(2 * q) & 15], S16[(2 * q) & 15]));
-            t[3 * 4 + q] = cmul(a3, make_float2(C16[(3 * q) & 15], S16[(3 * q) & 15]));
-        }
-    }
-#pragma unroll
-    for (int k0 = 0; k0 < 4; k0++) {
-        float2 b0 = t[k0 * 4 + 0], b1 = t[k0 * 4 + 1], b2 = t[k0 * 4 + 2], b3 = t[k0 * 4 + 3];
-        dft4(b0, b1, b2, b3, -1);
-        v[k0 + 0] = b0;
-        v[k0 + 4] = b1;
-        v[k0 + 8] = b2;
-        v[k0 + 12] = b3;
-    }
-}
-
-// exchange with the partner lane inside a quad through DPP (a VALU operand
-// modifier, no LDS crossbar): quad_perm [1,0,3,2] for xor 1, [2,3,0,1] for xor 2
-template <int X>
-__device__ __forceinline__ float2 quad_xor(float2 v)
-{
-    constexpr int ctrl = X == 1 ? 0xB1 : 0x4E;
-    const int a = __builtin_amdgcn_mov_dpp(__float_as_int(v.x), ctrl, 0xF, 0xF, false);
-    const int b = __builtin_amdgcn_mov_dpp(__float_as_int(v.y), ctrl, 0xF, 0xF, false);
-    return make_float2(__int_as_float(a), __int_as_float(b));
-}
-
-// streaming (non-temporal) store of one complex sample: output is written once
-__device__ __forceinline__ void st_nt(float2 *p, float2 v)
-{
-    v2f w = {v.x, v.y};
-    __builtin_nontemporal_store(w, reinterpret_cast<v2f *>(p));
-}
-
 __device__ __forceinline__ void lds_fence()
 {
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
@@ -139,22 +80,10 @@ struct Params {
     float2 *Y;
 };
 
-__device__ unsigned long long g_pfb2_clk[2 * 1024];   // dev experiments (XMODE >= 10)
-
-// XMODE (dev experiments, 0 in the library): 1 skip the FFT phase, 2 skip the
-// row loads, 3 skip the output stores; +10 records per-workgroup clocks
-// SMODE: output path. 0: per-lane 8-byte non-temporal stores straight from the
-// FFT layout; 1: same, plain stores; 2: through the block's LDS buffer into
-// 16-byte non-temporal stores; 3: 2 with plain stores
-template <int L, int XMODE = 0, int SMODE = 2, int PF = 8, int BAR = 1, int TRES = 0, int FM = 1>
+template <int L, int PF = 8>
 __global__ __launch_bounds__(NT, 1) void k_pfb2_an1024(Params P, const float *__restrict__ hsub,
                                                        const float2 *__restrict__ tw4096)
 {
-    unsigned long long clk0 = 0, rt0 = 0;
-    if (XMODE >= 10) {
-        clk0 = __builtin_amdgcn_s_memtime();
-        rt0 = __builtin_amdgcn_s_memrealtime();
-    }
     static_assert(L <= NS, "ring too small");
     __shared__ __attribute__((aligned(16))) float2 xb[NBUF * BSTR];
     __shared__ __attribute__((aligned(16))) float2 tw1[16 * 64]; // W_1024^{+t k1}
@@ -189,7 +118,7 @@ __global__ __launch_bounds__(NT, 1) void k_pfb2_an1024(Params P, const float *__
     float ta[L], tb[L];
     auto load_taps = [&]() {
         int oa = (lo ? j : (j ^ M2)) * L, ob = (lo ? (j ^ M2) : j) * L;
-        if (!TRES) asm volatile("" : "+v"(oa), "+v"(ob)); // keep the reload inside the loop
+        asm volatile("" : "+v"(oa), "+v"(ob)); // keep the reload inside the loop
 #pragma unroll
         for (int n = 0; n < L; n++) {
             ta[n] = hsub[oa + n];
@@ -221,13 +150,19 @@ __global__ __launch_bounds__(NT, 1) void k_pfb2_an1024(Params P, const float *__
     // local index of row (8gs - NS)'s sample for this lane; rows step by M
     const long long ibase = (8 * gs - NS) * M + (long long)tid - P.B0 * M2;
     const unsigned ox0 = (unsigned)(ibase * 8), oh0 = (unsigned)((HL + ibase) * 8);
-    auto fetch = [&](long long c) -> float2 {
-        if (XMODE % 10 == 2) return make_float2((float)(c & 7), 0.5f);
-        const unsigned k = (unsigned)(c - (8 * gs - NS)) * (unsigned)(M * 8);
-        const float2 a = __builtin_bit_cast(float2, __builtin_amdgcn_raw_buffer_load_b64(rx, ox0 + k, 0, 0));
-        const float2 b = __builtin_bit_cast(float2, __builtin_amdgcn_raw_buffer_load_b64(rh, oh0 + k, 0, 0));
-        return make_float2(a.x + b.x, a.y + b.y);
+    // a row is fetched as its two raw loads; they are added only where the
+    // sample is consumed, so a prefetch does not wait for its data (an add at
+    // fetch time made every wave wait for the next iteration's rows before the
+    // transform phase: the loads then never overlapped the transforms)
+    struct Raw {
+        float2 a, b;
     };
+    auto fetch = [&](long long c) -> Raw {
+        const unsigned k = (unsigned)(c - (8 * gs - NS)) * (unsigned)(M * 8);
+        return {__builtin_bit_cast(float2, __builtin_amdgcn_raw_buffer_load_b64(rx, ox0 + k, 0, 0)),
+                __builtin_bit_cast(float2, __builtin_amdgcn_raw_buffer_load_b64(rh, oh0 + k, 0, 0))};
+    };
+    auto sum = [](Raw r) -> float2 { return make_float2(r.a.x + r.b.x, r.a.y + r.b.y); };
     // taps arrive scaled by 1/M (firpfbch2.c:277-278's output scale, exact for M = 2^10)
     auto dot = [&](int newest, const float (&h)[L]) -> float2 {
         float2 acc = make_float2(0.f, 0.f);
@@ -243,24 +178,37 @@ __global__ __launch_bounds__(NT, 1) void k_pfb2_an1024(Params P, const float *__
     // warm-up: rows 8gs-8 .. 8gs-1 fill the ring; the last gives the hi-bin
     // half of block 16gs (hi lanes, even taps)
 #pragma unroll
-    for (int s = 0; s < NS; s++) w[s] = fetch(8 * gs - NS + s);
+    for (int s = 0; s < NS; s++) w[s] = sum(fetch(8 * gs - NS + s));
     int slot0 = (int)((16 * gs) % NBUF); // buffer of block 16g (advances by 16 mod 17 = -1)
     if (!lo) xb[slot0 * BSTR + j] = dot(NS - 1, tb);
     __syncthreads(); // twiddle tables ready
 
     // next iteration's first PF rows are prefetched into registers while the
     // FFTs run; the rest are fetched as the rows are consumed
-    float2 pf[PF];
+    Raw pf[PF];
 #pragma unroll
     for (int r = 0; r < PF; r++) pf[r] = fetch(8 * gs + r);
+    // Drain everything once before the loop: the loop header then merges an
+    // empty vector-memory queue with the loop's own steady state (prefetched
+    // rows, taps, then this wave's stores), and the compiler's vmcnt at the
+    // first use of a prefetched row leaves the stores in flight instead of
+    // waiting for the whole queue (vmcnt(0)) every iteration.
+    __builtin_amdgcn_s_waitcnt(0);
+
+    // outputs leave through a range-checked buffer descriptor over the call's
+    // nblk blocks: stores of blocks outside the call (b < B0 wraps to a huge
+    // unsigned offset) are dropped by the hardware, so the store path has no
+    // branch and every wave issues the same vector-memory sequence each
+    // iteration (the compiler's vmcnt bookkeeping stays exact, see below)
+    const __amdgpu_buffer_rsrc_t ry =
+        __builtin_amdgcn_make_buffer_rsrc((void *)P.Y, (short)0, (int)(P.nblk * M * 8), 0x00020000);
 
     for (long long g = gs; g < ge; g++) {
         const long long b0 = 16 * g;
-        if (!TRES) load_taps();
 #pragma unroll
         for (int r = 0; r < 8; r++) {
             // row c = 8g + r -> blocks b0 + 2r + dA (first), b0 + 2r + dA + 1 (second)
-            w[r] = r < PF ? pf[r] : fetch(8 * g + r);
+            w[r] = sum(r < PF ? pf[r] : fetch(8 * g + r));
             int s1 = slot0 + 2 * r + dA;
             s1 -= (s1 >= NBUF) ? NBUF : 0;
             int s2 = s1 + 1;
@@ -272,21 +220,10 @@ __global__ __launch_bounds__(NT, 1) void k_pfb2_an1024(Params P, const float *__
 #pragma unroll
             for (int r = 0; r < PF; r++) pf[r] = fetch(8 * (g + 1) + r);
         }
-        if (BAR) lds_barrier();
-        else __syncthreads();
+        lds_barrier();
 
         // ---- one 1024-point IFFT per wave: block b0 + wave
-        if (XMODE % 10 == 1) {
-            const long long b = b0 + wave;
-            int sb = slot0 + wave;
-            sb -= (sb >= NBUF) ? NBUF : 0;
-            float2 *B = xb + sb * BSTR;
-            if (b >= P.B0 && b < P.B0 + P.nblk) {
-                float2 *Yb = P.Y + (b - P.B0) * M;
-#pragma unroll
-                for (int r = 0; r < 16; r++) st_nt(Yb + lane + 64 * r, B[lane + 64 * r]);
-            }
-        } else if constexpr (FM == 1) {
+        {
             // 1024 = 16 x 16 x 4, every radix in registers with packed math:
             // DFT16 over k (j = lane + 64k), twiddle, transpose, DFT16 over a
             // (l = 4a + bq), twiddle, transpose, 4 x DFT4 over bq; the last
@@ -318,9 +255,7 @@ __global__ __launch_bounds__(NT, 1) void k_pfb2_an1024(Params P, const float *__
                 if ((r & 3) == 0) __builtin_amdgcn_sched_barrier(0);
                 v[r] = pk_cmul(v[r], pk(tw2[r * 4 + bq]));
             }
-            if (XMODE % 10 == 3) {
-                if (v[0].x == 12345.f && v[5].y == 3.f) P.Y[0] = unpk(v[3]);
-            } else if (b >= P.B0 && b < P.B0 + P.nblk) {
+            {
                 // C[k1][bq][r] at k1 + 16 r + 260 bq: the b64 writes of each
                 // 16-lane group hit 16 distinct bank pairs, the b128 reads below
                 // are conflict-free (MI355X_MICROARCH.md LDS table)
@@ -328,10 +263,16 @@ __global__ __launch_bounds__(NT, 1) void k_pfb2_an1024(Params P, const float *__
 #pragma unroll
                 for (int r = 0; r < 16; r++) B[k1 + 16 * r + 260 * bq] = unpk(v[r]);
                 lds_fence();
+                // The next iteration's taps are loaded here, BEFORE this wave's
+                // output stores: vmcnt counts stores too, so a tap load issued
+                // after them (at the top of the dot phase) would make the dot
+                // phase wait until every store of the block had drained.
+                load_taps();
+                __builtin_amdgcn_sched_barrier(0);
                 typedef float v4f __attribute__((ext_vector_type(4)));
                 // lane (t2, p2): bins k1 = 2 p2 + {0, 1}, r = t2 + 8u
                 const int t2 = lane >> 3, p2 = lane & 7;
-                v4f *Yb = reinterpret_cast<v4f *>(P.Y + (b - P.B0) * M + 2 * p2 + 16 * t2);
+                const unsigned yo = (unsigned)((b - P.B0) * (M * 8)) + (unsigned)(8 * (2 * p2 + 16 * t2));
 #pragma unroll
                 for (int u = 0; u < 2; u++) {
                     v4f c[4];
@@ -342,93 +283,17 @@ __global__ __launch_bounds__(NT, 1) void k_pfb2_an1024(Params P, const float *__
                     v2f e1[4] = {c[0].zw, c[1].zw, c[2].zw, c[3].zw};
                     pk_dft4<-1>(e0[0], e0[1], e0[2], e0[3]);
                     pk_dft4<-1>(e1[0], e1[1], e1[2], e1[3]);
-                    // Y[k1 + 16 r + 256 s]
+                    // Y[k1 + 16 r + 256 s], streaming (non-temporal) stores
 #pragma unroll
                     for (int sidx = 0; sidx < 4; sidx++) {
                         const v4f val = {e0[sidx].x, e0[sidx].y, e1[sidx].x, e1[sidx].y};
-                        __builtin_nontemporal_store(val, Yb + (128 * u + 256 * sidx) / 2);
-                    }
-                }
-            }
-        } else {
-            const long long b = b0 + wave;
-            int sb = slot0 + wave;
-            sb -= (sb >= NBUF) ? NBUF : 0;
-            float2 *B = xb + sb * BSTR;
-            float2 v[16];
-#pragma unroll
-            for (int k = 0; k < 16; k++) v[k] = B[lane + 64 * k];
-            dft16_bwd(v);
-            // twiddles in groups of four: bounds the loads in flight (VGPRs)
-#pragma unroll
-            for (int k1 = 1; k1 < 16; k1++) {
-                if ((k1 & 3) == 0) __builtin_amdgcn_sched_barrier(0);
-                v[k1] = cmul(v[k1], tw1[k1 * 64 + lane]);
-            }
-            lds_fence();
-#pragma unroll
-            for (int k1 = 0; k1 < 16; k1++) B[k1 * TSTR + lane] = v[k1];
-            lds_fence();
-            const int k1 = lane >> 2, bq = lane & 3;
-#pragma unroll
-            for (int a = 0; a < 16; a++) v[a] = B[k1 * TSTR + 4 * a + bq];
-            dft16_bwd(v);
-#pragma unroll
-            for (int r = 1; r < 16; r++) {
-                if ((r & 3) == 0) __builtin_amdgcn_sched_barrier(0);
-                v[r] = cmul(v[r], tw2[r * 4 + bq]);
-            }
-            // 4-point DFT over bq across the lane quad (radix-2 x 2):
-            // stage 1 pairs bq, bq^2; twiddle W4^{+1} on bq=3; stage 2 pairs bq, bq^1
-            // butterflies as p + sign * own (one fma per component instead of
-            // both sum and difference plus a select)
-            const float sg2 = (bq & 2) ? -1.0f : 1.0f, sg1 = (bq & 1) ? -1.0f : 1.0f;
-#pragma unroll
-            for (int r = 0; r < 16; r++) {
-                const float2 p = quad_xor<2>(v[r]);
-                float2 u = make_float2(fmaf(sg2, v[r].x, p.x), fmaf(sg2, v[r].y, p.y));
-                if (bq == 3) u = cmul_pj(u);
-                const float2 p2 = quad_xor<1>(u);
-                v[r] = make_float2(fmaf(sg1, u.x, p2.x), fmaf(sg1, u.y, p2.y));
-            }
-            // lane (k1, bq) holds Y[k1 + 16 r + 256 s], s = bitrev2(bq)
-            if (XMODE % 10 == 3) {
-                if (v[0].x == 12345.f && v[5].y == 3.f) P.Y[0] = v[3];
-            } else if (b >= P.B0 && b < P.B0 + P.nblk) {
-                const int s = ((bq & 1) << 1) | (bq >> 1);
-                if constexpr (SMODE < 2) {
-                    float2 *Yb = P.Y + (b - P.B0) * M + k1 + 256 * s;
-#pragma unroll
-                    for (int r = 0; r < 16; r++) {
-                        if (SMODE == 0) st_nt(Yb + 16 * r, v[r]);
-                        else Yb[16 * r] = v[r];
-                    }
-                } else {
-                    // natural order in LDS, 4 pad slots per 256 (ds_write_b64
-                    // conflict-free), then whole 16-byte pairs per lane
-                    lds_fence();
-#pragma unroll
-                    for (int r = 0; r < 16; r++) B[k1 + 16 * r + 260 * s] = v[r];
-                    lds_fence();
-                    typedef float v4f __attribute__((ext_vector_type(4)));
-                    v4f *Yb = reinterpret_cast<v4f *>(P.Y + (b - P.B0) * M);
-#pragma unroll
-                    for (int q = 0; q < 8; q++) {
-                        const int o = 2 * (lane + 64 * q);
-                        const v4f val = *reinterpret_cast<const v4f *>(B + o + 4 * (o >> 8));
-                        if (SMODE == 2) __builtin_nontemporal_store(val, Yb + (o >> 1));
-                        else Yb[o >> 1] = val;
+                        __builtin_amdgcn_raw_buffer_store_b128(val, ry, yo + 8 * (128 * u + 256 * sidx), 0, 2);
                     }
                 }
             }
         }
         slot0 = slot0 == 0 ? NBUF - 1 : slot0 - 1; // (16(g+1)) mod 17
-        if (BAR) lds_barrier();
-        else __syncthreads();
-    }
-    if (XMODE >= 10 && tid == 0 && blockIdx.x < 1024) {
-        g_pfb2_clk[2 * blockIdx.x] = __builtin_amdgcn_s_memtime() - clk0;
-        g_pfb2_clk[2 * blockIdx.x + 1] = __builtin_amdgcn_s_memrealtime() - rt0;
+        lds_barrier();
     }
 }
 

@@ -21,33 +21,22 @@ extern "C" const float *lqrt_twiddles(void) { return (const float *)g_tw; }
 extern "C" void lqk_fft_batch(unsigned int, int, const void *, void *, unsigned long long, void *) {}
 extern "C" void lqk_fft_batch_scaled(unsigned int, int, const void *, void *, unsigned long long, float, float, void *) {}
 
-template <int X, int SM = 2, int PF = 4, int BAR = 1, int TRES = 0, int FM = 1>
+template <int PF>
 static void run(const char *name, Params P, const float *hsub, unsigned nwg, int iters)
 {
     hipEvent_t e0, e1;
     LQ_CHECK(hipEventCreate(&e0));
     LQ_CHECK(hipEventCreate(&e1));
-    hipLaunchKernelGGL((k_pfb2_an1024<8, X, SM, PF, BAR, TRES, FM>), dim3(nwg), dim3(NT), 0, 0, P, hsub, g_tw);
+    hipLaunchKernelGGL((k_pfb2_an1024<8, PF>), dim3(nwg), dim3(NT), 0, 0, P, hsub, g_tw);
     LQ_CHECK(hipEventRecord(e0));
-    for (int i = 0; i < iters; i++) hipLaunchKernelGGL((k_pfb2_an1024<8, X, SM, PF, BAR, TRES, FM>), dim3(nwg), dim3(NT), 0, 0, P, hsub, g_tw);
+    for (int i = 0; i < iters; i++) hipLaunchKernelGGL((k_pfb2_an1024<8, PF>), dim3(nwg), dim3(NT), 0, 0, P, hsub, g_tw);
     LQ_CHECK(hipEventRecord(e1));
     LQ_CHECK(hipEventSynchronize(e1));
     float ms;
     LQ_CHECK(hipEventElapsedTime(&ms, e0, e1));
     ms /= iters;
     const double n = (double)P.n_in;
-    printf("%-28s %8.3f ms  %7.1f GS/s  %6.0f GB/s", name, ms, n / (ms * 1e-3) / 1e9, 24.0 * n / (ms * 1e-3) / 1e9);
-    if (X >= 10) {
-        std::vector<unsigned long long> c(2 * nwg);
-        LQ_CHECK(hipMemcpyFromSymbol(c.data(), HIP_SYMBOL(g_pfb2_clk), c.size() * 8));
-        double cy = 0, rt = 0;
-        for (unsigned i = 0; i < nwg; i++) {
-            cy += c[2 * i];
-            rt += c[2 * i + 1];
-        }
-        printf("  clock %.3f GHz", cy / rt * 0.1);
-    }
-    printf("\n");
+    printf("%-28s %8.3f ms  %7.1f GS/s  %6.0f GB/s\n", name, ms, n / (ms * 1e-3) / 1e9, 24.0 * n / (ms * 1e-3) / 1e9);
     fflush(stdout);
 }
 
@@ -109,30 +98,16 @@ int main()
     P.gpw = (int)gpw;
     P.gend = ngroups;
     const int it = 10;
-    for (int rep = 0; rep < 2; rep++) run<10, 2, 6, 1, 0, 1>("warm", P, hsub, nwg, it);
-    // outputs of the two transform modes must agree
-    std::vector<float2> ya(nb * M), yb(nb * M);
-    run<0, 2, 6, 1, 0, 0>("FM0 (dpp quad)", P, hsub, nwg, 1);
-    LQ_CHECK(hipMemcpy(ya.data(), y, nb * M * 8, hipMemcpyDeviceToHost));
-    LQ_CHECK(hipMemset(y, 0, nb * M * 8));
-    run<0, 2, 6, 1, 0, 1>("FM1 (packed 16x16x4)", P, hsub, nwg, 1);
-    LQ_CHECK(hipMemcpy(yb.data(), y, nb * M * 8, hipMemcpyDeviceToHost));
-    double md = 0, mx = 0;
-    for (long long i = 0; i < nb * M; i++) {
-        md = fmax(md, fmax(fabs(ya[i].x - yb[i].x), fabs(ya[i].y - yb[i].y)));
-        mx = fmax(mx, fmax(fabs(ya[i].x), fabs(ya[i].y)));
-    }
-    printf("FM0 vs FM1: max|d| %.3e  max|y| %.3e  rel %.3e\n", md, mx, md / mx);
-    // segment-size aliasing check: 64 groups per workgroup (power-of-two
-    // segments, 256 WGs) against 65 / 63 groups
     for (int rep = 0; rep < 3; rep++) {
-        for (int g : {64, 65, 63, 66}) {
+        run<8>("library PF8", P, hsub, nwg, it);
+        run<6>("PF6", P, hsub, nwg, it);
+        for (int g : {64, 65}) {
             Params Q = P;
             Q.gpw = g;
             const unsigned nw = (unsigned)((ngroups + g - 1) / g);
             char nm[64];
             snprintf(nm, sizeof nm, "gpw %d (%u WGs)", g, nw);
-            run<10, 2, 8, 1, 0, 1>(nm, Q, hsub, nw, it);
+            run<8>(nm, Q, hsub, nw, it);
         }
     }
     return 0;

@@ -10,6 +10,67 @@
 
 namespace {
 
+// helpers of the scalar transform form (moved out of the library kernel)
+// cos/sin(2 pi e / 16), e = 0..15
+__device__ constexpr float C16[16] = {1.0f,         0.92387953f,  0.70710678f,  0.38268343f,
+                                      0.0f,         -0.38268343f, -0.70710678f, -0.92387953f,
+                                      -1.0f,        -0.92387953f, -0.70710678f, -0.38268343f,
+                                      0.0f,         0.38268343f,  0.70710678f,  0.92387953f};
+__device__ constexpr float S16[16] = {0.0f,         0.38268343f,  0.70710678f,  0.92387953f,
+                                      1.0f,         0.92387953f,  0.70710678f,  0.38268343f,
+                                      0.0f,         -0.38268343f, -0.70710678f, -0.92387953f,
+                                      -1.0f,        -0.92387953f, -0.70710678f, -0.38268343f};
+
+// 16-point backward DFT (e^{+j2pi nk/16}) in registers, natural order in/out.
+__device__ __forceinline__ void dft16_bwd(float2 (&v)[16])
+{
+    float2 t[16];
+#pragma unroll
+    for (int q = 0; q < 4; q++) {
+        float2 a0 = v[q], a1 = v[4 + q], a2 = v[8 + q], a3 = v[12 + q];
+        dft4(a0, a1, a2, a3, -1);
+        // twiddle W16^{+q k0}
+        t[0 * 4 + q] = a0;
+        if (q == 0) {
+            t[1 * 4 + q] = a1;
+            t[2 * 4 + q] = a2;
+            t[3 * 4 + q] = a3;
+        } else {
+            t[1 * 4 + q] = cmul(a1, make_float2(C16[(1 * q) & 15], S16[(1 * q) & 15]));
+            t[2 * 4 + q] = cmul(a2, make_float2(C16[(2 * q) & 15], S16[(2 * q) & 15]));
+            t[3 * 4 + q] = cmul(a3, make_float2(C16[(3 * q) & 15], S16[(3 * q) & 15]));
+        }
+    }
+#pragma unroll
+    for (int k0 = 0; k0 < 4; k0++) {
+        float2 b0 = t[k0 * 4 + 0], b1 = t[k0 * 4 + 1], b2 = t[k0 * 4 + 2], b3 = t[k0 * 4 + 3];
+        dft4(b0, b1, b2, b3, -1);
+        v[k0 + 0] = b0;
+        v[k0 + 4] = b1;
+        v[k0 + 8] = b2;
+        v[k0 + 12] = b3;
+    }
+}
+
+// exchange with the partner lane inside a quad through DPP (a VALU operand
+// modifier, no LDS crossbar): quad_perm [1,0,3,2] for xor 1, [2,3,0,1] for xor 2
+template <int X>
+__device__ __forceinline__ float2 quad_xor(float2 v)
+{
+    constexpr int ctrl = X == 1 ? 0xB1 : 0x4E;
+    const int a = __builtin_amdgcn_mov_dpp(__float_as_int(v.x), ctrl, 0xF, 0xF, false);
+    const int b = __builtin_amdgcn_mov_dpp(__float_as_int(v.y), ctrl, 0xF, 0xF, false);
+    return make_float2(__int_as_float(a), __int_as_float(b));
+}
+
+// streaming (non-temporal) store of one complex sample: output is written once
+__device__ __forceinline__ void st_nt(float2 *p, float2 v)
+{
+    v2f w = {v.x, v.y};
+    __builtin_nontemporal_store(w, reinterpret_cast<v2f *>(p));
+}
+
+
 // one 1024-point IFFT of the block in LDS buffer B by one wave, natural-order
 // result through B into 16-byte non-temporal stores (the SMODE 2 path above)
 __device__ __forceinline__ void fft1024_store(float2 *B, long long b, const Params &P, int lane,
