@@ -461,11 +461,20 @@ def percall_baseline():
         out = subprocess.run([exe, "--runtime", "0.25"] + names, capture_output=True, text=True, timeout=240)
     except subprocess.TimeoutExpired:
         return {"error": "timeout"}
+    # the reference's own `make bench` rates for the same bodies, one core of
+    # the survey container (trials/s)
+    ref = {"firfilt_crcf_64": 35.4e6, "dotprod_crcf_64": 62.7e6, "dotprod_cccf_64": 38.4e6,
+           "firpfbch2_crcf_a1024": 41.5e3, "firpfbch_crcf_a1024": 31.1e3, "resamp_crcf_m8": 17.8e6,
+           "firdecim_crcf_m8_h32": 22.4e6, "firinterp_crcf_m8_h32": 10.6e6, "fftfilt_crcf_64": 25.5e6}
     res = {}
     for line in out.stdout.splitlines():
         if line.startswith("{"):
             d = json.loads(line)
-            res[d.pop("name")] = d
+            name = d.pop("name")
+            if name in ref and d.get("trials_per_s"):
+                d["reference_trials_per_s"] = ref[name]
+                d["vs_reference"] = d["trials_per_s"] / ref[name]
+            res[name] = d
     if out.returncode != 0:
         res["error"] = "exit %d: %s" % (out.returncode, out.stderr[-300:])
     return res

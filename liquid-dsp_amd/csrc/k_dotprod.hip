@@ -174,6 +174,61 @@ void launch(const void *h, unsigned n, const void *X, long long stride, long lon
 
 } // namespace
 
+// one vector, 256 lanes, result straight to pinned host memory + completion
+// flag: the per-call dotprod_*_execute() (one launch, no stream sync)
+template <int KIND>
+__global__ __launch_bounds__(256) void k_dot_single(const float *__restrict__ h, int n, const float *__restrict__ x,
+                                                    float *y, unsigned *flag, unsigned seq)
+{
+    typedef typename dp<KIND>::acc_t A;
+    __shared__ A part[256];
+    A acc{};
+    for (int i = threadIdx.x; i < n; i += 256) {
+        if constexpr (KIND == 0) {
+            acc = fmaf(h[i], x[i], acc);
+        } else if constexpr (KIND == 1) {
+            const float hv = h[i];
+            acc.x = fmaf(hv, x[2 * i], acc.x);
+            acc.y = fmaf(hv, x[2 * i + 1], acc.y);
+        } else {
+            const float hr = h[2 * i], hi = h[2 * i + 1], xr = x[2 * i], xi = x[2 * i + 1];
+            acc.x = fmaf(-hi, xi, fmaf(hr, xr, acc.x));
+            acc.y = fmaf(hi, xr, fmaf(hr, xi, acc.y));
+        }
+    }
+    part[threadIdx.x] = acc;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        A s{};
+        for (int t = 0; t < 256; t++) {
+            if constexpr (KIND == 0) s += part[t];
+            else s = make_float2(s.x + part[t].x, s.y + part[t].y);
+        }
+        if constexpr (KIND == 0) y[0] = s;
+        else {
+            y[0] = s.x;
+            y[1] = s.y;
+        }
+        lq_signal(flag, seq);
+    }
+}
+
+extern "C" void lqk_dotprod_single(int kind, const void *h, unsigned int n, const void *x, void *y, unsigned *flag,
+                                   unsigned seq, void *stream)
+{
+    hipStream_t st = (hipStream_t)stream;
+    const float *hf = (const float *)h, *xf = (const float *)x;
+    switch (kind) {
+    case 0: hipLaunchKernelGGL(k_dot_single<0>, dim3(1), dim3(256), 0, st, hf, (int)n, xf, (float *)y, flag, seq); break;
+    case 1: hipLaunchKernelGGL(k_dot_single<1>, dim3(1), dim3(256), 0, st, hf, (int)n, xf, (float *)y, flag, seq); break;
+    case 2: hipLaunchKernelGGL(k_dot_single<2>, dim3(1), dim3(256), 0, st, hf, (int)n, xf, (float *)y, flag, seq); break;
+    default:
+        fprintf(stderr, "error: dotprod: invalid kind %d\n", kind);
+        exit(1);
+    }
+    LQ_CHECK_LAUNCH();
+}
+
 extern "C" void lqk_dotprod_batch(int kind, const void *h, unsigned int n, const void *X, unsigned long long stride,
                                   unsigned long long nvec, void *Y, void *stream)
 {

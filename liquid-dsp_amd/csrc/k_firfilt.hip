@@ -256,7 +256,7 @@ __global__ __launch_bounds__(NT) void k_firfilt(const typename kt<KIND>::T *__re
 template <int KIND>
 __global__ void k_firpfb_single(const typename kt<KIND>::TC *__restrict__ hpoly, int L, int i,
                                 const typename kt<KIND>::T *__restrict__ win, float sre, float sim,
-                                typename kt<KIND>::T *y)
+                                typename kt<KIND>::T *y, unsigned *flag, unsigned seq)
 {
     typedef typename kt<KIND>::T T;
     __shared__ T part[64];
@@ -268,6 +268,7 @@ __global__ void k_firpfb_single(const typename kt<KIND>::TC *__restrict__ hpoly,
         T s = zero<T>();
         for (int t = 0; t < 64; t++) s = vadd(s, part[t]);
         y[0] = oscale<KIND>(s, sre, sim);
+        lq_signal(flag, seq);
     }
 }
 
@@ -300,7 +301,7 @@ __global__ void k_window_append(const T *__restrict__ src, int L, const T *__res
 template <int KIND>
 __global__ void k_fir_single(const typename kt<KIND>::TC *__restrict__ hpad, int HP, int hlen,
                              const typename kt<KIND>::T *__restrict__ win, float sre, float sim,
-                             typename kt<KIND>::T *y)
+                             typename kt<KIND>::T *y, unsigned *flag, unsigned seq)
 {
     typedef typename kt<KIND>::T T;
     __shared__ T part[64];
@@ -312,6 +313,7 @@ __global__ void k_fir_single(const typename kt<KIND>::TC *__restrict__ hpad, int
         T s = zero<T>();
         for (int i = 0; i < 64; i++) s = vadd(s, part[i]);
         y[0] = oscale<KIND>(s, sre, sim);
+        lq_signal(flag, seq);
     }
 }
 
@@ -636,22 +638,23 @@ extern "C" void lqk_window_append(int is_complex, const void *src_hist, unsigned
     LQ_CHECK_LAUNCH();
 }
 
-extern "C" void lqk_fir_single(const lqk_fir_desc *d, const void *win, void *y, void *stream)
+extern "C" void lqk_fir_single(const lqk_fir_desc *d, const void *win, void *y, unsigned *flag, unsigned seq,
+                               void *stream)
 {
     hipStream_t st = (hipStream_t)stream;
     const int HP = (int)(d->hc * d->nchunk);
     switch (d->kind) {
     case 0:
         hipLaunchKernelGGL(k_fir_single<0>, dim3(1), dim3(64), 0, st, (const float *)d->hpad, HP, (int)d->hlen,
-                           (const float *)win, d->scale_re, d->scale_im, (float *)y);
+                           (const float *)win, d->scale_re, d->scale_im, (float *)y, flag, seq);
         break;
     case 1:
         hipLaunchKernelGGL(k_fir_single<1>, dim3(1), dim3(64), 0, st, (const float *)d->hpad, HP, (int)d->hlen,
-                           (const float2 *)win, d->scale_re, d->scale_im, (float2 *)y);
+                           (const float2 *)win, d->scale_re, d->scale_im, (float2 *)y, flag, seq);
         break;
     case 2:
         hipLaunchKernelGGL(k_fir_single<2>, dim3(1), dim3(64), 0, st, (const float2 *)d->hpad, HP, (int)d->hlen,
-                           (const float2 *)win, d->scale_re, d->scale_im, (float2 *)y);
+                           (const float2 *)win, d->scale_re, d->scale_im, (float2 *)y, flag, seq);
         break;
     }
     LQ_CHECK_LAUNCH();
@@ -804,21 +807,21 @@ extern "C" void lqk_firinterp(int kind, const void *hpoly, unsigned int M, unsig
 }
 
 extern "C" void lqk_firpfb_single(int kind, const void *hpoly, unsigned int L, unsigned int i, const void *win,
-                                  float sre, float sim, void *y, void *stream)
+                                  float sre, float sim, void *y, unsigned *flag, unsigned seq, void *stream)
 {
     hipStream_t st = (hipStream_t)stream;
     switch (kind) {
     case 0:
         hipLaunchKernelGGL(k_firpfb_single<0>, dim3(1), dim3(64), 0, st, (const float *)hpoly, (int)L, (int)i,
-                           (const float *)win, sre, sim, (float *)y);
+                           (const float *)win, sre, sim, (float *)y, flag, seq);
         break;
     case 1:
         hipLaunchKernelGGL(k_firpfb_single<1>, dim3(1), dim3(64), 0, st, (const float *)hpoly, (int)L, (int)i,
-                           (const float2 *)win, sre, sim, (float2 *)y);
+                           (const float2 *)win, sre, sim, (float2 *)y, flag, seq);
         break;
     case 2:
         hipLaunchKernelGGL(k_firpfb_single<2>, dim3(1), dim3(64), 0, st, (const float2 *)hpoly, (int)L, (int)i,
-                           (const float2 *)win, sre, sim, (float2 *)y);
+                           (const float2 *)win, sre, sim, (float2 *)y, flag, seq);
         break;
     }
     LQ_CHECK_LAUNCH();

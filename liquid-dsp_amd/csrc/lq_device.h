@@ -11,6 +11,16 @@ void lq_check(hipError_t e, const char *what, const char *file, int line);
 
 #define LQ_TW_N 4096
 
+// Small-call completion (lq_runtime.hip): after this thread's result stores,
+// release them at system scope and raise the host's pinned flag word.  A
+// null flag (device-resident calls) does nothing.
+__device__ __forceinline__ void lq_signal(unsigned *flag, unsigned seq)
+{
+    if (flag == nullptr) return;
+    __threadfence_system();
+    __hip_atomic_store(flag, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
 __device__ __forceinline__ float2 cadd(float2 a, float2 b) { return make_float2(a.x + b.x, a.y + b.y); }
 __device__ __forceinline__ float2 csub(float2 a, float2 b) { return make_float2(a.x - b.x, a.y - b.y); }
 __device__ __forceinline__ float2 cmul(float2 a, float2 b)

@@ -31,11 +31,23 @@ void   lqrt_sync(void *stream);
 void   lqrt_device_sync(void);
 int    lqrt_is_device_ptr(const void *p);
 const float *lqrt_twiddles(void);               /* W_4096^e = exp(-2 pi i e/4096), e<4096 */
+/* small-call completion: one kernel copies `bytes` (a multiple of 4, at most
+ * LQRT_COPYOUT_MAX) from device memory src to pinned host memory dst, makes
+ * them visible system-wide and then stores `seq` to the pinned word *flag;
+ * lqrt_wait_flag spins until it sees seq (then falls back to a stream sync,
+ * which also reports a kernel fault). */
+#define LQRT_COPYOUT_MAX (64u << 10)
+void   lqrt_copyout_signal(const void *src, void *dst, size_t bytes, unsigned *flag, unsigned seq, void *stream);
+void   lqrt_wait_flag(const unsigned *flag, unsigned seq, void *stream);
 
 /* ---------------------------------------------------------------- dotprod
  * Y[v] = sum_i h[i] X[v*stride + i], v < nvec.  kind: 0 rrrf, 1 crcf, 2 cccf */
 void lqk_dotprod_batch(int kind, const void *h, unsigned int n, const void *X,
                        unsigned long long stride, unsigned long long nvec, void *Y, void *stream);
+/* one dot product (dotprod_*_execute): x may be pinned host memory, y is
+ * pinned host memory, *flag = seq is raised once y is visible to the host */
+void lqk_dotprod_single(int kind, const void *h, unsigned int n, const void *x, void *y, unsigned *flag,
+                        unsigned seq, void *stream);
 
 /* ---------------------------------------------------------------- firfilt
  * Streaming FIR: y[i] = scale * sum_{k<hlen} h[k] ext[i-k], where ext[t] = x[t]
@@ -67,8 +79,10 @@ void lqk_window_append(int is_complex, const void *src_hist, unsigned int L, con
                        unsigned long long n, void *dst_hist, void *stream);
 
 /* one output of a dot product of hr (reversed coefficients, hlen) against
- * win (oldest first), times scale: the per-sample firfilt_execute() path */
-void lqk_fir_single(const lqk_fir_desc *d, const void *win, void *y, void *stream);
+ * win (oldest first), times scale: the per-sample firfilt_execute() path.
+ * With a flag, y is pinned host memory and the kernel raises *flag = seq
+ * once y is visible to the host (see lqrt_wait_flag); flag may be NULL. */
+void lqk_fir_single(const lqk_fir_desc *d, const void *win, void *y, unsigned *flag, unsigned seq, void *stream);
 
 /* ---------------------------------------------------------------- firdecim / firinterp
  * decim: y[o] = sum_k h[k] ext[o*M + phase - k]  (o < nout)
@@ -167,7 +181,7 @@ void lqk_resamp(int real_io, const lqk_rs_plan *pl, unsigned long long g0, unsig
  * npfb the BOUNDARY pair (h_{npfb-1}[L-1-p], h_0[L-p]); zero elsewhere (NULL: untiled kernel) */
 /* firpfb_execute(i): y = scale * sum_n hpoly[i*L + n] win[L-1-n] (win: L samples, oldest first) */
 void lqk_firpfb_single(int kind, const void *hpoly, unsigned int L, unsigned int i, const void *win,
-                       float scale_re, float scale_im, void *y, void *stream);
+                       float scale_re, float scale_im, void *y, unsigned *flag, unsigned seq, void *stream);
 
 /* ---------------------------------------------------------------- FFT of any size (csrc/k_fft.hip)
  * batch transforms of n points (complex, contiguous), dir +1 forward / -1

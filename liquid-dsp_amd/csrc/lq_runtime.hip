@@ -149,6 +149,52 @@ extern "C" const float *lqrt_twiddles(void)
     return tables[dev];
 }
 
+// ------------------------------------------------------------ small calls
+// The per-call liquid.h API (firfilt_execute, dotprod_execute,
+// firpfbch2_execute ...) returns only after its result is in host memory.
+// A stream synchronisation costs about 5 us on top of the kernels
+// (tools/mb/mb_latency.hip); instead the last kernel of a call copies the
+// result into pinned host memory, releases it at system scope and raises a
+// per-object flag word the host spins on.
+__global__ __launch_bounds__(256) void k_copyout_signal(const unsigned *__restrict__ src, unsigned *dst,
+                                                        unsigned nw, unsigned *flag, unsigned seq)
+{
+    const unsigned n4 = nw >> 2;
+    const uint4 *s4 = reinterpret_cast<const uint4 *>(src);
+    uint4 *d4 = reinterpret_cast<uint4 *>(dst);
+    for (unsigned i = threadIdx.x; i < n4; i += 256) d4[i] = s4[i];
+    for (unsigned i = 4 * n4 + threadIdx.x; i < nw; i += 256) dst[i] = src[i];
+    __threadfence_system();
+    __syncthreads();
+    if (threadIdx.x == 0) __hip_atomic_store(flag, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+extern "C" void lqrt_copyout_signal(const void *src, void *dst, size_t bytes, unsigned *flag, unsigned seq,
+                                    void *stream)
+{
+    if (bytes > LQRT_COPYOUT_MAX || (bytes & 3) || ((uintptr_t)src & 15) || ((uintptr_t)dst & 15)) {
+        fprintf(stderr, "error: liquid-mi355x: copy-out of %zu bytes out of contract\n", bytes);
+        exit(1);
+    }
+    hipLaunchKernelGGL(k_copyout_signal, dim3(1), dim3(256), 0, (hipStream_t)stream, (const unsigned *)src,
+                       (unsigned *)dst, (unsigned)(bytes >> 2), flag, seq);
+    LQ_CHECK(hipGetLastError());
+}
+
+extern "C" void lqrt_wait_flag(const unsigned *flag, unsigned seq, void *stream)
+{
+    // spin for up to ~2 ms (a small call takes ~10 us), then block on the stream
+    for (long i = 0; i < (1L << 21); i++) {
+        if (__atomic_load_n(flag, __ATOMIC_ACQUIRE) == seq) return;
+        __builtin_ia32_pause();
+    }
+    LQ_CHECK(hipStreamSynchronize((hipStream_t)stream));
+    if (__atomic_load_n(flag, __ATOMIC_ACQUIRE) != seq) {
+        fprintf(stderr, "error: liquid-mi355x: small-call completion flag not raised\n");
+        exit(1);
+    }
+}
+
 extern "C" void lqrt_device_sync(void)
 {
     LQ_CHECK(hipDeviceSynchronize());

@@ -82,12 +82,21 @@ void lq_dotprod_execute_batch(lq_dotprod *q, const void *X, unsigned long long n
 {
     if (nvec == 0) return;
     size_t xb = (size_t)nvec * q->n * q->esz, yb = (size_t)nvec * q->esz;
-    void *dX = lq_devbuf_get(&q->xbuf, xb ? xb : 16);
+    const void *dX = lq_call_in(&q->ctx, &q->xbuf, X, xb);
     void *dY = lq_devbuf_get(&q->ybuf, yb);
-    lqrt_h2d(dX, X, xb, q->ctx.stream);
     lq_dotprod_execute_batch_dev(q, dX, nvec, dY);
-    lqrt_d2h(Y, dY, yb, q->ctx.stream);
-    lqrt_sync(q->ctx.stream);
+    lq_call_out(&q->ctx, Y, dY, yb);
+}
+
+/* one dot product (the reference's dotprod_*_execute): x staged in pinned
+ * memory, one kernel writes the pinned result and raises the flag */
+static void lq_dotprod_execute1(lq_dotprod *q, const void *x, void *y)
+{
+    const void *dx = lq_call_in(&q->ctx, &q->xbuf, x, (size_t)q->n * q->esz);
+    unsigned *flag, seq;
+    void *py = lq_sig_out(&q->ctx, q->esz, &flag, &seq);
+    lqk_dotprod_single(q->kind, q->d_h, q->n, dx, py, flag, seq, q->ctx.stream);
+    lq_sig_wait(&q->ctx, y, q->esz, seq);
 }
 
 lq_ctx *lq_dotprod_ctx(lq_dotprod *q) { return &q->ctx; }
@@ -128,7 +137,7 @@ void lq_dotprod_run(int kind, const float *h, const void *x, unsigned int n, voi
         free(_q);                                                                                   \
     }                                                                                               \
     void NAME##_print(NAME _q) { lq_dotprod_print(_q->d); }                                         \
-    void NAME##_execute(NAME _q, TI *_v, TO *_y) { lq_dotprod_execute_batch(_q->d, _v, 1, _y); }    \
+    void NAME##_execute(NAME _q, TI *_v, TO *_y) { lq_dotprod_execute1(_q->d, _v, _y); }           \
     void NAME##_execute_batch(NAME _q, TI *_X, unsigned long long _nvec, TO *_Y)                    \
     {                                                                                               \
         lq_dotprod_execute_batch(_q->d, _X, _nvec, _Y);                                             \

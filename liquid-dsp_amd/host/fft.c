@@ -101,11 +101,10 @@ void fft_execute_batch(fftplan _p, const void *_x, void *_y, unsigned long long 
 {
     if (_batch == 0) return;
     const size_t bytes = (size_t)_p->n * _batch * (_p->r2r ? 4 : 8);
+    const void *dx = lq_call_in(&_p->ctx, &_p->dx, _x, bytes);
     void *d = lq_devbuf_get(&_p->dx, bytes);
-    lqrt_h2d(d, _x, bytes, _p->ctx.stream);
-    fft_execute_batch_dev(_p, d, d, _batch);
-    lqrt_d2h(_y, d, bytes, _p->ctx.stream);
-    lqrt_sync(_p->ctx.stream);
+    fft_execute_batch_dev(_p, dx, d, _batch);
+    lq_call_out(&_p->ctx, _y, d, bytes);
 }
 
 void fft_execute(fftplan _p) { fft_execute_batch(_p, _p->x, _p->y, 1); }

@@ -120,12 +120,10 @@ static void lq_fftf_block(lq_fftf *q, const void *x, unsigned long long n, void 
 {
     if (n == 0) return;
     size_t bytes = (size_t)n * q->esz;
-    void *dx = lq_devbuf_get(&q->xbuf, bytes);
+    const void *dx = lq_call_in(&q->ctx, &q->xbuf, x, bytes);
     void *dy = lq_devbuf_get(&q->ybuf, bytes);
-    lqrt_h2d(dx, x, bytes, q->ctx.stream);
     lq_fftf_block_dev(q, dx, n, dy);
-    lqrt_d2h(y, dy, bytes, q->ctx.stream);
-    lqrt_sync(q->ctx.stream);
+    lq_call_out(&q->ctx, y, dy, bytes);
 }
 
 #define LQ_FFTFILT_FRONT(NAME, KIND, TO, TC, TI, SRE, SIM)                                          \

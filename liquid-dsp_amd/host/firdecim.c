@@ -134,12 +134,10 @@ static void lq_decim_block(lq_decim *q, const void *x, unsigned long long nout, 
 {
     if (nout == 0) return;
     size_t nin = (size_t)nout * q->M * q->esz, nb = (size_t)nout * q->esz;
-    void *dx = lq_devbuf_get(&q->xbuf, nin);
+    const void *dx = lq_call_in(&q->ctx, &q->xbuf, x, nin);
     void *dy = lq_devbuf_get(&q->ybuf, nb);
-    lqrt_h2d(dx, x, nin, q->ctx.stream);
     lq_decim_block_dev(q, dx, nout, dy);
-    lqrt_d2h(y, dy, nb, q->ctx.stream);
-    lqrt_sync(q->ctx.stream);
+    lq_call_out(&q->ctx, y, dy, nb);
 }
 
 #define LQ_FIRDECIM_FRONT(NAME, KIND, TO, TC, TI)                                                   \
@@ -302,12 +300,10 @@ static void lq_interp_block(lq_interp *q, const void *x, unsigned long long n, v
 {
     if (n == 0) return;
     size_t nin = (size_t)n * q->esz, nout = (size_t)n * q->M * q->esz;
-    void *dx = lq_devbuf_get(&q->xbuf, nin);
+    const void *dx = lq_call_in(&q->ctx, &q->xbuf, x, nin);
     void *dy = lq_devbuf_get(&q->ybuf, nout);
-    lqrt_h2d(dx, x, nin, q->ctx.stream);
     lq_interp_block_dev(q, dx, n, dy);
-    lqrt_d2h(y, dy, nout, q->ctx.stream);
-    lqrt_sync(q->ctx.stream);
+    lq_call_out(&q->ctx, y, dy, nout);
 }
 
 #define LQ_FIRINTERP_FRONT(NAME, KIND, TO, TC, TI)                                                  \

@@ -56,7 +56,9 @@ static void lq_firfilt_alloc_state(lq_firfilt *q)
     q->d_hpad = lqrt_malloc((size_t)q->HP * q->csz);
     q->d_win[0] = lqrt_malloc((size_t)q->HP * q->esz);
     q->d_win[1] = lqrt_malloc((size_t)q->HP * q->esz);
-    q->h_win = (unsigned char *)lq_xmalloc((size_t)q->HP * q->esz);
+    /* pinned: the per-sample execute() reads it in place (zero copy) */
+    q->h_win = (unsigned char *)lqrt_host_alloc((size_t)q->HP * q->esz);
+    memset(q->h_win, 0, (size_t)q->HP * q->esz);
     q->cur = 0;
     q->host_valid = q->dev_valid = 1;
 }
@@ -66,7 +68,7 @@ static void lq_firfilt_free_state(lq_firfilt *q)
     lqrt_free(q->d_hpad);
     lqrt_free(q->d_win[0]);
     lqrt_free(q->d_win[1]);
-    free(q->h_win);
+    lqrt_host_free(q->h_win);
 }
 
 static void lq_firfilt_upload_coefs(lq_firfilt *q)
@@ -195,13 +197,18 @@ void lq_firfilt_push(lq_firfilt *q, const void *x)
     q->dev_valid = 0;
 }
 
+/* one output from the current window: the kernel reads the window where it
+ * is authoritative -- in place from the pinned host mirror after push()es,
+ * or the device copy after a device block -- and writes the result to
+ * pinned host memory and raises the completion flag itself (one launch, no
+ * stream sync) */
 void lq_firfilt_execute(lq_firfilt *q, void *y)
 {
-    lq_firfilt_need_dev(q);
-    void *dy = lq_devbuf_get(&q->one, 16);
-    lqk_fir_single(&q->d, q->d_win[q->cur], dy, q->ctx.stream);
-    lqrt_d2h(y, dy, q->esz, q->ctx.stream);
-    lqrt_sync(q->ctx.stream);
+    const void *win = q->dev_valid ? q->d_win[q->cur] : (const void *)q->h_win;
+    unsigned *flag, seq;
+    void *py = lq_sig_out(&q->ctx, q->esz, &flag, &seq);
+    lqk_fir_single(&q->d, win, py, flag, seq, q->ctx.stream);
+    lq_sig_wait(&q->ctx, y, q->esz, seq);
 }
 
 /* device-resident block: window update first (reads x before an in-place
@@ -224,12 +231,10 @@ void lq_firfilt_execute_block(lq_firfilt *q, const void *x, unsigned long long n
 {
     if (n == 0) return;
     size_t bytes = (size_t)n * q->esz;
-    void *dx = lq_devbuf_get(&q->xbuf, bytes);
+    const void *dx = lq_call_in(&q->ctx, &q->xbuf, x, bytes);
     void *dy = lq_devbuf_get(&q->ybuf, bytes);
-    lqrt_h2d(dx, x, bytes, q->ctx.stream);
     lq_firfilt_execute_block_dev(q, dx, n, dy);
-    lqrt_d2h(y, dy, bytes, q->ctx.stream);
-    lqrt_sync(q->ctx.stream);
+    lq_call_out(&q->ctx, y, dy, bytes);
 }
 
 unsigned int lq_firfilt_get_length(lq_firfilt *q) { return q->hlen; }

@@ -62,7 +62,9 @@ static lq_pfb *lq_pfb_create(int kind, unsigned int M, const float *h, unsigned 
     lqrt_h2d(q->d_hpoly, q->hpoly, (size_t)M * q->L * q->csz, q->ctx.stream);
     q->d_win[0] = lqrt_malloc((size_t)q->L * q->esz);
     q->d_win[1] = lqrt_malloc((size_t)q->L * q->esz);
-    q->h_win = (unsigned char *)lq_xmalloc((size_t)q->L * q->esz);
+    /* pinned: execute() reads it in place (zero copy) */
+    q->h_win = (unsigned char *)lqrt_host_alloc((size_t)q->L * q->esz);
+    memset(q->h_win, 0, (size_t)q->L * q->esz);
     q->host_valid = q->dev_valid = 1;
     lqrt_sync(q->ctx.stream);
     return q;
@@ -117,7 +119,7 @@ static void lq_pfb_destroy(lq_pfb *q)
     lq_devbuf_free(&q->one);
     lq_ctx_free(&q->ctx);
     free(q->hpoly);
-    free(q->h_win);
+    lqrt_host_free(q->h_win);
     free(q);
 }
 
@@ -170,11 +172,11 @@ static void lq_pfb_push(lq_pfb *q, const void *x)
 static void lq_pfb_execute(lq_pfb *q, unsigned int i, void *y)
 {
     if (i >= q->M) LQ_FAIL("error: firpfb_execute(), filterbank index (%u) exceeds maximum (%u)\n", i, q->M);
-    lq_pfb_need_dev(q);
-    void *dy = lq_devbuf_get(&q->one, 16);
-    lqk_firpfb_single(q->kind, q->d_hpoly, q->L, i, q->d_win[q->cur], q->sre, q->sim, dy, q->ctx.stream);
-    lqrt_d2h(y, dy, q->esz, q->ctx.stream);
-    lqrt_sync(q->ctx.stream);
+    const void *win = q->dev_valid ? q->d_win[q->cur] : (const void *)q->h_win;
+    unsigned *flag, seq;
+    void *py = lq_sig_out(&q->ctx, q->esz, &flag, &seq);
+    lqk_firpfb_single(q->kind, q->d_hpoly, q->L, i, win, q->sre, q->sim, py, flag, seq, q->ctx.stream);
+    lq_sig_wait(&q->ctx, y, q->esz, seq);
 }
 
 static void lq_pfb_block_dev(lq_pfb *q, const void *dx, unsigned long long n, void *dy)
@@ -195,12 +197,10 @@ static void lq_pfb_block(lq_pfb *q, const void *x, unsigned long long n, void *y
 {
     if (n == 0) return;
     size_t nin = (size_t)n * q->esz, nout = nin * q->M;
-    void *dx = lq_devbuf_get(&q->xbuf, nin);
+    const void *dx = lq_call_in(&q->ctx, &q->xbuf, x, nin);
     void *dy = lq_devbuf_get(&q->ybuf, nout);
-    lqrt_h2d(dx, x, nin, q->ctx.stream);
     lq_pfb_block_dev(q, dx, n, dy);
-    lqrt_d2h(y, dy, nout, q->ctx.stream);
-    lqrt_sync(q->ctx.stream);
+    lq_call_out(&q->ctx, y, dy, nout);
 }
 
 #define LQ_FIRPFB_FRONT(NAME, KIND, TO, TC, TI, SRE, SIM)                                           \

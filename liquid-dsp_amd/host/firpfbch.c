@@ -172,12 +172,10 @@ static void lq_pfbch_block(lq_pfbch *q, const void *x, unsigned long long nblock
 {
     if (nblocks == 0) return;
     size_t bytes = (size_t)nblocks * q->M * 8;
-    void *dx = lq_devbuf_get(&q->xbuf, bytes);
+    const void *dx = lq_call_in(&q->ctx, &q->xbuf, x, bytes);
     void *dy = lq_devbuf_get(&q->ybuf, bytes);
-    lqrt_h2d(dx, x, bytes, q->ctx.stream);
     lq_pfbch_block_dev(q, dx, nblocks, dy);
-    lqrt_d2h(y, dy, bytes, q->ctx.stream);
-    lqrt_sync(q->ctx.stream);
+    lq_call_out(&q->ctx, y, dy, bytes);
 }
 
 #define LQ_FIRPFBCH_FRONT(NAME, KIND, TC)                                                           \

@@ -152,12 +152,10 @@ void firpfbch2_crcf_execute_block(firpfbch2_crcf _q, liquid_float_complex *_x, u
     if (_nblocks == 0) return;
     size_t nin = (size_t)_nblocks * (_q->type == LIQUID_ANALYZER ? _q->M / 2 : _q->M);
     size_t nout = (size_t)_nblocks * (_q->type == LIQUID_ANALYZER ? _q->M : _q->M / 2);
-    void *dx = lq_devbuf_get(&_q->xbuf, nin * 8);
+    const void *dx = lq_call_in(&_q->ctx, &_q->xbuf, _x, nin * 8);
     void *dy = lq_devbuf_get(&_q->ybuf, nout * 8);
-    lqrt_h2d(dx, _x, nin * 8, _q->ctx.stream);
     firpfbch2_crcf_execute_block_dev(_q, (const liquid_float_complex *)dx, _nblocks, (liquid_float_complex *)dy);
-    lqrt_d2h(_y, dy, nout * 8, _q->ctx.stream);
-    lqrt_sync(_q->ctx.stream);
+    lq_call_out(&_q->ctx, _y, dy, nout * 8);
 }
 
 /* firpfbch2.c:342-357: one block (the reference's only execute form) */

@@ -54,17 +54,95 @@ void lq_ctx_init(lq_ctx *c)
 
 void lq_ctx_free(lq_ctx *c)
 {
-    if (c->own && c->stream) {
-        lqrt_sync(c->stream);
-        lqrt_stream_destroy(c->stream);
-    }
+    if (c->stream) lqrt_sync(c->stream);
+    if (c->own && c->stream) lqrt_stream_destroy(c->stream);
     c->stream = NULL;
+    lqrt_host_free(c->pin_in);
+    lqrt_host_free(c->pin_out);
+    lqrt_host_free(c->flag);
+    c->pin_in = c->pin_out = NULL;
+    c->flag = NULL;
+    c->in_cap = c->out_cap = 0;
+}
+
+static void *lq_pin_grow(void *p, size_t *cap, size_t bytes)
+{
+    if (bytes <= *cap) return p;
+    lqrt_host_free(p);
+    size_t n = 4096;
+    while (n < bytes) n *= 2;
+    *cap = n;
+    return lqrt_host_alloc(n);
+}
+
+const void *lq_call_in(lq_ctx *c, lq_devbuf *b, const void *x, size_t bytes)
+{
+    if (c->in_busy) {   /* a previous call without a result may still read pin_in */
+        lqrt_sync(c->stream);
+        c->in_busy = 0;
+    }
+    if (bytes == 0) return lq_devbuf_get(b, 16);
+    if (bytes > LQ_PIN_IN) {
+        void *d = lq_devbuf_get(b, bytes);
+        lqrt_h2d(d, x, bytes, c->stream);
+        return d;
+    }
+    c->pin_in = lq_pin_grow(c->pin_in, &c->in_cap, bytes);
+    memcpy(c->pin_in, x, bytes);
+    c->in_busy = 1;
+    return c->pin_in;
+}
+
+void lq_call_out(lq_ctx *c, void *y, const void *dy, size_t bytes)
+{
+    if (bytes == 0 || bytes > LQRT_COPYOUT_MAX || (bytes & 3)) {
+        if (bytes) lqrt_d2h(y, dy, bytes, c->stream);
+        lqrt_sync(c->stream);
+        c->in_busy = 0;
+        return;
+    }
+    c->pin_out = lq_pin_grow(c->pin_out, &c->out_cap, bytes);
+    if (!c->flag) {
+        c->flag = (unsigned *)lqrt_host_alloc(64);
+        *c->flag = c->seq = 0;
+    }
+    const unsigned seq = ++c->seq;
+    lqrt_copyout_signal(dy, c->pin_out, bytes, c->flag, seq, c->stream);
+    lqrt_wait_flag(c->flag, seq, c->stream);
+    memcpy(y, c->pin_out, bytes);
+    c->in_busy = 0;
+}
+
+void *lq_sig_out(lq_ctx *c, size_t bytes, unsigned **flag, unsigned *seq)
+{
+    c->pin_out = lq_pin_grow(c->pin_out, &c->out_cap, bytes);
+    if (!c->flag) {
+        c->flag = (unsigned *)lqrt_host_alloc(64);
+        *c->flag = c->seq = 0;
+    }
+    *flag = c->flag;
+    *seq = ++c->seq;
+    return c->pin_out;
+}
+
+void lq_sig_wait(lq_ctx *c, void *y, size_t bytes, unsigned seq)
+{
+    lqrt_wait_flag(c->flag, seq, c->stream);
+    memcpy(y, c->pin_out, bytes);
+    c->in_busy = 0;
+}
+
+void lq_call_done(lq_ctx *c)
+{
+    lqrt_sync(c->stream);
+    c->in_busy = 0;
 }
 
 void lq_ctx_set_stream(lq_ctx *c, void *stream)
 {
     if (c->stream) lqrt_sync(c->stream);
     if (c->own && c->stream) lqrt_stream_destroy(c->stream);
+    c->in_busy = 0;
     if (stream) {
         c->stream = stream;
         c->own = 0;

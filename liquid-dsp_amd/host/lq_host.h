@@ -36,15 +36,40 @@ typedef struct {
 void *lq_devbuf_get(lq_devbuf *b, size_t bytes);
 void lq_devbuf_free(lq_devbuf *b);
 
-/* per-object execution context: a HIP stream (owned unless supplied) */
+/* per-object execution context: a HIP stream (owned unless supplied) and
+ * the pinned host staging of the per-call (host-pointer) API */
 typedef struct {
     void *stream;
     int own;
+    void *pin_in, *pin_out;   /* pinned host buffers (lazily allocated) */
+    size_t in_cap, out_cap;
+    unsigned *flag;           /* pinned completion word */
+    unsigned seq;
+    int in_busy;              /* pin_in may still be read by queued kernels */
 } lq_ctx;
 
 void lq_ctx_init(lq_ctx *c);
 void lq_ctx_free(lq_ctx *c);
 void lq_ctx_set_stream(lq_ctx *c, void *stream);
+
+/* Host-pointer calls (the reference's own API, which returns with the result
+ * in host memory).  lq_call_in stages x: up to LQ_PIN_IN bytes are copied
+ * into pinned host memory that the kernels then read in place (no copy
+ * command), larger inputs go to device buffer b by DMA; returns the pointer
+ * to hand to the device path.  lq_call_out delivers a device result of up to
+ * LQRT_COPYOUT_MAX bytes through one copy-out kernel + completion flag
+ * (spin-wait, no stream synchronisation), larger ones by DMA + sync.
+ * lq_call_done waits for a call without a result. */
+#define LQ_PIN_IN (256u << 10)
+const void *lq_call_in(lq_ctx *c, lq_devbuf *b, const void *x, size_t bytes);
+void lq_call_out(lq_ctx *c, void *y, const void *dy, size_t bytes);
+void lq_call_done(lq_ctx *c);
+/* single results (firfilt/firpfb/dotprod execute) whose kernel writes the
+ * pinned result itself and raises the flag: lq_sig_out returns the pinned
+ * destination, the flag word and the sequence number to hand to the kernel;
+ * lq_sig_wait spins for it and copies the result to y */
+void *lq_sig_out(lq_ctx *c, size_t bytes, unsigned **flag, unsigned *seq);
+void lq_sig_wait(lq_ctx *c, void *y, size_t bytes, unsigned seq);
 
 void *lq_xmalloc(size_t bytes);
 unsigned int lq_msb_index(unsigned int x);

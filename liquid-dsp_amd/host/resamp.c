@@ -28,6 +28,7 @@
 #define RS_PERIODIC_MIN (1ull << 16)   /* calls at least this long use (and build) a periodic plan */
 #define RS_MAX_PERIOD (1ull << 25)     /* give up on periodic plans beyond this many inputs */
 #define RS_DIRECT_CHUNK (1ull << 24)   /* direct plans cover at most this many inputs */
+#define RS_DIRECT_AHEAD (1ull << 14)   /* ... and at least this many (built ahead for short calls) */
 
 enum { RS_BOUNDARY = 0, RS_INTERP = 1 };
 
@@ -246,8 +247,12 @@ static unsigned long long rs_ensure_plan(lq_rs *q, unsigned long long nx)
         }
         q->periodic_failed = 1;
     }
+    /* a direct plan covers this call and, for short calls, the next
+     * RS_DIRECT_AHEAD inputs too: the schedule does not depend on the data,
+     * so per-sample execute() calls reuse one plan instead of building and
+     * uploading one each (two stream synchronisations per call) */
     unsigned long long c = nx < RS_DIRECT_CHUNK ? nx : RS_DIRECT_CHUNK;
-    rs_plan_build_direct(q, c);
+    rs_plan_build_direct(q, c > RS_DIRECT_AHEAD ? c : RS_DIRECT_AHEAD);
     rs_plan_upload(q);
     return c;
 }
@@ -444,13 +449,11 @@ static void lq_rs_block(lq_rs *_q, const void *_x, unsigned int _nx, void *_y, u
         return;
     }
     unsigned long long nout = lq_rs_num_output(_q, _nx);
-    void *dx = lq_devbuf_get(&_q->xbuf, (size_t)_nx * _q->esz);
+    const void *dx = lq_call_in(&_q->ctx, &_q->xbuf, _x, (size_t)_nx * _q->esz);
     void *dy = lq_devbuf_get(&_q->ybuf, (size_t)(nout ? nout : 1) * _q->esz);
-    lqrt_h2d(dx, _x, (size_t)_nx * _q->esz, _q->ctx.stream);
     unsigned long long ny = 0;
     lq_rs_block_dev(_q, dx, _nx, dy, &ny);
-    if (ny) lqrt_d2h(_y, dy, (size_t)ny * _q->esz, _q->ctx.stream);
-    lqrt_sync(_q->ctx.stream);
+    lq_call_out(&_q->ctx, _y, dy, (size_t)ny * _q->esz);
     *_ny = (unsigned int)ny;
 }
 

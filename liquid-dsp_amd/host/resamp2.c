@@ -150,14 +150,12 @@ static void lq_r2_run(lq_r2 *q, int mode, const void *x, unsigned long long n, v
     if (n == 0) return;
     const size_t bx = (size_t)n * lq_r2_nin(mode) * q->esz;
     const size_t by = (size_t)n * (mode == LQK_R2_FILTER ? 1 : lq_r2_nout(mode)) * q->esz;
-    void *dx = lq_devbuf_get(&q->xbuf, bx);
+    const void *dx = lq_call_in(&q->ctx, &q->xbuf, x, bx);
     void *dy = lq_devbuf_get(&q->ybuf, by);
     void *dy1 = mode == LQK_R2_FILTER ? lq_devbuf_get(&q->y1buf, by) : NULL;
-    lqrt_h2d(dx, x, bx, q->ctx.stream);
     lq_r2_run_dev(q, mode, dx, n, dy, dy1, 1.0f);
-    lqrt_d2h(y0, dy, by, q->ctx.stream);
-    if (dy1) lqrt_d2h(y1, dy1, by, q->ctx.stream);
-    lqrt_sync(q->ctx.stream);
+    if (dy1) lqrt_d2h(y1, dy1, by, q->ctx.stream);   /* ordered before the copy-out's flag */
+    lq_call_out(&q->ctx, y0, dy, by);
 }
 
 #define LQ_RESAMP2_FRONT(NAME, KIND, T)                                                             \
@@ -342,12 +340,10 @@ static void lq_ms2_block(lq_ms2 *q, const void *x, unsigned long long n, void *y
     if (n == 0) return;
     const size_t bx = (size_t)n * (q->type == LIQUID_RESAMP_INTERP ? 1 : q->M) * q->esz;
     const size_t by = (size_t)n * (q->type == LIQUID_RESAMP_INTERP ? q->M : 1) * q->esz;
-    void *dx = lq_devbuf_get(&q->xbuf, bx);
+    const void *dx = lq_call_in(&q->ctx, &q->xbuf, x, bx);
     void *dy = lq_devbuf_get(&q->ybuf, by);
-    lqrt_h2d(dx, x, bx, q->ctx.stream);
     lq_ms2_block_dev(q, dx, n, dy);
-    lqrt_d2h(y, dy, by, q->ctx.stream);
-    lqrt_sync(q->ctx.stream);
+    lq_call_out(&q->ctx, y, dy, by);
 }
 
 #define LQ_MSRESAMP2_FRONT(NAME, KIND, T)                                                           \
@@ -523,12 +519,10 @@ static void lq_ms_block_dev(lq_ms *q, const void *dx, unsigned long long nx, voi
 static void lq_ms_block(lq_ms *q, const void *x, unsigned int nx, void *y, unsigned int *ny)
 {
     unsigned long long nout = lq_ms_num_output(q, nx), n = 0;
-    void *dx = lq_devbuf_get(&q->xbuf, (size_t)(nx ? nx : 1) * q->esz);
+    const void *dx = lq_call_in(&q->ctx, &q->xbuf, x, (size_t)nx * q->esz);
     void *dy = lq_devbuf_get(&q->ybuf, (size_t)(nout ? nout : 1) * q->esz);
-    if (nx) lqrt_h2d(dx, x, (size_t)nx * q->esz, q->ctx.stream);
     lq_ms_block_dev(q, dx, nx, dy, &n);
-    if (n) lqrt_d2h(y, dy, (size_t)n * q->esz, q->ctx.stream);
-    lqrt_sync(q->ctx.stream);
+    lq_call_out(&q->ctx, y, dy, (size_t)n * q->esz);
     *ny = (unsigned int)n;
 }
 

@@ -224,10 +224,9 @@ static void lq_spg_accumulate_dev(lq_spg *q, const void *dx, unsigned long long 
 
 static void lq_spg_accumulate(lq_spg *q, const void *x, float alpha, unsigned int n)
 {
-    void *dx = lq_devbuf_get(&q->xbuf, (size_t)(n ? n : 1) * q->esz);
-    if (n) lqrt_h2d(dx, x, (size_t)n * q->esz, q->ctx.stream);
+    const void *dx = lq_call_in(&q->ctx, &q->xbuf, x, (size_t)n * q->esz);
     lq_spg_accumulate_dev(q, dx, n, alpha);
-    lqrt_sync(q->ctx.stream);
+    lq_call_done(&q->ctx);
 }
 
 static void lq_spg_write_accumulation(lq_spg *q, float *out)
