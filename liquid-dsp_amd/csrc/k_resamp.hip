@@ -436,7 +436,17 @@ extern "C" void lqk_resamp(int real_io, const lqk_rs_plan *pl, unsigned long lon
 {
     if (n == 0) return;
     hipStream_t st = (hipStream_t)stream;
-    if (real_io) run_rs<float>(pl, g0, K0, npfb, L, del, taps, taps2, hist, x, n, y, st);
-    else run_rs<float2>(pl, g0, K0, npfb, L, del, taps, taps2, hist, x, n, y, st);
-    LQ_CHECK_LAUNCH();
+    // launches of at most 2^27 inputs keep the range-checked byte offsets in
+    // 32 bits; outputs are placed by plan position, so a later launch only
+    // moves g0, x and its history (the L inputs before it)
+    const size_t es = real_io ? 4 : 8;
+    const unsigned long long CHN = 1ull << 27;
+    for (unsigned long long o = 0; o < n; o += CHN) {
+        const unsigned long long nn = (n - o) < CHN ? (n - o) : CHN;
+        const char *xo = (const char *)x + o * es;
+        const void *ho = o == 0 ? hist : (const void *)(xo - (size_t)L * es);
+        if (real_io) run_rs<float>(pl, g0 + o, K0, npfb, L, del, taps, taps2, ho, xo, nn, y, st);
+        else run_rs<float2>(pl, g0 + o, K0, npfb, L, del, taps, taps2, ho, xo, nn, y, st);
+        LQ_CHECK_LAUNCH();
+    }
 }
