@@ -285,18 +285,22 @@ def bench_dotprod(args, world, rank, stream):
     nvec = args.dp_vectors
     g = torch.Generator()
     g.manual_seed(11)
-    for n in (16, 64, 256, 1024):
-        X = synth_complex(n * nvec, 99 + n + rank)
-        Y = torch.empty(2 * nvec, dtype=torch.float32, device="cuda")
+    # the config's 1M vectors at n = 16 / 64 are 134 MB / 537 MB: the n = 16
+    # set fits the 256 MB Infinity Cache, so "n16_hbm" repeats it on 2^23
+    # vectors (1 GiB) for an HBM figure
+    for n, nv, key in ((16, nvec, 16), (64, nvec, 64), (256, nvec, 256), (1024, nvec, 1024),
+                       (16, 8 * nvec, "16_hbm")):
+        X = synth_complex(n * nv, 99 + n + rank)
+        Y = torch.empty(2 * nv, dtype=torch.float32, device="cuda")
         h = ((torch.rand(n, generator=g) - 0.5) + 1j * (torch.rand(n, generator=g) - 0.5)).numpy()
         q = LQ.DotProd("cccf", h)
         q.set_stream(stream.cuda_stream)
 
         def step():
-            q.execute_batch_dev(X.data_ptr(), nvec, Y.data_ptr())
+            q.execute_batch_dev(X.data_ptr(), nv, Y.data_ptr())
 
         wall, gpu_ms = time_steps(step, args.steps, args.warmup, world, stream)
-        out[n] = {"wall": wall, "gpu_ms": gpu_ms}
+        out[key] = {"wall": wall, "gpu_ms": gpu_ms, "n": n, "nvec": nv}
         q.destroy()
         del X, Y
         torch.cuda.empty_cache()
@@ -653,11 +657,13 @@ def main():
                                                      "launch_ms": rl_ms}}
         if dp is not None:
             legs = {}
-            for n, (tw, tg) in dp_t.items():
+            for key, (tw, tg) in dp_t.items():
                 ms = tg / args.steps
-                legs["n%d" % n] = {"value": world * dp["nvec"] * args.steps / tw / 1e6, "unit": "M dot products/s",
-                                   "launch_ms": ms, "achieved_GBps": (8.0 * n + 8.0) * dp["nvec"] / (ms * 1e-3) / 1e9,
-                                   "frac": (8.0 * n + 8.0) * dp["nvec"] / (ms * 1e-3) / 1e9 / HBM_PEAK_GBPS}
+                n, nv = dp["runs"][key]["n"], dp["runs"][key]["nvec"]
+                legs["n%s" % key] = {"value": world * nv * args.steps / tw / 1e6, "unit": "M dot products/s",
+                                     "vectors": nv, "working_set_MB": (8.0 * n + 8.0) * nv / 1e6,
+                                     "launch_ms": ms, "achieved_GBps": (8.0 * n + 8.0) * nv / (ms * 1e-3) / 1e9,
+                                     "frac": (8.0 * n + 8.0) * nv / (ms * 1e-3) / 1e9 / HBM_PEAK_GBPS}
             out["dotprod_cccf"] = {"workload": "dotprod_cccf batched, %d vectors/GPU (BASELINE configs[1])"
                                    % dp["nvec"], "bytes_per_unit": "8n+8 B/vector", "legs": legs}
             ms = ff_t[1] / args.steps

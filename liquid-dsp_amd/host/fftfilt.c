@@ -12,6 +12,11 @@
  * (execute_block extension) run all segments in parallel.  rrrf runs the
  * real-I/O form of the kernel; crcf and cccf share the complex form (H is
  * the transform of real or complex taps).
+ *
+ * Filters longer than the transform allows (h_len - 1 > 2048, which the
+ * reference accepts for any n >= h_len - 1) run the same convolution as a
+ * direct FIR (the firfilt engine, csrc/k_firfilt.hip) on the object's
+ * stream: y = s * (h * x) either way, to float32 rounding.
  */
 #include <complex.h>
 
@@ -28,6 +33,7 @@ typedef struct {
     void *d_hist[2];    /* previous h_len-1 inputs */
     int cur;
     float sre, sim;     /* user scale s */
+    lq_firfilt *direct; /* h_len - 1 > NFFT/2: direct convolution */
     lq_ctx ctx;
     lq_devbuf xbuf, ybuf, cbuf;
 } lq_fftf;
@@ -39,9 +45,6 @@ static lq_fftf *lq_fftf_create(int kind, const float *h, unsigned int h_len, uns
         LQ_FAIL("error: fftfilt_%s_create(), block length must be greater than _h_len-1 (%u)\n", lq_ext[kind],
                 h_len - 1);
     lqrt_require_device("fftfilt_create");
-    if (h_len - 1 > lqk_fftfilt_nfft() / 2)
-        LQ_FAIL("error: fftfilt_%s_create(), filter length %u exceeds the GPU limit %u\n", lq_ext[kind], h_len,
-                lqk_fftfilt_nfft() / 2 + 1);
     lq_fftf *q = (lq_fftf *)lq_xmalloc(sizeof(*q));
     q->kind = kind;
     q->esz = kind == LQ_RRRF ? 4 : 8;
@@ -56,7 +59,13 @@ static lq_fftf *lq_fftf_create(int kind, const float *h, unsigned int h_len, uns
     q->d_hist[0] = lqrt_malloc((size_t)h_len * q->esz);
     q->d_hist[1] = lqrt_malloc((size_t)h_len * q->esz);
     lqrt_h2d(q->d_h, q->h, h_len * q->csz, q->ctx.stream);
-    lqk_fftfilt_make_H(q->d_h, h_len, kind == LQ_CCCF, q->d_H, q->ctx.stream);
+    if (h_len - 1 > lqk_fftfilt_nfft() / 2) {
+        static const char *who[] = {"fftfilt_rrrf", "fftfilt_crcf", "fftfilt_cccf"};
+        q->direct = lq_firfilt_create(kind, h, h_len, who[kind]);
+        lq_ctx_set_stream(lq_firfilt_ctx(q->direct), q->ctx.stream);
+    } else {
+        lqk_fftfilt_make_H(q->d_h, h_len, kind == LQ_CCCF, q->d_H, q->ctx.stream);
+    }
     lqrt_sync(q->ctx.stream);
     q->sre = 1.0f;
     q->sim = 0.0f;
@@ -67,6 +76,7 @@ static lq_fftf *lq_fftf_create(int kind, const float *h, unsigned int h_len, uns
 static void lq_fftf_destroy(lq_fftf *q)
 {
     lqrt_sync(q->ctx.stream);
+    if (q->direct) lq_firfilt_destroy(q->direct);
     lqrt_free(q->d_h);
     lqrt_free(q->d_H);
     lqrt_free(q->d_hist[0]);
@@ -84,6 +94,7 @@ static void lq_fftf_reset(lq_fftf *q)
     lqrt_memset(q->d_hist[0], (size_t)q->h_len * q->esz, q->ctx.stream);
     lqrt_memset(q->d_hist[1], (size_t)q->h_len * q->esz, q->ctx.stream);
     lqrt_sync(q->ctx.stream);
+    if (q->direct) lq_firfilt_reset(q->direct);
 }
 
 static void lq_fftf_print(lq_fftf *q)
@@ -100,6 +111,11 @@ static void lq_fftf_print(lq_fftf *q)
 static void lq_fftf_block_dev(lq_fftf *q, const void *dx, unsigned long long n, void *dy)
 {
     if (n == 0) return;
+    if (q->direct) {
+        lq_firfilt_set_scale(q->direct, q->sre, q->sim);
+        lq_firfilt_execute_block_dev(q->direct, dx, n, dy);
+        return;
+    }
     const void *x = dx;
     if (dx == dy) { /* kernel segments read overlapping halos */
         void *c = lq_devbuf_get(&q->cbuf, (size_t)n * q->esz);
@@ -159,7 +175,11 @@ static void lq_fftf_block(lq_fftf *q, const void *x, unsigned long long n, void 
     {                                                                                               \
         lq_fftf_block_dev(_q->e, _dx, _n, _dy);                                                     \
     }                                                                                               \
-    void NAME##_set_stream(NAME _q, void *_s) { lq_ctx_set_stream(&_q->e->ctx, _s); }
+    void NAME##_set_stream(NAME _q, void *_s)                                                       \
+    {                                                                                               \
+        lq_ctx_set_stream(&_q->e->ctx, _s);                                                         \
+        if (_q->e->direct) lq_ctx_set_stream(lq_firfilt_ctx(_q->e->direct), _q->e->ctx.stream);      \
+    }
 
 LQ_FFTFILT_FRONT(fftfilt_rrrf, LQ_RRRF, float, float, float, _scale, 0.0f)
 LQ_FFTFILT_FRONT(fftfilt_crcf, LQ_CRCF, liquid_float_complex, float, liquid_float_complex, _scale, 0.0f)

@@ -97,3 +97,27 @@ def test_firfilt_extreme_taps_stay_exact():
     x = ((r.uniform(-0.5, 0.5, 30000) + 1j * r.uniform(-0.5, 0.5, 30000)) * 2.0 ** -20).astype(np.complex64)
     ref = O.FirFilt(O.CRCF, h).execute_block(x)
     _check(_run("crcf", h, x, dev=True), ref)
+
+
+@pytest.mark.parametrize("t", ["rrrf", "crcf", "cccf"])
+@pytest.mark.parametrize("h_len,n", [(2050, 2049), (4000, 4096), (6001, 8000)])
+def test_fftfilt_long_filters(t, h_len, n):
+    # the reference accepts any h_len with n >= h_len - 1 (fftfilt.c:78-83);
+    # past the 4096-point transform's reach the object runs the convolution
+    # directly -- same output, same scale semantics
+    r = np.random.default_rng(h_len)
+    h = (r.uniform(-0.5, 0.5, h_len) + (1j * r.uniform(-0.5, 0.5, h_len) if t == "cccf" else 0)).astype(
+        np.complex64 if t == "cccf" else np.float32)
+    nb = 5
+    if t == "rrrf":
+        x = r.uniform(-0.5, 0.5, nb * n).astype(np.float32)
+    else:
+        x = (r.uniform(-0.5, 0.5, nb * n) + 1j * r.uniform(-0.5, 0.5, nb * n)).astype(np.complex64)
+    s = 0.5   # the oracle's fftfilt scale is real (fftfilt.c:182-187 with a real s)
+    g = LQ.FftFilt(h, n, t=t)
+    g.set_scale(s)
+    o = O.FftFilt(TYPES[t], h, n)
+    o.set_scale(s)
+    got = np.concatenate([g.execute(x[i * n:(i + 1) * n]) for i in range(nb)])
+    ref = np.concatenate([o.execute(x[i * n:(i + 1) * n]) for i in range(nb)])
+    assert np.max(np.abs(got - ref)) <= 1e-5 * np.max(np.abs(ref))
