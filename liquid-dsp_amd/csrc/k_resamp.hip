@@ -25,6 +25,7 @@
 #include "lq_kernels.h"
 
 #include <cstdlib>
+#include <type_traits>
 
 namespace {
 
@@ -212,9 +213,25 @@ __global__ __launch_bounds__(NT) void k_resamp2(lqk_rs_plan pl, unsigned long lo
     const long long ntiles = (n + TIN - 1) / TIN;
     constexpr int NXV = (TS + NT - 1) / NT;       // tile samples per lane
 
-    // everything a tile needs from HBM, fetched one tile ahead into registers
+    // everything a tile needs from HBM, fetched one tile ahead into registers.
+    // Samples come through two range-checked descriptors (x: n samples, the
+    // history: the L before it); each sample is in range in at most one, so
+    // their sum is the sample and the loads carry no branch -- a branchy load
+    // merged its result through register copies, which made the prefetch wait
+    // for its data at once.  The host keeps n * sizeof(S) below 2^31.
+    const __amdgpu_buffer_rsrc_t rx =
+        __builtin_amdgcn_make_buffer_rsrc((void *)x, (short)0, (int)(n * (long long)sizeof(S)), 0x00020000);
+    const __amdgpu_buffer_rsrc_t rh =
+        __builtin_amdgcn_make_buffer_rsrc((void *)hist, (short)0, (int)(L * sizeof(S)), 0x00020000);
+    auto ld = [&](__amdgpu_buffer_rsrc_t r, long long e) -> S {
+        const unsigned off = (unsigned)(e * (long long)sizeof(S));   // negative: out of range, reads 0
+        if constexpr (sizeof(S) == 8)
+            return __builtin_bit_cast(S, __builtin_amdgcn_raw_buffer_load_b64(r, off, 0, 0));
+        else
+            return __builtin_bit_cast(S, __builtin_amdgcn_raw_buffer_load_b32(r, off, 0, 0));
+    };
     struct Pre {
-        S xv[NXV];
+        S xa[NXV], xb[NXV];
         rs_state s;
         unsigned long long K, Kb, Ke;
     };
@@ -222,14 +239,9 @@ __global__ __launch_bounds__(NT) void k_resamp2(lqk_rs_plan pl, unsigned long lo
         const long long i0 = tile * TIN;
 #pragma unroll
         for (int u = 0; u < NXV; u++) {
-            const int t = tid + u * NT;
-            const long long sx = i0 - L - 1 + t;
-            S v{};
-            if (t < TS) {
-                if (sx >= 0 && sx < n) v = x[sx];
-                else if (sx < 0 && sx >= -L) v = hist[L + sx];
-            }
-            f.xv[u] = v;
+            const long long sx = i0 - L - 1 + tid + u * NT;
+            f.xa[u] = ld(rx, sx);
+            f.xb[u] = ld(rh, L + sx);
         }
         const unsigned long long gt = g0 + (unsigned long long)i0;
         unsigned long long jt = gt, ct = 0;
@@ -256,15 +268,22 @@ __global__ __launch_bounds__(NT) void k_resamp2(lqk_rs_plan pl, unsigned long lo
         for (int u = 0; u < NXV; u++) {
             const int t = tid + u * NT;
             if (t < TS) {
-                cp0[t] = cur.xv[u];
-                cp1[t + 1] = cur.xv[u];
+                const S a = cur.xa[u], b = cur.xb[u];
+                S v;
+                if constexpr (sizeof(S) == 8) v = make_float2(a.x + b.x, a.y + b.y);
+                else v = a + b;
+                cp0[t] = v;
+                cp1[t + 1] = v;
             }
         }
         const unsigned long long Kb = cur.Kb;
         const long long ntile = (long long)(cur.Ke - Kb);
         const rs_state slane = cur.s;
         const unsigned long long Klane = cur.K;
-        if (tile + gridDim.x < ntiles) fetch(tile + gridDim.x, cur);   // in flight during this tile
+        // in flight during this tile; unconditional (a tile past the end loads
+        // out of range: zeros, and plan positions any plan resolves) so the
+        // loads stay outstanding across the evaluation
+        fetch(tile + gridDim.x, cur);
         const long long ia = i0 + (long long)tid * RIN;   // this lane's first input
         for (long long r0 = 0; r0 < ntile; r0 += CAP) {
             if (r0 > 0) __syncthreads();                   // previous round consumed
@@ -304,25 +323,43 @@ __global__ __launch_bounds__(NT) void k_resamp2(lqk_rs_plan pl, unsigned long lo
                 const S *wp = (sw & 1) ? cp1 + sw + 1 : cp0 + sw;
                 const float2 *tp = tpl + rowoff(bb);
                 S acc{};
+                // the tap row and the window are read in two batches of NW/2
+                // 16-byte pairs, all reads of a batch issued before its math:
+                // two LDS round trips per output instead of one per pair
+                constexpr int HB = NW / 2 > 0 ? NW / 2 : 1;
 #pragma unroll
-                for (int q = 0; q < NW; q++) {
-                    const v4f t = *reinterpret_cast<const v4f *>(tp + 2 * q);
-                    if constexpr (sizeof(S) == 8) {    // two complex samples: one 16-byte read
-                        // packed: (c0, c1) = (t.x, t.z) + mu ((t.y, t.w) - (t.x, t.z)), then
-                        // acc += c0 w0 + c1 w1 as two v_pk_fma_f32 on (re, im)
-                        const v2f lo = {t.x, t.y}, hi = {t.z, t.w};
-                        const v2f c = lo + v2f{mu, mu} * (hi - lo);
-                        const v4f w = *reinterpret_cast<const v4f *>(wp + 2 * q);
-                        v2f a2 = {acc.x, acc.y};
-                        a2 = v2f{c.x, c.x} * v2f{w.x, w.y} + a2;
-                        a2 = v2f{c.y, c.y} * v2f{w.z, w.w} + a2;
-                        acc = make_float2(a2.x, a2.y);
-                    } else {                           // two real samples: one 8-byte read
-                        const float c0 = t.x + mu * (t.z - t.x);
-                        const float c1 = t.y + mu * (t.w - t.y);
-                        const float2 w = *reinterpret_cast<const float2 *>(wp + 2 * q);
-                        acc = rs_axpy(c0, w.x, acc);
-                        acc = rs_axpy(c1, w.y, acc);
+                for (int q0 = 0; q0 < NW; q0 += HB) {
+                    v4f tt[HB];
+                    typedef typename std::conditional<sizeof(S) == 8, v4f, float2>::type WT;
+                    WT ww[HB];
+#pragma unroll
+                    for (int k = 0; k < HB; k++) {
+                        if (q0 + k < NW) {
+                            tt[k] = *reinterpret_cast<const v4f *>(tp + 2 * (q0 + k));
+                            ww[k] = *reinterpret_cast<const WT *>(wp + 2 * (q0 + k));
+                        }
+                    }
+#pragma unroll
+                    for (int k = 0; k < HB; k++) {
+                        if (q0 + k >= NW) break;
+                        const v4f t = tt[k];
+                        if constexpr (sizeof(S) == 8) {    // two complex samples: one 16-byte read
+                            // packed: (c0, c1) = (t.x, t.y) + mu ((t.z, t.w) - (t.x, t.y)), then
+                            // acc += c0 w0 + c1 w1 as two v_pk_fma_f32 on (re, im)
+                            const v2f lo = {t.x, t.y}, hi = {t.z, t.w};
+                            const v2f c = lo + v2f{mu, mu} * (hi - lo);
+                            const v4f w = ww[k];
+                            v2f a2 = {acc.x, acc.y};
+                            a2 = v2f{c.x, c.x} * v2f{w.x, w.y} + a2;
+                            a2 = v2f{c.y, c.y} * v2f{w.z, w.w} + a2;
+                            acc = make_float2(a2.x, a2.y);
+                        } else {                           // two real samples: one 8-byte read
+                            const float c0 = t.x + mu * (t.z - t.x);
+                            const float c1 = t.y + mu * (t.w - t.y);
+                            const float2 w = ww[k];
+                            acc = rs_axpy(c0, w.x, acc);
+                            acc = rs_axpy(c1, w.y, acc);
+                        }
                     }
                 }
                 yo[o] = acc;

@@ -31,7 +31,7 @@ for r in rows:
     agg[k][r["Counter_Name"]] += float(r["Counter_Value"])
     cnt[k].add(r.get("Dispatch_Id", ""))
 for k, d in agg.items():
-    if "pfb2" in k or "firfilt" in k:
+    if "pfb2" in k or "firfilt" in k or "resamp" in k:
         print(k, len(cnt[k]), {c: "%.4g" % (v / max(1, len(cnt[k]))) for c, v in d.items()})
 PY
 done
