@@ -9,14 +9,14 @@ export TMPDIR=/tmp
 STEP=${1:-all}
 timeout -k 10 600 python -c "import __graft_entry__ as g; g.build()" > gpurun_out/build.log 2>&1 || { echo "build failed"; tail -30 gpurun_out/build.log; exit 1; }
 if [ "$STEP" = "all" ] || [ "$STEP" = "test" ]; then
-  timeout -k 10 900 python -m pytest tests -m gpu -x -q > gpurun_out/pytest_gpu.log 2>&1; rc=$?
+  timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread > gpurun_out/pytest_gpu.log 2>&1; rc=$?
   tail -25 gpurun_out/pytest_gpu.log
   [ $rc -eq 0 ] || exit $rc
   timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke.log 2>&1 || { cat gpurun_out/smoke.log; exit 1; }
   cat gpurun_out/smoke.log
 fi
 if [ "$STEP" = "all" ] || [ "$STEP" = "bench" ]; then
-  timeout -k 10 600 python bench.py --steps 10 --warmup 2 --cpu-seconds 10 > gpurun_out/bench.log 2>&1 || { tail -30 gpurun_out/bench.log; exit 1; }
+  timeout -k 10 600 python bench.py > gpurun_out/bench.log 2>&1 || { tail -30 gpurun_out/bench.log; exit 1; }
   tail -3 gpurun_out/bench.log
 fi
 if [ "$STEP" = "all" ] || [ "$STEP" = "prof" ]; then
