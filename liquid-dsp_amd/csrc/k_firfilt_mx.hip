@@ -59,12 +59,11 @@ constexpr int NT = 256;           // 4 waves
 constexpr int CH = 2048;          // outputs per chunk (4 tiles of 512)
 constexpr int SPAN = CH + 64;     // samples a chunk's tiles read (64-sample halo)
 constexpr int PLB = SPAN * 2 + 16 * (SPAN / 32);   // bytes per plane (5280)
-constexpr int HPB = 64 * 2 + 16 * 2;               // bytes per plane of a halo buffer
 constexpr int SSTR = 68;          // floats per staged segment (32 x re/im + pad)
-// crcf: one staged accumulator per wave (51008 B: three workgroups per CU);
-// cccf: two (the real- and imaginary-tap products; 68416 B: two per CU)
+// crcf: one staged accumulator per wave (49088 B: three workgroups per CU);
+// cccf: two (the real- and imaginary-tap products; 66496 B: two per CU)
 template <bool CC>
-constexpr int lds_bytes_mx() { return 6 * PLB + 2 * 6 * HPB + (CC ? 2 : 1) * 4 * 16 * SSTR * 4; }
+constexpr int lds_bytes_mx() { return 6 * PLB + (CC ? 2 : 1) * 4 * 16 * SSTR * 4; }
 
 __device__ __forceinline__ int poff(int pos) { return 2 * pos + 16 * (pos >> 5); }
 
@@ -113,6 +112,20 @@ __device__ __forceinline__ void put8(unsigned char *planes, int pstride, int pos
         }
 }
 
+// one complex sample at ring position pos into the six planes
+__device__ __forceinline__ void put1(unsigned char *planes, int pstride, int pos, v2f v)
+{
+    bf16x2 t1, t2, t3;
+    split3(v, t1, t2, t3);   // (re, im) terms
+    const int o = poff(pos);
+    const bf16x2 t[3] = {t1, t2, t3};
+#pragma unroll
+    for (int p = 0; p < 3; p++) {
+        *reinterpret_cast<__bf16 *>(planes + (2 * p) * pstride + o) = t[p].x;
+        *reinterpret_cast<__bf16 *>(planes + (2 * p + 1) * pstride + o) = t[p].y;
+    }
+}
+
 // 8 complex samples of the stream starting at s (a multiple of 8); ext[t<0]
 // comes from the 64-sample history win, samples at or past n are zero
 __device__ __forceinline__ v2f sample_at(const v2f *__restrict__ win, const v2f *__restrict__ x, long long n,
@@ -120,22 +133,6 @@ __device__ __forceinline__ v2f sample_at(const v2f *__restrict__ win, const v2f 
 {
     return t < 0 ? win[64 + t] : (t < n ? x[t] : v2f{0.f, 0.f});
 }
-__device__ __forceinline__ void load8(const v2f *__restrict__ win, const v2f *__restrict__ x, long long n,
-                                      long long s, v4f (&v)[4])
-{
-    if (s >= 0 && s + 8 <= n) {
-        const v4f *p = reinterpret_cast<const v4f *>(x + s);
-#pragma unroll
-        for (int q = 0; q < 4; q++) v[q] = p[q];   // plain loads: non-temporal ones cost 15 %
-    } else {
-#pragma unroll
-        for (int q = 0; q < 4; q++) {
-            const v2f e0 = sample_at(win, x, n, s + 2 * q), e1 = sample_at(win, x, n, s + 2 * q + 1);
-            v[q] = v4f{e0.x, e0.y, e1.x, e1.y};
-        }
-    }
-}
-
 // Exact float32 outputs t0 .. t0+cnt-1 (the range guard's path): the
 // reference's dot product over the true taps, firfilt.c:322-338, then the
 // scale.  Out of line, so the matrix path's register allocation is unchanged.
@@ -180,24 +177,17 @@ template <bool CC>
 __global__ __launch_bounds__(NT, CC ? 2 : 3) void k_firfilt_mx(const v2f *__restrict__ win,
                                                               const v2f *__restrict__ x, long long n,
                                                               v2f *__restrict__ y, const float *__restrict__ hpad,
-                                                              float sre, float sim, long long nch, long long cpw,
-                                                              int hlen)
+                                                              float sre, float sim, long long nch, int hlen)
 {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-    // per chunk c % 3: bit 0 any unsafe sample, bit 1 one in the tail (the next chunk's halo);
+    // per step k % 3: nonzero if the chunk's span holds an unsafe sample;
     // kept after the dynamic region so its base stays 16-byte aligned
     unsigned *sbad = reinterpret_cast<unsigned *>(smem + lds_bytes_mx<CC>());
     unsigned char *planes = smem;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int r32 = lane & 31, hh = lane >> 5;
-    unsigned char *halo = smem + 6 * PLB;   // two halo buffers (chunk tails), 6 planes each
     constexpr int NA = CC ? 2 : 1;   // tap matrices
-    float *stage = reinterpret_cast<float *>(smem + 6 * PLB + 2 * 6 * HPB) + wave * NA * 16 * SSTR;
-
-    const long long c0 = (long long)blockIdx.x * cpw;
-    long long c1 = c0 + cpw;
-    if (c1 > nch) c1 = nch;
-    if (c0 >= c1) return;
+    float *stage = reinterpret_cast<float *>(smem + 6 * PLB) + wave * NA * 16 * SSTR;
 
     // A fragments: lane (row i = r32, k half hh) holds H[i][16s + 8hh + e]
     // (cccf: hpad holds (re, im) pairs; matrix a takes component a)
@@ -223,59 +213,72 @@ __global__ __launch_bounds__(NT, CC ? 2 : 3) void k_firfilt_mx(const v2f *__rest
                     bf16x8{t[p][0].x, t[p][0].y, t[p][1].x, t[p][1].y, t[p][2].x, t[p][2].y, t[p][3].x, t[p][3].y};
         }
 
-    // plane position p of chunk c = stream sample CH c - 64 + p; positions
-    // 0..63 (the previous chunk's tail) come from halo buffer (c - 1) & 1,
-    // filled by the lanes holding that tail one iteration earlier (from
-    // memory for the first chunk)
+    // Chunks are dealt grid-stride (workgroup w takes chunks w, w + G, ...):
+    // the chip then streams one contiguous window of the input at a time.
+    // Contiguous runs of chunks per workgroup put ~800 concurrent streams on
+    // addresses a run apart and ran the same memory pattern 9 % slower
+    // (0.80 vs 0.73 ms per 2^28 samples, tools/mb/mb_bw4.hip).  So a chunk's
+    // 64-sample halo (the previous chunk's tail, another workgroup's) is
+    // loaded with it: wave 0 fetches one sample per lane.  Plane position
+    // p of chunk c = stream sample CH c - 64 + p.
+    const long long G = gridDim.x, w = blockIdx.x;
+    if (w >= nch) return;
+    const long long cnt = (nch - w + G - 1) / G;
     if (tid < 3) sbad[tid] = 0u;
-    __syncthreads();
-    if (tid < 8) {
-        v4f v[4];
-        load8(win, x, n, CH * c0 - 64 + 8 * tid, v);
-        put8(halo + ((c0 - 1) & 1) * 6 * HPB, HPB, 8 * tid, v);
-        if (unsafe4(v[0]) | unsafe4(v[1]) | unsafe4(v[2]) | unsafe4(v[3])) atomicOr(&sbad[(c0 + 2) % 3], 2u);
-    }
-    // two chunks in flight per workgroup: register sets xa / xb alternate
-    // (the loop is unrolled by two so neither set is ever copied, which would
-    // wait on its loads early).  The loop body is branch-free in its memory
-    // operations -- range-checked buffer loads and stores, a step past the
-    // workgroup's last chunk (odd chunk counts) lands out of range -- so the
-    // compiler's vmcnt waits only for the rows a step consumes and the
-    // previous chunks' stores stay in flight.  The host keeps n * 8 bytes
-    // below 2^31 per launch and cpw even (chunk c1 then lies past n).
+    unsigned *bad_mask = sbad + 4;   // steps k of this workgroup that need the exact path
+    if (tid < 16) bad_mask[tid] = 0u;
+    // The loop's memory operations are branch-free -- range-checked buffer
+    // loads and stores; a step past the workgroup's last chunk (odd counts)
+    // lands out of range -- so the compiler's vmcnt waits only for the rows a
+    // step consumes and earlier stores stay in flight.  The host keeps n * 8
+    // bytes below 2^31 per launch.
     const __amdgpu_buffer_rsrc_t rx = __builtin_amdgcn_make_buffer_rsrc((void *)x, (short)0, (int)(n * 8), 0x00020000);
     const __amdgpu_buffer_rsrc_t ry = __builtin_amdgcn_make_buffer_rsrc((void *)y, (short)0, (int)(n * 8), 0x00020000);
     const unsigned OOB = 0xfffff000u;   // an offset past any launch's range
+    auto main_off = [&](long long k) -> unsigned {
+        const long long c = w + k * G;
+        return c < nch ? (unsigned)(CH * c + 8 * tid) * 8u : OOB;
+    };
+    // halo sample of lane tid < 64; chunk 0's halo is the history (prologue)
+    auto halo_off = [&](long long k) -> unsigned {
+        const long long c = w + k * G;
+        return (c > 0 && c < nch && tid < 64) ? (unsigned)(CH * c - 64 + tid) * 8u : OOB;
+    };
+    auto ldh = [&](unsigned off) -> v2f { return __builtin_bit_cast(v2f, __builtin_amdgcn_raw_buffer_load_b64(rx, off, 0, 0)); };
+    __syncthreads();
+    if (w == 0 && tid < 64) {
+        const v2f hv = win[tid];
+        put1(planes, PLB, tid, hv);
+        if (unsafe_bits(hv.x) | unsafe_bits(hv.y)) atomicOr(&sbad[0], 1u);
+    }
+    // two chunks in flight per workgroup: register sets (xa, ha) / (xb, hb)
+    // alternate (the loop is unrolled by two so neither set is ever copied,
+    // which would wait on its loads early)
     v4f xa[4], xb[4];
-    load8b(rx, (unsigned)(CH * c0 + 8 * tid) * 8u, xa);
-    load8b(rx, c0 + 1 < c1 ? (unsigned)(CH * (c0 + 1) + 8 * tid) * 8u : OOB, xb);
-    // chunks of this workgroup that need the exact path (bit c - c0), done after the loop
-    unsigned *bad_mask = sbad + 4;
-    if (tid < 16) bad_mask[tid] = 0u;
+    v2f ha, hb;
+    load8b(rx, main_off(0), xa);
+    ha = ldh(halo_off(0));
+    load8b(rx, main_off(1), xb);
+    hb = ldh(halo_off(1));
 
     // B operand: lane column n = r32 -> segment sg = n & 15, component n >> 4
     const int sg = r32 & 15, comp = r32 >> 4;
-    auto step = [&](long long c, v4f (&xv)[4]) {
+    auto step = [&](long long k, v4f (&xv)[4], v2f &hv) {
+        const long long c = w + k * G;
         __syncthreads();   // the previous chunk's MFMA reads are done
-        if (tid < 8) {
-            const unsigned char *hs = halo + ((c - 1) & 1) * 6 * HPB + poff(8 * tid);
-#pragma unroll
-            for (int p = 0; p < 6; p++)
-                *reinterpret_cast<u32x4 *>(planes + p * PLB + poff(8 * tid)) =
-                    *reinterpret_cast<const u32x4 *>(hs + p * HPB);
+        const int cs = (int)(k % 3);
+        // chunk 0's halo planes came from the history in the prologue
+        if (tid < 64 && c != 0) {
+            put1(planes, PLB, tid, hv);
+            if (unsafe_bits(hv.x) | unsafe_bits(hv.y)) atomicOr(&sbad[cs], 1u);
         }
         put8(planes, PLB, 64 + 8 * tid, xv);
-        if (tid >= NT - 8) put8(halo + (c & 1) * 6 * HPB, HPB, 8 * (tid - (NT - 8)), xv);
-        const int cs = (int)(c % 3);
-        if (unsafe4(xv[0]) | unsafe4(xv[1]) | unsafe4(xv[2]) | unsafe4(xv[3]))
-            atomicOr(&sbad[cs], tid >= NT - 8 ? 3u : 1u);
-        if (tid == 0) sbad[(cs + 1) % 3] = 0u;   // chunk c+1's slot (last read in step c-2)
-        load8b(rx, c + 2 < c1 ? (unsigned)(CH * (c + 2) + 8 * tid) * 8u : OOB, xv);
+        if (unsafe4(xv[0]) | unsafe4(xv[1]) | unsafe4(xv[2]) | unsafe4(xv[3])) atomicOr(&sbad[cs], 1u);
+        if (tid == 0) sbad[(cs + 1) % 3] = 0u;   // step k+1's slot (last read in step k-2)
+        load8b(rx, main_off(k + 2), xv);
+        hv = ldh(halo_off(k + 2));
         __syncthreads();
-        if (tid == 0 && ((sbad[cs] & 1u) | (sbad[(cs + 2) % 3] & 2u)) && c < c1) {
-            const int k = (int)(c - c0);
-            bad_mask[k >> 5] |= 1u << (k & 31);
-        }
+        if (tid == 0 && sbad[cs] && c < nch) bad_mask[k >> 5] |= 1u << (k & 31);
 
         f32x16 C[NA];
 #pragma unroll
@@ -322,15 +325,15 @@ __global__ __launch_bounds__(NT, CC ? 2 : 3) void k_firfilt_mx(const v2f *__rest
             const v4f r = CC ? v4f{a.x * sre - a.y * sim, a.x * sim + a.y * sre, a.z * sre - a.w * sim,
                                    a.z * sim + a.w * sre}
                              : a * sre;   // crcf: real scale per component (firfilt.c:337)
-            __builtin_amdgcn_raw_buffer_store_b128(r, ry, c < c1 ? o0 + 8u * o : OOB, 0, 2);
+            __builtin_amdgcn_raw_buffer_store_b128(r, ry, c < nch ? o0 + 8u * o : OOB, 0, 2);
         }
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
         __builtin_amdgcn_wave_barrier();
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
     };
-    for (long long c = c0; c < c1; c += 2) {
-        step(c, xa);
-        step(c + 1, xb);
+    for (long long k = 0; k < cnt; k += 2) {
+        step(k, xa, ha);
+        step(k + 1, xb, hb);
     }
     // the range guard's chunks: the exact float32 outputs overwrite what the
     // matrix path stored for them.  Only workgroup-scope ordering is needed
@@ -344,9 +347,9 @@ __global__ __launch_bounds__(NT, CC ? 2 : 3) void k_firfilt_mx(const v2f *__rest
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
         __syncthreads();
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
-        for (int k = 0; k < (int)(c1 - c0); k++)
+        for (int k = 0; k < (int)cnt; k++)
             if (bad_mask[k >> 5] & (1u << (k & 31)))
-                exact_chunk_c<CC>(win, x, n, y, hpad, hlen, CH * (c0 + k) + 8 * tid, 8, sre, sim);
+                exact_chunk_c<CC>(win, x, n, y, hpad, hlen, CH * (w + k * G) + 8 * tid, 8, sre, sim);
     }
 }
 
@@ -357,27 +360,12 @@ constexpr int CHR = 4096;
 constexpr int SPANR = CHR + 64;
 constexpr int PLBR = SPANR * 2 + 16 * (SPANR / 32);   // 10400
 constexpr int SSTRR = 36;                              // floats per staged segment (32 + pad)
-constexpr int LDS_BYTES_R = 3 * PLBR + 2 * 3 * HPB + 4 * 32 * SSTRR * 4;
+constexpr int LDS_BYTES_R = 3 * PLBR + 4 * 32 * SSTRR * 4;
 
 __device__ __forceinline__ float rsample_at(const float *__restrict__ win, const float *__restrict__ x, long long n,
                                             long long t)
 {
     return t < 0 ? win[64 + t] : (t < n ? x[t] : 0.f);
-}
-// 16 real samples from s (a multiple of 8)
-__device__ __forceinline__ void load16r(const float *__restrict__ win, const float *__restrict__ x, long long n,
-                                        long long s, v4f (&v)[4])
-{
-    if (s >= 0 && s + 16 <= n) {
-        const v4f *p = reinterpret_cast<const v4f *>(x + s);
-#pragma unroll
-        for (int q = 0; q < 4; q++) v[q] = p[q];
-    } else {
-#pragma unroll
-        for (int q = 0; q < 4; q++)
-            v[q] = v4f{rsample_at(win, x, n, s + 4 * q), rsample_at(win, x, n, s + 4 * q + 1),
-                       rsample_at(win, x, n, s + 4 * q + 2), rsample_at(win, x, n, s + 4 * q + 3)};
-    }
 }
 // 8 real samples (v4f pair) into the three planes at pos (a multiple of 8)
 __device__ __forceinline__ void put8r(unsigned char *planes, int pstride, int pos, v4f a, v4f b)
@@ -394,6 +382,20 @@ __device__ __forceinline__ void put8r(unsigned char *planes, int pstride, int po
                          __builtin_bit_cast(unsigned, t[p][2]), __builtin_bit_cast(unsigned, t[p][3])};
         *reinterpret_cast<u32x4 *>(planes + p * pstride + o) = w;
     }
+}
+
+// 4 real samples into the three planes at pos (a multiple of 4)
+__device__ __forceinline__ void put4r(unsigned char *planes, int pstride, int pos, v4f a)
+{
+    bf16x2 t[3][2];
+    split3(v2f{a.x, a.y}, t[0][0], t[1][0], t[2][0]);
+    split3(v2f{a.z, a.w}, t[0][1], t[1][1], t[2][1]);
+    const int o = poff(pos);
+    typedef unsigned u32x2 __attribute__((ext_vector_type(2)));
+#pragma unroll
+    for (int p = 0; p < 3; p++)
+        *reinterpret_cast<u32x2 *>(planes + p * pstride + o) =
+            u32x2{__builtin_bit_cast(unsigned, t[p][0]), __builtin_bit_cast(unsigned, t[p][1])};
 }
 
 __device__ __attribute__((noinline)) void exact_chunk_r(const float *__restrict__ win, const float *__restrict__ x,
@@ -419,19 +421,19 @@ __device__ __forceinline__ void load16rb(__amdgpu_buffer_rsrc_t rx, unsigned off
 __global__ __launch_bounds__(NT, 3) void k_firfilt_mx_r(const float *__restrict__ win, const float *__restrict__ x,
                                                        long long n, float *__restrict__ y,
                                                        const float *__restrict__ hpad, float sre, long long nch,
-                                                       long long cpw, int hlen)
+                                                       int hlen)
 {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     unsigned *sbad = reinterpret_cast<unsigned *>(smem + LDS_BYTES_R);   // as k_firfilt_mx
     unsigned char *planes = smem;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int r32 = lane & 31, hh = lane >> 5;
-    unsigned char *halo = smem + 3 * PLBR;
-    float *stage = reinterpret_cast<float *>(smem + 3 * PLBR + 2 * 3 * HPB) + wave * 32 * SSTRR;
-    const long long c0 = (long long)blockIdx.x * cpw;
-    long long c1 = c0 + cpw;
-    if (c1 > nch) c1 = nch;
-    if (c0 >= c1) return;
+    float *stage = reinterpret_cast<float *>(smem + 3 * PLBR) + wave * 32 * SSTRR;
+    // grid-stride chunks, each with its own 64-sample halo (lanes 0..15, four
+    // samples each), as k_firfilt_mx
+    const long long G = gridDim.x, w = blockIdx.x;
+    if (w >= nch) return;
+    const long long cnt = (nch - w + G - 1) / G;
 
     bf16x8 A[3][6];
 #pragma unroll
@@ -451,53 +453,48 @@ __global__ __launch_bounds__(NT, 3) void k_firfilt_mx_r(const float *__restrict_
         for (int p = 0; p < 3; p++)
             A[p][s] = bf16x8{t[p][0].x, t[p][0].y, t[p][1].x, t[p][1].y, t[p][2].x, t[p][2].y, t[p][3].x, t[p][3].y};
     }
-    // halo of the first chunk: 64 samples by threads 0..3 (16 each)
     if (tid < 3) sbad[tid] = 0u;
-    __syncthreads();
-    if (tid < 4) {
-        v4f v[4];
-        load16r(win, x, n, CHR * c0 - 64 + 16 * tid, v);
-        unsigned char *hb = halo + ((c0 - 1) & 1) * 3 * HPB;
-        put8r(hb, HPB, 16 * tid, v[0], v[1]);
-        put8r(hb, HPB, 16 * tid + 8, v[2], v[3]);
-        if (unsafe4(v[0]) | unsafe4(v[1]) | unsafe4(v[2]) | unsafe4(v[3])) atomicOr(&sbad[(c0 + 2) % 3], 2u);
-    }
-    // branch-free memory operations in the loop, as k_firfilt_mx
+    unsigned *bad_mask = sbad + 4;
+    if (tid < 16) bad_mask[tid] = 0u;
     const __amdgpu_buffer_rsrc_t rx = __builtin_amdgcn_make_buffer_rsrc((void *)x, (short)0, (int)(n * 4), 0x00020000);
     const __amdgpu_buffer_rsrc_t ry = __builtin_amdgcn_make_buffer_rsrc((void *)y, (short)0, (int)(n * 4), 0x00020000);
     const unsigned OOB = 0xfffff000u;
-    v4f xa[4], xb[4];
-    load16rb(rx, (unsigned)(CHR * c0 + 16 * tid) * 4u, xa);
-    load16rb(rx, c0 + 1 < c1 ? (unsigned)(CHR * (c0 + 1) + 16 * tid) * 4u : OOB, xb);
-    unsigned *bad_mask = sbad + 4;
-    if (tid < 16) bad_mask[tid] = 0u;
+    auto main_off = [&](long long k) -> unsigned {
+        const long long c = w + k * G;
+        return c < nch ? (unsigned)(CHR * c + 16 * tid) * 4u : OOB;
+    };
+    auto halo_off = [&](long long k) -> unsigned {
+        const long long c = w + k * G;
+        return (c > 0 && c < nch && tid < 16) ? (unsigned)(CHR * c - 64 + 4 * tid) * 4u : OOB;
+    };
+    __syncthreads();
+    if (w == 0 && tid < 16) {
+        const v4f hv = {win[4 * tid], win[4 * tid + 1], win[4 * tid + 2], win[4 * tid + 3]};
+        put4r(planes, PLBR, 4 * tid, hv);
+        if (unsafe4(hv)) atomicOr(&sbad[0], 1u);
+    }
+    v4f xa[4], xb[4], ha, hb;
+    load16rb(rx, main_off(0), xa);
+    ha = __builtin_amdgcn_raw_buffer_load_b128(rx, halo_off(0), 0, 0);
+    load16rb(rx, main_off(1), xb);
+    hb = __builtin_amdgcn_raw_buffer_load_b128(rx, halo_off(1), 0, 0);
     const int sg = r32;   // B column = segment
-    auto step = [&](long long c, v4f (&xv)[4]) {
+    auto step = [&](long long k, v4f (&xv)[4], v4f &hv) {
+        const long long c = w + k * G;
         __syncthreads();
-        if (tid < 8) {
-            const unsigned char *hs = halo + ((c - 1) & 1) * 3 * HPB + poff(8 * tid);
-#pragma unroll
-            for (int p = 0; p < 3; p++)
-                *reinterpret_cast<u32x4 *>(planes + p * PLBR + poff(8 * tid)) =
-                    *reinterpret_cast<const u32x4 *>(hs + p * HPB);
+        const int cs = (int)(k % 3);
+        if (tid < 16 && c != 0) {
+            put4r(planes, PLBR, 4 * tid, hv);
+            if (unsafe4(hv)) atomicOr(&sbad[cs], 1u);
         }
         put8r(planes, PLBR, 64 + 16 * tid, xv[0], xv[1]);
         put8r(planes, PLBR, 64 + 16 * tid + 8, xv[2], xv[3]);
-        if (tid >= NT - 4) {
-            unsigned char *hb = halo + (c & 1) * 3 * HPB;
-            put8r(hb, HPB, 16 * (tid - (NT - 4)), xv[0], xv[1]);
-            put8r(hb, HPB, 16 * (tid - (NT - 4)) + 8, xv[2], xv[3]);
-        }
-        const int cs = (int)(c % 3);
-        if (unsafe4(xv[0]) | unsafe4(xv[1]) | unsafe4(xv[2]) | unsafe4(xv[3]))
-            atomicOr(&sbad[cs], tid >= NT - 4 ? 3u : 1u);
+        if (unsafe4(xv[0]) | unsafe4(xv[1]) | unsafe4(xv[2]) | unsafe4(xv[3])) atomicOr(&sbad[cs], 1u);
         if (tid == 0) sbad[(cs + 1) % 3] = 0u;
-        load16rb(rx, c + 2 < c1 ? (unsigned)(CHR * (c + 2) + 16 * tid) * 4u : OOB, xv);
+        load16rb(rx, main_off(k + 2), xv);
+        hv = __builtin_amdgcn_raw_buffer_load_b128(rx, halo_off(k + 2), 0, 0);
         __syncthreads();
-        if (tid == 0 && ((sbad[cs] & 1u) | (sbad[(cs + 2) % 3] & 2u)) && c < c1) {
-            const int k = (int)(c - c0);
-            bad_mask[k >> 5] |= 1u << (k & 31);
-        }
+        if (tid == 0 && sbad[cs] && c < nch) bad_mask[k >> 5] |= 1u << (k & 31);
         f32x16 C = {};
 #pragma unroll
         for (int s = 0; s < 6; s++) {
@@ -523,15 +520,15 @@ __global__ __launch_bounds__(NT, 3) void k_firfilt_mx_r(const float *__restrict_
         for (int q = 0; q < 4; q++) {
             const int o = 4 * (lane + 64 * q);
             const v4f a = *reinterpret_cast<const v4f *>(stage + (o >> 5) * SSTRR + (o & 31)) * sre;
-            __builtin_amdgcn_raw_buffer_store_b128(a, ry, c < c1 ? o0 + 4u * o : OOB, 0, 2);
+            __builtin_amdgcn_raw_buffer_store_b128(a, ry, c < nch ? o0 + 4u * o : OOB, 0, 2);
         }
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
         __builtin_amdgcn_wave_barrier();
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
     };
-    for (long long c = c0; c < c1; c += 2) {
-        step(c, xa);
-        step(c + 1, xb);
+    for (long long k = 0; k < cnt; k += 2) {
+        step(k, xa, ha);
+        step(k + 1, xb, hb);
     }
     __syncthreads();
     unsigned anybad = 0;
@@ -541,9 +538,9 @@ __global__ __launch_bounds__(NT, 3) void k_firfilt_mx_r(const float *__restrict_
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
         __syncthreads();
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
-        for (int k = 0; k < (int)(c1 - c0); k++)
+        for (int k = 0; k < (int)cnt; k++)
             if (bad_mask[k >> 5] & (1u << (k & 31)))
-                exact_chunk_r(win, x, n, y, hpad, hlen, CHR * (c0 + k) + 16 * tid, 16, sre);
+                exact_chunk_r(win, x, n, y, hpad, hlen, CHR * (w + k * G) + 16 * tid, 16, sre);
     }
 }
 
@@ -551,25 +548,6 @@ __global__ __launch_bounds__(NT, 3) void k_firfilt_mx_r(const float *__restrict_
 
 // Returns 1 if the call was handled on the matrix cores: rrrf, crcf or cccf,
 // 33..64 taps (HP = 64, one chunk), not in place, 16-byte aligned x and y.
-// Chunks per workgroup: each workgroup streams a contiguous segment of cpw
-// chunks and all of them run at once, so the segment length is the stride
-// between concurrent accesses.  An even cpw put those strides on a power-of-
-// two multiple of the chunk size and the segments onto the same HBM channels:
-// cpw 172 ran 12-15 % slower than 171 or 173 (2^28 samples, tools/mb/
-// mb_firmx_sweep.hip).  So cpw is odd; an odd count leaves each workgroup one
-// step past its last chunk, which the loop's range checks turn into no-ops.
-// At most 511: the per-workgroup guard mask holds 512 chunks (16 words after
-// the three guard slots: the kernels' dynamic LDS carries 80 extra bytes).
-static long long odd_cpw(long long nch, long long nwg)
-{
-    const long long cpw = ((nch + nwg - 1) / nwg) | 1;
-    if (cpw > 511) {
-        fprintf(stderr, "error: firfilt: %lld chunks per workgroup exceed the guard mask\n", cpw);
-        exit(1);
-    }
-    return cpw;
-}
-
 // Launches cover at most 2^28 complex / 2^29 real samples (2 GiB) so the
 // range-checked load offsets fit 32 bits; a later launch takes its 64-sample
 // history straight from the preceding input.
@@ -579,26 +557,22 @@ static void launch_mx(const lqk_fir_desc *d, const void *hist, const void *x, lo
     if (d->kind == 0) {   // rrrf: 4096-output chunks, three workgroups per CU
         const long long nch = (n + CHR - 1) / CHR;
         const long long nwg = nch < 768 ? nch : 768;
-        const long long cpw = odd_cpw(nch, nwg);
-        hipLaunchKernelGGL(k_firfilt_mx_r, dim3((unsigned)((nch + cpw - 1) / cpw)), dim3(NT), LDS_BYTES_R + 80, st,
-                           (const float *)hist, (const float *)x, n, (float *)y, (const float *)d->hpad, d->scale_re,
-                           nch, cpw, (int)d->hlen);
+        hipLaunchKernelGGL(k_firfilt_mx_r, dim3((unsigned)nwg), dim3(NT), LDS_BYTES_R + 80, st, (const float *)hist,
+                           (const float *)x, n, (float *)y, (const float *)d->hpad, d->scale_re, nch, (int)d->hlen);
         LQ_CHECK_LAUNCH();
         return;
     }
     const bool cc = d->kind == 2;
     const long long nch = (n + CH - 1) / CH;
     const long long wgs = cc ? 512 : 768;   // resident workgroups (two / three per CU)
-    const long long nwg = nch < wgs ? nch : wgs;
-    const long long cpw = odd_cpw(nch, nwg);
-    const dim3 grid((unsigned)((nch + cpw - 1) / cpw));
+    const dim3 grid((unsigned)(nch < wgs ? nch : wgs));
     if (cc)
         hipLaunchKernelGGL(k_firfilt_mx<true>, grid, dim3(NT), lds_bytes_mx<true>() + 80, st, (const v2f *)hist,
-                           (const v2f *)x, n, (v2f *)y, (const float *)d->hpad, d->scale_re, d->scale_im, nch, cpw,
+                           (const v2f *)x, n, (v2f *)y, (const float *)d->hpad, d->scale_re, d->scale_im, nch,
                            (int)d->hlen);
     else
         hipLaunchKernelGGL(k_firfilt_mx<false>, grid, dim3(NT), lds_bytes_mx<false>() + 80, st, (const v2f *)hist,
-                           (const v2f *)x, n, (v2f *)y, (const float *)d->hpad, d->scale_re, d->scale_im, nch, cpw,
+                           (const v2f *)x, n, (v2f *)y, (const float *)d->hpad, d->scale_re, d->scale_im, nch,
                            (int)d->hlen);
     LQ_CHECK_LAUNCH();
 }
