@@ -58,10 +58,14 @@ typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
 constexpr int NT = 256;           // 4 waves
 constexpr int CH = 2048;          // outputs per chunk (4 tiles of 512)
 constexpr int SPAN = CH + 64;     // samples a chunk's tiles read (64-sample halo)
-constexpr int PLB = SPAN * 2 + 16 * (SPAN / 32);   // bytes per plane (5280)
+// bytes per plane: the span (5280) rounded up to 256 B, so the planes of the
+// two components start on the same bank -- with the 5280-byte stride every
+// 16-lane group of a B-operand ds_read_b128 had a 2-way bank conflict
+// (SQ_LDS_BANK_CONFLICT was half of the LDS-active cycles)
+constexpr int PLB = (SPAN * 2 + 16 * (SPAN / 32) + 255) & ~255;   // 5376
 constexpr int SSTR = 68;          // floats per staged segment (32 x re/im + pad)
-// crcf: one staged accumulator per wave (49088 B: three workgroups per CU);
-// cccf: two (the real- and imaginary-tap products; 66496 B: two per CU)
+// crcf: one staged accumulator per wave (49664 B: three workgroups per CU);
+// cccf: two (the real- and imaginary-tap products; 67072 B: two per CU)
 template <bool CC>
 constexpr int lds_bytes_mx() { return 6 * PLB + (CC ? 2 : 1) * 4 * 16 * SSTR * 4; }
 

@@ -138,9 +138,7 @@ __global__ __launch_bounds__(NT) void k_resamp(lqk_rs_plan pl, unsigned long lon
 }
 
 // Tiled form (L even, table in LDS).  A workgroup owns TIN consecutive inputs:
-//  1. the input window [i0-L-1, i0+TIN) goes to LDS twice, the second copy
-//     shifted by one sample, so every (L+1)-sample window starts 16-byte
-//     aligned in one of them;
+//  1. the input window [i0-L-1, i0+TIN) goes to LDS;
 //  2. each lane replays the float32 timing of its RIN inputs and writes one
 //     descriptor per output (mu, input, bank) at the output's index in the
 //     tile -- the output list is now dense;
@@ -150,6 +148,14 @@ __global__ __launch_bounds__(NT) void k_resamp(lqk_rs_plan pl, unsigned long lon
 //     window one input older and h_0), so both states are one dot product,
 //     and the stores are coalesced.  Outputs beyond CAP per tile take more
 //     rounds of 2-3.
+// LDS reads of step 3 are 8-byte (one tap pair, one sample).  A ds_read_b64
+// is serviced in two 32-lane groups over all 64 banks: 32 consecutive
+// outputs read a window span of ~32 samples (256 B, conflict-free), and the
+// pair table is laid out pair-major, T2[p][b] at 8 ((2p + (b & 1)) RS + b/2):
+// consecutive outputs step the bank by ~npfb/r, never by 1, so the 32 rows a
+// group reads sit on 32 distinct 8-byte slots.  (The earlier 16-byte reads of
+// whole tap rows and of a doubled, shifted window copy were 2-way conflicted
+// in every 16-lane group: half the LDS cycles of the kernel.)
 // plan position g = gt + d for a tile base gt (entry jt, cycles ct already
 // resolved once per tile) and a small lane offset d: 32-bit arithmetic
 __device__ __forceinline__ void rs_lookup_near(const lqk_rs_plan &pl, unsigned long long gt, unsigned long long jt,
@@ -175,6 +181,16 @@ __device__ __forceinline__ void rs_lookup_near(const lqk_rs_plan &pl, unsigned l
     K = (unsigned long long)e.K + c * pl.Q;
 }
 
+template <int L>
+constexpr int rs2_tin() { return NT * 4; }
+// LDS bytes of k_resamp2<L, S>: window copy, output descriptors, pair table
+template <int L, typename S>
+inline size_t rs2_lds_bytes(int npfb)
+{
+    constexpr int TS = rs2_tin<L>() + L + 2;
+    return (size_t)(TS + 2) * sizeof(S) + 1536 * 8 + (size_t)2 * (L + 1) * ((npfb >> 1) + 1) * sizeof(float2);
+}
+
 template <int L, typename S>
 __global__ __launch_bounds__(NT) void k_resamp2(lqk_rs_plan pl, unsigned long long g0, unsigned long long K0,
                                                 int npfb, float del, const float2 *__restrict__ taps2,
@@ -182,32 +198,21 @@ __global__ __launch_bounds__(NT) void k_resamp2(lqk_rs_plan pl, unsigned long lo
                                                 long long n, S *__restrict__ y)
 {
     constexpr int RIN = 4;
-    constexpr int TIN = NT * RIN;
-    constexpr int LP = (L + 2 + 1) & ~1;         // pair-table stride (>= L+1, even)
-    constexpr int LPS = LP + 2;                  // LDS row stride: 16 bytes of pad spread the banks
-    // rows 16 apart would share bank groups (consecutive outputs step the bank
-    // by ~npfb/r): shift every 16-row block by 4 more 16-byte slots
-    auto rowoff = [](int b) { return b * LPS + 8 * (b >> 4); };
-    constexpr int NW = LP / 2;                   // 16-byte reads per window / per tap row
-    constexpr int TS = TIN + L + 2;              // tile samples per copy (+1 for the shifted copy)
-    constexpr int CS = TS + 2;                   // copy stride (even: both copies 16-byte aligned)
+    constexpr int TIN = rs2_tin<L>();
+    constexpr int LP = (L + 2 + 1) & ~1;         // pair stride of taps2 (host layout, >= L+1)
+    constexpr int TS = TIN + L + 2;              // tile samples
+    constexpr int CS = TS + 2;                   // copy size (keeps what follows 16-byte aligned)
     constexpr int CAP = 1536;                    // outputs per round
-    typedef float v4f __attribute__((ext_vector_type(4)));
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     S *cp0 = reinterpret_cast<S *>(smem);
-    S *cp1 = cp0 + CS;
-    uint2 *desc = reinterpret_cast<uint2 *>(cp1 + CS);
+    uint2 *desc = reinterpret_cast<uint2 *>(cp0 + CS);
     float2 *tpl = reinterpret_cast<float2 *>(desc + CAP);
+    const int RS = (npfb >> 1) + 1;              // 8-byte slots per half row
 
     const int tid = threadIdx.x;
-    // pair p = 2q + e of a row goes to floats 4q + e (h_b) and 4q + 2 + e (h_b+1),
-    // so a 16-byte read gives (h_b[2q], h_b[2q+1], h_b+1[2q], h_b+1[2q+1])
-    for (int t = tid; t < (npfb + 1) * LP; t += NT) {
-        const int b = t / LP, p = t % LP;
-        float *row = reinterpret_cast<float *>(tpl + rowoff(b));
-        const float2 v = taps2[t];
-        row[4 * (p >> 1) + (p & 1)] = v.x;
-        row[4 * (p >> 1) + 2 + (p & 1)] = v.y;
+    for (int t = tid; t < (npfb + 1) * (L + 1); t += NT) {
+        const int b = t / (L + 1), p = t % (L + 1);
+        tpl[(2 * p + (b & 1)) * RS + (b >> 1)] = taps2[b * LP + p];
     }
     const float fnpfb = (float)npfb;
     const long long ntiles = (n + TIN - 1) / TIN;
@@ -273,7 +278,6 @@ __global__ __launch_bounds__(NT) void k_resamp2(lqk_rs_plan pl, unsigned long lo
                 if constexpr (sizeof(S) == 8) v = make_float2(a.x + b.x, a.y + b.y);
                 else v = a + b;
                 cp0[t] = v;
-                cp1[t + 1] = v;
             }
         }
         const unsigned long long Kb = cur.Kb;
@@ -319,46 +323,32 @@ __global__ __launch_bounds__(NT) void k_resamp2(lqk_rs_plan pl, unsigned long lo
                 const float mu = __uint_as_float(d.x);
                 const int iloc = (int)(d.y & 4095u);
                 const int bb = (int)(d.y >> 12);
-                const int sw = iloc + 1;                  // tile index of x[i-L]
-                const S *wp = (sw & 1) ? cp1 + sw + 1 : cp0 + sw;
-                const float2 *tp = tpl + rowoff(bb);
+                const S *wp = cp0 + iloc + 1;             // x[i-L]
+                const float2 *tp = tpl + (bb & 1) * RS + (bb >> 1);
+                // reads in two batches, each issued before its math: two LDS
+                // round trips per output, half the registers of one batch
+                constexpr int HB = (L + 2) / 2;
                 S acc{};
-                // the tap row and the window are read in two batches of NW/2
-                // 16-byte pairs, all reads of a batch issued before its math:
-                // two LDS round trips per output instead of one per pair
-                constexpr int HB = NW / 2 > 0 ? NW / 2 : 1;
 #pragma unroll
-                for (int q0 = 0; q0 < NW; q0 += HB) {
-                    v4f tt[HB];
-                    typedef typename std::conditional<sizeof(S) == 8, v4f, float2>::type WT;
-                    WT ww[HB];
+                for (int p0 = 0; p0 <= L; p0 += HB) {
+                    float2 tt[HB];
+                    S ww[HB];
 #pragma unroll
-                    for (int k = 0; k < HB; k++) {
-                        if (q0 + k < NW) {
-                            tt[k] = *reinterpret_cast<const v4f *>(tp + 2 * (q0 + k));
-                            ww[k] = *reinterpret_cast<const WT *>(wp + 2 * (q0 + k));
+                    for (int k = 0; k < HB; k++)
+                        if (p0 + k <= L) {
+                            tt[k] = tp[2 * (p0 + k) * RS];
+                            ww[k] = wp[p0 + k];
                         }
-                    }
 #pragma unroll
                     for (int k = 0; k < HB; k++) {
-                        if (q0 + k >= NW) break;
-                        const v4f t = tt[k];
-                        if constexpr (sizeof(S) == 8) {    // two complex samples: one 16-byte read
-                            // packed: (c0, c1) = (t.x, t.y) + mu ((t.z, t.w) - (t.x, t.y)), then
-                            // acc += c0 w0 + c1 w1 as two v_pk_fma_f32 on (re, im)
-                            const v2f lo = {t.x, t.y}, hi = {t.z, t.w};
-                            const v2f c = lo + v2f{mu, mu} * (hi - lo);
-                            const v4f w = ww[k];
+                        if (p0 + k > L) break;
+                        const float c = tt[k].x + mu * (tt[k].y - tt[k].x);
+                        if constexpr (sizeof(S) == 8) {
                             v2f a2 = {acc.x, acc.y};
-                            a2 = v2f{c.x, c.x} * v2f{w.x, w.y} + a2;
-                            a2 = v2f{c.y, c.y} * v2f{w.z, w.w} + a2;
+                            a2 = v2f{c, c} * v2f{ww[k].x, ww[k].y} + a2;
                             acc = make_float2(a2.x, a2.y);
-                        } else {                           // two real samples: one 8-byte read
-                            const float c0 = t.x + mu * (t.z - t.x);
-                            const float c1 = t.y + mu * (t.w - t.y);
-                            const float2 w = ww[k];
-                            acc = rs_axpy(c0, w.x, acc);
-                            acc = rs_axpy(c1, w.y, acc);
+                        } else {
+                            acc = rs_axpy(c, ww[k], acc);
                         }
                     }
                 }
@@ -408,10 +398,8 @@ void launch_rs(const lqk_rs_plan &pl, unsigned long long g0, unsigned long long 
                const float2 *taps, const float2 *taps2, const S *hist, const S *x, long long n, S *y,
                hipStream_t st)
 {
-    constexpr int LP = (L + 2 + 1) & ~1;
-    constexpr int TIN = NT * 4;
-    const size_t lds2 =
-        (size_t)2 * (TIN + L + 4) * sizeof(S) + 1536 * 8 + ((size_t)(npfb + 1) * (LP + 2) + 8 * (npfb / 16 + 1)) * sizeof(float2);
+    constexpr int TIN = rs2_tin<L>();
+    const size_t lds2 = rs2_lds_bytes<L, S>(npfb);
     if (taps2 != nullptr && lds2 <= 64 * 1024 && pl.P < (1ull << 31) && pl.pre < (1ull << 62)) {
         const long long ntiles = (n + TIN - 1) / TIN;
         const unsigned nb = (unsigned)(ntiles < 1024 ? ntiles : 1024);   // persistent: ~4 per CU

@@ -3,7 +3,7 @@
 # sys/runtime traces with --pmc) over tools/prof_run.py.  Usage: pmc.sh <what> <tag>
 set -o pipefail
 cd "$(dirname "$0")/.."
-WHAT=${1:-pfb2}; TAG=${2:-pmc}
+WHAT=${1:-pfb2}; TAG=${2:-pmc}; SQONLY=${3:-}
 export TMPDIR=/tmp
 OUT=gpurun_out/$TAG; rm -rf $OUT; mkdir -p $OUT
 python -c "import __graft_entry__ as g; g.build()" > $OUT/build.log 2>&1 || exit 1
@@ -11,6 +11,8 @@ i=0
 while read -r CTRS; do
   [ -z "$CTRS" ] && continue
   i=$((i+1))
+  # third argument "sq": the two SQ passes only
+  [ -n "$SQONLY" ] && [ $i -gt 2 ] && continue
   timeout -k 10 300 rocprofv3 --pmc $CTRS --output-format csv -d $OUT/p$i -o run -- python3 tools/prof_run.py --what $WHAT --iters 2 > $OUT/p$i.log 2>&1 || { echo "pass $i failed"; tail -5 $OUT/p$i.log; exit 1; }
 done <<LIST
 SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS
@@ -31,7 +33,7 @@ for r in rows:
     agg[k][r["Counter_Name"]] += float(r["Counter_Value"])
     cnt[k].add(r.get("Dispatch_Id", ""))
 for k, d in agg.items():
-    if "pfb2" in k or "firfilt" in k or "resamp" in k:
+    if "pfb2" in k or "firfilt" in k or "resamp" in k or "fftfilt" in k:
         print(k, len(cnt[k]), {c: "%.4g" % (v / max(1, len(cnt[k]))) for c, v in d.items()})
 PY
 done

@@ -13,7 +13,7 @@ import liquidmi as LQ  # noqa: E402
 
 p = argparse.ArgumentParser()
 p.add_argument("--iters", type=int, default=3)
-p.add_argument("--what", default="both", choices=["both", "all", "pfb2", "fir", "resamp"])
+p.add_argument("--what", default="both", choices=["both", "all", "pfb2", "fir", "resamp", "fftfilt"])
 a = p.parse_args()
 s = torch.cuda.Stream()
 if a.what in ("both", "all", "pfb2"):
@@ -48,5 +48,15 @@ if a.what in ("all", "resamp"):
         r.execute_block_dev(x.data_ptr(), n, y.data_ptr())
     r.synchronize()
     r.destroy()
+if a.what in ("all", "fftfilt"):
+    n = 1 << 26
+    x = torch.rand(2 * n, device="cuda") - 0.5
+    y = torch.empty(2 * n, device="cuda")
+    ff = LQ.FftFilt((torch.rand(512) - 0.5).numpy(), 2048)
+    ff.set_stream(s.cuda_stream)
+    for _ in range(a.iters):
+        ff.execute_block_dev(x.data_ptr(), n, y.data_ptr())
+    torch.cuda.synchronize()
+    ff.destroy()
 torch.cuda.synchronize()
 print("done")
