@@ -137,17 +137,22 @@ __global__ __launch_bounds__(NT) void k_resamp(lqk_rs_plan pl, unsigned long lon
     }
 }
 
-// Tiled form (L even, table in LDS).  A workgroup owns TIN consecutive inputs:
-//  1. the input window [i0-L-1, i0+TIN) goes to LDS;
+// Tiled form (L even, table in LDS).  A persistent workgroup (five per CU)
+// walks tiles of TIN consecutive inputs:
+//  1. the input window [i0-L-1, i0+TIN) goes to LDS from registers that were
+//     loaded two tiles earlier (two register sets alternate, so two tiles of
+//     loads are in flight while one is evaluated: 0.226 -> 0.218 ms);
 //  2. each lane replays the float32 timing of its RIN inputs and writes one
 //     descriptor per output (mu, input, bank) at the output's index in the
-//     tile -- the output list is now dense;
+//     tile -- the output list is now dense (writes are branch-free: outputs
+//     outside the round go to a sink slot);
 //  3. lanes take consecutive outputs: y = sum_p c[p] x[i-L+p], p <= L, with
-//     c[p] = T.x + mu (T.y - T.x) from the pair table T2 (bank b: h_b, h_b+1
-//     on the same window; bank npfb: the BOUNDARY pair h_{npfb-1} on the
-//     window one input older and h_0), so both states are one dot product,
-//     and the stores are coalesced.  Outputs beyond CAP per tile take more
-//     rounds of 2-3.
+//     c[p] = T.x + mu T.d from the table (T.x, T.d = T.y - T.x) of pairs T2
+//     (bank b: h_b, h_b+1 on the same window; bank npfb: the BOUNDARY pair
+//     h_{npfb-1} on the window one input older and h_0), so both states are
+//     one dot product, and the stores (32-bit offsets through a buffer
+//     descriptor over the round's outputs) are coalesced.  Outputs beyond CAP
+//     per tile take more rounds of 2-3.
 // LDS reads of step 3 are 8-byte (one tap pair, one sample).  A ds_read_b64
 // is serviced in two 32-lane groups over all 64 banks: 32 consecutive
 // outputs read a window span of ~32 samples (256 B, conflict-free), and the
@@ -156,6 +161,10 @@ __global__ __launch_bounds__(NT) void k_resamp(lqk_rs_plan pl, unsigned long lon
 // group reads sit on 32 distinct 8-byte slots.  (The earlier 16-byte reads of
 // whole tap rows and of a doubled, shifted window copy were 2-way conflicted
 // in every 16-lane group: half the LDS cycles of the kernel.)
+// Measured and dropped: a run of consecutive outputs per lane with the window
+// in registers (one LDS read per input instead of L+1 per output) -- the run
+// is a dependent chain and the reads conflict 4-way: 0.226 -> 0.265 ms;
+// 2048-input tiles (0.247 ms); six workgroups per CU (spills: 0.52 ms).
 // plan position g = gt + d for a tile base gt (entry jt, cycles ct already
 // resolved once per tile) and a small lane offset d: 32-bit arithmetic
 __device__ __forceinline__ void rs_lookup_near(const lqk_rs_plan &pl, unsigned long long gt, unsigned long long jt,
@@ -181,38 +190,47 @@ __device__ __forceinline__ void rs_lookup_near(const lqk_rs_plan &pl, unsigned l
     K = (unsigned long long)e.K + c * pl.Q;
 }
 
+#ifndef RS_RIN
+#define RS_RIN 4
+#endif
+#ifndef RS_BLK
+#define RS_BLK 5   // workgroups per CU (96 VGPRs: five waves per SIMD)
+#endif
 template <int L>
-constexpr int rs2_tin() { return NT * 4; }
+constexpr int rs2_tin() { return NT * RS_RIN; }
 // LDS bytes of k_resamp2<L, S>: window copy, output descriptors, pair table
 template <int L, typename S>
 inline size_t rs2_lds_bytes(int npfb)
 {
     constexpr int TS = rs2_tin<L>() + L + 2;
-    return (size_t)(TS + 2) * sizeof(S) + 1536 * 8 + (size_t)2 * (L + 1) * ((npfb >> 1) + 1) * sizeof(float2);
+    return (size_t)(TS + 2) * sizeof(S) + (rs2_tin<L>() * 3 / 2 + 2) * 8 + (size_t)2 * (L + 1) * ((npfb >> 1) + 1) * sizeof(float2);
 }
 
 template <int L, typename S>
-__global__ __launch_bounds__(NT) void k_resamp2(lqk_rs_plan pl, unsigned long long g0, unsigned long long K0,
+__global__ __launch_bounds__(NT, RS_BLK) void k_resamp2(lqk_rs_plan pl, unsigned long long g0, unsigned long long K0,
                                                 int npfb, float del, const float2 *__restrict__ taps2,
                                                 const S *__restrict__ hist, const S *__restrict__ x,
                                                 long long n, S *__restrict__ y)
 {
-    constexpr int RIN = 4;
+    constexpr int RIN = RS_RIN;
     constexpr int TIN = rs2_tin<L>();
     constexpr int LP = (L + 2 + 1) & ~1;         // pair stride of taps2 (host layout, >= L+1)
     constexpr int TS = TIN + L + 2;              // tile samples
     constexpr int CS = TS + 2;                   // copy size (keeps what follows 16-byte aligned)
-    constexpr int CAP = 1536;                    // outputs per round
+    constexpr int CAP = TIN + TIN / 2;           // outputs per round
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     S *cp0 = reinterpret_cast<S *>(smem);
     uint2 *desc = reinterpret_cast<uint2 *>(cp0 + CS);
-    float2 *tpl = reinterpret_cast<float2 *>(desc + CAP);
+    float2 *tpl = reinterpret_cast<float2 *>(desc + CAP + 2);   // desc[CAP]: sink of out-of-round outputs
     const int RS = (npfb >> 1) + 1;              // 8-byte slots per half row
 
     const int tid = threadIdx.x;
     for (int t = tid; t < (npfb + 1) * (L + 1); t += NT) {
         const int b = t / (L + 1), p = t % (L + 1);
-        tpl[(2 * p + (b & 1)) * RS + (b >> 1)] = taps2[b * LP + p];
+        const float2 v = taps2[b * LP + p];
+        // (h_b, h_b+1 - h_b): c = h_b + mu (h_b+1 - h_b) is one fma, the same
+        // float32 operations as before (the difference rounded once here)
+        tpl[(2 * p + (b & 1)) * RS + (b >> 1)] = make_float2(v.x, v.y - v.x);
     }
     const float fnpfb = (float)npfb;
     const long long ntiles = (n + TIN - 1) / TIN;
@@ -236,18 +254,14 @@ __global__ __launch_bounds__(NT) void k_resamp2(lqk_rs_plan pl, unsigned long lo
             return __builtin_bit_cast(S, __builtin_amdgcn_raw_buffer_load_b32(r, off, 0, 0));
     };
     struct Pre {
-        S xa[NXV], xb[NXV];
+        S xa[NXV];
         rs_state s;
         unsigned long long K, Kb, Ke;
     };
     auto fetch = [&](long long tile, Pre &f) {
         const long long i0 = tile * TIN;
 #pragma unroll
-        for (int u = 0; u < NXV; u++) {
-            const long long sx = i0 - L - 1 + tid + u * NT;
-            f.xa[u] = ld(rx, sx);
-            f.xb[u] = ld(rh, L + sx);
-        }
+        for (int u = 0; u < NXV; u++) f.xa[u] = ld(rx, i0 - L - 1 + tid + u * NT);
         const unsigned long long gt = g0 + (unsigned long long)i0;
         unsigned long long jt = gt, ct = 0;
         if (gt >= pl.pre) {
@@ -262,32 +276,35 @@ __global__ __launch_bounds__(NT) void k_resamp2(lqk_rs_plan pl, unsigned long lo
         rs_lookup_near(pl, gt, jt, ct, (unsigned)(tid * RIN), f.s, f.K);
     };
 
-    long long tile = blockIdx.x;
-    if (tile >= ntiles) return;
-    Pre cur;
-    fetch(tile, cur);
-    for (; tile < ntiles; tile += gridDim.x) {
+    const long long G = gridDim.x;
+    long long tile0 = blockIdx.x;
+    if (tile0 >= ntiles) return;
+    // two register sets, two tiles in flight while one is evaluated (the
+    // kernel waited on its loads with one); the loop is unrolled by two so a
+    // set is never copied, which would wait on its loads at once
+    Pre pa, pb;
+    fetch(tile0, pa);
+    fetch(tile0 + G, pb);
+    auto body = [&](long long tile, Pre &cur) {
         const long long i0 = tile * TIN;
         __syncthreads();                              // previous tile consumed
 #pragma unroll
         for (int u = 0; u < NXV; u++) {
             const int t = tid + u * NT;
-            if (t < TS) {
-                const S a = cur.xa[u], b = cur.xb[u];
-                S v;
-                if constexpr (sizeof(S) == 8) v = make_float2(a.x + b.x, a.y + b.y);
-                else v = a + b;
-                cp0[t] = v;
-            }
+            if (t < TS) cp0[t] = cur.xa[u];
+        }
+        if (i0 == 0 && tid <= L) {                    // samples before the call: the history
+            const long long sx = (long long)tid - L - 1;
+            cp0[tid] = ld(rh, L + sx);
         }
         const unsigned long long Kb = cur.Kb;
         const long long ntile = (long long)(cur.Ke - Kb);
         const rs_state slane = cur.s;
         const unsigned long long Klane = cur.K;
-        // in flight during this tile; unconditional (a tile past the end loads
-        // out of range: zeros, and plan positions any plan resolves) so the
-        // loads stay outstanding across the evaluation
-        fetch(tile + gridDim.x, cur);
+        // in flight during this tile and the next; unconditional (a tile past
+        // the end loads out of range: zeros, and plan positions any plan
+        // resolves) so the loads stay outstanding across the evaluation
+        fetch(tile + 2 * G, cur);
         const long long ia = i0 + (long long)tid * RIN;   // this lane's first input
         for (long long r0 = 0; r0 < ntile; r0 += CAP) {
             if (r0 > 0) __syncthreads();                   // previous round consumed
@@ -304,9 +321,8 @@ __global__ __launch_bounds__(NT) void k_resamp2(lqk_rs_plan pl, unsigned long lo
                             s.b = npfb;
                             break;
                         }
-                        if (o >= 0 && o < CAP)
-                            desc[o] = make_uint2(__float_as_uint(s.mu),
-                                                 (unsigned)iloc | ((unsigned)(s.st ? s.b : npfb) << 12));
+                        desc[(unsigned long long)o < (unsigned long long)CAP ? (int)o : CAP] =
+                            make_uint2(__float_as_uint(s.mu), (unsigned)iloc | ((unsigned)(s.st ? s.b : npfb) << 12));
                         o++;
                         rs_advance(s, del, fnpfb);
                         s.st = 1;
@@ -318,43 +334,42 @@ __global__ __launch_bounds__(NT) void k_resamp2(lqk_rs_plan pl, unsigned long lo
             __syncthreads();
             const int nr = (int)((ntile - r0) < CAP ? (ntile - r0) : CAP);
             S *yo = y + (Kb - K0) + r0;
-            for (int o = tid; o < nr; o += NT) {
-                const uint2 d = desc[o];
-                const float mu = __uint_as_float(d.x);
-                const int iloc = (int)(d.y & 4095u);
-                const int bb = (int)(d.y >> 12);
-                const S *wp = cp0 + iloc + 1;             // x[i-L]
+            auto dot = [&](const S *wv, int bb, float mu) -> S {
                 const float2 *tp = tpl + (bb & 1) * RS + (bb >> 1);
-                // reads in two batches, each issued before its math: two LDS
-                // round trips per output, half the registers of one batch
-                constexpr int HB = (L + 2) / 2;
                 S acc{};
 #pragma unroll
-                for (int p0 = 0; p0 <= L; p0 += HB) {
-                    float2 tt[HB];
-                    S ww[HB];
-#pragma unroll
-                    for (int k = 0; k < HB; k++)
-                        if (p0 + k <= L) {
-                            tt[k] = tp[2 * (p0 + k) * RS];
-                            ww[k] = wp[p0 + k];
-                        }
-#pragma unroll
-                    for (int k = 0; k < HB; k++) {
-                        if (p0 + k > L) break;
-                        const float c = tt[k].x + mu * (tt[k].y - tt[k].x);
-                        if constexpr (sizeof(S) == 8) {
-                            v2f a2 = {acc.x, acc.y};
-                            a2 = v2f{c, c} * v2f{ww[k].x, ww[k].y} + a2;
-                            acc = make_float2(a2.x, a2.y);
-                        } else {
-                            acc = rs_axpy(c, ww[k], acc);
-                        }
+                for (int p = 0; p <= L; p++) {
+                    const float2 t = tp[2 * p * RS];
+                    const float c = fmaf(mu, t.y, t.x);
+                    if constexpr (sizeof(S) == 8) {
+                        v2f a2 = {acc.x, acc.y};
+                        a2 = v2f{c, c} * v2f{wv[p].x, wv[p].y} + a2;
+                        acc = make_float2(a2.x, a2.y);
+                    } else {
+                        acc = rs_axpy(c, wv[p], acc);
                     }
                 }
-                yo[o] = acc;
+                return acc;
+            };
+            // stores through a descriptor over this round's outputs: 32-bit offsets
+            const __amdgpu_buffer_rsrc_t ry =
+                __builtin_amdgcn_make_buffer_rsrc((void *)yo, (short)0, nr * (int)sizeof(S), 0x00020000);
+            for (int o = tid; o < nr; o += NT) {
+                const uint2 d = desc[o];
+                const S v = dot(cp0 + (int)(d.y & 4095u) + 1, (int)(d.y >> 12), __uint_as_float(d.x));
+                if constexpr (sizeof(S) == 8) {
+                    typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
+                    __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2, v), ry, (unsigned)o * 8u, 0, 0);
+                } else {
+                    __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, v), ry, (unsigned)o * 4u, 0, 0);
+                }
             }
         }
+    };
+    for (long long tile = tile0; tile < ntiles; tile += 2 * G) {
+        body(tile, pa);
+        if (tile + G >= ntiles) break;
+        body(tile + G, pb);
     }
 }
 
@@ -402,7 +417,7 @@ void launch_rs(const lqk_rs_plan &pl, unsigned long long g0, unsigned long long 
     const size_t lds2 = rs2_lds_bytes<L, S>(npfb);
     if (taps2 != nullptr && lds2 <= 64 * 1024 && pl.P < (1ull << 31) && pl.pre < (1ull << 62)) {
         const long long ntiles = (n + TIN - 1) / TIN;
-        const unsigned nb = (unsigned)(ntiles < 1024 ? ntiles : 1024);   // persistent: ~4 per CU
+        const unsigned nb = (unsigned)(ntiles < 256 * RS_BLK ? ntiles : 256 * RS_BLK);   // persistent: RS_BLK per CU
         hipLaunchKernelGGL((k_resamp2<L, S>), dim3(nb), dim3(NT), lds2, st, pl, g0, K0, npfb, del, taps2, hist, x,
                            n, y);
         return;

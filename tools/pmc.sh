@@ -11,12 +11,13 @@ i=0
 while read -r CTRS; do
   [ -z "$CTRS" ] && continue
   i=$((i+1))
-  # third argument "sq": the two SQ passes only
-  [ -n "$SQONLY" ] && [ $i -gt 2 ] && continue
+  # third argument "sq": the three SQ passes only
+  [ -n "$SQONLY" ] && [ $i -gt 3 ] && continue
   timeout -k 10 300 rocprofv3 --pmc $CTRS --output-format csv -d $OUT/p$i -o run -- python3 tools/prof_run.py --what $WHAT --iters 2 > $OUT/p$i.log 2>&1 || { echo "pass $i failed"; tail -5 $OUT/p$i.log; exit 1; }
 done <<LIST
 SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS
 SQ_INSTS_VALU SQ_INSTS_LDS SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_LDS_BANK_CONFLICT SQ_WAIT_INST_LDS SQ_LDS_IDX_ACTIVE SQ_ACTIVE_INST_VMEM
+SQ_INSTS_SALU SQ_INSTS_SMEM SQ_ACTIVE_INST_SCA SQ_INSTS_BRANCH SQ_ACTIVE_INST_MISC SQ_INSTS_VALU_CVT_F32 SQ_INSTS_VALU_TRANS_F32 SQ_INSTS_VALU_INT32
 FETCH_SIZE
 WRITE_SIZE
 GRBM_GUI_ACTIVE GRBM_COUNT
