@@ -85,6 +85,122 @@ __global__ __launch_bounds__(NT) void k_pfb2_an(int m, const float *__restrict__
     }
 }
 
+// Polyphase pass for power-of-two M >= 64 (M != 1024, which has the fused
+// kernel of k_pfb2_fast.hip), followed by a batched transform over Y in
+// place.  Same column view as the fused kernel: in aligned coordinates
+// t' = t + p0 M/2 the stream is rows of M samples, column col feeds bin
+// j = M/2-1-col (lo) or 3M/2-1-col (hi), and row c completes blocks 2c + dA
+// and 2c + dA + 1 (dA = 0 lo, 1 hi) with the L = 2m taps of bin j for the
+// even block and of bin j ^ M/2 for the odd one:
+//     X_b[j] = sum_n h[i + nM] row[c - n][col]
+// A workgroup owns a slice of min(M, 256) columns (one per lane) and a run
+// of S rows; L-1 rows before the run warm its register ring up.  Rows are
+// read once per slice and run (2 KB coalesced per row and workgroup), a
+// group of L rows is prefetched while the previous group is evaluated, and
+// X goes straight into Y (coalesced: consecutive columns are consecutive
+// bins, reversed), where the batched transform then runs in place.
+// Samples come through two range-checked descriptors (history: HL samples,
+// x: n_in), each sample in range in at most one of them.
+template <int L>
+__global__ __launch_bounds__(256) void k_pfb2_poly(int M, int nsl, const float *__restrict__ hsub,
+                                                  const float2 *__restrict__ hist, const float2 *__restrict__ x,
+                                                  int n_in, int p0, int nb, int cmin, int cmax, int S,
+                                                  float2 *__restrict__ Y)
+{
+    const int M2 = M >> 1, HL = L * M - M2;
+    const int sl = (int)(blockIdx.x % (unsigned)nsl), seg = (int)(blockIdx.x / (unsigned)nsl);
+    const int col = sl * (int)blockDim.x + (int)threadIdx.x;
+    const bool lo = col < M2;
+    const int j = lo ? (M2 - 1 - col) : (3 * M2 - 1 - col);
+    const int dA = lo ? 0 : 1;
+    // taps of the first (ta) and second (tb) block a row completes: lo: even
+    // block 2c (bin j), odd 2c+1 (j ^ M/2); hi: odd 2c+1, even 2c+2
+    float ta[L], tb[L];
+    {
+        const int ia = lo ? j : (j ^ M2), ib = lo ? (j ^ M2) : j;
+#pragma unroll
+        for (int n = 0; n < L; n++) {
+            ta[n] = hsub[ia * L + n];
+            tb[n] = hsub[ib * L + n];
+        }
+    }
+    const __amdgpu_buffer_rsrc_t rx =
+        __builtin_amdgcn_make_buffer_rsrc((void *)x, (short)0, n_in * 8, 0x00020000);
+    const __amdgpu_buffer_rsrc_t rh =
+        __builtin_amdgcn_make_buffer_rsrc((void *)hist, (short)0, HL * 8, 0x00020000);
+    // Y: nb blocks of M; a store outside (blocks before / after the call) is dropped
+    const __amdgpu_buffer_rsrc_t ry =
+        __builtin_amdgcn_make_buffer_rsrc((void *)Y, (short)0, nb * M * 8, 0x00020000);
+    auto row_sample = [&](int r) -> float2 {
+        const int t = r * M + col - p0 * M2;              // stream sample (t < 0: history)
+        const float2 a = __builtin_bit_cast(float2, __builtin_amdgcn_raw_buffer_load_b64(rx, (unsigned)t * 8u, 0, 0));
+        const float2 b =
+            __builtin_bit_cast(float2, __builtin_amdgcn_raw_buffer_load_b64(rh, (unsigned)(t + HL) * 8u, 0, 0));
+        return make_float2(a.x + b.x, a.y + b.y);
+    };
+    typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
+    auto put = [&](int bt, float2 v) {   // block bt of the aligned numbering, bin j
+        const int gb = bt - p0;
+        const unsigned off = (gb >= 0 && gb < nb) ? ((unsigned)gb * (unsigned)M + (unsigned)j) * 8u : 0xFFFFFFF0u;
+        __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2, v), ry, off, 0, 0);
+    };
+    const int cs = cmin + seg * S;
+    int ce = cs + S;
+    if (ce > cmax + 1) ce = cmax + 1;
+    // register ring over groups of L rows: step u of a group puts row
+    // r + u into w[u] (the slot of row r + u - L, no longer needed), so row
+    // c - n is in w[(u - n) mod L] -- static indices, no moves.  The next
+    // group's samples are loaded one per step, L loads in flight.
+    float2 w[L], pf[L];
+    int r = cs - (L - 1);
+#pragma unroll
+    for (int u = 0; u < L; u++) pf[u] = row_sample(r + u);
+    for (; r < ce; r += L) {
+#pragma unroll
+        for (int u = 0; u < L; u++) {
+            w[u] = pf[u];
+            pf[u] = row_sample(r + L + u);
+            const int c = r + u;
+            if (c >= cs && c < ce) {
+                float2 da = make_float2(0.f, 0.f), db = make_float2(0.f, 0.f);
+#pragma unroll
+                for (int n = 0; n < L; n++) {
+                    const float2 v = w[(u - n + L) % L];
+                    da.x = fmaf(ta[n], v.x, da.x);
+                    da.y = fmaf(ta[n], v.y, da.y);
+                    db.x = fmaf(tb[n], v.x, db.x);
+                    db.y = fmaf(tb[n], v.y, db.y);
+                }
+                put(2 * c + dA, da);
+                put(2 * c + dA + 1, db);
+            }
+        }
+    }
+}
+
+template <int L>
+bool launch_pfb2_poly(int M, const void *hsub, const void *hist, const void *x, long long nb, int p0, void *Y,
+                      hipStream_t st)
+{
+    const long long n_in = nb * (M / 2);
+    if (n_in * 8 >= (1ll << 31) || nb * (long long)M * 8 >= (1ll << 31)) return false;   // 32-bit buffer offsets
+    const int cmin = (p0 - 1) >> 1;                            // floor((p0 - 1) / 2)
+    const int cmax = (int)((p0 + nb - 1) >> 1);
+    const int rows = cmax - cmin + 1;
+    const int nt = M < 256 ? M : 256;
+    const int nsl = M / nt;
+    // runs of S rows: >= 2048 workgroups when the call is long, and runs of
+    // at least 4L rows so the L-1 warm-up rows stay a small overhead
+    long long S = ((long long)rows * nsl + 2047) / 2048;
+    if (S < 4 * L) S = 4 * L;
+    const long long nseg = (rows + S - 1) / S;
+    hipLaunchKernelGGL((k_pfb2_poly<L>), dim3((unsigned)(nseg * nsl)), dim3(nt), 0, st, M, nsl, (const float *)hsub,
+                       (const float2 *)hist, (const float2 *)x, (int)n_in, p0, (int)nb, cmin, cmax, (int)S,
+                       (float2 *)Y);
+    LQ_CHECK_LAUNCH();
+    return true;
+}
+
 // generic even M (not a power of two): direct O(M^2) DFT, one workgroup per block
 __global__ __launch_bounds__(NT) void k_pfb2_an_generic(int M, int m, const float *__restrict__ hsub,
                                                         const float2 *__restrict__ hist,
@@ -556,6 +672,39 @@ extern "C" void lqk_firpfbch2_analyzer(unsigned int M, unsigned int m, const voi
     if (nblocks == 0) return;
     hipStream_t st = (hipStream_t)stream;
     const long long nb = (long long)nblocks;
+    if (M >= 64 && is_pow2(M) && 2 * m <= 16 && m >= 1) {
+        // polyphase pass into Y, then the batched inverse transform in place
+        // (each transform kernel reads its whole block before writing it).
+        // Calls run in chunks of an even number of blocks whose outputs fit
+        // 1 GiB (32-bit buffer offsets); a later chunk's history is the
+        // input just before it (a chunk spans far more than 2mM samples).
+        const long long CB = (1ll << 27) / M;
+        const long long M2 = M / 2, HL = 2ll * m * M - M2;
+        for (long long b0 = 0; b0 < nb; b0 += CB) {
+            const long long nbc = (nb - b0) < CB ? (nb - b0) : CB;
+            const float2 *xc = (const float2 *)x + b0 * M2;
+            const void *hc = b0 == 0 ? hist : (const void *)(xc - HL);
+            float2 *Yc = (float2 *)Y + b0 * M;
+            bool ok = false;
+            switch (2 * m) {
+            case 2: ok = launch_pfb2_poly<2>((int)M, hsub, hc, xc, nbc, p0, Yc, st); break;
+            case 4: ok = launch_pfb2_poly<4>((int)M, hsub, hc, xc, nbc, p0, Yc, st); break;
+            case 6: ok = launch_pfb2_poly<6>((int)M, hsub, hc, xc, nbc, p0, Yc, st); break;
+            case 8: ok = launch_pfb2_poly<8>((int)M, hsub, hc, xc, nbc, p0, Yc, st); break;
+            case 10: ok = launch_pfb2_poly<10>((int)M, hsub, hc, xc, nbc, p0, Yc, st); break;
+            case 12: ok = launch_pfb2_poly<12>((int)M, hsub, hc, xc, nbc, p0, Yc, st); break;
+            case 14: ok = launch_pfb2_poly<14>((int)M, hsub, hc, xc, nbc, p0, Yc, st); break;
+            case 16: ok = launch_pfb2_poly<16>((int)M, hsub, hc, xc, nbc, p0, Yc, st); break;
+            default: break;
+            }
+            if (!ok) {
+                fprintf(stderr, "error: firpfbch2: polyphase pass rejected a %lld-block chunk\n", nbc);
+                exit(1);
+            }
+            fft_batch_scaled(M, -1, Yc, Yc, nbc, 1.0f / (float)M, 1.0f, 1, 0, st);
+        }
+        return;
+    }
     switch (M) {
     case 2: launch_pfb2_an<2>(m, hsub, hist, x, nb, p0, Y, st); return;
     case 4: launch_pfb2_an<4>(m, hsub, hist, x, nb, p0, Y, st); return;

@@ -339,6 +339,36 @@ def test_firpfbch2_analyzer_vs_oracle(M, m):
     assert G.nrm_err(y, o.execute_block(x)) < NRM
 
 
+@pytest.mark.parametrize("M,m", [(64, 4), (128, 1), (256, 4), (512, 3), (1024, 5), (2048, 4), (4096, 2), (256, 8)])
+def test_firpfbch2_analyzer_polyphase_pass_vs_oracle(M, m):
+    # power-of-two M other than the fused M=1024/m=4 path: polyphase pass
+    # (column slices x row runs with a warm-up of 2m-1 rows each) + batched
+    # transform in place.  Enough blocks for many row runs per slice; ragged
+    # calls start on both block parities.
+    r = rng(7 * M + m)
+    nblocks = max(64, (1 << 21) // M)
+    x = cx(r, nblocks * M // 2)
+    g = LQ.FirPfbch2(LQ.LIQUID_ANALYZER, M, m, 60.0)
+    o = O.FirPfbch2(O.ANALYZER, M, m, 60.0)
+    cuts = [0, 1, 6, 7, nblocks // 2 + 1, nblocks]
+    step = M // 2
+    y = np.concatenate([g.execute_block(x[a * step:b * step]) for a, b in zip(cuts[:-1], cuts[1:])])
+    assert G.nrm_err(y, o.execute_block(x)) < NRM
+
+
+def test_firpfbch2_analyzer_polyphase_chunks_vs_oracle():
+    # a call longer than one polyphase chunk (2^27 / M blocks): the second
+    # chunk takes its history from the input before it; odd start parity
+    M, m = 4096, 2
+    r = rng(4097)
+    nb = (1 << 27) // M + 301
+    x = cx(r, (nb + 1) * M // 2)
+    g = LQ.FirPfbch2(LQ.LIQUID_ANALYZER, M, m, 60.0)
+    o = O.FirPfbch2(O.ANALYZER, M, m, 60.0)
+    y = np.concatenate([g.execute_block(x[:M // 2]), g.execute_block(x[M // 2:])])
+    assert G.nrm_err(y, o.execute_block(x)) < NRM
+
+
 def test_firpfbch2_baseline_config4_slice_vs_oracle():
     # BASELINE config 4 geometry: M=1024, m=4, As=60, 2^20 samples (2048 blocks)
     r = rng(31)

@@ -82,6 +82,20 @@ def main():
     it.set_stream(S)
     ms = timed(lambda: L.firinterp_crcf_execute_block_dev(it.q, xi.data_ptr(), n // 8, y.data_ptr()))
     report("firinterp_crcf M=8 m=8", ms, n, "output samples", 8 * n + n, "8 B/output + 8 B/input")
+    # firpfbch2 analyzer at other channel counts (M = 1024 is the bench's
+    # fused fast path; the others take the generic polyphase + transform kernels)
+    n = 1 << 27
+    x = cbuf(n)
+    y = torch.empty(4 * n, device="cuda")
+    for M in (64, 256, 512, 1024, 2048, 4096):
+        a2 = LQ.FirPfbch2(LQ.LIQUID_ANALYZER, M, 4, 60.0)
+        a2.set_stream(S)
+        nb = n // (M // 2)
+        ms = timed(lambda: L.firpfbch2_crcf_execute_block_dev(a2.q, x.data_ptr(), nb, y.data_ptr()), it=10, w=5)
+        report("firpfbch2_crcf analyzer M=%d m=4" % M, ms, n, "input samples", 24 * n,
+               "8 B/input + 16 B/output (2 per input)")
+        a2.destroy()
+    del x, y
     # firpfbch2 synthesizer, firpfbch analyzer / synthesizer, M = 1024
     M, nb = 1024, 1 << 17
     X = cbuf(nb * M)
