@@ -583,6 +583,56 @@ __global__ __launch_bounds__(256, 2) void k_fft4096_batch(const float2 *__restri
     }
 }
 
+// batched N = 256 R point transforms (R = 1, 2, 8: 256, 512, 2048 points),
+// 16 R threads per transform, 16 / R transforms per 256-thread workgroup,
+// register passes (fft_r16x16xR); persistent over the batch
+template <int R, int DIR>
+__global__ __launch_bounds__(256, 2) void k_fftr16_batch(const float2 *__restrict__ x, float2 *__restrict__ y,
+                                                          long long batch, float s1, float s2, int use_s1,
+                                                          int use_s2, const float2 *__restrict__ tw4096)
+{
+    constexpr int T = 16 * R, N = 16 * T, G = 256 / T, P = FFTR16_LDS<R>();
+    __shared__ __attribute__((aligned(16))) float2 lds[G * P];
+    const int g = threadIdx.x / T, t = threadIdx.x % T;
+    for (long long b0 = (long long)blockIdx.x * G; b0 < batch; b0 += (long long)gridDim.x * G) {
+        const long long b = b0 + g;
+        const bool in = b < batch;
+        float2 v[16];
+        const float2 *xb = x + (in ? b : 0) * N;
+#pragma unroll
+        for (int n = 0; n < 16; n++) v[n] = in ? xb[t + T * n] : make_float2(0.f, 0.f);
+        fft_r16x16xR<R, DIR>(v, lds + g * P, tw4096, t);
+        if (in) {
+            float2 *yb = y + b * N;
+#pragma unroll
+            for (int s = 0; s < 16 / R; s++)
+#pragma unroll
+                for (int q = 0; q < R; q++) {
+                    float2 w = v[s * R + q];
+                    if (use_s1) w = cscale(w, s1);
+                    if (use_s2) w = cscale(w, s2);
+                    yb[t + T * s + 256 * q] = w;
+                }
+        }
+    }
+}
+
+template <int R>
+void launch_fftr16(const void *x, void *y, long long batch, int dir, float s1, float s2, int u1, int u2,
+                   hipStream_t st)
+{
+    constexpr int G = 16 / R;
+    const long long g = (batch + G - 1) / G;
+    const unsigned grid = (unsigned)(g < 2048 ? g : 2048);
+    if (dir > 0)
+        hipLaunchKernelGGL((k_fftr16_batch<R, +1>), dim3(grid), dim3(256), 0, st, (const float2 *)x, (float2 *)y,
+                           batch, s1, s2, u1, u2, (const float2 *)lqrt_twiddles());
+    else
+        hipLaunchKernelGGL((k_fftr16_batch<R, -1>), dim3(grid), dim3(256), 0, st, (const float2 *)x, (float2 *)y,
+                           batch, s1, s2, u1, u2, (const float2 *)lqrt_twiddles());
+    LQ_CHECK_LAUNCH();
+}
+
 template <int N>
 void launch_fft_batch(const void *x, void *y, long long batch, int dir, float s1, float s2, int u1, int u2,
                       hipStream_t st)
@@ -608,8 +658,8 @@ void fft_batch_scaled(unsigned n, int dir, const void *x, void *y, long long bat
     case 32: launch_fft_batch<32>(x, y, batch, dir, s1, s2, u1, u2, st); return;
     case 64: launch_fft_batch<64>(x, y, batch, dir, s1, s2, u1, u2, st); return;
     case 128: launch_fft_batch<128>(x, y, batch, dir, s1, s2, u1, u2, st); return;
-    case 256: launch_fft_batch<256>(x, y, batch, dir, s1, s2, u1, u2, st); return;
-    case 512: launch_fft_batch<512>(x, y, batch, dir, s1, s2, u1, u2, st); return;
+    case 256: launch_fftr16<1>(x, y, batch, dir, s1, s2, u1, u2, st); return;
+    case 512: launch_fftr16<2>(x, y, batch, dir, s1, s2, u1, u2, st); return;
     case 1024: {
         const long long g = (batch + 3) / 4;
         const unsigned grid = (unsigned)(g < 4096 ? g : 4096);
@@ -622,7 +672,7 @@ void fft_batch_scaled(unsigned n, int dir, const void *x, void *y, long long bat
         LQ_CHECK_LAUNCH();
         return;
     }
-    case 2048: launch_fft_batch<2048>(x, y, batch, dir, s1, s2, u1, u2, st); return;
+    case 2048: launch_fftr16<8>(x, y, batch, dir, s1, s2, u1, u2, st); return;
     case 4096: {
         const unsigned grid = (unsigned)(batch < 2048 ? batch : 2048);
         if (dir > 0)

@@ -268,6 +268,90 @@ __device__ __forceinline__ void twiddle16(float2 (&v)[16], const float2 *__restr
         v[k] = unpk(pk_cmul(pk(v[k]), w));
     }
 }
+// R-point DFT (R = 1, 2, 4, 8, 16) on v[0..R), natural order in and out
+template <int R, int DIR>
+__device__ __forceinline__ void dft_small(float2 *v)
+{
+    if constexpr (R == 2) {
+        const float2 a = v[0], b = v[1];
+        v[0] = cadd(a, b);
+        v[1] = csub(a, b);
+    } else if constexpr (R == 4) {
+        v2f a0 = pk(v[0]), a1 = pk(v[1]), a2 = pk(v[2]), a3 = pk(v[3]);
+        pk_dft4<DIR>(a0, a1, a2, a3);
+        v[0] = unpk(a0); v[1] = unpk(a1); v[2] = unpk(a2); v[3] = unpk(a3);
+    } else if constexpr (R == 8) {
+        // n = n1 + 2 n2: DFT4 over n2 per n1, twiddle W8^{n1 k1}, DFT2 over n1
+        constexpr float h = 0.70710678f;
+        v2f e0 = pk(v[0]), e1 = pk(v[2]), e2 = pk(v[4]), e3 = pk(v[6]);
+        v2f o0 = pk(v[1]), o1 = pk(v[3]), o2 = pk(v[5]), o3 = pk(v[7]);
+        pk_dft4<DIR>(e0, e1, e2, e3);
+        pk_dft4<DIR>(o0, o1, o2, o3);
+        o1 = pk_cmulk(o1, v2f{h, -DIR * h});                          // W8^1
+        o2 = DIR > 0 ? pk_subpj(v2f{0.f, 0.f}, o2) : pk_addpj(v2f{0.f, 0.f}, o2);   // W8^2 = -DIR j
+        o3 = pk_cmulk(o3, v2f{-h, -DIR * h});                         // W8^3
+        v[0] = unpk(e0 + o0); v[4] = unpk(e0 - o0);
+        v[1] = unpk(e1 + o1); v[5] = unpk(e1 - o1);
+        v[2] = unpk(e2 + o2); v[6] = unpk(e2 - o2);
+        v[3] = unpk(e3 + o3); v[7] = unpk(e3 - o3);
+    } else if constexpr (R == 16) {
+        v2f p[16];
+#pragma unroll
+        for (int k = 0; k < 16; k++) p[k] = pk(v[k]);
+        pk_dft16<DIR>(p);
+#pragma unroll
+        for (int k = 0; k < 16; k++) v[k] = unpk(p[k]);
+    }
+}
+
+// N = 256 R point FFT (R = 1, 2, 4, 8, 16: N = 256 .. 4096) by T = 16 R
+// threads, three register passes and two LDS transposes; the generalisation
+// of fft4096_r16 below (R = 16).  In: thread t < T holds x[t + T n] in v[n];
+// out: v[s R + q] = X[t + T s + 256 q] (s < 16/R, q < R).  lds: FFTR16_LDS(R)
+// float2 for this transform; every thread of the workgroup calls it (it
+// synchronises).
+//   pass 1: DFT16 over n, twiddle W_N^{t k2}
+//   pass 2: t = a + R b (a < R): unit (k2, a) runs a DFT16 over b -> q1,
+//           twiddle W_T^{a q1}
+//   pass 3: unit (k2, q1) runs a DFT_R over a -> q2; X[k2 + 16 q1 + 256 q2]
+template <int R>
+constexpr int fftr16_s1() { return 16 * R + 2; }            // pass-1 row stride (conflict-free reads)
+template <int R>
+constexpr int fftr16_s2() { return R == 1 ? 1 : R + 1; }    // pass-2 unit stride (odd)
+template <int R>
+constexpr int FFTR16_LDS()
+{
+    return (16 * fftr16_s1<R>() > 256 * fftr16_s2<R>() ? 16 * fftr16_s1<R>() : 256 * fftr16_s2<R>()) | 1;
+}
+template <int R, int DIR>
+__device__ __forceinline__ void fft_r16x16xR(float2 (&v)[16], float2 *lds, const float2 *__restrict__ tw, int t)
+{
+    constexpr int T = 16 * R, N = 16 * T;
+    constexpr int S1 = fftr16_s1<R>(), S2 = fftr16_s2<R>();
+    dft16<DIR>(v);
+    twiddle16<DIR>(v, tw, t * (4096 / N));   // W_N^{t k2}
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < 16; k++) lds[k * S1 + t] = v[k];
+    __syncthreads();
+    const int k2 = t & 15, a = t >> 4;
+#pragma unroll
+    for (int b = 0; b < 16; b++) v[b] = lds[k2 * S1 + a + R * b];
+    dft16<DIR>(v);
+    if constexpr (R > 1) twiddle16<DIR>(v, tw, a * (4096 / T));   // W_T^{a q1}
+    __syncthreads();
+#pragma unroll
+    for (int q1 = 0; q1 < 16; q1++) lds[(k2 + 16 * q1) * S2 + a] = v[q1];
+    __syncthreads();
+    // unit k2 + 16 q1 with q1 = (t >> 4) + R s is t + T s
+#pragma unroll
+    for (int s = 0; s < 16 / R; s++)
+#pragma unroll
+        for (int e = 0; e < R; e++) v[s * R + e] = lds[(t + T * s) * S2 + e];
+#pragma unroll
+    for (int s = 0; s < 16 / R; s++) dft_small<R, DIR>(v + s * R);
+}
+
 template <int DIR>
 __device__ __forceinline__ void fft4096_r16(float2 (&v)[16], float2 *lds, const float2 *__restrict__ tw, int t)
 {
