@@ -106,11 +106,21 @@ def main():
     report("firpfbch2_crcf synthesizer M=1024 m=4", ms, nb * M // 2, "output samples", 12 * nb * M,
            "8 B/channel sample in + 8 B/output (M/2 per block)")
     for typ, nm in ((LQ.LIQUID_ANALYZER, "analyzer"), (LQ.LIQUID_SYNTHESIZER, "synthesizer")):
-        p = LQ.FirPfbch(typ, M, m=4, As=60.0)
-        p.set_stream(S)
-        ms = timed(lambda: L.firpfbch_crcf_execute_block_dev(p.q, X.data_ptr(), nb, Y.data_ptr()))
-        report("firpfbch_crcf %s M=1024 m=4" % nm, ms, nb * M, "samples", 16 * nb * M, "16 B/sample")
-        p.destroy()
+        for Mc in (256, 1024, 4096):
+            nbc = nb * M // Mc
+            p = LQ.FirPfbch(typ, Mc, m=4, As=60.0)
+            p.set_stream(S)
+            ms = timed(lambda: L.firpfbch_crcf_execute_block_dev(p.q, X.data_ptr(), nbc, Y.data_ptr()), it=10, w=5)
+            report("firpfbch_crcf %s M=%d m=4" % (nm, Mc), ms, nbc * Mc, "samples", 16 * nbc * Mc, "16 B/sample")
+            p.destroy()
+    for Mc in (256, 4096):
+        nbc = nb * M // Mc
+        q2 = LQ.FirPfbch2(LQ.LIQUID_SYNTHESIZER, Mc, 4, 60.0)
+        q2.set_stream(S)
+        ms = timed(lambda: L.firpfbch2_crcf_execute_block_dev(q2.q, X.data_ptr(), nbc, Y.data_ptr()), it=10, w=5)
+        report("firpfbch2_crcf synthesizer M=%d m=4" % Mc, ms, nbc * Mc // 2, "output samples", 12 * nbc * Mc,
+               "8 B/channel sample in + 8 B/output (M/2 per block)")
+        q2.destroy()
     # resamp2 decim / interp (m = 12), msresamp r = 0.3 / 3.3
     n = 1 << 26
     x = cbuf(n)
