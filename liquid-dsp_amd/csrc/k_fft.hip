@@ -75,6 +75,78 @@ __global__ __launch_bounds__(NT) void k_fft2p_rows(const float2 *__restrict__ wo
     }
 }
 
+// Register forms of both passes for N1 / N2 = 256 R (R = 1, 2, 4, 8, 16):
+// the transforms run in registers (fft_r16x16xR, 16 R threads each, 16 / R
+// per workgroup) instead of the LDS Stockham passes.  Consecutive threads
+// take consecutive columns (pass A) / rows (pass B), so the column loads and
+// stores of pass A and the transposed stores of pass B move G consecutive
+// samples per instruction and lane group.
+template <int R, int DIR>
+__global__ __launch_bounds__(NT) void k_fft2p_cols_r(const float2 *__restrict__ x, float2 *__restrict__ work,
+                                                     long long n, int N2, const float2 *__restrict__ tw)
+{
+    constexpr int T = 16 * R, G = 256 / T, P = FFTR16_LDS<R>();
+    __shared__ __attribute__((aligned(16))) float2 lds[G * P];
+    const long long off = (long long)blockIdx.z * n;
+    const int g = threadIdx.x % G, t = threadIdx.x / G;
+    const int j2 = blockIdx.x * G + g;
+    float2 v[16];
+#pragma unroll
+    for (int q = 0; q < 16; q++) v[q] = x[off + (long long)N2 * (t + T * q) + j2];
+    fft_r16x16xR<R, DIR>(v, lds + g * P, tw, t);
+#pragma unroll
+    for (int s = 0; s < 16 / R; s++)
+#pragma unroll
+        for (int q = 0; q < R; q++) {
+            const int k1 = t + T * s + 256 * q;
+            work[off + (long long)N2 * k1 + j2] = cmul(v[s * R + q], tw_exp((long long)j2 * k1, n, DIR));
+        }
+}
+
+template <int R, int DIR>
+__global__ __launch_bounds__(NT) void k_fft2p_rows_r(const float2 *__restrict__ work, float2 *__restrict__ y,
+                                                     long long n, int N1, const float2 *__restrict__ tw)
+{
+    constexpr int T = 16 * R, N2 = 16 * T, G = 256 / T, P = FFTR16_LDS<R>();
+    __shared__ __attribute__((aligned(16))) float2 lds[G * P];
+    const long long off = (long long)blockIdx.z * n;
+    const int g = threadIdx.x % G, t = threadIdx.x / G;
+    const int k1 = blockIdx.x * G + g;
+    float2 v[16];
+#pragma unroll
+    for (int q = 0; q < 16; q++) v[q] = work[off + (long long)N2 * k1 + t + T * q];
+    fft_r16x16xR<R, DIR>(v, lds + g * P, tw, t);
+#pragma unroll
+    for (int s = 0; s < 16 / R; s++)
+#pragma unroll
+        for (int q = 0; q < R; q++) y[off + k1 + (long long)N1 * (t + T * s + 256 * q)] = v[s * R + q];
+}
+
+template <int R>
+void launch_cols_r(const void *x, void *work, long long n, int N2, int dir, long long batch, hipStream_t st)
+{
+    const dim3 g((unsigned)(N2 / (16 / R)), 1, (unsigned)batch);
+    if (dir > 0)
+        hipLaunchKernelGGL((k_fft2p_cols_r<R, +1>), g, dim3(NT), 0, st, (const float2 *)x, (float2 *)work, n, N2,
+                           (const float2 *)lqrt_twiddles());
+    else
+        hipLaunchKernelGGL((k_fft2p_cols_r<R, -1>), g, dim3(NT), 0, st, (const float2 *)x, (float2 *)work, n, N2,
+                           (const float2 *)lqrt_twiddles());
+    LQ_CHECK_LAUNCH();
+}
+template <int R>
+void launch_rows_r(const void *work, void *y, long long n, int N1, int dir, long long batch, hipStream_t st)
+{
+    const dim3 g((unsigned)(N1 / (16 / R)), 1, (unsigned)batch);
+    if (dir > 0)
+        hipLaunchKernelGGL((k_fft2p_rows_r<R, +1>), g, dim3(NT), 0, st, (const float2 *)work, (float2 *)y, n, N1,
+                           (const float2 *)lqrt_twiddles());
+    else
+        hipLaunchKernelGGL((k_fft2p_rows_r<R, -1>), g, dim3(NT), 0, st, (const float2 *)work, (float2 *)y, n, N1,
+                           (const float2 *)lqrt_twiddles());
+    LQ_CHECK_LAUNCH();
+}
+
 template <int N>
 void launch_cols(const void *x, void *work, long long n, int N2, int dir, long long batch, hipStream_t st)
 {
@@ -100,19 +172,19 @@ void fft_four_step(unsigned n, int dir, const void *x, void *y, long long batch,
     switch (N1) {
     case 64: launch_cols<64>(x, work, n, N2, dir, batch, st); break;
     case 128: launch_cols<128>(x, work, n, N2, dir, batch, st); break;
-    case 256: launch_cols<256>(x, work, n, N2, dir, batch, st); break;
-    case 512: launch_cols<512>(x, work, n, N2, dir, batch, st); break;
-    case 1024: launch_cols<1024>(x, work, n, N2, dir, batch, st); break;
-    case 2048: launch_cols<2048>(x, work, n, N2, dir, batch, st); break;
-    default: launch_cols<4096>(x, work, n, N2, dir, batch, st); break;
+    case 256: launch_cols_r<1>(x, work, n, N2, dir, batch, st); break;
+    case 512: launch_cols_r<2>(x, work, n, N2, dir, batch, st); break;
+    case 1024: launch_cols_r<4>(x, work, n, N2, dir, batch, st); break;
+    case 2048: launch_cols_r<8>(x, work, n, N2, dir, batch, st); break;
+    default: launch_cols_r<16>(x, work, n, N2, dir, batch, st); break;
     }
     switch (N2) {
     case 128: launch_rows<128>(work, y, n, N1, dir, batch, st); break;
-    case 256: launch_rows<256>(work, y, n, N1, dir, batch, st); break;
-    case 512: launch_rows<512>(work, y, n, N1, dir, batch, st); break;
-    case 1024: launch_rows<1024>(work, y, n, N1, dir, batch, st); break;
-    case 2048: launch_rows<2048>(work, y, n, N1, dir, batch, st); break;
-    default: launch_rows<4096>(work, y, n, N1, dir, batch, st); break;
+    case 256: launch_rows_r<1>(work, y, n, N1, dir, batch, st); break;
+    case 512: launch_rows_r<2>(work, y, n, N1, dir, batch, st); break;
+    case 1024: launch_rows_r<4>(work, y, n, N1, dir, batch, st); break;
+    case 2048: launch_rows_r<8>(work, y, n, N1, dir, batch, st); break;
+    default: launch_rows_r<16>(work, y, n, N1, dir, batch, st); break;
     }
 }
 
