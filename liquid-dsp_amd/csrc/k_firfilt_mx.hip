@@ -57,17 +57,21 @@ typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
 
 constexpr int NT = 256;           // 4 waves
 constexpr int CH = 2048;          // outputs per chunk (4 tiles of 512)
-constexpr int SPAN = CH + 64;     // samples a chunk's tiles read (64-sample halo)
-// bytes per plane: the span (5280) rounded up to 256 B, so the planes of the
-// two components start on the same bank -- with the 5280-byte stride every
-// 16-lane group of a B-operand ds_read_b128 had a 2-way bank conflict
-// (SQ_LDS_BANK_CONFLICT was half of the LDS-active cycles)
-constexpr int PLB = (SPAN * 2 + 16 * (SPAN / 32) + 255) & ~255;   // 5376
+// Span: the samples a chunk's tiles read, CH plus a halo of 64 KB samples
+// (KB = 1: 33..64 taps, every type; KB = 2: 65..128 taps, crcf -- a
+// 160-wide band, ten K steps instead of six).  Bytes per plane: the span
+// (5280 for KB = 1) rounded up to 256 B, so the planes of the two components
+// start on the same bank -- with the 5280-byte stride every 16-lane group of
+// a B-operand ds_read_b128 had a 2-way bank conflict (SQ_LDS_BANK_CONFLICT
+// was half of the LDS-active cycles).
+template <int KB>
+constexpr int plb_kb() { return ((CH + 64 * KB) * 2 + 16 * ((CH + 64 * KB) / 32) + 255) & ~255; }
 constexpr int SSTR = 68;          // floats per staged segment (32 x re/im + pad)
-// crcf: one staged accumulator per wave (49664 B: three workgroups per CU);
-// cccf: two (the real- and imaginary-tap products; 67072 B: two per CU)
-template <bool CC>
-constexpr int lds_bytes_mx() { return 6 * PLB + (CC ? 2 : 1) * 4 * 16 * SSTR * 4; }
+// crcf: one staged accumulator per wave (49664 B: three workgroups per CU;
+// KB = 2: 53504 B and 219 VGPRs, two per CU); cccf: two (the real- and
+// imaginary-tap products; 67072 B: two per CU)
+template <bool CC, int KB = 1>
+constexpr int lds_bytes_mx() { return 6 * plb_kb<KB>() + (CC ? 2 : 1) * 4 * 16 * SSTR * 4; }
 
 __device__ __forceinline__ int poff(int pos) { return 2 * pos + 16 * (pos >> 5); }
 
@@ -132,15 +136,16 @@ __device__ __forceinline__ void put1(unsigned char *planes, int pstride, int pos
 
 // 8 complex samples of the stream starting at s (a multiple of 8); ext[t<0]
 // comes from the 64-sample history win, samples at or past n are zero
+template <int HALO = 64>
 __device__ __forceinline__ v2f sample_at(const v2f *__restrict__ win, const v2f *__restrict__ x, long long n,
                                          long long t)
 {
-    return t < 0 ? win[64 + t] : (t < n ? x[t] : v2f{0.f, 0.f});
+    return t < 0 ? win[HALO + t] : (t < n ? x[t] : v2f{0.f, 0.f});
 }
 // Exact float32 outputs t0 .. t0+cnt-1 (the range guard's path): the
 // reference's dot product over the true taps, firfilt.c:322-338, then the
 // scale.  Out of line, so the matrix path's register allocation is unchanged.
-template <bool CC>
+template <bool CC, int HALO>
 __device__ __attribute__((noinline)) void exact_chunk_c(const v2f *__restrict__ win, const v2f *__restrict__ x,
                                                          long long n, v2f *__restrict__ y,
                                                          const float *__restrict__ hpad, int hlen, long long t0,
@@ -151,7 +156,7 @@ __device__ __attribute__((noinline)) void exact_chunk_c(const v2f *__restrict__ 
         if (t >= n) break;
         v2f acc = {0.f, 0.f};
         for (int k = 0; k < hlen; k++) {
-            const v2f v = sample_at(win, x, n, t - k);
+            const v2f v = sample_at<HALO>(win, x, n, t - k);
             if constexpr (CC) {
                 const float hr = hpad[2 * k], hi = hpad[2 * k + 1];
                 acc = v2f{fmaf(-hi, v.y, fmaf(hr, v.x, acc.x)), fmaf(hi, v.x, fmaf(hr, v.y, acc.y))};
@@ -177,8 +182,8 @@ __device__ __forceinline__ void load8b(__amdgpu_buffer_rsrc_t rx, unsigned off, 
 // CC: complex taps (cccf).  Then H = Hr + j Hi and the tile keeps two
 // accumulators, C1 = Hr [Xr | Xi] and C2 = Hi [Xr | Xi]; y = (C1.re - C2.im,
 // C1.im + C2.re) is formed when the staged accumulators are read back.
-template <bool CC>
-__global__ __launch_bounds__(NT, CC ? 2 : 3) void k_firfilt_mx(const v2f *__restrict__ win,
+template <bool CC, int KB>
+__global__ __launch_bounds__(NT, (CC || KB > 1) ? 2 : 3) void k_firfilt_mx(const v2f *__restrict__ win,
                                                               const v2f *__restrict__ x, long long n,
                                                               v2f *__restrict__ y, const float *__restrict__ hpad,
                                                               float sre, float sim, long long nch, int hlen)
@@ -186,7 +191,8 @@ __global__ __launch_bounds__(NT, CC ? 2 : 3) void k_firfilt_mx(const v2f *__rest
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     // per step k % 3: nonzero if the chunk's span holds an unsafe sample;
     // kept after the dynamic region so its base stays 16-byte aligned
-    unsigned *sbad = reinterpret_cast<unsigned *>(smem + lds_bytes_mx<CC>());
+    constexpr int HALO = 64 * KB, NS = 2 + 4 * KB, PLB = plb_kb<KB>();
+    unsigned *sbad = reinterpret_cast<unsigned *>(smem + lds_bytes_mx<CC, KB>());
     unsigned char *planes = smem;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int r32 = lane & 31, hh = lane >> 5;
@@ -195,19 +201,19 @@ __global__ __launch_bounds__(NT, CC ? 2 : 3) void k_firfilt_mx(const v2f *__rest
 
     // A fragments: lane (row i = r32, k half hh) holds H[i][16s + 8hh + e]
     // (cccf: hpad holds (re, im) pairs; matrix a takes component a)
-    bf16x8 A[NA][3][6];
+    bf16x8 A[NA][3][NS];
 #pragma unroll
     for (int a = 0; a < NA; a++)
 #pragma unroll
-        for (int s = 0; s < 6; s++) {
+        for (int s = 0; s < NS; s++) {
             bf16x2 t[3][4];
 #pragma unroll
             for (int q = 0; q < 4; q++) {
                 float hv[2];
 #pragma unroll
                 for (int u = 0; u < 2; u++) {
-                    const int k = r32 + 64 - (16 * s + 8 * hh + 2 * q + u);
-                    hv[u] = (k >= 0 && k < 64) ? hpad[CC ? 2 * k + a : k] : 0.f;
+                    const int k = r32 + HALO - (16 * s + 8 * hh + 2 * q + u);
+                    hv[u] = (k >= 0 && k < HALO) ? hpad[CC ? 2 * k + a : k] : 0.f;
                 }
                 split3(v2f{hv[0], hv[1]}, t[0][q], t[1][q], t[2][q]);
             }
@@ -246,11 +252,11 @@ __global__ __launch_bounds__(NT, CC ? 2 : 3) void k_firfilt_mx(const v2f *__rest
     // halo sample of lane tid < 64; chunk 0's halo is the history (prologue)
     auto halo_off = [&](long long k) -> unsigned {
         const long long c = w + k * G;
-        return (c > 0 && c < nch && tid < 64) ? (unsigned)(CH * c - 64 + tid) * 8u : OOB;
+        return (c > 0 && c < nch && tid < HALO) ? (unsigned)(CH * c - HALO + tid) * 8u : OOB;
     };
     auto ldh = [&](unsigned off) -> v2f { return __builtin_bit_cast(v2f, __builtin_amdgcn_raw_buffer_load_b64(rx, off, 0, 0)); };
     __syncthreads();
-    if (w == 0 && tid < 64) {
+    if (w == 0 && tid < HALO) {
         const v2f hv = win[tid];
         put1(planes, PLB, tid, hv);
         if (unsafe_bits(hv.x) | unsafe_bits(hv.y)) atomicOr(&sbad[0], 1u);
@@ -272,11 +278,11 @@ __global__ __launch_bounds__(NT, CC ? 2 : 3) void k_firfilt_mx(const v2f *__rest
         __syncthreads();   // the previous chunk's MFMA reads are done
         const int cs = (int)(k % 3);
         // chunk 0's halo planes came from the history in the prologue
-        if (tid < 64 && c != 0) {
+        if (tid < HALO && c != 0) {
             put1(planes, PLB, tid, hv);
             if (unsafe_bits(hv.x) | unsafe_bits(hv.y)) atomicOr(&sbad[cs], 1u);
         }
-        put8(planes, PLB, 64 + 8 * tid, xv);
+        put8(planes, PLB, HALO + 8 * tid, xv);
         if (unsafe4(xv[0]) | unsafe4(xv[1]) | unsafe4(xv[2]) | unsafe4(xv[3])) atomicOr(&sbad[cs], 1u);
         if (tid == 0) sbad[(cs + 1) % 3] = 0u;   // step k+1's slot (last read in step k-2)
         load8b(rx, main_off(k + 2), xv);
@@ -288,7 +294,7 @@ __global__ __launch_bounds__(NT, CC ? 2 : 3) void k_firfilt_mx(const v2f *__rest
 #pragma unroll
         for (int a = 0; a < NA; a++) C[a] = f32x16{};
 #pragma unroll
-        for (int s = 0; s < 6; s++) {
+        for (int s = 0; s < NS; s++) {
             const int pos = 512 * wave + 32 * sg + 16 * s + 8 * hh;
             const unsigned char *bp = planes + comp * PLB + poff(pos);
             const bf16x8 b0 = *reinterpret_cast<const bf16x8 *>(bp);
@@ -353,7 +359,7 @@ __global__ __launch_bounds__(NT, CC ? 2 : 3) void k_firfilt_mx(const v2f *__rest
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
         for (int k = 0; k < (int)cnt; k++)
             if (bad_mask[k >> 5] & (1u << (k & 31)))
-                exact_chunk_c<CC>(win, x, n, y, hpad, hlen, CH * (w + k * G) + 8 * tid, 8, sre, sim);
+                exact_chunk_c<CC, HALO>(win, x, n, y, hpad, hlen, CH * (w + k * G) + 8 * tid, 8, sre, sim);
     }
 }
 
@@ -567,15 +573,21 @@ static void launch_mx(const lqk_fir_desc *d, const void *hist, const void *x, lo
         return;
     }
     const bool cc = d->kind == 2;
+    const bool kb2 = d->nchunk == 2;   // crcf, 65..128 taps
     const long long nch = (n + CH - 1) / CH;
-    const long long wgs = cc ? 512 : 768;   // resident workgroups (two / three per CU)
+    const long long wgs = (cc || kb2) ? 512 : 768;   // resident workgroups (two / three per CU)
     const dim3 grid((unsigned)(nch < wgs ? nch : wgs));
-    if (cc)
-        hipLaunchKernelGGL(k_firfilt_mx<true>, grid, dim3(NT), lds_bytes_mx<true>() + 80, st, (const v2f *)hist,
+    constexpr int lds_kb2 = lds_bytes_mx<false, 2>() + 80;
+    if (kb2)
+        hipLaunchKernelGGL((k_firfilt_mx<false, 2>), grid, dim3(NT), lds_kb2, st,
+                           (const v2f *)hist, (const v2f *)x, n, (v2f *)y, (const float *)d->hpad, d->scale_re,
+                           d->scale_im, nch, (int)d->hlen);
+    else if (cc)
+        hipLaunchKernelGGL((k_firfilt_mx<true, 1>), grid, dim3(NT), lds_bytes_mx<true>() + 80, st, (const v2f *)hist,
                            (const v2f *)x, n, (v2f *)y, (const float *)d->hpad, d->scale_re, d->scale_im, nch,
                            (int)d->hlen);
     else
-        hipLaunchKernelGGL(k_firfilt_mx<false>, grid, dim3(NT), lds_bytes_mx<false>() + 80, st, (const v2f *)hist,
+        hipLaunchKernelGGL((k_firfilt_mx<false, 1>), grid, dim3(NT), lds_bytes_mx<false>() + 80, st, (const v2f *)hist,
                            (const v2f *)x, n, (v2f *)y, (const float *)d->hpad, d->scale_re, d->scale_im, nch,
                            (int)d->hlen);
     LQ_CHECK_LAUNCH();
@@ -587,7 +599,8 @@ static void launch_mx(const lqk_fir_desc *d, const void *hist, const void *x, lo
 extern "C" int lqk_firfilt_mx(const lqk_fir_desc *d, const void *hist, const void *x, unsigned long long n,
                               void *y, void *stream)
 {
-    if (d->hc != 64 || d->nchunk != 1 || x == y || !d->mx_ok) return 0;
+    // 33..64 taps (one 64-tap block) for every type; 65..128 (two) for crcf
+    if (d->hc != 64 || !(d->nchunk == 1 || (d->nchunk == 2 && d->kind == 1)) || x == y || !d->mx_ok) return 0;
     if (((uintptr_t)x & 15) || ((uintptr_t)y & 15)) return 0;
     if (n == 0) return 1;
     const size_t es = d->kind == 0 ? 4 : 8;
@@ -595,7 +608,8 @@ extern "C" int lqk_firfilt_mx(const lqk_fir_desc *d, const void *hist, const voi
     for (long long o = 0; o < (long long)n; o += LCH) {
         const long long nn = ((long long)n - o) < LCH ? ((long long)n - o) : LCH;
         const char *xo = (const char *)x + o * es;
-        launch_mx(d, o == 0 ? hist : (const void *)(xo - 64 * es), xo, nn, (char *)y + o * es, (hipStream_t)stream);
+        launch_mx(d, o == 0 ? hist : (const void *)(xo - (size_t)64 * d->nchunk * es), xo, nn, (char *)y + o * es,
+                  (hipStream_t)stream);
     }
     return 1;
 }

@@ -69,6 +69,18 @@ def main():
         ms = timed(lambda: fn(q.q, x.data_ptr(), n, y.data_ptr()))
         report("firfilt_%s h=64" % t, ms, n, "samples", 2 * esz * n, "%d B/sample" % (2 * esz))
         q.destroy()
+    # firfilt crcf at other lengths (h <= 32 and h > 64: the VALU kernel)
+    n = 1 << 27
+    x = cbuf(n)
+    y = torch.empty_like(x)
+    for hl in (16, 32, 48, 128, 256):
+        h = (torch.rand(hl) - 0.5).numpy().astype("float32")
+        q = LQ.FirFilt("crcf", h)
+        q.set_stream(S)
+        ms = timed(lambda: L.firfilt_crcf_execute_block_dev(q.q, x.data_ptr(), n, y.data_ptr()), it=10, w=5)
+        report("firfilt_crcf h=%d" % hl, ms, n, "samples", 16 * n, "16 B/sample")
+        q.destroy()
+    del x, y
     # firdecim / firinterp crcf M = 8, m = 8 (Kaiser, 2Mm taps)
     n = 1 << 27
     x = cbuf(n)
