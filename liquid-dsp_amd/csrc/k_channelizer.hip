@@ -565,12 +565,13 @@ __global__ __launch_bounds__(256, 2) void k_fft4096_batch(const float2 *__restri
 {
     __shared__ __attribute__((aligned(16))) float2 lds[FFT4096_LDS];
     const int t = threadIdx.x;
+    const tw16x2 w16 = fft4096_tw(tw4096, t);
     for (long long b = blockIdx.x; b < batch; b += gridDim.x) {
         float2 v[16];
         const float2 *xb = x + b * 4096;
 #pragma unroll
         for (int k = 0; k < 16; k++) v[k] = xb[t + 256 * k];
-        fft4096_r16<DIR>(v, lds, tw4096, t);
+        fft4096_r16<DIR>(v, lds, w16, t);
         float2 *yb = y + b * 4096;
 #pragma unroll
         for (int k = 0; k < 16; k++) {
@@ -594,6 +595,7 @@ __global__ __launch_bounds__(256, 2) void k_fftr16_batch(const float2 *__restric
     constexpr int T = 16 * R, N = 16 * T, G = 256 / T, P = FFTR16_LDS<R>();
     __shared__ __attribute__((aligned(16))) float2 lds[G * P];
     const int g = threadIdx.x / T, t = threadIdx.x % T;
+    const tw16x2 w16 = fftr16_tw<R>(tw4096, t);
     for (long long b0 = (long long)blockIdx.x * G; b0 < batch; b0 += (long long)gridDim.x * G) {
         const long long b = b0 + g;
         const bool in = b < batch;
@@ -601,7 +603,7 @@ __global__ __launch_bounds__(256, 2) void k_fftr16_batch(const float2 *__restric
         const float2 *xb = x + (in ? b : 0) * N;
 #pragma unroll
         for (int n = 0; n < 16; n++) v[n] = in ? xb[t + T * n] : make_float2(0.f, 0.f);
-        fft_r16x16xR<R, DIR>(v, lds + g * P, tw4096, t);
+        fft_r16x16xR<R, DIR>(v, lds + g * P, w16, t);
         if (in) {
             float2 *yb = y + b * N;
 #pragma unroll

@@ -90,10 +90,11 @@ __global__ __launch_bounds__(NT) void k_fft2p_cols_r(const float2 *__restrict__ 
     const long long off = (long long)blockIdx.z * n;
     const int g = threadIdx.x % G, t = threadIdx.x / G;
     const int j2 = blockIdx.x * G + g;
+    const tw16x2 w16 = fftr16_tw<R>(tw, t);   // issued before the data loads
     float2 v[16];
 #pragma unroll
     for (int q = 0; q < 16; q++) v[q] = x[off + (long long)N2 * (t + T * q) + j2];
-    fft_r16x16xR<R, DIR>(v, lds + g * P, tw, t);
+    fft_r16x16xR<R, DIR>(v, lds + g * P, w16, t);
 #pragma unroll
     for (int s = 0; s < 16 / R; s++)
 #pragma unroll
@@ -112,10 +113,11 @@ __global__ __launch_bounds__(NT) void k_fft2p_rows_r(const float2 *__restrict__ 
     const long long off = (long long)blockIdx.z * n;
     const int g = threadIdx.x % G, t = threadIdx.x / G;
     const int k1 = blockIdx.x * G + g;
+    const tw16x2 w16 = fftr16_tw<R>(tw, t);
     float2 v[16];
 #pragma unroll
     for (int q = 0; q < 16; q++) v[q] = work[off + (long long)N2 * k1 + t + T * q];
-    fft_r16x16xR<R, DIR>(v, lds + g * P, tw, t);
+    fft_r16x16xR<R, DIR>(v, lds + g * P, w16, t);
 #pragma unroll
     for (int s = 0; s < 16 / R; s++)
 #pragma unroll

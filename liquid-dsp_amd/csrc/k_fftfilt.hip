@@ -112,6 +112,7 @@ __global__ __launch_bounds__(NT, WPE) void k_fftfilt_r16(int hm1, const float2 *
     const __amdgpu_buffer_rsrc_t rx = __builtin_amdgcn_make_buffer_rsrc((void *)xin, (short)0, (int)(n * ES), 0x00020000);
     const __amdgpu_buffer_rsrc_t rh = __builtin_amdgcn_make_buffer_rsrc((void *)hist, (short)0, hm1 * ES, 0x00020000);
     const __amdgpu_buffer_rsrc_t ry = __builtin_amdgcn_make_buffer_rsrc(yout, (short)0, (int)(n * ES), 0x00020000);
+    const tw16x2 w16 = fft4096_tw(tw, t);   // the thread's twiddles, loaded once
     for (long long seg = blockIdx.x; seg < nseg; seg += gridDim.x) {
     // segment sample i = t + 256 q is stream sample s0 - hm1 + i
     const int sb = (int)(seg * L) - hm1;   // stream index of segment sample 0
@@ -141,10 +142,10 @@ __global__ __launch_bounds__(NT, WPE) void k_fftfilt_r16(int hm1, const float2 *
                 v[q] = __builtin_bit_cast(float2, __builtin_amdgcn_raw_buffer_load_b64(rx, ox, 0, 0));
         }
     }
-    fft4096_r16<+1>(v, lds, tw, t);
+    fft4096_r16<+1>(v, lds, w16, t);
 #pragma unroll
     for (int k = 0; k < 16; k++) v[k] = unpk(pk_cmul(pk(v[k]), pk(HREG ? hv[k & (HREG ? 15 : 0)] : H[t + 256 * k])));
-    fft4096_r16<-1>(v, lds, tw, t);
+    fft4096_r16<-1>(v, lds, w16, t);
 #pragma unroll
     for (int q = 0; q < 16; q++) {
         const int i = t + 256 * q;

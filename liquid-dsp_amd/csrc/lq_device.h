@@ -249,9 +249,18 @@ __device__ __forceinline__ void dft16(float2 (&v)[16])
 // W^{e k} = W^{e (k & 3)} W^{e (k & 12)}, each factor at most two products
 // from a table value (keeps the cached-table traffic at 2 loads per pass)
 template <int DIR>
+__device__ __forceinline__ void twiddle16v(float2 (&v)[16], float2 a1, float2 a4);
+template <int DIR>
 __device__ __forceinline__ void twiddle16(float2 (&v)[16], const float2 *__restrict__ tw, int e)
 {
-    float2 a1 = tw[e & 4095], a4 = tw[(4 * e) & 4095];
+    twiddle16v<DIR>(v, tw[e & 4095], tw[(4 * e) & 4095]);
+}
+// the same from the two table values W^e, W^{4e} (forward direction) held
+// in registers: kernels that run many transforms load them once per thread
+// instead of twice per pass (each a dependent L2 round trip)
+template <int DIR>
+__device__ __forceinline__ void twiddle16v(float2 (&v)[16], float2 a1, float2 a4)
+{
     if (DIR < 0) {
         a1.y = -a1.y;
         a4.y = -a4.y;
@@ -323,13 +332,32 @@ constexpr int FFTR16_LDS()
 {
     return (16 * fftr16_s1<R>() > 256 * fftr16_s2<R>() ? 16 * fftr16_s1<R>() : 256 * fftr16_s2<R>()) | 1;
 }
+// the four twiddle-table values a thread of fft_r16x16xR<R> uses (both
+// directions: the inverse conjugates them)
+struct tw16x2 {
+    float2 p1a, p1b, p2a, p2b;
+};
+template <int R>
+__device__ __forceinline__ tw16x2 fftr16_tw(const float2 *__restrict__ tw, int t)
+{
+    constexpr int T = 16 * R, N = 16 * T;
+    const int e1 = t * (4096 / N), e2 = (t >> 4) * (4096 / T);
+    return tw16x2{tw[e1 & 4095], tw[(4 * e1) & 4095], tw[e2 & 4095], tw[(4 * e2) & 4095]};
+}
+template <int R, int DIR>
+__device__ __forceinline__ void fft_r16x16xR(float2 (&v)[16], float2 *lds, const tw16x2 &w, int t);
 template <int R, int DIR>
 __device__ __forceinline__ void fft_r16x16xR(float2 (&v)[16], float2 *lds, const float2 *__restrict__ tw, int t)
 {
-    constexpr int T = 16 * R, N = 16 * T;
+    fft_r16x16xR<R, DIR>(v, lds, fftr16_tw<R>(tw, t), t);
+}
+template <int R, int DIR>
+__device__ __forceinline__ void fft_r16x16xR(float2 (&v)[16], float2 *lds, const tw16x2 &w, int t)
+{
+    constexpr int T = 16 * R;
     constexpr int S1 = fftr16_s1<R>(), S2 = fftr16_s2<R>();
     dft16<DIR>(v);
-    twiddle16<DIR>(v, tw, t * (4096 / N));   // W_N^{t k2}
+    twiddle16v<DIR>(v, w.p1a, w.p1b);   // W_N^{t k2}
     __syncthreads();
 #pragma unroll
     for (int k = 0; k < 16; k++) lds[k * S1 + t] = v[k];
@@ -338,7 +366,7 @@ __device__ __forceinline__ void fft_r16x16xR(float2 (&v)[16], float2 *lds, const
 #pragma unroll
     for (int b = 0; b < 16; b++) v[b] = lds[k2 * S1 + a + R * b];
     dft16<DIR>(v);
-    if constexpr (R > 1) twiddle16<DIR>(v, tw, a * (4096 / T));   // W_T^{a q1}
+    if constexpr (R > 1) twiddle16v<DIR>(v, w.p2a, w.p2b);   // W_T^{a q1}
     __syncthreads();
 #pragma unroll
     for (int q1 = 0; q1 < 16; q1++) lds[(k2 + 16 * q1) * S2 + a] = v[q1];
@@ -352,11 +380,23 @@ __device__ __forceinline__ void fft_r16x16xR(float2 (&v)[16], float2 *lds, const
     for (int s = 0; s < 16 / R; s++) dft_small<R, DIR>(v + s * R);
 }
 
+__device__ __forceinline__ tw16x2 fft4096_tw(const float2 *__restrict__ tw, int t)
+{
+    const int e2 = 16 * (t & 15);
+    return tw16x2{tw[t & 4095], tw[(4 * t) & 4095], tw[e2 & 4095], tw[(4 * e2) & 4095]};
+}
+template <int DIR>
+__device__ __forceinline__ void fft4096_r16(float2 (&v)[16], float2 *lds, const tw16x2 &w, int t);
 template <int DIR>
 __device__ __forceinline__ void fft4096_r16(float2 (&v)[16], float2 *lds, const float2 *__restrict__ tw, int t)
 {
+    fft4096_r16<DIR>(v, lds, fft4096_tw(tw, t), t);
+}
+template <int DIR>
+__device__ __forceinline__ void fft4096_r16(float2 (&v)[16], float2 *lds, const tw16x2 &w, int t)
+{
     dft16<DIR>(v);
-    twiddle16<DIR>(v, tw, t);   // W_4096^{t k}
+    twiddle16v<DIR>(v, w.p1a, w.p1b);   // W_4096^{t k}
     __syncthreads();
 #pragma unroll
     for (int k = 0; k < 16; k++) lds[k * 272 + t] = v[k];   // row pad 16: conflict-free reads below
@@ -365,7 +405,7 @@ __device__ __forceinline__ void fft4096_r16(float2 (&v)[16], float2 *lds, const 
 #pragma unroll
     for (int m = 0; m < 16; m++) v[m] = lds[k2 * 272 + m0 + 16 * m];
     dft16<DIR>(v);
-    twiddle16<DIR>(v, tw, 16 * m0);   // W_256^{m0 j} = W_4096^{16 m0 j}
+    twiddle16v<DIR>(v, w.p2a, w.p2b);   // W_256^{m0 j} = W_4096^{16 m0 j}
     __syncthreads();
 #pragma unroll
     for (int j = 0; j < 16; j++) lds[(k2 + 16 * j) * 17 + m0] = v[j];
