@@ -170,7 +170,9 @@ void fft_four_step(unsigned n, int dir, const void *x, void *y, long long batch,
 {
     unsigned lg = 0;
     while ((1u << lg) < n) lg++;
-    const int N1 = 1 << (lg / 2), N2 = (int)(n / (unsigned)N1);   // N1 <= N2 <= 4096 for n <= 2^24
+    // the larger factor on the column pass (N2 <= N1 <= 4096 for n <= 2^24): for odd lg the
+    // 2^k-point column transforms with the double-precision twiddle run in registers
+    const int N1 = 1 << ((lg + 1) / 2), N2 = (int)(n / (unsigned)N1);
     switch (N1) {
     case 64: launch_cols<64>(x, work, n, N2, dir, batch, st); break;
     case 128: launch_cols<128>(x, work, n, N2, dir, batch, st); break;
@@ -181,6 +183,7 @@ void fft_four_step(unsigned n, int dir, const void *x, void *y, long long batch,
     default: launch_cols_r<16>(x, work, n, N2, dir, batch, st); break;
     }
     switch (N2) {
+    case 64: launch_rows<64>(work, y, n, N1, dir, batch, st); break;
     case 128: launch_rows<128>(work, y, n, N1, dir, batch, st); break;
     case 256: launch_rows_r<1>(work, y, n, N1, dir, batch, st); break;
     case 512: launch_rows_r<2>(work, y, n, N1, dir, batch, st); break;
@@ -205,23 +208,31 @@ __device__ __forceinline__ float2 chirp(long long j, long long n, int dir)
     return make_float2((float)c, (float)s);
 }
 
+// the chirp table c[j], j < n, once per call (double phases, rounded once)
+__global__ void k_bs_chirp(long long n, int dir, float2 *__restrict__ c)
+{
+    const long long j = (long long)blockIdx.x * NT + threadIdx.x;
+    if (j < n) c[j] = chirp(j, n, dir);
+}
+
 // b[j] = conj(c[j]) circularly on M points (|j| < n)
-__global__ void k_bs_kernel(long long n, long long M, int dir, float2 *__restrict__ b)
+__global__ void k_bs_kernel(long long n, long long M, const float2 *__restrict__ c, float2 *__restrict__ b)
 {
     const long long j = (long long)blockIdx.x * NT + threadIdx.x;
     if (j >= M) return;
     float2 v = make_float2(0.f, 0.f);
-    if (j < n) v = chirp(j, n, dir);
-    else if (j > M - n) v = chirp(M - j, n, dir);
+    if (j < n) v = c[j];
+    else if (j > M - n) v = c[M - j];
     b[j] = make_float2(v.x, -v.y);
 }
 
-__global__ void k_bs_pre(const float2 *__restrict__ x, float2 *__restrict__ a, long long n, long long M, int dir)
+__global__ void k_bs_pre(const float2 *__restrict__ x, float2 *__restrict__ a, long long n, long long M,
+                         const float2 *__restrict__ c)
 {
     const long long e = (long long)blockIdx.x * NT + threadIdx.x;
     const long long z = blockIdx.y;
     if (e >= M) return;
-    a[z * M + e] = e < n ? cmul(x[z * n + e], chirp(e, n, dir)) : make_float2(0.f, 0.f);
+    a[z * M + e] = e < n ? cmul(x[z * n + e], c[e]) : make_float2(0.f, 0.f);
 }
 
 __global__ void k_bs_mul(float2 *__restrict__ a, const float2 *__restrict__ B, long long M)
@@ -232,13 +243,14 @@ __global__ void k_bs_mul(float2 *__restrict__ a, const float2 *__restrict__ B, l
     a[z * M + e] = cmul(a[z * M + e], B[e]);
 }
 
-__global__ void k_bs_post(const float2 *__restrict__ a, float2 *__restrict__ y, long long n, long long M, int dir)
+__global__ void k_bs_post(const float2 *__restrict__ a, float2 *__restrict__ y, long long n, long long M,
+                          const float2 *__restrict__ c)
 {
     const long long k = (long long)blockIdx.x * NT + threadIdx.x;
     const long long z = blockIdx.y;
     if (k >= n) return;
     const float inv = 1.0f / (float)M;
-    y[z * n + k] = cscale(cmul(a[z * M + k], chirp(k, n, dir)), inv);
+    y[z * n + k] = cscale(cmul(a[z * M + k], c[k]), inv);
 }
 
 // real-to-real transforms: fft_r2r_1d.c:95-250 (un-normalised, factor 2)
@@ -299,8 +311,8 @@ extern "C" size_t lqk_fft_work_bytes(unsigned int n, unsigned long long batch)
     if (n <= 16) return 0;
     unsigned long long M = 1;
     while (M < 2ull * n - 1) M <<= 1;
-    // a: M per transform, B: M, four-step scratch for M
-    return (size_t)(M * batch + M + (M > 4096 ? M * batch : 0)) * sizeof(float2);
+    // a: M per transform, B: M, four-step scratch for M, the n-entry chirp table
+    return (size_t)(M * batch + M + (M > 4096 ? M * batch : 0) + n) * sizeof(float2);
 }
 
 extern "C" void lqk_fft_any(unsigned int n, int dir, const void *x, void *y, unsigned long long batch, void *work,
@@ -326,19 +338,24 @@ extern "C" void lqk_fft_any(unsigned int n, int dir, const void *x, void *y, uns
     float2 *a = (float2 *)work;
     float2 *B = a + M * (long long)batch;
     float2 *w4 = B + M;
-    // chirp transform (cached by the caller through lqk_fft_plan when repeated; cheap relative to n log n)
-    hipLaunchKernelGGL(k_bs_kernel, dim3((unsigned)((M + NT - 1) / NT)), dim3(NT), 0, st, (long long)n, M, dir, B);
+    float2 *ct = w4 + (M > 4096 ? M * (long long)batch : 0);
+    hipLaunchKernelGGL(k_bs_chirp, dim3((unsigned)((n + NT - 1) / NT)), dim3(NT), 0, st, (long long)n, dir, ct);
+    LQ_CHECK_LAUNCH();
+    // chirp transform (once per call; cheap relative to the batch's n log n)
+    hipLaunchKernelGGL(k_bs_kernel, dim3((unsigned)((M + NT - 1) / NT)), dim3(NT), 0, st, (long long)n, M,
+                       (const float2 *)ct, B);
     LQ_CHECK_LAUNCH();
     fft_pow2((unsigned)M, +1, B, B, 1, w4, st);
     const dim3 gM((unsigned)((M + NT - 1) / NT), (unsigned)batch);
-    hipLaunchKernelGGL(k_bs_pre, gM, dim3(NT), 0, st, (const float2 *)x, a, (long long)n, M, dir);
+    hipLaunchKernelGGL(k_bs_pre, gM, dim3(NT), 0, st, (const float2 *)x, a, (long long)n, M, (const float2 *)ct);
     LQ_CHECK_LAUNCH();
     fft_pow2((unsigned)M, +1, a, a, (long long)batch, w4, st);
     hipLaunchKernelGGL(k_bs_mul, gM, dim3(NT), 0, st, a, (const float2 *)B, M);
     LQ_CHECK_LAUNCH();
     fft_pow2((unsigned)M, -1, a, a, (long long)batch, w4, st);
     const dim3 gn((unsigned)((n + NT - 1) / NT), (unsigned)batch);
-    hipLaunchKernelGGL(k_bs_post, gn, dim3(NT), 0, st, (const float2 *)a, (float2 *)y, (long long)n, M, dir);
+    hipLaunchKernelGGL(k_bs_post, gn, dim3(NT), 0, st, (const float2 *)a, (float2 *)y, (long long)n, M,
+                       (const float2 *)ct);
     LQ_CHECK_LAUNCH();
 }
 
