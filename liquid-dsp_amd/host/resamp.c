@@ -55,6 +55,7 @@ struct lq_rs_s {
     void *d_taps2;                /* (npfb+1) x LP interpolation pairs on one window (lq_kernels.h) */
     rs_plan pl;
     int periodic_failed;          /* no period <= RS_MAX_PERIOD at this rate */
+    int rate_changed;             /* set_rate / adjust_rate since the last plan */
     unsigned long long gpos;      /* inputs consumed since the plan origin */
     rs_state now;                 /* timing state at gpos */
     void *d_hist[2];              /* last L inputs */
@@ -252,7 +253,11 @@ static unsigned long long rs_ensure_plan(lq_rs *q, unsigned long long nx)
      * so per-sample execute() calls reuse one plan instead of building and
      * uploading one each (two stream synchronisations per call) */
     unsigned long long c = nx < RS_DIRECT_CHUNK ? nx : RS_DIRECT_CHUNK;
-    rs_plan_build_direct(q, c > RS_DIRECT_AHEAD ? c : RS_DIRECT_AHEAD);
+    /* right after a rate change the plan covers just this call: a loop that
+     * steers the rate before every call (symsync-style) would otherwise build
+     * RS_DIRECT_AHEAD inputs of schedule per call and use a fraction */
+    rs_plan_build_direct(q, (c > RS_DIRECT_AHEAD || q->rate_changed) ? c : RS_DIRECT_AHEAD);
+    q->rate_changed = 0;
     rs_plan_upload(q);
     return c;
 }
@@ -379,6 +384,7 @@ static void rs_new_del(lq_rs *q, float del)
     q->del = del;
     q->pl.valid = 0;
     q->periodic_failed = 0;
+    q->rate_changed = 1;
 }
 
 static void lq_rs_set_rate(lq_rs *_q, float _rate)

@@ -133,6 +133,46 @@ def main():
         report("firpfbch2_crcf synthesizer M=%d m=4" % Mc, ms, nbc * Mc // 2, "output samples", 12 * nbc * Mc,
                "8 B/channel sample in + 8 B/output (M/2 per block)")
         q2.destroy()
+    # resamp timing plans (host/resamp.c): wall clock per call including the
+    # host's plan work -- a periodic rate (plan built once, then cached), a
+    # rate whose float32 timing has no period <= 2^25 inputs (a direct plan of
+    # the call's inputs built serially on the host per call), and a
+    # symsync-style loop that steers the rate before every 4096-input call
+    import time
+    n = 1 << 24
+    x = cbuf(n)
+    y = torch.empty(2 * 2 * n, device="cuda")
+    # (float32 timing periods at npfb = 64: r = 1.037 1 011 163 inputs,
+    # r = 0.9999999 8 388 609; every rate tried has a period below 2^24)
+    for name, rate in (("r=1.037", 1.037), ("r=0.9999999", 0.9999999)):
+        rs = LQ.Resamp(rate, 7, 0.4, 60.0, 64)
+        rs.set_stream(S)
+        t0 = time.perf_counter()
+        rs.execute_block_dev(x.data_ptr(), n, y.data_ptr())   # first call: period search + plan build
+        rs.synchronize()
+        print(json.dumps({"workload": "resamp_crcf %s m=7, first 2^24-input call (host period search + plan)" % name,
+                          "ms": round((time.perf_counter() - t0) * 1e3, 2)}))
+        t0 = time.perf_counter()
+        for _ in range(4):
+            rs.execute_block_dev(x.data_ptr(), n, y.data_ptr())
+        rs.synchronize()
+        dt = (time.perf_counter() - t0) / 4
+        print(json.dumps({"workload": "resamp_crcf %s m=7, later 2^24-input calls (plan cached), wall clock" % name,
+                          "ms": round(dt * 1e3, 3), "value": n / dt / 1e6, "unit": "M input samples/s"}))
+        rs.destroy()
+    rs = LQ.Resamp(1.037, 7, 0.4, 60.0, 64)
+    rs.set_stream(S)
+    nc, calls = 4096, 200
+    t0 = time.perf_counter()
+    for i in range(calls):
+        rs.set_rate(1.037 + (1e-6 if i & 1 else -1e-6))   # (adjust_rate clips the rate to 0.5, resamp.c:222-239)
+        rs.execute_block_dev(x.data_ptr(), nc, y.data_ptr())
+    rs.synchronize()
+    dt = (time.perf_counter() - t0) / calls
+    print(json.dumps({"workload": "resamp_crcf set_rate before every 4096-input call (direct plan per call)",
+                      "ms": round(dt * 1e3, 4), "value": nc / dt / 1e6, "unit": "M input samples/s"}))
+    rs.destroy()
+    del x, y
     # resamp2 decim / interp (m = 12), msresamp r = 0.3 / 3.3
     n = 1 << 26
     x = cbuf(n)
