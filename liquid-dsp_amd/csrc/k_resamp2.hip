@@ -171,6 +171,107 @@ __global__ __launch_bounds__(NT) void k_resamp2_tiled(R2Args a, const C *__restr
     }
 }
 
+// k_resamp2_tiled with the mode a template parameter and the E_0 / E_1
+// spans staged branch-free: every sample comes through range-checked buffer
+// loads of the history (2m samples) and of x (zero outside), all of a lane's
+// loads issued before the first LDS store (the generic staging loop branched
+// per element and waited for each load in turn).  32-bit offsets: the host
+// takes this path for calls of < 2^31 bytes of input.
+template <typename S>
+__device__ __forceinline__ S r2_ldb(__amdgpu_buffer_rsrc_t r, long long idx)
+{
+    const unsigned off = (unsigned)(idx * (long long)sizeof(S));   // idx < 0: out of range, 0
+    if constexpr (sizeof(S) == 8)
+        return __builtin_bit_cast(S, __builtin_amdgcn_raw_buffer_load_b64(r, off, 0, 0));
+    else
+        return __builtin_bit_cast(S, __builtin_amdgcn_raw_buffer_load_b32(r, off, 0, 0));
+}
+
+template <typename S, typename C, int R, int MODE>
+__global__ __launch_bounds__(NT) void k_resamp2_tiled_b(R2Args a, const C *__restrict__ taps,
+                                                        const S *__restrict__ hist0, const S *__restrict__ hist1,
+                                                        const S *__restrict__ x, S *__restrict__ y0)
+{
+    constexpr int CT = NT * R;
+    constexpr int NU = (CT + 32 - 1 + NT - 1) / NT;   // staging slots per lane (2m <= 32)
+    extern __shared__ __attribute__((aligned(16))) unsigned char r2_smem[];
+    const int m = a.m, W = 2 * m;
+    C *th = reinterpret_cast<C *>(r2_smem);
+    S *e1 = reinterpret_cast<S *>(r2_smem + ((2 * W * sizeof(C) + 15) & ~15));
+    S *e0 = e1 + CT + W;
+    const long long i0 = (long long)blockIdx.x * CT;
+    const int ES = (int)sizeof(S);
+    const long long nx = MODE == LQK_R2_INTERP ? a.n : 2 * a.n;
+    const __amdgpu_buffer_rsrc_t rx = __builtin_amdgcn_make_buffer_rsrc((void *)x, (short)0, (int)(nx * ES), 0x00020000);
+    const __amdgpu_buffer_rsrc_t rh0 = __builtin_amdgcn_make_buffer_rsrc((void *)hist0, (short)0, W * ES, 0x00020000);
+    const __amdgpu_buffer_rsrc_t rh1 = __builtin_amdgcn_make_buffer_rsrc((void *)hist1, (short)0, W * ES, 0x00020000);
+    // E_p[k]: history part (k < W) + push part c = k - W (zero where out of range)
+    auto E = [&](int p, long long k, S &h, S &u, S &v) {
+        const long long c = k - W;
+        h = r2_ldb<S>(p ? rh1 : rh0, k);
+        if constexpr (MODE == LQK_R2_INTERP) {
+            u = r2_ldb<S>(rx, c);
+        } else if constexpr (MODE == LQK_R2_SYNTHESIZER) {
+            u = r2_ldb<S>(rx, 2 * c);
+            v = r2_ldb<S>(rx, 2 * c + 1);
+        } else {   // decim, analyzer: w1 <- x[2c], w0 <- x[2c+1]
+            u = r2_ldb<S>(rx, 2 * c + (p ? 0 : 1));
+        }
+    };
+    auto combine = [&](int p, S h, S u, S v) -> S {
+        if constexpr (MODE == LQK_R2_SYNTHESIZER) return r2_add(h, p ? r2_sub(u, v) : r2_add(u, v));
+        else if constexpr (MODE == LQK_R2_ANALYZER) return r2_add(h, r2_scale(0.5f, u));
+        else return r2_add(h, u);
+    };
+    for (int j = threadIdx.x; j < W; j += NT) th[j] = taps[j];
+    {
+        S h[NU], u[NU], v[NU];
+#pragma unroll
+        for (int q = 0; q < NU; q++) E(1, i0 + 1 + threadIdx.x + q * NT, h[q], u[q], v[q]);
+#pragma unroll
+        for (int q = 0; q < NU; q++) {
+            const int idx = threadIdx.x + q * NT;
+            if (idx < CT + W - 1) e1[idx] = combine(1, h[q], u[q], v[q]);
+        }
+    }
+    {
+        constexpr int N0 = CT / NT;
+        S h[N0], u[N0], v[N0];
+#pragma unroll
+        for (int q = 0; q < N0; q++) E(0, W + i0 + threadIdx.x + q * NT - m, h[q], u[q], v[q]);
+#pragma unroll
+        for (int q = 0; q < N0; q++) e0[threadIdx.x + q * NT] = combine(0, h[q], u[q], v[q]);
+    }
+    __syncthreads();
+    // lane t takes calls t, t + NT, ...: the window reads of a wave are
+    // consecutive (conflict-free) and every store instruction covers
+    // consecutive outputs
+    const int l0 = threadIdx.x;
+    S acc[R];
+#pragma unroll
+    for (int r = 0; r < R; r++) acc[r] = S{};
+    for (int j = 0; j < W; j++) {
+        const C hj = th[j];
+#pragma unroll
+        for (int r = 0; r < R; r++) acc[r] = r2_mac(hj, e1[l0 + NT * r + j], acc[r]);
+    }
+#pragma unroll
+    for (int r = 0; r < R; r++) {
+        const long long i = i0 + l0 + NT * r;
+        if (i >= a.n) break;
+        const S yq = acc[r], yd = e0[l0 + NT * r];
+        if constexpr (MODE == LQK_R2_DECIM) {
+            y0[i] = r2_scale(a.scale, r2_add(yd, yq));
+        } else if constexpr (MODE == LQK_R2_ANALYZER) {
+            y0[2 * i] = r2_add(yq, yd);
+            y0[2 * i + 1] = r2_sub(yq, yd);
+        } else {
+            y0[2 * i] = yd;
+            y0[2 * i + 1] = yq;
+        }
+    }
+}
+
 // new history: hist_p[k] = E_p[pushes_p + k], k < 2m
 template <typename S>
 __global__ __launch_bounds__(NT) void k_resamp2_hist(R2Args a, long long push0, long long push1,
@@ -207,8 +308,21 @@ void run_r2(const R2Args &a, const void *taps, const void *h0, const void *h1, v
         constexpr int R = 4, CT = NT * R;
         const size_t lds = ((2 * 2 * a.m * sizeof(C) + 15) & ~(size_t)15) + (size_t)(2 * CT + 2 * a.m) * sizeof(S);
         const unsigned grid = (unsigned)((a.n + CT - 1) / CT);
-        hipLaunchKernelGGL((k_resamp2_tiled<S, C, R>), dim3(grid), dim3(NT), lds, st, a, (const C *)taps,
-                           (const S *)h0, (const S *)h1, (const S *)x, (S *)y0);
+        const long long xbytes = (a.mode == LQK_R2_INTERP ? a.n : 2 * a.n) * (long long)sizeof(S);
+        if (a.m <= 16 && xbytes < (1ll << 31)) {
+            switch (a.mode) {
+#define LQ_R2B(MD)                                                                                         \
+    case MD:                                                                                               \
+        hipLaunchKernelGGL((k_resamp2_tiled_b<S, C, R, MD>), dim3(grid), dim3(NT), lds, st, a, (const C *)taps, \
+                           (const S *)h0, (const S *)h1, (const S *)x, (S *)y0);                           \
+        break;
+                LQ_R2B(LQK_R2_DECIM) LQ_R2B(LQK_R2_ANALYZER) LQ_R2B(LQK_R2_INTERP) LQ_R2B(LQK_R2_SYNTHESIZER)
+#undef LQ_R2B
+            }
+        } else {
+            hipLaunchKernelGGL((k_resamp2_tiled<S, C, R>), dim3(grid), dim3(NT), lds, st, a, (const C *)taps,
+                               (const S *)h0, (const S *)h1, (const S *)x, (S *)y0);
+        }
     }
     LQ_CHECK_LAUNCH();
     hipLaunchKernelGGL((k_resamp2_hist<S>), dim3((unsigned)((4 * a.m + NT - 1) / NT)), dim3(NT), 0, st, a, p0, p1,
