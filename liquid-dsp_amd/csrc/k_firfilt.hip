@@ -442,6 +442,140 @@ __global__ __launch_bounds__(NT_) void k_firdecim_ph(const typename kt<KIND>::T 
         if (o + rr < nout) y[o + rr] = acc[rr];
 }
 
+// Phase-layout decimator, second form: four consecutive outputs per lane
+// and taps in chunks of four (QC a multiple of 4 instead of 4/8/16/32: the
+// BASELINE-style M = 8, m = 8 filter has 17 taps per phase, padded to 20
+// rather than 32).  Each phase row is stored de-interleaved by four
+// (column j at (j & 3) Q4 + j / 4), so the window reads of a wave -- lanes
+// four outputs apart -- are consecutive (conflict-free) and a lane's seven
+// window samples per tap chunk serve 16 multiply-adds.  The staging divides
+// by M with a float reciprocal and an exact integer correction.
+template <int R>
+__host__ __device__ __forceinline__ int dph2_q(int J) { return (J + R - 1) / R + 1; }   // 1/R-row stride (+1 pad)
+
+#ifndef DNU
+#define DNU 4
+#endif
+template <int KIND, int R, int NT_>
+__global__ __launch_bounds__(NT_) void k_firdecim_ph2(const typename kt<KIND>::T *__restrict__ hist, int hl1,
+                                                      const typename kt<KIND>::T *__restrict__ x, long long nout,
+                                                      int M, int QC, typename kt<KIND>::T *__restrict__ y,
+                                                      const typename kt<KIND>::TC *__restrict__ hq)
+{
+    typedef typename kt<KIND>::T T;
+    typedef typename kt<KIND>::TC TC;
+    constexpr int TO = NT_ * R;
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    T *P = reinterpret_cast<T *>(smem);
+    const int J = TO + QC - 1;
+    const int QR = dph2_q<R>(J), pitch = R * QR + 1;
+    const long long o0 = (long long)blockIdx.x * TO;
+    const long long nin = nout * M;
+    const long long sa = o0 * M - (long long)QC * M;
+    const int S = J * M + 1;
+    const float rM = 1.0f / (float)M;
+    constexpr int VW = 16 / (int)sizeof(T);
+    const bool vec_ok = (reinterpret_cast<uintptr_t>(x) & 15) == 0;
+    auto put = [&](int v0, const T (&e)[VW]) {
+#pragma unroll
+        for (int i = 0; i < VW; i++) {
+            const int u = v0 + i - 1;
+            if (u >= 0 && u < S - 1) {
+                int j = (int)((float)u * rM);   // u < 2^24: off by at most one
+                j -= (j * M > u) ? 1 : 0;
+                j += ((j + 1) * M <= u) ? 1 : 0;
+                const int ph = u - j * M;
+                P[ph * pitch + (j % R) * QR + j / R] = e[i];
+            }
+        }
+    };
+    if (vec_ok && nin * (long long)sizeof(T) < (1ll << 31)) {
+        // DNU 16-byte loads per lane in flight at a time through a
+        // range-checked descriptor (zeros outside x; sa is a multiple of VW,
+        // so a vector never straddles x's start); the history only reaches
+        // the first tile
+        typedef float v4f_ __attribute__((ext_vector_type(4)));
+        const __amdgpu_buffer_rsrc_t rx =
+            __builtin_amdgcn_make_buffer_rsrc((void *)x, (short)0, (int)(nin * (long long)sizeof(T)), 0x00020000);
+        for (int vb = threadIdx.x * VW; vb < S; vb += DNU * NT_ * VW) {
+            T e[DNU][VW];
+#pragma unroll
+            for (int k = 0; k < DNU; k++) {
+                const long long sk = sa + vb + k * NT_ * VW;
+                const unsigned off = (unsigned)(sk * (long long)sizeof(T));
+                const v4f_ v = __builtin_bit_cast(v4f_, __builtin_amdgcn_raw_buffer_load_b128(rx, off, 0, 0));
+                if constexpr (VW == 2) {
+                    e[k][0] = make_float2(v.x, v.y);
+                    e[k][1] = make_float2(v.z, v.w);
+                } else {
+                    e[k][0] = v.x;
+                    e[k][1] = v.y;
+                    e[k][2] = v.z;
+                    e[k][3] = v.w;
+                }
+            }
+            if (sa < 0) {   // first tile: samples before the call come from the history
+#pragma unroll
+                for (int k = 0; k < DNU; k++)
+#pragma unroll
+                    for (int i = 0; i < VW; i++) {
+                        const long long si = sa + vb + k * NT_ * VW + i;
+                        if (si < 0 && si >= -(long long)hl1) e[k][i] = hist[hl1 + si];
+                    }
+            }
+#pragma unroll
+            for (int k = 0; k < DNU; k++) {
+                const int v0 = vb + k * NT_ * VW;
+                if (v0 < S) put(v0, e[k]);
+            }
+        }
+    } else {
+        for (int v0 = threadIdx.x * VW; v0 < S; v0 += NT_ * VW) {
+            const long long s = sa + v0;
+            T e[VW];
+#pragma unroll
+            for (int i = 0; i < VW; i++) {
+                const long long si = s + i;
+                T val = zero<T>();
+                if (si < 0) {
+                    if (si >= -(long long)hl1) val = hist[hl1 + si];
+                } else if (si < nin) {
+                    val = x[si];
+                }
+                e[i] = val;
+            }
+            put(v0, e);
+        }
+    }
+    __syncthreads();
+    T acc[R];
+#pragma unroll
+    for (int rr = 0; rr < R; rr++) acc[rr] = zero<T>();
+    const int tb = threadIdx.x * R;
+    for (int ph = 0; ph < M; ph++) {
+        const T *row = P + ph * pitch;
+        const TC *hr = hq + (M - 1 - ph) * QC;
+        for (int c = 0; c < QC; c += 4) {
+            // window columns tb + QC - c - 4 + i, i < R + 3; the base is a
+            // multiple of R, so column base + i sits at (i % R) QR + base/R + i/R
+            const int bR = (tb + QC - c - 4) / R;
+            T w[R + 3];
+#pragma unroll
+            for (int i = 0; i < R + 3; i++) w[i] = row[(i % R) * QR + bR + i / R];
+#pragma unroll
+            for (int q = 0; q < 4; q++) {
+                const TC h = hr[c + q];
+#pragma unroll
+                for (int rr = 0; rr < R; rr++) mac(acc[rr], h, w[3 + rr - q]);
+            }
+        }
+    }
+    const long long o = o0 + tb;
+#pragma unroll
+    for (int rr = 0; rr < R; rr++)
+        if (o + rr < nout) y[o + rr] = acc[rr];
+}
+
 // ------------------------------------------------------------------ firinterp
 // one input sample per lane -> M outputs; hpoly[p*L + l] = h'[p + l*M]
 template <int KIND>
@@ -726,8 +860,9 @@ int decim_ph_qct(unsigned M, unsigned QC, const void *hq, unsigned hl1, const vo
     case 16: return decim_ph_shape<KIND, 16>(M, QC, hq, hl1, hist, x, nout, y, st);
     case 32: return decim_ph_shape<KIND, 32>(M, QC, hq, hl1, hist, x, nout, y, st);
     default:
-        if (QC % 16) return -1;
-        return decim_ph_shape<KIND, 16>(M, QC, hq, hl1, hist, x, nout, y, st);
+        if (QC % 16 == 0) return decim_ph_shape<KIND, 16>(M, QC, hq, hl1, hist, x, nout, y, st);
+        if (QC % 4 == 0) return decim_ph_shape<KIND, 4>(M, QC, hq, hl1, hist, x, nout, y, st);
+        return -1;
     }
 }
 } // namespace
@@ -735,11 +870,7 @@ int decim_ph_qct(unsigned M, unsigned QC, const void *hq, unsigned hl1, const vo
 extern "C" unsigned lqk_firdecim_ph_qc(unsigned M, unsigned hlen)
 {
     const unsigned q0 = (hlen + M - 1) / M;
-    if (q0 <= 4) return 4;
-    if (q0 <= 8) return 8;
-    if (q0 <= 16) return 16;
-    if (q0 <= 32) return 32;
-    return (q0 + 15) / 16 * 16;
+    return (q0 + 3) / 4 * 4;   // k_firdecim_ph2 runs taps in chunks of four
 }
 
 extern "C" int lqk_firdecim_ph(int kind, unsigned int M, unsigned int QC, const void *hq, unsigned int hl1,
@@ -747,6 +878,31 @@ extern "C" int lqk_firdecim_ph(int kind, unsigned int M, unsigned int QC, const 
 {
     if (nout == 0) return 0;
     hipStream_t st = (hipStream_t)stream;
+    {
+        // four outputs per lane, 128 lanes: 512 outputs and (512 + QC - 1) M
+        // input samples per workgroup in LDS
+#ifndef LQ_D2R
+#define LQ_D2R 2
+#define LQ_D2NT 256
+#endif
+        constexpr int TO2 = LQ_D2R * LQ_D2NT;
+        const int J = TO2 + (int)QC - 1;
+        const size_t lds = (size_t)M * (LQ_D2R * dph2_q<LQ_D2R>(J) + 1) * elem_size(kind);
+        if ((QC % 4) == 0 && lds <= 64 * 1024 && (unsigned long long)(J) * M < (1u << 24)) {
+            const unsigned nb = (unsigned)((nout + TO2 - 1) / TO2);
+#define LQ_D2(K)                                                                                          \
+    hipLaunchKernelGGL((k_firdecim_ph2<K, LQ_D2R, LQ_D2NT>), dim3(nb), dim3(LQ_D2NT), lds, st, (const kt<K>::T *)hist, (int)hl1, \
+                       (const kt<K>::T *)x, (long long)nout, (int)M, (int)QC, (kt<K>::T *)y, (const kt<K>::TC *)hq);
+            switch (kind) {
+            case 0: LQ_D2(0) break;
+            case 1: LQ_D2(1) break;
+            default: LQ_D2(2) break;
+            }
+#undef LQ_D2
+            LQ_CHECK_LAUNCH();
+            return 0;
+        }
+    }
     switch (kind) {
     case 0: return decim_ph_qct<0>(M, QC, hq, hl1, hist, x, (long long)nout, y, st);
     case 1: return decim_ph_qct<1>(M, QC, hq, hl1, hist, x, (long long)nout, y, st);

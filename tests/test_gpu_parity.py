@@ -239,7 +239,7 @@ def test_dotprod_batch_vs_oracle(t, n):
 
 
 @pytest.mark.parametrize("t", ["rrrf", "crcf", "cccf"])
-@pytest.mark.parametrize("M,m", [(2, 2), (4, 3), (8, 5), (16, 4), (64, 4)])
+@pytest.mark.parametrize("M,m", [(2, 2), (4, 3), (8, 5), (8, 8), (16, 4), (64, 4)])
 def test_firdecim_vs_oracle(M, m, t):
     r = rng(M)
     x = samples(r, t, M * 5000)
