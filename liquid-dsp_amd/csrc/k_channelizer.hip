@@ -367,6 +367,7 @@ __global__ void k_pfb_syn_out(int M, int p, const TC *__restrict__ hsub, const f
 // P times and each tap once per run (the per-element kernels above re-load
 // both for every output).
 constexpr int RUN = 64;
+constexpr int RPF = 4;   // column samples kept in flight by the run kernels
 
 // firpfbch analyzer X (firpfbch.c:346-409): X[b][j] = sum_n h[i*P + n] x[(b-n)M + j], i = M-1-j
 template <int P, typename TC>
@@ -386,14 +387,25 @@ __global__ __launch_bounds__(256) void k_pfb_an_X_run(int M, const TC *__restric
 #pragma unroll
     for (int n = 1; n < P; n++) w[n] = ext_load(hist, HL, x, (b0 - n) * M + j);
     const long long be = b0 + RUN < nblocks ? b0 + RUN : nblocks;
-    for (long long b = b0; b < be; b++) {
-        w[0] = x[b * M + j];
-        float2 acc = make_float2(0.f, 0.f);
+    // the next RPF samples of the column are in flight (clamped indices, no
+    // branch): one load latency per RPF blocks instead of per block
+    float2 nx[RPF];
 #pragma unroll
-        for (int n = 0; n < P; n++) acc = pfb_mac(h[n], w[n], acc);
-        X[b * M + j] = acc;
+    for (int d = 0; d < RPF; d++) nx[d] = x[(b0 + d < be ? b0 + d : be - 1) * M + j];
+    for (long long b = b0; b < be; b += RPF) {
 #pragma unroll
-        for (int n = P - 1; n > 0; n--) w[n] = w[n - 1];
+        for (int d = 0; d < RPF; d++) {
+            if (b + d >= be) break;
+            w[0] = nx[d];
+            const long long bn = b + d + RPF;
+            nx[d] = x[(bn < be ? bn : be - 1) * M + j];
+            float2 acc = make_float2(0.f, 0.f);
+#pragma unroll
+            for (int n = 0; n < P; n++) acc = pfb_mac(h[n], w[n], acc);
+            X[(b + d) * M + j] = acc;
+#pragma unroll
+            for (int n = P - 1; n > 0; n--) w[n] = w[n - 1];
+        }
     }
 }
 
@@ -414,14 +426,23 @@ __global__ __launch_bounds__(256) void k_pfb_syn_out_run(int M, const TC *__rest
 #pragma unroll
     for (int n = 1; n < P; n++) w[n] = Z[(P - 1 + b0 - n) * M + i];
     const long long be = b0 + RUN < nblocks ? b0 + RUN : nblocks;
-    for (long long b = b0; b < be; b++) {
-        w[0] = Z[(P - 1 + b) * M + i];
-        float2 acc = make_float2(0.f, 0.f);
+    float2 nz[RPF];   // next RPF transforms' column samples in flight
 #pragma unroll
-        for (int n = 0; n < P; n++) acc = pfb_mac(h[n], w[n], acc);
-        y[b * M + i] = acc;
+    for (int d = 0; d < RPF; d++) nz[d] = Z[(P - 1 + (b0 + d < be ? b0 + d : be - 1)) * M + i];
+    for (long long b = b0; b < be; b += RPF) {
 #pragma unroll
-        for (int n = P - 1; n > 0; n--) w[n] = w[n - 1];
+        for (int d = 0; d < RPF; d++) {
+            if (b + d >= be) break;
+            w[0] = nz[d];
+            const long long bn = b + d + RPF;
+            nz[d] = Z[(P - 1 + (bn < be ? bn : be - 1)) * M + i];
+            float2 acc = make_float2(0.f, 0.f);
+#pragma unroll
+            for (int n = 0; n < P; n++) acc = pfb_mac(h[n], w[n], acc);
+            y[(b + d) * M + i] = acc;
+#pragma unroll
+            for (int n = P - 1; n > 0; n--) w[n] = w[n - 1];
+        }
     }
 }
 
@@ -451,25 +472,39 @@ __global__ __launch_bounds__(256) void k_pfb2_syn_out_run(int M, const float *__
         wb[k] = Z[(HB + b0 - k) * M + i + M2];
     }
     const long long be = b0 + RUN < nblocks ? b0 + RUN : nblocks;
-    for (long long b = b0; b < be; b++) {
-        wa[0] = Z[(HB + b) * M + i];
-        wb[0] = Z[(HB + b) * M + i + M2];
-        const bool f = ((p0 + b) & 1) != 0;
-        float2 acc0 = make_float2(0.f, 0.f), acc1 = make_float2(0.f, 0.f);
+    float2 na[RPF], nb2[RPF];   // next RPF transforms' column samples in flight
 #pragma unroll
-        for (int n = 0; n < L; n++) {
-            const float2 z0 = f ? wb[2 * n] : wa[2 * n];
-            const float2 z1 = f ? wb[2 * n + 1] : wa[2 * n + 1];
-            acc0.x = fmaf(h0[n], z0.x, acc0.x);
-            acc0.y = fmaf(h0[n], z0.y, acc0.y);
-            acc1.x = fmaf(h1[n], z1.x, acc1.x);
-            acc1.y = fmaf(h1[n], z1.y, acc1.y);
-        }
-        y[b * M2 + i] = cadd(acc0, acc1);
+    for (int d = 0; d < RPF; d++) {
+        const long long bc = b0 + d < be ? b0 + d : be - 1;
+        na[d] = Z[(HB + bc) * M + i];
+        nb2[d] = Z[(HB + bc) * M + i + M2];
+    }
+    for (long long b = b0; b < be; b += RPF) {
 #pragma unroll
-        for (int k = 2 * L - 1; k > 0; k--) {
-            wa[k] = wa[k - 1];
-            wb[k] = wb[k - 1];
+        for (int d = 0; d < RPF; d++) {
+            if (b + d >= be) break;
+            wa[0] = na[d];
+            wb[0] = nb2[d];
+            const long long bn = b + d + RPF < be ? b + d + RPF : be - 1;
+            na[d] = Z[(HB + bn) * M + i];
+            nb2[d] = Z[(HB + bn) * M + i + M2];
+            const bool f = ((p0 + b + d) & 1) != 0;
+            float2 acc0 = make_float2(0.f, 0.f), acc1 = make_float2(0.f, 0.f);
+#pragma unroll
+            for (int n = 0; n < L; n++) {
+                const float2 z0 = f ? wb[2 * n] : wa[2 * n];
+                const float2 z1 = f ? wb[2 * n + 1] : wa[2 * n + 1];
+                acc0.x = fmaf(h0[n], z0.x, acc0.x);
+                acc0.y = fmaf(h0[n], z0.y, acc0.y);
+                acc1.x = fmaf(h1[n], z1.x, acc1.x);
+                acc1.y = fmaf(h1[n], z1.y, acc1.y);
+            }
+            y[(b + d) * M2 + i] = cadd(acc0, acc1);
+#pragma unroll
+            for (int k = 2 * L - 1; k > 0; k--) {
+                wa[k] = wa[k - 1];
+                wb[k] = wb[k - 1];
+            }
         }
     }
 }
