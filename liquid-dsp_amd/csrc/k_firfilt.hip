@@ -160,23 +160,56 @@ __global__ __launch_bounds__(NT) void k_firfilt(const typename kt<KIND>::T *__re
     // (firfilt.c:322-338, hlen taps) keeps finite, so a tile holding a
     // non-finite sample runs the exact loop over the true taps instead
     bool bad = false;
-    for (int e = threadIdx.x; e < S / VE; e += NT) {
-        const int u = e * VE;
-        const long long s = t0 - HP + u;
-        T o[VE];
-        if (s < 0) {
-            load16(win + HP + s, o);
-        } else if (halo != nullptr && u < HP && blockIdx.x > 0) {
-            load16(halo + (size_t)blockIdx.x * HP + u, o);
-        } else if (s + VE <= n) {
-            load16(x + s, o);
-        } else {
+    if (halo == nullptr && ((reinterpret_cast<uintptr_t>(x) & 15) == 0) && n * (long long)sizeof(T) < (1ll << 31)) {
+        // four 16-byte loads per lane in flight through a range-checked
+        // descriptor (zeros past n, and before x: the first tile then takes
+        // those samples from the history) -- the branchy per-vector loop
+        // below waited for one load latency per iteration
+        const __amdgpu_buffer_rsrc_t rx =
+            __builtin_amdgcn_make_buffer_rsrc((void *)x, (short)0, (int)(n * (long long)sizeof(T)), 0x00020000);
+        constexpr int NV = 4;
+        for (int e0 = threadIdx.x; e0 < S / VE; e0 += NV * NT) {
+            float4 pv[NV];
 #pragma unroll
-            for (int i = 0; i < VE; i++) o[i] = (s + i < n) ? x[s + i] : zero<T>();
+            for (int k = 0; k < NV; k++) {
+                const long long s = t0 - HP + (long long)(e0 + k * NT) * VE;
+                pv[k] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(
+                                                       rx, (unsigned)(s * (long long)sizeof(T)), 0, 0));
+            }
+#pragma unroll
+            for (int k = 0; k < NV; k++) {
+                const int e = e0 + k * NT;
+                if (e >= S / VE) break;
+                const int u = e * VE;
+                const long long s = t0 - HP + u;
+                if (s < 0) {
+                    T o[VE];
+                    load16(win + HP + s, o);
+                    pv[k] = pack16(o);
+                }
+                if (hexact) bad |= !(isfinite(pv[k].x) && isfinite(pv[k].y) && isfinite(pv[k].z) && isfinite(pv[k].w));
+                *reinterpret_cast<float4 *>(smem + lds_off<T>(u)) = pv[k];
+            }
         }
-        const float4 pv = pack16(o);
-        if (hexact) bad |= !(isfinite(pv.x) && isfinite(pv.y) && isfinite(pv.z) && isfinite(pv.w));
-        *reinterpret_cast<float4 *>(smem + lds_off<T>(u)) = pv;
+    } else {
+        for (int e = threadIdx.x; e < S / VE; e += NT) {
+            const int u = e * VE;
+            const long long s = t0 - HP + u;
+            T o[VE];
+            if (s < 0) {
+                load16(win + HP + s, o);
+            } else if (halo != nullptr && u < HP && blockIdx.x > 0) {
+                load16(halo + (size_t)blockIdx.x * HP + u, o);
+            } else if (s + VE <= n) {
+                load16(x + s, o);
+            } else {
+#pragma unroll
+                for (int i = 0; i < VE; i++) o[i] = (s + i < n) ? x[s + i] : zero<T>();
+            }
+            const float4 pv = pack16(o);
+            if (hexact) bad |= !(isfinite(pv.x) && isfinite(pv.y) && isfinite(pv.z) && isfinite(pv.w));
+            *reinterpret_cast<float4 *>(smem + lds_off<T>(u)) = pv;
+        }
     }
     const bool exact = hexact ? __syncthreads_or(bad) : (__syncthreads(), false);
 
