@@ -588,13 +588,14 @@ def main():
         launch_ms = g_pfb / args.steps
         alg_bytes = 24.0 * pfb["n"]
         achieved = alg_bytes / (launch_ms * 1e-3) / 1e9
-        traffic = fir_traffic = rs_traffic = None
+        traffic = fir_traffic = rs_traffic = ff_traffic = None
         if os.path.exists(args.traffic_json):
             with open(args.traffic_json) as f:
                 tj = json.load(f)
             traffic = tj.get("firpfbch2_bytes_per_launch")
             fir_traffic = tj.get("firfilt_bytes_per_launch")
             rs_traffic = tj.get("resamp_bytes_per_launch")
+            ff_traffic = tj.get("fftfilt_bytes_per_launch")
         out = {
             "metric": "Msamples/s: firfilt_crcf h=64 & firpfbch2_crcf M=1024; %HBM roofline",
             "value": tot_pfb / t_pfb / 1e6,
@@ -672,7 +673,13 @@ def main():
                                                     "(BASELINE configs[2])" % ff["n"],
                                         "launch_ms": ms, "achieved_GBps": 16.0 * ff["n"] / (ms * 1e-3) / 1e9,
                                         "frac": 16.0 * ff["n"] / (ms * 1e-3) / 1e9 / HBM_PEAK_GBPS,
-                                        "bytes_per_unit": "16 B/sample"}
+                                        "bytes_per_unit": "16 B/sample",
+                                        "roofline": {"bound": "hbm",
+                                                     "achieved": 16.0 * ff["n"] / (ms * 1e-3) / 1e9,
+                                                     "peak": HBM_PEAK_GBPS, "unit": "GB/s",
+                                                     "frac": 16.0 * ff["n"] / (ms * 1e-3) / 1e9 / HBM_PEAK_GBPS,
+                                                     "traffic": ff_traffic, "bytes_per_unit": "16 B/sample",
+                                                     "launch_ms": ms}}
         if percall is not None:
             out["per_call"] = {"what": "the reference's per-call benchmark loops (src/*/bench/*_benchmark.c) "
                                        "linked against this library; wall clock; one GPU round trip per call",

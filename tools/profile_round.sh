@@ -21,7 +21,8 @@ for c in ("FETCH_SIZE", "WRITE_SIZE"):
     for r in csv.DictReader(open(f)):
         agg[r["Kernel_Name"]].append(float(r["Counter_Value"]))
     for k, v in agg.items():
-        key = "firpfbch2" if "pfb2" in k else ("firfilt" if "firfilt" in k else ("resamp" if "k_resamp" in k else None))
+        key = "firpfbch2" if "pfb2" in k else ("firfilt" if "firfilt" in k else ("resamp" if "k_resamp" in k else
+                                                                              ("fftfilt" if "k_fftfilt" in k else None)))
         if key:
             res.setdefault(key, {})[c] = sum(v) / len(v)
 traffic = {}
@@ -35,10 +36,12 @@ for key, d in res.items():
 json.dump({"firpfbch2_bytes_per_launch": traffic.get("firpfbch2", {}).get("total_bytes"),
            "firfilt_bytes_per_launch": traffic.get("firfilt", {}).get("total_bytes"),
            "resamp_bytes_per_launch": traffic.get("resamp", {}).get("total_bytes"),
+           "fftfilt_bytes_per_launch": traffic.get("fftfilt", {}).get("total_bytes"),
            "detail": traffic,
            "launch_shapes": {"firpfbch2": "M=1024 m=4, 2^27 input samples", "firfilt": "h=64, 2^28 samples",
                              "resamp": "r=1.037 m=7 npfb=64, 2^25 input samples (8-byte loads: the x2 FETCH "
-                                       "correction is calibrated for 16-byte streams only)"},
+                                       "correction is calibrated for 16-byte streams only)",
+                             "fftfilt": "h=512, 4096-point overlap-save, 2^26 samples"},
            "method": "rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE in separate passes over tools/prof_run.py; "
                      "FETCH_SIZE doubled per the gfx950 correction"},
           open(os.path.join(out, "traffic.json"), "w"), indent=1)
@@ -56,7 +59,8 @@ for r in csv.DictReader(open(f)):
     d[r["Kernel_Name"]].append((int(r["Start_Timestamp"]), int(r["End_Timestamp"])))
 res = {}
 for k, v in d.items():
-    key = "firpfbch2" if "pfb2" in k else ("firfilt" if ("k_firfilt<" in k or "k_firfilt_mx" in k) else ("resamp" if "k_resamp" in k else None))
+    key = "firpfbch2" if "pfb2" in k else ("firfilt" if ("k_firfilt<" in k or "k_firfilt_mx" in k) else
+                                           ("resamp" if "k_resamp" in k else ("fftfilt" if "k_fftfilt" in k else None)))
     if not key or len(v) < 50:
         continue
     v.sort()
