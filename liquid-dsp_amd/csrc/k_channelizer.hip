@@ -178,6 +178,124 @@ __global__ __launch_bounds__(256) void k_pfb2_poly(int M, int nsl, const float *
     }
 }
 
+// M = 256 analyzer fused: the polyphase pass above with all 256 columns in
+// one workgroup (one per lane), a ring of 8 rows in registers (L = 2m <= 8),
+// and each group of 8 rows' 16 completed blocks transformed in the same
+// kernel: X goes to a 17-buffer LDS ring (block b in buffer b mod 17; the
+// hi half of block 2r0+16 is written one group early), then 16 inverse
+// 256-point transforms run in registers (fft_r16x16xR<1>, 16 lanes each) and
+// the outputs, times 1/M, leave as consecutive 8-byte stores -- Y is written
+// once and never re-read (24 B per input instead of the two-pass 56).
+template <int L>
+__global__ __launch_bounds__(256, 2) void k_pfb2_an256(const float *__restrict__ hsub,
+                                                       const float2 *__restrict__ hist,
+                                                       const float2 *__restrict__ x, int n_in, int p0, int nb,
+                                                       int cmin, int cmax, int S, float2 *__restrict__ Y,
+                                                       const float2 *__restrict__ tw4096)
+{
+    constexpr int M = 256, M2 = 128, HL = L * M - M2, NS = 8, NBUF = 17;
+    constexpr int P = FFTR16_LDS<1>();
+    __shared__ __attribute__((aligned(16))) float2 xr[NBUF * M];
+    __shared__ __attribute__((aligned(16))) float2 scr[16 * P];
+    const int col = threadIdx.x;
+    const bool lo = col < M2;
+    const int j = lo ? (M2 - 1 - col) : (3 * M2 - 1 - col);
+    const int dA = lo ? 0 : 1;
+    float ta[L], tb[L];
+    {
+        const int ia = lo ? j : (j ^ M2), ib = lo ? (j ^ M2) : j;
+#pragma unroll
+        for (int n = 0; n < L; n++) {
+            ta[n] = hsub[ia * L + n];
+            tb[n] = hsub[ib * L + n];
+        }
+    }
+    const __amdgpu_buffer_rsrc_t rx = __builtin_amdgcn_make_buffer_rsrc((void *)x, (short)0, n_in * 8, 0x00020000);
+    const __amdgpu_buffer_rsrc_t rh = __builtin_amdgcn_make_buffer_rsrc((void *)hist, (short)0, HL * 8, 0x00020000);
+    const __amdgpu_buffer_rsrc_t ry = __builtin_amdgcn_make_buffer_rsrc((void *)Y, (short)0, nb * M * 8, 0x00020000);
+    auto row_sample = [&](int r) -> float2 {
+        const int t = r * M + col - p0 * M2;
+        const float2 a = __builtin_bit_cast(float2, __builtin_amdgcn_raw_buffer_load_b64(rx, (unsigned)t * 8u, 0, 0));
+        const float2 b =
+            __builtin_bit_cast(float2, __builtin_amdgcn_raw_buffer_load_b64(rh, (unsigned)(t + HL) * 8u, 0, 0));
+        return make_float2(a.x + b.x, a.y + b.y);
+    };
+    auto dot = [&](const float2 (&w)[NS], int newest, const float (&h)[L]) -> float2 {
+        float2 acc = make_float2(0.f, 0.f);
+#pragma unroll
+        for (int n = 0; n < L; n++) {
+            const float2 v = w[(newest - n) & (NS - 1)];
+            acc.x = fmaf(h[n], v.x, acc.x);
+            acc.y = fmaf(h[n], v.y, acc.y);
+        }
+        return acc;
+    };
+    auto slot = [](int b) { return ((b % NBUF) + NBUF) % NBUF; };
+    const int g = threadIdx.x >> 4, t = threadIdx.x & 15;   // transform g (block 2 r0 + g), its lane t
+    const tw16x2 w16 = fftr16_tw<1>(tw4096, t);
+    const float inv = 1.0f / (float)M;
+    typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
+
+    const int cs = cmin + (int)blockIdx.x * S;
+    int ce = cs + S;
+    if (ce > cmax + 1) ce = cmax + 1;
+    // rows cs-8 .. cs-1 fill the ring (slots r & 7); the last gives the hi
+    // half of block 2cs
+    float2 w[NS], pf[NS];
+#pragma unroll
+    for (int u = 0; u < NS; u++) w[u] = row_sample(cs - NS + u);
+    if (!lo) xr[slot(2 * cs) * M + j] = dot(w, NS - 1, tb);
+#pragma unroll
+    for (int u = 0; u < NS; u++) pf[u] = row_sample(cs + u);
+    for (int r0 = cs; r0 < ce; r0 += NS) {
+#pragma unroll
+        for (int u = 0; u < NS; u++) {
+            w[u] = pf[u];
+            pf[u] = row_sample(r0 + NS + u);
+            const int c = r0 + u;
+            xr[slot(2 * c + dA) * M + j] = dot(w, u, ta);
+            xr[slot(2 * c + dA + 1) * M + j] = dot(w, u, tb);
+        }
+        __syncthreads();
+        // blocks 2 r0 .. 2 r0 + 15 are complete: one transform per 16 lanes
+        const int b = 2 * r0 + g;
+        float2 v[16];
+        const float2 *B = xr + slot(b) * M;
+#pragma unroll
+        for (int n = 0; n < 16; n++) v[n] = B[t + 16 * n];
+        fft_r16x16xR<1, -1>(v, scr + g * P, w16, t);   // (its barriers also free the ring buffers)
+        const int gb = b - p0;
+        const bool keep = gb >= 0 && gb < nb && b < 2 * ce;
+        const unsigned base = keep ? (unsigned)gb * (unsigned)(M * 8) : 0xFFFFF000u;
+#pragma unroll
+        for (int sidx = 0; sidx < 16; sidx++) {
+            const float2 o = make_float2(v[sidx].x * inv, v[sidx].y * inv);
+            __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2, o), ry, base + (unsigned)(t + 16 * sidx) * 8u, 0, 0);
+        }
+    }
+}
+
+template <int L>
+bool launch_pfb2_an256(const void *hsub, const void *hist, const void *x, long long nb, int p0, void *Y, hipStream_t st)
+{
+    constexpr int M = 256;
+    const long long n_in = nb * (M / 2);
+    if (n_in * 8 >= (1ll << 31) || nb * (long long)M * 8 >= (1ll << 31)) return false;
+    const int cmin = (p0 - 1) >> 1;
+    const int cmax = (int)((p0 + nb - 1) >> 1);
+    const int rows = cmax - cmin + 1;
+    // runs of S rows (a multiple of 8): about 1024 workgroups on long calls
+    long long S = ((long long)rows + 1023) / 1024;
+    S = (S + 7) / 8 * 8;
+    if (S < 32) S = 32;
+    const long long nseg = (rows + S - 1) / S;
+    hipLaunchKernelGGL((k_pfb2_an256<L>), dim3((unsigned)nseg), dim3(256), 0, st, (const float *)hsub,
+                       (const float2 *)hist, (const float2 *)x, (int)n_in, p0, (int)nb, cmin, cmax, (int)S,
+                       (float2 *)Y, (const float2 *)lqrt_twiddles());
+    LQ_CHECK_LAUNCH();
+    return true;
+}
+
 template <int L>
 bool launch_pfb2_poly(int M, const void *hsub, const void *hist, const void *x, long long nb, int p0, void *Y,
                       hipStream_t st)
@@ -772,6 +890,17 @@ extern "C" void lqk_firpfbch2_analyzer(unsigned int M, unsigned int m, const voi
             const float2 *xc = (const float2 *)x + b0 * M2;
             const void *hc = b0 == 0 ? hist : (const void *)(xc - HL);
             float2 *Yc = (float2 *)Y + b0 * M;
+            if (M == 256 && 2 * m <= 8 && !getenv("LQ_PFB2_TWO_PASS")) {
+                bool f = false;
+                switch (2 * m) {
+                case 2: f = launch_pfb2_an256<2>(hsub, hc, xc, nbc, p0, Yc, st); break;
+                case 4: f = launch_pfb2_an256<4>(hsub, hc, xc, nbc, p0, Yc, st); break;
+                case 6: f = launch_pfb2_an256<6>(hsub, hc, xc, nbc, p0, Yc, st); break;
+                case 8: f = launch_pfb2_an256<8>(hsub, hc, xc, nbc, p0, Yc, st); break;
+                default: break;
+                }
+                if (f) continue;
+            }
             bool ok = false;
             switch (2 * m) {
             case 2: ok = launch_pfb2_poly<2>((int)M, hsub, hc, xc, nbc, p0, Yc, st); break;
