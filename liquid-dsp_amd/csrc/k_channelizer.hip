@@ -186,15 +186,18 @@ __global__ __launch_bounds__(256) void k_pfb2_poly(int M, int nsl, const float *
 // 256-point transforms run in registers (fft_r16x16xR<1>, 16 lanes each) and
 // the outputs, times 1/M, leave as consecutive 8-byte stores -- Y is written
 // once and never re-read (24 B per input instead of the two-pass 56).
-template <int L>
-__global__ __launch_bounds__(256, 2) void k_pfb2_an256(const float *__restrict__ hsub,
+template <int L, int R>
+__global__ __launch_bounds__(256 * R, R == 1 ? 2 : 1) void k_pfb2_an256(const float *__restrict__ hsub,
                                                        const float2 *__restrict__ hist,
                                                        const float2 *__restrict__ x, int n_in, int p0, int nb,
                                                        int cmin, int cmax, int S, float2 *__restrict__ Y,
                                                        const float2 *__restrict__ tw4096)
 {
-    constexpr int M = 256, M2 = 128, HL = L * M - M2, NS = 8, NBUF = 17;
-    constexpr int P = FFTR16_LDS<1>();
+    // M = 256 R columns, one per lane; R = 2 takes the tight transform
+    // scratch (17 x 4 KB ring + 16 x 4.3 KB scratch fits 160 KB)
+    constexpr int M = 256 * R, M2 = M / 2, HL = L * M - M2, NS = 8, NBUF = 17;
+    constexpr bool TIGHT = R > 1;
+    constexpr int P = FFTR16_LDS<R, TIGHT>();
     __shared__ __attribute__((aligned(16))) float2 xr[NBUF * M];
     __shared__ __attribute__((aligned(16))) float2 scr[16 * P];
     const int col = threadIdx.x;
@@ -231,8 +234,8 @@ __global__ __launch_bounds__(256, 2) void k_pfb2_an256(const float *__restrict__
         return acc;
     };
     auto slot = [](int b) { return ((b % NBUF) + NBUF) % NBUF; };
-    const int g = threadIdx.x >> 4, t = threadIdx.x & 15;   // transform g (block 2 r0 + g), its lane t
-    const tw16x2 w16 = fftr16_tw<1>(tw4096, t);
+    const int g = threadIdx.x / (16 * R), t = threadIdx.x % (16 * R);   // transform g (block 2 r0 + g), its lane t
+    const tw16x2 w16 = fftr16_tw<R>(tw4096, t);
     const float inv = 1.0f / (float)M;
     typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
 
@@ -262,23 +265,28 @@ __global__ __launch_bounds__(256, 2) void k_pfb2_an256(const float *__restrict__
         float2 v[16];
         const float2 *B = xr + slot(b) * M;
 #pragma unroll
-        for (int n = 0; n < 16; n++) v[n] = B[t + 16 * n];
-        fft_r16x16xR<1, -1>(v, scr + g * P, w16, t);   // (its barriers also free the ring buffers)
+        for (int n = 0; n < 16; n++) v[n] = B[t + 16 * R * n];
+        fft_r16x16xR<R, -1, TIGHT>(v, scr + g * P, w16, t);   // (its barriers also free the ring buffers)
         const int gb = b - p0;
         const bool keep = gb >= 0 && gb < nb && b < 2 * ce;
         const unsigned base = keep ? (unsigned)gb * (unsigned)(M * 8) : 0xFFFFF000u;
+        // v[s R + q] = X[t + 16 R s + 256 q]
 #pragma unroll
-        for (int sidx = 0; sidx < 16; sidx++) {
-            const float2 o = make_float2(v[sidx].x * inv, v[sidx].y * inv);
-            __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2, o), ry, base + (unsigned)(t + 16 * sidx) * 8u, 0, 0);
-        }
+        for (int sidx = 0; sidx < 16 / R; sidx++)
+#pragma unroll
+            for (int q = 0; q < R; q++) {
+                const float2 vv = v[sidx * R + q];
+                const float2 o = make_float2(vv.x * inv, vv.y * inv);
+                __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2, o), ry,
+                                                      base + (unsigned)(t + 16 * R * sidx + 256 * q) * 8u, 0, 0);
+            }
     }
 }
 
-template <int L>
+template <int L, int R>
 bool launch_pfb2_an256(const void *hsub, const void *hist, const void *x, long long nb, int p0, void *Y, hipStream_t st)
 {
-    constexpr int M = 256;
+    constexpr int M = 256 * R;
     const long long n_in = nb * (M / 2);
     if (n_in * 8 >= (1ll << 31) || nb * (long long)M * 8 >= (1ll << 31)) return false;
     const int cmin = (p0 - 1) >> 1;
@@ -289,7 +297,7 @@ bool launch_pfb2_an256(const void *hsub, const void *hist, const void *x, long l
     S = (S + 7) / 8 * 8;
     if (S < 32) S = 32;
     const long long nseg = (rows + S - 1) / S;
-    hipLaunchKernelGGL((k_pfb2_an256<L>), dim3((unsigned)nseg), dim3(256), 0, st, (const float *)hsub,
+    hipLaunchKernelGGL((k_pfb2_an256<L, R>), dim3((unsigned)nseg), dim3(256 * R), 0, st, (const float *)hsub,
                        (const float2 *)hist, (const float2 *)x, (int)n_in, p0, (int)nb, cmin, cmax, (int)S,
                        (float2 *)Y, (const float2 *)lqrt_twiddles());
     LQ_CHECK_LAUNCH();
@@ -890,15 +898,18 @@ extern "C" void lqk_firpfbch2_analyzer(unsigned int M, unsigned int m, const voi
             const float2 *xc = (const float2 *)x + b0 * M2;
             const void *hc = b0 == 0 ? hist : (const void *)(xc - HL);
             float2 *Yc = (float2 *)Y + b0 * M;
-            if (M == 256 && 2 * m <= 8 && !getenv("LQ_PFB2_TWO_PASS")) {
+            if ((M == 256 || M == 512) && 2 * m <= 8 && !getenv("LQ_PFB2_TWO_PASS")) {
                 bool f = false;
+#define LQ_F(LL)                                                                                           \
+    case LL:                                                                                               \
+        f = M == 256 ? launch_pfb2_an256<LL, 1>(hsub, hc, xc, nbc, p0, Yc, st)                            \
+                     : launch_pfb2_an256<LL, 2>(hsub, hc, xc, nbc, p0, Yc, st);                           \
+        break;
                 switch (2 * m) {
-                case 2: f = launch_pfb2_an256<2>(hsub, hc, xc, nbc, p0, Yc, st); break;
-                case 4: f = launch_pfb2_an256<4>(hsub, hc, xc, nbc, p0, Yc, st); break;
-                case 6: f = launch_pfb2_an256<6>(hsub, hc, xc, nbc, p0, Yc, st); break;
-                case 8: f = launch_pfb2_an256<8>(hsub, hc, xc, nbc, p0, Yc, st); break;
+                    LQ_F(2) LQ_F(4) LQ_F(6) LQ_F(8)
                 default: break;
                 }
+#undef LQ_F
                 if (f) continue;
             }
             bool ok = false;

@@ -325,12 +325,14 @@ __device__ __forceinline__ void dft_small(float2 *v)
 //   pass 3: unit (k2, q1) runs a DFT_R over a -> q2; X[k2 + 16 q1 + 256 q2]
 template <int R>
 constexpr int fftr16_s1() { return 16 * R + 2; }            // pass-1 row stride (conflict-free reads)
-template <int R>
-constexpr int fftr16_s2() { return R == 1 ? 1 : R + 1; }    // pass-2 unit stride (odd)
-template <int R>
+// pass-2 unit stride: odd (conflict-free pass-3 reads); TIGHT: R (2-way
+// conflicted, a smaller scratch for kernels short of LDS)
+template <int R, bool TIGHT = false>
+constexpr int fftr16_s2() { return (R == 1 || TIGHT) ? R : R + 1; }
+template <int R, bool TIGHT = false>
 constexpr int FFTR16_LDS()
 {
-    return (16 * fftr16_s1<R>() > 256 * fftr16_s2<R>() ? 16 * fftr16_s1<R>() : 256 * fftr16_s2<R>()) | 1;
+    return (16 * fftr16_s1<R>() > 256 * fftr16_s2<R, TIGHT>() ? 16 * fftr16_s1<R>() : 256 * fftr16_s2<R, TIGHT>()) | 1;
 }
 // the four twiddle-table values a thread of fft_r16x16xR<R> uses (both
 // directions: the inverse conjugates them)
@@ -344,18 +346,18 @@ __device__ __forceinline__ tw16x2 fftr16_tw(const float2 *__restrict__ tw, int t
     const int e1 = t * (4096 / N), e2 = (t >> 4) * (4096 / T);
     return tw16x2{tw[e1 & 4095], tw[(4 * e1) & 4095], tw[e2 & 4095], tw[(4 * e2) & 4095]};
 }
-template <int R, int DIR>
+template <int R, int DIR, bool TIGHT = false>
 __device__ __forceinline__ void fft_r16x16xR(float2 (&v)[16], float2 *lds, const tw16x2 &w, int t);
-template <int R, int DIR>
+template <int R, int DIR, bool TIGHT = false>
 __device__ __forceinline__ void fft_r16x16xR(float2 (&v)[16], float2 *lds, const float2 *__restrict__ tw, int t)
 {
-    fft_r16x16xR<R, DIR>(v, lds, fftr16_tw<R>(tw, t), t);
+    fft_r16x16xR<R, DIR, TIGHT>(v, lds, fftr16_tw<R>(tw, t), t);
 }
-template <int R, int DIR>
+template <int R, int DIR, bool TIGHT>
 __device__ __forceinline__ void fft_r16x16xR(float2 (&v)[16], float2 *lds, const tw16x2 &w, int t)
 {
     constexpr int T = 16 * R;
-    constexpr int S1 = fftr16_s1<R>(), S2 = fftr16_s2<R>();
+    constexpr int S1 = fftr16_s1<R>(), S2 = fftr16_s2<R, TIGHT>();
     dft16<DIR>(v);
     twiddle16v<DIR>(v, w.p1a, w.p1b);   // W_N^{t k2}
     __syncthreads();
