@@ -635,6 +635,103 @@ __global__ __launch_bounds__(256) void k_pfb2_syn_out_run(int M, const float *__
     }
 }
 
+// firpfbch analyzer, M = 256 R (R = 1, 2), fused like k_pfb2_an256: a lane
+// per column j with the column's P taps (h[(M-1-j) + nM]) and a 16-row
+// register ring, X of each 16-row group's 16 blocks in LDS, then 16 forward
+// M-point transforms in registers and one store of Y (16 B per sample
+// instead of the two-pass 48).
+template <int P, typename TC, int R>
+__global__ __launch_bounds__(256 * R, R == 1 ? 2 : 1) void k_pfb_an_fused(const TC *__restrict__ hsub,
+                                                                          const float2 *__restrict__ hist,
+                                                                          const float2 *__restrict__ x, int n_in,
+                                                                          int nb, int S, float2 *__restrict__ Y,
+                                                                          const float2 *__restrict__ tw4096)
+{
+    constexpr int M = 256 * R, HL = (P - 1) * M, NS = 16;
+    constexpr bool TIGHT = R > 1;
+    constexpr int PS = FFTR16_LDS<R, TIGHT>();
+    __shared__ __attribute__((aligned(16))) float2 xr[NS * M];
+    __shared__ __attribute__((aligned(16))) float2 scr[16 * PS];
+    const int j = threadIdx.x;
+    TC h[P];
+#pragma unroll
+    for (int n = 0; n < P; n++) h[n] = hsub[(M - 1 - j) * P + n];
+    const __amdgpu_buffer_rsrc_t rx = __builtin_amdgcn_make_buffer_rsrc((void *)x, (short)0, n_in * 8, 0x00020000);
+    const __amdgpu_buffer_rsrc_t rh =
+        __builtin_amdgcn_make_buffer_rsrc((void *)hist, (short)0, (HL > 0 ? HL : 1) * 8, 0x00020000);
+    const __amdgpu_buffer_rsrc_t ry = __builtin_amdgcn_make_buffer_rsrc((void *)Y, (short)0, nb * M * 8, 0x00020000);
+    auto row_sample = [&](int b) -> float2 {
+        const int t = b * M + j;
+        const float2 a = __builtin_bit_cast(float2, __builtin_amdgcn_raw_buffer_load_b64(rx, (unsigned)t * 8u, 0, 0));
+        if constexpr (HL == 0) return a;
+        const float2 c =
+            __builtin_bit_cast(float2, __builtin_amdgcn_raw_buffer_load_b64(rh, (unsigned)(t + HL) * 8u, 0, 0));
+        return make_float2(a.x + c.x, a.y + c.y);
+    };
+    const int g = threadIdx.x / (16 * R), t = threadIdx.x % (16 * R);
+    const tw16x2 w16 = fftr16_tw<R>(tw4096, t);
+    typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
+    const int cs = (int)blockIdx.x * S;
+    const int ce = cs + S < nb ? cs + S : nb;
+    float2 w[NS], pf[NS];
+#pragma unroll
+    for (int u = 0; u < NS; u++) w[u] = row_sample(cs - NS + u);
+#pragma unroll
+    for (int u = 0; u < NS; u++) pf[u] = row_sample(cs + u);
+    for (int r0 = cs; r0 < ce; r0 += NS) {
+#pragma unroll
+        for (int u = 0; u < NS; u++) {
+            w[u] = pf[u];
+            pf[u] = row_sample(r0 + NS + u);
+            float2 acc = make_float2(0.f, 0.f);
+#pragma unroll
+            for (int n = 0; n < P; n++) acc = pfb_mac(h[n], w[(u - n) & (NS - 1)], acc);
+            xr[u * M + j] = acc;
+        }
+        __syncthreads();
+        float2 v[16];
+#pragma unroll
+        for (int n = 0; n < 16; n++) v[n] = xr[g * M + t + 16 * R * n];
+        fft_r16x16xR<R, +1, TIGHT>(v, scr + g * PS, w16, t);
+        const int b = r0 + g;
+        const unsigned base = b < ce ? (unsigned)b * (unsigned)(M * 8) : 0xFFFFF000u;
+#pragma unroll
+        for (int sidx = 0; sidx < 16 / R; sidx++)
+#pragma unroll
+            for (int q = 0; q < R; q++)
+                __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2, v[sidx * R + q]), ry,
+                                                      base + (unsigned)(t + 16 * R * sidx + 256 * q) * 8u, 0, 0);
+    }
+}
+
+template <typename TC>
+bool launch_pfb_an_fused(int M, int p, const void *hsub, const void *hist, const void *x, long long nb, void *Y,
+                         hipStream_t st)
+{
+    if ((M != 256 && M != 512) || nb * (long long)M * 8 >= (1ll << 31)) return false;
+    long long S = (nb + 1023) / 1024;
+    S = (S + 15) / 16 * 16;
+    if (S < 32) S = 32;
+    const unsigned grid = (unsigned)((nb + S - 1) / S);
+#define LQ_PF(PP)                                                                                          \
+    case PP:                                                                                               \
+        if (M == 256)                                                                                      \
+            hipLaunchKernelGGL((k_pfb_an_fused<PP, TC, 1>), dim3(grid), dim3(256), 0, st, (const TC *)hsub, \
+                               (const float2 *)hist, (const float2 *)x, (int)(nb * M), (int)nb, (int)S,   \
+                               (float2 *)Y, (const float2 *)lqrt_twiddles());                             \
+        else                                                                                               \
+            hipLaunchKernelGGL((k_pfb_an_fused<PP, TC, 2>), dim3(grid), dim3(512), 0, st, (const TC *)hsub, \
+                               (const float2 *)hist, (const float2 *)x, (int)(nb * M), (int)nb, (int)S,   \
+                               (float2 *)Y, (const float2 *)lqrt_twiddles());                             \
+        LQ_CHECK_LAUNCH();                                                                                 \
+        return true;
+    switch (p) {
+        LQ_PF(2) LQ_PF(4) LQ_PF(6) LQ_PF(8) LQ_PF(10) LQ_PF(12) LQ_PF(14) LQ_PF(16)
+    }
+#undef LQ_PF
+    return false;
+}
+
 // dispatch helpers: compile-time ring depths for the common shapes, else the
 // per-element kernels
 template <typename TC>
@@ -997,6 +1094,10 @@ extern "C" void lqk_firpfbch_analyzer(int ctaps, unsigned int M, unsigned int p,
     if (nblocks == 0) return;
     if (lqk_firpfbch_analyzer_fast(ctaps, M, p, hsub, hist, x, nblocks, Y, stream)) return;
     hipStream_t st = (hipStream_t)stream;
+    if (!getenv("LQ_PFB_TWO_PASS") &&
+        (ctaps ? launch_pfb_an_fused<float2>((int)M, (int)p, hsub, hist, x, (long long)nblocks, Y, st)
+               : launch_pfb_an_fused<float>((int)M, (int)p, hsub, hist, x, (long long)nblocks, Y, st)))
+        return;
     const long long tot = (long long)nblocks * M;
     const dim3 grid((unsigned)((tot + 255) / 256));
     // X is formed in Y then transformed in place

@@ -438,6 +438,40 @@ def test_firpfbch_vs_oracle(typ, M, m):
     assert G.nrm_err(y, ref) < NRM
 
 
+@pytest.mark.parametrize("typ", [LQ.LIQUID_ANALYZER, LQ.LIQUID_SYNTHESIZER])
+@pytest.mark.parametrize("M,m", [(256, 2), (256, 4), (512, 3), (512, 8)])
+def test_firpfbch_m256_512_long_stream(typ, M, m):
+    # the fused M = 256 / 512 analyzer (16-row groups, runs of rows per
+    # workgroup with a 16-row warm-up) and the generic synthesizer over
+    # thousands of blocks in ragged calls
+    r = rng(M + 31 * m + typ)
+    nb = (1 << 20) // M
+    x = cx(r, nb * M)
+    g = LQ.FirPfbch(typ, M, m=m, As=60.0)
+    o = O.FirPfbch(typ, M, m=m, As=60.0)
+    cuts = [0, 1, 778, nb]
+    y = np.concatenate([g.execute_block(x[a * M:b * M]) for a, b in zip(cuts[:-1], cuts[1:])])
+    ref = o.execute_block(x) if hasattr(o, "execute_block") else \
+        np.concatenate([o.execute(x[b * M:(b + 1) * M]) for b in range(nb)])
+    assert G.nrm_err(y, ref) < NRM
+
+
+@pytest.mark.parametrize("typ", [LQ.LIQUID_ANALYZER, LQ.LIQUID_SYNTHESIZER])
+def test_firpfbch_cccf_m256_complex_taps(typ):
+    M, p = 256, 6
+    r = rng(999 + typ)
+    h = cx(r, M * p)
+    nb = 600
+    x = cx(r, nb * M)
+    g = LQ.FirPfbch(typ, M, p=p, h=h, t="cccf")
+    o_re = O.FirPfbch(typ, M, p=p, h=h.real.copy())
+    o_im = O.FirPfbch(typ, M, p=p, h=h.imag.copy())
+    y = np.concatenate([g.execute(x[:M]), g.execute_block(x[M:])])
+    ref = np.concatenate([o_re.execute(x[b * M:(b + 1) * M]).astype(np.complex128)
+                          + 1j * o_im.execute(x[b * M:(b + 1) * M]) for b in range(nb)])
+    assert G.nrm_err(y, ref) < NRM
+
+
 # ============================================================== drop-in programs
 # ------------------------------------------------------------------ firpfb / resamp
 def test_firpfb_known_answer():
