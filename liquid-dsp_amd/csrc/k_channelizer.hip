@@ -732,6 +732,105 @@ bool launch_pfb_an_fused(int M, int p, const void *hsub, const void *hist, const
     return false;
 }
 
+// firpfbch synthesizer, M = 256 R, fused: per group of 16 blocks, 16
+// inverse register transforms of X (z_b = IFFT(X_b)) into LDS, then a lane
+// per column i runs y_b[i] = sum_n h[i p + n] z_{b-n}[i] from a 16-deep
+// register ring.  A workgroup's run of blocks warms its ring up on the 16
+// blocks before it (transformed again, outputs dropped) or, for the call's
+// first run, on the object's last p-1 transforms (state); the z of the
+// call's last p-1 blocks go to znew for the next call.
+template <int P, typename TC, int R>
+__global__ __launch_bounds__(256 * R, R == 1 ? 2 : 1) void k_pfb_syn_fused(const TC *__restrict__ hsub,
+                                                                           const float2 *__restrict__ state,
+                                                                           const float2 *__restrict__ X, int nb,
+                                                                           int S, float2 *__restrict__ y,
+                                                                           float2 *__restrict__ znew,
+                                                                           const float2 *__restrict__ tw4096)
+{
+    constexpr int M = 256 * R, HB = P - 1, NS = 16;
+    constexpr bool TIGHT = R > 1;
+    constexpr int PS = FFTR16_LDS<R, TIGHT>();
+    __shared__ __attribute__((aligned(16))) float2 zr[NS * M];
+    __shared__ __attribute__((aligned(16))) float2 scr[16 * PS];
+    const int i = threadIdx.x;
+    TC h[P];
+#pragma unroll
+    for (int n = 0; n < P; n++) h[n] = hsub[i * P + n];
+    const int g = threadIdx.x / (16 * R), t = threadIdx.x % (16 * R);
+    const tw16x2 w16 = fftr16_tw<R>(tw4096, t);
+    const int cs = (int)blockIdx.x * S;
+    const int ce = cs + S < nb ? cs + S : nb;
+    float2 w[NS];
+    int r0 = cs;
+    if (cs == 0) {   // z_{-16} .. z_{-1}: the state's last p-1 transforms, zeros before
+#pragma unroll
+        for (int u = 0; u < NS; u++) {
+            const int b = u - NS;
+            w[u] = (b >= -HB) ? state[(HB + b) * M + i] : make_float2(0.f, 0.f);
+        }
+    } else {
+        r0 = cs - NS;    // warm-up group: transformed, outputs dropped
+    }
+    for (; r0 < ce; r0 += NS) {
+        {
+            const int b = r0 + g;
+            float2 v[16];
+            const float2 *xb = X + (long long)(b < nb ? b : nb - 1) * M;
+#pragma unroll
+            for (int n = 0; n < 16; n++) v[n] = xb[t + 16 * R * n];
+            fft_r16x16xR<R, -1, TIGHT>(v, scr + g * PS, w16, t);
+            float2 *zb = zr + g * M;
+#pragma unroll
+            for (int sidx = 0; sidx < 16 / R; sidx++)
+#pragma unroll
+                for (int q = 0; q < R; q++) {
+                    const int k = t + 16 * R * sidx + 256 * q;
+                    zb[k] = v[sidx * R + q];
+                    if (b >= nb - HB && b < nb && b >= cs && b < ce) znew[(b - (nb - HB)) * M + k] = v[sidx * R + q];
+                }
+        }
+        __syncthreads();
+#pragma unroll
+        for (int u = 0; u < NS; u++) {
+            w[u] = zr[u * M + i];
+            const int b = r0 + u;
+            float2 acc = make_float2(0.f, 0.f);
+#pragma unroll
+            for (int n = 0; n < P; n++) acc = pfb_mac(h[n], w[(u - n) & (NS - 1)], acc);
+            if (b >= cs && b < ce) y[(long long)b * M + i] = acc;
+        }
+        __syncthreads();   // zr is rewritten by the next group's transforms
+    }
+}
+
+template <typename TC>
+bool launch_pfb_syn_fused(int M, int p, const void *hsub, const void *state, const void *X, long long nb, void *y,
+                          void *znew, hipStream_t st)
+{
+    if ((M != 256 && M != 512) || p > 16 || nb < p || nb * (long long)M >= (1ll << 31)) return false;
+    long long S = (nb + 1023) / 1024;
+    S = (S + 15) / 16 * 16;
+    if (S < 64) S = 64;
+    const unsigned grid = (unsigned)((nb + S - 1) / S);
+#define LQ_SF(PP)                                                                                          \
+    case PP:                                                                                               \
+        if (M == 256)                                                                                      \
+            hipLaunchKernelGGL((k_pfb_syn_fused<PP, TC, 1>), dim3(grid), dim3(256), 0, st, (const TC *)hsub, \
+                               (const float2 *)state, (const float2 *)X, (int)nb, (int)S, (float2 *)y,     \
+                               (float2 *)znew, (const float2 *)lqrt_twiddles());                          \
+        else                                                                                               \
+            hipLaunchKernelGGL((k_pfb_syn_fused<PP, TC, 2>), dim3(grid), dim3(512), 0, st, (const TC *)hsub, \
+                               (const float2 *)state, (const float2 *)X, (int)nb, (int)S, (float2 *)y,     \
+                               (float2 *)znew, (const float2 *)lqrt_twiddles());                          \
+        LQ_CHECK_LAUNCH();                                                                                 \
+        return true;
+    switch (p) {
+        LQ_SF(2) LQ_SF(4) LQ_SF(6) LQ_SF(8) LQ_SF(10) LQ_SF(12) LQ_SF(14) LQ_SF(16)
+    }
+#undef LQ_SF
+    return false;
+}
+
 // dispatch helpers: compile-time ring depths for the common shapes, else the
 // per-element kernels
 template <typename TC>
@@ -1123,6 +1222,14 @@ extern "C" void lqk_firpfbch_synthesizer(int ctaps, unsigned int M, unsigned int
     hipStream_t st = (hipStream_t)stream;
     const long long HB = (long long)p - 1;
     float2 *Z = (float2 *)zscratch;
+    // fused M = 256 / 512: the last p-1 transforms land in the scratch, then
+    // become the state (every workgroup reads the old state first)
+    if (!getenv("LQ_PFB_TWO_PASS") &&
+        (ctaps ? launch_pfb_syn_fused<float2>((int)M, (int)p, hsub, state, X, (long long)nblocks, y, Z, st)
+               : launch_pfb_syn_fused<float>((int)M, (int)p, hsub, state, X, (long long)nblocks, y, Z, st))) {
+        if (HB > 0) LQ_CHECK(hipMemcpyAsync(state, Z, HB * M * sizeof(float2), hipMemcpyDeviceToDevice, st));
+        return;
+    }
     if (HB > 0) LQ_CHECK(hipMemcpyAsync(Z, state, HB * M * sizeof(float2), hipMemcpyDeviceToDevice, st));
     fft_batch_scaled(M, -1, X, Z + HB * M, (long long)nblocks, 1.f, 1.f, 0, 0, st);
     const long long tot = (long long)nblocks * M;
