@@ -831,6 +831,123 @@ bool launch_pfb_syn_fused(int M, int p, const void *hsub, const void *state, con
     return false;
 }
 
+// firpfbch2 synthesizer, M = 256 R, m <= 4, fused the same way: 16 inverse
+// transforms per group (scaled 1/M then M/2, as firpfbch2.c:303-307) into
+// LDS, then lane i < M/2 keeps 16-deep rings of columns i and i + M/2 and
+// emits y_b[i] = sum_n h[i + nM] z_{b-2n}[c] + h[i + M/2 + nM] z_{b-1-2n}[c],
+// c = i + f M/2 (f = block parity).
+template <int L, int R>
+__global__ __launch_bounds__(256 * R, R == 1 ? 2 : 1) void k_pfb2_syn_fused(const float *__restrict__ hsub,
+                                                                            const float2 *__restrict__ state,
+                                                                            const float2 *__restrict__ X, int nb,
+                                                                            int p0, int S, float2 *__restrict__ y,
+                                                                            float2 *__restrict__ znew,
+                                                                            const float2 *__restrict__ tw4096)
+{
+    constexpr int M = 256 * R, M2 = M / 2, HB = 2 * L - 1, NS = 16;
+    static_assert(2 * L <= NS, "ring too small");
+    constexpr bool TIGHT = R > 1;
+    constexpr int PS = FFTR16_LDS<R, TIGHT>();
+    __shared__ __attribute__((aligned(16))) float2 zr[NS * M];
+    __shared__ __attribute__((aligned(16))) float2 scr[16 * PS];
+    const int i = threadIdx.x;   // output column (lanes < M/2)
+    const bool outl = i < M2;
+    float h0[L], h1[L];
+#pragma unroll
+    for (int n = 0; n < L; n++) {
+        h0[n] = outl ? hsub[i * L + n] : 0.f;
+        h1[n] = outl ? hsub[(i + M2) * L + n] : 0.f;
+    }
+    const int g = threadIdx.x / (16 * R), t = threadIdx.x % (16 * R);
+    const tw16x2 w16 = fftr16_tw<R>(tw4096, t);
+    const float s1 = 1.0f / (float)M, s2 = (float)M2;
+    const int cs = (int)blockIdx.x * S;
+    const int ce = cs + S < nb ? cs + S : nb;
+    float2 wa[NS], wb[NS];
+    int r0 = cs;
+    if (cs == 0) {
+#pragma unroll
+        for (int u = 0; u < NS; u++) {
+            const int b = u - NS;
+            const bool in = b >= -HB && outl;
+            wa[u] = in ? state[(HB + b) * M + i] : make_float2(0.f, 0.f);
+            wb[u] = in ? state[(HB + b) * M + i + M2] : make_float2(0.f, 0.f);
+        }
+    } else {
+        r0 = cs - NS;
+    }
+    for (; r0 < ce; r0 += NS) {
+        {
+            const int b = r0 + g;
+            float2 v[16];
+            const float2 *xb = X + (long long)(b < nb ? b : nb - 1) * M;
+#pragma unroll
+            for (int n = 0; n < 16; n++) v[n] = xb[t + 16 * R * n];
+            fft_r16x16xR<R, -1, TIGHT>(v, scr + g * PS, w16, t);
+            float2 *zb = zr + g * M;
+#pragma unroll
+            for (int sidx = 0; sidx < 16 / R; sidx++)
+#pragma unroll
+                for (int q = 0; q < R; q++) {
+                    const int k = t + 16 * R * sidx + 256 * q;
+                    const float2 z = cscale(cscale(v[sidx * R + q], s1), s2);
+                    zb[k] = z;
+                    if (b >= nb - HB && b < nb && b >= cs && b < ce) znew[(b - (nb - HB)) * M + k] = z;
+                }
+        }
+        __syncthreads();
+        if (outl) {
+#pragma unroll
+            for (int u = 0; u < NS; u++) {
+                wa[u] = zr[u * M + i];
+                wb[u] = zr[u * M + i + M2];
+                const int b = r0 + u;
+                const bool f = ((p0 + b) & 1) != 0;
+                float2 acc0 = make_float2(0.f, 0.f), acc1 = make_float2(0.f, 0.f);
+#pragma unroll
+                for (int n = 0; n < L; n++) {
+                    const int k0 = (u - 2 * n) & (NS - 1), k1 = (u - 2 * n - 1) & (NS - 1);
+                    const float2 z0 = f ? wb[k0] : wa[k0];
+                    const float2 z1 = f ? wb[k1] : wa[k1];
+                    acc0.x = fmaf(h0[n], z0.x, acc0.x);
+                    acc0.y = fmaf(h0[n], z0.y, acc0.y);
+                    acc1.x = fmaf(h1[n], z1.x, acc1.x);
+                    acc1.y = fmaf(h1[n], z1.y, acc1.y);
+                }
+                if (b >= cs && b < ce) y[(long long)b * M2 + i] = cadd(acc0, acc1);
+            }
+        }
+        __syncthreads();
+    }
+}
+
+bool launch_pfb2_syn_fused(int M, int m, const void *hsub, const void *state, const void *X, long long nb, int p0,
+                           void *y, void *znew, hipStream_t st)
+{
+    if ((M != 256 && M != 512) || m < 1 || m > 4 || nb < 16 || nb * (long long)M >= (1ll << 31)) return false;
+    long long S = (nb + 1023) / 1024;
+    S = (S + 15) / 16 * 16;
+    if (S < 64) S = 64;
+    const unsigned grid = (unsigned)((nb + S - 1) / S);
+#define LQ_S2(LL)                                                                                          \
+    case LL / 2:                                                                                           \
+        if (M == 256)                                                                                      \
+            hipLaunchKernelGGL((k_pfb2_syn_fused<LL, 1>), dim3(grid), dim3(256), 0, st, (const float *)hsub, \
+                               (const float2 *)state, (const float2 *)X, (int)nb, p0, (int)S, (float2 *)y, \
+                               (float2 *)znew, (const float2 *)lqrt_twiddles());                          \
+        else                                                                                               \
+            hipLaunchKernelGGL((k_pfb2_syn_fused<LL, 2>), dim3(grid), dim3(512), 0, st, (const float *)hsub, \
+                               (const float2 *)state, (const float2 *)X, (int)nb, p0, (int)S, (float2 *)y, \
+                               (float2 *)znew, (const float2 *)lqrt_twiddles());                          \
+        LQ_CHECK_LAUNCH();                                                                                 \
+        return true;
+    switch (m) {
+        LQ_S2(2) LQ_S2(4) LQ_S2(6) LQ_S2(8)
+    }
+#undef LQ_S2
+    return false;
+}
+
 // dispatch helpers: compile-time ring depths for the common shapes, else the
 // per-element kernels
 template <typename TC>
@@ -1164,6 +1281,11 @@ extern "C" void lqk_firpfbch2_synthesizer(unsigned int M, unsigned int m, const 
     hipStream_t st = (hipStream_t)stream;
     const long long HB = 4 * (long long)m - 1;
     float2 *Z = (float2 *)zscratch;
+    if (!getenv("LQ_PFB2_TWO_PASS") &&
+        launch_pfb2_syn_fused((int)M, (int)m, hsub, state, X, (long long)nblocks, p0, Y, Z, st)) {
+        LQ_CHECK(hipMemcpyAsync(state, Z, HB * M * sizeof(float2), hipMemcpyDeviceToDevice, st));
+        return;
+    }
     LQ_CHECK(hipMemcpyAsync(Z, state, HB * M * sizeof(float2), hipMemcpyDeviceToDevice, st));
     fft_batch_scaled(M, -1, X, Z + HB * M, (long long)nblocks, 1.0f / (float)M, (float)(M / 2), 1, 1, st);
     const long long tot = (long long)nblocks * (M / 2);

@@ -410,6 +410,21 @@ def test_firpfbch2_synthesizer_vs_oracle(M, m):
     assert G.nrm_err(y, o.execute_block(X)) < NRM
 
 
+@pytest.mark.parametrize("M,m", [(256, 4), (256, 1), (512, 3), (512, 2)])
+def test_firpfbch2_synthesizer_m256_512_fused(M, m):
+    # fused M = 256 / 512 synthesizer: many 64-block runs per call (each
+    # warming up on the 16 blocks before it), an odd first call so later
+    # calls start on the other block parity, state carried across calls
+    r = rng(M + 5 * m)
+    nb = 2000 if M == 256 else 1000
+    X = cx(r, nb * M)
+    g = LQ.FirPfbch2(LQ.LIQUID_SYNTHESIZER, M, m, 60.0)
+    o = O.FirPfbch2(O.SYNTHESIZER, M, m, 60.0)
+    cuts = [0, 17, 300, nb]
+    y = np.concatenate([g.execute_block(X[a * M:b * M]) for a, b in zip(cuts[:-1], cuts[1:])])
+    assert G.nrm_err(y, o.execute_block(X)) < NRM
+
+
 @pytest.mark.parametrize("m", [4, 2])
 def test_firpfbch2_synthesizer_m1024_many_workgroups(m):
     # k_pfb2_syn1024: 701 blocks over ~22 workgroups (history rebuilt from the
