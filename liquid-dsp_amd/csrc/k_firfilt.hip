@@ -475,20 +475,19 @@ __global__ __launch_bounds__(NT_) void k_firdecim_ph(const typename kt<KIND>::T 
         if (o + rr < nout) y[o + rr] = acc[rr];
 }
 
-// Phase-layout decimator, second form: four consecutive outputs per lane
-// and taps in chunks of four (QC a multiple of 4 instead of 4/8/16/32: the
-// BASELINE-style M = 8, m = 8 filter has 17 taps per phase, padded to 20
-// rather than 32).  Each phase row is stored de-interleaved by four
-// (column j at (j & 3) Q4 + j / 4), so the window reads of a wave -- lanes
-// four outputs apart -- are consecutive (conflict-free) and a lane's seven
-// window samples per tap chunk serve 16 multiply-adds.  The staging divides
-// by M with a float reciprocal and an exact integer correction.
+// Phase-layout decimator, second form: R consecutive outputs per lane (R =
+// 2 as launched) and taps in chunks of four (QC a multiple of 4 instead of
+// 4/8/16/32: the M = 8, m = 8 filter has 17 taps per phase, padded to 20
+// rather than 32).  Each phase row is stored de-interleaved by R (column j
+// at (j mod R) Q + j / R), so the window reads of a wave -- lanes R outputs
+// apart -- are consecutive (conflict-free) and a lane's R + 3 window samples
+// per tap chunk serve 4 R multiply-adds.  The staging issues four 16-byte
+// loads per lane before any LDS store and divides by M with a float
+// reciprocal and an exact integer correction.
 template <int R>
 __host__ __device__ __forceinline__ int dph2_q(int J) { return (J + R - 1) / R + 1; }   // 1/R-row stride (+1 pad)
 
-#ifndef DNU
-#define DNU 4
-#endif
+constexpr int DNU = 4;   // staging loads in flight per lane (8 and 12 measured the same)
 template <int KIND, int R, int NT_>
 __global__ __launch_bounds__(NT_) void k_firdecim_ph2(const typename kt<KIND>::T *__restrict__ hist, int hl1,
                                                       const typename kt<KIND>::T *__restrict__ x, long long nout,
@@ -523,7 +522,7 @@ __global__ __launch_bounds__(NT_) void k_firdecim_ph2(const typename kt<KIND>::T
         }
     };
     if (vec_ok && nin * (long long)sizeof(T) < (1ll << 31)) {
-        // DNU 16-byte loads per lane in flight at a time through a
+        // four 16-byte loads per lane in flight at a time through a
         // range-checked descriptor (zeros outside x; sa is a multiple of VW,
         // so a vector never straddles x's start); the history only reaches
         // the first tile
@@ -912,12 +911,10 @@ extern "C" int lqk_firdecim_ph(int kind, unsigned int M, unsigned int QC, const 
     if (nout == 0) return 0;
     hipStream_t st = (hipStream_t)stream;
     {
-        // four outputs per lane, 128 lanes: 512 outputs and (512 + QC - 1) M
-        // input samples per workgroup in LDS
-#ifndef LQ_D2R
-#define LQ_D2R 2
-#define LQ_D2NT 256
-#endif
+        // 512 outputs and (512 + QC - 1) M input samples per workgroup in LDS:
+        // two outputs per lane, 256 lanes (four per lane on 128 lanes halves
+        // the occupancy: 0.51 vs 0.34 ms for M = 8 m = 8)
+        constexpr int LQ_D2R = 2, LQ_D2NT = 256;
         constexpr int TO2 = LQ_D2R * LQ_D2NT;
         const int J = TO2 + (int)QC - 1;
         const size_t lds = (size_t)M * (LQ_D2R * dph2_q<LQ_D2R>(J) + 1) * elem_size(kind);
