@@ -1093,6 +1093,58 @@ __global__ __launch_bounds__(256, 2) void k_fftr16_batch(const float2 *__restric
     }
 }
 
+// batched 32 / 64 / 128-point transforms (fft_small16xR): R lanes per
+// transform, 256 / R transforms per workgroup, persistent over the batch
+template <int R, int DIR>
+__global__ __launch_bounds__(256) void k_fftsmall_batch(const float2 *__restrict__ x, float2 *__restrict__ y,
+                                                         long long batch, float s1, float s2, int use_s1,
+                                                         int use_s2, const float2 *__restrict__ tw4096)
+{
+    constexpr int N = 16 * R, G = 256 / R, P = FFTS_LDS<R>();
+    __shared__ __attribute__((aligned(16))) float2 lds[G * P];
+    const int g = threadIdx.x / R, t = threadIdx.x % R;
+    const int e = t * (4096 / N);
+    const float2 a1 = tw4096[e & 4095], a4 = tw4096[(4 * e) & 4095];
+    for (long long b0 = (long long)blockIdx.x * G; b0 < batch; b0 += (long long)gridDim.x * G) {
+        const long long b = b0 + g;
+        const bool in = b < batch;
+        float2 v[16];
+        const float2 *xb = x + (in ? b : 0) * N;
+#pragma unroll
+        for (int n = 0; n < 16; n++) v[n] = in ? xb[t + R * n] : make_float2(0.f, 0.f);
+        fft_small16xR<R, DIR>(v, lds + g * P, a1, a4, t);
+        if (in) {
+            float2 *yb = y + b * N;
+#pragma unroll
+            for (int u = 0; u < 16 / R; u++)
+#pragma unroll
+                for (int q = 0; q < R; q++) {
+                    float2 w = v[u * R + q];
+                    if (use_s1) w = cscale(w, s1);
+                    if (use_s2) w = cscale(w, s2);
+                    yb[t * (16 / R) + u + 16 * q] = w;
+                }
+        }
+        __syncthreads();   // lds is reused by the next batch of transforms
+    }
+}
+
+template <int R>
+void launch_fftsmall(const void *x, void *y, long long batch, int dir, float s1, float s2, int u1, int u2,
+                     hipStream_t st)
+{
+    constexpr int G = 256 / R;
+    const long long gb = (batch + G - 1) / G;
+    const unsigned grid = (unsigned)(gb < 4096 ? gb : 4096);
+    if (dir > 0)
+        hipLaunchKernelGGL((k_fftsmall_batch<R, +1>), dim3(grid), dim3(256), 0, st, (const float2 *)x, (float2 *)y,
+                           batch, s1, s2, u1, u2, (const float2 *)lqrt_twiddles());
+    else
+        hipLaunchKernelGGL((k_fftsmall_batch<R, -1>), dim3(grid), dim3(256), 0, st, (const float2 *)x, (float2 *)y,
+                           batch, s1, s2, u1, u2, (const float2 *)lqrt_twiddles());
+    LQ_CHECK_LAUNCH();
+}
+
 template <int R>
 void launch_fftr16(const void *x, void *y, long long batch, int dir, float s1, float s2, int u1, int u2,
                    hipStream_t st)
@@ -1131,9 +1183,9 @@ void fft_batch_scaled(unsigned n, int dir, const void *x, void *y, long long bat
     case 4: launch_fft_batch<4>(x, y, batch, dir, s1, s2, u1, u2, st); return;
     case 8: launch_fft_batch<8>(x, y, batch, dir, s1, s2, u1, u2, st); return;
     case 16: launch_fft_batch<16>(x, y, batch, dir, s1, s2, u1, u2, st); return;
-    case 32: launch_fft_batch<32>(x, y, batch, dir, s1, s2, u1, u2, st); return;
-    case 64: launch_fft_batch<64>(x, y, batch, dir, s1, s2, u1, u2, st); return;
-    case 128: launch_fft_batch<128>(x, y, batch, dir, s1, s2, u1, u2, st); return;
+    case 32: launch_fftsmall<2>(x, y, batch, dir, s1, s2, u1, u2, st); return;
+    case 64: launch_fftsmall<4>(x, y, batch, dir, s1, s2, u1, u2, st); return;
+    case 128: launch_fftsmall<8>(x, y, batch, dir, s1, s2, u1, u2, st); return;
     case 256: launch_fftr16<1>(x, y, batch, dir, s1, s2, u1, u2, st); return;
     case 512: launch_fftr16<2>(x, y, batch, dir, s1, s2, u1, u2, st); return;
     case 1024: {

@@ -382,6 +382,32 @@ __device__ __forceinline__ void fft_r16x16xR(float2 (&v)[16], float2 *lds, const
     for (int s = 0; s < 16 / R; s++) dft_small<R, DIR>(v + s * R);
 }
 
+// N = 16 R point FFT (R = 2, 4, 8: N = 32, 64, 128) by T = R threads: a
+// register DFT16 over n (x[t + R n]), the twiddle W_N^{t k2}, one padded LDS
+// transpose, then 16 / R DFT_R's per thread.  Out: v[u R + q] = X[t (16/R) + u
+// + 16 q].  lds: 16 (R + 1) float2 for this transform; every thread of the
+// workgroup calls it (it synchronises).
+template <int R>
+constexpr int FFTS_LDS() { return 16 * (R + 1); }
+template <int R, int DIR>
+__device__ __forceinline__ void fft_small16xR(float2 (&v)[16], float2 *lds, float2 a1, float2 a4, int t)
+{
+    constexpr int S = R + 1;
+    dft16<DIR>(v);
+    twiddle16v<DIR>(v, a1, a4);   // W_N^{t k2}
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < 16; k++) lds[k * S + t] = v[k];
+    __syncthreads();
+    constexpr int U = 16 / R;
+#pragma unroll
+    for (int u = 0; u < U; u++)
+#pragma unroll
+        for (int e = 0; e < R; e++) v[u * R + e] = lds[(t * U + u) * S + e];
+#pragma unroll
+    for (int u = 0; u < U; u++) dft_small<R, DIR>(v + u * R);
+}
+
 __device__ __forceinline__ tw16x2 fft4096_tw(const float2 *__restrict__ tw, int t)
 {
     const int e2 = 16 * (t & 15);

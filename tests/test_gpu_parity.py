@@ -948,7 +948,8 @@ def test_fft_r2r_golden(case):
     assert np.max(np.abs(y - np.asarray(case["y"]))) < case["tol"]
 
 
-@pytest.mark.parametrize("n", [256, 512, 2048, 4096, 8192, 1 << 15, 65536, 1 << 17, 1 << 20, 1000, 4099, 12345, 100003, 17,
+@pytest.mark.parametrize("n", [32, 64, 128, 256, 512, 2048, 4096, 8192, 1 << 15, 65536, 1 << 17, 1 << 20, 1000, 4099, 12345,
+                               100003, 17,
                                3 * 4096])
 @pytest.mark.parametrize("direction", [+1, -1])
 def test_fft_sizes_vs_float64(n, direction):
