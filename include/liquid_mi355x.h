@@ -50,6 +50,10 @@ int liquid_libversion_number(void);
 #endif
 LIQUID_DEFINE_COMPLEX(float, liquid_float_complex);
 
+/* liquid.h:6662 (src/utility/src/msb_index.c:110-135): index of the most
+   significant set bit, 1-based (floor(log2 x)+1), 0 for x = 0 */
+unsigned int liquid_msb_index(unsigned int _x);
+
 /* liquid.h:5651-5652 */
 #define LIQUID_ANALYZER 0
 #define LIQUID_SYNTHESIZER 1

@@ -749,6 +749,17 @@ size_t elem_size(int kind) { return kind == 0 ? sizeof(float) : sizeof(float2); 
 
 } // namespace
 
+extern "C" unsigned int lqk_firfilt_max_history(int kind)
+{
+    // lds_bytes(TILE + HP) <= 160 KB; HP a multiple of 64
+    unsigned int hp = 0;
+    for (;;) {
+        const size_t b = kind == 0 ? (size_t)lds_bytes<float>(TILE + hp + 64) : (size_t)lds_bytes<float2>(TILE + hp + 64);
+        if (b > 160 * 1024) return hp;
+        hp += 64;
+    }
+}
+
 extern "C" size_t lqk_firfilt_scratch_bytes(const lqk_fir_desc *d, unsigned long long n)
 {
     const int tl = tile_of(d->kind);

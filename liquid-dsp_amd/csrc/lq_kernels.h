@@ -73,6 +73,8 @@ int lqk_firfilt_mx(const lqk_fir_desc *d, const void *hist, const void *x, unsig
                    void *stream);
 /* bytes of scratch lqk_firfilt needs for an in-place call of n samples */
 size_t lqk_firfilt_scratch_bytes(const lqk_fir_desc *d, unsigned long long n);
+/* longest history (padded tap count) the direct FIR kernel can hold in LDS */
+unsigned int lqk_firfilt_max_history(int kind);
 
 /* window maintenance: dst[0..L) = last L samples of (src_hist[0..L) ++ x[0..n)) */
 void lqk_window_append(int is_complex, const void *src_hist, unsigned int L, const void *x,

@@ -62,7 +62,12 @@ extern "C" void *lqrt_host_alloc(size_t bytes)
     lqrt_require_device("lqrt_host_alloc");
     void *p = nullptr;
     if (bytes == 0) bytes = 16;
-    LQ_CHECK(hipHostMalloc(&p, bytes, hipHostMallocDefault));
+    // fine-grained (coherent) memory: the small-call path reads and writes
+    // these buffers while kernels run (the host spins on a flag the kernel
+    // raises; kernels read inputs in place right after the host wrote them),
+    // which HIP guarantees to be visible without a synchronisation only for
+    // coherent allocations
+    LQ_CHECK(hipHostMalloc(&p, bytes, hipHostMallocCoherent | hipHostMallocMapped));
     return p;
 }
 
@@ -132,6 +137,10 @@ extern "C" const float *lqrt_twiddles(void)
     static float *tables[64] = {nullptr};
     int dev = 0;
     LQ_CHECK(hipGetDevice(&dev));
+    if (dev < 0 || dev >= 64) {
+        fprintf(stderr, "error: liquid-mi355x: device index %d out of range (64 devices max)\n", dev);
+        exit(1);
+    }
     std::lock_guard<std::mutex> g(mu);
     if (!tables[dev]) {
         float h[2 * LQ_TW_N];

@@ -49,6 +49,13 @@ static void lq_firfilt_layout(lq_firfilt *q, unsigned int n)
     }
     q->HP = q->d.hc * q->d.nchunk;
     q->d.hlen = n;
+    /* the direct kernel holds a tile plus the HP-sample history in LDS:
+       refuse at create time what no launch could run (fftfilt's long-filter
+       path lands here too) */
+    if (q->HP > lqk_firfilt_max_history(q->d.kind))
+        LQ_FAIL("error: firfilt_%s_create(), filter length %u exceeds the GPU kernel limit of %u taps\n",
+                q->d.kind == 0 ? "rrrf" : (q->d.kind == 1 ? "crcf" : "cccf"), n,
+                lqk_firfilt_max_history(q->d.kind));
 }
 
 static void lq_firfilt_alloc_state(lq_firfilt *q)

@@ -158,6 +158,9 @@ unsigned int lq_msb_index(unsigned int x)
     return b;
 }
 
+/* liquid.h:6662, msb_index.c:110-135 (the x86 build's bsr: 0 for x = 0) */
+unsigned int liquid_msb_index(unsigned int _x) { return _x ? 32u - (unsigned int)__builtin_clz(_x) : 0u; }
+
 int lq_is_pow2(unsigned int x) { return x && !(x & (x - 1)); }
 
 /* ----------------------------------------------------------------- design */

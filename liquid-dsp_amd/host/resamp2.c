@@ -151,11 +151,31 @@ static void lq_r2_run(lq_r2 *q, int mode, const void *x, unsigned long long n, v
     const size_t bx = (size_t)n * lq_r2_nin(mode) * q->esz;
     const size_t by = (size_t)n * (mode == LQK_R2_FILTER ? 1 : lq_r2_nout(mode)) * q->esz;
     const void *dx = lq_call_in(&q->ctx, &q->xbuf, x, bx);
-    void *dy = lq_devbuf_get(&q->ybuf, by);
-    void *dy1 = mode == LQK_R2_FILTER ? lq_devbuf_get(&q->y1buf, by) : NULL;
-    lq_r2_run_dev(q, mode, dx, n, dy, dy1, 1.0f);
-    if (dy1) lqrt_d2h(y1, dy1, by, q->ctx.stream);   /* ordered before the copy-out's flag */
-    lq_call_out(&q->ctx, y0, dy, by);
+    if (mode != LQK_R2_FILTER) {
+        void *dy = lq_devbuf_get(&q->ybuf, by);
+        lq_r2_run_dev(q, mode, dx, n, dy, NULL, 1.0f);
+        lq_call_out(&q->ctx, y0, dy, by);
+        return;
+    }
+    /* filter mode: y0 and y1 side by side in one device buffer (y1 at a
+       16-byte aligned offset) so both come back through the same pinned
+       copy-out and completion flag; past the copy-out size, two copies and
+       a stream synchronisation */
+    const size_t off = (by + 15) & ~(size_t)15;
+    unsigned char *dy = (unsigned char *)lq_devbuf_get(&q->ybuf, off + by);
+    lq_r2_run_dev(q, mode, dx, n, dy, dy + off, 1.0f);
+    if (off + by <= LQRT_COPYOUT_MAX) {
+        unsigned char small[256];
+        unsigned char *tmp = off + by <= sizeof(small) ? small : (unsigned char *)lq_xmalloc(off + by);
+        lq_call_out(&q->ctx, tmp, dy, off + by);
+        memcpy(y0, tmp, by);
+        memcpy(y1, tmp + off, by);
+        if (tmp != small) free(tmp);
+    } else {
+        lqrt_d2h(y0, dy, by, q->ctx.stream);
+        lqrt_d2h(y1, dy + off, by, q->ctx.stream);
+        lq_call_done(&q->ctx);
+    }
 }
 
 #define LQ_RESAMP2_FRONT(NAME, KIND, T)                                                             \

@@ -62,5 +62,13 @@ def firpfbch2_plan(nblocks, world, M, m):
     return [Shard(r, a, c, min(halo, a)) for r, (a, c) in enumerate(_split(nblocks, world, align=2))]
 
 
-def fftfilt_plan(n, world, h_len):
-    return firfilt_plan(n, world, h_len)
+def fftfilt_plan(n, world, h_len, block=1):
+    """Shards of an fftfilt stream.  The output is the linear convolution
+    (fftfilt.c:193-260 carries the last n inputs' tail), so the warm-up is
+    h_len-1 samples; with `block` > 1 shard starts and the warm-up are whole
+    multiples of the reference's block size n, for callers that must feed
+    exactly n samples per execute() (the reference's own API)."""
+    if block <= 1:
+        return firfilt_plan(n, world, h_len)
+    halo = -(-max(0, h_len - 1) // block) * block
+    return [Shard(r, a, c, min(halo, a)) for r, (a, c) in enumerate(_split(n, world, align=block))]

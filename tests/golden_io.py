@@ -107,3 +107,32 @@ def msresamp_spectral_case():
         if side >= -As: bad.append("sidelobe %g dB" % side)
         return bad
     return r, As, x, check
+
+
+def firpfbch2_downconverter(x, h, M, m, nblocks, firfilt):
+    """The firpfbch2 analyzer restated as a bank of M "traditional" down-
+    converters -- the reference's own methodology for pinning a channelizer
+    to a filter it already pins: firpfbch_crcf_analyzer_autotest.c:30-146
+    (mixer + firfilt, tol 1e-4) and, for firpfbch2 itself,
+    sandbox/firpfbch2_analysis_equivalence_test.c:182-215 (mix channel k
+    down by e^{-j2pi kt/M}, filter with the prototype, sample after every M/2
+    inputs).  Any taps work ("these coefficients can be random", :39-41).
+
+    With h the 2Mm prototype taps (firpfbch2.c:99-109 uses exactly those)
+    and t_b = (b+1)M/2 - 1 the last input of block b, the closed form
+     gives
+        Y_b[k] = (1/M) e^{+j2pi k (offset_b + t_b)/M} y_k[t_b],
+        y_k = firfilt(h, x[t] e^{-j2pi kt/M}),  offset_b = (b mod 2) M/2,
+    the phase term being the commutator's rotation of the bins.
+    `firfilt(h, z)` is the pinned FIR filter to use (complex64 in and out).
+    """
+    L = 2 * M * m
+    t = (np.arange(nblocks) + 1) * (M // 2) - 1
+    off = (np.arange(nblocks) % 2) * (M // 2)
+    n = np.arange(len(x))
+    Y = np.zeros((nblocks, M), np.complex128)
+    for k in range(M):
+        z = (x.astype(np.complex128) * np.exp(-2j * np.pi * ((k * n) % M) / M)).astype(np.complex64)
+        y = np.asarray(firfilt(np.asarray(h[:L], np.float32), z))
+        Y[:, k] = np.exp(2j * np.pi * ((k * (off + t)) % M) / M) * y[t] / M
+    return Y

@@ -46,6 +46,11 @@ def _worker(job):
         q = O.FirFilt(O.CRCF, np.asarray(h, np.float32))
         ref = q.execute_block(np.asarray(x[sh["first"]:sh["start"] + sh["count"]]))[sh["warm"]:]
         got = np.asarray(y[sh["start"]:sh["start"] + sh["count"]])
+    elif kind == "fftfilt":
+        h, n = args
+        q = O.FftFilt(O.CRCF, np.asarray(h, np.float32), n)
+        ref = q.execute_stream(np.asarray(x[sh["first"]:sh["start"] + sh["count"]]))[sh["warm"]:]
+        got = np.asarray(y[sh["start"]:sh["start"] + sh["count"]])
     else:
         raise ValueError(kind)
     fin = np.isfinite(ref) & np.isfinite(got)

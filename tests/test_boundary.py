@@ -52,7 +52,8 @@ def test_liquid_h_hot_path_symbols_present():
                   "analyzer_execute")]
     expected += ["firpfbch2_crcf_%s" % s for s in
                  ("create", "create_kaiser", "destroy", "reset", "print", "execute")]
-    expected += ["liquid_firdes_kaiser", "kaiser_beta_As", "liquid_libversion", "liquid_libversion_number"]
+    expected += ["liquid_firdes_kaiser", "kaiser_beta_As", "liquid_libversion", "liquid_libversion_number",
+                 "liquid_msb_index"]
     L = C.CDLL(LQ.LIB_PATH)
     missing = [n for n in expected if not hasattr(L, n)]
     assert not missing, missing
@@ -85,3 +86,16 @@ def test_reference_examples_compile_unchanged():
     subprocess.check_call(["bash", os.path.join(ROOT, "tools", "build_ref_examples.sh")])
     built = os.listdir(os.path.join(ROOT, "build", "ref_examples"))
     assert len(built) == 25
+
+
+def test_liquid_msb_index_known_answers():
+    """src/utility/tests/count_bits_autotest.c:140-177: msb_index(0) = 0,
+    msb_index(2^k) = k + 1; plus the table in msb_index.c:90-108 (255 -> 8).
+    Host-side integer helper (no GPU call)."""
+    f = C.CDLL(LQ.LIB_PATH).liquid_msb_index
+    f.restype, f.argtypes = C.c_uint, [C.c_uint]
+    assert f(0) == 0
+    for k in range(32):
+        assert f(1 << k) == k + 1
+    for x, b in ((3, 2), (126, 7), (127, 7), (128, 8), (129, 8), (253, 8), (255, 8), (0xFFFFFFFF, 32)):
+        assert f(x) == b

@@ -121,3 +121,33 @@ def test_fftfilt_long_filters(t, h_len, n):
     got = np.concatenate([g.execute(x[i * n:(i + 1) * n]) for i in range(nb)])
     ref = np.concatenate([o.execute(x[i * n:(i + 1) * n]) for i in range(nb)])
     assert np.max(np.abs(got - ref)) <= 1e-5 * np.max(np.abs(ref))
+
+
+def test_fftfilt_longest_filter_and_limit():
+    """fftfilt hands filters past its 4096-point transforms to the direct FIR
+    kernel, which holds a tile plus the history in LDS: the longest filter it
+    can take runs (vs the oracle), one tap more is refused at create time
+    with a message and exit(1) -- the reference's error convention
+    (fftfilt.c:74-83) -- instead of failing at the first execute."""
+    import ctypes as C
+    import subprocess
+    import sys
+    f = LQ.lib().lqk_firfilt_max_history
+    f.restype, f.argtypes = C.c_uint, [C.c_int]
+    L = int(f(1))
+    assert L >= 8192
+    r = np.random.default_rng(L)
+    h = r.uniform(-0.5, 0.5, L).astype(np.float32)
+    n = L
+    x = (r.uniform(-0.5, 0.5, 2 * n) + 1j * r.uniform(-0.5, 0.5, 2 * n)).astype(np.complex64)
+    g, o = LQ.FftFilt(h, n), O.FftFilt(O.CRCF, h, n)
+    got = np.concatenate([g.execute(x[:n]), g.execute(x[n:])])
+    ref = np.concatenate([o.execute(x[:n]), o.execute(x[n:])])
+    assert np.max(np.abs(got - ref)) <= 1e-5 * np.max(np.abs(ref))
+    code = ("import sys, numpy as np; sys.path.insert(0, %r); import liquidmi as LQ; "
+            "LQ.FftFilt(np.ones(%d, np.float32), %d); print('created')") % (
+                LQ.os.path.dirname(LQ.__file__), L + 65, L + 65)
+    p = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=120)
+    assert p.returncode == 1, (p.returncode, p.stdout, p.stderr)
+    assert "exceeds the GPU kernel limit" in p.stderr
+    assert "created" not in p.stdout

@@ -370,6 +370,19 @@ def test_firpfbch2_analyzer_polyphase_chunks_vs_oracle():
     assert G.nrm_err(y, o.execute_block(x)) < NRM
 
 
+@pytest.mark.parametrize("M,m", [(64, 4), (256, 4)])
+def test_firpfbch2_analyzer_vs_downconverter_bank(M, m):
+    """the GPU analyzer against the reference's down-converter equivalence
+    built on the golden-pinned firfilt oracle (golden_io.firpfbch2_downconverter)"""
+    r = rng(M * 3 + m)
+    nblocks = 40
+    x = cx(r, nblocks * M // 2)
+    y = LQ.FirPfbch2(LQ.LIQUID_ANALYZER, M, m, 60.0).execute_block(x).reshape(nblocks, M)
+    h = O.firpfbch2_prototype(O.ANALYZER, M, m, 60.0)
+    ref = G.firpfbch2_downconverter(x, h, M, m, nblocks, lambda hh, z: O.FirFilt(O.CRCF, hh).execute_block(z))
+    assert G.nrm_err(y, ref) < NRM
+
+
 def test_firpfbch2_baseline_config4_slice_vs_oracle():
     # BASELINE config 4 geometry: M=1024, m=4, As=60, 2^20 samples (2048 blocks)
     r = rng(31)

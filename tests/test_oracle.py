@@ -177,6 +177,27 @@ def test_firpfbch2_analyzer_closed_form(M, m):
     assert G.nrm_err(y, ref) < 2e-6
 
 
+@pytest.mark.parametrize("M,m", [(8, 2), (16, 5), (64, 4)])
+@pytest.mark.parametrize("kaiser", [False, True])
+def test_firpfbch2_analyzer_equals_downconverter_bank(M, m, kaiser):
+    """pins the analyzer ALONE to the golden-pinned firfilt oracle
+    (test_firfilt_golden) through the reference's down-converter equivalence
+    (G.firpfbch2_downconverter): random taps and the Kaiser prototype, both
+    block parities, from a zero state"""
+    rng = _rng(M + m)
+    nblocks = 64
+    x = _cx(rng, nblocks * M // 2)
+    if kaiser:
+        q = O.FirPfbch2(O.ANALYZER, M, m, 60.0)
+        h = O.firpfbch2_prototype(O.ANALYZER, M, m, 60.0)
+    else:
+        h = rng.uniform(-0.5, 0.5, 2 * M * m).astype(np.float32)
+        q = O.FirPfbch2(O.ANALYZER, M, m, h=h)
+    y = q.execute_block(x).reshape(nblocks, M)
+    ref = G.firpfbch2_downconverter(x, h, M, m, nblocks, lambda hh, z: O.FirFilt(O.CRCF, hh).execute_block(z))
+    assert G.nrm_err(y, ref) < 1e-5
+
+
 @pytest.mark.parametrize("M", [8, 16, 32, 64])
 def test_firpfbch2_perfect_reconstruction(M):
     # src/multichannel/tests/firpfbch2_crcf_autotest.c:28-98 (m=5, As=60, tol 1e-3)
