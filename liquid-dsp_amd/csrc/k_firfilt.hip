@@ -712,6 +712,11 @@ __global__ __launch_bounds__(NT) void k_firinterp_t(const typename kt<KIND>::T *
 
 int tile_of(int) { return TILE; }
 
+// dynamic LDS budget of k_firfilt: the 160 KB of a CU minus a margin for the
+// kernel's own (static) group segment, which the dispatch adds on top (a
+// 163 600-byte request dispatched as 163 856 bytes and faulted)
+constexpr size_t FIR_LDS_MAX = 160 * 1024 - 1024;
+
 template <int KIND, int HC>
 void launch_firfilt(const lqk_fir_desc *d, const void *hist, const void *x, long long n, void *y,
                     const void *halo, hipStream_t st)
@@ -721,7 +726,12 @@ void launch_firfilt(const lqk_fir_desc *d, const void *hist, const void *x, long
     const int HP = HC * (int)d->nchunk;
     const long long ntiles = (n + TILE - 1) / TILE;
     const size_t lds = (size_t)lds_bytes<T>(TILE + HP);
-    if (lds > 160 * 1024) {
+    static const size_t lds_static = [] {
+        hipFuncAttributes a;
+        LQ_CHECK(hipFuncGetAttributes(&a, reinterpret_cast<const void *>(&k_firfilt<KIND, HC>)));
+        return a.sharedSizeBytes;
+    }();
+    if (lds > FIR_LDS_MAX || lds + lds_static > 160 * 1024) {
         fprintf(stderr, "error: firfilt: filter length %u exceeds the GPU tile limit\n", d->hlen);
         exit(1);
     }
@@ -755,7 +765,7 @@ extern "C" unsigned int lqk_firfilt_max_history(int kind)
     unsigned int hp = 0;
     for (;;) {
         const size_t b = kind == 0 ? (size_t)lds_bytes<float>(TILE + hp + 64) : (size_t)lds_bytes<float2>(TILE + hp + 64);
-        if (b > 160 * 1024) return hp;
+        if (b > FIR_LDS_MAX) return hp;
         hp += 64;
     }
 }
@@ -845,7 +855,7 @@ extern "C" void lqk_firdecim(const lqk_fir_desc *d, unsigned int M, const void *
     const int HP = (int)(d->hc * d->nchunk);
     const unsigned nb = (unsigned)((nout + NT - 1) / NT);
     const size_t lds = (size_t)(NT * M + HP) * elem_size(d->kind);
-    if (lds > 160 * 1024) {
+    if (lds > FIR_LDS_MAX) {
         fprintf(stderr, "error: firdecim: decimation/filter length exceeds the GPU tile limit\n");
         exit(1);
     }
@@ -888,7 +898,7 @@ int decim_ph_shape(unsigned M, unsigned QC, const void *hq, unsigned hl1, const 
     const size_t lds_a = (size_t)M * dph_pitch(256 * 2 + (int)QC - 1) * es;
     const size_t lds_b = (size_t)M * dph_pitch(64 + (int)QC - 1) * es;
     if (lds_a <= 64 * 1024) launch_decim_ph<KIND, QCT, 2, 256>(M, QC, hq, hl1, hist, x, nout, y, lds_a, st);
-    else if (lds_b <= 160 * 1024) launch_decim_ph<KIND, QCT, 1, 64>(M, QC, hq, hl1, hist, x, nout, y, lds_b, st);
+    else if (lds_b <= FIR_LDS_MAX) launch_decim_ph<KIND, QCT, 1, 64>(M, QC, hq, hl1, hist, x, nout, y, lds_b, st);
     else return -1;
     return 0;
 }
