@@ -40,6 +40,7 @@
 #include <cstdint>
 #include <cstdio>
 #include <cstdlib>
+#include <type_traits>
 
 namespace {
 
@@ -78,9 +79,10 @@ struct Params {
     int gpw;          // groups per workgroup
     long long gend;   // one past the last group needed
     float2 *Y;
+    const float2 *zero; // >= 8 bytes of zeros (lqrt_zeros)
 };
 
-template <int L, int PF = 8>
+template <int L, bool PAIR>
 __global__ __launch_bounds__(NT, 1) void k_pfb2_an1024(Params P, const float *__restrict__ hsub,
                                                        const float2 *__restrict__ tw4096)
 {
@@ -137,32 +139,30 @@ __global__ __launch_bounds__(NT, 1) void k_pfb2_an1024(Params P, const float *__
     long long ge = gs + P.gpw;
     if (ge > P.gend) ge = P.gend;
     const long long HL = 2 * (L / 2) * M - M2;
-    // Row fetches go through two buffer descriptors whose range checks do the
-    // boundary work: x (n_in samples) and the history (HL samples before x).
-    // For any row exactly one of the two byte offsets is in range (or none,
-    // past either end) and out-of-range buffer loads return 0, so the sum of
-    // both loads is the sample -- no branches, 32-bit offsets (the host keeps
-    // each launch below 2^28 samples).
-    const __amdgpu_buffer_rsrc_t rx =
-        __builtin_amdgcn_make_buffer_rsrc((void *)P.x, (short)0, (int)(P.n_in * 8), 0x00020000);
-    const __amdgpu_buffer_rsrc_t rh =
-        __builtin_amdgcn_make_buffer_rsrc((void *)P.hist, (short)0, (int)(HL * 8), 0x00020000);
-    // local index of row (8gs - NS)'s sample for this lane; rows step by M
-    const long long ibase = (8 * gs - NS) * M + (long long)tid - P.B0 * M2;
-    const unsigned ox0 = (unsigned)(ibase * 8), oh0 = (unsigned)((HL + ibase) * 8);
-    // a row is fetched as its two raw loads; they are added only where the
-    // sample is consumed, so a prefetch does not wait for its data (an add at
-    // fetch time made every wave wait for the next iteration's rows before the
-    // transform phase: the loads then never overlapped the transforms)
-    struct Raw {
-        float2 a, b;
+    // Row fetches: one 8-byte load per lane and row from a pointer chosen per
+    // lane -- the history (the HL samples before x), x, or a zero word for
+    // samples before the history or past the call -- so the load needs no
+    // branch and no merge.  (Two range-checked loads per row, one of them out
+    // of range, cost a second vector-memory instruction and 16 VGPRs of
+    // prefetch registers.)  ls0 = local index of row (8gs - NS)'s first sample.
+    const long long ls0 = (8 * gs - NS) * M - P.B0 * M2;
+    const unsigned long long ah = (unsigned long long)(uintptr_t)(P.hist + HL);
+    const unsigned long long ax = (unsigned long long)(uintptr_t)P.x;
+    const unsigned long long az = (unsigned long long)(uintptr_t)P.zero;
+    auto fetch = [&](long long c) -> float2 {
+        const long long li = ls0 + (c - (8 * gs - NS)) * M + tid;
+        // address = (history or x) + 8 li, or the zero word: integer selects
+        // (v_cndmask), no branch around the load
+        const bool neg = li < 0;
+        const bool in = neg ? (li >= -HL) : (li < P.n_in);
+        unsigned long long a = (neg ? ah : ax) + (unsigned long long)(li * 8);
+        a = in ? a : az;
+        // a global (not flat) load: flat loads also count in lgkmcnt, which
+        // the LDS barriers wait on
+        typedef const v2f __attribute__((address_space(1))) *gptr;
+        const v2f v = __builtin_nontemporal_load(reinterpret_cast<gptr>(a));
+        return make_float2(v.x, v.y);
     };
-    auto fetch = [&](long long c) -> Raw {
-        const unsigned k = (unsigned)(c - (8 * gs - NS)) * (unsigned)(M * 8);
-        return {__builtin_bit_cast(float2, __builtin_amdgcn_raw_buffer_load_b64(rx, ox0 + k, 0, 0)),
-                __builtin_bit_cast(float2, __builtin_amdgcn_raw_buffer_load_b64(rh, oh0 + k, 0, 0))};
-    };
-    auto sum = [](Raw r) -> float2 { return make_float2(r.a.x + r.b.x, r.a.y + r.b.y); };
     // taps arrive scaled by 1/M (firpfbch2.c:277-278's output scale, exact for M = 2^10)
     auto dot = [&](int newest, const float (&h)[L]) -> float2 {
         float2 acc = make_float2(0.f, 0.f);
@@ -178,16 +178,52 @@ __global__ __launch_bounds__(NT, 1) void k_pfb2_an1024(Params P, const float *__
     // warm-up: rows 8gs-8 .. 8gs-1 fill the ring; the last gives the hi-bin
     // half of block 16gs (hi lanes, even taps)
 #pragma unroll
-    for (int s = 0; s < NS; s++) w[s] = sum(fetch(8 * gs - NS + s));
+    for (int s = 0; s < NS; s++) w[s] = fetch(8 * gs - NS + s);
     int slot0 = (int)((16 * gs) % NBUF); // buffer of block 16g (advances by 16 mod 17 = -1)
     if (!lo) xb[slot0 * BSTR + j] = dot(NS - 1, tb);
     __syncthreads(); // twiddle tables ready
 
-    // next iteration's first PF rows are prefetched into registers while the
-    // FFTs run; the rest are fetched as the rows are consumed
-    Raw pf[PF];
+    // Rows of later groups are prefetched into registers while a group is
+    // processed.  PAIR (16-byte aligned x): lane 2t loads row c, lane 2t+1
+    // row c+1, both at columns (2t, 2t+1) with one 16-byte load, and a DPP
+    // swap inside the lane pair gives every lane its own column of both rows
+    // -- half the load instructions of one 8-byte load per row and lane
+    // (0.636 -> 0.607 ms per 2^27 samples).  Otherwise one 8-byte load per
+    // row.  One group ahead: a second register set (the loop unrolled by
+    // two) gained 0.5 % with 8-byte loads and spills with pairs.
+    typedef float v4f_ __attribute__((ext_vector_type(4)));
+    const int odd = tid & 1;
+    auto fetch2 = [&](long long c) -> v4f_ {
+        const long long li = ls0 + (c + odd - (8 * gs - NS)) * M + (tid - odd);
+        const bool neg = li < 0;
+        const bool in = neg ? (li >= -HL) : (li < P.n_in);
+        unsigned long long a = (neg ? ah : ax) + (unsigned long long)(li * 8);
+        a = in ? a : az;
+        typedef const v4f_ __attribute__((address_space(1))) *gptr;
+        return __builtin_nontemporal_load(reinterpret_cast<gptr>(a));
+    };
+    // quad_perm [1,0,3,2]: swap with the pair partner
+    auto swp = [](float v) -> float {
+        return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0xB1, 0xF, 0xF, false));
+    };
+    auto split = [&](v4f_ v, float2 &rc, float2 &rn) {
+        // even lane holds row c (own, partner's column), odd lane row c+1
+        // (partner's column, own); each sends the sample its partner owns
+        const float sx = swp(odd ? v.x : v.z), sy = swp(odd ? v.y : v.w);
+        rc = odd ? make_float2(sx, sy) : make_float2(v.x, v.y);
+        rn = odd ? make_float2(v.z, v.w) : make_float2(sx, sy);
+    };
+    typedef typename std::conditional<PAIR, v4f_, float2>::type PfT;
+    constexpr int NPF = PAIR ? 4 : 8;
+    auto fetch_group = [&](long long g, PfT (&pf)[NPF]) {
 #pragma unroll
-    for (int r = 0; r < PF; r++) pf[r] = fetch(8 * gs + r);
+        for (int q = 0; q < NPF; q++) {
+            if constexpr (PAIR) pf[q] = fetch2(8 * g + 2 * q);
+            else pf[q] = fetch(8 * g + q);
+        }
+    };
+    PfT pf[NPF];
+    fetch_group(gs, pf);
     // Drain everything once before the loop: the loop header then merges an
     // empty vector-memory queue with the loop's own steady state (prefetched
     // rows, taps, then this wave's stores), and the compiler's vmcnt at the
@@ -205,10 +241,18 @@ __global__ __launch_bounds__(NT, 1) void k_pfb2_an1024(Params P, const float *__
 
     for (long long g = gs; g < ge; g++) {
         const long long b0 = 16 * g;
+        float2 nxt;
 #pragma unroll
         for (int r = 0; r < 8; r++) {
             // row c = 8g + r -> blocks b0 + 2r + dA (first), b0 + 2r + dA + 1 (second)
-            w[r] = sum(r < PF ? pf[r] : fetch(8 * g + r));
+            if constexpr (PAIR) {
+                // (the odd row waits in nxt: its ring slot still holds row
+                // r-7, which row r's dot product reads)
+                if ((r & 1) == 0) split(pf[r >> 1], w[r], nxt);
+                else w[r] = nxt;
+            } else {
+                w[r] = pf[r];
+            }
             int s1 = slot0 + 2 * r + dA;
             s1 -= (s1 >= NBUF) ? NBUF : 0;
             int s2 = s1 + 1;
@@ -216,10 +260,7 @@ __global__ __launch_bounds__(NT, 1) void k_pfb2_an1024(Params P, const float *__
             xb[s1 * BSTR + j] = dot(r, ta);
             xb[s2 * BSTR + j] = dot(r, tb);
         }
-        if (g + 1 < ge) {
-#pragma unroll
-            for (int r = 0; r < PF; r++) pf[r] = fetch(8 * (g + 1) + r);
-        }
+        if (g + 1 < ge) fetch_group(g + 1, pf);
         lds_barrier();
 
         // ---- one 1024-point IFFT per wave: block b0 + wave
@@ -664,6 +705,7 @@ extern "C" int lqk_firpfbch2_analyzer_fast(unsigned int Mch, unsigned int m, con
         P.B0 = B0 + ob;
         P.nblk = nb;
         P.Y = (float2 *)Y + ob * M;
+        P.zero = (const float2 *)lqrt_zeros();
         const long long gfirst = P.B0 / 16;                // 16-block group containing the first block
         const long long glast = (P.B0 + nb - 1) / 16;      // inclusive
         const long long ngroups = glast - gfirst + 1;
@@ -674,10 +716,16 @@ extern "C" int lqk_firpfbch2_analyzer_fast(unsigned int Mch, unsigned int m, con
         P.gs0 = gfirst;
         P.gpw = (int)gpw;
         P.gend = glast + 1;
-        if (m == 4)
-            hipLaunchKernelGGL(k_pfb2_an1024<8>, dim3((unsigned)nwg), dim3(NT), 0, st, P, (const float *)hsub, tw);
+        // paired 16-byte row loads need x and the history 16-byte aligned
+        const bool pair = ((uintptr_t)P.x & 15) == 0 && ((uintptr_t)(P.hist + HL) & 15) == 0;
+        if (m == 4 && pair)
+            hipLaunchKernelGGL((k_pfb2_an1024<8, true>), dim3((unsigned)nwg), dim3(NT), 0, st, P, (const float *)hsub, tw);
+        else if (m == 4)
+            hipLaunchKernelGGL((k_pfb2_an1024<8, false>), dim3((unsigned)nwg), dim3(NT), 0, st, P, (const float *)hsub, tw);
+        else if (pair)
+            hipLaunchKernelGGL((k_pfb2_an1024<4, true>), dim3((unsigned)nwg), dim3(NT), 0, st, P, (const float *)hsub, tw);
         else
-            hipLaunchKernelGGL(k_pfb2_an1024<4>, dim3((unsigned)nwg), dim3(NT), 0, st, P, (const float *)hsub, tw);
+            hipLaunchKernelGGL((k_pfb2_an1024<4, false>), dim3((unsigned)nwg), dim3(NT), 0, st, P, (const float *)hsub, tw);
         LQ_CHECK_LAUNCH();
     }
     return 1;

@@ -31,6 +31,8 @@ void   lqrt_sync(void *stream);
 void   lqrt_device_sync(void);
 int    lqrt_is_device_ptr(const void *p);
 const float *lqrt_twiddles(void);               /* W_4096^e = exp(-2 pi i e/4096), e<4096 */
+#define LQRT_ZEROS 256
+const float *lqrt_zeros(void);                  /* LQRT_ZEROS bytes of zeros in device memory */
 /* small-call completion: one kernel copies `bytes` (a multiple of 4, at most
  * LQRT_COPYOUT_MAX) from device memory src to pinned host memory dst, makes
  * them visible system-wide and then stores `seq` to the pinned word *flag;

@@ -150,13 +150,17 @@ extern "C" const float *lqrt_twiddles(void)
             h[2 * e + 1] = (float)sin(a);
         }
         float *d = nullptr;
-        LQ_CHECK(hipMalloc(&d, sizeof(h)));
+        // the table is followed by LQRT_ZEROS bytes of zeros (lqrt_zeros)
+        LQ_CHECK(hipMalloc(&d, sizeof(h) + LQRT_ZEROS));
         LQ_CHECK(hipMemcpy(d, h, sizeof(h), hipMemcpyHostToDevice));
+        LQ_CHECK(hipMemset(d + 2 * LQ_TW_N, 0, LQRT_ZEROS));
         LQ_CHECK(hipDeviceSynchronize());
         tables[dev] = d;
     }
     return tables[dev];
 }
+
+extern "C" const float *lqrt_zeros(void) { return lqrt_twiddles() + 2 * LQ_TW_N; }
 
 // ------------------------------------------------------------ small calls
 // The per-call liquid.h API (firfilt_execute, dotprod_execute,

@@ -102,3 +102,24 @@ def test_firpfbch2_output_8byte_aligned():
     y = dy.to_array(np.complex64, nb * 1024 + 1)[1:]
     ref = O.FirPfbch2(O.ANALYZER, 1024, 4, 60.0).execute_block(x)
     assert G.nrm_err(y, ref) < 1e-5
+
+
+@pytest.mark.parametrize("m", [4, 2])
+def test_firpfbch2_input_8byte_aligned(m):
+    """x only 8-byte aligned: the M = 1024 analyzer takes its one-load-per-row
+    kernel instead of the paired 16-byte loads; calls of both parities and
+    ragged lengths, compared with the oracle"""
+    r = np.random.default_rng(9 + m)
+    nb = 333
+    x = cx(r, nb * 512)
+    dx = LQ.DeviceBuffer(nb * 512 * 8 + 8)
+    LQ.lib().liquid_mi355x_memcpy_h2d(dx.p + 8, LQ.ptr(x), x.nbytes)
+    dy = LQ.DeviceBuffer(nb * 1024 * 8)
+    q = LQ.FirPfbch2(LQ.LIQUID_ANALYZER, 1024, m, 60.0)
+    cut = 101   # odd: the second call starts on an odd block
+    q.execute_block_dev(dx.p + 8, cut, dy.p)
+    q.execute_block_dev(dx.p + 8 + cut * 512 * 8, nb - cut, dy.p + cut * 1024 * 8)
+    q.synchronize()
+    y = dy.to_array(np.complex64, nb * 1024)
+    ref = O.FirPfbch2(O.ANALYZER, 1024, m, 60.0).execute_block(x)
+    assert G.nrm_err(y, ref) < 1e-5
