@@ -105,7 +105,7 @@ template <int L>
 __global__ __launch_bounds__(256) void k_pfb2_poly(int M, int nsl, const float *__restrict__ hsub,
                                                   const float2 *__restrict__ hist, const float2 *__restrict__ x,
                                                   int n_in, int p0, int nb, int cmin, int cmax, int S,
-                                                  float2 *__restrict__ Y)
+                                                  float2 *__restrict__ Y, const float2 *__restrict__ zero)
 {
     const int M2 = M >> 1, HL = L * M - M2;
     const int sl = (int)(blockIdx.x % (unsigned)nsl), seg = (int)(blockIdx.x / (unsigned)nsl);
@@ -124,19 +124,12 @@ __global__ __launch_bounds__(256) void k_pfb2_poly(int M, int nsl, const float *
             tb[n] = hsub[ib * L + n];
         }
     }
-    const __amdgpu_buffer_rsrc_t rx =
-        __builtin_amdgcn_make_buffer_rsrc((void *)x, (short)0, n_in * 8, 0x00020000);
-    const __amdgpu_buffer_rsrc_t rh =
-        __builtin_amdgcn_make_buffer_rsrc((void *)hist, (short)0, HL * 8, 0x00020000);
     // Y: nb blocks of M; a store outside (blocks before / after the call) is dropped
     const __amdgpu_buffer_rsrc_t ry =
         __builtin_amdgcn_make_buffer_rsrc((void *)Y, (short)0, nb * M * 8, 0x00020000);
     auto row_sample = [&](int r) -> float2 {
         const int t = r * M + col - p0 * M2;              // stream sample (t < 0: history)
-        const float2 a = __builtin_bit_cast(float2, __builtin_amdgcn_raw_buffer_load_b64(rx, (unsigned)t * 8u, 0, 0));
-        const float2 b =
-            __builtin_bit_cast(float2, __builtin_amdgcn_raw_buffer_load_b64(rh, (unsigned)(t + HL) * 8u, 0, 0));
-        return make_float2(a.x + b.x, a.y + b.y);
+        return lq_load_hx(hist + HL, x, zero, t, HL, n_in);
     };
     typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
     auto put = [&](int bt, float2 v) {   // block bt of the aligned numbering, bin j
@@ -213,15 +206,11 @@ __global__ __launch_bounds__(256 * R, R == 1 ? 2 : 1) void k_pfb2_an256(const fl
             tb[n] = hsub[ib * L + n];
         }
     }
-    const __amdgpu_buffer_rsrc_t rx = __builtin_amdgcn_make_buffer_rsrc((void *)x, (short)0, n_in * 8, 0x00020000);
-    const __amdgpu_buffer_rsrc_t rh = __builtin_amdgcn_make_buffer_rsrc((void *)hist, (short)0, HL * 8, 0x00020000);
     const __amdgpu_buffer_rsrc_t ry = __builtin_amdgcn_make_buffer_rsrc((void *)Y, (short)0, nb * M * 8, 0x00020000);
+    const float2 *zero = tw4096 + LQ_TW_N;   // lqrt_zeros(): the table's zero tail
     auto row_sample = [&](int r) -> float2 {
         const int t = r * M + col - p0 * M2;
-        const float2 a = __builtin_bit_cast(float2, __builtin_amdgcn_raw_buffer_load_b64(rx, (unsigned)t * 8u, 0, 0));
-        const float2 b =
-            __builtin_bit_cast(float2, __builtin_amdgcn_raw_buffer_load_b64(rh, (unsigned)(t + HL) * 8u, 0, 0));
-        return make_float2(a.x + b.x, a.y + b.y);
+        return lq_load_hx(hist + HL, x, zero, t, HL, n_in);
     };
     auto dot = [&](const float2 (&w)[NS], int newest, const float (&h)[L]) -> float2 {
         float2 acc = make_float2(0.f, 0.f);
@@ -322,7 +311,7 @@ bool launch_pfb2_poly(int M, const void *hsub, const void *hist, const void *x, 
     const long long nseg = (rows + S - 1) / S;
     hipLaunchKernelGGL((k_pfb2_poly<L>), dim3((unsigned)(nseg * nsl)), dim3(nt), 0, st, M, nsl, (const float *)hsub,
                        (const float2 *)hist, (const float2 *)x, (int)n_in, p0, (int)nb, cmin, cmax, (int)S,
-                       (float2 *)Y);
+                       (float2 *)Y, (const float2 *)lqrt_zeros());
     LQ_CHECK_LAUNCH();
     return true;
 }
@@ -656,17 +645,11 @@ __global__ __launch_bounds__(256 * R, R == 1 ? 2 : 1) void k_pfb_an_fused(const 
     TC h[P];
 #pragma unroll
     for (int n = 0; n < P; n++) h[n] = hsub[(M - 1 - j) * P + n];
-    const __amdgpu_buffer_rsrc_t rx = __builtin_amdgcn_make_buffer_rsrc((void *)x, (short)0, n_in * 8, 0x00020000);
-    const __amdgpu_buffer_rsrc_t rh =
-        __builtin_amdgcn_make_buffer_rsrc((void *)hist, (short)0, (HL > 0 ? HL : 1) * 8, 0x00020000);
     const __amdgpu_buffer_rsrc_t ry = __builtin_amdgcn_make_buffer_rsrc((void *)Y, (short)0, nb * M * 8, 0x00020000);
+    const float2 *zero = tw4096 + LQ_TW_N;   // lqrt_zeros(): the table's zero tail
     auto row_sample = [&](int b) -> float2 {
         const int t = b * M + j;
-        const float2 a = __builtin_bit_cast(float2, __builtin_amdgcn_raw_buffer_load_b64(rx, (unsigned)t * 8u, 0, 0));
-        if constexpr (HL == 0) return a;
-        const float2 c =
-            __builtin_bit_cast(float2, __builtin_amdgcn_raw_buffer_load_b64(rh, (unsigned)(t + HL) * 8u, 0, 0));
-        return make_float2(a.x + c.x, a.y + c.y);
+        return lq_load_hx(hist + HL, x, zero, t, HL, n_in);
     };
     const int g = threadIdx.x / (16 * R), t = threadIdx.x % (16 * R);
     const tw16x2 w16 = fftr16_tw<R>(tw4096, t);

@@ -47,6 +47,10 @@
 #include <cstdint>
 #include <cstdio>
 
+#ifndef FMX_VARIANT
+#define FMX_VARIANT 0
+#endif
+
 namespace {
 
 typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
@@ -282,7 +286,11 @@ __global__ __launch_bounds__(NT, (CC || KB > 1) ? 2 : 3) void k_firfilt_mx(const
             put1(planes, PLB, tid, hv);
             if (unsafe_bits(hv.x) | unsafe_bits(hv.y)) atomicOr(&sbad[cs], 1u);
         }
+#if FMX_VARIANT & 2   // timing experiment: no plane writes (wrong results)
+        if (__float_as_uint(xv[0].x + xv[1].y + xv[2].z + xv[3].w) == 0x7fc00001u) put8(planes, PLB, HALO + 8 * tid, xv);
+#else
         put8(planes, PLB, HALO + 8 * tid, xv);
+#endif
         if (unsafe4(xv[0]) | unsafe4(xv[1]) | unsafe4(xv[2]) | unsafe4(xv[3])) atomicOr(&sbad[cs], 1u);
         if (tid == 0) sbad[(cs + 1) % 3] = 0u;   // step k+1's slot (last read in step k-2)
         load8b(rx, main_off(k + 2), xv);
@@ -301,6 +309,13 @@ __global__ __launch_bounds__(NT, (CC || KB > 1) ? 2 : 3) void k_firfilt_mx(const
             const bf16x8 b1 = *reinterpret_cast<const bf16x8 *>(bp + 2 * PLB);
             const bf16x8 b2 = *reinterpret_cast<const bf16x8 *>(bp + 4 * PLB);
             // terms of order 2^-16 first, then 2^-8, then the leading product
+#if FMX_VARIANT & 1   // timing experiment: no MFMA (wrong results)
+#pragma unroll
+            for (int a = 0; a < NA; a++) {
+                C[a][s] += (float)b0[0] + (float)b1[1] + (float)b2[2] + (float)A[a][0][s][0];
+            }
+            continue;
+#endif
 #pragma unroll
             for (int a = 0; a < NA; a++) {
                 C[a] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(A[a][0][s], b2, C[a], 0, 0, 0);

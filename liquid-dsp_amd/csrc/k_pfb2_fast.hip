@@ -406,12 +406,14 @@ __device__ __forceinline__ void fft1k_wave_store(float2 *B, const float2 *tw1, c
     }
 }
 
-template <int P, int PF>
+template <int P, int PF, bool PAIR>
 __global__ __launch_bounds__(NT, 1) void k_pfb_an1024(const float2 *hist, const float2 *x, long long nblk, int gpw,
                                                       const float *__restrict__ hsub,
-                                                      const float2 *__restrict__ tw4096, float2 *Y)
+                                                      const float2 *__restrict__ tw4096, float2 *Y,
+                                                      const float2 *__restrict__ zero)
 {
     static_assert(P <= 8, "ring of 8 rows");
+    static_assert(PF % 2 == 0, "whole row pairs");
     __shared__ __attribute__((aligned(16))) float2 xb[16 * BSTR];
     __shared__ __attribute__((aligned(16))) float2 tw1[16 * 64];
     __shared__ __attribute__((aligned(16))) float2 tw2[16 * 4];
@@ -430,35 +432,69 @@ __global__ __launch_bounds__(NT, 1) void k_pfb_an1024(const float2 *hist, const 
     long long ge = gs + gpw;
     if (ge > ngroups) ge = ngroups;
     const long long HL = (long long)(P - 1) * M;
-    // rows through two range-checked buffer descriptors: x (nblk rows) and
-    // the history (P-1 rows before x); out-of-range loads return 0
-    const __amdgpu_buffer_rsrc_t rx =
-        __builtin_amdgcn_make_buffer_rsrc((void *)x, (short)0, (int)(nblk * M * 8), 0x00020000);
-    const __amdgpu_buffer_rsrc_t rh =
-        __builtin_amdgcn_make_buffer_rsrc((void *)hist, (short)0, (int)(HL * 8), 0x00020000);
-    const long long R0 = 16 * gs - 8;   // first row this workgroup touches
-    const long long ib = R0 * M + tid;
-    const unsigned ox0 = (unsigned)(ib * 8), oh0 = (unsigned)((HL + ib) * 8);
+    // One load per row and lane from a pointer chosen per lane (the history's
+    // P-1 rows before x, x, or a zero word), as k_pfb2_an1024; with PAIR
+    // (16-byte aligned x) lane 2t loads row c and lane 2t+1 row c+1 at
+    // columns (2t, 2t+1) and a DPP swap splits the pair.
+    typedef float v4f_ __attribute__((ext_vector_type(4)));
+    const unsigned long long ah = (unsigned long long)(uintptr_t)(hist + HL);
+    const unsigned long long ax = (unsigned long long)(uintptr_t)x;
+    const unsigned long long az = (unsigned long long)(uintptr_t)zero;
+    const long long nx = nblk * M;
+    auto addr = [&](long long li) -> unsigned long long {
+        const bool neg = li < 0;
+        const bool in = neg ? (li >= -HL) : (li < nx);
+        const unsigned long long a = (neg ? ah : ax) + (unsigned long long)(li * 8);
+        return in ? a : az;
+    };
     auto fetch = [&](long long c) -> float2 {
-        const unsigned k = (unsigned)(c - R0) * (unsigned)(M * 8);
-        const float2 a = __builtin_bit_cast(float2, __builtin_amdgcn_raw_buffer_load_b64(rx, ox0 + k, 0, 0));
-        const float2 b = __builtin_bit_cast(float2, __builtin_amdgcn_raw_buffer_load_b64(rh, oh0 + k, 0, 0));
-        return make_float2(a.x + b.x, a.y + b.y);
+        typedef const v2f __attribute__((address_space(1))) *gptr;
+        const v2f v = __builtin_nontemporal_load(reinterpret_cast<gptr>(addr(c * M + tid)));
+        return make_float2(v.x, v.y);
+    };
+    const int odd = tid & 1;
+    auto fetch2 = [&](long long c) -> v4f_ {
+        typedef const v4f_ __attribute__((address_space(1))) *gptr;
+        return __builtin_nontemporal_load(reinterpret_cast<gptr>(addr((c + odd) * M + (tid - odd))));
+    };
+    auto swp = [](float v) -> float {
+        return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0xB1, 0xF, 0xF, false));
+    };
+    auto split = [&](v4f_ v, float2 &rc, float2 &rn) {
+        const float sx = swp(odd ? v.x : v.z), sy = swp(odd ? v.y : v.w);
+        rc = odd ? make_float2(sx, sy) : make_float2(v.x, v.y);
+        rn = odd ? make_float2(v.z, v.w) : make_float2(sx, sy);
+    };
+    typedef typename std::conditional<PAIR, v4f_, float2>::type PfT;
+    constexpr int NPF = PAIR ? PF / 2 : PF;
+    auto fetch_pf = [&](long long g, PfT (&pf)[NPF]) {
+#pragma unroll
+        for (int q = 0; q < NPF; q++) {
+            if constexpr (PAIR) pf[q] = fetch2(16 * g + 2 * q);
+            else pf[q] = fetch(16 * g + q);
+        }
     };
     // row c lives in ring slot c & 7
     float2 w[8];
 #pragma unroll
     for (int s = 1; s < 8; s++) w[(8 - s) & 7] = fetch(16 * gs - s);
     w[0] = make_float2(0.f, 0.f);
-    float2 pf[PF];
-#pragma unroll
-    for (int r = 0; r < PF; r++) pf[r] = fetch(16 * gs + r);
+    PfT pf[NPF];
+    fetch_pf(gs, pf);
     __syncthreads();   // twiddle tables ready
 
     for (long long g = gs; g < ge; g++) {
+        float2 nxt;
 #pragma unroll
         for (int r = 0; r < 16; r++) {
-            w[r & 7] = r < PF ? pf[r] : fetch(16 * g + r);
+            if constexpr (PAIR) {
+                // the odd row waits in nxt: its ring slot holds row r-7 until
+                // row r's dot product has read it
+                if ((r & 1) == 0) split(r < PF ? pf[r >> 1] : fetch2(16 * g + r), w[r & 7], nxt);
+                else w[r & 7] = nxt;
+            } else {
+                w[r & 7] = r < PF ? pf[r] : fetch(16 * g + r);
+            }
             float2 acc = make_float2(0.f, 0.f);
 #pragma unroll
             for (int n = 0; n < P; n++) {
@@ -468,10 +504,7 @@ __global__ __launch_bounds__(NT, 1) void k_pfb_an1024(const float2 *hist, const 
             }
             xb[r * BSTR + tid] = acc;   // X[j], j = the lane's column
         }
-        if (g + 1 < ge) {
-#pragma unroll
-            for (int r = 0; r < PF; r++) pf[r] = fetch(16 * (g + 1) + r);
-        }
+        if (g + 1 < ge) fetch_pf(g + 1, pf);
         lds_barrier();
         const long long b = 16 * g + wave;
         if (b < nblk) fft1k_wave_store<+1>(xb + wave * BSTR, tw1, tw2, lane, Y + b * M);
@@ -753,12 +786,20 @@ extern "C" int lqk_firpfbch_analyzer_fast(int ctaps, unsigned int Mch, unsigned 
         long long gpw = (ngroups + 255) / 256;
         if (gpw < 2) gpw = 2;
         const unsigned nwg = (unsigned)((ngroups + gpw - 1) / gpw);
-        if (p == 8)
-            hipLaunchKernelGGL((k_pfb_an1024<8, 12>), dim3(nwg), dim3(NT), 0, st, hs, xs, nb, (int)gpw,
-                               (const float *)hsub, tw, (float2 *)Y + ob * M);
+        const float2 *zero = (const float2 *)lqrt_zeros();
+        const bool pair = ((uintptr_t)xs & 15) == 0 && ((uintptr_t)hs & 15) == 0;
+        if (p == 8 && pair)
+            hipLaunchKernelGGL((k_pfb_an1024<8, 12, true>), dim3(nwg), dim3(NT), 0, st, hs, xs, nb, (int)gpw,
+                               (const float *)hsub, tw, (float2 *)Y + ob * M, zero);
+        else if (p == 8)
+            hipLaunchKernelGGL((k_pfb_an1024<8, 12, false>), dim3(nwg), dim3(NT), 0, st, hs, xs, nb, (int)gpw,
+                               (const float *)hsub, tw, (float2 *)Y + ob * M, zero);
+        else if (pair)
+            hipLaunchKernelGGL((k_pfb_an1024<4, 16, true>), dim3(nwg), dim3(NT), 0, st, hs, xs, nb, (int)gpw,
+                               (const float *)hsub, tw, (float2 *)Y + ob * M, zero);
         else
-            hipLaunchKernelGGL((k_pfb_an1024<4, 16>), dim3(nwg), dim3(NT), 0, st, hs, xs, nb, (int)gpw,
-                               (const float *)hsub, tw, (float2 *)Y + ob * M);
+            hipLaunchKernelGGL((k_pfb_an1024<4, 16, false>), dim3(nwg), dim3(NT), 0, st, hs, xs, nb, (int)gpw,
+                               (const float *)hsub, tw, (float2 *)Y + ob * M, zero);
         LQ_CHECK_LAUNCH();
     }
     return 1;

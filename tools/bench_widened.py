@@ -77,7 +77,7 @@ def main():
         h = (torch.rand(hl) - 0.5).numpy().astype("float32")
         q = LQ.FirFilt("crcf", h)
         q.set_stream(S)
-        ms = timed(lambda: L.firfilt_crcf_execute_block_dev(q.q, x.data_ptr(), n, y.data_ptr()), it=10, w=5)
+        ms = timed(lambda: L.firfilt_crcf_execute_block_dev(q.q, x.data_ptr(), n, y.data_ptr()))
         report("firfilt_crcf h=%d" % hl, ms, n, "samples", 16 * n, "16 B/sample")
         q.destroy()
     del x, y
@@ -103,7 +103,7 @@ def main():
         a2 = LQ.FirPfbch2(LQ.LIQUID_ANALYZER, M, 4, 60.0)
         a2.set_stream(S)
         nb = n // (M // 2)
-        ms = timed(lambda: L.firpfbch2_crcf_execute_block_dev(a2.q, x.data_ptr(), nb, y.data_ptr()), it=10, w=5)
+        ms = timed(lambda: L.firpfbch2_crcf_execute_block_dev(a2.q, x.data_ptr(), nb, y.data_ptr()))
         report("firpfbch2_crcf analyzer M=%d m=4" % M, ms, n, "input samples", 24 * n,
                "8 B/input + 16 B/output (2 per input)")
         a2.destroy()
@@ -122,14 +122,14 @@ def main():
             nbc = nb * M // Mc
             p = LQ.FirPfbch(typ, Mc, m=4, As=60.0)
             p.set_stream(S)
-            ms = timed(lambda: L.firpfbch_crcf_execute_block_dev(p.q, X.data_ptr(), nbc, Y.data_ptr()), it=10, w=5)
+            ms = timed(lambda: L.firpfbch_crcf_execute_block_dev(p.q, X.data_ptr(), nbc, Y.data_ptr()))
             report("firpfbch_crcf %s M=%d m=4" % (nm, Mc), ms, nbc * Mc, "samples", 16 * nbc * Mc, "16 B/sample")
             p.destroy()
     for Mc in (256, 4096):
         nbc = nb * M // Mc
         q2 = LQ.FirPfbch2(LQ.LIQUID_SYNTHESIZER, Mc, 4, 60.0)
         q2.set_stream(S)
-        ms = timed(lambda: L.firpfbch2_crcf_execute_block_dev(q2.q, X.data_ptr(), nbc, Y.data_ptr()), it=10, w=5)
+        ms = timed(lambda: L.firpfbch2_crcf_execute_block_dev(q2.q, X.data_ptr(), nbc, Y.data_ptr()))
         report("firpfbch2_crcf synthesizer M=%d m=4" % Mc, ms, nbc * Mc // 2, "output samples", 12 * nbc * Mc,
                "8 B/channel sample in + 8 B/output (M/2 per block)")
         q2.destroy()
@@ -190,7 +190,7 @@ def main():
         ms_.set_stream(S)
         nin = n if rate < 1 else n // 4
         nout = ms_.num_output(nin)
-        ms = timed(lambda: ms_.execute_block_dev(x.data_ptr(), nin, y.data_ptr()), it=10, w=5)
+        ms = timed(lambda: ms_.execute_block_dev(x.data_ptr(), nin, y.data_ptr()))
         report("msresamp_crcf r=%g" % rate, ms, nin, "input samples", 8 * nin + 8 * nout,
                "8 B/input + 8 B/output")
         ms_.destroy()
@@ -200,7 +200,7 @@ def main():
         Z = cbuf(B * N)
         pl = L.fft_create_plan(N, None, None, 1, 0)
         L.fft_set_stream(pl, S)
-        ms = timed(lambda: L.fft_execute_batch_dev(pl, Z.data_ptr(), Z.data_ptr(), B), it=10, w=5)
+        ms = timed(lambda: L.fft_execute_batch_dev(pl, Z.data_ptr(), Z.data_ptr(), B))
         report("fft n=%d batch %d" % (N, B), ms, B * N, "points", 16 * B * N, "16 B/point (one pass)")
         L.fft_destroy_plan(pl)
     # spgram estimate, nfft = 1024 (window 512, transforms every 256 samples)
