@@ -11,12 +11,13 @@
 //
 // Parallel form.  The timing state at the start of every input is a pure
 // function of the previous one (it does not depend on the data), so the host
-// tabulates it once per rate (`plan`, see host/resamp.c): entry j holds
-// (tau, mu, b, state) before input j and K[j] = outputs emitted by inputs
-// < j; the sequence is eventually periodic (pre-period `pre`, period `P`
-// inputs, `Q` outputs per period).  Lanes look up the entry of their first
-// input and replay the reference's float32 recurrence bit-exactly for a few
-// inputs (contraction off).  k_resamp2 (the default) turns the replay into a
+// tabulates it once per rate (`plan`, see host/resamp.c): checkpoint c holds
+// (tau, mu, b, state) before input 32c and K = outputs emitted by the inputs
+// before it; the sequence is eventually periodic (pre-period `pre`, period
+// `P` inputs, `Q` outputs per period).  Lanes read the checkpoint at or before
+// their first input (16 B per 32 inputs: 0.5 B / input of plan traffic), step
+// the reference's float32 recurrence forward to it and replay their own
+// inputs, bit-exactly (contraction off).  k_resamp2 (the default) turns the replay into a
 // dense per-tile output list and evaluates it with coalesced stores;
 // k_resamp / k_resamp_generic cover shapes whose tables do not fit LDS.
 #include <hip/hip_runtime.h>
@@ -61,22 +62,96 @@ __device__ __forceinline__ void rs_advance(rs_state &s, float del, float fnpfb)
     s.mu = bf - fb;
 }
 
-__device__ __forceinline__ void rs_lookup(const lqk_rs_plan &pl, unsigned long long g, rs_state &s,
-                                          unsigned long long &K)
+// one input of the timing recurrence (resamp.c:253-307) without the data
+// path; returns the number of outputs it emits
+__device__ __forceinline__ unsigned rs_step(rs_state &s, float del, float fnpfb, int npfb)
 {
-    unsigned long long j = g, add = 0;
-    if (g >= pl.pre) {
-        const unsigned long long t = g - pl.pre;
-        const unsigned long long c = t / pl.P;
-        j = pl.pre + (t - c * pl.P);
-        add = c * pl.Q;
+    unsigned n = 0;
+    while (s.b < npfb) {
+        if (s.st && s.b == npfb - 1) {
+            s.st = 0;
+            s.b = npfb;
+            break;
+        }
+        n++;
+        rs_advance(s, del, fnpfb);
+        s.st = 1;
     }
-    const lqk_rs_entry e = pl.tab[(j & 3) * pl.qs + (j >> 2)];
+    s.tau -= 1.0f;
+    s.b -= npfb;
+    return n;
+}
+
+__device__ __forceinline__ void rs_entry(const lqk_rs_entry &e, rs_state &s)
+{
     s.tau = e.tau;
     s.mu = e.mu;
     s.b = e.bst >> 1;
     s.st = e.bst & 1;
+}
+
+// the state a power-of-two bank count derives from tau (host/resamp.c
+// rs_from_tau): BOUNDARY iff tau < 0, b = floor(tau npfb), mu its fraction
+__device__ __forceinline__ void rs_derive(float tau, float fnpfb, rs_state &s)
+{
+#pragma clang fp contract(off)
+    const float bf = tau * fnpfb;
+    const float fb = __builtin_floorf(bf);
+    s.tau = tau;
+    s.mu = bf - fb;
+    s.st = tau >= 0.0f ? 1 : 0;
+    s.b = s.st ? (int)fb : 0;
+}
+
+// the checkpoint (its fields in e) stepped `skip` inputs forward; K counts
+// the outputs of those inputs.  Power-of-two banks step tau alone: add del
+// until tau reaches 1 - 1/npfb, subtract 1 (host/resamp.c rs_step_p2)
+__device__ __forceinline__ void rs_skip(const lqk_rs_entry &e, int p2, int skip, float del, float fnpfb, int npfb,
+                                        rs_state &s, unsigned long long &K)
+{
+    if (p2) {
+#pragma clang fp contract(off)
+        const float z = 1.0f - 1.0f / fnpfb;
+        float x = e.tau;
+        unsigned k = 0;
+        for (int i = 0; i < skip; i++) {
+            while (x < z) {
+                x = x + del;
+                k++;
+            }
+            x = x - 1.0f;
+        }
+        K += k;
+        rs_derive(x, fnpfb, s);
+    } else {
+        rs_entry(e, s);
+        for (int i = 0; i < skip; i++) K += rs_step(s, del, fnpfb, npfb);
+    }
+}
+
+__device__ __forceinline__ lqk_rs_entry rs_load(const lqk_rs_plan &pl, unsigned ck)
+{
+    if (pl.p2) {
+        const lqk_rs_entry_p2 e = static_cast<const lqk_rs_entry_p2 *>(pl.tab)[ck];
+        return lqk_rs_entry{e.tau, 0.0f, 0, e.K};
+    }
+    return static_cast<const lqk_rs_entry *>(pl.tab)[ck];
+}
+
+// plan position g -> (state before input g, outputs before it)
+__device__ __forceinline__ void rs_lookup(const lqk_rs_plan &pl, unsigned long long g, float del, float fnpfb,
+                                          int npfb, rs_state &s, unsigned long long &K)
+{
+    unsigned long long j = g < pl.end ? g : pl.end, add = 0;
+    if (j >= pl.pre) {
+        const unsigned long long t = j - pl.pre;
+        const unsigned long long c = t / pl.P;
+        j = pl.pre + (t - c * pl.P);
+        add = c * pl.Q;
+    }
+    const lqk_rs_entry e = rs_load(pl, (unsigned)(j / LQK_RS_CK));
     K = (unsigned long long)e.K + add;
+    rs_skip(e, pl.p2, (int)(j & (LQK_RS_CK - 1)), del, fnpfb, npfb, s, K);
 }
 
 // taps[b*L + n] = (h[b + n*npfb], h[(b+1)%npfb + n*npfb]) -- the (y0, y1) pair
@@ -92,9 +167,10 @@ __global__ __launch_bounds__(NT) void k_resamp(lqk_rs_plan pl, unsigned long lon
 
     const long long i0 = ((long long)blockIdx.x * NT + threadIdx.x) * RS_R;
     if (i0 >= n) return;
+    const float fnpfb = (float)npfb;
     rs_state s;
     unsigned long long K;
-    rs_lookup(pl, g0 + (unsigned long long)i0, s, K);
+    rs_lookup(pl, g0 + (unsigned long long)i0, del, fnpfb, npfb, s, K);
     S *yo = y + (K - K0);
 
     // w[k] = x[i0 - L + k]; samples before the call come from the history
@@ -107,7 +183,6 @@ __global__ __launch_bounds__(NT) void k_resamp(lqk_rs_plan pl, unsigned long lon
         else if (idx < n) v = x[idx];
         w[k] = v;
     }
-    const float fnpfb = (float)npfb;
 #pragma unroll
     for (int r = 0; r < RS_R; ++r) {
         if (i0 + r >= n) break;
@@ -165,33 +240,39 @@ __global__ __launch_bounds__(NT) void k_resamp(lqk_rs_plan pl, unsigned long lon
 // in registers (one LDS read per input instead of L+1 per output) -- the run
 // is a dependent chain and the reads conflict 4-way: 0.226 -> 0.265 ms;
 // 2048-input tiles (0.247 ms); six workgroups per CU (spills: 0.52 ms).
-// plan position g = gt + d for a tile base gt (entry jt, cycles ct already
-// resolved once per tile) and a small lane offset d: 32-bit arithmetic
-__device__ __forceinline__ void rs_lookup_near(const lqk_rs_plan &pl, unsigned long long gt, unsigned long long jt,
-                                               unsigned long long ct, unsigned d, rs_state &s, unsigned long long &K)
+// plan position g = gt + d for a tile base gt (position jt, cycles ct already
+// resolved once per tile) and a small lane offset d, in 32-bit arithmetic:
+// the checkpoint to read, the periods before it and the inputs to step
+struct rs_ref {
+    unsigned ck;
+    int skip;
+    unsigned long long cyc;
+};
+__device__ __forceinline__ rs_ref rs_locate_near(const lqk_rs_plan &pl, unsigned long long gt, unsigned long long jt,
+                                                 unsigned long long ct, unsigned d)
 {
-    unsigned long long j = jt + d, c = ct;
-    if (gt >= pl.pre) {
+    unsigned long long j = gt + d, c = 0;
+    if (gt + d > pl.end) {                     // direct plans: clamp (pre = end + 1)
+        j = pl.end;
+    } else if (gt >= pl.pre) {
         const unsigned off = (unsigned)(jt - pl.pre) + d;
         const unsigned w = off / (unsigned)pl.P;
         j = pl.pre + (off - w * (unsigned)pl.P);
-        c += w;
+        c = ct + w;
     } else if (gt + d >= pl.pre) {
-        const unsigned long long t = gt + d - pl.pre;
-        const unsigned long long w = t / pl.P;
-        j = pl.pre + (t - w * pl.P);
+        const unsigned t = (unsigned)(gt + d - pl.pre);
+        const unsigned w = t / (unsigned)pl.P;
+        j = pl.pre + (t - w * (unsigned)pl.P);
         c = w;
     }
-    const lqk_rs_entry e = pl.tab[(j & 3) * pl.qs + (j >> 2)];
-    s.tau = e.tau;
-    s.mu = e.mu;
-    s.b = e.bst >> 1;
-    s.st = e.bst & 1;
-    K = (unsigned long long)e.K + c * pl.Q;
+    return rs_ref{(unsigned)(j / LQK_RS_CK), (int)(j & (LQK_RS_CK - 1)), c};
 }
 
 #ifndef RS_RIN
 #define RS_RIN 4
+#endif
+#ifndef RS_EXP
+#define RS_EXP 0   // timing experiments (wrong outputs): 1 no checkpoint skip, 2 no evaluation, 4 no replay
 #endif
 #ifndef RS_BLK
 #define RS_BLK 5   // workgroups per CU (96 VGPRs: five waves per SIMD)
@@ -203,7 +284,8 @@ template <int L, typename S>
 inline size_t rs2_lds_bytes(int npfb)
 {
     constexpr int TS = rs2_tin<L>() + L + 2;
-    return (size_t)(TS + 2) * sizeof(S) + (rs2_tin<L>() * 3 / 2 + 2) * 8 + (size_t)2 * (L + 1) * ((npfb >> 1) + 1) * sizeof(float2);
+    return (size_t)(TS + 2) * sizeof(S) + (rs2_tin<L>() * 3 / 2 + 2) * 8 + (size_t)2 * (L + 1) * ((npfb >> 1) + 1) * sizeof(float2) +
+           (size_t)(NT + 1) * 8;
 }
 
 template <int L, typename S>
@@ -225,6 +307,7 @@ __global__ __launch_bounds__(NT, RS_BLK) void k_resamp2(lqk_rs_plan pl, unsigned
     const int RS = (npfb >> 1) + 1;              // 8-byte slots per half row
 
     const int tid = threadIdx.x;
+    const float fnpfb = (float)npfb;
     for (int t = tid; t < (npfb + 1) * (L + 1); t += NT) {
         const int b = t / (L + 1), p = t % (L + 1);
         const float2 v = taps2[b * LP + p];
@@ -232,7 +315,6 @@ __global__ __launch_bounds__(NT, RS_BLK) void k_resamp2(lqk_rs_plan pl, unsigned
         // float32 operations as before (the difference rounded once here)
         tpl[(2 * p + (b & 1)) * RS + (b >> 1)] = make_float2(v.x, v.y - v.x);
     }
-    const float fnpfb = (float)npfb;
     const long long ntiles = (n + TIN - 1) / TIN;
     constexpr int NXV = (TS + NT - 1) / NT;       // tile samples per lane
 
@@ -255,25 +337,26 @@ __global__ __launch_bounds__(NT, RS_BLK) void k_resamp2(lqk_rs_plan pl, unsigned
     };
     struct Pre {
         S xa[NXV];
-        rs_state s;
-        unsigned long long K, Kb, Ke;
+        lqk_rs_entry e;                          // the checkpoint at or before the lane's first input
+        unsigned long long cyc;                  // periods before it
+        int skip;                                // inputs from it to the lane's first input
     };
+    unsigned long long *kx = reinterpret_cast<unsigned long long *>(tpl + 2 * (L + 1) * RS);   // [NT + 1]
     auto fetch = [&](long long tile, Pre &f) {
         const long long i0 = tile * TIN;
 #pragma unroll
         for (int u = 0; u < NXV; u++) f.xa[u] = ld(rx, i0 - L - 1 + tid + u * NT);
         const unsigned long long gt = g0 + (unsigned long long)i0;
         unsigned long long jt = gt, ct = 0;
-        if (gt >= pl.pre) {
+        if (gt >= pl.pre && gt <= pl.end) {
             const unsigned long long t = gt - pl.pre;
             ct = t / pl.P;
             jt = pl.pre + (t - ct * pl.P);
         }
-        rs_state tmp;
-        rs_lookup_near(pl, gt, jt, ct, 0, tmp, f.Kb);
-        const long long ie = (i0 + TIN < n) ? i0 + TIN : n;
-        rs_lookup_near(pl, gt, jt, ct, (unsigned)(ie - i0), tmp, f.Ke);
-        rs_lookup_near(pl, gt, jt, ct, (unsigned)(tid * RIN), f.s, f.K);
+        const rs_ref r = rs_locate_near(pl, gt, jt, ct, (unsigned)(tid * RIN));
+        f.e = rs_load(pl, r.ck);
+        f.cyc = r.cyc;
+        f.skip = r.skip;
     };
 
     const long long G = gridDim.x;
@@ -287,7 +370,13 @@ __global__ __launch_bounds__(NT, RS_BLK) void k_resamp2(lqk_rs_plan pl, unsigned
     fetch(tile0 + G, pb);
     auto body = [&](long long tile, Pre &cur) {
         const long long i0 = tile * TIN;
-        __syncthreads();                              // previous tile consumed
+        const long long ia = i0 + (long long)tid * RIN;   // this lane's first input
+        // the lane's state: its checkpoint stepped forward to input ia
+        rs_state slane;
+        unsigned long long Klane = (unsigned long long)cur.e.K + cur.cyc * pl.Q;
+        rs_skip(cur.e, pl.p2, (RS_EXP & 1) ? 0 : cur.skip, del, fnpfb, npfb, slane, Klane);
+        if (tid == 0) kx[0] = Klane;                  // the previous tile read kx[0] before its
+        __syncthreads();                              // second barrier; previous tile consumed
 #pragma unroll
         for (int u = 0; u < NXV; u++) {
             const int t = tid + u * NT;
@@ -297,20 +386,21 @@ __global__ __launch_bounds__(NT, RS_BLK) void k_resamp2(lqk_rs_plan pl, unsigned
             const long long sx = (long long)tid - L - 1;
             cp0[tid] = ld(rh, L + sx);
         }
-        const unsigned long long Kb = cur.Kb;
-        const long long ntile = (long long)(cur.Ke - Kb);
-        const rs_state slane = cur.s;
-        const unsigned long long Klane = cur.K;
+        const unsigned long long Kb = kx[0];
         // in flight during this tile and the next; unconditional (a tile past
-        // the end loads out of range: zeros, and plan positions any plan
-        // resolves) so the loads stay outstanding across the evaluation
+        // the end loads out of range: zeros, and positions the plan clamps)
+        // so the loads stay outstanding across the evaluation
         fetch(tile + 2 * G, cur);
-        const long long ia = i0 + (long long)tid * RIN;   // this lane's first input
+        // rounds of CAP outputs: replay the lane's inputs into the output list
+        // (round 0 also publishes the outputs before input ia + RIN, so the
+        // tile's output count is known after the barrier), evaluate
+        const long long nlane = (n - i0 + RIN - 1) / RIN;
+        long long ntile = CAP;
         for (long long r0 = 0; r0 < ntile; r0 += CAP) {
             if (r0 > 0) __syncthreads();                   // previous round consumed
             if (ia < n) {
                 rs_state s = slane;
-                long long o = (long long)(Klane - Kb) - r0;
+                unsigned long long Ko = Klane;
 #pragma unroll
                 for (int r = 0; r < RIN; r++) {
                     if (ia + r >= n) break;
@@ -321,17 +411,20 @@ __global__ __launch_bounds__(NT, RS_BLK) void k_resamp2(lqk_rs_plan pl, unsigned
                             s.b = npfb;
                             break;
                         }
-                        desc[(unsigned long long)o < (unsigned long long)CAP ? (int)o : CAP] =
+                        const unsigned long long o = Ko - Kb - (unsigned long long)r0;
+                        if (!(RS_EXP & 4)) desc[o < (unsigned long long)CAP ? (int)o : CAP] =
                             make_uint2(__float_as_uint(s.mu), (unsigned)iloc | ((unsigned)(s.st ? s.b : npfb) << 12));
-                        o++;
+                        Ko++;
                         rs_advance(s, del, fnpfb);
                         s.st = 1;
                     }
                     s.tau -= 1.0f;
                     s.b -= npfb;
                 }
+                if (r0 == 0) kx[tid + 1] = Ko;
             }
             __syncthreads();
+            if (r0 == 0) ntile = (long long)(kx[nlane < NT ? nlane : NT] - Kb);
             const int nr = (int)((ntile - r0) < CAP ? (ntile - r0) : CAP);
             S *yo = y + (Kb - K0) + r0;
             auto dot = [&](const S *wv, int bb, float mu) -> S {
@@ -356,7 +449,8 @@ __global__ __launch_bounds__(NT, RS_BLK) void k_resamp2(lqk_rs_plan pl, unsigned
                 __builtin_amdgcn_make_buffer_rsrc((void *)yo, (short)0, nr * (int)sizeof(S), 0x00020000);
             for (int o = tid; o < nr; o += NT) {
                 const uint2 d = desc[o];
-                const S v = dot(cp0 + (int)(d.y & 4095u) + 1, (int)(d.y >> 12), __uint_as_float(d.x));
+                S v{};
+                if (!(RS_EXP & 2)) v = dot(cp0 + (int)(d.y & 4095u) + 1, (int)(d.y >> 12), __uint_as_float(d.x));
                 if constexpr (sizeof(S) == 8) {
                     typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
                     __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2, v), ry, (unsigned)o * 8u, 0, 0);
@@ -384,12 +478,12 @@ __global__ __launch_bounds__(NT) void k_resamp_generic(lqk_rs_plan pl, unsigned 
 {
     const long long i = (long long)blockIdx.x * NT + threadIdx.x;
     if (i >= n) return;
+    const float fnpfb = (float)npfb;
     rs_state s;
     unsigned long long K;
-    rs_lookup(pl, g0 + (unsigned long long)i, s, K);
+    rs_lookup(pl, g0 + (unsigned long long)i, del, fnpfb, npfb, s, K);
     S *yo = y + (K - K0);
     auto X = [&](long long idx) -> S { return idx < 0 ? hist[L + idx] : x[idx]; };
-    const float fnpfb = (float)npfb;
     while (s.b < npfb) {
         if (s.st && s.b == npfb - 1) break;
         const bool bnd = !s.st;
@@ -415,7 +509,7 @@ void launch_rs(const lqk_rs_plan &pl, unsigned long long g0, unsigned long long 
 {
     constexpr int TIN = rs2_tin<L>();
     const size_t lds2 = rs2_lds_bytes<L, S>(npfb);
-    if (taps2 != nullptr && lds2 <= 64 * 1024 && pl.P < (1ull << 31) && pl.pre < (1ull << 62)) {
+    if (taps2 != nullptr && lds2 <= 64 * 1024 && pl.P < (1ull << 31) && (pl.pre < (1ull << 62) || pl.end < (1ull << 62))) {
         const long long ntiles = (n + TIN - 1) / TIN;
         const unsigned nb = (unsigned)(ntiles < 256 * RS_BLK ? ntiles : 256 * RS_BLK);   // persistent: RS_BLK per CU
         hipLaunchKernelGGL((k_resamp2<L, S>), dim3(nb), dim3(NT), lds2, st, pl, g0, K0, npfb, del, taps2, hist, x,

@@ -161,19 +161,30 @@ void lqk_fftfilt_make_H(const void *h_dev, unsigned int hlen, int is_complex, vo
 unsigned int lqk_fftfilt_nfft(void);
 
 /* ---------------------------------------------------------------- resamp / firpfb
- * Timing plan: entry j = the resampler's timing state before input j of the
- * plan (tau, mu, b, state; bst = b*2 + (state == INTERP)) and K = outputs
- * emitted by the plan's inputs < j.  Inputs g >= pre repeat with period P
- * (Q outputs per period): entry(g) = entry(pre + (g-pre) % P), K += Q per period. */
+ * Timing plan: checkpoint c = the resampler's timing state before plan input
+ * c*LQK_RS_CK and K = outputs emitted by the plan's inputs before it; the
+ * state at any other input is the checkpoint before it stepped forward
+ * (< LQK_RS_CK inputs).  Power-of-two bank counts store (tau, K) -- the rest
+ * of the state is a function of tau there (host/resamp.c) -- other bank
+ * counts the whole state (tau, mu, b, state; bst = b*2 + (state == INTERP)).
+ * Inputs g >= pre repeat with period P (Q outputs per period): state(g) =
+ * state(pre + (g-pre) % P), K += Q per period; positions beyond `end` are
+ * clamped to it (direct plans cover end + 1 positions). */
+#define LQK_RS_CK 16
 typedef struct {
     float tau, mu;
     int bst;
     unsigned int K;
 } lqk_rs_entry;
 typedef struct {
-    const lqk_rs_entry *tab;   /* device, entry j at tab[(j & 3) * qs + (j >> 2)] */
+    float tau;
+    unsigned int K;
+} lqk_rs_entry_p2;
+typedef struct {
+    const void *tab;           /* device: lqk_rs_entry_p2[] (p2) or lqk_rs_entry[], checkpoint c at [c] */
     unsigned long long pre, P, Q;
-    unsigned long long qs;     /* quarter-table stride */
+    unsigned long long end;
+    int p2;
 } lqk_rs_plan;
 /* n inputs x (plan positions g0 .. g0+n) -> outputs y[K(g) - K0 ...];
  * taps: npfb x L pairs (h[b + n*npfb], h[(b+1)%npfb + n*npfb]); hist = last L inputs.

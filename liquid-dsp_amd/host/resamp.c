@@ -29,6 +29,7 @@
 #define RS_MAX_PERIOD (1ull << 25)     /* give up on periodic plans beyond this many inputs */
 #define RS_DIRECT_CHUNK (1ull << 24)   /* direct plans cover at most this many inputs */
 #define RS_DIRECT_AHEAD (1ull << 14)   /* ... and at least this many (built ahead for short calls) */
+#define RS_EARLY 4                     /* a cycle may start at any of the first RS_EARLY states */
 
 enum { RS_BOUNDARY = 0, RS_INTERP = 1 };
 
@@ -40,10 +41,10 @@ typedef struct {
 typedef struct {
     int valid, periodic;
     rs_state origin;
-    lqk_rs_entry *tab;            /* host copy */
-    size_t nent, cap;
+    lqk_rs_entry *tab;            /* host copy: checkpoint c = state at plan position c * LQK_RS_CK */
+    size_t nck, cap;
     lq_devbuf d_tab;
-    unsigned long long pre, P, Q, qs;
+    unsigned long long pre, P, Q, end;
 } rs_plan;
 
 struct lq_rs_s {
@@ -98,6 +99,37 @@ static unsigned int rs_step(rs_state *s, float del, unsigned int npfb)
     return n;
 }
 
+/* Power-of-two banks: tau*npfb is exact, so the state before an input is a
+ * function of tau alone -- b < npfb <=> tau < 1, the INTERP check b == npfb-1
+ * <=> tau in [1 - 1/npfb, 1), BOUNDARY <=> tau < 0 (b = 0), and mu =
+ * frac(tau*npfb) equals the fraction of the last update (tau then differed by
+ * whole samples).  One input is then: add del until tau reaches 1 - 1/npfb,
+ * subtract 1 (the same float32 operations as rs_step, in the same order). */
+static inline unsigned int rs_step_p2(float *t, float del, float z)
+{
+    float x = *t;
+    unsigned int n = 0;
+    while (x < z) {
+        x += del;
+        n++;
+    }
+    *t = x - 1.0f;
+    return n;
+}
+
+static rs_state rs_from_tau(float tau, unsigned int npfb)
+{
+    rs_state s;
+    const float bf = tau * (float)npfb, fb = floorf(bf);
+    s.tau = tau;
+    s.mu = bf - fb;
+    s.st = tau < 0.0f ? RS_BOUNDARY : RS_INTERP;
+    s.b = s.st == RS_INTERP ? (int)fb : 0;
+    return s;
+}
+
+static int rs_pow2(unsigned int npfb) { return (npfb & (npfb - 1)) == 0; }
+
 static void rs_put(lqk_rs_entry *e, const rs_state *s, unsigned long long K)
 {
     e->tau = s->tau;
@@ -115,85 +147,241 @@ static rs_state rs_get(const lqk_rs_entry *e)
 static void rs_plan_reserve(rs_plan *pl, size_t n)
 {
     if (n > pl->cap) {
+        size_t c = pl->cap ? pl->cap : 1024;
+        while (c < n) c *= 2;
+        lqk_rs_entry *t = (lqk_rs_entry *)lq_xmalloc(c * sizeof(lqk_rs_entry));
+        if (pl->tab) memcpy(t, pl->tab, pl->nck * sizeof(lqk_rs_entry));
         free(pl->tab);
-        pl->tab = (lqk_rs_entry *)lq_xmalloc(n * sizeof(lqk_rs_entry));
-        pl->cap = n;
+        pl->tab = t;
+        pl->cap = c;
     }
 }
 
-/* plan entry index and K for plan position g */
-static const lqk_rs_entry *rs_plan_at(const rs_plan *pl, unsigned long long g, unsigned long long *K)
+/* state and K at plan position g: the checkpoint at or before g, then the
+ * remaining (< LQK_RS_CK) inputs stepped -- as k_resamp does on the GPU */
+static rs_state rs_plan_at(const rs_plan *pl, unsigned long long g, float del, unsigned int npfb,
+                           unsigned long long *K)
 {
     unsigned long long j = g, add = 0;
-    if (g >= pl->pre) {
-        unsigned long long t = g - pl->pre, c = t / pl->P;
+    if (g > pl->end) j = pl->end;
+    if (j >= pl->pre) {
+        unsigned long long t = j - pl->pre, c = t / pl->P;
         j = pl->pre + (t - c * pl->P);
         add = c * pl->Q;
     }
-    *K = (unsigned long long)pl->tab[j].K + add;
-    return &pl->tab[j];
+    const lqk_rs_entry *e = &pl->tab[j / LQK_RS_CK];
+    rs_state s = rs_get(e);
+    unsigned long long k = (unsigned long long)e->K + add;
+    for (unsigned long long i = j & ~(unsigned long long)(LQK_RS_CK - 1); i < j; i++) k += rs_step(&s, del, npfb);
+    *K = k;
+    return s;
 }
 
 static void rs_plan_upload(lq_rs *q)
 {
-    /* device layout: four quarter tables by j mod 4, so lanes looking up
-     * positions 4 apart read consecutive entries (lqk_rs_plan.qs) */
-    const size_t n = q->pl.nent, qs = (n + 3) / 4;
-    size_t bytes = 4 * qs * sizeof(lqk_rs_entry);
-    lqk_rs_entry *perm = (lqk_rs_entry *)lq_xmalloc(bytes);
-    memset(perm, 0, bytes);
-    for (size_t j = 0; j < n; j++) perm[(j & 3) * qs + (j >> 2)] = q->pl.tab[j];
+    if (rs_pow2(q->npfb)) {                  /* (tau, K): 8 B per LQK_RS_CK inputs */
+        size_t bytes = q->pl.nck * sizeof(lqk_rs_entry_p2);
+        lqk_rs_entry_p2 *t = (lqk_rs_entry_p2 *)lq_xmalloc(bytes);
+        for (size_t c = 0; c < q->pl.nck; c++) {
+            t[c].tau = q->pl.tab[c].tau;
+            t[c].K = q->pl.tab[c].K;
+        }
+        void *d = lq_devbuf_get(&q->pl.d_tab, bytes);
+        lqrt_h2d(d, t, bytes, q->ctx.stream);
+        lqrt_sync(q->ctx.stream);
+        free(t);
+        return;
+    }
+    size_t bytes = q->pl.nck * sizeof(lqk_rs_entry);
     void *d = lq_devbuf_get(&q->pl.d_tab, bytes);
-    lqrt_h2d(d, perm, bytes, q->ctx.stream);
+    lqrt_h2d(d, q->pl.tab, bytes, q->ctx.stream);
     lqrt_sync(q->ctx.stream);
-    free(perm);
-    q->pl.qs = qs;
 }
 
-/* Brent's cycle detection on the per-input timing state, from q->now */
+/* walk n inputs from x0 recording a checkpoint every LQK_RS_CK of them (from
+ * the plan's first); with `early` set, stop as soon as the state returns to one
+ * of the first RS_EARLY states (a cycle without a pre-period beyond them):
+ * returns the position of the return (or n), *q0 the state index it returned to */
+#define RS_BRENT (~1ull)
+
+static unsigned long long rs_walk(lq_rs *q, rs_state x0, unsigned long long n, int early, unsigned long long *q0,
+                                  unsigned long long *Kend, unsigned long long *lam_out)
+{
+    rs_plan *pl = &q->pl;
+    const unsigned long long CK = LQK_RS_CK;
+    pl->nck = 0;
+    unsigned long long K = 0, i = 0;
+    if (rs_pow2(q->npfb)) {
+        /* the hot loop: runs of steps between checkpoints; with `early`, the
+         * first RS_EARLY states are compared with each other, and every later
+         * state (branch-free) with the first and with Brent's tortoise, the
+         * state at position 2^k - 1: a pure cycle ends the walk on its first
+         * return, any other once the tortoise sits on the cycle (r = 1.037:
+         * 1 011 163 steps, ~3 ms) */
+        const float del = q->del, z = 1.0f - 1.0f / (float)q->npfb;
+        float t = x0.tau;
+        unsigned int eb[RS_EARLY], tort;
+        unsigned long long tpos = 0, reset = 1;
+        for (int k = 0; k < RS_EARLY; k++) eb[k] = 0x7fc00001u;
+        memcpy(&tort, &t, 4);
+        for (;;) {
+            if ((i & (CK - 1)) == 0) {
+                rs_plan_reserve(pl, pl->nck + 1);
+                rs_state s = i == 0 ? x0 : rs_from_tau(t, q->npfb);
+                rs_put(&pl->tab[pl->nck++], &s, K);
+            }
+            if (K > 0xffffffffull || i == n) break;
+            unsigned long long stop = (n - i) < CK - (i & (CK - 1)) ? n : (i | (CK - 1)) + 1;
+            if (!early) {
+                for (; i < stop; i++) K += rs_step_p2(&t, del, z);
+                continue;
+            }
+            if (i < RS_EARLY) {                     /* position i: compare, record, step */
+                unsigned int tb;
+                memcpy(&tb, &t, 4);
+                for (unsigned long long k = 0; k < i; k++)
+                    if (eb[k] == tb) {
+                        *q0 = k;
+                        *Kend = K;
+                        return i;
+                    }
+                eb[i] = tb;
+                if (i == reset) {
+                    tort = eb[i];
+                    tpos = i;
+                    reset = 2 * i + 1;
+                }
+                K += rs_step_p2(&t, del, z);
+                i++;
+                continue;
+            }
+            if (stop > reset + 1) stop = reset + 1;
+            for (; i < stop; i++) {
+                unsigned int tb;
+                memcpy(&tb, &t, 4);
+                if ((tb == eb[0]) | (tb == tort)) {
+                    for (int k = RS_EARLY - 1; k >= 0; k--)
+                        if (eb[k] == tb) {
+                            *q0 = (unsigned long long)k;
+                            *Kend = K;
+                            return i;
+                        }
+                    *q0 = RS_BRENT;
+                    *lam_out = i - tpos;
+                    *Kend = K;
+                    return i;
+                }
+                if (i == reset) {
+                    tort = tb;
+                    tpos = i;
+                    reset = 2 * i + 1;
+                }
+                K += rs_step_p2(&t, del, z);
+            }
+        }
+    } else {
+        rs_state s = x0, e[RS_EARLY];
+        int ne = 0;
+        for (;;) {
+            if ((i & (CK - 1)) == 0) {
+                rs_plan_reserve(pl, pl->nck + 1);
+                rs_put(&pl->tab[pl->nck++], &s, K);
+                if (K > 0xffffffffull) break;
+            }
+            if (i == n) break;
+            if (early) {
+                for (int k = 0; k < ne; k++)
+                    if (rs_eq(&e[k], &s)) {
+                        *q0 = (unsigned long long)k;
+                        *Kend = K;
+                        return i;
+                    }
+                if (ne < RS_EARLY) e[ne++] = s;
+            }
+            K += rs_step(&s, q->del, q->npfb);
+            i++;
+        }
+    }
+    *q0 = ~0ull;
+    *Kend = K;
+    return K > 0xffffffffull ? 0 : i;   /* K must fit the table's 32 bits */
+}
+
+/* the plan's K at position g < pre + P (no wrap) */
+static unsigned long long rs_K_lin(lq_rs *q, unsigned long long g)
+{
+    rs_plan save = q->pl;
+    q->pl.pre = ~0ull;
+    q->pl.end = ~0ull;
+    unsigned long long K;
+    rs_plan_at(&q->pl, g, q->del, q->npfb, &K);
+    q->pl.pre = save.pre;
+    q->pl.end = save.end;
+    return K;
+}
+
+/* Periodic plan from q->now.  The timing state visits a finite set, so the
+ * walk is eventually periodic; usually the orbit returns to one of its first
+ * states (r = 1.037: to the initial state after 1 011 163 inputs), found in
+ * one pass that records the checkpoints as it goes.  Otherwise Brent's cycle
+ * detection finds pre-period and period, and a second pass records them. */
 static int rs_plan_build_periodic(lq_rs *q)
 {
     const rs_state x0 = q->now;
-    rs_state tort = x0, hare = x0;
-    unsigned long long power = 1, lam = 1;
-    rs_step(&hare, q->del, q->npfb);
-    while (!rs_eq(&tort, &hare)) {
-        if (power == lam) {
-            if (power > RS_MAX_PERIOD) return 0;
-            tort = hare;
-            power *= 2;
-            lam = 0;
+    unsigned long long q0, Kend, lam = 0;
+    unsigned long long n = rs_walk(q, x0, RS_MAX_PERIOD + RS_EARLY, 1, &q0, &Kend, &lam);
+    unsigned long long pre, P;
+    if (q0 != ~0ull && q0 != RS_BRENT) {
+        pre = q0;
+        P = n - q0;
+    } else {
+        int recorded = q0 == RS_BRENT;            /* the walk already covers [0, mu + lam) */
+        if (!recorded) {                          /* general banks: Brent on the full state */
+            rs_state tort = x0, hare = x0;
+            unsigned long long power = 1;
+            lam = 1;
+            rs_step(&hare, q->del, q->npfb);
+            while (!rs_eq(&tort, &hare)) {
+                if (power == lam) {
+                    if (power > RS_MAX_PERIOD) return 0;
+                    tort = hare;
+                    power *= 2;
+                    lam = 0;
+                }
+                rs_step(&hare, q->del, q->npfb);
+                lam++;
+            }
         }
-        rs_step(&hare, q->del, q->npfb);
-        lam++;
+        /* pre-period: one copy lam steps ahead, both walked until they meet */
+        unsigned long long mu = 0;
+        if (rs_pow2(q->npfb)) {
+            const float z = 1.0f - 1.0f / (float)q->npfb;
+            float a = x0.tau, h = x0.tau;
+            for (unsigned long long i = 0; i < lam; i++) rs_step_p2(&h, q->del, z);
+            while (memcmp(&a, &h, 4) != 0) {
+                if (mu > RS_MAX_PERIOD) return 0;
+                rs_step_p2(&a, q->del, z);
+                rs_step_p2(&h, q->del, z);
+                mu++;
+            }
+        } else {
+            rs_state tort = x0, hare = x0;
+            for (unsigned long long i = 0; i < lam; i++) rs_step(&hare, q->del, q->npfb);
+            while (!rs_eq(&tort, &hare)) {
+                if (mu > RS_MAX_PERIOD) return 0;
+                rs_step(&tort, q->del, q->npfb);
+                rs_step(&hare, q->del, q->npfb);
+                mu++;
+            }
+        }
+        pre = mu;
+        P = lam;
+        if (!recorded && rs_walk(q, x0, pre + P, 0, &q0, &Kend, &lam) != pre + P) return 0;
     }
-    /* pre-period: advance one copy lam steps, then walk both until they meet */
-    tort = x0;
-    hare = x0;
-    for (unsigned long long i = 0; i < lam; i++) rs_step(&hare, q->del, q->npfb);
-    unsigned long long mu = 0;
-    while (!rs_eq(&tort, &hare)) {
-        if (mu > RS_MAX_PERIOD) return 0;
-        rs_step(&tort, q->del, q->npfb);
-        rs_step(&hare, q->del, q->npfb);
-        mu++;
-    }
-    /* table of pre + P entries; K must fit 32 bits */
-    size_t n = (size_t)(mu + lam);
-    rs_plan_reserve(&q->pl, n);
-    rs_state s = x0;
-    unsigned long long K = 0, Kpre = 0;
-    for (size_t j = 0; j < n; j++) {
-        if (K > 0xffffffffull) return 0;
-        if (j == mu) Kpre = K;
-        rs_put(&q->pl.tab[j], &s, K);
-        K += rs_step(&s, q->del, q->npfb);
-    }
-    if (K > 0xffffffffull) return 0;
-    q->pl.nent = n;
-    q->pl.pre = mu;
-    q->pl.P = lam;
-    q->pl.Q = K - Kpre;
+    q->pl.pre = pre;
+    q->pl.P = P;
+    q->pl.end = ~0ull;
+    q->pl.Q = rs_K_lin(q, pre + P) - rs_K_lin(q, pre);
     q->pl.origin = x0;
     q->pl.periodic = 1;
     q->pl.valid = 1;
@@ -204,19 +392,14 @@ static int rs_plan_build_periodic(lq_rs *q)
 /* plan covering exactly the next nx inputs (nx <= RS_DIRECT_CHUNK) */
 static void rs_plan_build_direct(lq_rs *q, unsigned long long nx)
 {
-    size_t n = (size_t)nx + 1;
-    rs_plan_reserve(&q->pl, n);
-    rs_state s = q->now;
-    unsigned long long K = 0;
-    for (size_t j = 0; j < n; j++) {
-        rs_put(&q->pl.tab[j], &s, K);
-        if (j + 1 < n) K += rs_step(&s, q->del, q->npfb);
-    }
-    if (K > 0xffffffffull) LQ_FAIL("error: resamp_%s: too many outputs for one call\n", lq_ext[q->kind]);
-    q->pl.nent = n;
-    q->pl.pre = n;
+    unsigned long long q0, Kend;
+    unsigned long long lam;
+    if (rs_walk(q, q->now, nx, 0, &q0, &Kend, &lam) != nx || Kend > 0xffffffffull)
+        LQ_FAIL("error: resamp_%s: too many outputs for one call\n", lq_ext[q->kind]);
+    q->pl.pre = nx + 1;
     q->pl.P = 1;
     q->pl.Q = 0;
+    q->pl.end = nx;
     q->pl.origin = q->now;
     q->pl.periodic = 0;
     q->pl.valid = 1;
@@ -234,11 +417,11 @@ static unsigned long long rs_ensure_plan(lq_rs *q, unsigned long long nx)
 {
     rs_check_rate(q);
     if (q->pl.valid && q->pl.periodic) return nx;
-    if (q->pl.valid && q->gpos + nx <= q->pl.nent - 1) return nx;
+    if (q->pl.valid && q->gpos + nx <= q->pl.end) return nx;
     lqrt_sync(q->ctx.stream);                /* the old table may still be in use */
     if (q->pl.valid) {                       /* state at the end of the old plan's coverage */
         unsigned long long K;
-        q->now = rs_get(rs_plan_at(&q->pl, q->gpos, &K));
+        q->now = rs_plan_at(&q->pl, q->gpos, q->del, q->npfb, &K);
     }
     q->pl.valid = 0;
     if (!q->periodic_failed && nx >= RS_PERIODIC_MIN) {
@@ -265,7 +448,7 @@ static unsigned long long rs_ensure_plan(lq_rs *q, unsigned long long nx)
 static unsigned long long rs_K(lq_rs *q, unsigned long long g)
 {
     unsigned long long K;
-    rs_plan_at(&q->pl, g, &K);
+    rs_plan_at(&q->pl, g, q->del, q->npfb, &K);
     return K;
 }
 
@@ -274,7 +457,7 @@ static void rs_sync_now(lq_rs *q)
 {
     if (q->pl.valid) {
         unsigned long long K;
-        q->now = rs_get(rs_plan_at(&q->pl, q->gpos, &K));
+        q->now = rs_plan_at(&q->pl, q->gpos, q->del, q->npfb, &K);
     }
 }
 
@@ -411,15 +594,21 @@ unsigned long long lq_rs_num_output(lq_rs *_q, unsigned long long _nx)
     unsigned long long done = 0, total = 0;
     /* periodic plans answer directly; otherwise simulate on a copy of the state */
     if (!(_q->pl.valid && _q->pl.periodic) && _nx >= RS_PERIODIC_MIN) rs_ensure_plan(_q, _nx);
-    if (_q->pl.valid && (_q->pl.periodic || _q->gpos + _nx <= _q->pl.nent - 1))
+    if (_q->pl.valid && (_q->pl.periodic || _q->gpos + _nx <= _q->pl.end))
         return rs_K(_q, _q->gpos + _nx) - rs_K(_q, _q->gpos);
     rs_check_rate(_q);
     rs_state s = _q->now;
     if (_q->pl.valid) {
         unsigned long long K;
-        s = rs_get(rs_plan_at(&_q->pl, _q->gpos, &K));
+        s = rs_plan_at(&_q->pl, _q->gpos, _q->del, _q->npfb, &K);
     }
-    for (; done < _nx; done++) total += rs_step(&s, _q->del, _q->npfb);
+    if (rs_pow2(_q->npfb)) {
+        const float z = 1.0f - 1.0f / (float)_q->npfb;
+        float t = s.tau;
+        for (; done < _nx; done++) total += rs_step_p2(&t, _q->del, z);
+    } else {
+        for (; done < _nx; done++) total += rs_step(&s, _q->del, _q->npfb);
+    }
     return total;
 }
 
@@ -432,7 +621,7 @@ void lq_rs_block_dev(lq_rs *_q, const void *_dxv, unsigned long long _nx, void *
     while (_nx > 0) {
         unsigned long long c = rs_ensure_plan(_q, _nx);
         unsigned long long K0 = rs_K(_q, _q->gpos), K1 = rs_K(_q, _q->gpos + c);
-        lqk_rs_plan kp = {(const lqk_rs_entry *)_q->pl.d_tab.p, _q->pl.pre, _q->pl.P, _q->pl.Q, _q->pl.qs};
+        lqk_rs_plan kp = {_q->pl.d_tab.p, _q->pl.pre, _q->pl.P, _q->pl.Q, _q->pl.end, rs_pow2(_q->npfb)};
         void *hold = _q->d_hist[_q->cur], *hnew = _q->d_hist[_q->cur ^ 1];
         lqk_resamp(_q->kind == LQ_RRRF, &kp, _q->gpos, K0, _q->npfb, _q->L, _q->del, _q->d_taps, _q->d_taps2, hold, _dx, c, _dy,
                    _q->ctx.stream);
@@ -548,7 +737,7 @@ long long liquid_mi355x_resamp_schedule(float _rate, unsigned int _npfb, unsigne
     const int np = (int)_npfb;
     for (unsigned long long g = 0; g < _nx; g++) {
         unsigned long long K;
-        rs_state s = rs_get(rs_plan_at(&q.pl, g, &K));
+        rs_state s = rs_plan_at(&q.pl, g, q.del, q.npfb, &K);
         if (K != k) {
             free(q.pl.tab);
             return -2;                       /* plan's output count disagrees with the replay */
