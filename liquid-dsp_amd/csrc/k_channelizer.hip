@@ -293,6 +293,136 @@ bool launch_pfb2_an256(const void *hsub, const void *hist, const void *x, long l
     return true;
 }
 
+// M = 64 / 128 analyzer fused (the two-pass path moved 56 B per input): as
+// k_pfb2_an256, with Q = 256 / M column sets per workgroup, each a lane per
+// column over its own run of rows (segment blockIdx.x Q + set), and each
+// group of 8 rows' 16 blocks per set transformed in registers by R = M / 16
+// lanes (fft_small16xR: 16 Q transforms of M points per workgroup, all 256
+// lanes).  Every set runs the same number of groups (its stores past its
+// rows are dropped), so the barriers stay uniform.
+template <int L, int MS>
+__global__ __launch_bounds__(256, 2) void k_pfb2_an_small(const float *__restrict__ hsub,
+                                                         const float2 *__restrict__ hist,
+                                                         const float2 *__restrict__ x, int n_in, int p0, int nb,
+                                                         int cmin, int cmax, int S, float2 *__restrict__ Y,
+                                                         const float2 *__restrict__ tw4096)
+{
+    constexpr int M = MS, M2 = M / 2, HL = L * M - M2, NS = 8, NBUF = 17;
+    constexpr int Q = 256 / M, R = M / 16, P = FFTS_LDS<R>();
+    __shared__ __attribute__((aligned(16))) float2 xr[Q * NBUF * M];
+    __shared__ __attribute__((aligned(16))) float2 scr[16 * Q * P];
+    const int set = threadIdx.x / M, col = threadIdx.x % M;
+    float2 *xs = xr + set * (NBUF * M);
+    const bool lo = col < M2;
+    const int j = lo ? (M2 - 1 - col) : (3 * M2 - 1 - col);
+    const int dA = lo ? 0 : 1;
+    float ta[L], tb[L];
+    {
+        const int ia = lo ? j : (j ^ M2), ib = lo ? (j ^ M2) : j;
+#pragma unroll
+        for (int n = 0; n < L; n++) {
+            ta[n] = hsub[ia * L + n];
+            tb[n] = hsub[ib * L + n];
+        }
+    }
+    const __amdgpu_buffer_rsrc_t ry = __builtin_amdgcn_make_buffer_rsrc((void *)Y, (short)0, nb * M * 8, 0x00020000);
+    const float2 *zero = tw4096 + LQ_TW_N;   // lqrt_zeros(): the table's zero tail
+    auto row_sample = [&](int r) -> float2 {
+        const int t = r * M + col - p0 * M2;
+        return lq_load_hx(hist + HL, x, zero, t, HL, n_in);
+    };
+    auto dot = [&](const float2 (&w)[NS], int newest, const float (&h)[L]) -> float2 {
+        float2 acc = make_float2(0.f, 0.f);
+#pragma unroll
+        for (int n = 0; n < L; n++) {
+            const float2 v = w[(newest - n) & (NS - 1)];
+            acc.x = fmaf(h[n], v.x, acc.x);
+            acc.y = fmaf(h[n], v.y, acc.y);
+        }
+        return acc;
+    };
+    auto slot = [](int b) { return ((b % NBUF) + NBUF) % NBUF; };
+    // transform phase: transform tg = threadIdx.x / R of set tg / 16 (its block
+    // 2 r0 + tg % 16), lane t
+    const int tg = threadIdx.x / R, t = threadIdx.x % R;
+    const int tset = tg / 16, tb16 = tg % 16;
+    const int e = t * (4096 / M);
+    const float2 a1 = tw4096[e & 4095], a4 = tw4096[(4 * e) & 4095];
+    const float inv = 1.0f / (float)M;
+    typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
+
+    const int seg = (int)blockIdx.x * Q + set;
+    const int cs = cmin + seg * S;
+    int ce = cs + S;
+    if (ce > cmax + 1) ce = cmax + 1;
+    // the transform lanes' set (another set's rows)
+    const int tcs = cmin + ((int)blockIdx.x * Q + tset) * S;
+    int tce = tcs + S;
+    if (tce > cmax + 1) tce = cmax + 1;
+    float2 w[NS], pf[NS];
+#pragma unroll
+    for (int u = 0; u < NS; u++) w[u] = row_sample(cs - NS + u);
+    if (!lo) xs[slot(2 * cs) * M + j] = dot(w, NS - 1, tb);
+#pragma unroll
+    for (int u = 0; u < NS; u++) pf[u] = row_sample(cs + u);
+    for (int g0 = 0; g0 < S; g0 += NS) {
+        const int r0 = cs + g0;
+#pragma unroll
+        for (int u = 0; u < NS; u++) {
+            w[u] = pf[u];
+            pf[u] = row_sample(r0 + NS + u);
+            const int c = r0 + u;
+            xs[slot(2 * c + dA) * M + j] = dot(w, u, ta);
+            xs[slot(2 * c + dA + 1) * M + j] = dot(w, u, tb);
+        }
+        __syncthreads();
+        // blocks 2 r0 .. 2 r0 + 15 of every set are complete
+        const int tr0 = tcs + g0;
+        const int b = 2 * tr0 + tb16;
+        float2 v[16];
+        const float2 *B = xr + tset * (NBUF * M) + slot(b) * M;
+#pragma unroll
+        for (int n = 0; n < 16; n++) v[n] = B[t + R * n];
+        fft_small16xR<R, -1>(v, scr + tg * P, a1, a4, t);   // (its barriers also free the ring buffers)
+        const int gb = b - p0;
+        const bool keep = gb >= 0 && gb < nb && tr0 < tce;
+        const unsigned base = keep ? (unsigned)gb * (unsigned)(M * 8) : 0xFFFFF000u;
+        // v[u R + q] = X[t (16/R) + u + 16 q]
+#pragma unroll
+        for (int u = 0; u < 16 / R; u++)
+#pragma unroll
+            for (int q = 0; q < R; q++) {
+                const float2 vv = v[u * R + q];
+                const float2 o = make_float2(vv.x * inv, vv.y * inv);
+                __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2, o), ry,
+                                                      base + (unsigned)(t * (16 / R) + u + 16 * q) * 8u, 0, 0);
+            }
+    }
+}
+
+template <int L, int MS>
+bool launch_pfb2_an_small(const void *hsub, const void *hist, const void *x, long long nb, int p0, void *Y,
+                          hipStream_t st)
+{
+    constexpr int M = MS, Q = 256 / M;
+    const long long n_in = nb * (M / 2);
+    if (n_in * 8 >= (1ll << 31) || nb * (long long)M * 8 >= (1ll << 31)) return false;
+    const int cmin = (p0 - 1) >> 1;
+    const int cmax = (int)((p0 + nb - 1) >> 1);
+    const int rows = cmax - cmin + 1;
+    // runs of S rows (a multiple of 8) per set: about 2048 sets on long calls
+    long long S = ((long long)rows + 2047) / 2048;
+    S = (S + 7) / 8 * 8;
+    if (S < 32) S = 32;
+    const long long nseg = (rows + S - 1) / S;
+    const long long nwg = (nseg + Q - 1) / Q;
+    hipLaunchKernelGGL((k_pfb2_an_small<L, MS>), dim3((unsigned)nwg), dim3(256), 0, st, (const float *)hsub,
+                       (const float2 *)hist, (const float2 *)x, (int)n_in, p0, (int)nb, cmin, cmax, (int)S,
+                       (float2 *)Y, (const float2 *)lqrt_twiddles());
+    LQ_CHECK_LAUNCH();
+    return true;
+}
+
 template <int L>
 bool launch_pfb2_poly(int M, const void *hsub, const void *hist, const void *x, long long nb, int p0, void *Y,
                       hipStream_t st)
@@ -1252,6 +1382,20 @@ extern "C" void lqk_firpfbch2_analyzer(unsigned int M, unsigned int m, const voi
     case LL:                                                                                               \
         f = M == 256 ? launch_pfb2_an256<LL, 1>(hsub, hc, xc, nbc, p0, Yc, st)                            \
                      : launch_pfb2_an256<LL, 2>(hsub, hc, xc, nbc, p0, Yc, st);                           \
+        break;
+                switch (2 * m) {
+                    LQ_F(2) LQ_F(4) LQ_F(6) LQ_F(8)
+                default: break;
+                }
+#undef LQ_F
+                if (f) continue;
+            }
+            if ((M == 64 || M == 128) && 2 * m <= 8 && !getenv("LQ_PFB2_TWO_PASS")) {
+                bool f = false;
+#define LQ_F(LL)                                                                                           \
+    case LL:                                                                                               \
+        f = M == 64 ? launch_pfb2_an_small<LL, 64>(hsub, hc, xc, nbc, p0, Yc, st)                          \
+                    : launch_pfb2_an_small<LL, 128>(hsub, hc, xc, nbc, p0, Yc, st);                        \
         break;
                 switch (2 * m) {
                     LQ_F(2) LQ_F(4) LQ_F(6) LQ_F(8)

@@ -25,6 +25,8 @@
 #include "lq_device.h"
 #include "lq_kernels.h"
 
+#include <cmath>
+#include <cstdio>
 #include <cstdlib>
 #include <type_traits>
 
@@ -274,36 +276,44 @@ __device__ __forceinline__ rs_ref rs_locate_near(const lqk_rs_plan &pl, unsigned
 #ifndef RS_EXP
 #define RS_EXP 0   // timing experiments (wrong outputs): 1 no checkpoint skip, 2 no evaluation, 4 no replay
 #endif
-#ifndef RS_BLK
-#define RS_BLK 5   // workgroups per CU (96 VGPRs: five waves per SIMD)
+// workgroups per CU: six for L <= 16 (25.5 KB LDS, <= 80 VGPRs each: L = 14
+// 0.236 -> 0.221 ms against five); longer filters spill at 80 VGPRs
+template <int L>
+constexpr int rs2_blk() { return L <= 16 ? 6 : 5; }
+#ifndef RS_CAPX
+#define RS_CAPX 64    // output slots per tile beyond TIN (r = 1.037: <= 1066 outputs per 1024 inputs)
 #endif
 template <int L>
 constexpr int rs2_tin() { return NT * RS_RIN; }
+constexpr int rs2_cap() { return NT * RS_RIN + RS_CAPX; }
 // LDS bytes of k_resamp2<L, S>: window copy, output descriptors, pair table
 template <int L, typename S>
 inline size_t rs2_lds_bytes(int npfb)
 {
     constexpr int TS = rs2_tin<L>() + L + 2;
-    return (size_t)(TS + 2) * sizeof(S) + (rs2_tin<L>() * 3 / 2 + 2) * 8 + (size_t)2 * (L + 1) * ((npfb >> 1) + 1) * sizeof(float2) +
-           (size_t)(NT + 1) * 8;
+    return (size_t)(TS + 2) * sizeof(S) + (rs2_cap() + 2) * 8 + (size_t)2 * (L + 1) * ((npfb >> 1) + 1) * sizeof(float2) +
+           (size_t)(rs2_tin<L>() / LQK_RS_CK + 1) * 8;
 }
 
 template <int L, typename S>
-__global__ __launch_bounds__(NT, RS_BLK) void k_resamp2(lqk_rs_plan pl, unsigned long long g0, unsigned long long K0,
+__global__ __launch_bounds__(NT, rs2_blk<L>()) void k_resamp2(lqk_rs_plan pl, unsigned long long g0, unsigned long long K0,
                                                 int npfb, float del, const float2 *__restrict__ taps2,
                                                 const S *__restrict__ hist, const S *__restrict__ x,
-                                                long long n, S *__restrict__ y)
+                                                long long n, S *__restrict__ y, int nout, int tin)
 {
-    constexpr int RIN = RS_RIN;
     constexpr int TIN = rs2_tin<L>();
     constexpr int LP = (L + 2 + 1) & ~1;         // pair stride of taps2 (host layout, >= L+1)
     constexpr int TS = TIN + L + 2;              // tile samples
     constexpr int CS = TS + 2;                   // copy size (keeps what follows 16-byte aligned)
-    constexpr int CAP = TIN + TIN / 2;           // outputs per round
+    constexpr int CAP = rs2_cap();               // outputs per tile (the host sizes tin to fit)
+    constexpr int NSLOT = (CAP + NT - 1) / NT;   // output slots per lane
+    constexpr int SPAN = LQK_RS_CK;              // inputs replayed per lane of wave 0
+    constexpr int NSPAN = TIN / SPAN;            // = 64: the tile's spans, one per lane of wave 0
+    static_assert(NSPAN == 64, "one wave replays a tile");
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     S *cp0 = reinterpret_cast<S *>(smem);
     uint2 *desc = reinterpret_cast<uint2 *>(cp0 + CS);
-    float2 *tpl = reinterpret_cast<float2 *>(desc + CAP + 2);   // desc[CAP]: sink of out-of-round outputs
+    float2 *tpl = reinterpret_cast<float2 *>(desc + CAP + 2);   // desc[CAP]: sink of out-of-tile outputs
     const int RS = (npfb >> 1) + 1;              // 8-byte slots per half row
 
     const int tid = threadIdx.x;
@@ -315,19 +325,25 @@ __global__ __launch_bounds__(NT, RS_BLK) void k_resamp2(lqk_rs_plan pl, unsigned
         // float32 operations as before (the difference rounded once here)
         tpl[(2 * p + (b & 1)) * RS + (b >> 1)] = make_float2(v.x, v.y - v.x);
     }
-    const long long ntiles = (n + TIN - 1) / TIN;
+    const long long ntiles = (n + tin - 1) / tin;
     constexpr int NXV = (TS + NT - 1) / NT;       // tile samples per lane
 
-    // everything a tile needs from HBM, fetched one tile ahead into registers.
+    // everything a tile needs from HBM, fetched two tiles ahead into registers.
     // Samples come through two range-checked descriptors (x: n samples, the
     // history: the L before it); each sample is in range in at most one, so
-    // their sum is the sample and the loads carry no branch -- a branchy load
-    // merged its result through register copies, which made the prefetch wait
-    // for its data at once.  The host keeps n * sizeof(S) below 2^31.
+    // their sum is the sample and the loads carry no branch.  Every tile issues
+    // the same loads and stores (a store outside the launch's outputs is
+    // dropped): with a fixed count of memory operations per tile the compiler
+    // waits for exactly the prefetched registers it needs -- a data-dependent
+    // store count made it drain everything (vmcnt(0)), the prefetch included,
+    // at the start of every tile.  The host keeps n * sizeof(S) below 2^31.
     const __amdgpu_buffer_rsrc_t rx =
         __builtin_amdgcn_make_buffer_rsrc((void *)x, (short)0, (int)(n * (long long)sizeof(S)), 0x00020000);
     const __amdgpu_buffer_rsrc_t rh =
         __builtin_amdgcn_make_buffer_rsrc((void *)hist, (short)0, (int)(L * sizeof(S)), 0x00020000);
+    // stores through a descriptor over the launch's nout outputs: 32-bit
+    // offsets, and a store outside them is dropped
+    const __amdgpu_buffer_rsrc_t ry = __builtin_amdgcn_make_buffer_rsrc((void *)y, (short)0, nout * (int)sizeof(S), 0x00020000);
     auto ld = [&](__amdgpu_buffer_rsrc_t r, long long e) -> S {
         const unsigned off = (unsigned)(e * (long long)sizeof(S));   // negative: out of range, reads 0
         if constexpr (sizeof(S) == 8)
@@ -336,16 +352,17 @@ __global__ __launch_bounds__(NT, RS_BLK) void k_resamp2(lqk_rs_plan pl, unsigned
             return __builtin_bit_cast(S, __builtin_amdgcn_raw_buffer_load_b32(r, off, 0, 0));
     };
     struct Pre {
-        S xa[NXV];
+        S xa[NXV], xh;                           // tile window; the history part of its first vector
         lqk_rs_entry e;                          // the checkpoint at or before the lane's first input
         unsigned long long cyc;                  // periods before it
         int skip;                                // inputs from it to the lane's first input
     };
-    unsigned long long *kx = reinterpret_cast<unsigned long long *>(tpl + 2 * (L + 1) * RS);   // [NT + 1]
+    unsigned long long *kx = reinterpret_cast<unsigned long long *>(tpl + 2 * (L + 1) * RS);   // [NSPAN + 1]
     auto fetch = [&](long long tile, Pre &f) {
-        const long long i0 = tile * TIN;
+        const long long i0 = tile * tin;
 #pragma unroll
         for (int u = 0; u < NXV; u++) f.xa[u] = ld(rx, i0 - L - 1 + tid + u * NT);
+        f.xh = ld(rh, i0 == 0 ? (long long)tid - 1 : -1);   // tile 0's first L samples: the history
         const unsigned long long gt = g0 + (unsigned long long)i0;
         unsigned long long jt = gt, ct = 0;
         if (gt >= pl.pre && gt <= pl.end) {
@@ -353,7 +370,8 @@ __global__ __launch_bounds__(NT, RS_BLK) void k_resamp2(lqk_rs_plan pl, unsigned
             ct = t / pl.P;
             jt = pl.pre + (t - ct * pl.P);
         }
-        const rs_ref r = rs_locate_near(pl, gt, jt, ct, (unsigned)(tid * RIN));
+        const int d = tid < NSPAN && tid * SPAN < tin ? tid * SPAN : 0;
+        const rs_ref r = rs_locate_near(pl, gt, jt, ct, (unsigned)d);
         f.e = rs_load(pl, r.ck);
         f.cyc = r.cyc;
         f.skip = r.skip;
@@ -362,101 +380,134 @@ __global__ __launch_bounds__(NT, RS_BLK) void k_resamp2(lqk_rs_plan pl, unsigned
     const long long G = gridDim.x;
     long long tile0 = blockIdx.x;
     if (tile0 >= ntiles) return;
-    // two register sets, two tiles in flight while one is evaluated (the
-    // kernel waited on its loads with one); the loop is unrolled by two so a
-    // set is never copied, which would wait on its loads at once
+    // two register sets, two tiles in flight while one is evaluated; the loop
+    // is unrolled by two so a set is never copied, which would wait on its
+    // loads at once
     Pre pa, pb;
     fetch(tile0, pa);
     fetch(tile0 + G, pb);
     auto body = [&](long long tile, Pre &cur) {
-        const long long i0 = tile * TIN;
-        const long long ia = i0 + (long long)tid * RIN;   // this lane's first input
-        // the lane's state: its checkpoint stepped forward to input ia
-        rs_state slane;
-        unsigned long long Klane = (unsigned long long)cur.e.K + cur.cyc * pl.Q;
-        rs_skip(cur.e, pl.p2, (RS_EXP & 1) ? 0 : cur.skip, del, fnpfb, npfb, slane, Klane);
-        if (tid == 0) kx[0] = Klane;                  // the previous tile read kx[0] before its
-        __syncthreads();                              // second barrier; previous tile consumed
+        const long long i0 = tile * tin;
+        const long long ie = (i0 + tin < n) ? i0 + tin : n;   // the tile's inputs [i0, ie)
+        const lqk_rs_entry e = cur.e;                         // (fetch overwrites cur below)
+        const unsigned long long cyc = cur.cyc;
+        const int skip = (RS_EXP & 1) ? 0 : cur.skip;
+        __syncthreads();                              // previous tile consumed
 #pragma unroll
         for (int u = 0; u < NXV; u++) {
             const int t = tid + u * NT;
-            if (t < TS) cp0[t] = cur.xa[u];
+            if (t < TS) cp0[t] = u == 0 ? cur.xa[0] + cur.xh : cur.xa[u];
         }
-        if (i0 == 0 && tid <= L) {                    // samples before the call: the history
-            const long long sx = (long long)tid - L - 1;
-            cp0[tid] = ld(rh, L + sx);
-        }
-        const unsigned long long Kb = kx[0];
         // in flight during this tile and the next; unconditional (a tile past
         // the end loads out of range: zeros, and positions the plan clamps)
-        // so the loads stay outstanding across the evaluation
         fetch(tile + 2 * G, cur);
-        // rounds of CAP outputs: replay the lane's inputs into the output list
-        // (round 0 also publishes the outputs before input ia + RIN, so the
-        // tile's output count is known after the barrier), evaluate
-        const long long nlane = (n - i0 + RIN - 1) / RIN;
-        long long ntile = CAP;
-        for (long long r0 = 0; r0 < ntile; r0 += CAP) {
-            if (r0 > 0) __syncthreads();                   // previous round consumed
-            if (ia < n) {
-                rs_state s = slane;
-                unsigned long long Ko = Klane;
-#pragma unroll
-                for (int r = 0; r < RIN; r++) {
-                    if (ia + r >= n) break;
+        // wave 0 replays the timing: lane s the SPAN inputs from i0 + s SPAN,
+        // starting at its checkpoint (skip < SPAN inputs before them), writing
+        // the tile's output list and the outputs before its last input
+        if (tid < NSPAN) {
+            const long long ia = i0 + (long long)tid * SPAN;
+            const int nin = ia < ie ? (int)((ie - ia) < SPAN ? (ie - ia) : SPAN) : 0;
+            unsigned long long k = (unsigned long long)e.K + cyc * pl.Q;
+            auto put = [&](unsigned long long Kb, int iloc, int bank, float mu) {
+                const unsigned long long o = k - Kb;
+                if (!(RS_EXP & 4))
+                    desc[o < (unsigned long long)CAP ? (int)o : CAP] =
+                        make_uint2(__float_as_uint(mu), (unsigned)iloc | ((unsigned)bank << 12));
+            };
+            unsigned long long Kb;
+            if (pl.p2) {
+                // power-of-two banks: the state is tau alone (rs_derive); an
+                // input emits while tau < 1 - 1/npfb, then tau -= 1
+#pragma clang fp contract(off)
+                const float z = 1.0f - 1.0f / fnpfb;
+                float xx = e.tau;
+                for (int i = 0; i < skip; i++) {
+                    while (xx < z) {
+                        xx = xx + del;
+                        k++;
+                    }
+                    xx = xx - 1.0f;
+                }
+                Kb = ((unsigned long long)(unsigned)__builtin_amdgcn_readlane((int)(k >> 32), 0) << 32) |
+                     (unsigned)__builtin_amdgcn_readlane((int)k, 0);
+                for (int r = 0; r < nin; r++) {
                     const int iloc = (int)(ia + r - i0);
-                    while (s.b < npfb) {
-                        if (s.st && s.b == npfb - 1) {
-                            s.st = 0;
-                            s.b = npfb;
+                    while (xx < z) {
+                        const float bf = xx * fnpfb;
+                        const float fb = __builtin_floorf(bf);
+                        put(Kb, iloc, xx < 0.0f ? npfb : (int)fb, bf - fb);
+                        k++;
+                        xx = xx + del;
+                    }
+                    xx = xx - 1.0f;
+                }
+            } else {
+                rs_state st;
+                rs_entry(e, st);
+                for (int i = 0; i < skip; i++) k += rs_step(st, del, fnpfb, npfb);
+                Kb = ((unsigned long long)(unsigned)__builtin_amdgcn_readlane((int)(k >> 32), 0) << 32) |
+                     (unsigned)__builtin_amdgcn_readlane((int)k, 0);
+                for (int r = 0; r < nin; r++) {
+                    const int iloc = (int)(ia + r - i0);
+                    while (st.b < npfb) {
+                        if (st.st && st.b == npfb - 1) {
+                            st.st = 0;
+                            st.b = npfb;
                             break;
                         }
-                        const unsigned long long o = Ko - Kb - (unsigned long long)r0;
-                        if (!(RS_EXP & 4)) desc[o < (unsigned long long)CAP ? (int)o : CAP] =
-                            make_uint2(__float_as_uint(s.mu), (unsigned)iloc | ((unsigned)(s.st ? s.b : npfb) << 12));
-                        Ko++;
-                        rs_advance(s, del, fnpfb);
-                        s.st = 1;
+                        put(Kb, iloc, st.st ? st.b : npfb, st.mu);
+                        k++;
+                        rs_advance(st, del, fnpfb);
+                        st.st = 1;
                     }
-                    s.tau -= 1.0f;
-                    s.b -= npfb;
+                    st.tau -= 1.0f;
+                    st.b -= npfb;
                 }
-                if (r0 == 0) kx[tid + 1] = Ko;
             }
-            __syncthreads();
-            if (r0 == 0) ntile = (long long)(kx[nlane < NT ? nlane : NT] - Kb);
-            const int nr = (int)((ntile - r0) < CAP ? (ntile - r0) : CAP);
-            S *yo = y + (Kb - K0) + r0;
-            auto dot = [&](const S *wv, int bb, float mu) -> S {
-                const float2 *tp = tpl + (bb & 1) * RS + (bb >> 1);
-                S acc{};
+            if (nin > 0) kx[tid + 1] = k;
+            if (tid == 0) kx[0] = Kb;
+        }
+        __syncthreads();
+        const unsigned long long Kb = kx[0];
+        const long long nlane = (ie - i0 + SPAN - 1) / SPAN;
+        long long ntile = (long long)(kx[nlane] - Kb);
+        ntile = ntile < 0 ? 0 : (ntile > CAP ? CAP : ntile);   // exact; the clamp is a guard
+        const int nr = (int)ntile;
+        const unsigned ob = (unsigned)(Kb - K0);              // the tile's first output
+        auto dot = [&](const S *wv, int bb, float mu) -> S {
+            const float2 *tp = tpl + (bb & 1) * RS + (bb >> 1);
+            S acc{};
 #pragma unroll
-                for (int p = 0; p <= L; p++) {
-                    const float2 t = tp[2 * p * RS];
-                    const float c = fmaf(mu, t.y, t.x);
-                    if constexpr (sizeof(S) == 8) {
-                        v2f a2 = {acc.x, acc.y};
-                        a2 = v2f{c, c} * v2f{wv[p].x, wv[p].y} + a2;
-                        acc = make_float2(a2.x, a2.y);
-                    } else {
-                        acc = rs_axpy(c, wv[p], acc);
-                    }
-                }
-                return acc;
-            };
-            // stores through a descriptor over this round's outputs: 32-bit offsets
-            const __amdgpu_buffer_rsrc_t ry =
-                __builtin_amdgcn_make_buffer_rsrc((void *)yo, (short)0, nr * (int)sizeof(S), 0x00020000);
-            for (int o = tid; o < nr; o += NT) {
-                const uint2 d = desc[o];
-                S v{};
-                if (!(RS_EXP & 2)) v = dot(cp0 + (int)(d.y & 4095u) + 1, (int)(d.y >> 12), __uint_as_float(d.x));
+            for (int p = 0; p <= L; p++) {
+                const float2 t = tp[2 * p * RS];
+                const float c = fmaf(mu, t.y, t.x);
                 if constexpr (sizeof(S) == 8) {
-                    typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
-                    __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2, v), ry, (unsigned)o * 8u, 0, 0);
+                    v2f a2 = {acc.x, acc.y};
+                    a2 = v2f{c, c} * v2f{wv[p].x, wv[p].y} + a2;
+                    acc = make_float2(a2.x, a2.y);
                 } else {
-                    __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, v), ry, (unsigned)o * 4u, 0, 0);
+                    acc = rs_axpy(c, wv[p], acc);
                 }
+            }
+            return acc;
+        };
+        // NSLOT outputs per lane, every store issued (slots past the tile's
+        // outputs go out of range and are dropped): a fixed store count
+#pragma unroll
+        for (int k = 0; k < NSLOT; k++) {
+            const int o = tid + k * NT;
+            S v{};
+            if (o < nr && !(RS_EXP & 2)) {
+                const uint2 dd = desc[o];
+                v = (RS_EXP & 4) ? dot(cp0 + (int)(dd.y & 1023u) + 1, (int)((dd.y >> 12) & 63u), __uint_as_float(dd.x))
+                                 : dot(cp0 + (int)(dd.y & 4095u) + 1, (int)(dd.y >> 12), __uint_as_float(dd.x));
+            }
+            const unsigned off = o < nr ? (ob + (unsigned)o) * (unsigned)sizeof(S) : 0xFFFFFFF0u;
+            if constexpr (sizeof(S) == 8) {
+                typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
+                __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2, v), ry, off, 0, 0);
+            } else {
+                __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, v), ry, off, 0, 0);
             }
         }
     };
@@ -505,15 +556,23 @@ __global__ __launch_bounds__(NT) void k_resamp_generic(lqk_rs_plan pl, unsigned 
 template <int L, typename S>
 void launch_rs(const lqk_rs_plan &pl, unsigned long long g0, unsigned long long K0, int npfb, float del,
                const float2 *taps, const float2 *taps2, const S *hist, const S *x, long long n, S *y,
-               hipStream_t st)
+               unsigned long long nout, hipStream_t st)
 {
     constexpr int TIN = rs2_tin<L>();
     const size_t lds2 = rs2_lds_bytes<L, S>(npfb);
     if (taps2 != nullptr && lds2 <= 64 * 1024 && pl.P < (1ull << 31) && (pl.pre < (1ull << 62) || pl.end < (1ull << 62))) {
-        const long long ntiles = (n + TIN - 1) / TIN;
-        const unsigned nb = (unsigned)(ntiles < 256 * RS_BLK ? ntiles : 256 * RS_BLK);   // persistent: RS_BLK per CU
+        // inputs per tile: every tile's outputs fit the CAP output slots (at
+        // most (tin + 2) r + 2 outputs: tau moves by 1/r per output and by -1
+        // per input within [-1/npfb, 1 + 1/r))
+        constexpr int CAP = rs2_cap();
+        const double r = 1.0 / (double)del;
+        int tin = TIN;
+        while (tin > LQK_RS_CK && std::ceil((tin + 2) * r) + 2 > CAP) tin -= LQK_RS_CK;
+        const long long ntiles = (n + tin - 1) / tin;
+        constexpr int BLK = rs2_blk<L>();
+        const unsigned nb = (unsigned)(ntiles < 256 * BLK ? ntiles : 256 * BLK);   // persistent: BLK per CU
         hipLaunchKernelGGL((k_resamp2<L, S>), dim3(nb), dim3(NT), lds2, st, pl, g0, K0, npfb, del, taps2, hist, x,
-                           n, y);
+                           n, y, (int)nout, tin);
         return;
     }
     const long long lanes = (n + RS_R - 1) / RS_R;
@@ -525,7 +584,7 @@ void launch_rs(const lqk_rs_plan &pl, unsigned long long g0, unsigned long long 
 template <typename S>
 void run_rs(const lqk_rs_plan *pl, unsigned long long g0, unsigned long long K0, unsigned int npfb, unsigned int L,
             float del, const void *taps, const void *taps2, const void *hist, const void *x, unsigned long long n,
-            void *y, hipStream_t st)
+            void *y, unsigned long long nout, hipStream_t st)
 {
     const float2 *tp = (const float2 *)taps;
     const S *hs = (const S *)hist, *xi = (const S *)x;
@@ -534,7 +593,7 @@ void run_rs(const lqk_rs_plan *pl, unsigned long long g0, unsigned long long K0,
     const bool lds_ok = (size_t)npfb * L * sizeof(float2) <= 64 * 1024;
 #define LQ_RS_CASE(LL)                                                                                     \
     case LL:                                                                                               \
-        launch_rs<LL, S>(*pl, g0, K0, (int)npfb, del, tp, (const float2 *)taps2, hs, xi, nn, yo, st);     \
+        launch_rs<LL, S>(*pl, g0, K0, (int)npfb, del, tp, (const float2 *)taps2, hs, xi, nn, yo, nout, st); \
         return;
     if (lds_ok && L <= 32 && (L % 2) == 0) {
         switch (L) {
@@ -566,21 +625,17 @@ void run_rs(const lqk_rs_plan *pl, unsigned long long g0, unsigned long long K0,
 
 extern "C" void lqk_resamp(int real_io, const lqk_rs_plan *pl, unsigned long long g0, unsigned long long K0,
                            unsigned int npfb, unsigned int L, float del, const void *taps, const void *taps2,
-                           const void *hist, const void *x, unsigned long long n, void *y, void *stream)
+                           const void *hist, const void *x, unsigned long long n, void *y, unsigned long long nout,
+                           void *stream)
 {
     if (n == 0) return;
-    hipStream_t st = (hipStream_t)stream;
-    // launches of at most 2^27 inputs keep the range-checked byte offsets in
-    // 32 bits; outputs are placed by plan position, so a later launch only
-    // moves g0, x and its history (the L inputs before it)
     const size_t es = real_io ? 4 : 8;
-    const unsigned long long CHN = 1ull << 27;
-    for (unsigned long long o = 0; o < n; o += CHN) {
-        const unsigned long long nn = (n - o) < CHN ? (n - o) : CHN;
-        const char *xo = (const char *)x + o * es;
-        const void *ho = o == 0 ? hist : (const void *)(xo - (size_t)L * es);
-        if (real_io) run_rs<float>(pl, g0 + o, K0, npfb, L, del, taps, taps2, ho, xo, nn, y, st);
-        else run_rs<float2>(pl, g0 + o, K0, npfb, L, del, taps, taps2, ho, xo, nn, y, st);
-        LQ_CHECK_LAUNCH();
+    if (n > LQK_RS_MAXN || nout * es >= (1ull << 31)) {
+        fprintf(stderr, "error: liquid-mi355x: resamp launch of %llu inputs / %llu outputs exceeds one launch\n", n, nout);
+        exit(1);
     }
+    hipStream_t st = (hipStream_t)stream;
+    if (real_io) run_rs<float>(pl, g0, K0, npfb, L, del, taps, taps2, hist, x, n, y, nout, st);
+    else run_rs<float2>(pl, g0, K0, npfb, L, del, taps, taps2, hist, x, n, y, nout, st);
+    LQ_CHECK_LAUNCH();
 }

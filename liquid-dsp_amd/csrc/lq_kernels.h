@@ -186,12 +186,14 @@ typedef struct {
     unsigned long long end;
     int p2;
 } lqk_rs_plan;
-/* n inputs x (plan positions g0 .. g0+n) -> outputs y[K(g) - K0 ...];
+/* n inputs x (plan positions g0 .. g0+n) -> the nout outputs y[K(g) - K0 ...]
+ * (n <= LQK_RS_MAXN, nout * sample size < 2^31);
  * taps: npfb x L pairs (h[b + n*npfb], h[(b+1)%npfb + n*npfb]); hist = last L inputs.
  * real_io: float samples (rrrf), else interleaved complex (crcf, cccf: the taps are real for every type) */
+#define LQK_RS_MAXN (1ull << 27)
 void lqk_resamp(int real_io, const lqk_rs_plan *pl, unsigned long long g0, unsigned long long K0, unsigned int npfb,
                 unsigned int L, float del, const void *taps, const void *taps2, const void *hist, const void *x,
-                unsigned long long n, void *y, void *stream);
+                unsigned long long n, void *y, unsigned long long nout, void *stream);
 /* taps2: (npfb+1) x LP pairs, LP = (L+3) & ~1: row b < npfb (h_b[L-p], h_{b+1}[L-p]) for p = 1..L, row
  * npfb the BOUNDARY pair (h_{npfb-1}[L-1-p], h_0[L-p]); zero elsewhere (NULL: untiled kernel) */
 /* firpfb_execute(i): y = scale * sum_n hpoly[i*L + n] win[L-1-n] (win: L samples, oldest first) */

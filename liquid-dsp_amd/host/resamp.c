@@ -618,13 +618,17 @@ void lq_rs_block_dev(lq_rs *_q, const void *_dxv, unsigned long long _nx, void *
     const char *_dx = (const char *)_dxv;
     char *_dy = (char *)_dyv;
     unsigned long long total = 0;
+    /* launches of at most LQK_RS_MAXN inputs and 2^27 outputs (32-bit
+     * buffer offsets in the kernel) */
+    const double r = _q->rate > 1.0f ? (double)_q->rate : 1.0;
+    const unsigned long long cmax = (unsigned long long)((double)LQK_RS_MAXN / (r + 1.0)) + 1;
     while (_nx > 0) {
-        unsigned long long c = rs_ensure_plan(_q, _nx);
+        unsigned long long c = rs_ensure_plan(_q, _nx < cmax ? _nx : cmax);
         unsigned long long K0 = rs_K(_q, _q->gpos), K1 = rs_K(_q, _q->gpos + c);
         lqk_rs_plan kp = {_q->pl.d_tab.p, _q->pl.pre, _q->pl.P, _q->pl.Q, _q->pl.end, rs_pow2(_q->npfb)};
         void *hold = _q->d_hist[_q->cur], *hnew = _q->d_hist[_q->cur ^ 1];
-        lqk_resamp(_q->kind == LQ_RRRF, &kp, _q->gpos, K0, _q->npfb, _q->L, _q->del, _q->d_taps, _q->d_taps2, hold, _dx, c, _dy,
-                   _q->ctx.stream);
+        lqk_resamp(_q->kind == LQ_RRRF, &kp, _q->gpos, K0, _q->npfb, _q->L, _q->del, _q->d_taps, _q->d_taps2, hold, _dx, c,
+                   _dy, K1 - K0, _q->ctx.stream);
         lqk_window_append(_q->kind != LQ_RRRF, hold, _q->L, _dx, c, hnew, _q->ctx.stream);
         _q->cur ^= 1;
         _q->gpos += c;

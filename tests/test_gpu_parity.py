@@ -357,6 +357,22 @@ def test_firpfbch2_analyzer_polyphase_pass_vs_oracle(M, m):
     assert G.nrm_err(y, o.execute_block(x)) < NRM
 
 
+@pytest.mark.parametrize("M,m", [(64, 1), (64, 2), (64, 3), (64, 4), (128, 2), (128, 4)])
+def test_firpfbch2_analyzer_small_fused_vs_oracle(M, m):
+    # M = 64 / 128 with m <= 4: the fused kernel (k_pfb2_an_small, several
+    # column sets per workgroup, each on its own run of rows); enough blocks
+    # for many workgroups and a ragged last run, calls on both block parities
+    r = rng(11 * M + m)
+    nblocks = (1 << 20) // M + 37
+    x = cx(r, nblocks * M // 2)
+    g = LQ.FirPfbch2(LQ.LIQUID_ANALYZER, M, m, 60.0)
+    o = O.FirPfbch2(O.ANALYZER, M, m, 60.0)
+    cuts = [0, 3, 4, 1001, nblocks - 5, nblocks]
+    step = M // 2
+    y = np.concatenate([g.execute_block(x[a * step:b * step]) for a, b in zip(cuts[:-1], cuts[1:])])
+    assert G.nrm_err(y, o.execute_block(x)) < NRM
+
+
 def test_firpfbch2_analyzer_polyphase_chunks_vs_oracle():
     # a call longer than one polyphase chunk (2^27 / M blocks): the second
     # chunk takes its history from the input before it; odd start parity
