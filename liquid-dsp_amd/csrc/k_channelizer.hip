@@ -845,6 +845,102 @@ bool launch_pfb_an_fused(int M, int p, const void *hsub, const void *hist, const
     return false;
 }
 
+// firpfbch analyzer, M = 64 / 128, fused as k_pfb_an_fused with Q = 256 / M
+// column sets per workgroup (each on its own run of blocks; every set runs
+// the same number of 16-block groups, stores past its run dropped) and the
+// 16 Q forward M-point transforms of a group on R = M / 16 lanes each
+// (fft_small16xR)
+template <int P, typename TC, int MS>
+__global__ __launch_bounds__(256, 2) void k_pfb_an_small(const TC *__restrict__ hsub, const float2 *__restrict__ hist,
+                                                        const float2 *__restrict__ x, int n_in, int nb, int S,
+                                                        float2 *__restrict__ Y, const float2 *__restrict__ tw4096)
+{
+    constexpr int M = MS, HL = (P - 1) * M, NS = 16, Q = 256 / M, R = M / 16, PS = FFTS_LDS<R>();
+    __shared__ __attribute__((aligned(16))) float2 xr[Q * NS * M];
+    __shared__ __attribute__((aligned(16))) float2 scr[16 * Q * PS];
+    const int set = threadIdx.x / M, j = threadIdx.x % M;
+    float2 *xs = xr + set * (NS * M);
+    TC h[P];
+#pragma unroll
+    for (int n = 0; n < P; n++) h[n] = hsub[(M - 1 - j) * P + n];
+    const __amdgpu_buffer_rsrc_t ry = __builtin_amdgcn_make_buffer_rsrc((void *)Y, (short)0, nb * M * 8, 0x00020000);
+    const float2 *zero = tw4096 + LQ_TW_N;   // lqrt_zeros(): the table's zero tail
+    auto row_sample = [&](int b) -> float2 {
+        const int t = b * M + j;
+        return lq_load_hx(hist + HL, x, zero, t, HL, n_in);
+    };
+    const int tg = threadIdx.x / R, t = threadIdx.x % R;   // transform tg: set tg / 16, block tg % 16
+    const int tset = tg / 16, tb16 = tg % 16;
+    const int e = t * (4096 / M);
+    const float2 a1 = tw4096[e & 4095], a4 = tw4096[(4 * e) & 4095];
+    typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
+    const int cs = ((int)blockIdx.x * Q + set) * S;
+    const int tcs = ((int)blockIdx.x * Q + tset) * S;
+    const int tce = tcs + S < nb ? tcs + S : nb;
+    float2 w[NS], pf[NS];
+#pragma unroll
+    for (int u = 0; u < NS; u++) w[u] = row_sample(cs - NS + u);
+#pragma unroll
+    for (int u = 0; u < NS; u++) pf[u] = row_sample(cs + u);
+    for (int g0 = 0; g0 < S; g0 += NS) {
+        const int r0 = cs + g0;
+#pragma unroll
+        for (int u = 0; u < NS; u++) {
+            w[u] = pf[u];
+            pf[u] = row_sample(r0 + NS + u);
+            float2 acc = make_float2(0.f, 0.f);
+#pragma unroll
+            for (int n = 0; n < P; n++) acc = pfb_mac(h[n], w[(u - n) & (NS - 1)], acc);
+            xs[u * M + j] = acc;
+        }
+        __syncthreads();
+        float2 v[16];
+        const float2 *B = xr + tset * (NS * M) + tb16 * M;
+#pragma unroll
+        for (int n = 0; n < 16; n++) v[n] = B[t + R * n];
+        fft_small16xR<R, +1>(v, scr + tg * PS, a1, a4, t);   // (its barriers also free xr)
+        const int b = tcs + g0 + tb16;
+        const unsigned base = b < tce ? (unsigned)b * (unsigned)(M * 8) : 0xFFFFF000u;
+        // v[u R + q] = X[t (16/R) + u + 16 q]
+#pragma unroll
+        for (int u = 0; u < 16 / R; u++)
+#pragma unroll
+            for (int q = 0; q < R; q++)
+                __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2, v[u * R + q]), ry,
+                                                      base + (unsigned)(t * (16 / R) + u + 16 * q) * 8u, 0, 0);
+    }
+}
+
+template <typename TC>
+bool launch_pfb_an_small(int M, int p, const void *hsub, const void *hist, const void *x, long long nb, void *Y,
+                         hipStream_t st)
+{
+    if ((M != 64 && M != 128) || nb * (long long)M * 8 >= (1ll << 31)) return false;
+    const int Q = 256 / M;
+    long long S = (nb + 2047) / 2048;
+    S = (S + 15) / 16 * 16;
+    if (S < 32) S = 32;
+    const long long nseg = (nb + S - 1) / S;
+    const unsigned grid = (unsigned)((nseg + Q - 1) / Q);
+#define LQ_PF(PP)                                                                                          \
+    case PP:                                                                                               \
+        if (M == 64)                                                                                       \
+            hipLaunchKernelGGL((k_pfb_an_small<PP, TC, 64>), dim3(grid), dim3(256), 0, st, (const TC *)hsub, \
+                               (const float2 *)hist, (const float2 *)x, (int)(nb * M), (int)nb, (int)S,   \
+                               (float2 *)Y, (const float2 *)lqrt_twiddles());                             \
+        else                                                                                               \
+            hipLaunchKernelGGL((k_pfb_an_small<PP, TC, 128>), dim3(grid), dim3(256), 0, st, (const TC *)hsub, \
+                               (const float2 *)hist, (const float2 *)x, (int)(nb * M), (int)nb, (int)S,   \
+                               (float2 *)Y, (const float2 *)lqrt_twiddles());                             \
+        LQ_CHECK_LAUNCH();                                                                                 \
+        return true;
+    switch (p) {
+        LQ_PF(2) LQ_PF(4) LQ_PF(6) LQ_PF(8) LQ_PF(10) LQ_PF(12) LQ_PF(14) LQ_PF(16)
+    }
+#undef LQ_PF
+    return false;
+}
+
 // firpfbch synthesizer, M = 256 R, fused: per group of 16 blocks, 16
 // inverse register transforms of X (z_b = IFFT(X_b)) into LDS, then a lane
 // per column i runs y_b[i] = sum_n h[i p + n] z_{b-n}[i] from a 16-deep
@@ -1497,6 +1593,10 @@ extern "C" void lqk_firpfbch_analyzer(int ctaps, unsigned int M, unsigned int p,
     if (!getenv("LQ_PFB_TWO_PASS") &&
         (ctaps ? launch_pfb_an_fused<float2>((int)M, (int)p, hsub, hist, x, (long long)nblocks, Y, st)
                : launch_pfb_an_fused<float>((int)M, (int)p, hsub, hist, x, (long long)nblocks, Y, st)))
+        return;
+    if (!getenv("LQ_PFB_TWO_PASS") &&
+        (ctaps ? launch_pfb_an_small<float2>((int)M, (int)p, hsub, hist, x, (long long)nblocks, Y, st)
+               : launch_pfb_an_small<float>((int)M, (int)p, hsub, hist, x, (long long)nblocks, Y, st)))
         return;
     const long long tot = (long long)nblocks * M;
     const dim3 grid((unsigned)((tot + 255) / 256));

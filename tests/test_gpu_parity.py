@@ -500,6 +500,38 @@ def test_firpfbch_m256_512_long_stream(typ, M, m):
     assert G.nrm_err(y, ref) < NRM
 
 
+@pytest.mark.parametrize("M,m", [(64, 1), (64, 4), (128, 3), (128, 8)])
+def test_firpfbch_analyzer_small_m_long_stream(M, m):
+    # the fused M = 64 / 128 analyzer (k_pfb_an_small: several column sets per
+    # workgroup, each on its own run of blocks) over thousands of blocks in
+    # ragged calls
+    r = rng(5 * M + m)
+    nb = (1 << 20) // M + 21
+    x = cx(r, nb * M)
+    g = LQ.FirPfbch(LQ.LIQUID_ANALYZER, M, m=m, As=60.0)
+    o = O.FirPfbch(O.ANALYZER, M, m=m, As=60.0)
+    cuts = [0, 1, 779, nb - 3, nb]
+    y = np.concatenate([g.execute_block(x[a * M:b * M]) for a, b in zip(cuts[:-1], cuts[1:])])
+    ref = o.execute_block(x) if hasattr(o, "execute_block") else \
+        np.concatenate([o.execute(x[b * M:(b + 1) * M]) for b in range(nb)])
+    assert G.nrm_err(y, ref) < NRM
+
+
+def test_firpfbch_analyzer_small_m_complex_taps():
+    M, p = 64, 6
+    r = rng(4242)
+    h = cx(r, M * p)
+    nb = 4000
+    x = cx(r, nb * M)
+    g = LQ.FirPfbch(LQ.LIQUID_ANALYZER, M, p=p, h=h, t="cccf")
+    o_re = O.FirPfbch(O.ANALYZER, M, p=p, h=h.real.copy())
+    o_im = O.FirPfbch(O.ANALYZER, M, p=p, h=h.imag.copy())
+    y = np.concatenate([g.execute(x[:M]), g.execute_block(x[M:])])
+    ref = np.concatenate([o_re.execute(x[b * M:(b + 1) * M]).astype(np.complex128)
+                          + 1j * o_im.execute(x[b * M:(b + 1) * M]) for b in range(nb)])
+    assert G.nrm_err(y, ref) < NRM
+
+
 @pytest.mark.parametrize("typ", [LQ.LIQUID_ANALYZER, LQ.LIQUID_SYNTHESIZER])
 def test_firpfbch_cccf_m256_complex_taps(typ):
     M, p = 256, 6

@@ -99,7 +99,7 @@ def main():
     n = 1 << 27
     x = cbuf(n)
     y = torch.empty(4 * n, device="cuda")
-    for M in (64, 256, 512, 1024, 2048, 4096):
+    for M in (64, 128, 256, 512, 1024, 2048, 4096):
         a2 = LQ.FirPfbch2(LQ.LIQUID_ANALYZER, M, 4, 60.0)
         a2.set_stream(S)
         nb = n // (M // 2)
@@ -118,7 +118,7 @@ def main():
     report("firpfbch2_crcf synthesizer M=1024 m=4", ms, nb * M // 2, "output samples", 12 * nb * M,
            "8 B/channel sample in + 8 B/output (M/2 per block)")
     for typ, nm in ((LQ.LIQUID_ANALYZER, "analyzer"), (LQ.LIQUID_SYNTHESIZER, "synthesizer")):
-        for Mc in (256, 1024, 4096):
+        for Mc in (64, 256, 1024, 4096):
             nbc = nb * M // Mc
             p = LQ.FirPfbch(typ, Mc, m=4, As=60.0)
             p.set_stream(S)
