@@ -1040,6 +1040,99 @@ bool launch_pfb_syn_fused(int M, int p, const void *hsub, const void *state, con
     return false;
 }
 
+// firpfbch synthesizer, M = 64 / 128, fused as k_pfb_syn_fused with Q = 256
+// / M column sets per workgroup on their own runs of blocks, the 16 Q inverse
+// transforms of a group on M / 16 lanes each (fft_small16xR).  Every set runs
+// the same groups g0 = -16, 0, 16, .. < S relative to its run: the first is
+// the warm-up (blocks before the run transformed again, or for the call's
+// first run the object's last p-1 transforms, zeros before them).
+template <int P, typename TC, int MS>
+__global__ __launch_bounds__(256, 2) void k_pfb_syn_small(const TC *__restrict__ hsub,
+                                                         const float2 *__restrict__ state,
+                                                         const float2 *__restrict__ X, int nb, int S,
+                                                         float2 *__restrict__ y, float2 *__restrict__ znew,
+                                                         const float2 *__restrict__ tw4096)
+{
+    constexpr int M = MS, HB = P - 1, NS = 16, Q = 256 / M, R = M / 16, PS = FFTS_LDS<R>();
+    __shared__ __attribute__((aligned(16))) float2 zr[Q * NS * M];
+    __shared__ __attribute__((aligned(16))) float2 scr[16 * Q * PS];
+    const int set = threadIdx.x / M, i = threadIdx.x % M;
+    TC h[P];
+#pragma unroll
+    for (int n = 0; n < P; n++) h[n] = hsub[i * P + n];
+    const int tg = threadIdx.x / R, t = threadIdx.x % R;   // transform tg: set tg / 16, block tg % 16
+    const int tset = tg / 16, tb16 = tg % 16;
+    const int e = t * (4096 / M);
+    const float2 a1 = tw4096[e & 4095], a4 = tw4096[(4 * e) & 4095];
+    const int cs = ((int)blockIdx.x * Q + set) * S;
+    const int ce = cs + S < nb ? cs + S : nb;
+    const int tcs = ((int)blockIdx.x * Q + tset) * S;
+    const int tce = tcs + S < nb ? tcs + S : nb;
+    float2 w[NS];
+    for (int g0 = -NS; g0 < S; g0 += NS) {
+        {
+            const int b = tcs + g0 + tb16;
+            float2 v[16];
+            const float2 *xb = X + (long long)(b < 0 ? 0 : (b < nb ? b : nb - 1)) * M;
+#pragma unroll
+            for (int n = 0; n < 16; n++) v[n] = xb[t + R * n];
+            fft_small16xR<R, -1>(v, scr + tg * PS, a1, a4, t);
+            float2 *zb = zr + tset * (NS * M) + tb16 * M;
+#pragma unroll
+            for (int u = 0; u < 16 / R; u++)
+#pragma unroll
+                for (int q = 0; q < R; q++) {
+                    const int k = t * (16 / R) + u + 16 * q;
+                    float2 z = v[u * R + q];
+                    if (b < 0) z = (b >= -HB) ? state[(HB + b) * M + k] : make_float2(0.f, 0.f);
+                    zb[k] = z;
+                    if (b >= nb - HB && b < nb && b >= tcs && b < tce) znew[(b - (nb - HB)) * M + k] = z;
+                }
+        }
+        __syncthreads();
+#pragma unroll
+        for (int u = 0; u < NS; u++) {
+            w[u] = zr[set * (NS * M) + u * M + i];
+            const int b = cs + g0 + u;
+            float2 acc = make_float2(0.f, 0.f);
+#pragma unroll
+            for (int n = 0; n < P; n++) acc = pfb_mac(h[n], w[(u - n) & (NS - 1)], acc);
+            if (b >= cs && b < ce) y[(long long)b * M + i] = acc;
+        }
+        __syncthreads();   // zr is rewritten by the next group's transforms
+    }
+}
+
+template <typename TC>
+bool launch_pfb_syn_small(int M, int p, const void *hsub, const void *state, const void *X, long long nb, void *y,
+                          void *znew, hipStream_t st)
+{
+    if ((M != 64 && M != 128) || p > 16 || nb < p || nb * (long long)M >= (1ll << 31)) return false;
+    const int Q = 256 / M;
+    long long S = (nb + 2047) / 2048;
+    S = (S + 15) / 16 * 16;
+    if (S < 64) S = 64;
+    const long long nseg = (nb + S - 1) / S;
+    const unsigned grid = (unsigned)((nseg + Q - 1) / Q);
+#define LQ_SF(PP)                                                                                          \
+    case PP:                                                                                               \
+        if (M == 64)                                                                                       \
+            hipLaunchKernelGGL((k_pfb_syn_small<PP, TC, 64>), dim3(grid), dim3(256), 0, st, (const TC *)hsub, \
+                               (const float2 *)state, (const float2 *)X, (int)nb, (int)S, (float2 *)y,     \
+                               (float2 *)znew, (const float2 *)lqrt_twiddles());                          \
+        else                                                                                               \
+            hipLaunchKernelGGL((k_pfb_syn_small<PP, TC, 128>), dim3(grid), dim3(256), 0, st, (const TC *)hsub, \
+                               (const float2 *)state, (const float2 *)X, (int)nb, (int)S, (float2 *)y,     \
+                               (float2 *)znew, (const float2 *)lqrt_twiddles());                          \
+        LQ_CHECK_LAUNCH();                                                                                 \
+        return true;
+    switch (p) {
+        LQ_SF(2) LQ_SF(4) LQ_SF(6) LQ_SF(8) LQ_SF(10) LQ_SF(12) LQ_SF(14) LQ_SF(16)
+    }
+#undef LQ_SF
+    return false;
+}
+
 // firpfbch2 synthesizer, M = 256 R, m <= 4, fused the same way: 16 inverse
 // transforms per group (scaled 1/M then M/2, as firpfbch2.c:303-307) into
 // LDS, then lane i < M/2 keeps 16-deep rings of columns i and i + M/2 and
@@ -1628,6 +1721,12 @@ extern "C" void lqk_firpfbch_synthesizer(int ctaps, unsigned int M, unsigned int
     if (!getenv("LQ_PFB_TWO_PASS") &&
         (ctaps ? launch_pfb_syn_fused<float2>((int)M, (int)p, hsub, state, X, (long long)nblocks, y, Z, st)
                : launch_pfb_syn_fused<float>((int)M, (int)p, hsub, state, X, (long long)nblocks, y, Z, st))) {
+        if (HB > 0) LQ_CHECK(hipMemcpyAsync(state, Z, HB * M * sizeof(float2), hipMemcpyDeviceToDevice, st));
+        return;
+    }
+    if (!getenv("LQ_PFB_TWO_PASS") &&
+        (ctaps ? launch_pfb_syn_small<float2>((int)M, (int)p, hsub, state, X, (long long)nblocks, y, Z, st)
+               : launch_pfb_syn_small<float>((int)M, (int)p, hsub, state, X, (long long)nblocks, y, Z, st))) {
         if (HB > 0) LQ_CHECK(hipMemcpyAsync(state, Z, HB * M * sizeof(float2), hipMemcpyDeviceToDevice, st));
         return;
     }

@@ -517,6 +517,23 @@ def test_firpfbch_analyzer_small_m_long_stream(M, m):
     assert G.nrm_err(y, ref) < NRM
 
 
+@pytest.mark.parametrize("M,m", [(64, 1), (64, 4), (128, 3), (128, 8)])
+def test_firpfbch_synthesizer_small_m_long_stream(M, m):
+    # the fused M = 64 / 128 synthesizer (k_pfb_syn_small): runs of blocks per
+    # column set, warm-up on the blocks before a run or on the object's state;
+    # ragged calls (short ones take the two-pass path) carry the state across
+    r = rng(9 * M + m)
+    nb = (1 << 20) // M + 21
+    x = cx(r, nb * M)
+    g = LQ.FirPfbch(LQ.LIQUID_SYNTHESIZER, M, m=m, As=60.0)
+    o = O.FirPfbch(O.SYNTHESIZER, M, m=m, As=60.0)
+    cuts = [0, 1, 779, nb - 3, nb]
+    y = np.concatenate([g.execute_block(x[a * M:b * M]) for a, b in zip(cuts[:-1], cuts[1:])])
+    ref = o.execute_block(x) if hasattr(o, "execute_block") else \
+        np.concatenate([o.execute(x[b * M:(b + 1) * M]) for b in range(nb)])
+    assert G.nrm_err(y, ref) < NRM
+
+
 def test_firpfbch_analyzer_small_m_complex_taps():
     M, p = 64, 6
     r = rng(4242)
