@@ -74,8 +74,18 @@ constexpr int SSTR = 68;          // floats per staged segment (32 x re/im + pad
 // crcf: one staged accumulator per wave (49664 B: three workgroups per CU;
 // KB = 2: 53504 B and 219 VGPRs, two per CU); cccf: two (the real- and
 // imaginary-tap products; 67072 B: two per CU)
+// KB > 2 (129..256 taps, crcf): the A fragments (3 terms x 2 + 4 KB steps,
+// 216 VGPRs at KB = 4) come from LDS instead: the band H[i][j] = h[i + 64 KB -
+// j] is Toeplitz, so lane row i's fragment of step s is 8 consecutive entries
+// of g[k] = h[64 KB + 31 - k] from k = 31 - i + 16 s + 8 hh; eight copies of
+// each term's g shifted by c = (31 - i) mod 8 make every fragment one aligned
+// 16-byte read
+template <int KB>
+constexpr int glen_kb() { return 16 * (2 + 4 * KB) + 32; }
+template <int KB>
+constexpr int acp_bytes() { return KB > 2 ? 8 * 3 * glen_kb<KB>() * 2 : 0; }
 template <bool CC, int KB = 1>
-constexpr int lds_bytes_mx() { return 6 * plb_kb<KB>() + (CC ? 2 : 1) * 4 * 16 * SSTR * 4; }
+constexpr int lds_bytes_mx() { return 6 * plb_kb<KB>() + (CC ? 2 : 1) * 4 * 16 * SSTR * 4 + acp_bytes<KB>(); }
 
 __device__ __forceinline__ int poff(int pos) { return 2 * pos + 16 * (pos >> 5); }
 
@@ -187,7 +197,7 @@ __device__ __forceinline__ void load8b(__amdgpu_buffer_rsrc_t rx, unsigned off, 
 // accumulators, C1 = Hr [Xr | Xi] and C2 = Hi [Xr | Xi]; y = (C1.re - C2.im,
 // C1.im + C2.re) is formed when the staged accumulators are read back.
 template <bool CC, int KB>
-__global__ __launch_bounds__(NT, (CC || KB > 1) ? 2 : 3) void k_firfilt_mx(const v2f *__restrict__ win,
+__global__ __launch_bounds__(NT, KB > 2 ? 2 : ((CC || KB > 1) ? 2 : 3)) void k_firfilt_mx(const v2f *__restrict__ win,
                                                               const v2f *__restrict__ x, long long n,
                                                               v2f *__restrict__ y, const float *__restrict__ hpad,
                                                               float sre, float sim, long long nch, int hlen)
@@ -205,7 +215,23 @@ __global__ __launch_bounds__(NT, (CC || KB > 1) ? 2 : 3) void k_firfilt_mx(const
 
     // A fragments: lane (row i = r32, k half hh) holds H[i][16s + 8hh + e]
     // (cccf: hpad holds (re, im) pairs; matrix a takes component a)
-    bf16x8 A[NA][3][NS];
+    constexpr bool AL = KB > 2;   // fragments read from LDS per step
+    bf16x8 A[NA][3][AL ? 1 : NS];
+    __bf16 *acp = reinterpret_cast<__bf16 *>(smem + 6 * PLB + NA * 4 * 16 * SSTR * 4);
+    constexpr int GL = glen_kb<KB>();
+    if constexpr (AL) {
+        // copy c, term p: G[c][p][k] = term p of g[k + c], g[k] = h[HALO + 31 - k]
+        for (int e = tid; e < 8 * GL; e += NT) {
+            const int c = e / GL, k = e - c * GL;
+            const int hk = HALO + 31 - (k + c);
+            const float hv = (hk >= 0 && hk < HALO) ? hpad[hk] : 0.f;
+            bf16x2 t1, t2, t3;
+            split3(v2f{hv, 0.f}, t1, t2, t3);
+            acp[(c * 3 + 0) * GL + k] = t1.x;
+            acp[(c * 3 + 1) * GL + k] = t2.x;
+            acp[(c * 3 + 2) * GL + k] = t3.x;
+        }
+    } else {
 #pragma unroll
     for (int a = 0; a < NA; a++)
 #pragma unroll
@@ -223,9 +249,12 @@ __global__ __launch_bounds__(NT, (CC || KB > 1) ? 2 : 3) void k_firfilt_mx(const
             }
 #pragma unroll
             for (int p = 0; p < 3; p++)
-                A[a][p][s] =
+                A[a][p][AL ? 0 : s] =
                     bf16x8{t[p][0].x, t[p][0].y, t[p][1].x, t[p][1].y, t[p][2].x, t[p][2].y, t[p][3].x, t[p][3].y};
         }
+    }
+    // this lane's copy (31 - r32) mod 8 and its fragment base (+ 16 s: step s; + p GL: term p)
+    const __bf16 *acl = AL ? acp + ((31 - r32) & 7) * 3 * GL + ((31 - r32) & ~7) + 8 * hh : nullptr;
 
     // Chunks are dealt grid-stride (workgroup w takes chunks w, w + G, ...):
     // the chip then streams one contiguous window of the input at a time.
@@ -312,18 +341,30 @@ __global__ __launch_bounds__(NT, (CC || KB > 1) ? 2 : 3) void k_firfilt_mx(const
 #if FMX_VARIANT & 1   // timing experiment: no MFMA (wrong results)
 #pragma unroll
             for (int a = 0; a < NA; a++) {
-                C[a][s] += (float)b0[0] + (float)b1[1] + (float)b2[2] + (float)A[a][0][s][0];
+                C[a][s] += (float)b0[0] + (float)b1[1] + (float)b2[2] + (float)A[a][0][AL ? 0 : s][0];
             }
             continue;
 #endif
+            if constexpr (AL) {
+                const bf16x8 a0 = *reinterpret_cast<const bf16x8 *>(acl + 16 * s);
+                const bf16x8 a1 = *reinterpret_cast<const bf16x8 *>(acl + GL + 16 * s);
+                const bf16x8 a2 = *reinterpret_cast<const bf16x8 *>(acl + 2 * GL + 16 * s);
+                C[0] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a0, b2, C[0], 0, 0, 0);
+                C[0] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a1, b1, C[0], 0, 0, 0);
+                C[0] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a2, b0, C[0], 0, 0, 0);
+                C[0] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a0, b1, C[0], 0, 0, 0);
+                C[0] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a1, b0, C[0], 0, 0, 0);
+                C[0] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a0, b0, C[0], 0, 0, 0);
+                continue;
+            }
 #pragma unroll
             for (int a = 0; a < NA; a++) {
-                C[a] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(A[a][0][s], b2, C[a], 0, 0, 0);
-                C[a] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(A[a][1][s], b1, C[a], 0, 0, 0);
-                C[a] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(A[a][2][s], b0, C[a], 0, 0, 0);
-                C[a] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(A[a][0][s], b1, C[a], 0, 0, 0);
-                C[a] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(A[a][1][s], b0, C[a], 0, 0, 0);
-                C[a] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(A[a][0][s], b0, C[a], 0, 0, 0);
+                C[a] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(A[a][0][AL ? 0 : s], b2, C[a], 0, 0, 0);
+                C[a] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(A[a][1][AL ? 0 : s], b1, C[a], 0, 0, 0);
+                C[a] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(A[a][2][AL ? 0 : s], b0, C[a], 0, 0, 0);
+                C[a] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(A[a][0][AL ? 0 : s], b1, C[a], 0, 0, 0);
+                C[a] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(A[a][1][AL ? 0 : s], b0, C[a], 0, 0, 0);
+                C[a] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(A[a][0][AL ? 0 : s], b0, C[a], 0, 0, 0);
             }
         }
 
@@ -589,11 +630,22 @@ static void launch_mx(const lqk_fir_desc *d, const void *hist, const void *x, lo
     }
     const bool cc = d->kind == 2;
     const bool kb2 = d->nchunk == 2;   // crcf, 65..128 taps
+    const int kb = (int)d->nchunk;     // crcf: 129..192 / 193..256 taps with the A fragments in LDS
     const long long nch = (n + CH - 1) / CH;
     const long long wgs = (cc || kb2) ? 512 : 768;   // resident workgroups (two / three per CU)
     const dim3 grid((unsigned)(nch < wgs ? nch : wgs));
     constexpr int lds_kb2 = lds_bytes_mx<false, 2>() + 80;
-    if (kb2)
+    if (!cc && kb > 2) {
+        const dim3 g2((unsigned)(nch < 512 ? nch : 512));
+        if (kb == 3)
+            hipLaunchKernelGGL((k_firfilt_mx<false, 3>), g2, dim3(NT), (lds_bytes_mx<false, 3>() + 80), st,
+                               (const v2f *)hist, (const v2f *)x, n, (v2f *)y, (const float *)d->hpad, d->scale_re,
+                               d->scale_im, nch, (int)d->hlen);
+        else
+            hipLaunchKernelGGL((k_firfilt_mx<false, 4>), g2, dim3(NT), (lds_bytes_mx<false, 4>() + 80), st,
+                               (const v2f *)hist, (const v2f *)x, n, (v2f *)y, (const float *)d->hpad, d->scale_re,
+                               d->scale_im, nch, (int)d->hlen);
+    } else if (kb2)
         hipLaunchKernelGGL((k_firfilt_mx<false, 2>), grid, dim3(NT), lds_kb2, st,
                            (const v2f *)hist, (const v2f *)x, n, (v2f *)y, (const float *)d->hpad, d->scale_re,
                            d->scale_im, nch, (int)d->hlen);
@@ -615,7 +667,7 @@ extern "C" int lqk_firfilt_mx(const lqk_fir_desc *d, const void *hist, const voi
                               void *y, void *stream)
 {
     // 33..64 taps (one 64-tap block) for every type; 65..128 (two) for crcf
-    if (d->hc != 64 || !(d->nchunk == 1 || (d->nchunk == 2 && d->kind == 1)) || x == y || !d->mx_ok) return 0;
+    if (d->hc != 64 || !(d->nchunk == 1 || (d->nchunk <= 4 && d->kind == 1)) || x == y || !d->mx_ok) return 0;
     if (((uintptr_t)x & 15) || ((uintptr_t)y & 15)) return 0;
     if (n == 0) return 1;
     const size_t es = d->kind == 0 ? 4 : 8;

@@ -62,7 +62,7 @@ def _run(t, h, x, dev):
 
 
 @pytest.mark.parametrize("t", ["rrrf", "crcf", "cccf"])
-@pytest.mark.parametrize("h_len", [64, 45, 20, 100])
+@pytest.mark.parametrize("h_len", [64, 45, 20, 100, 200])
 @pytest.mark.parametrize("e", [-120, -60, -40, 40, 60, 120])
 def test_firfilt_input_scale_sweep(t, h_len, e):
     h, x = _data(t, 50001, h_len, 7 + h_len, 2.0 ** e)
@@ -71,7 +71,7 @@ def test_firfilt_input_scale_sweep(t, h_len, e):
 
 
 @pytest.mark.parametrize("t", ["rrrf", "crcf", "cccf"])
-@pytest.mark.parametrize("h_len", [64, 45, 20, 100])
+@pytest.mark.parametrize("h_len", [64, 45, 20, 100, 200])
 def test_firfilt_nonfinite_samples(t, h_len):
     h, x = _data(t, 70001, h_len, 11 + h_len, 1.0)
     # isolated +Inf, -Inf and NaN, one in the first chunk's halo region, one

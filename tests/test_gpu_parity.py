@@ -174,10 +174,11 @@ def test_firfilt_device_path_in_place():
 
 
 @pytest.mark.parametrize("t", ["rrrf", "crcf", "cccf"])
-@pytest.mark.parametrize("hlen", [33, 45, 64, 65, 100, 128])
+@pytest.mark.parametrize("hlen", [33, 45, 64, 65, 100, 128, 129, 192, 193, 256])
 def test_firfilt_crcf_matrix_core_path_long_stream(t, hlen):
-    # h in 33..64 (every type) and 65..128 (crcf: two 64-tap blocks, a
-    # 128-sample halo), device pointers, not in place: the MFMA kernel
+    # h in 33..64 (every type), 65..128 (crcf: two 64-tap blocks, a
+    # 128-sample halo) and 129..256 (crcf: three / four blocks, the A
+    # fragments read from LDS), device pointers, not in place: the MFMA kernel
     # (k_firfilt_mx.hip; rrrf / cccf past 64 taps: the VALU kernel).  Several 2048-output chunks per workgroup, a ragged
     # tail, a second call continuing the stream, and a complex scale.  Held to
     # the oracle at the usual bound and to a float64 convolution at 2e-6 (the
