@@ -308,23 +308,24 @@ __global__ __launch_bounds__(NT, KB > 2 ? 2 : ((CC || KB > 1) ? 2 : 3)) void k_f
     const int sg = r32 & 15, comp = r32 >> 4;
     auto step = [&](long long k, v4f (&xv)[4], v2f &hv) {
         const long long c = w + k * G;
-        __syncthreads();   // the previous chunk's MFMA reads are done
+        if (!(FMX_VARIANT & 32)) __syncthreads();   // the previous chunk's MFMA reads are done (32: experiment)
         const int cs = (int)(k % 3);
         // chunk 0's halo planes came from the history in the prologue
-        if (tid < HALO && c != 0) {
+        if (!(FMX_VARIANT & 8) && tid < HALO && c != 0) {   // 8: timing experiment, no halo
             put1(planes, PLB, tid, hv);
-            if (unsafe_bits(hv.x) | unsafe_bits(hv.y)) atomicOr(&sbad[cs], 1u);
+            if (!(FMX_VARIANT & 16) && (unsafe_bits(hv.x) | unsafe_bits(hv.y))) atomicOr(&sbad[cs], 1u);
         }
 #if FMX_VARIANT & 2   // timing experiment: no plane writes (wrong results)
         if (__float_as_uint(xv[0].x + xv[1].y + xv[2].z + xv[3].w) == 0x7fc00001u) put8(planes, PLB, HALO + 8 * tid, xv);
 #else
         put8(planes, PLB, HALO + 8 * tid, xv);
 #endif
-        if (unsafe4(xv[0]) | unsafe4(xv[1]) | unsafe4(xv[2]) | unsafe4(xv[3])) atomicOr(&sbad[cs], 1u);
+        if (!(FMX_VARIANT & 16) && (unsafe4(xv[0]) | unsafe4(xv[1]) | unsafe4(xv[2]) | unsafe4(xv[3])))
+            atomicOr(&sbad[cs], 1u);   // 16: timing experiment, no range guard
         if (tid == 0) sbad[(cs + 1) % 3] = 0u;   // step k+1's slot (last read in step k-2)
         load8b(rx, main_off(k + 2), xv);
-        hv = ldh(halo_off(k + 2));
-        __syncthreads();
+        if (!(FMX_VARIANT & 8)) hv = ldh(halo_off(k + 2));
+        if (!(FMX_VARIANT & 32)) __syncthreads();
         if (tid == 0 && sbad[cs] && c < nch) bad_mask[k >> 5] |= 1u << (k & 31);
 
         f32x16 C[NA];
@@ -368,6 +369,17 @@ __global__ __launch_bounds__(NT, KB > 2 ? 2 : ((CC || KB > 1) ? 2 : 3)) void k_f
             }
         }
 
+#if FMX_VARIANT & 4   // timing experiment: accumulators stored as they are, no staging (wrong layout)
+        if constexpr (!CC) {
+            const unsigned o0x = (unsigned)(CH * c + 512 * wave) * 8u;
+#pragma unroll
+            for (int q = 0; q < 4; q++)
+                __builtin_amdgcn_raw_buffer_store_b128(v4f{C[0][4 * q], C[0][4 * q + 1], C[0][4 * q + 2], C[0][4 * q + 3]},
+                                                       ry, c < nch ? o0x + 16u * (lane + 64 * q) : OOB, 0,
+                                                       (FMX_VARIANT & 64) ? 0 : 2);
+            return;
+        }
+#endif
         // accumulator (col r32, row (r&3) + 8(r>>2) + 4hh) -> stage[a][sg][i][comp]
 #pragma unroll
         for (int a = 0; a < NA; a++)
@@ -391,7 +403,7 @@ __global__ __launch_bounds__(NT, KB > 2 ? 2 : ((CC || KB > 1) ? 2 : 3)) void k_f
             const v4f r = CC ? v4f{a.x * sre - a.y * sim, a.x * sim + a.y * sre, a.z * sre - a.w * sim,
                                    a.z * sim + a.w * sre}
                              : a * sre;   // crcf: real scale per component (firfilt.c:337)
-            __builtin_amdgcn_raw_buffer_store_b128(r, ry, c < nch ? o0 + 8u * o : OOB, 0, 2);
+            __builtin_amdgcn_raw_buffer_store_b128(r, ry, c < nch ? o0 + 8u * o : OOB, 0, (FMX_VARIANT & 64) ? 0 : 2);
         }
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
         __builtin_amdgcn_wave_barrier();
@@ -555,7 +567,8 @@ __global__ __launch_bounds__(NT, 3) void k_firfilt_mx_r(const float *__restrict_
         }
         put8r(planes, PLBR, 64 + 16 * tid, xv[0], xv[1]);
         put8r(planes, PLBR, 64 + 16 * tid + 8, xv[2], xv[3]);
-        if (unsafe4(xv[0]) | unsafe4(xv[1]) | unsafe4(xv[2]) | unsafe4(xv[3])) atomicOr(&sbad[cs], 1u);
+        if (!(FMX_VARIANT & 16) && (unsafe4(xv[0]) | unsafe4(xv[1]) | unsafe4(xv[2]) | unsafe4(xv[3])))
+            atomicOr(&sbad[cs], 1u);   // 16: timing experiment, no range guard
         if (tid == 0) sbad[(cs + 1) % 3] = 0u;
         load16rb(rx, main_off(k + 2), xv);
         hv = __builtin_amdgcn_raw_buffer_load_b128(rx, halo_off(k + 2), 0, 0);
