@@ -120,8 +120,14 @@ __global__ __launch_bounds__(NT, WPE) void k_fftfilt_r16(int hm1, const float2 *
     if (seg == 0) {   // the only segment that reaches into the history
 #pragma unroll
         for (int q = 0; q < 16; q++) {
+            // samples before x read 0 from an out-of-range offset.  The
+            // select is explicit: with a negative si, (unsigned)si * ES lets
+            // the compiler move the constant 256 q ES into the instruction's
+            // offset field, which the hardware adds without 32-bit
+            // wrap-around (a sample t + 1 at q = 2 then reads 0: seen in a
+            // variant of this loop)
             const int si = sb + t + 256 * q;
-            const unsigned ox = (unsigned)si * ES, oh = (unsigned)(si + hm1) * ES;
+            const unsigned ox = si < 0 ? 0xFFFFFFF0u : (unsigned)si * ES, oh = (unsigned)(si + hm1) * ES;
             if constexpr (REAL) {
                 const float a = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rx, ox, 0, 0)) +
                                 __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rh, oh, 0, 0));
