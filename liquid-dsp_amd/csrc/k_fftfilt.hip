@@ -120,12 +120,11 @@ __global__ __launch_bounds__(NT, WPE) void k_fftfilt_r16(int hm1, const float2 *
     if (seg == 0) {   // the only segment that reaches into the history
 #pragma unroll
         for (int q = 0; q < 16; q++) {
-            // samples before x read 0 from an out-of-range offset.  The
-            // select is explicit: with a negative si, (unsigned)si * ES lets
-            // the compiler move the constant 256 q ES into the instruction's
-            // offset field, which the hardware adds without 32-bit
-            // wrap-around (a sample t + 1 at q = 2 then reads 0: seen in a
-            // variant of this loop)
+            // samples before x read 0 from an explicit out-of-range offset
+            // (a variant of this loop that relied on the wrapped unsigned
+            // (sb + i) * ES instead returned wrong rrrf outputs 0..hm1-1 on
+            // the GPU; the 32-bit wrap of an offset-field sum itself is fine,
+            // tools/mb/mb_bufwrap.hip, so the cause there stays unidentified)
             const int si = sb + t + 256 * q;
             const unsigned ox = si < 0 ? 0xFFFFFFF0u : (unsigned)si * ES, oh = (unsigned)(si + hm1) * ES;
             if constexpr (REAL) {
