@@ -293,6 +293,173 @@ bool launch_pfb2_an256(const void *hsub, const void *hist, const void *x, long l
     return true;
 }
 
+// M = 2048 analyzer fused (the two-pass path moved 56 B per input): 1024
+// lanes, lane t owning the lo column t (bin j = 1023 - t) and the hi column
+// t + 1024 (bin j ^ 1024), so both columns share the lane's two tap sets
+// (A: taps of bin j, B: of bin j ^ 1024):
+//     lo, row c:  block 2c   += A . column,  block 2c+1 += B . column
+//     hi, row c:  block 2c+1 += A . column,  block 2c+2 += B . column
+// A group of 4 rows completes 8 blocks into a 9-buffer LDS ring; a block's
+// buffer holds its even bins and its odd bins as two 1024-point halves.
+// Each of the 16 waves then inverse-transforms one half in registers
+// (fft1024_wave_rt: wave-local transposes, no workgroup barrier), and after
+// one barrier the wave combines its block's halves for 512 output pairs,
+//     Y[k] = E[k] + W_2048^-k O[k],  Y[k + 1024] = E[k] - W_2048^-k O[k],
+// times 1/M, stored as 1 KB coalesced rows.  Three barriers per group (a
+// 2048-point transform across two waves took six: 1.07 ms per 2^27 samples).
+constexpr int A2_HS = 1090;            // half stride: 1088-float2 transform scratch, +2 spreads the halves' banks
+constexpr int A2_BSTR = 2 * A2_HS;     // 16-byte aligned halves
+template <int L>
+__global__ __launch_bounds__(1024, 1) void k_pfb2_an2048(const float *__restrict__ hsub,
+                                                         const float2 *__restrict__ hist,
+                                                         const float2 *__restrict__ x, int n_in, int p0, int nb,
+                                                         int cmin, int cmax, int S, float2 *__restrict__ Y,
+                                                         const float2 *__restrict__ tw4096)
+{
+    constexpr int M = 2048, M2 = 1024, HL = L * M - M2, NS = 8, G = 4, NBUF = 2 * G + 1;
+    static_assert(L <= NS, "ring of 8 rows");
+    __shared__ __attribute__((aligned(16))) float2 xr[NBUF * A2_BSTR];
+    __shared__ __attribute__((aligned(16))) float2 tw2[64];
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    if (tid < 64) {   // W_64^{-b r} (inverse transform)
+        const float2 u = tw4096[(64 * (tid & 3) * (tid >> 2)) & 4095];
+        tw2[tid] = make_float2(u.x, -u.y);
+    }
+    const float2 a1 = tw4096[(4 * lane) & 4095], a4 = tw4096[(16 * lane) & 4095];
+    const int jl = M2 - 1 - tid, jh = jl ^ M2;   // bins of the lo / hi column
+    // split position of bin j in its block: half j & 1, index j >> 1
+    const int pl_lo = (jl & 1) * A2_HS + (jl >> 1), pl_hi = (jh & 1) * A2_HS + (jh >> 1);
+    // taps re-read (L1/L2 hits) at every group instead of held across the
+    // transforms: 16 VGPRs the ring and the prefetched rows need there
+    float ta[L], tb[L];
+    auto load_taps = [&]() {
+        int oa = jl * L, ob = jh * L;
+        asm volatile("" : "+v"(oa), "+v"(ob));   // keep the reload inside the loop
+#pragma unroll
+        for (int n = 0; n < L; n++) {
+            ta[n] = hsub[oa + n];
+            tb[n] = hsub[ob + n];
+        }
+    };
+    load_taps();
+    const __amdgpu_buffer_rsrc_t ry = __builtin_amdgcn_make_buffer_rsrc((void *)Y, (short)0, nb * M * 8, 0x00020000);
+    const float2 *zero = tw4096 + LQ_TW_N;   // lqrt_zeros(): the table's zero tail
+    auto row_sample = [&](int r, int col) -> float2 {
+        const int t = r * M + col - p0 * M2;
+        return lq_load_hx(hist + HL, x, zero, t, HL, n_in);
+    };
+    auto dot = [&](const float2 (&w)[NS], int newest, const float (&h)[L]) -> float2 {
+        float2 acc = make_float2(0.f, 0.f);
+#pragma unroll
+        for (int n = 0; n < L; n++) {
+            const float2 v = w[(newest - n) & (NS - 1)];
+            acc.x = fmaf(h[n], v.x, acc.x);
+            acc.y = fmaf(h[n], v.y, acc.y);
+        }
+        return acc;
+    };
+    auto slot = [](int b) { return ((b % NBUF) + NBUF) % NBUF; };
+    const int hb = wave >> 1, hh = wave & 1;   // this wave's block (2 r0 + hb) and half
+    const float inv = 1.0f / (float)M;
+    typedef float v4f __attribute__((ext_vector_type(4)));
+
+    const int cs = cmin + (int)blockIdx.x * S;
+    int ce = cs + S;
+    if (ce > cmax + 1) ce = cmax + 1;
+    // rows cs-8 .. cs-1 fill the ring (slot r & 7); the last gives the hi
+    // half of block 2cs
+    float2 wl[NS], wh[NS], pl[G], ph[G];
+#pragma unroll
+    for (int u = 0; u < NS; u++) {
+        wl[u] = row_sample(cs - NS + u, tid);
+        wh[u] = row_sample(cs - NS + u, tid + M2);
+    }
+    xr[slot(2 * cs) * A2_BSTR + pl_hi] = dot(wh, NS - 1, tb);
+#pragma unroll
+    for (int u = 0; u < G; u++) {
+        pl[u] = row_sample(cs + u, tid);
+        ph[u] = row_sample(cs + u, tid + M2);
+    }
+    __syncthreads();   // tw2 ready
+    // one group: rows r0 .. r0+3 into ring slots s0 .. s0+3 (s0 = 0 or 4),
+    // then the 8 completed blocks' transforms
+    auto group = [&](int r0, auto s0c) {
+        constexpr int s0 = decltype(s0c)::value;
+        load_taps();
+#pragma unroll
+        for (int u = 0; u < G; u++) {
+            wl[s0 + u] = pl[u];
+            wh[s0 + u] = ph[u];
+            pl[u] = row_sample(r0 + G + u, tid);
+            ph[u] = row_sample(r0 + G + u, tid + M2);
+            const int c = r0 + u;
+            xr[slot(2 * c) * A2_BSTR + pl_lo] = dot(wl, s0 + u, ta);
+            xr[slot(2 * c + 1) * A2_BSTR + pl_lo] = dot(wl, s0 + u, tb);
+            xr[slot(2 * c + 1) * A2_BSTR + pl_hi] = dot(wh, s0 + u, ta);
+            xr[slot(2 * c + 2) * A2_BSTR + pl_hi] = dot(wh, s0 + u, tb);
+        }
+        __syncthreads();
+        const int b = 2 * r0 + hb;
+        float2 *Bb = xr + slot(b) * A2_BSTR;
+        {
+            float2 *Bh = Bb + hh * A2_HS;
+            float2 v[16];
+#pragma unroll
+            for (int n = 0; n < 16; n++) v[n] = Bh[lane + 64 * n];
+            fft1024_wave_rt<-1>(v, Bh, a1, a4, tw2, lane);   // natural order at k + 4 (k >> 8)
+        }
+        __syncthreads();   // both halves of every block transformed
+        const int gb = b - p0;
+        const bool keep = gb >= 0 && gb < nb && b < 2 * ce;
+        // a dropped block's base: 2^31 (the launch's range is below it, and
+        // base + 16 KB cannot wrap around 2^32 into it)
+        const unsigned base = keep ? (unsigned)gb * (unsigned)(M * 8) : 0x80000000u;
+#pragma unroll
+        for (int i = 0; i < 4; i++) {
+            const int k = 512 * hh + 2 * lane + 128 * i;
+            const int pos = k + 4 * (k >> 8);
+            // W_2048^-k, W_2048^-(k+1) (table hits in L1 / L2)
+            const float2 u0 = tw4096[2 * k], u1 = tw4096[2 * k + 2];
+            const float2 wk[2] = {make_float2(u0.x, -u0.y), make_float2(u1.x, -u1.y)};
+            const v4f E = *reinterpret_cast<const v4f *>(Bb + pos);
+            const v4f O = *reinterpret_cast<const v4f *>(Bb + A2_HS + pos);
+            const v2f o0 = pk_cmul(v2f{O.x, O.y}, pk(wk[0])), o1 = pk_cmul(v2f{O.z, O.w}, pk(wk[1]));
+            const v2f e0 = v2f{E.x, E.y}, e1 = v2f{E.z, E.w};
+            const v2f s0v = (e0 + o0) * inv, s1v = (e1 + o1) * inv, d0 = (e0 - o0) * inv, d1 = (e1 - o1) * inv;
+            __builtin_amdgcn_raw_buffer_store_b128(v4f{s0v.x, s0v.y, s1v.x, s1v.y}, ry, base + (unsigned)k * 8u, 0, 2);
+            __builtin_amdgcn_raw_buffer_store_b128(v4f{d0.x, d0.y, d1.x, d1.y}, ry, base + (unsigned)(k + 1024) * 8u, 0, 2);
+        }
+        __syncthreads();   // the combine's reads are done before the next group's writes
+    };
+    // S is a multiple of 8 rows: the ring slot of row r0 + u is u (first
+    // group) or 4 + u (second)
+    for (int r0 = cs; r0 < ce; r0 += 2 * G) {
+        group(r0, std::integral_constant<int, 0>{});
+        if (r0 + G < ce) group(r0 + G, std::integral_constant<int, G>{});
+    }
+}
+
+template <int L>
+bool launch_pfb2_an2048(const void *hsub, const void *hist, const void *x, long long nb, int p0, void *Y, hipStream_t st)
+{
+    constexpr int M = 2048;
+    const long long n_in = nb * (M / 2);
+    if (n_in * 8 >= (1ll << 31) || nb * (long long)M * 8 >= (1ll << 31)) return false;
+    const int cmin = (p0 - 1) >> 1;
+    const int cmax = (int)((p0 + nb - 1) >> 1);
+    const int rows = cmax - cmin + 1;
+    // one workgroup per CU: runs of S rows (a multiple of 8), about 256 runs
+    long long S = ((long long)rows + 255) / 256;
+    S = (S + 7) / 8 * 8;
+    if (S < 32) S = 32;
+    const long long nseg = (rows + S - 1) / S;
+    hipLaunchKernelGGL((k_pfb2_an2048<L>), dim3((unsigned)nseg), dim3(1024), 0, st, (const float *)hsub,
+                       (const float2 *)hist, (const float2 *)x, (int)n_in, p0, (int)nb, cmin, cmax, (int)S,
+                       (float2 *)Y, (const float2 *)lqrt_twiddles());
+    LQ_CHECK_LAUNCH();
+    return true;
+}
+
 // M = 64 / 128 analyzer fused (the two-pass path moved 56 B per input): as
 // k_pfb2_an256, with Q = 256 / M column sets per workgroup, each a lane per
 // column over its own run of rows (segment blockIdx.x Q + set), and each
@@ -1577,6 +1744,17 @@ extern "C" void lqk_firpfbch2_analyzer(unsigned int M, unsigned int m, const voi
                 default: break;
                 }
 #undef LQ_F
+                if (f) continue;
+            }
+            if (M == 2048 && 2 * m <= 8 && !getenv("LQ_PFB2_TWO_PASS")) {
+                bool f = false;
+                switch (2 * m) {
+                case 2: f = launch_pfb2_an2048<2>(hsub, hc, xc, nbc, p0, Yc, st); break;
+                case 4: f = launch_pfb2_an2048<4>(hsub, hc, xc, nbc, p0, Yc, st); break;
+                case 6: f = launch_pfb2_an2048<6>(hsub, hc, xc, nbc, p0, Yc, st); break;
+                case 8: f = launch_pfb2_an2048<8>(hsub, hc, xc, nbc, p0, Yc, st); break;
+                default: break;
+                }
                 if (f) continue;
             }
             if ((M == 64 || M == 128) && 2 * m <= 8 && !getenv("LQ_PFB2_TWO_PASS")) {

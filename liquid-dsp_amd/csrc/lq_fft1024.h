@@ -86,3 +86,52 @@ __device__ __forceinline__ void fft1024_wave(float2 (&v)[16], float2 *B, const f
     }
     f1k_wave_fence();
 }
+
+// fft1024_wave with the first twiddle W_1024^{DIR lane k1} formed in
+// registers from a1 = W_4096^{4 lane}, a4 = W_4096^{16 lane} (forward
+// values; twiddle16v) instead of the 8 KB tw1 table, for kernels without
+// the LDS for it.  Same input and output layout.
+template <int DIR>
+__device__ __forceinline__ void fft1024_wave_rt(float2 (&v)[16], float2 *B, float2 a1, float2 a4, const float2 *tw2,
+                                                int lane)
+{
+    dft16<DIR>(v);
+    twiddle16v<DIR>(v, a1, a4);
+    v2f p[16];
+    f1k_wave_fence();
+#pragma unroll
+    for (int k1 = 0; k1 < 16; k1++) B[k1 * 68 + lane] = v[k1];
+    f1k_wave_fence();
+    const int k1 = lane >> 2, bq = lane & 3;
+#pragma unroll
+    for (int a = 0; a < 16; a++) p[a] = pk(B[k1 * 68 + 4 * a + bq]);
+    pk_dft16<DIR>(p);
+#pragma unroll
+    for (int r = 1; r < 16; r++) p[r] = pk_cmul(p[r], pk(tw2[r * 4 + bq]));
+    f1k_wave_fence();
+#pragma unroll
+    for (int r = 0; r < 16; r++) B[k1 + 16 * r + 260 * bq] = unpk(p[r]);
+    f1k_wave_fence();
+    typedef float v4f __attribute__((ext_vector_type(4)));
+    const int t2 = lane >> 3, p2 = lane & 7;
+    v4f c[2][4];
+#pragma unroll
+    for (int u = 0; u < 2; u++)
+#pragma unroll
+        for (int q = 0; q < 4; q++)
+            c[u][q] = *reinterpret_cast<const v4f *>(B + 2 * p2 + 16 * (t2 + 8 * u) + 260 * q);
+    f1k_wave_fence();
+#pragma unroll
+    for (int u = 0; u < 2; u++) {
+        v2f e0[4] = {c[u][0].xy, c[u][1].xy, c[u][2].xy, c[u][3].xy};
+        v2f e1[4] = {c[u][0].zw, c[u][1].zw, c[u][2].zw, c[u][3].zw};
+        pk_dft4<DIR>(e0[0], e0[1], e0[2], e0[3]);
+        pk_dft4<DIR>(e1[0], e1[1], e1[2], e1[3]);
+#pragma unroll
+        for (int sidx = 0; sidx < 4; sidx++) {
+            const v4f val = {e0[sidx].x, e0[sidx].y, e1[sidx].x, e1[sidx].y};
+            *reinterpret_cast<v4f *>(B + 2 * p2 + 16 * (t2 + 8 * u) + 260 * sidx) = val;
+        }
+    }
+    f1k_wave_fence();
+}

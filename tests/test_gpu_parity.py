@@ -374,6 +374,23 @@ def test_firpfbch2_analyzer_small_fused_vs_oracle(M, m):
     assert G.nrm_err(y, o.execute_block(x)) < NRM
 
 
+@pytest.mark.parametrize("m", [1, 2, 3, 4])
+def test_firpfbch2_analyzer_m2048_fused_vs_oracle(m):
+    # M = 2048 with m <= 4: the fused kernel (k_pfb2_an2048, two columns per
+    # lane, 4-row groups, register 2048-point transforms in the ring's own
+    # buffers); many workgroup runs, a ragged last run, calls on both parities
+    M = 2048
+    r = rng(7 * M + m)
+    nblocks = (1 << 22) // M + 29
+    x = cx(r, nblocks * M // 2)
+    g = LQ.FirPfbch2(LQ.LIQUID_ANALYZER, M, m, 60.0)
+    o = O.FirPfbch2(O.ANALYZER, M, m, 60.0)
+    cuts = [0, 1, 4, 777, nblocks - 3, nblocks]
+    step = M // 2
+    y = np.concatenate([g.execute_block(x[a * step:b * step]) for a, b in zip(cuts[:-1], cuts[1:])])
+    assert G.nrm_err(y, o.execute_block(x)) < NRM
+
+
 def test_firpfbch2_analyzer_polyphase_chunks_vs_oracle():
     # a call longer than one polyphase chunk (2^27 / M blocks): the second
     # chunk takes its history from the input before it; odd start parity
