@@ -82,10 +82,34 @@ constexpr int SSTR = 68;          // floats per staged segment (32 x re/im + pad
 // 16-byte read
 template <int KB>
 constexpr int glen_kb() { return 16 * (2 + 4 * KB) + 32; }
-template <int KB>
-constexpr int acp_bytes() { return KB > 2 ? 8 * 3 * glen_kb<KB>() * 2 : 0; }
+// bf16 terms of the taps whose A fragments come from LDS (the last NAL of
+// the three): all of them past 128 taps; at KB = 1 (crcf / rrrf-shaped, one
+// tap matrix) terms 2 and 3, which frees 48 VGPRs for a third chunk of loads
+// in flight while the 4 KB of copies still leave room for three workgroups
+// per CU
+#ifndef FMX_A2L
+#define FMX_A2L 0
+#endif
+#ifndef FMX_NBUF
+#define FMX_NBUF 2   // chunks of loads in flight per workgroup (register sets)
+#endif
+template <bool CC, int KB>
+constexpr int nal_kb() { return KB > 2 ? 3 : ((!CC && KB == 1 && FMX_A2L) ? 2 : 0); }
+template <bool CC, int KB>
+constexpr int nbuf_kb() { return (!CC && KB == 1) ? FMX_NBUF : 2; }
+// elements between the eight shifted copies: at least NAL GL, and 16 mod 128
+// (32 B mod 256), so the 16 lanes of a ds_read_b128 pass -- eight copies at
+// two bases 16 B apart -- land on 16 distinct bank groups (a stride that is
+// a multiple of 256 B put all eight copies on the same banks)
+template <bool CC, int KB>
+constexpr int acs_kb() { return nal_kb<CC, KB>() ? ((nal_kb<CC, KB>() * glen_kb<KB>() - 16 + 127) / 128) * 128 + 16 : 0; }
+template <bool CC, int KB>
+constexpr int acp_bytes() { return 8 * acs_kb<CC, KB>() * 2; }
 template <bool CC, int KB = 1>
-constexpr int lds_bytes_mx() { return 6 * plb_kb<KB>() + (CC ? 2 : 1) * 4 * 16 * SSTR * 4 + acp_bytes<KB>(); }
+constexpr int lds_bytes_mx() { return 6 * plb_kb<KB>() + (CC ? 2 : 1) * 4 * 16 * SSTR * 4 + acp_bytes<CC, KB>(); }
+
+static_assert(3 * (lds_bytes_mx<false, 1>() + 80) <= 160 * 1024, "crcf KB = 1: three workgroups per CU");
+static_assert(2 * (lds_bytes_mx<false, 4>() + 80) <= 160 * 1024, "crcf KB = 4: two workgroups per CU");
 
 __device__ __forceinline__ int poff(int pos) { return 2 * pos + 16 * (pos >> 5); }
 
@@ -214,24 +238,25 @@ __global__ __launch_bounds__(NT, KB > 2 ? 2 : ((CC || KB > 1) ? 2 : 3)) void k_f
     float *stage = reinterpret_cast<float *>(smem + 6 * PLB) + wave * NA * 16 * SSTR;
 
     // A fragments: lane (row i = r32, k half hh) holds H[i][16s + 8hh + e]
-    // (cccf: hpad holds (re, im) pairs; matrix a takes component a)
-    constexpr bool AL = KB > 2;   // fragments read from LDS per step
-    bf16x8 A[NA][3][AL ? 1 : NS];
+    // (cccf: hpad holds (re, im) pairs; matrix a takes component a); terms
+    // NAR.. come from LDS per step
+    constexpr int NAL = nal_kb<CC, KB>(), NAR = 3 - NAL;
+    bf16x8 A[NA][NAR > 0 ? NAR : 1][NAR > 0 ? NS : 1];
     __bf16 *acp = reinterpret_cast<__bf16 *>(smem + 6 * PLB + NA * 4 * 16 * SSTR * 4);
-    constexpr int GL = glen_kb<KB>();
-    if constexpr (AL) {
-        // copy c, term p: G[c][p][k] = term p of g[k + c], g[k] = h[HALO + 31 - k]
+    constexpr int GL = glen_kb<KB>(), ACS = acs_kb<CC, KB>();
+    if constexpr (NAL > 0) {
+        // copy c, term p >= NAR: G[c][p - NAR][k] = term p of g[k + c], g[k] = h[HALO + 31 - k]
         for (int e = tid; e < 8 * GL; e += NT) {
             const int c = e / GL, k = e - c * GL;
             const int hk = HALO + 31 - (k + c);
             const float hv = (hk >= 0 && hk < HALO) ? hpad[hk] : 0.f;
-            bf16x2 t1, t2, t3;
-            split3(v2f{hv, 0.f}, t1, t2, t3);
-            acp[(c * 3 + 0) * GL + k] = t1.x;
-            acp[(c * 3 + 1) * GL + k] = t2.x;
-            acp[(c * 3 + 2) * GL + k] = t3.x;
+            bf16x2 t[3];
+            split3(v2f{hv, 0.f}, t[0], t[1], t[2]);
+#pragma unroll
+            for (int p = NAR; p < 3; p++) acp[c * ACS + (p - NAR) * GL + k] = t[p].x;
         }
-    } else {
+    }
+    if constexpr (NAR > 0) {
 #pragma unroll
     for (int a = 0; a < NA; a++)
 #pragma unroll
@@ -248,13 +273,13 @@ __global__ __launch_bounds__(NT, KB > 2 ? 2 : ((CC || KB > 1) ? 2 : 3)) void k_f
                 split3(v2f{hv[0], hv[1]}, t[0][q], t[1][q], t[2][q]);
             }
 #pragma unroll
-            for (int p = 0; p < 3; p++)
-                A[a][p][AL ? 0 : s] =
+            for (int p = 0; p < NAR; p++)
+                A[a][p][s] =
                     bf16x8{t[p][0].x, t[p][0].y, t[p][1].x, t[p][1].y, t[p][2].x, t[p][2].y, t[p][3].x, t[p][3].y};
         }
     }
-    // this lane's copy (31 - r32) mod 8 and its fragment base (+ 16 s: step s; + p GL: term p)
-    const __bf16 *acl = AL ? acp + ((31 - r32) & 7) * 3 * GL + ((31 - r32) & ~7) + 8 * hh : nullptr;
+    // this lane's copy (31 - r32) mod 8 and its fragment base (+ 16 s: step s; + (p - NAR) GL: term p)
+    const __bf16 *acl = NAL > 0 ? acp + ((31 - r32) & 7) * ACS + ((31 - r32) & ~7) + 8 * hh : nullptr;
 
     // Chunks are dealt grid-stride (workgroup w takes chunks w, w + G, ...):
     // the chip then streams one contiguous window of the input at a time.
@@ -294,15 +319,20 @@ __global__ __launch_bounds__(NT, KB > 2 ? 2 : ((CC || KB > 1) ? 2 : 3)) void k_f
         put1(planes, PLB, tid, hv);
         if (unsafe_bits(hv.x) | unsafe_bits(hv.y)) atomicOr(&sbad[0], 1u);
     }
-    // two chunks in flight per workgroup: register sets (xa, ha) / (xb, hb)
-    // alternate (the loop is unrolled by two so neither set is ever copied,
-    // which would wait on its loads early)
-    v4f xa[4], xb[4];
-    v2f ha, hb;
+    // NB chunks in flight per workgroup: register sets (xa, ha) / (xb, hb)
+    // [/ (xc, hc)] rotate (the loop is unrolled by NB so no set is ever
+    // copied, which would wait on its loads early)
+    constexpr int NB = nbuf_kb<CC, KB>();
+    v4f xa[4], xb[4], xc[4];
+    v2f ha, hb, hc;
     load8b(rx, main_off(0), xa);
     ha = ldh(halo_off(0));
     load8b(rx, main_off(1), xb);
     hb = ldh(halo_off(1));
+    if constexpr (NB > 2) {
+        load8b(rx, main_off(2), xc);
+        hc = ldh(halo_off(2));
+    }
 
     // B operand: lane column n = r32 -> segment sg = n & 15, component n >> 4
     const int sg = r32 & 15, comp = r32 >> 4;
@@ -323,8 +353,8 @@ __global__ __launch_bounds__(NT, KB > 2 ? 2 : ((CC || KB > 1) ? 2 : 3)) void k_f
         if (!(FMX_VARIANT & 16) && (unsafe4(xv[0]) | unsafe4(xv[1]) | unsafe4(xv[2]) | unsafe4(xv[3])))
             atomicOr(&sbad[cs], 1u);   // 16: timing experiment, no range guard
         if (tid == 0) sbad[(cs + 1) % 3] = 0u;   // step k+1's slot (last read in step k-2)
-        load8b(rx, main_off(k + 2), xv);
-        if (!(FMX_VARIANT & 8)) hv = ldh(halo_off(k + 2));
+        load8b(rx, main_off(k + NB), xv);
+        if (!(FMX_VARIANT & 8)) hv = ldh(halo_off(k + NB));
         if (!(FMX_VARIANT & 32)) __syncthreads();
         if (tid == 0 && sbad[cs] && c < nch) bad_mask[k >> 5] |= 1u << (k & 31);
 
@@ -342,30 +372,24 @@ __global__ __launch_bounds__(NT, KB > 2 ? 2 : ((CC || KB > 1) ? 2 : 3)) void k_f
 #if FMX_VARIANT & 1   // timing experiment: no MFMA (wrong results)
 #pragma unroll
             for (int a = 0; a < NA; a++) {
-                C[a][s] += (float)b0[0] + (float)b1[1] + (float)b2[2] + (float)A[a][0][AL ? 0 : s][0];
+                C[a][s] += (float)b0[0] + (float)b1[1] + (float)b2[2] + (float)b0[1];
             }
             continue;
 #endif
-            if constexpr (AL) {
-                const bf16x8 a0 = *reinterpret_cast<const bf16x8 *>(acl + 16 * s);
-                const bf16x8 a1 = *reinterpret_cast<const bf16x8 *>(acl + GL + 16 * s);
-                const bf16x8 a2 = *reinterpret_cast<const bf16x8 *>(acl + 2 * GL + 16 * s);
-                C[0] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a0, b2, C[0], 0, 0, 0);
-                C[0] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a1, b1, C[0], 0, 0, 0);
-                C[0] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a2, b0, C[0], 0, 0, 0);
-                C[0] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a0, b1, C[0], 0, 0, 0);
-                C[0] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a1, b0, C[0], 0, 0, 0);
-                C[0] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a0, b0, C[0], 0, 0, 0);
-                continue;
-            }
+            bf16x8 al[NAL > 0 ? NAL : 1];
+#pragma unroll
+            for (int p = 0; p < NAL; p++) al[p] = *reinterpret_cast<const bf16x8 *>(acl + p * GL + 16 * s);
 #pragma unroll
             for (int a = 0; a < NA; a++) {
-                C[a] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(A[a][0][AL ? 0 : s], b2, C[a], 0, 0, 0);
-                C[a] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(A[a][1][AL ? 0 : s], b1, C[a], 0, 0, 0);
-                C[a] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(A[a][2][AL ? 0 : s], b0, C[a], 0, 0, 0);
-                C[a] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(A[a][0][AL ? 0 : s], b1, C[a], 0, 0, 0);
-                C[a] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(A[a][1][AL ? 0 : s], b0, C[a], 0, 0, 0);
-                C[a] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(A[a][0][AL ? 0 : s], b0, C[a], 0, 0, 0);
+                bf16x8 af[3];
+#pragma unroll
+                for (int p = 0; p < 3; p++) af[p] = p < NAR ? A[a][p < NAR ? p : 0][NAR > 0 ? s : 0] : al[p >= NAR ? p - NAR : 0];
+                C[a] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[0], b2, C[a], 0, 0, 0);
+                C[a] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[1], b1, C[a], 0, 0, 0);
+                C[a] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[2], b0, C[a], 0, 0, 0);
+                C[a] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[0], b1, C[a], 0, 0, 0);
+                C[a] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[1], b0, C[a], 0, 0, 0);
+                C[a] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[0], b0, C[a], 0, 0, 0);
             }
         }
 
@@ -409,9 +433,10 @@ __global__ __launch_bounds__(NT, KB > 2 ? 2 : ((CC || KB > 1) ? 2 : 3)) void k_f
         __builtin_amdgcn_wave_barrier();
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
     };
-    for (long long k = 0; k < cnt; k += 2) {
+    for (long long k = 0; k < cnt; k += NB) {
         step(k, xa, ha);
         step(k + 1, xb, hb);
+        if constexpr (NB > 2) step(k + 2, xc, hc);
     }
     // the range guard's chunks: the exact float32 outputs overwrite what the
     // matrix path stored for them.  Only workgroup-scope ordering is needed
