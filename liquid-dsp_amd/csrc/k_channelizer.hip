@@ -460,6 +460,220 @@ bool launch_pfb2_an2048(const void *hsub, const void *hist, const void *x, long 
     return true;
 }
 
+// M = 4096 analyzer fused (the two-pass path moved 56 B per input; the
+// same structure as k_pfb2_an2048 one size up): lane t owns four columns,
+// t + 1024 q.  The lo columns (q = 0, 1: bins j0 = 2047 - t, j1 = 1023 - t)
+// and the hi columns (q = 2, 3: bins j0 ^ 2048, j1 ^ 2048) share the lane's
+// four tap sets A_q = taps(j_q), B_q = taps(j_q ^ 2048), q = 0, 1:
+//     lo q, row c:  block 2c   += A_q . column,  block 2c+1 += B_q . column
+//     hi q, row c:  block 2c+1 += A_q . column,  block 2c+2 += B_q . column
+// A 32 KB block leaves room for a 3-buffer LDS ring only, so a group is one
+// row: it completes blocks 2c and 2c+1, whose buffers hold the four
+// 1024-point quarters of bins j = r (mod 4).  Waves 0-7 inverse-transform one
+// quarter each in registers (fft1024_wave_rt), and after a barrier all 16
+// waves combine their block's quarters (radix 4):
+//     Y[k + 1024 s] = sum_r W_4096^-(r k) Q_r[k] i^(r s)   (W^- : e^{+2 pi i ...})
+// times 1/M, stored as 16-byte rows.  The row ring is shifted in registers
+// (one row per loop iteration keeps the transform and combine code single).
+// m = 4: the next row's loads are issued after the transforms, so no
+// prefetch registers sit beside the ring and a transform (10 -> 2 spilled
+// VGPRs: 1.13 -> 1.11 ms per 2^27 samples; m <= 3 keep the early prefetch,
+// 0.995 vs 1.07 ms at m = 2)
+#ifndef A4_PF_LATE
+#define A4_PF_LATE (L > 6)
+#endif
+constexpr int A4_QS = 1092;            // quarter stride: 1088-float2 transform scratch; 1092 * 8 = 32 mod 128 B
+constexpr int A4_BSTR = 4 * A4_QS;     //   puts the four quarters of a dot-phase write on distinct bank groups
+template <int L>
+__global__ __launch_bounds__(1024, 1) void k_pfb2_an4096(const float *__restrict__ hsub,
+                                                         const float2 *__restrict__ hist,
+                                                         const float2 *__restrict__ x, int n_in, int p0, int nb,
+                                                         int cmin, int cmax, int S, float2 *__restrict__ Y,
+                                                         const float2 *__restrict__ tw4096)
+{
+    constexpr int M = 4096, M2 = 2048, HL = L * M - M2, NS = L, NBUF = 3;
+    __shared__ __attribute__((aligned(16))) float2 xr[NBUF * A4_BSTR];
+    __shared__ __attribute__((aligned(16))) float2 tw2[64];
+    __shared__ __attribute__((aligned(16))) float2 wold[4 * 1024];   // each column's oldest ring row
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    if (tid < 64) {   // W_64^{-b r} (inverse transform)
+        const float2 u = tw4096[(64 * (tid & 3) * (tid >> 2)) & 4095];
+        tw2[tid] = make_float2(u.x, -u.y);
+    }
+    const float2 a1 = tw4096[(4 * lane) & 4095], a4 = tw4096[(16 * lane) & 4095];
+    const int j0 = M2 - 1 - tid, j1 = M2 / 2 - 1 - tid;   // lo bins; hi bins j ^ M2
+    // split position of bin j in its block: quarter j & 3, index j >> 2
+    auto qpos = [](int j) { return (j & 3) * A4_QS + (j >> 2); };
+    const int pl0 = qpos(j0), pl1 = qpos(j1), ph0 = qpos(j0 ^ M2), ph1 = qpos(j1 ^ M2);
+    const __amdgpu_buffer_rsrc_t ry = __builtin_amdgcn_make_buffer_rsrc((void *)Y, (short)0, nb * M * 8, 0x00020000);
+    const float2 *zero = tw4096 + LQ_TW_N;   // lqrt_zeros(): the table's zero tail
+    auto row_sample = [&](int r, int col) -> float2 {
+        const int t = r * M + col - p0 * M2;
+        return lq_load_hx(hist + HL, x, zero, t, HL, n_in);
+    };
+    // Row ring of column q: the NS - 1 newest rows in registers, w[q][u] =
+    // row (newest - NS + 2 + u), and the oldest in LDS (wold[q][tid], private
+    // to the lane): 8 VGPRs fewer, which m = 4 needs to fit a transform
+    // beside the ring in 128
+    float2 w[4][NS - 1], pf[4], wo[4];
+    auto dot = [&](int q, const float *__restrict__ h) -> float2 {
+        float2 acc = make_float2(0.f, 0.f);
+#pragma unroll
+        for (int n = 0; n < NS; n++) {
+            const float hn = h[n];
+            const float2 v = n < NS - 1 ? w[q][NS - 2 - n] : wo[q];
+            acc.x = fmaf(hn, v.x, acc.x);
+            acc.y = fmaf(hn, v.y, acc.y);
+        }
+        return acc;
+    };
+    auto slot = [](int b) { return ((b % NBUF) + NBUF) % NBUF; };
+    const float inv = 1.0f / (float)M;
+    typedef float v4f __attribute__((ext_vector_type(4)));
+
+    const int cs = cmin + (int)blockIdx.x * S;
+    int ce = cs + S;
+    if (ce > cmax + 1) ce = cmax + 1;
+    // rows cs-NS .. cs-1 fill the ring; the last gives the hi half of block 2cs
+#pragma unroll
+    for (int q = 0; q < 4; q++) {
+        wo[q] = row_sample(cs - NS, tid + 1024 * q);
+#pragma unroll
+        for (int u = 0; u < NS - 1; u++) w[q][u] = row_sample(cs - NS + 1 + u, tid + 1024 * q);
+    }
+    {
+        float2 *B = xr + slot(2 * cs) * A4_BSTR;
+        B[ph0] = dot(2, hsub + (j0 ^ M2) * L);
+        B[ph1] = dot(3, hsub + (j1 ^ M2) * L);
+    }
+    if constexpr (NS > 1) {   // row cs - NS + 1: the oldest of row cs's dots
+#pragma unroll
+        for (int q = 0; q < 4; q++) wold[q * 1024 + tid] = w[q][0];
+    }
+#pragma unroll
+    for (int q = 0; q < 4; q++) pf[q] = row_sample(cs, tid + 1024 * q);
+    __syncthreads();   // tw2 ready
+    const int qb = wave >> 2, qq = wave & 3;   // transform phase: block 2c + qb, quarter qq (waves 0-7)
+    const int cb = wave >> 3, wb = wave & 7;   // combine phase: block 2c + cb, pairs lane + 64 wb
+    for (int c = cs; c < ce; c++) {
+#pragma unroll
+        for (int q = 0; q < 4; q++) {
+            // wold holds row c - NS + 1 (stored after the previous row's
+            // dots, below); w[q][0] died there, so the registers shift down
+            wo[q] = wold[q * 1024 + tid];
+            if constexpr (NS > 1) {
+#pragma unroll
+                for (int u = 0; u < NS - 2; u++) w[q][u] = w[q][u + 1];
+                w[q][NS - 2] = pf[q];
+            } else {
+                wo[q] = pf[q];
+            }
+            if (!A4_PF_LATE) pf[q] = row_sample(c + 1, tid + 1024 * q);
+        }
+        {
+            float2 *B0 = xr + slot(2 * c) * A4_BSTR, *B1 = xr + slot(2 * c + 1) * A4_BSTR,
+                   *B2 = xr + slot(2 * c + 2) * A4_BSTR;
+            // taps re-read (L1 / L2 hits) every row instead of held across
+            // the transforms: the opaque offsets keep the loads in the loop
+            int o0 = j0 * L, o1 = j1 * L, o2 = (j0 ^ M2) * L, o3 = (j1 ^ M2) * L;
+            asm volatile("" : "+v"(o0), "+v"(o1), "+v"(o2), "+v"(o3));
+            const float *A0 = hsub + o0, *A1 = hsub + o1, *Bt0 = hsub + o2, *Bt1 = hsub + o3;
+            // one tap set at a time (8 VGPRs of taps live, not 32)
+            B0[pl0] = dot(0, A0);
+            B1[ph0] = dot(2, A0);
+            asm volatile("" ::: "memory");
+            B1[pl0] = dot(0, Bt0);
+            B2[ph0] = dot(2, Bt0);
+            asm volatile("" ::: "memory");
+            B0[pl1] = dot(1, A1);
+            B1[ph1] = dot(3, A1);
+            asm volatile("" ::: "memory");
+            B1[pl1] = dot(1, Bt1);
+            B2[ph1] = dot(3, Bt1);
+            // the next row's oldest (row c - NS + 2) waits in LDS, not in
+            // registers, across the transforms
+            if constexpr (NS > 1) {
+#pragma unroll
+                for (int q = 0; q < 4; q++) wold[q * 1024 + tid] = w[q][0];
+            }
+        }
+        __syncthreads();
+        if (wave < 8) {
+            float2 *Bq = xr + slot(2 * c + qb) * A4_BSTR + qq * A4_QS;
+            float2 v[16];
+#pragma unroll
+            for (int n = 0; n < 16; n++) v[n] = Bq[lane + 64 * n];
+            fft1024_wave_rt<-1>(v, Bq, a1, a4, tw2, lane);   // natural order at k + 4 (k >> 8)
+        }
+        __syncthreads();   // every quarter of both blocks transformed
+        if (A4_PF_LATE) {   // the next row's loads, issued after the transforms (no prefetch registers across them)
+#pragma unroll
+            for (int q = 0; q < 4; q++) pf[q] = row_sample(c + 1, tid + 1024 * q);
+        }
+        {
+            const int b = 2 * c + cb;
+            const float2 *Bb = xr + slot(b) * A4_BSTR;
+            const int gb = b - p0;
+            const bool keep = gb >= 0 && gb < nb && b < 2 * ce;
+            // a dropped block's base: 2^31 (the launch's range is below it)
+            const unsigned base = keep ? (unsigned)gb * (unsigned)(M * 8) : 0x80000000u;
+            const int k = 2 * (lane + 64 * wb);   // bins k, k + 1 of each quarter
+            const int pos = k + 4 * (k >> 8);
+            v2f T[4][2];
+#pragma unroll
+            for (int r = 0; r < 4; r++) {
+                const v4f E = *reinterpret_cast<const v4f *>(Bb + r * A4_QS + pos);
+                T[r][0] = v2f{E.x, E.y};
+                T[r][1] = v2f{E.z, E.w};
+            }
+#pragma unroll
+            for (int e = 0; e < 2; e++)
+#pragma unroll
+                for (int r = 1; r < 4; r++) {
+                    const float2 u = tw4096[r * (k + e)];   // W_4096^(r k), r k < 4096 (L1 / L2 hits)
+                    T[r][e] = pk_cmul(T[r][e], v2f{u.x, -u.y});
+                }
+            v2f Yo[4][2];
+#pragma unroll
+            for (int e = 0; e < 2; e++) {
+                const v2f s02 = T[0][e] + T[2][e], d02 = T[0][e] - T[2][e];
+                const v2f s13 = T[1][e] + T[3][e], d13 = T[1][e] - T[3][e];
+                const v2f jd13 = v2f{-d13.y, d13.x};   // i (T1 - T3)
+                Yo[0][e] = (s02 + s13) * inv;
+                Yo[1][e] = (d02 + jd13) * inv;
+                Yo[2][e] = (s02 - s13) * inv;
+                Yo[3][e] = (d02 - jd13) * inv;
+            }
+#pragma unroll
+            for (int sq = 0; sq < 4; sq++)
+                __builtin_amdgcn_raw_buffer_store_b128(v4f{Yo[sq][0].x, Yo[sq][0].y, Yo[sq][1].x, Yo[sq][1].y}, ry,
+                                                       base + (unsigned)(k + 1024 * sq) * 8u, 0, 2);
+        }
+        __syncthreads();   // the combine's reads are done before the next row's writes
+    }
+}
+
+template <int L>
+bool launch_pfb2_an4096(const void *hsub, const void *hist, const void *x, long long nb, int p0, void *Y, hipStream_t st)
+{
+    constexpr int M = 4096;
+    const long long n_in = nb * (M / 2);
+    if (n_in * 8 >= (1ll << 31) || nb * (long long)M * 8 >= (1ll << 31)) return false;
+    const int cmin = (p0 - 1) >> 1;
+    const int cmax = (int)((p0 + nb - 1) >> 1);
+    const int rows = cmax - cmin + 1;
+    // one workgroup per CU: runs of S rows, about 256 runs (each warms up on
+    // the 2m rows before it)
+    long long S = ((long long)rows + 255) / 256;
+    if (S < 32) S = 32;
+    const long long nseg = (rows + S - 1) / S;
+    hipLaunchKernelGGL((k_pfb2_an4096<L>), dim3((unsigned)nseg), dim3(1024), 0, st, (const float *)hsub,
+                       (const float2 *)hist, (const float2 *)x, (int)n_in, p0, (int)nb, cmin, cmax, (int)S,
+                       (float2 *)Y, (const float2 *)lqrt_twiddles());
+    LQ_CHECK_LAUNCH();
+    return true;
+}
+
 // M = 64 / 128 analyzer fused (the two-pass path moved 56 B per input): as
 // k_pfb2_an256, with Q = 256 / M column sets per workgroup, each a lane per
 // column over its own run of rows (segment blockIdx.x Q + set), and each
@@ -1753,6 +1967,17 @@ extern "C" void lqk_firpfbch2_analyzer(unsigned int M, unsigned int m, const voi
                 case 4: f = launch_pfb2_an2048<4>(hsub, hc, xc, nbc, p0, Yc, st); break;
                 case 6: f = launch_pfb2_an2048<6>(hsub, hc, xc, nbc, p0, Yc, st); break;
                 case 8: f = launch_pfb2_an2048<8>(hsub, hc, xc, nbc, p0, Yc, st); break;
+                default: break;
+                }
+                if (f) continue;
+            }
+            if (M == 4096 && 2 * m <= 8 && !getenv("LQ_PFB2_TWO_PASS")) {
+                bool f = false;
+                switch (2 * m) {
+                case 2: f = launch_pfb2_an4096<2>(hsub, hc, xc, nbc, p0, Yc, st); break;
+                case 4: f = launch_pfb2_an4096<4>(hsub, hc, xc, nbc, p0, Yc, st); break;
+                case 6: f = launch_pfb2_an4096<6>(hsub, hc, xc, nbc, p0, Yc, st); break;
+                case 8: f = launch_pfb2_an4096<8>(hsub, hc, xc, nbc, p0, Yc, st); break;
                 default: break;
                 }
                 if (f) continue;

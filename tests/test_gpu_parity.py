@@ -341,7 +341,7 @@ def test_firpfbch2_analyzer_vs_oracle(M, m):
     assert G.nrm_err(y, o.execute_block(x)) < NRM
 
 
-@pytest.mark.parametrize("M,m", [(64, 4), (128, 1), (256, 4), (512, 3), (1024, 5), (2048, 4), (4096, 2), (256, 8)])
+@pytest.mark.parametrize("M,m", [(64, 4), (128, 1), (256, 4), (512, 3), (1024, 5), (2048, 4), (4096, 6), (256, 8)])
 def test_firpfbch2_analyzer_polyphase_pass_vs_oracle(M, m):
     # power-of-two M other than the fused M=1024/m=4 path: polyphase pass
     # (column slices x row runs with a warm-up of 2m-1 rows each) + batched
@@ -386,6 +386,24 @@ def test_firpfbch2_analyzer_m2048_fused_vs_oracle(m):
     g = LQ.FirPfbch2(LQ.LIQUID_ANALYZER, M, m, 60.0)
     o = O.FirPfbch2(O.ANALYZER, M, m, 60.0)
     cuts = [0, 1, 4, 777, nblocks - 3, nblocks]
+    step = M // 2
+    y = np.concatenate([g.execute_block(x[a * step:b * step]) for a, b in zip(cuts[:-1], cuts[1:])])
+    assert G.nrm_err(y, o.execute_block(x)) < NRM
+
+
+@pytest.mark.parametrize("m", [1, 2, 3, 4])
+def test_firpfbch2_analyzer_m4096_fused_vs_oracle(m):
+    # M = 4096 with m <= 4: the fused kernel (k_pfb2_an4096, four columns per
+    # lane, one-row groups, quarter transforms + radix-4 combine, the oldest
+    # ring row in LDS); many workgroup runs, a ragged last run, calls on both
+    # block parities
+    M = 4096
+    r = rng(5 * M + m)
+    nblocks = (1 << 22) // M + 41
+    x = cx(r, nblocks * M // 2)
+    g = LQ.FirPfbch2(LQ.LIQUID_ANALYZER, M, m, 60.0)
+    o = O.FirPfbch2(O.ANALYZER, M, m, 60.0)
+    cuts = [0, 1, 4, 333, nblocks - 3, nblocks]
     step = M // 2
     y = np.concatenate([g.execute_block(x[a * step:b * step]) for a, b in zip(cuts[:-1], cuts[1:])])
     assert G.nrm_err(y, o.execute_block(x)) < NRM
