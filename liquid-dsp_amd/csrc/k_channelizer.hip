@@ -1226,6 +1226,147 @@ bool launch_pfb_an_fused(int M, int p, const void *hsub, const void *hist, const
     return false;
 }
 
+// firpfbch analyzer, M = 4096 fused (the two-pass path moved 48 B per
+// sample): the structure of k_pfb2_an4096 for the critically sampled bank
+// (firpfbch.c:262-312).  Lane t owns columns t + 1024 q with their P taps
+// h[(M-1-col) + nM]; row b of the input is block b's polyphase row, and a
+// group of G = 3 rows fills three block buffers, whose twelve 1024-point
+// quarters (columns = r mod 4) waves 0-11 forward-transform (one row per
+// group: 0.72 ms per 2^27 samples at m = 4, four waves busy); all 16 waves
+// then combine
+//     Y[k + 1024 s] = sum_r W_4096^(r k) Q_r[k] (-i)^(r s)
+// into 8-byte coalesced stores.  The ring keeps its oldest row in LDS.
+#ifndef A4_G
+#define A4_G 3
+#endif
+template <int P, typename TC, int G = A4_G>
+__global__ __launch_bounds__(1024, 1) void k_pfb_an4096(const TC *__restrict__ hsub, const float2 *__restrict__ hist,
+                                                        const float2 *__restrict__ x, int n_in, int nb, int S,
+                                                        float2 *__restrict__ Y, const float2 *__restrict__ tw4096)
+{
+    constexpr int M = 4096, HL = (P - 1) * M, NS = P;
+    static_assert(P >= 2, "ring of at least two rows");
+    static_assert(G * A4_BSTR * 8 + 4 * 1024 * 8 + 512 <= 160 * 1024, "LDS");
+    __shared__ __attribute__((aligned(16))) float2 xr[G * A4_BSTR];
+    __shared__ __attribute__((aligned(16))) float2 tw2[64];
+    __shared__ __attribute__((aligned(16))) float2 wold[4 * 1024];
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    if (tid < 64) tw2[tid] = tw4096[(64 * (tid & 3) * (tid >> 2)) & 4095];   // W_64^{+b r} (forward)
+    const float2 a1 = tw4096[(4 * lane) & 4095], a4 = tw4096[(16 * lane) & 4095];
+    // column t + 1024 q sits in quarter t & 3 at index (t >> 2) + 256 q
+    const int pq = (tid & 3) * A4_QS + (tid >> 2);
+    typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
+    const __amdgpu_buffer_rsrc_t ry = __builtin_amdgcn_make_buffer_rsrc((void *)Y, (short)0, nb * M * 8, 0x00020000);
+    const float2 *zero = tw4096 + LQ_TW_N;
+    auto row_sample = [&](int b, int col) -> float2 {
+        return lq_load_hx(hist + HL, x, zero, b * M + col, HL, n_in);
+    };
+    // ring of column q: rows (newest - NS + 2 + u) in w[q][u], the oldest in
+    // wold (private to the lane); pf: the next group's rows, loaded after the
+    // transforms so they never sit beside a transform and the ring
+    float2 w[4][NS - 1], pf[G][4], wo[4];
+    const int cs = (int)blockIdx.x * S;
+    const int ce = cs + S < nb ? cs + S : nb;
+#pragma unroll
+    for (int q = 0; q < 4; q++) {
+#pragma unroll
+        for (int u = 0; u < NS - 1; u++) w[q][u] = row_sample(cs - NS + 1 + u, tid + 1024 * q);   // rows cs-P+1 .. cs-1
+        wold[q * 1024 + tid] = row_sample(cs - NS + 1, tid + 1024 * q);
+#pragma unroll
+        for (int g = 0; g < G; g++) pf[g][q] = row_sample(cs + g, tid + 1024 * q);
+    }
+    __syncthreads();   // tw2 ready
+    for (int b0 = cs; b0 < ce; b0 += G) {
+#pragma unroll
+        for (int g = 0; g < G; g++) {
+#pragma unroll
+            for (int q = 0; q < 4; q++) {
+                wo[q] = wold[q * 1024 + tid];   // row b - P + 1
+#pragma unroll
+                for (int u = 0; u < NS - 2; u++) w[q][u] = w[q][u + 1];
+                w[q][NS - 2] = pf[g][q];
+            }
+#pragma unroll
+            for (int q = 0; q < 4; q++) {
+                int o = (M - 1 - (tid + 1024 * q)) * P;
+                asm volatile("" : "+v"(o));   // taps re-read each row (L1 / L2 hits), not held across the transforms
+                const TC *h = hsub + o;
+                float2 acc = make_float2(0.f, 0.f);
+#pragma unroll
+                for (int n = 0; n < NS; n++) acc = pfb_mac(h[n], n < NS - 1 ? w[q][NS - 2 - n] : wo[q], acc);
+                xr[g * A4_BSTR + pq + 256 * q] = acc;
+                asm volatile("" ::: "memory");
+            }
+            // the next row's oldest (row b - P + 2) waits in LDS
+#pragma unroll
+            for (int q = 0; q < 4; q++) wold[q * 1024 + tid] = w[q][0];
+        }
+        __syncthreads();
+        if (wave < 4 * G) {   // block b0 + wave / 4, quarter wave % 4
+            float2 *Bq = xr + (wave >> 2) * A4_BSTR + (wave & 3) * A4_QS;
+            float2 v[16];
+#pragma unroll
+            for (int n = 0; n < 16; n++) v[n] = Bq[lane + 64 * n];
+            fft1024_wave_rt<+1>(v, Bq, a1, a4, tw2, lane);   // natural order at k + 4 (k >> 8)
+        }
+        __syncthreads();
+#pragma unroll
+        for (int g = 0; g < G; g++)
+#pragma unroll
+            for (int q = 0; q < 4; q++) pf[g][q] = row_sample(b0 + G + g, tid + 1024 * q);
+        {
+            const int k = tid;   // bin k of each quarter -> outputs k + 1024 s
+            const int pos = k + 4 * (k >> 8);
+            v2f W[4];
+#pragma unroll
+            for (int r = 1; r < 4; r++) W[r] = pk(tw4096[r * k]);   // W_4096^(r k), r k < 4096
+#pragma unroll
+            for (int g = 0; g < G; g++) {
+                const int b = b0 + g;
+                v2f T[4];
+#pragma unroll
+                for (int r = 0; r < 4; r++) T[r] = pk(xr[g * A4_BSTR + r * A4_QS + pos]);
+#pragma unroll
+                for (int r = 1; r < 4; r++) T[r] = pk_cmul(T[r], W[r]);
+                const v2f s02 = T[0] + T[2], d02 = T[0] - T[2], s13 = T[1] + T[3], d13 = T[1] - T[3];
+                const v2f jd13 = v2f{-d13.y, d13.x};   // i (T1 - T3)
+                const v2f Yo[4] = {s02 + s13, d02 - jd13, s02 - s13, d02 + jd13};
+                // a block past the run: a base the launch's range (< 2^31) never reaches
+                const unsigned base = b < ce ? (unsigned)b * (unsigned)(M * 8) : 0x80000000u;
+#pragma unroll
+                for (int sq = 0; sq < 4; sq++)
+                    __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2, Yo[sq]), ry,
+                                                          base + (unsigned)(k + 1024 * sq) * 8u, 0, 2);
+            }
+        }
+        __syncthreads();   // the combine's reads are done before the next group's writes
+    }
+}
+
+template <typename TC>
+bool launch_pfb_an4096(int p, const void *hsub, const void *hist, const void *x, long long nb, void *Y,
+                       hipStream_t st)
+{
+    constexpr int M = 4096;
+    if (nb * (long long)M * 8 >= (1ll << 31)) return false;
+    // one workgroup per CU: about 256 runs of S blocks (each warms up on the p - 1 rows before it)
+    long long S = (nb + 255) / 256;
+    if (S < 32) S = 32;
+    const unsigned grid = (unsigned)((nb + S - 1) / S);
+#define LQ_P4(PP)                                                                                          \
+    case PP:                                                                                               \
+        hipLaunchKernelGGL((k_pfb_an4096<PP, TC>), dim3(grid), dim3(1024), 0, st, (const TC *)hsub,        \
+                           (const float2 *)hist, (const float2 *)x, (int)(nb * M), (int)nb, (int)S, (float2 *)Y, \
+                           (const float2 *)lqrt_twiddles());                                              \
+        LQ_CHECK_LAUNCH();                                                                                 \
+        return true;
+    switch (p) {
+        LQ_P4(2) LQ_P4(4) LQ_P4(6) LQ_P4(8)
+    }
+#undef LQ_P4
+    return false;
+}
+
 // firpfbch analyzer, M = 64 / 128, fused as k_pfb_an_fused with Q = 256 / M
 // column sets per workgroup (each on its own run of blocks; every set runs
 // the same number of 16-block groups, stores past its run dropped) and the
@@ -2089,6 +2230,10 @@ extern "C" void lqk_firpfbch_analyzer(int ctaps, unsigned int M, unsigned int p,
     if (!getenv("LQ_PFB_TWO_PASS") &&
         (ctaps ? launch_pfb_an_fused<float2>((int)M, (int)p, hsub, hist, x, (long long)nblocks, Y, st)
                : launch_pfb_an_fused<float>((int)M, (int)p, hsub, hist, x, (long long)nblocks, Y, st)))
+        return;
+    if (M == 4096 && !getenv("LQ_PFB_TWO_PASS") &&
+        (ctaps ? launch_pfb_an4096<float2>((int)p, hsub, hist, x, (long long)nblocks, Y, st)
+               : launch_pfb_an4096<float>((int)p, hsub, hist, x, (long long)nblocks, Y, st)))
         return;
     if (!getenv("LQ_PFB_TWO_PASS") &&
         (ctaps ? launch_pfb_an_small<float2>((int)M, (int)p, hsub, hist, x, (long long)nblocks, Y, st)

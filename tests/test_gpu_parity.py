@@ -553,6 +553,40 @@ def test_firpfbch_analyzer_small_m_long_stream(M, m):
     assert G.nrm_err(y, ref) < NRM
 
 
+@pytest.mark.parametrize("m", [1, 2, 3, 4])
+def test_firpfbch_analyzer_m4096_long_stream(m):
+    # the fused M = 4096 analyzer (k_pfb_an4096: four columns per lane, one
+    # row per group, quarter transforms + radix-4 combine, the oldest ring
+    # row in LDS) over many workgroup runs in ragged calls
+    M = 4096
+    r = rng(3 * M + m)
+    nb = (1 << 22) // M + 23
+    x = cx(r, nb * M)
+    g = LQ.FirPfbch(LQ.LIQUID_ANALYZER, M, m=m, As=60.0)
+    o = O.FirPfbch(O.ANALYZER, M, m=m, As=60.0)
+    cuts = [0, 1, 333, nb - 3, nb]
+    y = np.concatenate([g.execute_block(x[a * M:b * M]) for a, b in zip(cuts[:-1], cuts[1:])])
+    ref = o.execute_block(x) if hasattr(o, "execute_block") else \
+        np.concatenate([o.execute(x[b * M:(b + 1) * M]) for b in range(nb)])
+    assert G.nrm_err(y, ref) < NRM
+
+
+def test_firpfbch_analyzer_m4096_cccf_complex_taps():
+    # k_pfb_an4096 with complex taps, pinned by linearity in the taps
+    M, p = 4096, 6
+    r = rng(4099)
+    h = cx(r, M * p)
+    nb = 300
+    x = cx(r, nb * M)
+    g = LQ.FirPfbch(LQ.LIQUID_ANALYZER, M, p=p, h=h, t="cccf")
+    o_re = O.FirPfbch(O.ANALYZER, M, p=p, h=h.real.copy())
+    o_im = O.FirPfbch(O.ANALYZER, M, p=p, h=h.imag.copy())
+    y = np.concatenate([g.execute(x[:M]), g.execute_block(x[M:])])
+    ref = np.concatenate([o_re.execute(x[b * M:(b + 1) * M]).astype(np.complex128)
+                          + 1j * o_im.execute(x[b * M:(b + 1) * M]) for b in range(nb)])
+    assert G.nrm_err(y, ref) < NRM
+
+
 @pytest.mark.parametrize("M,m", [(64, 1), (64, 4), (128, 3), (128, 8)])
 def test_firpfbch_synthesizer_small_m_long_stream(M, m):
     # the fused M = 64 / 128 synthesizer (k_pfb_syn_small): runs of blocks per
