@@ -1562,6 +1562,148 @@ bool launch_pfb_syn_fused(int M, int p, const void *hsub, const void *state, con
     return false;
 }
 
+// firpfbch synthesizer, M = 4096 fused (the two-pass path moved 48 B per
+// sample): z_b = IFFT(X_b) by quarters -- waves 0..4G-1 each load the bins
+// X_b[4i + r] of one block's quarter r straight from HBM and inverse-
+// transform them in registers (fft1024_wave_rt) -- then the radix-4 combine
+//     z[k + 1024 s] = sum_r W_4096^-(r k) Q_r[k] i^(r s)
+// leaves lane t exactly its own columns t + 1024 s, so the p-tap output
+// y_b[col] = sum_n h[col p + n] z_{b-n}[col] (firpfbch.c:314-336) runs from
+// a register ring (its oldest entry in LDS across the transforms) with no
+// further LDS traffic.  Runs warm up on the blocks before them (transformed
+// again, outputs dropped) or, for the call's first run, on the object's last
+// p-1 transforms (state); the z of the call's last p-1 blocks go to znew.
+template <int P, typename TC, int G = 3>
+__global__ __launch_bounds__(1024, 1) void k_pfb_syn4096(const TC *__restrict__ hsub, const float2 *__restrict__ state,
+                                                         const float2 *__restrict__ X, int nb, int S,
+                                                         float2 *__restrict__ y, float2 *__restrict__ znew,
+                                                         const float2 *__restrict__ tw4096)
+{
+    constexpr int M = 4096, HB = P - 1, NR = P > 2 ? P - 2 : 1;
+    constexpr int NW = G * ((HB + G - 1) / G);   // warm-up blocks before a run (whole groups)
+    static_assert(P >= 2, "two taps per column at least");
+    __shared__ __attribute__((aligned(16))) float2 xr[G * A4_BSTR];
+    __shared__ __attribute__((aligned(16))) float2 tw2[64];
+    __shared__ __attribute__((aligned(16))) float2 wold[4 * 1024];
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    if (tid < 64) {   // W_64^{-b r} (inverse transform)
+        const float2 u = tw4096[(64 * (tid & 3) * (tid >> 2)) & 4095];
+        tw2[tid] = make_float2(u.x, -u.y);
+    }
+    const float2 a1 = tw4096[(4 * lane) & 4095], a4 = tw4096[(16 * lane) & 4095];
+    typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
+    const __amdgpu_buffer_rsrc_t ry = __builtin_amdgcn_make_buffer_rsrc((void *)y, (short)0, nb * M * 8, 0x00020000);
+    const int cs = (int)blockIdx.x * S;
+    const int ce = cs + S < nb ? cs + S : nb;
+    // ring of column t + 1024 q before block b: wold = z_{b-P+1}, r[q][u] =
+    // z_{b-P+2+u} (u < P-2)
+    float2 r[4][NR];
+    int b0 = cs;
+    if (cs == 0) {   // the state's last p-1 transforms
+#pragma unroll
+        for (int q = 0; q < 4; q++) {
+            const int col = tid + 1024 * q;
+            wold[q * 1024 + tid] = state[col];
+#pragma unroll
+            for (int u = 0; u < P - 2; u++) r[q][u] = state[(1 + u) * M + col];
+        }
+    } else {
+        b0 = cs - NW;   // warm-up groups: transformed, outputs dropped
+#pragma unroll
+        for (int q = 0; q < 4; q++) {
+            wold[q * 1024 + tid] = make_float2(0.f, 0.f);
+#pragma unroll
+            for (int u = 0; u < NR; u++) r[q][u] = make_float2(0.f, 0.f);
+        }
+    }
+    __syncthreads();   // tw2 ready
+    for (; b0 < ce; b0 += G) {
+        if (wave < 4 * G) {   // block b0 + wave / 4, quarter wave % 4
+            const int g = wave >> 2, rq = wave & 3;
+            const int b = b0 + g < nb ? b0 + g : nb - 1;
+            const float2 *xb = X + (long long)b * M + rq;
+            float2 v[16];
+#pragma unroll
+            for (int n = 0; n < 16; n++) v[n] = xb[4 * (lane + 64 * n)];
+            float2 *Bq = xr + g * A4_BSTR + rq * A4_QS;
+            fft1024_wave_rt<-1>(v, Bq, a1, a4, tw2, lane);   // natural order at k + 4 (k >> 8)
+        }
+        __syncthreads();
+        {
+            const int k = tid, pos = k + 4 * (k >> 8);
+            v2f W[4];
+#pragma unroll
+            for (int rr = 1; rr < 4; rr++) {
+                const float2 u = tw4096[rr * k];   // W_4096^(r k), r k < 4096
+                W[rr] = v2f{u.x, -u.y};
+            }
+#pragma unroll
+            for (int g = 0; g < G; g++) {
+                const int b = b0 + g;
+                v2f T[4];
+#pragma unroll
+                for (int rr = 0; rr < 4; rr++) T[rr] = pk(xr[g * A4_BSTR + rr * A4_QS + pos]);
+#pragma unroll
+                for (int rr = 1; rr < 4; rr++) T[rr] = pk_cmul(T[rr], W[rr]);
+                const v2f s02 = T[0] + T[2], d02 = T[0] - T[2], s13 = T[1] + T[3], d13 = T[1] - T[3];
+                const v2f jd13 = v2f{-d13.y, d13.x};   // i (T1 - T3)
+                const v2f z[4] = {s02 + s13, d02 + jd13, s02 - s13, d02 - jd13};   // columns t + 1024 s
+                const bool out = b >= cs && b < ce;
+                const unsigned base = out ? (unsigned)b * (unsigned)(M * 8) : 0x80000000u;
+#pragma unroll
+                for (int q = 0; q < 4; q++) {
+                    const int col = tid + 1024 * q;
+                    int o = col * P;
+                    asm volatile("" : "+v"(o));   // taps re-read per block (L1 / L2 hits)
+                    const TC *h = hsub + o;
+                    const float2 zo = wold[q * 1024 + tid];
+                    float2 acc = pfb_mac(h[0], unpk(z[q]), make_float2(0.f, 0.f));
+#pragma unroll
+                    for (int n = 1; n < P - 1; n++) acc = pfb_mac(h[n], r[q][P - 2 - n], acc);
+                    acc = pfb_mac(h[P - 1], zo, acc);
+                    __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2, pk(acc)), ry,
+                                                          base + (unsigned)col * 8u, 0, 2);
+                    if (out && b >= nb - HB) znew[(long long)(b - (nb - HB)) * M + col] = unpk(z[q]);
+                    // advance the ring: z_{b-P+2} becomes the LDS-held oldest
+                    if constexpr (P > 2) {
+                        wold[q * 1024 + tid] = r[q][0];
+#pragma unroll
+                        for (int u = 0; u < P - 3; u++) r[q][u] = r[q][u + 1];
+                        r[q][P - 3] = unpk(z[q]);
+                    } else {
+                        wold[q * 1024 + tid] = unpk(z[q]);
+                    }
+                }
+            }
+        }
+        __syncthreads();   // the combine's reads are done before the next group's transforms
+    }
+}
+
+template <typename TC>
+bool launch_pfb_syn4096(int p, const void *hsub, const void *state, const void *X, long long nb, void *y, void *znew,
+                        hipStream_t st)
+{
+    constexpr int M = 4096;
+    if (nb < p || nb * (long long)M * 8 >= (1ll << 31)) return false;
+    long long S = (nb + 255) / 256;
+    S = (S + 2) / 3 * 3;
+    if (S < 33) S = 33;
+    const unsigned grid = (unsigned)((nb + S - 1) / S);
+#define LQ_S4(PP)                                                                                          \
+    case PP:                                                                                               \
+        hipLaunchKernelGGL((k_pfb_syn4096<PP, TC>), dim3(grid), dim3(1024), 0, st, (const TC *)hsub,       \
+                           (const float2 *)state, (const float2 *)X, (int)nb, (int)S, (float2 *)y,         \
+                           (float2 *)znew, (const float2 *)lqrt_twiddles());                              \
+        LQ_CHECK_LAUNCH();                                                                                 \
+        return true;
+    switch (p) {
+        LQ_S4(2) LQ_S4(4) LQ_S4(6) LQ_S4(8)
+    }
+#undef LQ_S4
+    return false;
+}
+
 // firpfbch synthesizer, M = 64 / 128, fused as k_pfb_syn_fused with Q = 256
 // / M column sets per workgroup on their own runs of blocks, the 16 Q inverse
 // transforms of a group on M / 16 lanes each (fft_small16xR).  Every set runs
@@ -2269,6 +2411,12 @@ extern "C" void lqk_firpfbch_synthesizer(int ctaps, unsigned int M, unsigned int
     if (!getenv("LQ_PFB_TWO_PASS") &&
         (ctaps ? launch_pfb_syn_fused<float2>((int)M, (int)p, hsub, state, X, (long long)nblocks, y, Z, st)
                : launch_pfb_syn_fused<float>((int)M, (int)p, hsub, state, X, (long long)nblocks, y, Z, st))) {
+        if (HB > 0) LQ_CHECK(hipMemcpyAsync(state, Z, HB * M * sizeof(float2), hipMemcpyDeviceToDevice, st));
+        return;
+    }
+    if (M == 4096 && !getenv("LQ_PFB_TWO_PASS") &&
+        (ctaps ? launch_pfb_syn4096<float2>((int)p, hsub, state, X, (long long)nblocks, y, Z, st)
+               : launch_pfb_syn4096<float>((int)p, hsub, state, X, (long long)nblocks, y, Z, st))) {
         if (HB > 0) LQ_CHECK(hipMemcpyAsync(state, Z, HB * M * sizeof(float2), hipMemcpyDeviceToDevice, st));
         return;
     }

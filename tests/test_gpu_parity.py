@@ -571,20 +571,42 @@ def test_firpfbch_analyzer_m4096_long_stream(m):
     assert G.nrm_err(y, ref) < NRM
 
 
-def test_firpfbch_analyzer_m4096_cccf_complex_taps():
-    # k_pfb_an4096 with complex taps, pinned by linearity in the taps
+@pytest.mark.parametrize("m", [1, 2, 3, 4])
+def test_firpfbch_synthesizer_m4096_long_stream(m):
+    # the fused M = 4096 synthesizer (k_pfb_syn4096: quarter transforms
+    # loaded straight from X, radix-4 combine into the lane's own columns,
+    # register ring): runs warm up on the blocks before them or on the
+    # object's state; a short call (fewer blocks than p: two-pass path)
+    # carries the state between fused calls
+    M = 4096
+    r = rng(13 * M + m)
+    nb = (1 << 22) // M + 23
+    x = cx(r, nb * M)
+    g = LQ.FirPfbch(LQ.LIQUID_SYNTHESIZER, M, m=m, As=60.0)
+    o = O.FirPfbch(O.SYNTHESIZER, M, m=m, As=60.0)
+    cuts = [0, 1, 333, nb - 3, nb]
+    y = np.concatenate([g.execute_block(x[a * M:b * M]) for a, b in zip(cuts[:-1], cuts[1:])])
+    ref = o.execute_block(x) if hasattr(o, "execute_block") else \
+        np.concatenate([o.execute(x[b * M:(b + 1) * M]) for b in range(nb)])
+    assert G.nrm_err(y, ref) < NRM
+
+
+@pytest.mark.parametrize("typ", [LQ.LIQUID_ANALYZER, LQ.LIQUID_SYNTHESIZER])
+def test_firpfbch_m4096_cccf_complex_taps(typ):
+    # the fused M = 4096 kernels with complex taps, pinned by linearity in the taps
     M, p = 4096, 6
-    r = rng(4099)
+    r = rng(4099 + typ)
     h = cx(r, M * p)
     nb = 300
     x = cx(r, nb * M)
-    g = LQ.FirPfbch(LQ.LIQUID_ANALYZER, M, p=p, h=h, t="cccf")
-    o_re = O.FirPfbch(O.ANALYZER, M, p=p, h=h.real.copy())
-    o_im = O.FirPfbch(O.ANALYZER, M, p=p, h=h.imag.copy())
+    g = LQ.FirPfbch(typ, M, p=p, h=h, t="cccf")
+    o_re = O.FirPfbch(typ, M, p=p, h=h.real.copy())
+    o_im = O.FirPfbch(typ, M, p=p, h=h.imag.copy())
     y = np.concatenate([g.execute(x[:M]), g.execute_block(x[M:])])
     ref = np.concatenate([o_re.execute(x[b * M:(b + 1) * M]).astype(np.complex128)
                           + 1j * o_im.execute(x[b * M:(b + 1) * M]) for b in range(nb)])
     assert G.nrm_err(y, ref) < NRM
+
 
 
 @pytest.mark.parametrize("M,m", [(64, 1), (64, 4), (128, 3), (128, 8)])
