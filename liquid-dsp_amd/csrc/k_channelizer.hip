@@ -1887,6 +1887,156 @@ __global__ __launch_bounds__(256 * R, R == 1 ? 2 : 1) void k_pfb2_syn_fused(cons
     }
 }
 
+// firpfbch2 synthesizer, M = 4096 fused: the z transforms as in
+// k_pfb_syn4096 (quarters of X straight from HBM, radix-4 combine into the
+// lane's own columns t + 1024 s, scaled 1/M then M/2 as firpfbch2.c:303-307).
+// Output i < M/2 of block b (parity f) is
+//     y_b[i] = sum_n h0[n] z_{b-2n}[c] + h1[n] z_{b-1-2n}[c],  c = i + f M/2
+// (h0 = h[i + nM], h1 = h[i + M/2 + nM]), so column c only ever feeds the
+// outputs of blocks of one parity; a 2L-deep ring of z per column (4 columns
+// x 16 x 8 B per lane at m = 4) would not fit, so each column keeps the L
+// partial outputs it still feeds instead (transposed form): z_b[c] adds
+// h0[j] z_b[c] to the block b + 2j output when b has c's parity (then that
+// output is complete and leaves), else h1[j] z_b[c] to block b + 1 + 2j.
+template <int L, int G = 3>
+__global__ __launch_bounds__(1024, 1) void k_pfb2_syn4096(const float *__restrict__ hsub,
+                                                          const float2 *__restrict__ state,
+                                                          const float2 *__restrict__ X, int nb, int p0, int S,
+                                                          float2 *__restrict__ y, float2 *__restrict__ znew,
+                                                          const float2 *__restrict__ tw4096)
+{
+    constexpr int M = 4096, M2 = 2048, HB = 2 * L - 1;
+    constexpr int NW = G * ((HB + G - 1) / G);   // warm-up blocks before a run (whole groups)
+    __shared__ __attribute__((aligned(16))) float2 xr[G * A4_BSTR];
+    __shared__ __attribute__((aligned(16))) float2 tw2[64];
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    if (tid < 64) {   // W_64^{-b r} (inverse transform)
+        const float2 u = tw4096[(64 * (tid & 3) * (tid >> 2)) & 4095];
+        tw2[tid] = make_float2(u.x, -u.y);
+    }
+    const float2 a1 = tw4096[(4 * lane) & 4095], a4 = tw4096[(16 * lane) & 4095];
+    const float s1 = 1.0f / (float)M, s2 = (float)M2;
+    typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
+    const __amdgpu_buffer_rsrc_t ry = __builtin_amdgcn_make_buffer_rsrc((void *)y, (short)0, nb * M2 * 8, 0x00020000);
+    const int cs = (int)blockIdx.x * S;
+    const int ce = cs + S < nb ? cs + S : nb;
+    // column q = t + 1024 q of this lane: q < 2 feeds even-parity blocks
+    // (output i = col), q >= 2 odd ones (output i = col - M/2)
+    v2f A[4][L];
+#pragma unroll
+    for (int q = 0; q < 4; q++)
+#pragma unroll
+        for (int j = 0; j < L; j++) A[q][j] = v2f{0.f, 0.f};
+    // one z vector (this lane's four columns) of block b into the partial outputs
+    auto feed = [&](int b, const v2f (&z)[4], bool emit) {
+        const int f = (p0 + b) & 1;
+        const bool out = emit && b >= cs && b < ce;
+        const unsigned base = out ? (unsigned)b * (unsigned)(M2 * 8) : 0x80000000u;
+#pragma unroll
+        for (int q = 0; q < 4; q++) {
+            const int fc = q >> 1, i = tid + 1024 * (q & 1);
+            // taps h0 (same parity) or h1, re-read per block (L1 / L2 hits)
+            int o = (f == fc ? i : i + M2) * L;
+            asm volatile("" : "+v"(o));
+            const float *h = hsub + o;
+#pragma unroll
+            for (int j = 0; j < L; j++) A[q][j] = v2f{h[j], h[j]} * z[q] + A[q][j];
+            if (f == fc) {
+                __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2, A[q][0]), ry, base + (unsigned)i * 8u, 0, 2);
+#pragma unroll
+                for (int j = 0; j < L - 1; j++) A[q][j] = A[q][j + 1];
+                A[q][L - 1] = v2f{0.f, 0.f};
+            }
+        }
+    };
+    int b0 = cs;
+    if (cs == 0) {   // the state's 2L-1 transforms (blocks -HB .. -1)
+        for (int b = -HB; b < 0; b++) {
+            v2f z[4];
+#pragma unroll
+            for (int q = 0; q < 4; q++) z[q] = pk(state[(long long)(HB + b) * M + tid + 1024 * q]);
+            feed(b, z, false);
+        }
+    } else {
+        b0 = cs - NW;   // warm-up groups: transformed, outputs dropped
+    }
+    __syncthreads();   // tw2 ready
+    for (; b0 < ce; b0 += G) {
+        if (wave < 4 * G) {   // block b0 + wave / 4, quarter wave % 4
+            const int g = wave >> 2, rq = wave & 3;
+            int b = b0 + g < nb ? b0 + g : nb - 1;
+            b = b < 0 ? 0 : b;
+            const float2 *xb = X + (long long)b * M + rq;
+            float2 v[16];
+#pragma unroll
+            for (int n = 0; n < 16; n++) v[n] = xb[4 * (lane + 64 * n)];
+            float2 *Bq = xr + g * A4_BSTR + rq * A4_QS;
+            fft1024_wave_rt<-1>(v, Bq, a1, a4, tw2, lane);   // natural order at k + 4 (k >> 8)
+        }
+        __syncthreads();
+        {
+            const int k = tid, pos = k + 4 * (k >> 8);
+            v2f W[4];
+#pragma unroll
+            for (int rr = 1; rr < 4; rr++) {
+                const float2 u = tw4096[rr * k];   // W_4096^(r k), r k < 4096
+                W[rr] = v2f{u.x, -u.y};
+            }
+#pragma unroll
+            for (int g = 0; g < G; g++) {
+                const int b = b0 + g;
+                v2f T[4];
+#pragma unroll
+                for (int rr = 0; rr < 4; rr++) T[rr] = pk(xr[g * A4_BSTR + rr * A4_QS + pos]);
+#pragma unroll
+                for (int rr = 1; rr < 4; rr++) T[rr] = pk_cmul(T[rr], W[rr]);
+                const v2f s02 = T[0] + T[2], d02 = T[0] - T[2], s13 = T[1] + T[3], d13 = T[1] - T[3];
+                const v2f jd13 = v2f{-d13.y, d13.x};   // i (T1 - T3)
+                v2f z[4] = {s02 + s13, d02 + jd13, s02 - s13, d02 - jd13};   // columns t + 1024 s
+#pragma unroll
+                for (int q = 0; q < 4; q++) z[q] = (z[q] * s1) * s2;
+                if (b < ce && b >= 0) {
+                    feed(b, z, true);
+                    if (b >= cs && b >= nb - HB) {
+#pragma unroll
+                        for (int q = 0; q < 4; q++) znew[(long long)(b - (nb - HB)) * M + tid + 1024 * q] = unpk(z[q]);
+                    }
+                }
+            }
+        }
+        __syncthreads();   // the combine's reads are done before the next group's transforms
+    }
+}
+
+template <int L>
+bool launch_pfb2_syn4096_l(const void *hsub, const void *state, const void *X, long long nb, int p0, void *y,
+                           void *znew, hipStream_t st)
+{
+    constexpr int M = 4096;
+    long long S = (nb + 255) / 256;
+    S = (S + 2) / 3 * 3;
+    if (S < 33) S = 33;
+    const unsigned grid = (unsigned)((nb + S - 1) / S);
+    hipLaunchKernelGGL((k_pfb2_syn4096<L>), dim3(grid), dim3(1024), 0, st, (const float *)hsub, (const float2 *)state,
+                       (const float2 *)X, (int)nb, p0, (int)S, (float2 *)y, (float2 *)znew,
+                       (const float2 *)lqrt_twiddles());
+    LQ_CHECK_LAUNCH();
+    (void)M;
+    return true;
+}
+
+bool launch_pfb2_syn4096(int m, const void *hsub, const void *state, const void *X, long long nb, int p0, void *y,
+                         void *znew, hipStream_t st)
+{
+    if (m < 1 || m > 4 || nb < 4 * m - 1 || nb * 4096ll * 8 >= (1ll << 31)) return false;
+    switch (m) {
+    case 1: return launch_pfb2_syn4096_l<2>(hsub, state, X, nb, p0, y, znew, st);
+    case 2: return launch_pfb2_syn4096_l<4>(hsub, state, X, nb, p0, y, znew, st);
+    case 3: return launch_pfb2_syn4096_l<6>(hsub, state, X, nb, p0, y, znew, st);
+    default: return launch_pfb2_syn4096_l<8>(hsub, state, X, nb, p0, y, znew, st);
+    }
+}
+
 bool launch_pfb2_syn_fused(int M, int m, const void *hsub, const void *state, const void *X, long long nb, int p0,
                            void *y, void *znew, hipStream_t st)
 {
@@ -2335,6 +2485,11 @@ extern "C" void lqk_firpfbch2_synthesizer(unsigned int M, unsigned int m, const 
     hipStream_t st = (hipStream_t)stream;
     const long long HB = 4 * (long long)m - 1;
     float2 *Z = (float2 *)zscratch;
+    if (!getenv("LQ_PFB2_TWO_PASS") && M == 4096 &&
+        launch_pfb2_syn4096((int)m, hsub, state, X, (long long)nblocks, p0, Y, Z, st)) {
+        LQ_CHECK(hipMemcpyAsync(state, Z, HB * M * sizeof(float2), hipMemcpyDeviceToDevice, st));
+        return;
+    }
     if (!getenv("LQ_PFB2_TWO_PASS") &&
         launch_pfb2_syn_fused((int)M, (int)m, hsub, state, X, (long long)nblocks, p0, Y, Z, st)) {
         LQ_CHECK(hipMemcpyAsync(state, Z, HB * M * sizeof(float2), hipMemcpyDeviceToDevice, st));

@@ -490,6 +490,24 @@ def test_firpfbch2_synthesizer_m256_512_fused(M, m):
     assert G.nrm_err(y, o.execute_block(X)) < NRM
 
 
+@pytest.mark.parametrize("m", [1, 2, 3, 4])
+def test_firpfbch2_synthesizer_m4096_fused(m):
+    # k_pfb2_syn4096 (quarter transforms, radix-4 combine into the lane's
+    # columns, L partial outputs per column): many runs per call (each
+    # warming up on the blocks before it), an odd first call so the next
+    # starts on the other block parity, a short call below 4m-1 blocks
+    # (two-pass path) carrying the state between fused calls
+    M = 4096
+    r = rng(M + 7 * m)
+    nb = 1200
+    X = cx(r, nb * M)
+    g = LQ.FirPfbch2(LQ.LIQUID_SYNTHESIZER, M, m, 60.0)
+    o = O.FirPfbch2(O.SYNTHESIZER, M, m, 60.0)
+    cuts = [0, 401, 402, nb]
+    y = np.concatenate([g.execute_block(X[a * M:b * M]) for a, b in zip(cuts[:-1], cuts[1:])])
+    assert G.nrm_err(y, o.execute_block(X)) < NRM
+
+
 @pytest.mark.parametrize("m", [4, 2])
 def test_firpfbch2_synthesizer_m1024_many_workgroups(m):
     # k_pfb2_syn1024: 701 blocks over ~22 workgroups (history rebuilt from the
