@@ -1573,7 +1573,10 @@ bool launch_pfb_syn_fused(int M, int p, const void *hsub, const void *state, con
 // further LDS traffic.  Runs warm up on the blocks before them (transformed
 // again, outputs dropped) or, for the call's first run, on the object's last
 // p-1 transforms (state); the z of the call's last p-1 blocks go to znew.
-template <int P, typename TC, int G = 3>
+#ifndef A4_SYN_G8
+#define A4_SYN_G8 3   // p = 8: three-block groups spill 18 VGPRs and still beat two-block groups (0.585 vs 0.615 ms)
+#endif
+template <int P, typename TC, int G = (P > 6 ? A4_SYN_G8 : 3)>
 __global__ __launch_bounds__(1024, 1) void k_pfb_syn4096(const TC *__restrict__ hsub, const float2 *__restrict__ state,
                                                          const float2 *__restrict__ X, int nb, int S,
                                                          float2 *__restrict__ y, float2 *__restrict__ znew,
