@@ -2015,8 +2015,7 @@ template <int L>
 bool launch_pfb2_syn4096_l(const void *hsub, const void *state, const void *X, long long nb, int p0, void *y,
                            void *znew, hipStream_t st)
 {
-    constexpr int M = 4096;
-    long long S = (nb + 255) / 256;
+    long long S = (nb + 255) / 256;   // about 256 runs (one workgroup per CU), whole groups of three
     S = (S + 2) / 3 * 3;
     if (S < 33) S = 33;
     const unsigned grid = (unsigned)((nb + S - 1) / S);
@@ -2024,7 +2023,6 @@ bool launch_pfb2_syn4096_l(const void *hsub, const void *state, const void *X, l
                        (const float2 *)X, (int)nb, p0, (int)S, (float2 *)y, (float2 *)znew,
                        (const float2 *)lqrt_twiddles());
     LQ_CHECK_LAUNCH();
-    (void)M;
     return true;
 }
 
