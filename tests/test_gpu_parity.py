@@ -1246,6 +1246,28 @@ def test_spgram_device_estimate_long():
     assert _db_close(dp.to_array(np.float32, nfft), o.estimate_psd(x))
 
 
+def test_spgram_device_estimate_full_round():
+    # 2^26 samples, a 512-sample window: 2^19 transforms through the fused
+    # kernel (lqk_spgram_fused1024: 8192 chunks of 64, two fold levels)
+    n, nfft = (1 << 26) + 12345, 1024
+    r = rng(78)
+    x = cx(r, n)
+    win = _kaiser_window(nfft // 2, 10.0)
+    g = LQ.Spgram(nfft, win)
+    o = O.Spgram(nfft, win)
+    dx = LQ.DeviceBuffer.from_array(x)
+    dp = LQ.DeviceBuffer(nfft * 4)
+    LQ.lib().spgramcf_estimate_psd_dev(g.q, dx.p, n, dp.p)
+    LQ.lib().spgramcf_synchronize(g.q)
+    # tolerance 1e-4, not NRM: the oracle (like the reference, spgram.c)
+    # sums the 2^19 periodograms serially in float32, whose own rounding is
+    # ~sqrt(T) eps ~ 4e-5 relative here; the kernel's two-level fold is the
+    # more accurate of the two (observed difference ~1e-5)
+    a = 10 ** (dp.to_array(np.float32, nfft).astype(np.float64) / 10)
+    b = 10 ** (np.asarray(o.estimate_psd(x), np.float64) / 10)
+    assert G.nrm_err(a, b) < 1e-4
+
+
 # ------------------------------------------------ launch-chunk boundaries
 # The fast kernels split very long calls into launches of 2^17 / 2^18 blocks
 # (firpfbch / firpfbch2) or 2^27 samples (fftfilt) so that 32-bit buffer
