@@ -280,6 +280,9 @@ __device__ __forceinline__ rs_ref rs_locate_near(const lqk_rs_plan &pl, unsigned
 // 0.236 -> 0.221 ms against five); longer filters spill at 80 VGPRs
 template <int L>
 constexpr int rs2_blk() { return L <= 16 ? 6 : 5; }
+#ifndef RS_O32
+#define RS_O32 1   // power-of-two replay: 32-bit output slot counter (A/B on one box: 0.213 vs 0.216 ms per 2^25 inputs)
+#endif
 #ifndef RS_CAPX
 #define RS_CAPX 64    // output slots per tile beyond TIN (r = 1.037: <= 1066 outputs per 1024 inputs)
 #endif
@@ -434,6 +437,30 @@ __global__ __launch_bounds__(NT, rs2_blk<L>()) void k_resamp2(lqk_rs_plan pl, un
                 }
                 Kb = ((unsigned long long)(unsigned)__builtin_amdgcn_readlane((int)(k >> 32), 0) << 32) |
                      (unsigned)__builtin_amdgcn_readlane((int)k, 0);
+#if RS_O32
+                // the lane's output slot as a 32-bit counter (a 64-bit k and
+                // its compare per output before); an offset at or past 2^30
+                // stays past CAP through the lane's outputs, as before
+                {
+                    const unsigned long long o64 = k - Kb;
+                    const int o0 = o64 < (1ull << 30) ? (int)o64 : (1 << 30);
+                    int o = o0;
+                    for (int r = 0; r < nin; r++) {
+                        const int iloc = (int)(ia + r - i0);
+                        while (xx < z) {
+                            const float bf = xx * fnpfb;
+                            const float fb = __builtin_floorf(bf);
+                            if (!(RS_EXP & 4))
+                                desc[(unsigned)o < (unsigned)CAP ? o : CAP] = make_uint2(
+                                    __float_as_uint(bf - fb), (unsigned)iloc | ((unsigned)(xx < 0.0f ? npfb : (int)fb) << 12));
+                            o++;
+                            xx = xx + del;
+                        }
+                        xx = xx - 1.0f;
+                    }
+                    k += (unsigned long long)(o - o0);
+                }
+#else
                 for (int r = 0; r < nin; r++) {
                     const int iloc = (int)(ia + r - i0);
                     while (xx < z) {
@@ -445,6 +472,7 @@ __global__ __launch_bounds__(NT, rs2_blk<L>()) void k_resamp2(lqk_rs_plan pl, un
                     }
                     xx = xx - 1.0f;
                 }
+#endif
             } else {
                 rs_state st;
                 rs_entry(e, st);
