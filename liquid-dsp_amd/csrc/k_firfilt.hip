@@ -717,6 +717,25 @@ int tile_of(int) { return TILE; }
 // 163 600-byte request dispatched as 163 856 bytes and faulted)
 constexpr size_t FIR_LDS_MAX = 160 * 1024 - 1024;
 
+// the kernel's static group segment (queried once per instantiation)
+template <int KIND, int HC>
+size_t fir_static_lds()
+{
+    static const size_t v = [] {
+        hipFuncAttributes a;
+        LQ_CHECK(hipFuncGetAttributes(&a, reinterpret_cast<const void *>(&k_firfilt<KIND, HC>)));
+        return (size_t)a.sharedSizeBytes;
+    }();
+    return v;
+}
+
+// the one rule for both the create-time limit and the launch: dynamic LDS
+// within the budget and, with the static segment on top, within the CU's 160 KB
+inline bool fir_lds_fits(size_t lds, size_t lds_static)
+{
+    return lds <= FIR_LDS_MAX && lds + lds_static <= 160 * 1024;
+}
+
 template <int KIND, int HC>
 void launch_firfilt(const lqk_fir_desc *d, const void *hist, const void *x, long long n, void *y,
                     const void *halo, hipStream_t st)
@@ -726,12 +745,7 @@ void launch_firfilt(const lqk_fir_desc *d, const void *hist, const void *x, long
     const int HP = HC * (int)d->nchunk;
     const long long ntiles = (n + TILE - 1) / TILE;
     const size_t lds = (size_t)lds_bytes<T>(TILE + HP);
-    static const size_t lds_static = [] {
-        hipFuncAttributes a;
-        LQ_CHECK(hipFuncGetAttributes(&a, reinterpret_cast<const void *>(&k_firfilt<KIND, HC>)));
-        return a.sharedSizeBytes;
-    }();
-    if (lds > FIR_LDS_MAX || lds + lds_static > 160 * 1024) {
+    if (!fir_lds_fits(lds, fir_static_lds<KIND, HC>())) {
         fprintf(stderr, "error: firfilt: filter length %u exceeds the GPU tile limit\n", d->hlen);
         exit(1);
     }
@@ -761,11 +775,13 @@ size_t elem_size(int kind) { return kind == 0 ? sizeof(float) : sizeof(float2); 
 
 extern "C" unsigned int lqk_firfilt_max_history(int kind)
 {
-    // lds_bytes(TILE + HP) <= 160 KB; HP a multiple of 64
+    // the launch rule (fir_lds_fits) for the HC = 64 kernel, which every
+    // filter past 32 taps runs; HP a multiple of 64
+    const size_t st = kind == 0 ? fir_static_lds<0, 64>() : (kind == 1 ? fir_static_lds<1, 64>() : fir_static_lds<2, 64>());
     unsigned int hp = 0;
     for (;;) {
         const size_t b = kind == 0 ? (size_t)lds_bytes<float>(TILE + hp + 64) : (size_t)lds_bytes<float2>(TILE + hp + 64);
-        if (b > FIR_LDS_MAX) return hp;
+        if (!fir_lds_fits(b, st)) return hp;
         hp += 64;
     }
 }

@@ -12,10 +12,13 @@
 // Parallel form.  The timing state at the start of every input is a pure
 // function of the previous one (it does not depend on the data), so the host
 // tabulates it once per rate (`plan`, see host/resamp.c): checkpoint c holds
-// (tau, mu, b, state) before input 32c and K = outputs emitted by the inputs
-// before it; the sequence is eventually periodic (pre-period `pre`, period
-// `P` inputs, `Q` outputs per period).  Lanes read the checkpoint at or before
-// their first input (16 B per 32 inputs: 0.5 B / input of plan traffic), step
+// the state before input LQK_RS_CK c (LQK_RS_CK = 16) and K = outputs emitted
+// by the inputs before it -- (tau, K), 8 B, for power-of-two bank counts with
+// del >= 1/npfb (the rest of the state follows from tau), else
+// (tau, mu, b, state, K), 16 B; the sequence is eventually periodic
+// (pre-period `pre`, period `P` inputs, `Q` outputs per period).  Lanes read
+// the checkpoint at or before their first input (0.5 B / input of plan
+// traffic for 8-byte checkpoints), step
 // the reference's float32 recurrence forward to it and replay their own
 // inputs, bit-exactly (contraction off).  k_resamp2 (the default) turns the replay into a
 // dense per-tile output list and evaluates it with coalesced stores;
@@ -69,7 +72,7 @@ __device__ __forceinline__ void rs_advance(rs_state &s, float del, float fnpfb)
 __device__ __forceinline__ unsigned rs_step(rs_state &s, float del, float fnpfb, int npfb)
 {
     unsigned n = 0;
-    while (s.b < npfb) {
+    while ((unsigned)s.b < (unsigned)npfb) {   // unsigned, as resamp.c:254 (int b vs unsigned npfb)
         if (s.st && s.b == npfb - 1) {
             s.st = 0;
             s.b = npfb;
@@ -80,7 +83,7 @@ __device__ __forceinline__ unsigned rs_step(rs_state &s, float del, float fnpfb,
         s.st = 1;
     }
     s.tau -= 1.0f;
-    s.b -= npfb;
+    s.b = (int)((unsigned)s.b - (unsigned)npfb);
     return n;
 }
 
@@ -188,7 +191,7 @@ __global__ __launch_bounds__(NT) void k_resamp(lqk_rs_plan pl, unsigned long lon
 #pragma unroll
     for (int r = 0; r < RS_R; ++r) {
         if (i0 + r >= n) break;
-        while (s.b < npfb) {
+        while ((unsigned)s.b < (unsigned)npfb) {
             if (s.st && s.b == npfb - 1) { // last filter: finish with the next input
                 s.st = 0;
                 s.b = npfb;
@@ -210,7 +213,7 @@ __global__ __launch_bounds__(NT) void k_resamp(lqk_rs_plan pl, unsigned long lon
             s.st = 1;
         }
         s.tau -= 1.0f;
-        s.b -= npfb;
+        s.b = (int)((unsigned)s.b - (unsigned)npfb);
     }
 }
 
@@ -278,8 +281,11 @@ __device__ __forceinline__ rs_ref rs_locate_near(const lqk_rs_plan &pl, unsigned
 #endif
 // workgroups per CU: six for L <= 16 (25.5 KB LDS, <= 80 VGPRs each: L = 14
 // 0.236 -> 0.221 ms against five); longer filters spill at 80 VGPRs
+#ifndef RS_BLK
+#define RS_BLK 5
+#endif
 template <int L>
-constexpr int rs2_blk() { return L <= 16 ? 6 : 5; }
+constexpr int rs2_blk() { return L <= 16 ? RS_BLK : 5; }
 #ifndef RS_O32
 #define RS_O32 1   // power-of-two replay: 32-bit output slot counter (A/B on one box: 0.213 vs 0.216 ms per 2^25 inputs)
 #endif
@@ -289,16 +295,113 @@ constexpr int rs2_blk() { return L <= 16 ? 6 : 5; }
 template <int L>
 constexpr int rs2_tin() { return NT * RS_RIN; }
 constexpr int rs2_cap() { return NT * RS_RIN + RS_CAPX; }
-// LDS bytes of k_resamp2<L, S>: window copy, output descriptors, pair table
-template <int L, typename S>
+#ifndef RS_ALD
+#define RS_ALD 1   // evaluation reads as single ds_read_b64 (relaxed workgroup atomics: never paired into ds_read2_b64)
+#endif
+#ifndef RS_RSC
+#define RS_RSC 1   // pair-table row stride a compile-time constant (npfb <= 64: 33) -> immediate tap offsets
+#endif
+#ifndef RS_UNR
+#define RS_UNR 0   // power-of-two replay: the first RS_UNR outputs of each input unrolled, predicated
+#endif
+#ifndef RS_PAIR
+#define RS_PAIR 0  // two consecutive outputs per lane over one window (rates >= 1)
+#endif
+#ifndef RS_CH
+#define RS_CH 0    // taps per read batch in the evaluation (0: the compiler's choice)
+#endif
+#ifndef RS_BF
+#define RS_BF 0    // slots below TIN evaluated without a branch (idle slots read a harmless descriptor)
+#endif
+// pair-table row stride (8-byte slots per half row): RSC, or npfb/2 + 1 at run time
+template <int RSC>
+__host__ __device__ inline int rs2_rs(int npfb) { return RSC ? RSC : (npfb >> 1) + 1; }
+// LDS bytes of k_resamp2<L, S, RSC, PR>: window copy, output descriptors, pair
+// table (L + 1 tap rows; PR adds a zero row on either side), replay counters
+template <int L, typename S, int RSC, bool PR>
 inline size_t rs2_lds_bytes(int npfb)
 {
     constexpr int TS = rs2_tin<L>() + L + 2;
-    return (size_t)(TS + 2) * sizeof(S) + (rs2_cap() + 2) * 8 + (size_t)2 * (L + 1) * ((npfb >> 1) + 1) * sizeof(float2) +
+    constexpr int NROW = L + 1 + (PR ? 2 : 0);
+    return (size_t)(TS + 2) * sizeof(S) + (rs2_cap() + 2) * 8 + (size_t)2 * NROW * rs2_rs<RSC>(npfb) * sizeof(float2) +
            (size_t)(rs2_tin<L>() / LQK_RS_CK + 1) * 8;
 }
 
-template <int L, typename S>
+// one LDS read of T as a relaxed workgroup-scope atomic: the compiler issues
+// it as its own ds_read_b64 / _b32 (2 LDS cycles per wave) and never pairs two
+// into a ds_read2_b64 (8 cycles, CDNA4 LDS table), and still batches them
+template <typename T>
+__device__ __forceinline__ T lds_rd(const T *p)
+{
+#if RS_ALD
+    if constexpr (sizeof(T) == 8) {
+        const unsigned long long u = __hip_atomic_load(reinterpret_cast<unsigned long long *>(const_cast<T *>(p)),
+                                                       __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        return __builtin_bit_cast(T, u);
+    } else {
+        const unsigned u = __hip_atomic_load(reinterpret_cast<unsigned *>(const_cast<T *>(p)), __ATOMIC_RELAXED,
+                                             __HIP_MEMORY_SCOPE_WORKGROUP);
+        return __builtin_bit_cast(T, u);
+    }
+#else
+    return *p;
+#endif
+}
+
+// PR (rates >= 1: consecutive outputs at most one input apart): each lane
+// evaluates two consecutive outputs A, B (inputs iA, iB = iA + d, d in {0, 1})
+// over one shared window W[p'] = x[iA - L + p'], p' <= L + 1: A's taps are rows
+// p' of the pair table, B's rows p' - d, the table padded with a zero row on
+// either side, so each window sample is read once for both outputs (16 + 15 +
+// 16 LDS reads per pair at L = 14 instead of 2 x 30) and the pair leaves as one
+// 16-byte store.  Terms outside an output's window are zero taps times a
+// sample; the samples there are replaced by 0, so a non-finite input never
+// reaches an output the reference keeps finite.
+__device__ __forceinline__ uint4 lds_rd4(const uint4 *p)
+{
+#if RS_ALD
+    // two relaxed 8-byte reads of adjacent words: the compiler may fuse
+    // these into one ds_read_b128 (4 cycles, as two ds_read_b64)
+    const uint2 a = lds_rd(reinterpret_cast<const uint2 *>(p)), b = lds_rd(reinterpret_cast<const uint2 *>(p) + 1);
+    return make_uint4(a.x, a.y, b.x, b.y);
+#else
+    return *p;
+#endif
+}
+
+// acc + c w for a real coefficient and a complex (packed FMA) or real sample
+__device__ __forceinline__ float2 rs_fma(float c, float2 w, float2 acc)
+{
+    v2f a2 = {acc.x, acc.y};
+    a2 = v2f{c, c} * v2f{w.x, w.y} + a2;
+    return make_float2(a2.x, a2.y);
+}
+__device__ __forceinline__ float rs_fma(float c, float w, float acc) { return fmaf(c, w, acc); }
+
+// stores through the output descriptor (an offset past it is dropped)
+__device__ __forceinline__ void rs_store1(__amdgpu_buffer_rsrc_t r, unsigned off, float2 v)
+{
+    typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
+    __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2, v), r, off, 0, 0);
+}
+__device__ __forceinline__ void rs_store1(__amdgpu_buffer_rsrc_t r, unsigned off, float v)
+{
+    __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, v), r, off, 0, 0);
+}
+__device__ __forceinline__ void rs_store2(__amdgpu_buffer_rsrc_t r, unsigned off, float2 a, float2 b)
+{
+    typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+    const u32x4 v = {__float_as_uint(a.x), __float_as_uint(a.y), __float_as_uint(b.x), __float_as_uint(b.y)};
+    __builtin_amdgcn_raw_buffer_store_b128(v, r, off, 0, 0);
+}
+__device__ __forceinline__ void rs_store2(__amdgpu_buffer_rsrc_t r, unsigned off, float a, float b)
+{
+    typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
+    const u32x2 v = {__float_as_uint(a), __float_as_uint(b)};
+    __builtin_amdgcn_raw_buffer_store_b64(v, r, off, 0, 0);
+}
+
+template <int L, typename S, int RSC, bool PR>
 __global__ __launch_bounds__(NT, rs2_blk<L>()) void k_resamp2(lqk_rs_plan pl, unsigned long long g0, unsigned long long K0,
                                                 int npfb, float del, const float2 *__restrict__ taps2,
                                                 const S *__restrict__ hist, const S *__restrict__ x,
@@ -317,16 +420,18 @@ __global__ __launch_bounds__(NT, rs2_blk<L>()) void k_resamp2(lqk_rs_plan pl, un
     S *cp0 = reinterpret_cast<S *>(smem);
     uint2 *desc = reinterpret_cast<uint2 *>(cp0 + CS);
     float2 *tpl = reinterpret_cast<float2 *>(desc + CAP + 2);   // desc[CAP]: sink of out-of-tile outputs
-    const int RS = (npfb >> 1) + 1;              // 8-byte slots per half row
+    const int RS = rs2_rs<RSC>(npfb);            // 8-byte slots per half row
+    constexpr int ROFF = PR ? 1 : 0;             // tap row p lives at table row p + ROFF
+    constexpr int NROW = L + 1 + 2 * ROFF;
 
     const int tid = threadIdx.x;
     const float fnpfb = (float)npfb;
-    for (int t = tid; t < (npfb + 1) * (L + 1); t += NT) {
-        const int b = t / (L + 1), p = t % (L + 1);
-        const float2 v = taps2[b * LP + p];
+    for (int t = tid; t < (npfb + 1) * NROW; t += NT) {
+        const int b = t / NROW, r = t % NROW, p = r - ROFF;
+        const float2 v = (p >= 0 && p <= L) ? taps2[b * LP + p] : make_float2(0.0f, 0.0f);
         // (h_b, h_b+1 - h_b): c = h_b + mu (h_b+1 - h_b) is one fma, the same
         // float32 operations as before (the difference rounded once here)
-        tpl[(2 * p + (b & 1)) * RS + (b >> 1)] = make_float2(v.x, v.y - v.x);
+        tpl[(2 * r + (b & 1)) * RS + (b >> 1)] = make_float2(v.x, v.y - v.x);
     }
     const long long ntiles = (n + tin - 1) / tin;
     constexpr int NXV = (TS + NT - 1) / NT;       // tile samples per lane
@@ -347,8 +452,11 @@ __global__ __launch_bounds__(NT, rs2_blk<L>()) void k_resamp2(lqk_rs_plan pl, un
     // stores through a descriptor over the launch's nout outputs: 32-bit
     // offsets, and a store outside them is dropped
     const __amdgpu_buffer_rsrc_t ry = __builtin_amdgcn_make_buffer_rsrc((void *)y, (short)0, nout * (int)sizeof(S), 0x00020000);
-    auto ld = [&](__amdgpu_buffer_rsrc_t r, long long e) -> S {
-        const unsigned off = (unsigned)(e * (long long)sizeof(S));   // negative: out of range, reads 0
+    // e: sample index (32-bit: the host keeps n * sizeof(S) below 2^31).
+    // Negative: an explicit out-of-range offset (reads 0) -- a negative index
+    // cast to 32 bits would land within 8 bytes of 2^32, where offset + size wraps
+    auto ld = [&](__amdgpu_buffer_rsrc_t r, int e) -> S {
+        const unsigned off = e < 0 ? 0xFFFFFFF0u : (unsigned)e * (unsigned)sizeof(S);
         if constexpr (sizeof(S) == 8)
             return __builtin_bit_cast(S, __builtin_amdgcn_raw_buffer_load_b64(r, off, 0, 0));
         else
@@ -360,7 +468,7 @@ __global__ __launch_bounds__(NT, rs2_blk<L>()) void k_resamp2(lqk_rs_plan pl, un
         unsigned long long cyc;                  // periods before it
         int skip;                                // inputs from it to the lane's first input
     };
-    unsigned long long *kx = reinterpret_cast<unsigned long long *>(tpl + 2 * (L + 1) * RS);   // [NSPAN + 1]
+    unsigned long long *kx = reinterpret_cast<unsigned long long *>(tpl + 2 * NROW * RS);   // [NSPAN + 1]
     auto fetch = [&](long long tile, Pre &f) {
         const long long i0 = tile * tin;
         // the last vector covers only TS - (NXV-1) NT samples: its other lanes
@@ -368,8 +476,8 @@ __global__ __launch_bounds__(NT, rs2_blk<L>()) void k_resamp2(lqk_rs_plan pl, un
         // the next tile per tile, +23 % of the input bytes)
 #pragma unroll
         for (int u = 0; u < NXV; u++)
-            f.xa[u] = ld(rx, (u < NXV - 1 || tid + u * NT < TS) ? i0 - L - 1 + tid + u * NT : -(1ll << 28));
-        f.xh = ld(rh, i0 == 0 ? (long long)tid - 1 : -1);   // tile 0's first L samples: the history
+            f.xa[u] = ld(rx, (u < NXV - 1 || tid + u * NT < TS) ? (int)i0 - L - 1 + tid + u * NT : -1);
+        f.xh = ld(rh, i0 == 0 ? tid - 1 : -1);   // tile 0's first L samples: the history
         const unsigned long long gt = g0 + (unsigned long long)i0;
         unsigned long long jt = gt, ct = 0;
         if (gt >= pl.pre && gt <= pl.end) {
@@ -447,6 +555,22 @@ __global__ __launch_bounds__(NT, rs2_blk<L>()) void k_resamp2(lqk_rs_plan pl, un
                     int o = o0;
                     for (int r = 0; r < nin; r++) {
                         const int iloc = (int)(ia + r - i0);
+#if RS_UNR > 0
+                        // the first RS_UNR outputs of the input without a loop:
+                        // predicated (a skipped one writes the sink slot)
+#pragma unroll
+                        for (int j = 0; j < RS_UNR; j++) {
+                            const bool e = xx < z;
+                            const float bf = xx * fnpfb;
+                            const float fb = __builtin_floorf(bf);
+                            if (!(RS_EXP & 4))
+                                desc[(e && (unsigned)o < (unsigned)CAP) ? o : CAP] = make_uint2(
+                                    __float_as_uint(bf - fb), (unsigned)iloc | ((unsigned)(xx < 0.0f ? npfb : (int)fb) << 12));
+                            o += e ? 1 : 0;
+                            const float xn = xx + del;
+                            xx = e ? xn : xx;
+                        }
+#endif
                         while (xx < z) {
                             const float bf = xx * fnpfb;
                             const float fb = __builtin_floorf(bf);
@@ -481,7 +605,7 @@ __global__ __launch_bounds__(NT, rs2_blk<L>()) void k_resamp2(lqk_rs_plan pl, un
                      (unsigned)__builtin_amdgcn_readlane((int)k, 0);
                 for (int r = 0; r < nin; r++) {
                     const int iloc = (int)(ia + r - i0);
-                    while (st.b < npfb) {
+                    while ((unsigned)st.b < (unsigned)npfb) {
                         if (st.st && st.b == npfb - 1) {
                             st.st = 0;
                             st.b = npfb;
@@ -493,7 +617,7 @@ __global__ __launch_bounds__(NT, rs2_blk<L>()) void k_resamp2(lqk_rs_plan pl, un
                         st.st = 1;
                     }
                     st.tau -= 1.0f;
-                    st.b -= npfb;
+                    st.b = (int)((unsigned)st.b - (unsigned)npfb);
                 }
             }
             if (nin > 0) kx[tid + 1] = k;
@@ -506,30 +630,83 @@ __global__ __launch_bounds__(NT, rs2_blk<L>()) void k_resamp2(lqk_rs_plan pl, un
         ntile = ntile < 0 ? 0 : (ntile > CAP ? CAP : ntile);   // exact; the clamp is a guard
         const int nr = (int)ntile;
         const unsigned ob = (unsigned)(Kb - K0);              // the tile's first output
+        // y = sum_p (T.x + mu T.d)[p] w[p]; with RS_CH > 0 the reads are issued
+        // RS_CH taps at a time, a scheduling barrier after each chunk, so the
+        // compiler batches that many round trips and no more (registers)
         auto dot = [&](const S *wv, int bb, float mu) -> S {
-            const float2 *tp = tpl + (bb & 1) * RS + (bb >> 1);
+            const float2 *tp = tpl + (2 * ROFF + (bb & 1)) * RS + (bb >> 1);
             S acc{};
 #pragma unroll
             for (int p = 0; p <= L; p++) {
-                const float2 t = tp[2 * p * RS];
+                const float2 t = lds_rd(tp + 2 * p * RS);
                 const float c = fmaf(mu, t.y, t.x);
+                const S w = lds_rd(wv + p);
                 if constexpr (sizeof(S) == 8) {
                     v2f a2 = {acc.x, acc.y};
-                    a2 = v2f{c, c} * v2f{wv[p].x, wv[p].y} + a2;
+                    a2 = v2f{c, c} * v2f{w.x, w.y} + a2;
                     acc = make_float2(a2.x, a2.y);
                 } else {
-                    acc = rs_axpy(c, wv[p], acc);
+                    acc = rs_axpy(c, w, acc);
                 }
+#if RS_CH > 0
+                if ((p + 1) % RS_CH == 0) __builtin_amdgcn_sched_barrier(0);
+#endif
             }
             return acc;
         };
+        if constexpr (PR) {
+            // pairs q = tid + k NT: outputs 2q, 2q + 1 (desc is 16-byte aligned)
+            constexpr int NPS = (CAP / 2 + NT - 1) / NT;
+#pragma unroll
+            for (int k = 0; k < NPS; k++) {
+                const int q = tid + k * NT, oa = 2 * q;
+                S va{}, vb{};
+                if (oa < nr && !(RS_EXP & 2)) {
+                    const uint4 dd = lds_rd4(reinterpret_cast<const uint4 *>(desc) + q);
+                    const bool hb = oa + 1 < nr;
+                    const int ia = (int)(dd.y & 4095u), bA = (int)(dd.y >> 12);
+                    const int d = hb ? (int)(dd.w & 4095u) - ia : 0;
+                    const int bB = hb ? (int)(dd.w >> 12) : 0;
+                    const float muA = __uint_as_float(dd.x), muB = hb ? __uint_as_float(dd.z) : 0.0f;
+                    const S *wv = cp0 + ia + 1;
+                    const float2 *tA = tpl + (2 * ROFF + (bA & 1)) * RS + (bA >> 1);
+                    const float2 *tB = tpl + (2 * (ROFF - d) + (bB & 1)) * RS + (bB >> 1);
+#pragma unroll
+                    for (int pp = 0; pp <= L + 1; pp++) {
+                        const S w = lds_rd(wv + pp);
+                        const float2 tb = lds_rd(tB + 2 * pp * RS);
+                        const float cb = fmaf(muB, tb.y, tb.x);
+                        // B's window is W[d .. d + L]: the sample outside it enters as 0
+                        const S wb = ((pp == 0 && d == 1) || (pp == L + 1 && d == 0)) ? S{} : w;
+                        if (pp <= L) {
+                            const float2 ta = lds_rd(tA + 2 * pp * RS);
+                            const float ca = fmaf(muA, ta.y, ta.x);
+                            va = rs_fma(ca, w, va);
+                        }
+                        vb = rs_fma(cb, wb, vb);
+                    }
+                }
+                const unsigned ob2 = ob + (unsigned)oa;
+                const unsigned offa = oa + 1 < nr ? ob2 * (unsigned)sizeof(S) : 0x80000000u;   // both
+                const unsigned offs = (oa < nr && oa + 1 >= nr) ? ob2 * (unsigned)sizeof(S) : 0x80000000u;   // A alone
+                rs_store2(ry, offa, va, vb);
+                rs_store1(ry, offs, va);
+            }
+        } else {
         // NSLOT outputs per lane, every store issued (slots past the tile's
-        // outputs go out of range and are dropped): a fixed store count
+        // outputs go out of range and are dropped): a fixed store count.
+        // With RS_BF the slots below TIN run without a branch (an idle slot
+        // evaluates window 0 / bank 0, its store dropped), so the compiler can
+        // interleave the reads of several outputs
 #pragma unroll
         for (int k = 0; k < NSLOT; k++) {
             const int o = tid + k * NT;
             S v{};
-            if (o < nr && !(RS_EXP & 2)) {
+            if (RS_BF && (k + 1) * NT <= TIN && !(RS_EXP & 2)) {
+                const uint2 d0 = lds_rd(&desc[o]);
+                const uint2 dd = o < nr ? d0 : make_uint2(0u, 0u);
+                v = dot(cp0 + (int)(dd.y & 4095u) + 1, (int)(dd.y >> 12), __uint_as_float(dd.x));
+            } else if (o < nr && !(RS_EXP & 2)) {
                 const uint2 dd = desc[o];
                 v = (RS_EXP & 4) ? dot(cp0 + (int)(dd.y & 1023u) + 1, (int)((dd.y >> 12) & 63u), __uint_as_float(dd.x))
                                  : dot(cp0 + (int)(dd.y & 4095u) + 1, (int)(dd.y >> 12), __uint_as_float(dd.x));
@@ -541,6 +718,7 @@ __global__ __launch_bounds__(NT, rs2_blk<L>()) void k_resamp2(lqk_rs_plan pl, un
             } else {
                 __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, v), ry, off, 0, 0);
             }
+        }
         }
     };
     for (long long tile = tile0; tile < ntiles; tile += 2 * G) {
@@ -567,7 +745,7 @@ __global__ __launch_bounds__(NT) void k_resamp_generic(lqk_rs_plan pl, unsigned 
     rs_lookup(pl, g0 + (unsigned long long)i, del, fnpfb, npfb, s, K);
     S *yo = y + (K - K0);
     auto X = [&](long long idx) -> S { return idx < 0 ? hist[L + idx] : x[idx]; };
-    while (s.b < npfb) {
+    while ((unsigned)s.b < (unsigned)npfb) {
         if (s.st && s.b == npfb - 1) break;
         const bool bnd = !s.st;
         const float2 *tp = taps + (size_t)(bnd ? npfb - 1 : s.b) * L;
@@ -585,13 +763,34 @@ __global__ __launch_bounds__(NT) void k_resamp_generic(lqk_rs_plan pl, unsigned 
     }
 }
 
+template <int L, typename S, int RSC, bool PR>
+void launch_rs2(const lqk_rs_plan &pl, unsigned long long g0, unsigned long long K0, int npfb, float del,
+                const float2 *taps2, const S *hist, const S *x, long long n, S *y, unsigned long long nout, int tin,
+                hipStream_t st)
+{
+    const long long ntiles = (n + tin - 1) / tin;
+    constexpr int BLK = rs2_blk<L>();
+    const unsigned nb = (unsigned)(ntiles < 256 * BLK ? ntiles : 256 * BLK);   // persistent: BLK per CU
+    const size_t lds = rs2_lds_bytes<L, S, RSC, PR>(npfb);
+    hipLaunchKernelGGL((k_resamp2<L, S, RSC, PR>), dim3(nb), dim3(NT), lds, st, pl, g0, K0, npfb, del, taps2, hist, x,
+                       n, y, (int)nout, tin);
+}
+
 template <int L, typename S>
 void launch_rs(const lqk_rs_plan &pl, unsigned long long g0, unsigned long long K0, int npfb, float del,
                const float2 *taps, const float2 *taps2, const S *hist, const S *x, long long n, S *y,
                unsigned long long nout, hipStream_t st)
 {
     constexpr int TIN = rs2_tin<L>();
-    const size_t lds2 = rs2_lds_bytes<L, S>(npfb);
+    constexpr int RSC = RS_RSC ? 33 : 0;       // constant stride for npfb <= 64
+    const bool cst = RSC && npfb <= 2 * (RSC - 1);
+    // pairs of outputs per lane when consecutive outputs are at most one input
+    // apart: tau moves by del per output and by -1 per input, and an input
+    // emits while tau < 1 - 1/npfb, so after an output at tau_k < 1 - 1/npfb
+    // the next input emits if tau_k + del - 1 < 1 - 1/npfb: del <= 1, here
+    // with a margin for the float32 rounding of tau_k + del
+    const bool pr = RS_PAIR && del <= 1.0f - 0x1p-22f;
+    const size_t lds2 = rs2_lds_bytes<L, S, 0, true>(npfb);   // at least that of any layout launched
     if (taps2 != nullptr && lds2 <= 64 * 1024 && pl.P < (1ull << 31) && (pl.pre < (1ull << 62) || pl.end < (1ull << 62))) {
         // inputs per tile: every tile's outputs fit the CAP output slots (at
         // most (tin + 2) r + 2 outputs: tau moves by 1/r per output and by -1
@@ -600,12 +799,12 @@ void launch_rs(const lqk_rs_plan &pl, unsigned long long g0, unsigned long long 
         const double r = 1.0 / (double)del;
         int tin = TIN;
         while (tin > LQK_RS_CK && std::ceil((tin + 2) * r) + 2 > CAP) tin -= LQK_RS_CK;
-        const long long ntiles = (n + tin - 1) / tin;
-        constexpr int BLK = rs2_blk<L>();
-        const unsigned nb = (unsigned)(ntiles < 256 * BLK ? ntiles : 256 * BLK);   // persistent: BLK per CU
-        hipLaunchKernelGGL((k_resamp2<L, S>), dim3(nb), dim3(NT), lds2, st, pl, g0, K0, npfb, del, taps2, hist, x,
-                           n, y, (int)nout, tin);
-        return;
+        if (std::ceil((tin + 2) * r) + 2 <= CAP) {   // else (r > ~60): the per-input kernel below
+            if (cst && pr) launch_rs2<L, S, RSC, true>(pl, g0, K0, npfb, del, taps2, hist, x, n, y, nout, tin, st);
+            else if (cst) launch_rs2<L, S, RSC, false>(pl, g0, K0, npfb, del, taps2, hist, x, n, y, nout, tin, st);
+            else launch_rs2<L, S, 0, false>(pl, g0, K0, npfb, del, taps2, hist, x, n, y, nout, tin, st);
+            return;
+        }
     }
     const long long lanes = (n + RS_R - 1) / RS_R;
     const unsigned nb = (unsigned)((lanes + NT - 1) / NT);

@@ -32,6 +32,7 @@ struct lq_firfilt_s {
     int host_valid, dev_valid;
     lq_ctx ctx;
     lq_devbuf xbuf, ybuf, scratch, one;
+    const char *who;   /* the public object name, for error messages */
 };
 
 static void lq_firfilt_layout(lq_firfilt *q, unsigned int n)
@@ -53,8 +54,7 @@ static void lq_firfilt_layout(lq_firfilt *q, unsigned int n)
        refuse at create time what no launch could run (fftfilt's long-filter
        path lands here too) */
     if (q->HP > lqk_firfilt_max_history(q->d.kind))
-        LQ_FAIL("error: firfilt_%s_create(), filter length %u exceeds the GPU kernel limit of %u taps\n",
-                q->d.kind == 0 ? "rrrf" : (q->d.kind == 1 ? "crcf" : "cccf"), n,
+        LQ_FAIL("error: %s_create(), filter length %u exceeds the GPU kernel limit of %u taps\n", q->who, n,
                 lqk_firfilt_max_history(q->d.kind));
 }
 
@@ -110,6 +110,7 @@ lq_firfilt *lq_firfilt_create(int kind, const float *h, unsigned int n, const ch
     q->d.kind = kind;
     q->d.scale_re = 1.0f;
     q->d.scale_im = 0.0f;
+    q->who = who;
     lq_firfilt_layout(q, n);
     q->h = (float *)lq_xmalloc((size_t)n * q->csz);
     memcpy(q->h, h, (size_t)n * q->csz);

@@ -81,7 +81,11 @@ static unsigned int rs_step(rs_state *s, float del, unsigned int npfb)
 {
     unsigned int n = 0;
     const int np = (int)npfb;
-    while (s->b < np) {
+    /* resamp.c:254 compares int b with unsigned npfb: the comparison is
+     * unsigned, so a negative b (a BOUNDARY update that leaves tau < 0, only
+     * when del < 1/npfb) ends the loop, and the decrement below (unsigned
+     * arithmetic there too) keeps b negative until it wraps modulo 2^32 */
+    while ((unsigned int)s->b < npfb) {
         if (s->st == RS_INTERP && s->b == np - 1) {
             s->st = RS_BOUNDARY;
             s->b = np;
@@ -95,7 +99,7 @@ static unsigned int rs_step(rs_state *s, float del, unsigned int npfb)
         s->st = RS_INTERP;
     }
     s->tau -= 1.0f;                                 /* resamp.c:305-307 */
-    s->b -= np;
+    s->b = (int)((unsigned int)s->b - npfb);
     return n;
 }
 
@@ -129,6 +133,12 @@ static rs_state rs_from_tau(float tau, unsigned int npfb)
 }
 
 static int rs_pow2(unsigned int npfb) { return (npfb & (npfb - 1)) == 0; }
+
+/* the tau-only plan form needs a power-of-two bank count and del >= 1/npfb:
+ * then tau >= 0 after every update (a BOUNDARY update adds del to a tau in
+ * [-1/npfb, 0), exactly) and b never goes negative.  Rates above npfb keep
+ * the full state, whose unsigned loop test stops a negative b (rs_step). */
+static int rs_p2(const lq_rs *q) { return rs_pow2(q->npfb) && q->del * (float)q->npfb >= 1.0f; }
 
 static void rs_put(lqk_rs_entry *e, const rs_state *s, unsigned long long K)
 {
@@ -179,7 +189,7 @@ static rs_state rs_plan_at(const rs_plan *pl, unsigned long long g, float del, u
 
 static void rs_plan_upload(lq_rs *q)
 {
-    if (rs_pow2(q->npfb)) {                  /* (tau, K): 8 B per LQK_RS_CK inputs */
+    if (rs_p2(q)) {                  /* (tau, K): 8 B per LQK_RS_CK inputs */
         size_t bytes = q->pl.nck * sizeof(lqk_rs_entry_p2);
         lqk_rs_entry_p2 *t = (lqk_rs_entry_p2 *)lq_xmalloc(bytes);
         for (size_t c = 0; c < q->pl.nck; c++) {
@@ -211,7 +221,7 @@ static unsigned long long rs_walk(lq_rs *q, rs_state x0, unsigned long long n, i
     const unsigned long long CK = LQK_RS_CK;
     pl->nck = 0;
     unsigned long long K = 0, i = 0;
-    if (rs_pow2(q->npfb)) {
+    if (rs_p2(q)) {
         /* the hot loop: runs of steps between checkpoints; with `early`, the
          * first RS_EARLY states are compared with each other, and every later
          * state (branch-free) with the first and with Brent's tortoise, the
@@ -354,7 +364,7 @@ static int rs_plan_build_periodic(lq_rs *q)
         }
         /* pre-period: one copy lam steps ahead, both walked until they meet */
         unsigned long long mu = 0;
-        if (rs_pow2(q->npfb)) {
+        if (rs_p2(q)) {
             const float z = 1.0f - 1.0f / (float)q->npfb;
             float a = x0.tau, h = x0.tau;
             for (unsigned long long i = 0; i < lam; i++) rs_step_p2(&h, q->del, z);
@@ -602,7 +612,7 @@ unsigned long long lq_rs_num_output(lq_rs *_q, unsigned long long _nx)
         unsigned long long K;
         s = rs_plan_at(&_q->pl, _q->gpos, _q->del, _q->npfb, &K);
     }
-    if (rs_pow2(_q->npfb)) {
+    if (rs_p2(_q)) {
         const float z = 1.0f - 1.0f / (float)_q->npfb;
         float t = s.tau;
         for (; done < _nx; done++) total += rs_step_p2(&t, _q->del, z);
@@ -625,7 +635,7 @@ void lq_rs_block_dev(lq_rs *_q, const void *_dxv, unsigned long long _nx, void *
     while (_nx > 0) {
         unsigned long long c = rs_ensure_plan(_q, _nx < cmax ? _nx : cmax);
         unsigned long long K0 = rs_K(_q, _q->gpos), K1 = rs_K(_q, _q->gpos + c);
-        lqk_rs_plan kp = {_q->pl.d_tab.p, _q->pl.pre, _q->pl.P, _q->pl.Q, _q->pl.end, rs_pow2(_q->npfb)};
+        lqk_rs_plan kp = {_q->pl.d_tab.p, _q->pl.pre, _q->pl.P, _q->pl.Q, _q->pl.end, rs_p2(_q)};
         void *hold = _q->d_hist[_q->cur], *hnew = _q->d_hist[_q->cur ^ 1];
         lqk_resamp(_q->kind == LQ_RRRF, &kp, _q->gpos, K0, _q->npfb, _q->L, _q->del, _q->d_taps, _q->d_taps2, hold, _dx, c,
                    _dy, K1 - K0, _q->ctx.stream);
@@ -746,7 +756,7 @@ long long liquid_mi355x_resamp_schedule(float _rate, unsigned int _npfb, unsigne
             free(q.pl.tab);
             return -2;                       /* plan's output count disagrees with the replay */
         }
-        while (s.b < np) {
+        while ((unsigned int)s.b < _npfb) {   /* unsigned, as resamp.c:254 */
             if (s.st == RS_INTERP && s.b == np - 1) break;
             if (k < _cap) {
                 _b[k] = s.st == RS_INTERP ? s.b : -1;

@@ -710,7 +710,7 @@ static unsigned int orc_resamp_exec1(orc_resamp q, orc_cf x, orc_cf *y)
 {
     orc_window_push(&q->f->w, x);
     unsigned int n = 0;
-    while (q->b < (int)q->npfb) {
+    while ((unsigned int)q->b < q->npfb) {   /* int vs unsigned in resamp.c:254: an unsigned compare */
         if (q->state == ORC_RS_BOUNDARY) {
             q->y1 = orc_firpfb_exec1(q->f, 0);
             y[n++] = orc_lerp(q->mu, q->y0, q->y1);
@@ -730,7 +730,7 @@ static unsigned int orc_resamp_exec1(orc_resamp q, orc_cf x, orc_cf *y)
     }
     q->tau -= 1.0f;
     q->bf -= (float)(q->npfb);
-    q->b -= q->npfb;
+    q->b = (int)((unsigned int)q->b - q->npfb);   /* resamp.c:307, unsigned arithmetic */
     return n;
 }
 
@@ -750,7 +750,7 @@ unsigned long orc_resamp_schedule(float rate, unsigned int npfb, unsigned long n
     int b = 0, state = ORC_RS_INTERP;
     unsigned long k = 0;
     for (unsigned long i = 0; i < nx; i++) {
-        while (b < (int)npfb) {
+        while ((unsigned int)b < npfb) {
             if (state == ORC_RS_BOUNDARY) {
                 if (k < cap) { bo[k] = -1; muo[k] = mu; in_idx[k] = (unsigned int)i; }
                 k++;
@@ -767,7 +767,7 @@ unsigned long orc_resamp_schedule(float rate, unsigned int npfb, unsigned long n
         }
         tau -= 1.0f;
         bf -= (float)npfb;
-        b -= npfb;
+        b = (int)((unsigned int)b - npfb);
     }
     return k;
 }

@@ -109,7 +109,7 @@ def msresamp_spectral_case():
     return r, As, x, check
 
 
-def firpfbch2_downconverter(x, h, M, m, nblocks, firfilt):
+def firpfbch2_downconverter(x, h, M, m, nblocks, firfilt, channels=None):
     """The firpfbch2 analyzer restated as a bank of M "traditional" down-
     converters -- the reference's own methodology for pinning a channelizer
     to a filter it already pins: firpfbch_crcf_analyzer_autotest.c:30-146
@@ -125,14 +125,73 @@ def firpfbch2_downconverter(x, h, M, m, nblocks, firfilt):
         y_k = firfilt(h, x[t] e^{-j2pi kt/M}),  offset_b = (b mod 2) M/2,
     the phase term being the commutator's rotation of the bins.
     `firfilt(h, z)` is the pinned FIR filter to use (complex64 in and out).
+    `channels` restricts the bank to a subset of k (the reference loops over
+    all of them; any subset is the same identity): returns (nblocks,
+    len(channels)) in that order, else (nblocks, M).
     """
     L = 2 * M * m
+    ks = list(range(M)) if channels is None else list(channels)
     t = (np.arange(nblocks) + 1) * (M // 2) - 1
     off = (np.arange(nblocks) % 2) * (M // 2)
     n = np.arange(len(x))
-    Y = np.zeros((nblocks, M), np.complex128)
-    for k in range(M):
+    Y = np.zeros((nblocks, len(ks)), np.complex128)
+    for c, k in enumerate(ks):
         z = (x.astype(np.complex128) * np.exp(-2j * np.pi * ((k * n) % M) / M)).astype(np.complex64)
         y = np.asarray(firfilt(np.asarray(h[:L], np.float32), z))
-        Y[:, k] = np.exp(2j * np.pi * ((k * (off + t)) % M) / M) * y[t] / M
+        Y[:, c] = np.exp(2j * np.pi * ((k * (off + t)) % M) / M) * y[t] / M
     return Y
+
+
+def firpfbch_downconverter(x, h, M, nsym, firfilt, channels=None):
+    """src/multichannel/tests/firpfbch_crcf_analyzer_autotest.c:88-115: the
+    critically sampled analyzer as M "traditional" down-converters -- channel
+    k mixed down by e^{-j 2 pi k j / M}, filtered by the full prototype h
+    (the pinned `firfilt`), sampled after every M inputs:
+        Y1[n][k] = firfilt(h, x[j] e^{-j2pi kj/M})[(n+1) M - 1]
+    (the reference compares this with the analyzer output at tol 1e-4,
+    no scaling).  The mixer phase is reduced exactly (k j mod M)."""
+    ks = list(range(M)) if channels is None else list(channels)
+    t = (np.arange(nsym) + 1) * M - 1
+    n = np.arange(len(x))
+    Y = np.zeros((nsym, len(ks)), np.complex128)
+    for c, k in enumerate(ks):
+        z = (x.astype(np.complex128) * np.exp(-2j * np.pi * ((k * n) % M) / M)).astype(np.complex64)
+        Y[:, c] = np.asarray(firfilt(np.asarray(h, np.float32), z))[t]
+    return Y
+
+
+def resamp_autotest_case():
+    """src/filter/tests/resamp_crcf_autotest.c:29-136 (autotest_resamp_crcf),
+    restated: r = 1.27115323, m = 13, bw = 0.45, As = 60, npfb = 64, a
+    Kaiser-windowed (beta 10) tone at fx = 0.254230646 over n = 400 samples
+    plus m zeros, pushed one sample per execute().  Returns (r, m, bw, As,
+    npfb, x, check); check(y) lists the failed conditions of :106-109 --
+    rate within 0.01, peak 0 +- 0.25 dB, peak at fy = fx / r +- 0.01, every
+    bin further than 0.07 from fy below -As."""
+    m, r, bw, As, npfb, n, fx = 13, 1.27115323, 0.45, 60.0, 64, 400, 0.254230646
+    r32 = float(np.float32(r))
+    nx = n + m
+    i = np.arange(nx)
+    w = np.where(i < n, liquid_kaiser(i, n, 10.0), 0.0).astype(np.float32)
+    x = (np.exp(1j * 2 * np.pi * fx * i) * w).astype(np.complex64)
+    wsum = float(np.sum(w, dtype=np.float32))
+
+    def check(y):
+        y = np.asarray(y, np.complex128)
+        ny = len(y)
+        r_actual = ny / nx
+        fy = fx / r32
+        nfft = 1 << int(np.ceil(np.log2(ny)))
+        Y = np.fft.fftshift(np.fft.fft(np.concatenate([y, np.zeros(nfft - ny)])))
+        Y = Y / (r32 * wsum)
+        f = np.arange(nfft) / nfft - 0.5
+        mag = 20 * np.log10(np.abs(Y) + 1e-30)
+        k = int(np.argmax(mag))
+        side = float(np.max(mag[np.abs(f - fy) > 0.07]))
+        bad = []
+        if abs(r_actual - r32) > 0.01: bad.append("rate %g" % r_actual)
+        if abs(mag[k]) > 0.25: bad.append("peak %g dB" % mag[k])
+        if abs(f[k] - fy) > 0.01: bad.append("peak freq %g (want %g)" % (f[k], fy))
+        if not side < -As: bad.append("sidelobe %g dB" % side)
+        return bad
+    return r32, m, bw, As, npfb, x, check

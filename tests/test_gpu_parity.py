@@ -435,6 +435,45 @@ def test_firpfbch2_analyzer_vs_downconverter_bank(M, m):
     assert G.nrm_err(y, ref) < NRM
 
 
+PFB2_CHANS = [0, 1, 255, 511, 512, 513, 1023]
+
+
+def test_firpfbch2_config4_vs_downconverter_bank():
+    """BASELINE config 4 geometry (M = 1024, m = 4, Kaiser As = 60) on the
+    fast kernel k_pfb2_an1024 against the reference's own equivalence method
+    (sandbox/firpfbch2_analysis_equivalence_test.c:182-215: mix down, filter
+    with the prototype, sample every M/2) built on the golden-pinned firfilt
+    oracle, on a channel subset; 32 blocks from a zero state in two calls,
+    the second starting at odd block parity"""
+    M, m = 1024, 4
+    r = rng(1024 * 4 + 1)
+    chans = PFB2_CHANS + sorted(int(c) for c in r.choice(np.arange(2, 1023), 9, replace=False))
+    nblocks = 32
+    x = cx(r, nblocks * M // 2)
+    g = LQ.FirPfbch2(LQ.LIQUID_ANALYZER, M, m, 60.0)
+    y = np.concatenate([g.execute_block(x[:7 * M // 2]), g.execute_block(x[7 * M // 2:])]).reshape(nblocks, M)
+    h = O.firpfbch2_prototype(O.ANALYZER, M, m, 60.0)
+    ref = G.firpfbch2_downconverter(x, h, M, m, nblocks, lambda hh, z: O.FirFilt(O.CRCF, hh).execute_block(z),
+                                    channels=chans)
+    assert G.nrm_err(y[:, chans], ref) < NRM
+
+
+def test_firpfbch_analyzer_m1024_vs_downconverter_bank():
+    """firpfbch_crcf_analyzer_autotest.c:30-146 (analyzer == mixer + firfilt,
+    tol 1e-4) on the GPU's M = 1024, p = 8 fast kernel (random taps, as the
+    reference allows), channel subset, two ragged calls"""
+    r = rng(1024 + 8)
+    M, p, ns = 1024, 8, 24
+    chans = PFB2_CHANS + [100, 300, 700, 900, 1022]
+    h = r.choice([-1.5, -0.5, 0.5, 1.5], M * p).astype(np.float32)
+    x = (0.1 * np.sqrt(0.5) * (r.choice([-1.5, -0.5, 0.5, 1.5], M * ns)
+                               + 1j * r.choice([-1.5, -0.5, 0.5, 1.5], M * ns))).astype(np.complex64)
+    g = LQ.FirPfbch(LQ.LIQUID_ANALYZER, M, p=p, h=h)
+    y = np.concatenate([g.execute_block(x[:5 * M]), g.execute_block(x[5 * M:])]).reshape(ns, M)
+    ref = G.firpfbch_downconverter(x, h, M, ns, lambda hh, z: O.FirFilt(O.CRCF, hh).execute_block(z), chans)
+    assert np.max(np.abs(y[:, chans] - ref)) < 1e-4
+
+
 def test_firpfbch2_baseline_config4_slice_vs_oracle():
     # BASELINE config 4 geometry: M=1024, m=4, As=60, 2^20 samples (2048 blocks)
     r = rng(31)
@@ -866,6 +905,40 @@ def test_resamp_vs_oracle_ragged(rate, m, npfb):
     ref = o.execute_block(x)
     assert len(y) == len(ref)
     assert G.nrm_err(y, ref) < NRM
+
+
+@pytest.mark.parametrize("rate,npfb", [(30.0, 64), (64.0, 64), (100.0, 64), (83.3, 64), (75.5, 64),
+                                       (130.7, 64), (57.3, 37)])
+def test_resamp_high_rate_vs_oracle(rate, npfb):
+    """rates whose 16-input tiles overflow the tiled kernel's 1088 output
+    slots (r > ~60) run the per-input kernel; rates above npfb follow the
+    reference's unsigned b < npfb test (resamp.c:254), which stops the stream
+    once a BOUNDARY update leaves b = -1.  Calls of >= 16 inputs, ragged."""
+    r = rng(int(rate * 10) + npfb)
+    x = cx(r, 6000)
+    g, o = _resamp_pair(rate, m=7, npfb=npfb)
+    cuts = [0, 1, 17, 18, 1000, 1001, 4096, 6000]
+    ys = [g.execute(x[a]) if b - a == 1 else g.execute_block(x[a:b]) for a, b in zip(cuts[:-1], cuts[1:])]
+    y = np.concatenate(ys)
+    ref = o.execute_block(x)
+    assert len(y) == len(ref)
+    assert G.nrm_err(y, ref) < NRM
+
+
+def test_resamp_reference_autotest_gpu():
+    """autotest_resamp_crcf (src/filter/tests/resamp_crcf_autotest.c:29-136)
+    on the GPU path: one execute() per input as the reference calls it, then
+    the same stream in one execute_block; both pass the reference's rate /
+    peak / peak-frequency / side-lobe checks and match the oracle"""
+    rr, m, bw, As, npfb, x, check = G.resamp_autotest_case()
+    g = LQ.Resamp(rr, m, bw, As, npfb)
+    y = np.concatenate([g.execute(v) for v in x])
+    assert check(y) == []
+    yb = LQ.Resamp(rr, m, bw, As, npfb).execute_block(x)
+    assert check(yb) == []
+    ref = O.Resamp(rr, m, bw, As, npfb).execute_block(x)
+    assert len(y) == len(ref) == len(yb)
+    assert G.nrm_err(y, ref) < NRM and G.nrm_err(yb, ref) < NRM
 
 
 def test_resamp_long_stream_crosses_period():

@@ -300,6 +300,51 @@ def test_resamp_exact_schedule_and_values():
     assert G.nrm_err(y, _resamp_ref(x, 1.037)) < 2e-6
 
 
+def test_resamp_reference_autotest():
+    """autotest_resamp_crcf restated exactly (resamp_crcf_autotest.c:29-136):
+    rate, peak level, peak frequency and side-lobes of the resampled
+    Kaiser-windowed tone, one execute() per input"""
+    r, m, bw, As, npfb, x, check = G.resamp_autotest_case()
+    q = O.Resamp(r, m, bw, As, npfb)
+    y = np.concatenate([q.execute_block(x[i:i + 1]) for i in range(len(x))])
+    assert check(y) == []
+    y2 = O.Resamp(r, m, bw, As, npfb).execute_block(x)
+    np.testing.assert_array_equal(y2, y)
+
+
+@pytest.mark.parametrize("M,m,chans", [
+    (1024, 4, [0, 1, 255, 511, 512, 513, 1023, 77, 140, 333, 600, 700, 801, 900, 950, 1000]),
+])
+def test_firpfbch2_downconverter_baseline_geometry(M, m, chans):
+    """sandbox/firpfbch2_analysis_equivalence_test.c:182-215 at BASELINE
+    config 4's geometry (M = 1024, m = 4, Kaiser As = 60): the oracle
+    analyzer against mixer + golden-pinned firfilt, on a channel subset,
+    24 blocks from a zero state (both block parities)"""
+    rng = _rng(1024 + 4)
+    nblocks = 24
+    x = _cx(rng, nblocks * M // 2)
+    y = O.FirPfbch2(O.ANALYZER, M, m, 60.0).execute_block(x).reshape(nblocks, M)
+    h = O.firpfbch2_prototype(O.ANALYZER, M, m, 60.0)
+    ref = G.firpfbch2_downconverter(x, h, M, m, nblocks, lambda hh, z: O.FirFilt(O.CRCF, hh).execute_block(z),
+                                    channels=chans)
+    assert G.nrm_err(y[:, chans], ref) < 1e-5
+
+
+def test_firpfbch_downconverter_baseline_geometry():
+    """firpfbch_crcf_analyzer_autotest.c:30-146 at M = 1024, p = 8 (random
+    taps, as the reference's "can be random" note allows), channel subset"""
+    rng = _rng(88)
+    M, p, ns = 1024, 8, 16
+    chans = [0, 1, 2, 511, 512, 513, 1022, 1023, 100, 300, 700, 900]
+    h = rng.choice([-1.5, -0.5, 0.5, 1.5], M * p).astype(np.float32)
+    x = (0.1 * np.sqrt(0.5) * (rng.choice([-1.5, -0.5, 0.5, 1.5], M * ns)
+                               + 1j * rng.choice([-1.5, -0.5, 0.5, 1.5], M * ns))).astype(np.complex64)
+    y = O.FirPfbch(O.ANALYZER, M, p=p, h=h)
+    Y0 = np.array([y.execute(x[i * M:(i + 1) * M]) for i in range(ns)])
+    Y1 = G.firpfbch_downconverter(x, h, M, ns, lambda hh, z: O.FirFilt(O.CRCF, hh).execute_block(z), chans)
+    assert np.max(np.abs(Y0[:, chans] - Y1)) < 1e-4
+
+
 def test_resamp_spectral():
     # src/filter/tests/resamp_crcf_autotest.c: a tone survives at unit gain
     q = O.Resamp(0.9)

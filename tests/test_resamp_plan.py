@@ -16,7 +16,7 @@ import liquidmi as LM
 import oracle_lib as O
 
 
-def _lib_schedule(rate, npfb, nx, periodic):
+def _lib_schedule(rate, npfb, nx, periodic, allow_none=False):
     L = LM.lib()
     fn = L.liquid_mi355x_resamp_schedule
     fn.restype = C.c_longlong
@@ -28,6 +28,8 @@ def _lib_schedule(rate, npfb, nx, periodic):
     idx = np.zeros(cap, np.uint32)
     pre, per = C.c_ulonglong(0), C.c_ulonglong(0)
     k = fn(rate, npfb, nx, periodic, LM.ptr(b), LM.ptr(mu), LM.ptr(idx), cap, C.byref(pre), C.byref(per))
+    if allow_none and k == -1:
+        return None
     assert k >= 0, "plan failed (%d)" % k
     return b[:k], mu[:k], idx[:k], pre.value, per.value
 
@@ -72,3 +74,35 @@ def test_config5_output_count():
     b, _, _, pre, per = _lib_schedule(rate, 64, 1 << 25, 1)
     assert (pre, per) == (0, 1_011_163)
     assert len(b) == 34_795_945
+
+
+@pytest.mark.parametrize("rate,npfb", [(83.3, 64), (75.5, 64), (100.0, 64), (64.0, 64), (130.7, 64), (57.3, 37)])
+@pytest.mark.parametrize("periodic", [0, 1])
+def test_rate_above_npfb_unsigned_semantics(rate, npfb, periodic):
+    """rates above npfb: resamp.c:254 compares int b with unsigned npfb, so a
+    BOUNDARY update that leaves tau < 0 (b = -1) ends the loop and the
+    resampler stops producing output (b stays negative); the plans and the
+    oracle (which states the comparison as the reference does) agree"""
+    rate = float(np.float32(rate))
+    nx = 3000
+    # a dying orbit has no period (b keeps decreasing): the periodic search
+    # gives up and the object runs on direct plans
+    got = _lib_schedule(rate, npfb, nx, periodic, allow_none=bool(periodic))
+    if got is None:
+        return
+    b, mu, idx, _, _ = got
+    ob, omu, oidx = O.resamp_schedule(rate, npfb, nx)
+    assert len(b) == len(ob)
+    np.testing.assert_array_equal(b, ob)
+    np.testing.assert_array_equal(mu.view(np.uint32), omu.view(np.uint32))
+    np.testing.assert_array_equal(idx, oidx)
+
+
+def test_rate_above_npfb_stops():
+    # r = 83.3, npfb = 64: del = 0.012 < 1/64; the first BOUNDARY update
+    # leaves tau < 0, so input 1 ends the stream: 84 outputs, none after
+    rate = float(np.float32(83.3))
+    ob, _, oidx = O.resamp_schedule(rate, 64, 1000)
+    assert len(ob) < 2 * rate and oidx.max() <= 1
+    b, _, idx, _, _ = _lib_schedule(rate, 64, 1000, 0)
+    assert len(b) == len(ob)
