@@ -463,10 +463,12 @@ def cpu_baseline(seconds, procs):
                                              "source": "BASELINE.md section 2"}}
 
 
-def percall_baseline():
+def percall_baseline(host_small_calls=False):
     """The reference's own per-call benchmark bodies linked against this
     library (tools/build_ref_benches.sh -> build/ref_bench/percall), wall
-    clock; None when the harness was not built."""
+    clock; None when the harness was not built.  host_small_calls: run them
+    with LQ_SMALL_CALLS=host (the opt-in host path for single-sample calls,
+    host/lq_small.c); otherwise every call runs on the GPU (the default)."""
     import subprocess
     exe = os.path.join(ROOT, "build", "ref_bench", "percall")
     if not os.path.exists(exe):
@@ -475,7 +477,12 @@ def percall_baseline():
              "firpfbch_crcf_a1024", "resamp_crcf_m8", "firdecim_crcf_m8_h32", "firinterp_crcf_m8_h32",
              "fftfilt_crcf_64", "windowcf_push_n64"]
     try:
-        out = subprocess.run([exe, "--runtime", "0.25"] + names, capture_output=True, text=True, timeout=240)
+        env = dict(os.environ)
+        env.pop("LQ_SMALL_CALLS", None)
+        if host_small_calls:
+            env["LQ_SMALL_CALLS"] = "host"
+        out = subprocess.run([exe, "--runtime", "0.25"] + names, capture_output=True, text=True, timeout=240,
+                             env=env)
     except subprocess.TimeoutExpired:
         return {"error": "timeout"}
     # the reference's own `make bench` rates for the same bodies, one core of
@@ -588,9 +595,10 @@ def main():
         ff_t = (allreduce_max(ff["wall"], world), allreduce_max(ff["gpu_ms"], world))
 
     copy_gbps = copy_bandwidth() if rank == 0 else None
-    percall = None
+    percall = percall_host = None
     if rank == 0 and world == 1 and not args.no_percall:
         percall = percall_baseline()
+        percall_host = percall_baseline(host_small_calls=True)
     cpu = cpu2 = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         cpu = cpu_baseline(args.cpu_seconds, args.cpu_procs or cpu_share())
@@ -702,6 +710,11 @@ def main():
             out["per_call"] = {"what": "the reference's per-call benchmark loops (src/*/bench/*_benchmark.c) "
                                        "linked against this library; wall clock; one GPU round trip per call",
                                "runs": percall}
+        if percall_host is not None:
+            out["per_call_host_small_calls"] = {
+                "what": "the same loops with LQ_SMALL_CALLS=host: the opt-in host path for single-sample "
+                        "calls (host/lq_small.c); block calls stay on the GPU; not the default",
+                "runs": percall_host}
         if cpu2:
             for leg, c in cpu2.items():
                 key = "dotprod_cccf" if leg == "dotprod_cccf_n64" else leg

@@ -92,6 +92,10 @@ void lq_dotprod_execute_batch(lq_dotprod *q, const void *X, unsigned long long n
  * memory, one kernel writes the pinned result and raises the flag */
 static void lq_dotprod_execute1(lq_dotprod *q, const void *x, void *y)
 {
+    if (lq_small_host()) {   /* opt-in host path (lq_small.c) */
+        lq_host_dot(q->kind, q->h, x, q->n, y);
+        return;
+    }
     const void *dx = lq_call_in(&q->ctx, &q->xbuf, x, (size_t)q->n * q->esz);
     unsigned *flag, seq;
     void *py = lq_sig_out(&q->ctx, q->esz, &flag, &seq);
@@ -107,6 +111,10 @@ static lq_dotprod *g_run[3];
 
 void lq_dotprod_run(int kind, const float *h, const void *x, unsigned int n, void *y)
 {
+    if (lq_small_host()) {
+        lq_host_dot(kind, h, x, n, y);
+        return;
+    }
     pthread_mutex_lock(&g_run_mu);
     if (!g_run[kind]) g_run[kind] = lq_dotprod_create(kind, h, n);
     else lq_dotprod_recreate(g_run[kind], h, n);

@@ -33,6 +33,7 @@ typedef struct {
     unsigned int QC;
     void *d_hist[2];   /* last hlen-1 inputs */
     int cur;
+    lq_mirror hm;      /* host copy of the history (small-call mode) */
     lq_ctx ctx;
     lq_devbuf xbuf, ybuf;
 } lq_decim;
@@ -73,6 +74,7 @@ static lq_decim *lq_decim_create(int kind, unsigned int M, const float *h, unsig
     q->d.hpad = q->d_hpad;
     q->d.scale_re = 1.0f;
     q->d.scale_im = 0.0f;
+    lq_mirror_init(&q->hm, hlen - 1, q->esz);
     return q;
 }
 
@@ -98,6 +100,7 @@ static void lq_decim_destroy(lq_decim *q)
     lq_devbuf_free(&q->xbuf);
     lq_devbuf_free(&q->ybuf);
     lq_ctx_free(&q->ctx);
+    lq_mirror_free(&q->hm);
     free(q->h);
     free(q);
 }
@@ -116,11 +119,14 @@ static void lq_decim_clear(lq_decim *q)
     lqrt_memset(q->d_hist[0], (size_t)q->hlen * q->esz, q->ctx.stream);
     lqrt_memset(q->d_hist[1], (size_t)q->hlen * q->esz, q->ctx.stream);
     lqrt_sync(q->ctx.stream);
+    lq_mirror_zero(&q->hm);
 }
 
 static void lq_decim_block_dev(lq_decim *q, const void *dx, unsigned long long nout, void *dy)
 {
     if (nout == 0) return;
+    lq_mirror_need_dev(&q->hm, q->d_hist[q->cur], q->ctx.stream);
+    q->hm.host_valid = 0;
     void *hold = q->d_hist[q->cur], *hnew = q->d_hist[q->cur ^ 1];
     if (lqk_firdecim_ph(q->kind, q->M, q->QC, q->d_hq, q->hlen - 1, hold, dx, nout, dy, q->ctx.stream) != 0)
         lqk_firdecim(&q->d, q->M, hold, dx, nout, dy, q->ctx.stream);
@@ -130,9 +136,23 @@ static void lq_decim_block_dev(lq_decim *q, const void *dx, unsigned long long n
     }
 }
 
+/* small-call mode: one output on the host (firdecim.c:189-205: the dot
+ * product right after the first of the M pushes) */
+static void lq_decim_exec1_host(lq_decim *q, const void *x, void *y)
+{
+    lq_mirror_need_host(&q->hm, q->d_hist[q->cur], q->ctx.stream);
+    lq_mirror_append(&q->hm, x, q->M);
+    lq_host_conv(q->kind, q->h, lq_mirror_ptr(&q->hm), q->hlen - 1, q->hlen, y);
+    lq_mirror_commit(&q->hm, q->M);
+}
+
 static void lq_decim_block(lq_decim *q, const void *x, unsigned long long nout, void *y)
 {
     if (nout == 0) return;
+    if (nout == 1 && lq_small_host()) {
+        lq_decim_exec1_host(q, x, y);
+        return;
+    }
     size_t nin = (size_t)nout * q->M * q->esz, nb = (size_t)nout * q->esz;
     const void *dx = lq_call_in(&q->ctx, &q->xbuf, x, nin);
     void *dy = lq_devbuf_get(&q->ybuf, nb);
@@ -212,6 +232,8 @@ typedef struct {
     void *d_hpoly;     /* M x L: hpoly[p*L + l] = h'[p + l*M] */
     void *d_hist[2];   /* last L-1 inputs */
     int cur;
+    float *hpoly;      /* host copy of the M x L phase taps (small-call mode) */
+    lq_mirror hm;      /* host copy of the history (small-call mode) */
     lq_ctx ctx;
     lq_devbuf xbuf, ybuf;
 } lq_interp;
@@ -243,7 +265,8 @@ static lq_interp *lq_interp_create(int kind, unsigned int M, const float *h, uns
     q->d_hist[0] = lqrt_malloc((size_t)q->L * q->esz);
     q->d_hist[1] = lqrt_malloc((size_t)q->L * q->esz);
     lqrt_sync(q->ctx.stream);
-    free(hp);
+    q->hpoly = hp;
+    lq_mirror_init(&q->hm, q->L - 1, q->esz);
     return q;
 }
 
@@ -267,6 +290,8 @@ static void lq_interp_destroy(lq_interp *q)
     lq_devbuf_free(&q->xbuf);
     lq_devbuf_free(&q->ybuf);
     lq_ctx_free(&q->ctx);
+    lq_mirror_free(&q->hm);
+    free(q->hpoly);
     free(q->h);
     free(q);
 }
@@ -283,11 +308,14 @@ static void lq_interp_reset(lq_interp *q)
     lqrt_memset(q->d_hist[0], (size_t)q->L * q->esz, q->ctx.stream);
     lqrt_memset(q->d_hist[1], (size_t)q->L * q->esz, q->ctx.stream);
     lqrt_sync(q->ctx.stream);
+    lq_mirror_zero(&q->hm);
 }
 
 static void lq_interp_block_dev(lq_interp *q, const void *dx, unsigned long long n, void *dy)
 {
     if (n == 0) return;
+    lq_mirror_need_dev(&q->hm, q->d_hist[q->cur], q->ctx.stream);
+    q->hm.host_valid = 0;
     void *hold = q->d_hist[q->cur], *hnew = q->d_hist[q->cur ^ 1];
     lqk_firinterp(q->kind, q->d_hpoly, q->M, q->L, 1.0f, 0.0f, hold, dx, n, dy, q->ctx.stream);
     if (q->L > 1) {
@@ -296,9 +324,26 @@ static void lq_interp_block_dev(lq_interp *q, const void *dx, unsigned long long
     }
 }
 
+/* small-call mode: the M outputs of one input on the host (firinterp.c:187-198:
+ * bank p of the polyphase filter over the last L inputs) */
+static void lq_interp_exec1_host(lq_interp *q, const void *x, void *y)
+{
+    lq_mirror_need_host(&q->hm, q->d_hist[q->cur], q->ctx.stream);
+    lq_mirror_append(&q->hm, x, 1);
+    const unsigned char *w = lq_mirror_ptr(&q->hm);
+    const size_t cf = q->csz / 4;
+    for (unsigned int p = 0; p < q->M; p++)
+        lq_host_conv(q->kind, q->hpoly + cf * p * q->L, w, q->L - 1, q->L, (unsigned char *)y + p * q->esz);
+    lq_mirror_commit(&q->hm, 1);
+}
+
 static void lq_interp_block(lq_interp *q, const void *x, unsigned long long n, void *y)
 {
     if (n == 0) return;
+    if (n == 1 && lq_small_host()) {
+        lq_interp_exec1_host(q, x, y);
+        return;
+    }
     size_t nin = (size_t)n * q->esz, nout = (size_t)n * q->M * q->esz;
     const void *dx = lq_call_in(&q->ctx, &q->xbuf, x, nin);
     void *dy = lq_devbuf_get(&q->ybuf, nout);

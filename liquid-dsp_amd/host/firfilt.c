@@ -212,6 +212,21 @@ void lq_firfilt_push(lq_firfilt *q, const void *x)
  * stream sync) */
 void lq_firfilt_execute(lq_firfilt *q, void *y)
 {
+    if (lq_small_host()) {   /* opt-in host path (lq_small.c): the window's newest sample is h_win[HP-1] */
+        lq_firfilt_need_host(q);
+        float v[2];
+        lq_host_conv(q->kind, q->h, q->h_win, q->HP - 1, q->hlen, v);
+        if (q->kind == LQ_RRRF) {
+            *(float *)y = v[0] * q->d.scale_re;
+        } else if (q->kind == LQ_CRCF) {   /* firfilt.c:337: real scale per component */
+            ((float *)y)[0] = v[0] * q->d.scale_re;
+            ((float *)y)[1] = v[1] * q->d.scale_re;
+        } else {
+            ((float *)y)[0] = v[0] * q->d.scale_re - v[1] * q->d.scale_im;
+            ((float *)y)[1] = v[0] * q->d.scale_im + v[1] * q->d.scale_re;
+        }
+        return;
+    }
     const void *win = q->dev_valid ? q->d_win[q->cur] : (const void *)q->h_win;
     unsigned *flag, seq;
     void *py = lq_sig_out(&q->ctx, q->esz, &flag, &seq);

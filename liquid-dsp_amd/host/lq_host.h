@@ -5,7 +5,9 @@
  * (include/liquid.h) and its failure style (message on stderr, exit(1)).
  * All sample arithmetic happens in the HIP kernels behind csrc/lq_kernels.h;
  * the host side only designs coefficients (create time, as the reference
- * does), validates arguments, moves buffers and tracks per-object state.
+ * does), validates arguments, moves buffers and tracks per-object state --
+ * except the opt-in small-call mode (lq_small.c: LQ_SMALL_CALLS=host), in
+ * which single-sample calls compute on the host.
  */
 #ifndef LQ_HOST_H
 #define LQ_HOST_H
@@ -70,6 +72,24 @@ void lq_call_done(lq_ctx *c);
  * lq_sig_wait spins for it and copies the result to y */
 void *lq_sig_out(lq_ctx *c, size_t bytes, unsigned **flag, unsigned *seq);
 void lq_sig_wait(lq_ctx *c, void *y, size_t bytes, unsigned seq);
+
+/* opt-in host path for single-sample calls (host/lq_small.c) */
+int lq_small_host(void);
+void lq_host_dot(int kind, const float *h, const void *x, unsigned int n, void *y);
+void lq_host_conv(int kind, const float *h, const void *w, unsigned int last, unsigned int n, void *y);
+typedef struct {
+    unsigned char *buf;
+    size_t n, esz, cap, off;   /* history = n samples at buf + off*esz */
+    int host_valid, dev_valid;
+} lq_mirror;
+void lq_mirror_init(lq_mirror *m, size_t n, size_t esz);
+void lq_mirror_free(lq_mirror *m);
+void lq_mirror_zero(lq_mirror *m);
+void lq_mirror_need_host(lq_mirror *m, const void *dev_hist, void *stream);
+void lq_mirror_need_dev(lq_mirror *m, void *dev_hist, void *stream);
+void lq_mirror_append(lq_mirror *m, const void *x, size_t k);
+void lq_mirror_commit(lq_mirror *m, size_t k);
+unsigned char *lq_mirror_ptr(lq_mirror *m);
 
 void *lq_xmalloc(size_t bytes);
 unsigned int lq_msb_index(unsigned int x);

@@ -61,6 +61,10 @@ struct lq_rs_s {
     rs_state now;                 /* timing state at gpos */
     void *d_hist[2];              /* last L inputs */
     int cur;
+    float *hbank;                 /* host bank taps hbank[b*L + n] = h[b + n*npfb] (small-call mode) */
+    lq_mirror hm;                 /* host copy of the history (small-call mode) */
+    rs_state hs;                  /* timing state of the host path, valid while hs_valid */
+    int hs_valid;
     lq_ctx ctx;
     lq_devbuf xbuf, ybuf;
 };
@@ -527,6 +531,11 @@ lq_rs *lq_rs_create(int kind, float _rate, unsigned int _m, float _fc, float _As
     q->d_hist[1] = lqrt_malloc((size_t)q->L * q->esz);
     lqrt_sync(q->ctx.stream);
     lqrt_sync(q->ctx.stream);
+    q->hbank = (float *)lq_xmalloc(ntap * sizeof(float));
+    for (unsigned int b = 0; b < _npfb; b++)
+        for (unsigned int k = 0; k < q->L; k++) q->hbank[b * q->L + k] = hf[b + k * _npfb];
+    lq_mirror_init(&q->hm, q->L, q->esz);
+    q->hs_valid = 0;
     free(tp);
     free(tp2);
     free(hf);
@@ -546,6 +555,8 @@ void lq_rs_destroy(lq_rs *_q)
     lq_devbuf_free(&_q->xbuf);
     lq_devbuf_free(&_q->ybuf);
     lq_ctx_free(&_q->ctx);
+    lq_mirror_free(&_q->hm);
+    free(_q->hbank);
     free(_q->pl.tab);
     free(_q);
 }
@@ -562,6 +573,8 @@ void lq_rs_reset(lq_rs *_q)
     lqrt_memset(_q->d_hist[0], (size_t)_q->L * _q->esz, _q->ctx.stream);
     lqrt_memset(_q->d_hist[1], (size_t)_q->L * _q->esz, _q->ctx.stream);
     lqrt_sync(_q->ctx.stream);
+    lq_mirror_zero(&_q->hm);
+    _q->hs_valid = 0;
     _q->now = rs_initial;
     _q->gpos = 0;
     /* a periodic plan that starts from the initial state stays usable */
@@ -574,6 +587,7 @@ static void rs_new_del(lq_rs *q, float del)
     if (memcmp(&del, &q->del, 4) == 0) return;
     lqrt_sync(q->ctx.stream);
     rs_sync_now(q);
+    q->hs_valid = 0;
     q->del = del;
     q->pl.valid = 0;
     q->periodic_failed = 0;
@@ -628,6 +642,9 @@ void lq_rs_block_dev(lq_rs *_q, const void *_dxv, unsigned long long _nx, void *
     const char *_dx = (const char *)_dxv;
     char *_dy = (char *)_dyv;
     unsigned long long total = 0;
+    lq_mirror_need_dev(&_q->hm, _q->d_hist[_q->cur], _q->ctx.stream);
+    _q->hm.host_valid = 0;
+    _q->hs_valid = 0;
     /* launches of at most LQK_RS_MAXN inputs and 2^27 outputs (32-bit
      * buffer offsets in the kernel) */
     const double r = _q->rate > 1.0f ? (double)_q->rate : 1.0;
@@ -651,10 +668,72 @@ void lq_rs_block_dev(lq_rs *_q, const void *_dxv, unsigned long long _nx, void *
     if (_ny) *_ny = total;
 }
 
+/* small-call mode: one input on the host, resamp.c:245-311 as written (the
+ * BOUNDARY state's y0 -- bank npfb-1 of the previous input, which the
+ * reference stored -- is recomputed on the window one input older) */
+static void lq_rs_exec1_host(lq_rs *q, const void *x, void *y, unsigned int *ny)
+{
+    rs_check_rate(q);
+    if (!q->hs_valid) {   /* the timing state at the stream position */
+        if (q->pl.valid) {
+            unsigned long long K;
+            q->hs = rs_plan_at(&q->pl, q->gpos, q->del, q->npfb, &K);
+        } else {
+            q->hs = q->now;
+        }
+        q->hs_valid = 1;
+    }
+    lq_mirror_need_host(&q->hm, q->d_hist[q->cur], q->ctx.stream);
+    lq_mirror_append(&q->hm, x, 1);
+    const unsigned char *w = lq_mirror_ptr(&q->hm);   /* L + 1 samples, x last */
+    const int ck = q->kind == LQ_RRRF ? LQ_RRRF : LQ_CRCF;   /* real taps for every type */
+    const unsigned int L = q->L, npfb = q->npfb;
+    const int np = (int)npfb;
+    rs_state *s = &q->hs;
+    unsigned int n = 0;
+    while ((unsigned int)s->b < npfb) {   /* unsigned, as resamp.c:254 */
+        if (s->st == RS_INTERP && s->b == np - 1) {
+            s->st = RS_BOUNDARY;
+            s->b = np;
+            break;
+        }
+        float y0[2] = {0.f, 0.f}, y1[2] = {0.f, 0.f};
+        if (s->st == RS_BOUNDARY) {
+            lq_host_conv(ck, q->hbank + (size_t)(npfb - 1) * L, w, L - 1, L, y0);
+            lq_host_conv(ck, q->hbank, w, L, L, y1);
+        } else {
+            lq_host_conv(ck, q->hbank + (size_t)s->b * L, w, L, L, y0);
+            lq_host_conv(ck, q->hbank + (size_t)(s->b + 1) * L, w, L, L, y1);
+        }
+        const float a = 1.0f - s->mu;
+        float *yo = (float *)((unsigned char *)y + (size_t)n * q->esz);
+        yo[0] = a * y0[0] + s->mu * y1[0];
+        if (q->kind != LQ_RRRF) yo[1] = a * y0[1] + s->mu * y1[1];
+        n++;
+        s->tau += q->del;                          /* resamp.c:352-363 */
+        const float bf = s->tau * (float)npfb;
+        s->b = (int)floorf(bf);
+        s->mu = bf - (float)s->b;
+        s->st = RS_INTERP;
+    }
+    s->tau -= 1.0f;
+    s->b = (int)((unsigned int)s->b - npfb);
+    lq_mirror_commit(&q->hm, 1);
+    /* the device path continues from here: its plan position, or its state */
+    if (q->pl.valid && (q->pl.periodic || q->gpos + 1 <= q->pl.end)) q->gpos += 1;
+    else q->pl.valid = 0;
+    q->now = *s;
+    *ny = n;
+}
+
 static void lq_rs_block(lq_rs *_q, const void *_x, unsigned int _nx, void *_y, unsigned int *_ny)
 {
     if (_nx == 0) {
         *_ny = 0;
+        return;
+    }
+    if (_nx == 1 && lq_small_host()) {
+        lq_rs_exec1_host(_q, _x, _y, _ny);
         return;
     }
     unsigned long long nout = lq_rs_num_output(_q, _nx);

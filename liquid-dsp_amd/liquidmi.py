@@ -48,6 +48,16 @@ def lib():
     return _lib
 
 
+def set_small_calls(host):
+    """Small-call mode (include/liquid_mi355x.h): True computes single-sample
+    calls on the host (host/lq_small.c), False (the default) on the GPU."""
+    lib().liquid_mi355x_set_small_calls(1 if host else 0)
+
+
+def get_small_calls():
+    return bool(lib().liquid_mi355x_get_small_calls())
+
+
 def header_functions():
     """Every function the public header declares (macros expanded by cpp)."""
     out = subprocess.check_output(["gcc", "-E", "-P", "-I", os.path.join(ROOT, "include"), HEADER],
