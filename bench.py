@@ -611,9 +611,16 @@ def main():
         alg_bytes = 24.0 * pfb["n"]
         achieved = alg_bytes / (launch_ms * 1e-3) / 1e9
         traffic = fir_traffic = rs_traffic = ff_traffic = None
+        tsrc = None
         if os.path.exists(args.traffic_json):
             with open(args.traffic_json) as f:
                 tj = json.load(f)
+            # the PMC bytes are not counted in this timed run: a separate
+            # rocprofv3 --pmc pass over the same launch shapes wrote them
+            tsrc = ("HBM bytes per launch from %s: rocprofv3 --pmc FETCH_SIZE (x2, gfx950) + WRITE_SIZE in "
+                    "separate passes over the same launch shapes (tools/profile_round.sh), not counted in this "
+                    "timed run%s" % (os.path.relpath(args.traffic_json, ROOT),
+                                     (", measured " + tj["measured"]) if tj.get("measured") else ""))
             traffic = tj.get("firpfbch2_bytes_per_launch")
             fir_traffic = tj.get("firfilt_bytes_per_launch")
             rs_traffic = tj.get("resamp_bytes_per_launch")
@@ -635,7 +642,7 @@ def main():
                                    % pfb["n"], "M": 1024, "m": 4, "samples_per_gpu": pfb["n"],
                        "blocks_per_step": pfb["nblocks"], "parallelism": "stream-per-gpu x%d" % world},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBPS, "unit": "GB/s",
-                         "frac": achieved / HBM_PEAK_GBPS, "traffic": traffic,
+                         "frac": achieved / HBM_PEAK_GBPS, "traffic": traffic, "traffic_source": tsrc,
                          "bytes_per_unit": "24 B/input sample (8 read + 16 write)",
                          "launch_ms": launch_ms, "measured_copy_GBps": copy_gbps},
             "cpu_baseline": cpu,
@@ -659,7 +666,7 @@ def main():
                                        "samples_per_gpu": fir["n"], "ms_per_step": t_fir / args.steps * 1e3,
                                        "roofline": {"bound": "hbm", "achieved": fach, "peak": HBM_PEAK_GBPS,
                                                     "unit": "GB/s", "frac": fach / HBM_PEAK_GBPS,
-                                                    "traffic": fir_traffic,
+                                                    "traffic": fir_traffic, "traffic_source": tsrc,
                                                     "bytes_per_unit": "16 B/sample", "launch_ms": fl_ms},
                                        "arith": ("f32-accurate: taps and samples split into three bf16 terms, "
                                                  "six exact products accumulated in f32 on "
@@ -679,7 +686,7 @@ def main():
                                                       "kernel), wall clock",
                                         "roofline": {"bound": "hbm", "achieved": rach, "peak": HBM_PEAK_GBPS,
                                                      "unit": "GB/s", "frac": rach / HBM_PEAK_GBPS,
-                                                     "traffic": rs_traffic,
+                                                     "traffic": rs_traffic, "traffic_source": tsrc,
                                                      "bytes_per_unit": "8 B/input + 8 B/output",
                                                      "launch_ms": rl_ms}}
         if dp is not None:
@@ -704,7 +711,7 @@ def main():
                                                      "achieved": 16.0 * ff["n"] / (ms * 1e-3) / 1e9,
                                                      "peak": HBM_PEAK_GBPS, "unit": "GB/s",
                                                      "frac": 16.0 * ff["n"] / (ms * 1e-3) / 1e9 / HBM_PEAK_GBPS,
-                                                     "traffic": ff_traffic, "bytes_per_unit": "16 B/sample",
+                                                     "traffic": ff_traffic, "traffic_source": tsrc, "bytes_per_unit": "16 B/sample",
                                                      "launch_ms": ms}}
         if percall is not None:
             out["per_call"] = {"what": "the reference's per-call benchmark loops (src/*/bench/*_benchmark.c) "

@@ -50,6 +50,10 @@
 #ifndef FMX_VARIANT
 #define FMX_VARIANT 0
 #endif
+#ifndef FMX_WGS
+#define FMX_WGS 512   // crcf 33..64 taps: persistent workgroups, two per CU (A/B on one box: 0.804 ms vs
+                      // 0.822-0.826 at three per CU with two chunks in flight, 0.819-0.821 two per CU with two)
+#endif
 
 namespace {
 
@@ -91,7 +95,7 @@ constexpr int glen_kb() { return 16 * (2 + 4 * KB) + 32; }
 #define FMX_A2L 0
 #endif
 #ifndef FMX_NBUF
-#define FMX_NBUF 2   // chunks of loads in flight per workgroup (register sets)
+#define FMX_NBUF 3   // chunks of loads in flight per workgroup (register sets; 2..4)
 #endif
 template <bool CC, int KB>
 constexpr int nal_kb() { return KB > 2 ? 3 : ((!CC && KB == 1 && FMX_A2L) ? 2 : 0); }
@@ -221,7 +225,7 @@ __device__ __forceinline__ void load8b(__amdgpu_buffer_rsrc_t rx, unsigned off, 
 // accumulators, C1 = Hr [Xr | Xi] and C2 = Hi [Xr | Xi]; y = (C1.re - C2.im,
 // C1.im + C2.re) is formed when the staged accumulators are read back.
 template <bool CC, int KB>
-__global__ __launch_bounds__(NT, KB > 2 ? 2 : ((CC || KB > 1) ? 2 : 3)) void k_firfilt_mx(const v2f *__restrict__ win,
+__global__ __launch_bounds__(NT, KB > 2 ? 2 : ((CC || KB > 1 || FMX_WGS <= 512) ? 2 : 3)) void k_firfilt_mx(const v2f *__restrict__ win,
                                                               const v2f *__restrict__ x, long long n,
                                                               v2f *__restrict__ y, const float *__restrict__ hpad,
                                                               float sre, float sim, long long nch, int hlen)
@@ -323,8 +327,8 @@ __global__ __launch_bounds__(NT, KB > 2 ? 2 : ((CC || KB > 1) ? 2 : 3)) void k_f
     // [/ (xc, hc)] rotate (the loop is unrolled by NB so no set is ever
     // copied, which would wait on its loads early)
     constexpr int NB = nbuf_kb<CC, KB>();
-    v4f xa[4], xb[4], xc[4];
-    v2f ha, hb, hc;
+    v4f xa[4], xb[4], xc[4], xd[4];
+    v2f ha, hb, hc, hd;
     load8b(rx, main_off(0), xa);
     ha = ldh(halo_off(0));
     load8b(rx, main_off(1), xb);
@@ -332,6 +336,10 @@ __global__ __launch_bounds__(NT, KB > 2 ? 2 : ((CC || KB > 1) ? 2 : 3)) void k_f
     if constexpr (NB > 2) {
         load8b(rx, main_off(2), xc);
         hc = ldh(halo_off(2));
+    }
+    if constexpr (NB > 3) {
+        load8b(rx, main_off(3), xd);
+        hd = ldh(halo_off(3));
     }
 
     // B operand: lane column n = r32 -> segment sg = n & 15, component n >> 4
@@ -437,6 +445,7 @@ __global__ __launch_bounds__(NT, KB > 2 ? 2 : ((CC || KB > 1) ? 2 : 3)) void k_f
         step(k, xa, ha);
         step(k + 1, xb, hb);
         if constexpr (NB > 2) step(k + 2, xc, hc);
+        if constexpr (NB > 3) step(k + 3, xd, hd);
     }
     // the range guard's chunks: the exact float32 outputs overwrite what the
     // matrix path stored for them.  Only workgroup-scope ordering is needed
@@ -453,159 +462,6 @@ __global__ __launch_bounds__(NT, KB > 2 ? 2 : ((CC || KB > 1) ? 2 : 3)) void k_f
         for (int k = 0; k < (int)cnt; k++)
             if (bad_mask[k >> 5] & (1u << (k & 31)))
                 exact_chunk_c<CC, HALO>(win, x, n, y, hpad, hlen, CH * (w + k * G) + 8 * tid, 8, sre, sim);
-    }
-}
-
-// ------------------------------------------------ crcf, wave-private form
-// The same tile, owned end to end by one wave: wave-granular quarters of 512
-// outputs are dealt grid-stride over all waves of the launch (global wave g
-// takes quarters g, g + GW, ...: the chip still streams one window), and each
-// wave loads its own span -- 512 samples, 8 per lane, plus the 64-sample halo
-// before them, one per lane (the neighbouring wave's tail, an L2 hit) -- into
-// its own bf16 planes.  No workgroup barrier: a wave orders its own LDS
-// traffic, so loads, plane writes, MFMAs, staging and stores of the four waves
-// of a workgroup no longer wait for one another, and the accumulator staging
-// reuses the wave's planes once its MFMAs have read them.  The range guard is
-// a wave ballot; the quarters holding an unsafe sample are recomputed by the
-// exact dot product after the loop (the wave's own outputs, stored again in
-// program order; a bit per quarter in a per-wave LDS mask).
-#ifndef FMX_WAVE
-#define FMX_WAVE 0
-#endif
-constexpr int QW = 512;                                                  // outputs per quarter (one tile)
-constexpr int PLBW = ((QW + 64) * 2 + 16 * ((QW + 64) / 32) + 255) & ~255;   // 1536 B per plane
-constexpr int LDSW = 6 * PLBW;                                           // per wave (staging overlays it)
-constexpr int QMASKW = 8;                                                // mask words per wave: <= 256 quarters
-static_assert(16 * SSTR * 4 <= LDSW, "staging fits the wave's planes");
-
-__global__ __launch_bounds__(NT, 3) void k_firfilt_mxw(const v2f *__restrict__ win, const v2f *__restrict__ x,
-                                                      long long n, v2f *__restrict__ y, const float *__restrict__ hpad,
-                                                      float sre, long long nq, int hlen)
-{
-    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-    constexpr int HALO = 64, NS = 6;
-    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    const int r32 = lane & 31, hh = lane >> 5;
-    unsigned char *planes = smem + wave * LDSW;
-    float *stage = reinterpret_cast<float *>(planes);
-    unsigned *qmask = reinterpret_cast<unsigned *>(smem + 4 * LDSW) + wave * QMASKW;
-
-    // A fragments (three bf16 terms x six K steps), as k_firfilt_mx
-    bf16x8 A[3][NS];
-#pragma unroll
-    for (int st = 0; st < NS; st++) {
-        bf16x2 t[3][4];
-#pragma unroll
-        for (int q = 0; q < 4; q++) {
-            float hv[2];
-#pragma unroll
-            for (int u = 0; u < 2; u++) {
-                const int k = r32 + HALO - (16 * st + 8 * hh + 2 * q + u);
-                hv[u] = (k >= 0 && k < HALO) ? hpad[k] : 0.f;
-            }
-            split3(v2f{hv[0], hv[1]}, t[0][q], t[1][q], t[2][q]);
-        }
-#pragma unroll
-        for (int p = 0; p < 3; p++)
-            A[p][st] = bf16x8{t[p][0].x, t[p][0].y, t[p][1].x, t[p][1].y, t[p][2].x, t[p][2].y, t[p][3].x, t[p][3].y};
-    }
-
-    const long long GW = (long long)gridDim.x * (NT / 64), gw = (long long)blockIdx.x * (NT / 64) + wave;
-    if (gw >= nq) return;   // wave-uniform; no workgroup barrier below
-    const long long cnt = (nq - gw + GW - 1) / GW;   // <= 32 QMASKW (host)
-    if (lane < QMASKW) qmask[lane] = 0u;
-    const __amdgpu_buffer_rsrc_t rx = __builtin_amdgcn_make_buffer_rsrc((void *)x, (short)0, (int)(n * 8), 0x00020000);
-    const __amdgpu_buffer_rsrc_t rh = __builtin_amdgcn_make_buffer_rsrc((void *)win, (short)0, HALO * 8, 0x00020000);
-    const __amdgpu_buffer_rsrc_t ry = __builtin_amdgcn_make_buffer_rsrc((void *)y, (short)0, (int)(n * 8), 0x00020000);
-    const unsigned OOB = 0xfffff000u;
-    auto main_off = [&](long long k) -> unsigned {
-        const long long q = gw + k * GW;
-        return q < nq ? (unsigned)(QW * q + 8 * lane) * 8u : OOB;
-    };
-    // the halo sample t = 512 q - 64 + lane: from x, or (quarter 0) from the
-    // history; each offset is in range in at most one descriptor, so the sum
-    // of the two loads is the sample, with no branch
-    auto halo_ld = [&](long long k) -> v2f {
-        const long long q = gw + k * GW;
-        const long long t = QW * q - HALO + lane;
-        const unsigned ox = (q < nq && t >= 0) ? (unsigned)t * 8u : OOB;
-        const unsigned oh = (q < nq && t < 0) ? (unsigned)(t + HALO) * 8u : OOB;
-        return __builtin_bit_cast(v2f, __builtin_amdgcn_raw_buffer_load_b64(rx, ox, 0, 0)) +
-               __builtin_bit_cast(v2f, __builtin_amdgcn_raw_buffer_load_b64(rh, oh, 0, 0));
-    };
-    v4f xa[4], xb[4];
-    v2f ha, hb;
-    load8b(rx, main_off(0), xa);
-    ha = halo_ld(0);
-    load8b(rx, main_off(1), xb);
-    hb = halo_ld(1);
-
-    const int sg = r32 & 15, comp = r32 >> 4;
-    auto step = [&](long long k, v4f (&xv)[4], v2f &hv) {
-        const long long q = gw + k * GW;
-        // the previous quarter's staging reads are done (same wave: LDS order)
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-        __builtin_amdgcn_wave_barrier();
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-        put1(planes, PLBW, lane, hv);
-        put8(planes, PLBW, HALO + 8 * lane, xv);
-        const bool bad = __builtin_amdgcn_ballot_w64((unsafe_bits(hv.x) | unsafe_bits(hv.y) | unsafe4(xv[0]) |
-                                                      unsafe4(xv[1]) | unsafe4(xv[2]) | unsafe4(xv[3])) != 0u) != 0;
-        load8b(rx, main_off(k + 2), xv);
-        hv = halo_ld(k + 2);
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-        __builtin_amdgcn_wave_barrier();
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-
-        f32x16 C = f32x16{};
-#pragma unroll
-        for (int st = 0; st < NS; st++) {
-            const int pos = 32 * sg + 16 * st + 8 * hh;
-            const unsigned char *bp = planes + comp * PLBW + poff(pos);
-            const bf16x8 b0 = *reinterpret_cast<const bf16x8 *>(bp);
-            const bf16x8 b1 = *reinterpret_cast<const bf16x8 *>(bp + 2 * PLBW);
-            const bf16x8 b2 = *reinterpret_cast<const bf16x8 *>(bp + 4 * PLBW);
-            C = __builtin_amdgcn_mfma_f32_32x32x16_bf16(A[0][st], b2, C, 0, 0, 0);
-            C = __builtin_amdgcn_mfma_f32_32x32x16_bf16(A[1][st], b1, C, 0, 0, 0);
-            C = __builtin_amdgcn_mfma_f32_32x32x16_bf16(A[2][st], b0, C, 0, 0, 0);
-            C = __builtin_amdgcn_mfma_f32_32x32x16_bf16(A[0][st], b1, C, 0, 0, 0);
-            C = __builtin_amdgcn_mfma_f32_32x32x16_bf16(A[1][st], b0, C, 0, 0, 0);
-            C = __builtin_amdgcn_mfma_f32_32x32x16_bf16(A[0][st], b0, C, 0, 0, 0);
-        }
-        // the MFMAs' plane reads are complete before the staging overwrites them
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-        __builtin_amdgcn_wave_barrier();
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-#pragma unroll
-        for (int r = 0; r < 16; r++) stage[sg * SSTR + 2 * ((r & 3) + 8 * (r >> 2) + 4 * hh) + comp] = C[r];
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-        __builtin_amdgcn_wave_barrier();
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-        const unsigned o0 = (unsigned)(QW * q) * 8u;
-#pragma unroll
-        for (int u = 0; u < 4; u++) {
-            const int o = 2 * (lane + 64 * u);
-            const v4f a = *reinterpret_cast<const v4f *>(stage + (o >> 5) * SSTR + 2 * (o & 31));
-            __builtin_amdgcn_raw_buffer_store_b128(a * sre, ry, q < nq ? o0 + 8u * o : OOB, 0, 2);
-        }
-        if (bad && q < nq && lane == 0) qmask[k >> 5] |= 1u << (k & 31);
-    };
-    for (long long k = 0; k < cnt; k += 2) {
-        step(k, xa, ha);
-        step(k + 1, xb, hb);
-    }
-    // the exact float32 outputs of the guarded quarters, after the matrix ones
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-    unsigned anybad = 0;
-#pragma unroll
-    for (int i = 0; i < QMASKW; i++) anybad |= qmask[i];
-    if (anybad) {
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-        for (int k = 0; k < (int)cnt; k++)
-            if (qmask[k >> 5] & (1u << (k & 31)))
-                exact_chunk_c<false, HALO>(win, x, n, y, hpad, hlen, QW * (gw + k * GW) + 8 * lane, 8, sre, 0.f);
     }
 }
 
@@ -823,7 +679,7 @@ static void launch_mx(const lqk_fir_desc *d, const void *hist, const void *x, lo
     const bool kb2 = d->nchunk == 2;   // crcf, 65..128 taps
     const int kb = (int)d->nchunk;     // crcf: 129..192 / 193..256 taps with the A fragments in LDS
     const long long nch = (n + CH - 1) / CH;
-    const long long wgs = (cc || kb2) ? 512 : 768;   // resident workgroups (two / three per CU)
+    const long long wgs = (cc || kb2) ? 512 : FMX_WGS;   // resident workgroups (two / three per CU)
     const dim3 grid((unsigned)(nch < wgs ? nch : wgs));
     constexpr int lds_kb2 = lds_bytes_mx<false, 2>() + 80;
     if (!cc && kb > 2) {
@@ -844,16 +700,7 @@ static void launch_mx(const lqk_fir_desc *d, const void *hist, const void *x, lo
         hipLaunchKernelGGL((k_firfilt_mx<true, 1>), grid, dim3(NT), lds_bytes_mx<true>() + 80, st, (const v2f *)hist,
                            (const v2f *)x, n, (v2f *)y, (const float *)d->hpad, d->scale_re, d->scale_im, nch,
                            (int)d->hlen);
-    else if (FMX_WAVE) {
-        const long long nq = (n + QW - 1) / QW;
-        const long long wg = (nq + 3) / 4 < 768 ? (nq + 3) / 4 : 768;   // three workgroups per CU
-        if ((nq + 4 * wg - 1) / (4 * wg) > 32 * QMASKW) {
-            fprintf(stderr, "error: firfilt: launch of %lld samples exceeds the guard mask\n", n);
-            exit(1);
-        }
-        hipLaunchKernelGGL(k_firfilt_mxw, dim3((unsigned)wg), dim3(NT), 4 * LDSW + 4 * QMASKW * 4, st, (const v2f *)hist,
-                           (const v2f *)x, n, (v2f *)y, (const float *)d->hpad, d->scale_re, nq, (int)d->hlen);
-    } else
+    else
         hipLaunchKernelGGL((k_firfilt_mx<false, 1>), grid, dim3(NT), lds_bytes_mx<false>() + 80, st, (const v2f *)hist,
                            (const v2f *)x, n, (v2f *)y, (const float *)d->hpad, d->scale_re, d->scale_im, nch,
                            (int)d->hlen);

@@ -277,7 +277,7 @@ __device__ __forceinline__ rs_ref rs_locate_near(const lqk_rs_plan &pl, unsigned
 #define RS_RIN 4
 #endif
 #ifndef RS_EXP
-#define RS_EXP 0   // timing experiments (wrong outputs): 1 no checkpoint skip, 2 no evaluation, 4 no replay
+#define RS_EXP 0   // timing experiments (wrong outputs): 1 no checkpoint skip, 2 no evaluation, 4 no descriptor writes
 #endif
 // workgroups per CU: six for L <= 16 (25.5 KB LDS, <= 80 VGPRs each: L = 14
 // 0.236 -> 0.221 ms against five); longer filters spill at 80 VGPRs
@@ -300,6 +300,15 @@ constexpr int rs2_cap() { return NT * RS_RIN + RS_CAPX; }
 #endif
 #ifndef RS_RSC
 #define RS_RSC 1   // pair-table row stride a compile-time constant (npfb <= 64: 33) -> immediate tap offsets
+#endif
+#ifndef RS_STAUX
+#define RS_STAUX 2  // cache policy of the output stores: non-temporal (A/B on one box: 0.197 vs 0.206 ms)
+#endif
+#ifndef RS_LDAUX
+#define RS_LDAUX 0  // cache policy of the input loads
+#endif
+#ifndef RS_RWAVE
+#define RS_RWAVE 0  // replay on wave blockIdx mod 4 instead of wave 0
 #endif
 #ifndef RS_UNR
 #define RS_UNR 0   // power-of-two replay: the first RS_UNR outputs of each input unrolled, predicated
@@ -382,23 +391,23 @@ __device__ __forceinline__ float rs_fma(float c, float w, float acc) { return fm
 __device__ __forceinline__ void rs_store1(__amdgpu_buffer_rsrc_t r, unsigned off, float2 v)
 {
     typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
-    __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2, v), r, off, 0, 0);
+    __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2, v), r, off, 0, RS_STAUX);
 }
 __device__ __forceinline__ void rs_store1(__amdgpu_buffer_rsrc_t r, unsigned off, float v)
 {
-    __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, v), r, off, 0, 0);
+    __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, v), r, off, 0, RS_STAUX);
 }
 __device__ __forceinline__ void rs_store2(__amdgpu_buffer_rsrc_t r, unsigned off, float2 a, float2 b)
 {
     typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
     const u32x4 v = {__float_as_uint(a.x), __float_as_uint(a.y), __float_as_uint(b.x), __float_as_uint(b.y)};
-    __builtin_amdgcn_raw_buffer_store_b128(v, r, off, 0, 0);
+    __builtin_amdgcn_raw_buffer_store_b128(v, r, off, 0, RS_STAUX);
 }
 __device__ __forceinline__ void rs_store2(__amdgpu_buffer_rsrc_t r, unsigned off, float a, float b)
 {
     typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
     const u32x2 v = {__float_as_uint(a), __float_as_uint(b)};
-    __builtin_amdgcn_raw_buffer_store_b64(v, r, off, 0, 0);
+    __builtin_amdgcn_raw_buffer_store_b64(v, r, off, 0, RS_STAUX);
 }
 
 template <int L, typename S, int RSC, bool PR>
@@ -426,6 +435,11 @@ __global__ __launch_bounds__(NT, rs2_blk<L>()) void k_resamp2(lqk_rs_plan pl, un
 
     const int tid = threadIdx.x;
     const float fnpfb = (float)npfb;
+    // the replaying wave: wave 0, or (RS_RWAVE) wave blockIdx mod 4, so the
+    // serial replays of the workgroups resident on a CU do not all land on the
+    // SIMD that holds their wave 0; rlane = lane in it, -1 elsewhere
+    const int rwave = RS_RWAVE ? (int)(blockIdx.x & 3) : 0;
+    const int rlane = (tid >> 6) == rwave ? (tid & 63) : -1;
     for (int t = tid; t < (npfb + 1) * NROW; t += NT) {
         const int b = t / NROW, r = t % NROW, p = r - ROFF;
         const float2 v = (p >= 0 && p <= L) ? taps2[b * LP + p] : make_float2(0.0f, 0.0f);
@@ -458,9 +472,9 @@ __global__ __launch_bounds__(NT, rs2_blk<L>()) void k_resamp2(lqk_rs_plan pl, un
     auto ld = [&](__amdgpu_buffer_rsrc_t r, int e) -> S {
         const unsigned off = e < 0 ? 0xFFFFFFF0u : (unsigned)e * (unsigned)sizeof(S);
         if constexpr (sizeof(S) == 8)
-            return __builtin_bit_cast(S, __builtin_amdgcn_raw_buffer_load_b64(r, off, 0, 0));
+            return __builtin_bit_cast(S, __builtin_amdgcn_raw_buffer_load_b64(r, off, 0, RS_LDAUX));
         else
-            return __builtin_bit_cast(S, __builtin_amdgcn_raw_buffer_load_b32(r, off, 0, 0));
+            return __builtin_bit_cast(S, __builtin_amdgcn_raw_buffer_load_b32(r, off, 0, RS_LDAUX));
     };
     struct Pre {
         S xa[NXV], xh;                           // tile window; the history part of its first vector
@@ -485,7 +499,7 @@ __global__ __launch_bounds__(NT, rs2_blk<L>()) void k_resamp2(lqk_rs_plan pl, un
             ct = t / pl.P;
             jt = pl.pre + (t - ct * pl.P);
         }
-        const int d = tid < NSPAN && tid * SPAN < tin ? tid * SPAN : 0;
+        const int d = rlane >= 0 && rlane * SPAN < tin ? rlane * SPAN : 0;
         const rs_ref r = rs_locate_near(pl, gt, jt, ct, (unsigned)d);
         f.e = rs_load(pl, r.ck);
         f.cyc = r.cyc;
@@ -519,8 +533,8 @@ __global__ __launch_bounds__(NT, rs2_blk<L>()) void k_resamp2(lqk_rs_plan pl, un
         // wave 0 replays the timing: lane s the SPAN inputs from i0 + s SPAN,
         // starting at its checkpoint (skip < SPAN inputs before them), writing
         // the tile's output list and the outputs before its last input
-        if (tid < NSPAN) {
-            const long long ia = i0 + (long long)tid * SPAN;
+        if (rlane >= 0) {
+            const long long ia = i0 + (long long)rlane * SPAN;
             const int nin = ia < ie ? (int)((ie - ia) < SPAN ? (ie - ia) : SPAN) : 0;
             unsigned long long k = (unsigned long long)e.K + cyc * pl.Q;
             auto put = [&](unsigned long long Kb, int iloc, int bank, float mu) {
@@ -620,8 +634,8 @@ __global__ __launch_bounds__(NT, rs2_blk<L>()) void k_resamp2(lqk_rs_plan pl, un
                     st.b = (int)((unsigned)st.b - (unsigned)npfb);
                 }
             }
-            if (nin > 0) kx[tid + 1] = k;
-            if (tid == 0) kx[0] = Kb;
+            if (nin > 0) kx[rlane + 1] = k;
+            if (rlane == 0) kx[0] = Kb;
         }
         __syncthreads();
         const unsigned long long Kb = kx[0];
@@ -714,9 +728,9 @@ __global__ __launch_bounds__(NT, rs2_blk<L>()) void k_resamp2(lqk_rs_plan pl, un
             const unsigned off = o < nr ? (ob + (unsigned)o) * (unsigned)sizeof(S) : 0xFFFFFFF0u;
             if constexpr (sizeof(S) == 8) {
                 typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
-                __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2, v), ry, off, 0, 0);
+                __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2, v), ry, off, 0, RS_STAUX);
             } else {
-                __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, v), ry, off, 0, 0);
+                __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, v), ry, off, 0, RS_STAUX);
             }
         }
         }

@@ -43,7 +43,8 @@ json.dump({"firpfbch2_bytes_per_launch": traffic.get("firpfbch2", {}).get("total
                                        "correction is calibrated for 16-byte streams only)",
                              "fftfilt": "h=512, 4096-point overlap-save, 2^26 samples"},
            "method": "rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE in separate passes over tools/prof_run.py; "
-                     "FETCH_SIZE doubled per the gfx950 correction"},
+                     "FETCH_SIZE doubled per the gfx950 correction",
+           "measured": "%s, profile tag %s" % (__import__("time").strftime("%Y-%m-%d"), os.path.basename(out))},
           open(os.path.join(out, "traffic.json"), "w"), indent=1)
 print(json.dumps(traffic))
 PY
