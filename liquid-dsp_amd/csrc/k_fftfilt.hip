@@ -32,6 +32,8 @@ constexpr int NFFT = 4096;
 // segment instead of the first only: 0.367 ms)
 #ifndef FF_HREG
 #define FF_HREG true
+#endif
+#ifndef FF_WPE
 #define FF_WPE 4
 #endif
 #ifndef FF_STAUX

@@ -99,8 +99,11 @@ constexpr int glen_kb() { return 16 * (2 + 4 * KB) + 32; }
 #endif
 template <bool CC, int KB>
 constexpr int nal_kb() { return KB > 2 ? 3 : ((!CC && KB == 1 && FMX_A2L) ? 2 : 0); }
+#ifndef FMX_NBUF_KB
+#define FMX_NBUF_KB 2   // the same for crcf with 65..256 taps (KB >= 2, two workgroups per CU)
+#endif
 template <bool CC, int KB>
-constexpr int nbuf_kb() { return (!CC && KB == 1) ? FMX_NBUF : 2; }
+constexpr int nbuf_kb() { return CC ? 2 : (KB == 1 ? FMX_NBUF : FMX_NBUF_KB); }
 // elements between the eight shifted copies: at least NAL GL, and 16 mod 128
 // (32 B mod 256), so the 16 lanes of a ds_read_b128 pass -- eight copies at
 // two bases 16 B apart -- land on 16 distinct bank groups (a stride that is
