@@ -170,7 +170,7 @@ unsigned int lqk_fftfilt_nfft(void);
  * Inputs g >= pre repeat with period P (Q outputs per period): state(g) =
  * state(pre + (g-pre) % P), K += Q per period; positions beyond `end` are
  * clamped to it (direct plans cover end + 1 positions). */
-#define LQK_RS_CK 16
+#define LQK_RS_CK 4   /* a checkpoint per replay lane's 4 inputs (csrc/k_resamp.hip k_resamp3) */
 typedef struct {
     float tau, mu;
     int bst;

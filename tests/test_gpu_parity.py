@@ -907,8 +907,8 @@ def test_resamp_vs_oracle_ragged(rate, m, npfb):
     assert G.nrm_err(y, ref) < NRM
 
 
-@pytest.mark.parametrize("rate,npfb", [(30.0, 64), (64.0, 64), (100.0, 64), (83.3, 64), (75.5, 64),
-                                       (130.7, 64), (57.3, 37)])
+@pytest.mark.parametrize("rate,npfb", [(30.0, 64), (58.9, 64), (59.9, 64), (64.0, 64), (100.0, 64), (83.3, 64),
+                                       (75.5, 64), (130.7, 64), (57.3, 37)])
 def test_resamp_high_rate_vs_oracle(rate, npfb):
     """rates whose 16-input tiles overflow the tiled kernel's 1088 output
     slots (r > ~60) run the per-input kernel; rates above npfb follow the
@@ -918,6 +918,22 @@ def test_resamp_high_rate_vs_oracle(rate, npfb):
     x = cx(r, 6000)
     g, o = _resamp_pair(rate, m=7, npfb=npfb)
     cuts = [0, 1, 17, 18, 1000, 1001, 4096, 6000]
+    ys = [g.execute(x[a]) if b - a == 1 else g.execute_block(x[a:b]) for a, b in zip(cuts[:-1], cuts[1:])]
+    y = np.concatenate(ys)
+    ref = o.execute_block(x)
+    assert len(y) == len(ref)
+    assert G.nrm_err(y, ref) < NRM
+
+
+@pytest.mark.parametrize("rate,m", [(40.0, 12), (45.3, 16), (35.0, 9), (20.0, 16)])
+def test_resamp_high_rate_long_filter_vs_oracle(rate, m):
+    """high rates shrink the tiles to 16-32 inputs, fewer than the L + 1 =
+    2m + 1 window samples: tiles after the first of a call also reach into
+    the history (a round-3 kernel read zeros there)"""
+    r = rng(int(rate * 7) + m)
+    x = cx(r, 3000)
+    g, o = _resamp_pair(rate, m=m, npfb=64)
+    cuts = [0, 1, 40, 41, 1000, 3000]
     ys = [g.execute(x[a]) if b - a == 1 else g.execute_block(x[a:b]) for a, b in zip(cuts[:-1], cuts[1:])]
     y = np.concatenate(ys)
     ref = o.execute_block(x)
@@ -1040,10 +1056,17 @@ REF_EX = os.path.join(LQ.ROOT, "build", "ref_examples")
 
 @pytest.mark.skipif(not os.path.isdir(REF_EX), reason="reference examples not built (tools/build_ref_examples.sh)")
 @pytest.mark.parametrize("exe", sorted(os.listdir(REF_EX)) if os.path.isdir(REF_EX) else [])
-def test_reference_examples_run(exe, tmp_path):
+@pytest.mark.parametrize("small_calls", ["gpu", "host"])
+def test_reference_examples_run(exe, small_calls, tmp_path):
     """liquid-dsp's own example programs, compiled unchanged against the
-    drop-in header, run to completion on the GPU (they write .m files)."""
-    res = subprocess.run([os.path.join(REF_EX, exe)], capture_output=True, text=True, timeout=120, cwd=tmp_path)
+    drop-in header, run to completion on the GPU (they write .m files); and
+    again with the opt-in host path for single-sample calls (LQ_SMALL_CALLS)."""
+    env = dict(os.environ)
+    env.pop("LQ_SMALL_CALLS", None)
+    if small_calls == "host":
+        env["LQ_SMALL_CALLS"] = "host"
+    res = subprocess.run([os.path.join(REF_EX, exe)], capture_output=True, text=True, timeout=120, cwd=tmp_path,
+                         env=env)
     print(res.stdout[-2000:], res.stderr[-2000:])
     assert res.returncode == 0
     assert "error" not in res.stderr.lower()
