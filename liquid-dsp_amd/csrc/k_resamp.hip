@@ -375,16 +375,31 @@ __global__ __launch_bounds__(NT) void k_resamp_generic(lqk_rs_plan pl, unsigned 
 #define RS3_BLK 5
 #endif
 constexpr int W3_TIN = 64 * 4;   // inputs per wave tile (64 lanes x 4)
-constexpr int W3_CAP = 320;      // output slots per wave tile
-template <int L, typename S, int RSC>
+#ifndef RS3_CAP
+#define RS3_CAP 320
+#endif
+constexpr int W3_CAP = RS3_CAP;  // output slots per wave tile
+#ifndef RS3_PAIR
+#define RS3_PAIR 0
+#endif
+// PR: the pair-table rows padded with a zero row on either side (pair mode)
+template <int L, typename S, int RSC, bool PR = false>
 inline size_t rs3_lds_bytes(int npfb)
 {
     constexpr int TS = W3_TIN + L + 2;
-    return (size_t)2 * (L + 1) * rs2_rs<RSC>(npfb) * sizeof(float2) +
+    return (size_t)2 * (L + 1 + (PR ? 2 : 0)) * rs2_rs<RSC>(npfb) * sizeof(float2) +
            (size_t)4 * (((TS + 2) * sizeof(S) + 15) / 16 * 16 + (W3_CAP + 2) * 8);
 }
 
-template <int L, typename S, int RSC>
+// PR (rates > 1: consecutive outputs at most one input apart, see
+// launch_rs): each lane evaluates two consecutive outputs A, B (inputs iA,
+// iB = iA + d, d in {0, 1}) over one shared window W[p'] = x[iA - L + p'],
+// p' <= L + 1; A's taps are table rows p', B's rows p' - d, the table padded
+// with a zero row on either side, so each window sample is read once for
+// both outputs (16 + 15 + 16 LDS reads per pair at L = 14 instead of
+// 2 x 30); the sample outside B's window enters as 0, so a non-finite input
+// there never reaches B
+template <int L, typename S, int RSC, bool PR>
 __global__ __launch_bounds__(NT, RS3_BLK) void k_resamp3(lqk_rs_plan pl, unsigned long long g0, unsigned long long K0,
                                                        int npfb, float del, const float2 *__restrict__ taps2,
                                                        const S *__restrict__ hist, const S *__restrict__ x,
@@ -399,16 +414,18 @@ __global__ __launch_bounds__(NT, RS3_BLK) void k_resamp3(lqk_rs_plan pl, unsigne
     constexpr int NSLOT = W3_CAP / 64;            // output slots per lane
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     const int RS = rs2_rs<RSC>(npfb);
+    constexpr int ROFF = PR ? 1 : 0;              // tap row p lives at table row p + ROFF
+    constexpr int NROW = L + 1 + 2 * ROFF;
     float2 *tpl = reinterpret_cast<float2 *>(smem);
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    unsigned char *wbase = smem + (size_t)2 * (L + 1) * RS * sizeof(float2) + (size_t)wave * WB;
+    unsigned char *wbase = smem + (size_t)2 * NROW * RS * sizeof(float2) + (size_t)wave * WB;
     S *cw = reinterpret_cast<S *>(wbase);
     uint2 *dsc = reinterpret_cast<uint2 *>(wbase + ((TS + 2) * (int)sizeof(S) + 15) / 16 * 16);   // dsc[W3_CAP]: sink
     const float fnpfb = (float)npfb;
-    for (int t = tid; t < (npfb + 1) * (L + 1); t += NT) {
-        const int b = t / (L + 1), p = t % (L + 1);
-        const float2 v = taps2[b * LP + p];
-        tpl[(2 * p + (b & 1)) * RS + (b >> 1)] = make_float2(v.x, v.y - v.x);
+    for (int t = tid; t < (npfb + 1) * NROW; t += NT) {
+        const int b = t / NROW, rr = t % NROW, p = rr - ROFF;
+        const float2 v = (p >= 0 && p <= L) ? taps2[b * LP + p] : make_float2(0.0f, 0.0f);
+        tpl[(2 * rr + (b & 1)) * RS + (b >> 1)] = make_float2(v.x, v.y - v.x);
     }
     __syncthreads();   // the only workgroup barrier
 
@@ -541,6 +558,43 @@ __global__ __launch_bounds__(NT, RS3_BLK) void k_resamp3(lqk_rs_plan pl, unsigne
         const int nr = __builtin_amdgcn_readlane(o, last);
         const unsigned ob = (unsigned)(Kb - K0);
         wave_fence();   // the output list is written
+        if constexpr (PR) {
+            // pairs q = lane + 64 k: outputs 2q, 2q + 1
+            constexpr int NPS = (W3_CAP / 2 + 63) / 64;
+#pragma unroll
+            for (int kq = 0; kq < NPS; kq++) {
+                const int q = lane + 64 * kq, oa = 2 * q;
+                S va{}, vb{};
+                if (oa < nr) {
+                    const uint2 da = lds_rd(&dsc[oa]), db = lds_rd(&dsc[oa + 1]);
+                    const bool hb = oa + 1 < nr;
+                    const int ia = (int)(da.y & 4095u), bA = (int)(da.y >> 12);
+                    const int dd = hb ? (((int)(db.y & 4095u) - ia) & 1) : 0;
+                    const int bB = hb ? (int)(db.y >> 12) : 0;
+                    const float muA = __uint_as_float(da.x), muB = hb ? __uint_as_float(db.x) : 0.0f;
+                    const S *wv = cw + ia + 1;
+                    const float2 *tA = tpl + (2 * ROFF + (bA & 1)) * RS + (bA >> 1);
+                    const float2 *tB = tpl + (2 * (ROFF - dd) + (bB & 1)) * RS + (bB >> 1);
+#pragma unroll
+                    for (int pp = 0; pp <= L + 1; pp++) {
+                        const S w = lds_rd(wv + pp);
+                        const float2 tb = lds_rd(tB + 2 * pp * RS);
+                        const float cb = fmaf(muB, tb.y, tb.x);
+                        // B's window is W[dd .. dd + L]: the sample outside it enters as 0
+                        const S wb = ((pp == 0 && dd == 1) || (pp == L + 1 && dd == 0)) ? S{} : w;
+                        if (pp <= L) {
+                            const float2 ta = lds_rd(tA + 2 * pp * RS);
+                            const float ca = fmaf(muA, ta.y, ta.x);
+                            va = rs_fma(ca, w, va);
+                        }
+                        vb = rs_fma(cb, wb, vb);
+                    }
+                }
+                const unsigned o2 = (ob + (unsigned)oa) * (unsigned)sizeof(S);
+                rs_store1(ry, oa < nr ? o2 : 0xFFFFFFF0u, va);
+                rs_store1(ry, oa + 1 < nr ? o2 + (unsigned)sizeof(S) : 0xFFFFFFF0u, vb);
+            }
+        } else {
         auto dot = [&](const S *wv, int bb, float mu) -> S {
             const float2 *tp = tpl + (bb & 1) * RS + (bb >> 1);
             S acc{};
@@ -563,6 +617,7 @@ __global__ __launch_bounds__(NT, RS3_BLK) void k_resamp3(lqk_rs_plan pl, unsigne
             }
             rs_store1(ry, oo < nr ? (ob + (unsigned)oo) * (unsigned)sizeof(S) : 0xFFFFFFF0u, v);
         }
+        }
     };
     for (long long tile = gw; tile < ntiles; tile += 2 * GW) {
         body(tile, pa);
@@ -578,7 +633,15 @@ void launch_rs(const lqk_rs_plan &pl, unsigned long long g0, unsigned long long 
 {
     constexpr int RSC = RS_RSC ? 33 : 0;       // constant stride for npfb <= 64
     const bool cst = RSC && npfb <= 2 * (RSC - 1);
-    const size_t lds3 = cst ? rs3_lds_bytes<L, S, RSC>(npfb) : rs3_lds_bytes<L, S, 0>(npfb);
+    // pairs of outputs per lane (constant-stride tables) when consecutive
+    // outputs are at most one input apart: tau moves by del per output and
+    // by -1 per input, and an input emits while tau < 1 - 1/npfb, so after
+    // an output at tau_k < 1 - 1/npfb the next input emits if
+    // tau_k + del - 1 < 1 - 1/npfb: del <= 1, with a margin for the float32
+    // rounding of tau_k + del
+    const bool pr = RS3_PAIR && cst && del <= 1.0f - 0x1p-22f;
+    const size_t lds3 = pr ? rs3_lds_bytes<L, S, RSC, true>(npfb)
+                      : cst ? rs3_lds_bytes<L, S, RSC>(npfb) : rs3_lds_bytes<L, S, 0>(npfb);
     if (taps2 != nullptr && lds3 <= 64 * 1024 && pl.P < (1ull << 31) && (pl.pre < (1ull << 62) || pl.end < (1ull << 62))) {
         // inputs per wave tile (a multiple of 4): its outputs, at most
         // (tin + 2) r + 2 (tau moves by 1/r per output and by -1 per input
@@ -591,12 +654,15 @@ void launch_rs(const lqk_rs_plan &pl, unsigned long long g0, unsigned long long 
             const long long wgs = (ntiles + 3) / 4;
             const int blk = lds3 <= 160 * 1024 / RS3_BLK ? RS3_BLK : (int)(160 * 1024 / lds3);
             const unsigned nb = (unsigned)(wgs < 256 * blk ? wgs : 256 * blk);   // persistent: blk per CU
-            if (cst)
-                hipLaunchKernelGGL((k_resamp3<L, S, RSC>), dim3(nb), dim3(NT), lds3, st, pl, g0, K0, npfb, del, taps2,
-                                   hist, x, n, y, (int)nout, tin);
+            if (pr)
+                hipLaunchKernelGGL((k_resamp3<L, S, RSC, true>), dim3(nb), dim3(NT), lds3, st, pl, g0, K0, npfb, del,
+                                   taps2, hist, x, n, y, (int)nout, tin);
+            else if (cst)
+                hipLaunchKernelGGL((k_resamp3<L, S, RSC, false>), dim3(nb), dim3(NT), lds3, st, pl, g0, K0, npfb, del,
+                                   taps2, hist, x, n, y, (int)nout, tin);
             else
-                hipLaunchKernelGGL((k_resamp3<L, S, 0>), dim3(nb), dim3(NT), lds3, st, pl, g0, K0, npfb, del, taps2,
-                                   hist, x, n, y, (int)nout, tin);
+                hipLaunchKernelGGL((k_resamp3<L, S, 0, false>), dim3(nb), dim3(NT), lds3, st, pl, g0, K0, npfb, del,
+                                   taps2, hist, x, n, y, (int)nout, tin);
             return;
         }
     }
