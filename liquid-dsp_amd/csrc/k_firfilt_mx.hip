@@ -102,8 +102,11 @@ constexpr int nal_kb() { return KB > 2 ? 3 : ((!CC && KB == 1 && FMX_A2L) ? 2 : 
 #ifndef FMX_NBUF_KB
 #define FMX_NBUF_KB 2   // the same for crcf with 65..256 taps (KB >= 2, two workgroups per CU)
 #endif
+#ifndef FMX_NBUF_CC
+#define FMX_NBUF_CC 2   // the same for cccf
+#endif
 template <bool CC, int KB>
-constexpr int nbuf_kb() { return CC ? 2 : (KB == 1 ? FMX_NBUF : FMX_NBUF_KB); }
+constexpr int nbuf_kb() { return CC ? FMX_NBUF_CC : (KB == 1 ? FMX_NBUF : FMX_NBUF_KB); }
 // elements between the eight shifted copies: at least NAL GL, and 16 mod 128
 // (32 B mod 256), so the 16 lanes of a ds_read_b128 pass -- eight copies at
 // two bases 16 B apart -- land on 16 distinct bank groups (a stride that is

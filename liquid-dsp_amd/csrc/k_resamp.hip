@@ -379,6 +379,9 @@ constexpr int W3_TIN = 64 * 4;   // inputs per wave tile (64 lanes x 4)
 #define RS3_CAP 320
 #endif
 constexpr int W3_CAP = RS3_CAP;  // output slots per wave tile
+#ifndef RS3_FIT
+#define RS3_FIT 15
+#endif
 #ifndef RS3_PAIR
 #define RS3_PAIR 0
 #endif
@@ -649,6 +652,25 @@ void launch_rs(const lqk_rs_plan &pl, unsigned long long g0, unsigned long long 
         const double r = 1.0 / (double)del;
         int tin = W3_TIN;
         while (tin > 4 && std::ceil((tin + 2) * r) + 2 > W3_CAP) tin -= 4;
+#if RS3_FIT
+        // then the tile size with the fewest evaluation passes (64 outputs
+        // each, a pass runs only where a lane has an output) per input,
+        // counting the tile's fixed cost (window store, replay) as RS3_FIT / 10
+        // passes: at r = 1.037 a 256-input tile's 265 outputs take five
+        // passes, the fifth for 9 lanes; 244 inputs (253 outputs) take four
+        if (std::ceil((tin + 2) * r) + 2 <= W3_CAP) {
+            double best = 1e300;
+            int bt = tin;
+            for (int t = tin; t >= 4 && t * 4 >= tin * 3; t -= 4) {
+                const double c = (std::ceil((std::ceil((t + 2) * r) + 2) / 64.0) + RS3_FIT / 10.0) / t;
+                if (c < best * (1.0 - 1e-9)) {
+                    best = c;
+                    bt = t;
+                }
+            }
+            tin = bt;
+        }
+#endif
         if (std::ceil((tin + 2) * r) + 2 <= W3_CAP) {   // else (r > ~52): the per-input kernel below
             const long long ntiles = (n + tin - 1) / tin;
             const long long wgs = (ntiles + 3) / 4;
