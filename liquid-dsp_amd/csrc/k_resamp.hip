@@ -382,6 +382,9 @@ constexpr int W3_CAP = RS3_CAP;  // output slots per wave tile
 #ifndef RS3_FIT
 #define RS3_FIT 15
 #endif
+#ifndef RS3_SU
+#define RS3_SU 1
+#endif
 #ifndef RS3_PAIR
 #define RS3_PAIR 0
 #endif
@@ -420,7 +423,10 @@ __global__ __launch_bounds__(NT, RS3_BLK) void k_resamp3(lqk_rs_plan pl, unsigne
     constexpr int ROFF = PR ? 1 : 0;              // tap row p lives at table row p + ROFF
     constexpr int NROW = L + 1 + 2 * ROFF;
     float2 *tpl = reinterpret_cast<float2 *>(smem);
-    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    // the wave index through readfirstlane: the compiler then knows every
+    // tile-level quantity (tile, i0, the plan position and its 64-bit period
+    // division) is wave-uniform and computes it on the scalar unit
+    const int tid = threadIdx.x, lane = tid & 63, wave = RS3_SU ? __builtin_amdgcn_readfirstlane(tid >> 6) : tid >> 6;
     unsigned char *wbase = smem + (size_t)2 * NROW * RS * sizeof(float2) + (size_t)wave * WB;
     S *cw = reinterpret_cast<S *>(wbase);
     uint2 *dsc = reinterpret_cast<uint2 *>(wbase + ((TS + 2) * (int)sizeof(S) + 15) / 16 * 16);   // dsc[W3_CAP]: sink
