@@ -374,6 +374,10 @@ __global__ __launch_bounds__(NT) void k_resamp_generic(lqk_rs_plan pl, unsigned 
 #ifndef RS3_BLK
 #define RS3_BLK 5
 #endif
+#ifndef RS3_NT
+#define RS3_NT 256
+#endif
+constexpr int NT3 = RS3_NT;       // threads per k_resamp3 workgroup (waves own their tiles)
 constexpr int W3_TIN = 64 * 4;   // inputs per wave tile (64 lanes x 4)
 #ifndef RS3_CAP
 #define RS3_CAP 320
@@ -385,6 +389,9 @@ constexpr int W3_CAP = RS3_CAP;  // output slots per wave tile
 #ifndef RS3_SU
 #define RS3_SU 1
 #endif
+#ifndef RS3_NPF
+#define RS3_NPF 2
+#endif
 #ifndef RS3_PAIR
 #define RS3_PAIR 0
 #endif
@@ -394,7 +401,7 @@ inline size_t rs3_lds_bytes(int npfb)
 {
     constexpr int TS = W3_TIN + L + 2;
     return (size_t)2 * (L + 1 + (PR ? 2 : 0)) * rs2_rs<RSC>(npfb) * sizeof(float2) +
-           (size_t)4 * (((TS + 2) * sizeof(S) + 15) / 16 * 16 + (W3_CAP + 2) * 8);
+           (size_t)(NT3 / 64) * (((TS + 2) * sizeof(S) + 15) / 16 * 16 + (W3_CAP + 2) * 8);
 }
 
 // PR (rates > 1: consecutive outputs at most one input apart, see
@@ -406,7 +413,7 @@ inline size_t rs3_lds_bytes(int npfb)
 // 2 x 30); the sample outside B's window enters as 0, so a non-finite input
 // there never reaches B
 template <int L, typename S, int RSC, bool PR>
-__global__ __launch_bounds__(NT, RS3_BLK) void k_resamp3(lqk_rs_plan pl, unsigned long long g0, unsigned long long K0,
+__global__ __launch_bounds__(NT3, RS3_BLK) void k_resamp3(lqk_rs_plan pl, unsigned long long g0, unsigned long long K0,
                                                        int npfb, float del, const float2 *__restrict__ taps2,
                                                        const S *__restrict__ hist, const S *__restrict__ x,
                                                        long long n, S *__restrict__ y, int nout, int tin)
@@ -431,7 +438,7 @@ __global__ __launch_bounds__(NT, RS3_BLK) void k_resamp3(lqk_rs_plan pl, unsigne
     S *cw = reinterpret_cast<S *>(wbase);
     uint2 *dsc = reinterpret_cast<uint2 *>(wbase + ((TS + 2) * (int)sizeof(S) + 15) / 16 * 16);   // dsc[W3_CAP]: sink
     const float fnpfb = (float)npfb;
-    for (int t = tid; t < (npfb + 1) * NROW; t += NT) {
+    for (int t = tid; t < (npfb + 1) * NROW; t += NT3) {
         const int b = t / NROW, rr = t % NROW, p = rr - ROFF;
         const float2 v = (p >= 0 && p <= L) ? taps2[b * LP + p] : make_float2(0.0f, 0.0f);
         tpl[(2 * rr + (b & 1)) * RS + (b >> 1)] = make_float2(v.x, v.y - v.x);
@@ -439,7 +446,7 @@ __global__ __launch_bounds__(NT, RS3_BLK) void k_resamp3(lqk_rs_plan pl, unsigne
     __syncthreads();   // the only workgroup barrier
 
     const long long ntiles = (n + tin - 1) / tin;
-    const long long GW = (long long)gridDim.x * (NT / 64), gw = (long long)blockIdx.x * (NT / 64) + wave;
+    const long long GW = (long long)gridDim.x * (NT3 / 64), gw = (long long)blockIdx.x * (NT3 / 64) + wave;
     if (gw >= ntiles) return;
     const __amdgpu_buffer_rsrc_t rx =
         __builtin_amdgcn_make_buffer_rsrc((void *)x, (short)0, (int)(n * (long long)sizeof(S)), 0x00020000);
@@ -487,9 +494,11 @@ __global__ __launch_bounds__(NT, RS3_BLK) void k_resamp3(lqk_rs_plan pl, unsigne
         __builtin_amdgcn_wave_barrier();
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
     };
+    // RS3_NPF tiles of loads in flight per wave (register sets pa [, pb])
+    constexpr int NPF = RS3_NPF;
     Pre pa, pb;
     fetch(gw, pa);
-    fetch(gw + GW, pb);
+    if constexpr (NPF > 1) fetch(gw + GW, pb);
     auto body = [&](long long tile, Pre &cur) {
         const long long i0 = tile * tin;
         const long long ie = (i0 + tin < n) ? i0 + tin : n;
@@ -502,7 +511,7 @@ __global__ __launch_bounds__(NT, RS3_BLK) void k_resamp3(lqk_rs_plan pl, unsigne
             const int t = lane + 64 * u;
             if (t < TS) cw[t] = u == 0 ? cur.xa[0] + cur.xh : cur.xa[u];
         }
-        fetch(tile + 2 * GW, cur);
+        fetch(tile + NPF * GW, cur);
         // replay: lane j, inputs ia .. ia + nin - 1
         const long long ia = i0 + (long long)lane * SPAN;
         const int nin = ia < ie ? (int)((ie - ia) < SPAN ? (ie - ia) : SPAN) : 0;
@@ -628,10 +637,12 @@ __global__ __launch_bounds__(NT, RS3_BLK) void k_resamp3(lqk_rs_plan pl, unsigne
         }
         }
     };
-    for (long long tile = gw; tile < ntiles; tile += 2 * GW) {
+    for (long long tile = gw; tile < ntiles; tile += NPF * GW) {
         body(tile, pa);
-        if (tile + GW >= ntiles) break;
-        body(tile + GW, pb);
+        if constexpr (NPF > 1) {
+            if (tile + GW >= ntiles) break;
+            body(tile + GW, pb);
+        }
     }
 }
 
@@ -651,7 +662,7 @@ void launch_rs(const lqk_rs_plan &pl, unsigned long long g0, unsigned long long 
     const bool pr = RS3_PAIR && cst && del <= 1.0f - 0x1p-22f;
     const size_t lds3 = pr ? rs3_lds_bytes<L, S, RSC, true>(npfb)
                       : cst ? rs3_lds_bytes<L, S, RSC>(npfb) : rs3_lds_bytes<L, S, 0>(npfb);
-    if (taps2 != nullptr && lds3 <= 64 * 1024 && pl.P < (1ull << 31) && (pl.pre < (1ull << 62) || pl.end < (1ull << 62))) {
+    if (taps2 != nullptr && lds3 <= 80 * 1024 && pl.P < (1ull << 31) && (pl.pre < (1ull << 62) || pl.end < (1ull << 62))) {
         // inputs per wave tile (a multiple of 4): its outputs, at most
         // (tin + 2) r + 2 (tau moves by 1/r per output and by -1 per input
         // within [-1/npfb, 1 + 1/r)), fit the W3_CAP output slots
@@ -679,17 +690,17 @@ void launch_rs(const lqk_rs_plan &pl, unsigned long long g0, unsigned long long 
 #endif
         if (std::ceil((tin + 2) * r) + 2 <= W3_CAP) {   // else (r > ~52): the per-input kernel below
             const long long ntiles = (n + tin - 1) / tin;
-            const long long wgs = (ntiles + 3) / 4;
+            const long long wgs = (ntiles + NT3 / 64 - 1) / (NT3 / 64);
             const int blk = lds3 <= 160 * 1024 / RS3_BLK ? RS3_BLK : (int)(160 * 1024 / lds3);
             const unsigned nb = (unsigned)(wgs < 256 * blk ? wgs : 256 * blk);   // persistent: blk per CU
             if (pr)
-                hipLaunchKernelGGL((k_resamp3<L, S, RSC, true>), dim3(nb), dim3(NT), lds3, st, pl, g0, K0, npfb, del,
+                hipLaunchKernelGGL((k_resamp3<L, S, RSC, true>), dim3(nb), dim3(NT3), lds3, st, pl, g0, K0, npfb, del,
                                    taps2, hist, x, n, y, (int)nout, tin);
             else if (cst)
-                hipLaunchKernelGGL((k_resamp3<L, S, RSC, false>), dim3(nb), dim3(NT), lds3, st, pl, g0, K0, npfb, del,
+                hipLaunchKernelGGL((k_resamp3<L, S, RSC, false>), dim3(nb), dim3(NT3), lds3, st, pl, g0, K0, npfb, del,
                                    taps2, hist, x, n, y, (int)nout, tin);
             else
-                hipLaunchKernelGGL((k_resamp3<L, S, 0, false>), dim3(nb), dim3(NT), lds3, st, pl, g0, K0, npfb, del,
+                hipLaunchKernelGGL((k_resamp3<L, S, 0, false>), dim3(nb), dim3(NT3), lds3, st, pl, g0, K0, npfb, del,
                                    taps2, hist, x, n, y, (int)nout, tin);
             return;
         }
