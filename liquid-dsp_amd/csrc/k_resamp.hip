@@ -390,7 +390,7 @@ constexpr int W3_CAP = RS3_CAP;  // output slots per wave tile
 #define RS3_SU 1
 #endif
 #ifndef RS3_NPF
-#define RS3_NPF 2
+#define RS3_NPF 1
 #endif
 #ifndef RS3_PAIR
 #define RS3_PAIR 0
