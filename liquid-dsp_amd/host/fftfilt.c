@@ -34,6 +34,7 @@ typedef struct {
     int cur;
     float sre, sim;     /* user scale s */
     lq_firfilt *direct; /* h_len - 1 > NFFT/2: direct convolution */
+    lq_mirror hm;       /* host copy of the history (small-call mode) */
     lq_ctx ctx;
     lq_devbuf xbuf, ybuf, cbuf;
 } lq_fftf;
@@ -58,6 +59,7 @@ static lq_fftf *lq_fftf_create(int kind, const float *h, unsigned int h_len, uns
     q->d_H = lqrt_malloc((size_t)lqk_fftfilt_nfft() * 8);
     q->d_hist[0] = lqrt_malloc((size_t)h_len * q->esz);
     q->d_hist[1] = lqrt_malloc((size_t)h_len * q->esz);
+    lq_mirror_init(&q->hm, h_len - 1, q->esz);
     lqrt_h2d(q->d_h, q->h, h_len * q->csz, q->ctx.stream);
     if (h_len - 1 > lqk_fftfilt_nfft() / 2) {
         static const char *who[] = {"fftfilt_rrrf", "fftfilt_crcf", "fftfilt_cccf"};
@@ -81,6 +83,7 @@ static void lq_fftf_destroy(lq_fftf *q)
     lqrt_free(q->d_H);
     lqrt_free(q->d_hist[0]);
     lqrt_free(q->d_hist[1]);
+    lq_mirror_free(&q->hm);
     lq_devbuf_free(&q->xbuf);
     lq_devbuf_free(&q->ybuf);
     lq_devbuf_free(&q->cbuf);
@@ -94,6 +97,7 @@ static void lq_fftf_reset(lq_fftf *q)
     lqrt_memset(q->d_hist[0], (size_t)q->h_len * q->esz, q->ctx.stream);
     lqrt_memset(q->d_hist[1], (size_t)q->h_len * q->esz, q->ctx.stream);
     lqrt_sync(q->ctx.stream);
+    lq_mirror_zero(&q->hm);
     if (q->direct) lq_firfilt_reset(q->direct);
 }
 
@@ -116,6 +120,8 @@ static void lq_fftf_block_dev(lq_fftf *q, const void *dx, unsigned long long n, 
         lq_firfilt_execute_block_dev(q->direct, dx, n, dy);
         return;
     }
+    lq_mirror_need_dev(&q->hm, q->d_hist[q->cur], q->ctx.stream);
+    q->hm.host_valid = 0;
     const void *x = dx;
     if (dx == dy) { /* kernel segments read overlapping halos */
         void *c = lq_devbuf_get(&q->cbuf, (size_t)n * q->esz);
@@ -132,9 +138,41 @@ static void lq_fftf_block_dev(lq_fftf *q, const void *dx, unsigned long long n, 
     }
 }
 
+/* small-call mode: one short call (n h_len <= LQ_FFTF_HOST_MACS) on the host
+ * as the direct convolution it equals, y[t] = s sum_k h[k] x[t - k] over the
+ * history and the call's samples (fftfilt.c:193-260 computes the same sum by
+ * a 2n-point overlap-add; the results agree to float32 rounding) */
+#define LQ_FFTF_HOST_MACS 65536u
+static void lq_fftf_exec_host(lq_fftf *q, const void *x, unsigned int n, void *y)
+{
+    const unsigned int hm1 = q->h_len - 1;
+    lq_mirror_need_host(&q->hm, q->d_hist[q->cur], q->ctx.stream);
+    lq_mirror_append(&q->hm, x, n);
+    const unsigned char *w = lq_mirror_ptr(&q->hm);
+    for (unsigned int t = 0; t < n; t++) {
+        float *yt = (float *)((unsigned char *)y + (size_t)t * q->esz);
+        lq_host_conv(q->kind, q->h, w, hm1 + t, q->h_len, yt);
+        if (q->kind == LQ_RRRF) {
+            yt[0] *= q->sre;
+        } else if (q->kind == LQ_CRCF) {   /* real scale per component */
+            yt[0] *= q->sre;
+            yt[1] *= q->sre;
+        } else {                           /* complex scale */
+            const float a = yt[0], b = yt[1];
+            yt[0] = a * q->sre - b * q->sim;
+            yt[1] = a * q->sim + b * q->sre;
+        }
+    }
+    lq_mirror_commit(&q->hm, n);
+}
+
 static void lq_fftf_block(lq_fftf *q, const void *x, unsigned long long n, void *y)
 {
     if (n == 0) return;
+    if (lq_small_host() && !q->direct && n * (unsigned long long)q->h_len <= LQ_FFTF_HOST_MACS) {
+        lq_fftf_exec_host(q, x, (unsigned int)n, y);
+        return;
+    }
     size_t bytes = (size_t)n * q->esz;
     const void *dx = lq_call_in(&q->ctx, &q->xbuf, x, bytes);
     void *dy = lq_devbuf_get(&q->ybuf, bytes);

@@ -3,7 +3,8 @@
  *
  * The per-call API (one sample, one dot product, one decimated output per
  * call: firfilt_*_push + _execute, dotprod_*_execute / _run, firdecim_*_execute,
- * firinterp_*_execute, resamp_*_execute) is what unchanged liquid-dsp programs
+ * firinterp_*_execute, resamp_*_execute, and fftfilt_*_execute on its short
+ * n-sample block, n h_len <= 65536) is what unchanged liquid-dsp programs
  * call in their inner loops.  On the GPU each such call is a launch plus two
  * PCIe crossings (~10 us); the reference does it in 20-60 ns.
  * With the small-call mode set to host -- environment LQ_SMALL_CALLS=host, or

@@ -202,3 +202,48 @@ def test_resamp_set_rate_reset_host():
     ya = np.concatenate([g.execute(v) for v in x[:2000]])
     yb = o.execute_block(x[:2000])
     assert len(ya) == len(yb) and G.nrm_err(ya, yb) < NRM
+
+
+def _nextpow2(v):
+    n = 0
+    while (1 << n) < v:
+        n += 1
+    return n
+
+
+@pytest.mark.parametrize("case", G.load("fftfilt"), ids=lambda c: c["name"])
+def test_fftfilt_golden_host(case):
+    # the golden vectors' short blocks run as host direct convolutions
+    h, x, y = G.arr(case["h"]), G.arr(case["x"]), G.arr(case["y"])
+    n = 1 << _nextpow2(len(h) - 1)
+    nb = -(-len(x) // n)
+    xp = np.zeros(nb * n, np.float32 if case["type"] == "rrrf" else np.complex64)
+    xp[: len(x)] = x
+    q = LQ.FftFilt(h, n, t=case["type"])
+    out = np.concatenate([q.execute(xp[b * n:(b + 1) * n]) for b in range(nb)])
+    assert np.max(np.abs(out[: len(y)] - y)) < case["tol"]
+
+
+@pytest.mark.parametrize("t", ["rrrf", "crcf", "cccf"])
+@pytest.mark.parametrize("hlen,n", [(1, 4), (23, 32), (65, 64), (512, 1024)])
+def test_fftfilt_mixed_vs_oracle(t, hlen, n):
+    # execute() calls of n samples (host while n h_len <= 65536, else GPU)
+    # interleaved with long execute_block calls (GPU) on one object
+    r = rng(hlen * 7 + n)
+    h = coefs(r, t, hlen)
+    nb = 60
+    x = samples(r, t, n * nb)
+    g, o = LQ.FftFilt(h, n, t=t), O.FftFilt(TYPES[t], h, n)
+    s = (1.5 - 0.25j) if t == "cccf" else 1.5
+    g.set_scale(s)
+    out = []
+    for a, b, per in [(0, 10, True), (10, 30, False), (30, 45, True), (45, 60, False)]:
+        if per:
+            out += [g.execute(x[i * n:(i + 1) * n]) for i in range(a, b)]
+        else:
+            out.append(g.execute_block(x[a * n:b * n]))
+    y = np.concatenate(out)
+    assert G.nrm_err(y, s * o.execute_stream(x)) < NRM
+    g.reset()
+    y2 = np.concatenate([g.execute(x[i * n:(i + 1) * n]) for i in range(4)])
+    assert G.nrm_err(y2, y[:4 * n]) < NRM
