@@ -38,57 +38,63 @@ void liquid_mi355x_set_small_calls(int host) { g_small = host ? 1 : 0; }
 int liquid_mi355x_get_small_calls(void) { return lq_small_host(); }
 
 /* y = sum_{i<n} h[i] x[i] (no conjugation; src/dotprod/src/dotprod.c:42-167
- * and the type-specific dotprod_crcf.c / dotprod_cccf.c); four partial sums
- * so the compiler can keep several multiply-adds in flight */
+ * and the type-specific dotprod_crcf.c / dotprod_cccf.c).  Four-float vectors
+ * (GCC vector extensions: SSE on x86-64 without intrinsics, the reference's
+ * dotprod_*.mmx.c do the same with SSE intrinsics) with two accumulators, so
+ * several multiply-adds are in flight: complex samples two per vector. */
+typedef float lq_v4 __attribute__((vector_size(16)));
+typedef int lq_v4i __attribute__((vector_size(16)));
+static inline lq_v4 lq_ld4(const float *p)
+{
+    lq_v4 v;
+    memcpy(&v, p, sizeof(v));
+    return v;
+}
 void lq_host_dot(int kind, const float *h, const void *xv, unsigned int n, void *y)
 {
+    const float *x = (const float *)xv;
+    lq_v4 a0 = {0, 0, 0, 0}, a1 = {0, 0, 0, 0};
+    unsigned int i = 0;
     if (kind == LQ_RRRF) {
-        const float *x = (const float *)xv;
-        float a0 = 0.f, a1 = 0.f, a2 = 0.f, a3 = 0.f;
-        unsigned int i = 0;
+        for (; i + 8 <= n; i += 8) {
+            a0 += lq_ld4(h + i) * lq_ld4(x + i);
+            a1 += lq_ld4(h + i + 4) * lq_ld4(x + i + 4);
+        }
+        a0 += a1;
+        float r = (a0[0] + a0[1]) + (a0[2] + a0[3]);
+        for (; i < n; i++) r += h[i] * x[i];
+        *(float *)y = r;
+    } else if (kind == LQ_CRCF) {   /* x: (re, im) pairs, real taps */
+        const lq_v4i dup01 = {0, 0, 1, 1}, dup23 = {2, 2, 3, 3};
         for (; i + 4 <= n; i += 4) {
-            a0 += h[i] * x[i];
-            a1 += h[i + 1] * x[i + 1];
-            a2 += h[i + 2] * x[i + 2];
-            a3 += h[i + 3] * x[i + 3];
+            const lq_v4 hv = lq_ld4(h + i);
+            a0 += __builtin_shuffle(hv, dup01) * lq_ld4(x + 2 * i);
+            a1 += __builtin_shuffle(hv, dup23) * lq_ld4(x + 2 * i + 4);
         }
-        for (; i < n; i++) a0 += h[i] * x[i];
-        *(float *)y = (a0 + a1) + (a2 + a3);
-    } else if (kind == LQ_CRCF) {
-        const float *x = (const float *)xv;   /* (re, im) pairs */
-        float r0 = 0.f, i0 = 0.f, r1 = 0.f, i1 = 0.f;
-        unsigned int i = 0;
-        for (; i + 2 <= n; i += 2) {
-            r0 += h[i] * x[2 * i];
-            i0 += h[i] * x[2 * i + 1];
-            r1 += h[i + 1] * x[2 * i + 2];
-            i1 += h[i + 1] * x[2 * i + 3];
-        }
+        a0 += a1;
+        float re = a0[0] + a0[2], im = a0[1] + a0[3];
         for (; i < n; i++) {
-            r0 += h[i] * x[2 * i];
-            i0 += h[i] * x[2 * i + 1];
+            re += h[i] * x[2 * i];
+            im += h[i] * x[2 * i + 1];
         }
-        ((float *)y)[0] = r0 + r1;
-        ((float *)y)[1] = i0 + i1;
-    } else {
-        const float *x = (const float *)xv;
-        float r0 = 0.f, i0 = 0.f, r1 = 0.f, i1 = 0.f;
-        unsigned int i = 0;
+        ((float *)y)[0] = re;
+        ((float *)y)[1] = im;
+    } else {   /* complex taps: a0 += hr x, a1 += hi swap(x) */
+        const lq_v4i re2 = {0, 0, 2, 2}, im2 = {1, 1, 3, 3}, sw = {1, 0, 3, 2};
         for (; i + 2 <= n; i += 2) {
-            const float hr = h[2 * i], hi = h[2 * i + 1], xr = x[2 * i], xi = x[2 * i + 1];
-            const float gr = h[2 * i + 2], gi = h[2 * i + 3], zr = x[2 * i + 2], zi = x[2 * i + 3];
-            r0 += hr * xr - hi * xi;
-            i0 += hr * xi + hi * xr;
-            r1 += gr * zr - gi * zi;
-            i1 += gr * zi + gi * zr;
+            const lq_v4 hv = lq_ld4(h + 2 * i), xv4 = lq_ld4(x + 2 * i);
+            a0 += __builtin_shuffle(hv, re2) * xv4;
+            a1 += __builtin_shuffle(hv, im2) * __builtin_shuffle(xv4, sw);
         }
+        /* a0 = (hr xr, hr xi, ..), a1 = (hi xi, hi xr, ..) */
+        float re = (a0[0] + a0[2]) - (a1[0] + a1[2]), im = (a0[1] + a0[3]) + (a1[1] + a1[3]);
         for (; i < n; i++) {
             const float hr = h[2 * i], hi = h[2 * i + 1], xr = x[2 * i], xi = x[2 * i + 1];
-            r0 += hr * xr - hi * xi;
-            i0 += hr * xi + hi * xr;
+            re += hr * xr - hi * xi;
+            im += hr * xi + hi * xr;
         }
-        ((float *)y)[0] = r0 + r1;
-        ((float *)y)[1] = i0 + i1;
+        ((float *)y)[0] = re;
+        ((float *)y)[1] = im;
     }
 }
 
@@ -98,42 +104,53 @@ void lq_host_dot(int kind, const float *h, const void *xv, unsigned int n, void 
  * oldest-first samples, the same terms) */
 void lq_host_conv(int kind, const float *h, const void *wv, unsigned int last, unsigned int n, void *y)
 {
+    lq_v4 a0 = {0, 0, 0, 0}, a1 = {0, 0, 0, 0};
+    unsigned int k = 0;
     if (kind == LQ_RRRF) {
-        const float *w = (const float *)wv + last;
-        float a0 = 0.f, a1 = 0.f;
-        unsigned int k = 0;
-        for (; k + 2 <= n; k += 2) {
-            a0 += h[k] * w[-(long)k];
-            a1 += h[k + 1] * w[-(long)k - 1];
+        const float *w = (const float *)wv + last;   /* w[-k]: sample last - k */
+        const lq_v4i rev = {3, 2, 1, 0};
+        for (; k + 8 <= n; k += 8) {
+            a0 += lq_ld4(h + k) * __builtin_shuffle(lq_ld4(w - (long)k - 3), rev);
+            a1 += lq_ld4(h + k + 4) * __builtin_shuffle(lq_ld4(w - (long)k - 7), rev);
         }
-        for (; k < n; k++) a0 += h[k] * w[-(long)k];
-        *(float *)y = a0 + a1;
+        a0 += a1;
+        float r = (a0[0] + a0[1]) + (a0[2] + a0[3]);
+        for (; k < n; k++) r += h[k] * w[-(long)k];
+        *(float *)y = r;
     } else if (kind == LQ_CRCF) {
         const float *w = (const float *)wv + 2 * (size_t)last;
-        float r0 = 0.f, i0 = 0.f, r1 = 0.f, i1 = 0.f;
-        unsigned int k = 0;
-        for (; k + 2 <= n; k += 2) {
-            r0 += h[k] * w[-2 * (long)k];
-            i0 += h[k] * w[-2 * (long)k + 1];
-            r1 += h[k + 1] * w[-2 * (long)k - 2];
-            i1 += h[k + 1] * w[-2 * (long)k - 1];
+        /* the pair (sample last-k-1, sample last-k) loaded as one vector,
+         * swapped to (last-k, last-k-1) against taps (h_k, h_k, h_k+1, h_k+1) */
+        const lq_v4i swp = {2, 3, 0, 1}, dup01 = {0, 0, 1, 1}, dup23 = {2, 2, 3, 3};
+        for (; k + 4 <= n; k += 4) {
+            const lq_v4 hv = lq_ld4(h + k);
+            a0 += __builtin_shuffle(hv, dup01) * __builtin_shuffle(lq_ld4(w - 2 * (long)k - 2), swp);
+            a1 += __builtin_shuffle(hv, dup23) * __builtin_shuffle(lq_ld4(w - 2 * (long)k - 6), swp);
         }
+        a0 += a1;
+        float re = a0[0] + a0[2], im = a0[1] + a0[3];
         for (; k < n; k++) {
-            r0 += h[k] * w[-2 * (long)k];
-            i0 += h[k] * w[-2 * (long)k + 1];
+            re += h[k] * w[-2 * (long)k];
+            im += h[k] * w[-2 * (long)k + 1];
         }
-        ((float *)y)[0] = r0 + r1;
-        ((float *)y)[1] = i0 + i1;
+        ((float *)y)[0] = re;
+        ((float *)y)[1] = im;
     } else {
         const float *w = (const float *)wv + 2 * (size_t)last;
-        float r0 = 0.f, i0 = 0.f;
-        for (unsigned int k = 0; k < n; k++) {
-            const float hr = h[2 * k], hi = h[2 * k + 1], xr = w[-2 * (long)k], xi = w[-2 * (long)k + 1];
-            r0 += hr * xr - hi * xi;
-            i0 += hr * xi + hi * xr;
+        const lq_v4i swp = {2, 3, 0, 1}, re2 = {0, 0, 2, 2}, im2 = {1, 1, 3, 3}, sw = {1, 0, 3, 2};
+        for (; k + 2 <= n; k += 2) {
+            const lq_v4 hv = lq_ld4(h + 2 * k), xv4 = __builtin_shuffle(lq_ld4(w - 2 * (long)k - 2), swp);
+            a0 += __builtin_shuffle(hv, re2) * xv4;
+            a1 += __builtin_shuffle(hv, im2) * __builtin_shuffle(xv4, sw);
         }
-        ((float *)y)[0] = r0;
-        ((float *)y)[1] = i0;
+        float re = (a0[0] + a0[2]) - (a1[0] + a1[2]), im = (a0[1] + a0[3]) + (a1[1] + a1[3]);
+        for (; k < n; k++) {
+            const float hr = h[2 * k], hi = h[2 * k + 1], xr = w[-2 * (long)k], xi = w[-2 * (long)k + 1];
+            re += hr * xr - hi * xi;
+            im += hr * xi + hi * xr;
+        }
+        ((float *)y)[0] = re;
+        ((float *)y)[1] = im;
     }
 }
 
