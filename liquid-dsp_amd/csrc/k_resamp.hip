@@ -395,12 +395,23 @@ constexpr int W3_CAP = RS3_CAP;  // output slots per wave tile
 #ifndef RS3_PAIR
 #define RS3_PAIR 0
 #endif
+#ifndef RS3_PK
+#define RS3_PK 0
+#endif
+#ifndef RS3_SLU
+#define RS3_SLU 1   // the evaluation's slot loop unrolled
+#endif
+// table rows (float2 units) of k_resamp3: PR pads a zero row on either side;
+// PK packs taps 2q, 2q + 1 of a bank as one 16-byte entry (h, h', dh, dh'),
+// ceil((L + 1) / 2) entries per bank
+template <int L, bool PR>
+constexpr int rs3_rows() { return PR ? L + 3 : (RS3_PK ? (L + 2) / 2 * 2 : L + 1); }
 // PR: the pair-table rows padded with a zero row on either side (pair mode)
 template <int L, typename S, int RSC, bool PR = false>
 inline size_t rs3_lds_bytes(int npfb)
 {
     constexpr int TS = W3_TIN + L + 2;
-    return (size_t)2 * (L + 1 + (PR ? 2 : 0)) * rs2_rs<RSC>(npfb) * sizeof(float2) +
+    return (size_t)2 * rs3_rows<L, PR>() * rs2_rs<RSC>(npfb) * sizeof(float2) +
            (size_t)(NT3 / 64) * (((TS + 2) * sizeof(S) + 15) / 16 * 16 + (W3_CAP + 2) * 8);
 }
 
@@ -428,8 +439,11 @@ __global__ __launch_bounds__(NT3, RS3_BLK) void k_resamp3(lqk_rs_plan pl, unsign
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     const int RS = rs2_rs<RSC>(npfb);
     constexpr int ROFF = PR ? 1 : 0;              // tap row p lives at table row p + ROFF
-    constexpr int NROW = L + 1 + 2 * ROFF;
+    constexpr int NROW = rs3_rows<L, PR>();
+    constexpr bool PK = RS3_PK && !PR;
+    constexpr int NQ = (L + 2) / 2;               // PK: tap pairs per bank
     float2 *tpl = reinterpret_cast<float2 *>(smem);
+    float4 *tq = reinterpret_cast<float4 *>(smem);
     // the wave index through readfirstlane: the compiler then knows every
     // tile-level quantity (tile, i0, the plan position and its 64-bit period
     // division) is wave-uniform and computes it on the scalar unit
@@ -438,10 +452,19 @@ __global__ __launch_bounds__(NT3, RS3_BLK) void k_resamp3(lqk_rs_plan pl, unsign
     S *cw = reinterpret_cast<S *>(wbase);
     uint2 *dsc = reinterpret_cast<uint2 *>(wbase + ((TS + 2) * (int)sizeof(S) + 15) / 16 * 16);   // dsc[W3_CAP]: sink
     const float fnpfb = (float)npfb;
-    for (int t = tid; t < (npfb + 1) * NROW; t += NT3) {
-        const int b = t / NROW, rr = t % NROW, p = rr - ROFF;
-        const float2 v = (p >= 0 && p <= L) ? taps2[b * LP + p] : make_float2(0.0f, 0.0f);
-        tpl[(2 * rr + (b & 1)) * RS + (b >> 1)] = make_float2(v.x, v.y - v.x);
+    if constexpr (PK) {
+        for (int t = tid; t < (npfb + 1) * NQ; t += NT3) {
+            const int b = t / NQ, q = t % NQ;
+            const float2 v0 = taps2[b * LP + 2 * q];
+            const float2 v1 = 2 * q + 1 <= L ? taps2[b * LP + 2 * q + 1] : make_float2(0.0f, 0.0f);
+            tq[(2 * q + (b & 1)) * RS + (b >> 1)] = make_float4(v0.x, v1.x, v0.y - v0.x, v1.y - v1.x);
+        }
+    } else {
+        for (int t = tid; t < (npfb + 1) * NROW; t += NT3) {
+            const int b = t / NROW, rr = t % NROW, p = rr - ROFF;
+            const float2 v = (p >= 0 && p <= L) ? taps2[b * LP + p] : make_float2(0.0f, 0.0f);
+            tpl[(2 * rr + (b & 1)) * RS + (b >> 1)] = make_float2(v.x, v.y - v.x);
+        }
     }
     __syncthreads();   // the only workgroup barrier
 
@@ -614,18 +637,35 @@ __global__ __launch_bounds__(NT3, RS3_BLK) void k_resamp3(lqk_rs_plan pl, unsign
             }
         } else {
         auto dot = [&](const S *wv, int bb, float mu) -> S {
-            const float2 *tp = tpl + (bb & 1) * RS + (bb >> 1);
             S acc{};
+            if constexpr (PK) {
+                // one 16-byte read and one packed FMA (c, c') = (h, h') + mu (dh, dh')
+                // per two taps; the terms in the same order as below
+                const float4 *tp = tq + (bb & 1) * RS + (bb >> 1);
 #pragma unroll
-            for (int p = 0; p <= L; p++) {
-                const float2 t = lds_rd(tp + 2 * p * RS);
-                const float c = fmaf(mu, t.y, t.x);
-                const S w = lds_rd(wv + p);
-                acc = rs_fma(c, w, acc);
+                for (int q = 0; q < NQ; q++) {
+                    const float4 t = tp[2 * q * RS];
+                    const v2f cc = __builtin_elementwise_fma(v2f{mu, mu}, v2f{t.z, t.w}, v2f{t.x, t.y});
+                    acc = rs_fma(cc.x, lds_rd(wv + 2 * q), acc);
+                    if (2 * q + 1 <= L) acc = rs_fma(cc.y, lds_rd(wv + 2 * q + 1), acc);
+                }
+            } else {
+                const float2 *tp = tpl + (bb & 1) * RS + (bb >> 1);
+#pragma unroll
+                for (int p = 0; p <= L; p++) {
+                    const float2 t = lds_rd(tp + 2 * p * RS);
+                    const float c = fmaf(mu, t.y, t.x);
+                    const S w = lds_rd(wv + p);
+                    acc = rs_fma(c, w, acc);
+                }
             }
             return acc;
         };
+#if RS3_SLU
 #pragma unroll
+#else
+#pragma unroll 1
+#endif
         for (int q = 0; q < NSLOT; q++) {
             const int oo = lane + 64 * q;
             S v{};
