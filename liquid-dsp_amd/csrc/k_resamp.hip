@@ -398,6 +398,12 @@ constexpr int W3_CAP = RS3_CAP;  // output slots per wave tile
 #ifndef RS3_PK
 #define RS3_PK 0
 #endif
+#ifndef RS3_SWZ
+#define RS3_SWZ 0   // output-list slot o stored at o + o / 16 (spreads the replay's strided writes over the banks)
+#endif
+// output-list slots per wave (RS3_SWZ: one pad slot per 16)
+constexpr int rs3_slots() { return RS3_SWZ ? (W3_CAP + 2) + (W3_CAP + 2) / 16 + 1 : W3_CAP + 2; }
+__device__ __forceinline__ int rs3_slot(int o) { return RS3_SWZ ? o + (o >> 4) : o; }
 #ifndef RS3_SLU
 #define RS3_SLU 1   // the evaluation's slot loop unrolled
 #endif
@@ -412,7 +418,7 @@ inline size_t rs3_lds_bytes(int npfb)
 {
     constexpr int TS = W3_TIN + L + 2;
     return (size_t)2 * rs3_rows<L, PR>() * rs2_rs<RSC>(npfb) * sizeof(float2) +
-           (size_t)(NT3 / 64) * (((TS + 2) * sizeof(S) + 15) / 16 * 16 + (W3_CAP + 2) * 8);
+           (size_t)(NT3 / 64) * (((TS + 2) * sizeof(S) + 15) / 16 * 16 + rs3_slots() * 8);
 }
 
 // PR (rates > 1: consecutive outputs at most one input apart, see
@@ -433,7 +439,7 @@ __global__ __launch_bounds__(NT3, RS3_BLK) void k_resamp3(lqk_rs_plan pl, unsign
     constexpr int SPAN = 4;
     constexpr int LP = (L + 2 + 1) & ~1;          // pair stride of taps2 (host layout)
     constexpr int TS = W3_TIN + L + 2;            // window samples of a tile
-    constexpr int WB = ((TS + 2) * (int)sizeof(S) + 15) / 16 * 16 + (W3_CAP + 2) * 8;   // bytes per wave
+    constexpr int WB = ((TS + 2) * (int)sizeof(S) + 15) / 16 * 16 + rs3_slots() * 8;   // bytes per wave
     constexpr int NXV = (TS + 63) / 64;           // window samples per lane
     constexpr int NSLOT = W3_CAP / 64;            // output slots per lane
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
@@ -561,7 +567,7 @@ __global__ __launch_bounds__(NT3, RS3_BLK) void k_resamp3(lqk_rs_plan pl, unsign
         const int o0 = o64 < (1ull << 30) ? (int)o64 : (1 << 30);
         int o = o0;
         auto put = [&](int iloc, int bank, float mu) {
-            dsc[(unsigned)o < (unsigned)W3_CAP ? o : W3_CAP] =
+            dsc[rs3_slot((unsigned)o < (unsigned)W3_CAP ? o : W3_CAP)] =
                 make_uint2(__float_as_uint(mu), (unsigned)iloc | ((unsigned)bank << 12));
             o++;
         };
@@ -607,7 +613,7 @@ __global__ __launch_bounds__(NT3, RS3_BLK) void k_resamp3(lqk_rs_plan pl, unsign
                 const int q = lane + 64 * kq, oa = 2 * q;
                 S va{}, vb{};
                 if (oa < nr) {
-                    const uint2 da = lds_rd(&dsc[oa]), db = lds_rd(&dsc[oa + 1]);
+                    const uint2 da = lds_rd(&dsc[rs3_slot(oa)]), db = lds_rd(&dsc[rs3_slot(oa + 1)]);
                     const bool hb = oa + 1 < nr;
                     const int ia = (int)(da.y & 4095u), bA = (int)(da.y >> 12);
                     const int dd = hb ? (((int)(db.y & 4095u) - ia) & 1) : 0;
@@ -670,7 +676,7 @@ __global__ __launch_bounds__(NT3, RS3_BLK) void k_resamp3(lqk_rs_plan pl, unsign
             const int oo = lane + 64 * q;
             S v{};
             if (oo < nr) {
-                const uint2 dd = dsc[oo];
+                const uint2 dd = dsc[rs3_slot(oo)];
                 v = dot(cw + (int)(dd.y & 4095u) + 1, (int)(dd.y >> 12), __uint_as_float(dd.x));
             }
             rs_store1(ry, oo < nr ? (ob + (unsigned)oo) * (unsigned)sizeof(S) : 0xFFFFFFF0u, v);
