@@ -41,8 +41,10 @@ their own one-core oracle rates (firfilt, resamp, fftfilt, dotprod n=64).
 per_call: the reference's own per-call benchmark bodies
 (src/*/bench/*_benchmark.c: push/execute one sample, one firpfbch2 block,
 one dot product per call) compiled unchanged against this library by
-tools/build_ref_benches.sh and timed in wall clock -- the latency of the
-unbatched liquid.h API, one GPU round trip per call.
+tools/build_ref_benches.sh and timed in wall clock -- the unbatched liquid.h
+API in the library's default mode (single-sample calls on the host, block
+calls on the GPU); per_call_gpu: the same loops with every call forced onto
+the GPU (one round trip per call).
 """
 import argparse
 import json
@@ -66,6 +68,8 @@ def parse():
     p.add_argument("--gpus", type=int, default=1)
     p.add_argument("--steps", type=int, default=50)
     p.add_argument("--warmup", type=int, default=20)
+    p.add_argument("--warmup-ms", type=float, default=150.0,
+                   help="per-leg warm-up floor: untimed launches continue until this much wall time has passed")
     p.add_argument("--samples", type=int, default=1 << 27, help="firpfbch2 input samples per GPU")
     p.add_argument("--fir-samples", type=int, default=1 << 28, help="firfilt samples per GPU")
     p.add_argument("--cpu-seconds", type=float, default=10.0, help="CPU baseline budget (rank 0, N=1)")
@@ -185,9 +189,28 @@ def synth_indexed(a, b, chunk=1 << 24):
     return out
 
 
-def time_steps(run_step, steps, warmup, world, stream):
+WARMUP_FLOOR_MS = 150.0   # per leg: keep launching until clocks have ramped (set by --warmup-ms)
+
+
+def time_steps(run_step, steps, warmup, world, stream, info=None):
+    """W untimed warm-up steps, then further untimed steps until the leg has
+    run for at least WARMUP_FLOOR_MS of wall time (the first launches after
+    idle run 5-10 % slower while clocks ramp; the driver's --warmup 5 alone
+    does not cover that), then exactly `steps` timed steps between a barrier
+    + synchronize on both sides.  `info` (a dict) receives the warm-up count
+    and duration."""
+    t_w = time.perf_counter()
+    nw = 0
     for _ in range(warmup):
         run_step()
+        nw += 1
+    stream.synchronize()
+    while (time.perf_counter() - t_w) * 1e3 < WARMUP_FLOOR_MS:
+        for _ in range(4):
+            run_step()
+            nw += 1
+        stream.synchronize()
+    warm_ms = (time.perf_counter() - t_w) * 1e3
     barrier(world)
     ev0 = torch.cuda.Event(enable_timing=True)
     ev1 = torch.cuda.Event(enable_timing=True)
@@ -199,6 +222,9 @@ def time_steps(run_step, steps, warmup, world, stream):
     barrier(world)
     wall = time.perf_counter() - t0
     gpu_ms = ev0.elapsed_time(ev1)
+    if info is not None:
+        info["warmup_launches"] = nw
+        info["warmup_ms"] = warm_ms
     return wall, gpu_ms
 
 
@@ -214,8 +240,9 @@ def bench_firpfbch2(args, world, rank, stream):
     def step():
         q.execute_block_dev(x.data_ptr(), nblocks, y.data_ptr())
 
-    wall, gpu_ms = time_steps(step, args.steps, args.warmup, world, stream)
-    res = {"n": n, "nblocks": nblocks, "wall": wall, "gpu_ms": gpu_ms}
+    wi = {}
+    wall, gpu_ms = time_steps(step, args.steps, args.warmup, world, stream, wi)
+    res = {"n": n, "nblocks": nblocks, "wall": wall, "gpu_ms": gpu_ms, "warm": wi}
     q.destroy()
     del x, y
     torch.cuda.empty_cache()
@@ -244,14 +271,15 @@ def bench_firpfbch2_sharded(args, world, rank, stream):
         if nb:
             q.execute_block_dev(x.data_ptr(), nb, y.data_ptr())
 
-    wall, gpu_ms = time_steps(step, args.steps, args.warmup, world, stream)
+    wi = {}
+    wall, gpu_ms = time_steps(step, args.steps, args.warmup, world, stream, wi)
     q.reset()                      # checksum pass from the stream's initial state
     step()
     stream.synchronize()
     own = y[2 * sh.warm * M:2 * nb * M]
     csum = int(own.view(torch.int32).sum(dtype=torch.int64).item()) if sh.count else 0
     res = {"wall": wall, "gpu_ms": gpu_ms, "owned": sh.count * (M // 2), "halo_blocks": sh.warm,
-           "total": nb_total * (M // 2), "checksum": csum}
+           "total": nb_total * (M // 2), "checksum": csum, "warm": wi}
     q.destroy()
     del x, y, own
     torch.cuda.empty_cache()
@@ -271,8 +299,9 @@ def bench_firfilt(args, world, rank, stream):
     def step():
         q.execute_block_dev(x.data_ptr(), n, y.data_ptr())
 
-    wall, gpu_ms = time_steps(step, args.steps, args.warmup, world, stream)
-    res = {"n": n, "wall": wall, "gpu_ms": gpu_ms}
+    wi = {}
+    wall, gpu_ms = time_steps(step, args.steps, args.warmup, world, stream, wi)
+    res = {"n": n, "wall": wall, "gpu_ms": gpu_ms, "warm": wi}
     q.destroy()
     del x, y
     torch.cuda.empty_cache()
@@ -299,8 +328,9 @@ def bench_dotprod(args, world, rank, stream):
         def step():
             q.execute_batch_dev(X.data_ptr(), nv, Y.data_ptr())
 
-        wall, gpu_ms = time_steps(step, args.steps, args.warmup, world, stream)
-        out[key] = {"wall": wall, "gpu_ms": gpu_ms, "n": n, "nvec": nv}
+        wi = {}
+        wall, gpu_ms = time_steps(step, args.steps, args.warmup, world, stream, wi)
+        out[key] = {"wall": wall, "gpu_ms": gpu_ms, "n": n, "nvec": nv, "warm": wi}
         q.destroy()
         del X, Y
         torch.cuda.empty_cache()
@@ -321,11 +351,12 @@ def bench_fftfilt(args, world, rank, stream):
     def step():
         q.execute_block_dev(x.data_ptr(), n, y.data_ptr())
 
-    wall, gpu_ms = time_steps(step, args.steps, args.warmup, world, stream)
+    wi = {}
+    wall, gpu_ms = time_steps(step, args.steps, args.warmup, world, stream, wi)
     q.destroy()
     del x, y
     torch.cuda.empty_cache()
-    return {"n": n, "wall": wall, "gpu_ms": gpu_ms}
+    return {"n": n, "wall": wall, "gpu_ms": gpu_ms, "warm": wi}
 
 
 def bench_resamp(args, world, rank, stream):
@@ -355,9 +386,10 @@ def bench_resamp(args, world, rank, stream):
     first_ms = (time.perf_counter() - t0) * 1e3
     q.reset()                # the periodic plan from the initial state is kept
     nys.clear()
-    wall, gpu_ms = time_steps(step, args.steps, args.warmup, world, stream)
-    nout = sum(nys[args.warmup:])
-    res = {"n": n, "wall": wall, "gpu_ms": gpu_ms, "nout": nout, "first_ms": first_ms}
+    wi = {}
+    wall, gpu_ms = time_steps(step, args.steps, args.warmup, world, stream, wi)
+    nout = sum(nys[-args.steps:])
+    res = {"n": n, "wall": wall, "gpu_ms": gpu_ms, "nout": nout, "first_ms": first_ms, "warm": wi}
     q.destroy()
     del x, y
     torch.cuda.empty_cache()
@@ -463,12 +495,12 @@ def cpu_baseline(seconds, procs):
                                              "source": "BASELINE.md section 2"}}
 
 
-def percall_baseline(host_small_calls=False):
+def percall_baseline(force_gpu=False):
     """The reference's own per-call benchmark bodies linked against this
     library (tools/build_ref_benches.sh -> build/ref_bench/percall), wall
-    clock; None when the harness was not built.  host_small_calls: run them
-    with LQ_SMALL_CALLS=host (the opt-in host path for single-sample calls,
-    host/lq_small.c); otherwise every call runs on the GPU (the default)."""
+    clock; None when the harness was not built.  Default mode: the library's
+    default (single-sample calls on the host, host/lq_small.c; block calls on
+    the GPU).  force_gpu: LQ_SMALL_CALLS=gpu, every call a GPU round trip."""
     import subprocess
     exe = os.path.join(ROOT, "build", "ref_bench", "percall")
     if not os.path.exists(exe):
@@ -479,8 +511,8 @@ def percall_baseline(host_small_calls=False):
     try:
         env = dict(os.environ)
         env.pop("LQ_SMALL_CALLS", None)
-        if host_small_calls:
-            env["LQ_SMALL_CALLS"] = "host"
+        if force_gpu:
+            env["LQ_SMALL_CALLS"] = "gpu"
         out = subprocess.run([exe, "--runtime", "0.25"] + names, capture_output=True, text=True, timeout=240,
                              env=env)
     except subprocess.TimeoutExpired:
@@ -551,7 +583,9 @@ def cpu_baselines_secondary(seconds):
 
 
 def main():
+    global WARMUP_FLOOR_MS
     args = parse()
+    WARMUP_FLOOR_MS = args.warmup_ms
     if "WORLD_SIZE" not in os.environ and args.gpus > 1:
         sys.exit(launch_ranks(args.gpus))
     world, rank, local = setup_dist()
@@ -595,10 +629,10 @@ def main():
         ff_t = (allreduce_max(ff["wall"], world), allreduce_max(ff["gpu_ms"], world))
 
     copy_gbps = copy_bandwidth() if rank == 0 else None
-    percall = percall_host = None
+    percall = percall_gpu = None
     if rank == 0 and world == 1 and not args.no_percall:
         percall = percall_baseline()
-        percall_host = percall_baseline(host_small_calls=True)
+        percall_gpu = percall_baseline(force_gpu=True)
     cpu = cpu2 = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         cpu = cpu_baseline(args.cpu_seconds, args.cpu_procs or cpu_share())
@@ -645,6 +679,10 @@ def main():
                          "frac": achieved / HBM_PEAK_GBPS, "traffic": traffic, "traffic_source": tsrc,
                          "bytes_per_unit": "24 B/input sample (8 read + 16 write)",
                          "launch_ms": launch_ms, "measured_copy_GBps": copy_gbps},
+            "warmup_floor": {"floor_ms": WARMUP_FLOOR_MS, "launches": pfb["warm"]["warmup_launches"],
+                             "ms": pfb["warm"]["warmup_ms"],
+                             "what": "untimed launches before the timed steps of every leg: --warmup W, then "
+                                     "more until floor_ms of wall time has passed (clock ramp)"},
             "cpu_baseline": cpu,
         }
         if shd is not None:
@@ -655,6 +693,7 @@ def main():
                 "plan": "liquid-dsp_amd/lqshard.py firpfbch2_plan: even-block shard starts, %d-block warm-up "
                         "halo recomputed per shard, no data-path collective" % shd["halo_blocks"],
                 "ms_per_step": t_shd / args.steps * 1e3, "launch_ms": g_shd / args.steps,
+                "warmup_launches": shd["warm"]["warmup_launches"],
                 "owned_samples": int(owned_shd),
                 "output_checksum": csum_shd,
                 "checksum_def": "sum of the int32 bit patterns of every owned output (fresh object, one pass); "
@@ -668,6 +707,8 @@ def main():
                                                     "unit": "GB/s", "frac": fach / HBM_PEAK_GBPS,
                                                     "traffic": fir_traffic, "traffic_source": tsrc,
                                                     "bytes_per_unit": "16 B/sample", "launch_ms": fl_ms},
+                                       "warmup_launches": fir["warm"]["warmup_launches"],
+                                       "warmup_ms": fir["warm"]["warmup_ms"],
                                        "arith": ("f32-accurate: taps and samples split into three bf16 terms, "
                                                  "six exact products accumulated in f32 on "
                                                  "v_mfma_f32_32x32x16_bf16 (k_firfilt_mx); "
@@ -688,7 +729,9 @@ def main():
                                                      "unit": "GB/s", "frac": rach / HBM_PEAK_GBPS,
                                                      "traffic": rs_traffic, "traffic_source": tsrc,
                                                      "bytes_per_unit": "8 B/input + 8 B/output",
-                                                     "launch_ms": rl_ms}}
+                                                     "launch_ms": rl_ms},
+                                        "warmup_launches": rs["warm"]["warmup_launches"],
+                                        "warmup_ms": rs["warm"]["warmup_ms"]}
         if dp is not None:
             legs = {}
             for key, (tw, tg) in dp_t.items():
@@ -697,7 +740,8 @@ def main():
                 legs["n%s" % key] = {"value": world * nv * args.steps / tw / 1e6, "unit": "M dot products/s",
                                      "vectors": nv, "working_set_MB": (8.0 * n + 8.0) * nv / 1e6,
                                      "launch_ms": ms, "achieved_GBps": (8.0 * n + 8.0) * nv / (ms * 1e-3) / 1e9,
-                                     "frac": (8.0 * n + 8.0) * nv / (ms * 1e-3) / 1e9 / HBM_PEAK_GBPS}
+                                     "frac": (8.0 * n + 8.0) * nv / (ms * 1e-3) / 1e9 / HBM_PEAK_GBPS,
+                                     "warmup_launches": dp["runs"][key]["warm"]["warmup_launches"]}
             out["dotprod_cccf"] = {"workload": "dotprod_cccf batched, %d vectors/GPU (BASELINE configs[1])"
                                    % dp["nvec"], "bytes_per_unit": "8n+8 B/vector", "legs": legs}
             ms = ff_t[1] / args.steps
@@ -712,16 +756,19 @@ def main():
                                                      "peak": HBM_PEAK_GBPS, "unit": "GB/s",
                                                      "frac": 16.0 * ff["n"] / (ms * 1e-3) / 1e9 / HBM_PEAK_GBPS,
                                                      "traffic": ff_traffic, "traffic_source": tsrc, "bytes_per_unit": "16 B/sample",
-                                                     "launch_ms": ms}}
+                                                     "launch_ms": ms},
+                                        "warmup_launches": ff["warm"]["warmup_launches"],
+                                        "warmup_ms": ff["warm"]["warmup_ms"]}
         if percall is not None:
             out["per_call"] = {"what": "the reference's per-call benchmark loops (src/*/bench/*_benchmark.c) "
-                                       "linked against this library; wall clock; one GPU round trip per call",
+                                       "linked against this library, default mode: single-sample calls on the "
+                                       "host (host/lq_small.c), block calls (firpfbch/firpfbch2 blocks) on the "
+                                       "GPU; wall clock",
                                "runs": percall}
-        if percall_host is not None:
-            out["per_call_host_small_calls"] = {
-                "what": "the same loops with LQ_SMALL_CALLS=host: the opt-in host path for single-sample "
-                        "calls (host/lq_small.c); block calls stay on the GPU; not the default",
-                "runs": percall_host}
+        if percall_gpu is not None:
+            out["per_call_gpu"] = {
+                "what": "the same loops with LQ_SMALL_CALLS=gpu: every call one GPU round trip",
+                "runs": percall_gpu}
         if cpu2:
             for leg, c in cpu2.items():
                 key = "dotprod_cccf" if leg == "dotprod_cccf_n64" else leg

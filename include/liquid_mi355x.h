@@ -534,13 +534,13 @@ void liquid_mi355x_memcpy_d2h(void *_dst, const void *_src, unsigned long long _
 void liquid_mi355x_device_synchronize(void);
 /* build identification (gfx target the kernels were compiled for) */
 const char *liquid_mi355x_build_target(void);
-/* Small-call mode (no reference counterpart).  0 (default): every call runs
- * on the GPU.  1: the single-sample / single-vector calls -- firfilt_*_execute
- * after push, dotprod_*_execute / _run / _run4, firdecim_*_execute,
- * firinterp_*_execute, resamp_*_execute, and fftfilt_*_execute on blocks with
- * n * h_len <= 65536 -- compute on the host (host/lq_small.c), block calls
- * stay on the GPU.  The environment variable LQ_SMALL_CALLS=host
- * sets 1 at load. */
+/* Small-call mode (no reference counterpart).  1 (default): the
+ * single-sample / single-vector entry points -- firfilt_*_execute after push,
+ * dotprod_*_execute / _run / _run4, firdecim_*_execute, firinterp_*_execute,
+ * resamp_*_execute, and fftfilt_*_execute when n * h_len <= 65536 -- compute
+ * on the host (host/lq_small.c); every *_execute_block[_dev] call, the
+ * channelizers, FFT plans and spgram run on the GPU.  0: every call runs on
+ * the GPU.  The environment variable LQ_SMALL_CALLS=gpu sets 0 at load. */
 void liquid_mi355x_set_small_calls(int _host);
 int liquid_mi355x_get_small_calls(void);
 

@@ -47,13 +47,10 @@
 #include <cstdint>
 #include <cstdio>
 
-#ifndef FMX_VARIANT
-#define FMX_VARIANT 0
-#endif
-#ifndef FMX_WGS
-#define FMX_WGS 512   // crcf 33..64 taps: persistent workgroups, two per CU (A/B on one box: 0.804 ms vs
-                      // 0.822-0.826 at three per CU with two chunks in flight, 0.819-0.821 two per CU with two)
-#endif
+// crcf 33..64 taps: persistent workgroups, two per CU (A/B on one box: 0.804 ms
+// vs 0.822-0.826 at three per CU with two chunks in flight, 0.819-0.821 two
+// per CU with two; profiles/r04_ab_experiments.txt)
+constexpr int FMX_WGS = 512;
 
 namespace {
 
@@ -86,27 +83,17 @@ constexpr int SSTR = 68;          // floats per staged segment (32 x re/im + pad
 // 16-byte read
 template <int KB>
 constexpr int glen_kb() { return 16 * (2 + 4 * KB) + 32; }
-// bf16 terms of the taps whose A fragments come from LDS (the last NAL of
-// the three): all of them past 128 taps; at KB = 1 (crcf / rrrf-shaped, one
-// tap matrix) terms 2 and 3, which frees 48 VGPRs for a third chunk of loads
-// in flight while the 4 KB of copies still leave room for three workgroups
-// per CU
-#ifndef FMX_A2L
-#define FMX_A2L 0
-#endif
-#ifndef FMX_NBUF
-#define FMX_NBUF 3   // chunks of loads in flight per workgroup (register sets; 2..4)
-#endif
+// bf16 terms of the taps whose A fragments come from LDS: all three past 128
+// taps (KB > 2), none below (taking terms 2 and 3 from LDS at KB = 1 to free
+// registers for a third chunk measured 0.915-0.925 ms against 0.803-0.805:
+// the fragment reads sit on the MFMA chain, DESIGN (f)3)
 template <bool CC, int KB>
-constexpr int nal_kb() { return KB > 2 ? 3 : ((!CC && KB == 1 && FMX_A2L) ? 2 : 0); }
-#ifndef FMX_NBUF_KB
-#define FMX_NBUF_KB 2   // the same for crcf with 65..256 taps (KB >= 2, two workgroups per CU)
-#endif
-#ifndef FMX_NBUF_CC
-#define FMX_NBUF_CC 2   // the same for cccf
-#endif
+constexpr int nal_kb() { return KB > 2 ? 3 : 0; }
+// chunks of loads in flight per workgroup (register sets): three for crcf
+// 33..64 taps, two for 65..256 taps and for cccf (two workgroups per CU each;
+// four measured the same as three)
 template <bool CC, int KB>
-constexpr int nbuf_kb() { return CC ? FMX_NBUF_CC : (KB == 1 ? FMX_NBUF : FMX_NBUF_KB); }
+constexpr int nbuf_kb() { return CC ? 2 : (KB == 1 ? 3 : 2); }
 // elements between the eight shifted copies: at least NAL GL, and 16 mod 128
 // (32 B mod 256), so the 16 lanes of a ds_read_b128 pass -- eight copies at
 // two bases 16 B apart -- land on 16 distinct bank groups (a stride that is
@@ -231,7 +218,7 @@ __device__ __forceinline__ void load8b(__amdgpu_buffer_rsrc_t rx, unsigned off, 
 // accumulators, C1 = Hr [Xr | Xi] and C2 = Hi [Xr | Xi]; y = (C1.re - C2.im,
 // C1.im + C2.re) is formed when the staged accumulators are read back.
 template <bool CC, int KB>
-__global__ __launch_bounds__(NT, KB > 2 ? 2 : ((CC || KB > 1 || FMX_WGS <= 512) ? 2 : 3)) void k_firfilt_mx(const v2f *__restrict__ win,
+__global__ __launch_bounds__(NT, 2) void k_firfilt_mx(const v2f *__restrict__ win,
                                                               const v2f *__restrict__ x, long long n,
                                                               v2f *__restrict__ y, const float *__restrict__ hpad,
                                                               float sre, float sim, long long nch, int hlen)
@@ -352,24 +339,19 @@ __global__ __launch_bounds__(NT, KB > 2 ? 2 : ((CC || KB > 1 || FMX_WGS <= 512) 
     const int sg = r32 & 15, comp = r32 >> 4;
     auto step = [&](long long k, v4f (&xv)[4], v2f &hv) {
         const long long c = w + k * G;
-        if (!(FMX_VARIANT & 32)) __syncthreads();   // the previous chunk's MFMA reads are done (32: experiment)
+        __syncthreads();   // the previous chunk's MFMA reads are done
         const int cs = (int)(k % 3);
         // chunk 0's halo planes came from the history in the prologue
-        if (!(FMX_VARIANT & 8) && tid < HALO && c != 0) {   // 8: timing experiment, no halo
+        if (tid < HALO && c != 0) {
             put1(planes, PLB, tid, hv);
-            if (!(FMX_VARIANT & 16) && (unsafe_bits(hv.x) | unsafe_bits(hv.y))) atomicOr(&sbad[cs], 1u);
+            if (unsafe_bits(hv.x) | unsafe_bits(hv.y)) atomicOr(&sbad[cs], 1u);
         }
-#if FMX_VARIANT & 2   // timing experiment: no plane writes (wrong results)
-        if (__float_as_uint(xv[0].x + xv[1].y + xv[2].z + xv[3].w) == 0x7fc00001u) put8(planes, PLB, HALO + 8 * tid, xv);
-#else
         put8(planes, PLB, HALO + 8 * tid, xv);
-#endif
-        if (!(FMX_VARIANT & 16) && (unsafe4(xv[0]) | unsafe4(xv[1]) | unsafe4(xv[2]) | unsafe4(xv[3])))
-            atomicOr(&sbad[cs], 1u);   // 16: timing experiment, no range guard
+        if (unsafe4(xv[0]) | unsafe4(xv[1]) | unsafe4(xv[2]) | unsafe4(xv[3])) atomicOr(&sbad[cs], 1u);
         if (tid == 0) sbad[(cs + 1) % 3] = 0u;   // step k+1's slot (last read in step k-2)
         load8b(rx, main_off(k + NB), xv);
-        if (!(FMX_VARIANT & 8)) hv = ldh(halo_off(k + NB));
-        if (!(FMX_VARIANT & 32)) __syncthreads();
+        hv = ldh(halo_off(k + NB));
+        __syncthreads();
         if (tid == 0 && sbad[cs] && c < nch) bad_mask[k >> 5] |= 1u << (k & 31);
 
         f32x16 C[NA];
@@ -383,13 +365,6 @@ __global__ __launch_bounds__(NT, KB > 2 ? 2 : ((CC || KB > 1 || FMX_WGS <= 512) 
             const bf16x8 b1 = *reinterpret_cast<const bf16x8 *>(bp + 2 * PLB);
             const bf16x8 b2 = *reinterpret_cast<const bf16x8 *>(bp + 4 * PLB);
             // terms of order 2^-16 first, then 2^-8, then the leading product
-#if FMX_VARIANT & 1   // timing experiment: no MFMA (wrong results)
-#pragma unroll
-            for (int a = 0; a < NA; a++) {
-                C[a][s] += (float)b0[0] + (float)b1[1] + (float)b2[2] + (float)b0[1];
-            }
-            continue;
-#endif
             bf16x8 al[NAL > 0 ? NAL : 1];
 #pragma unroll
             for (int p = 0; p < NAL; p++) al[p] = *reinterpret_cast<const bf16x8 *>(acl + p * GL + 16 * s);
@@ -407,17 +382,6 @@ __global__ __launch_bounds__(NT, KB > 2 ? 2 : ((CC || KB > 1 || FMX_WGS <= 512) 
             }
         }
 
-#if FMX_VARIANT & 4   // timing experiment: accumulators stored as they are, no staging (wrong layout)
-        if constexpr (!CC) {
-            const unsigned o0x = (unsigned)(CH * c + 512 * wave) * 8u;
-#pragma unroll
-            for (int q = 0; q < 4; q++)
-                __builtin_amdgcn_raw_buffer_store_b128(v4f{C[0][4 * q], C[0][4 * q + 1], C[0][4 * q + 2], C[0][4 * q + 3]},
-                                                       ry, c < nch ? o0x + 16u * (lane + 64 * q) : OOB, 0,
-                                                       (FMX_VARIANT & 64) ? 0 : 2);
-            return;
-        }
-#endif
         // accumulator (col r32, row (r&3) + 8(r>>2) + 4hh) -> stage[a][sg][i][comp]
 #pragma unroll
         for (int a = 0; a < NA; a++)
@@ -441,7 +405,7 @@ __global__ __launch_bounds__(NT, KB > 2 ? 2 : ((CC || KB > 1 || FMX_WGS <= 512) 
             const v4f r = CC ? v4f{a.x * sre - a.y * sim, a.x * sim + a.y * sre, a.z * sre - a.w * sim,
                                    a.z * sim + a.w * sre}
                              : a * sre;   // crcf: real scale per component (firfilt.c:337)
-            __builtin_amdgcn_raw_buffer_store_b128(r, ry, c < nch ? o0 + 8u * o : OOB, 0, (FMX_VARIANT & 64) ? 0 : 2);
+            __builtin_amdgcn_raw_buffer_store_b128(r, ry, c < nch ? o0 + 8u * o : OOB, 0, 2);
         }
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
         __builtin_amdgcn_wave_barrier();
@@ -607,8 +571,8 @@ __global__ __launch_bounds__(NT, 3) void k_firfilt_mx_r(const float *__restrict_
         }
         put8r(planes, PLBR, 64 + 16 * tid, xv[0], xv[1]);
         put8r(planes, PLBR, 64 + 16 * tid + 8, xv[2], xv[3]);
-        if (!(FMX_VARIANT & 16) && (unsafe4(xv[0]) | unsafe4(xv[1]) | unsafe4(xv[2]) | unsafe4(xv[3])))
-            atomicOr(&sbad[cs], 1u);   // 16: timing experiment, no range guard
+        if (unsafe4(xv[0]) | unsafe4(xv[1]) | unsafe4(xv[2]) | unsafe4(xv[3]))
+            atomicOr(&sbad[cs], 1u);
         if (tid == 0) sbad[(cs + 1) % 3] = 0u;
         load16rb(rx, main_off(k + 2), xv);
         hv = __builtin_amdgcn_raw_buffer_load_b128(rx, halo_off(k + 2), 0, 0);

@@ -20,7 +20,9 @@
 // 253 K checkpoints, 2 MB, read from L2 at 2 B / input).  Lanes read
 // the checkpoint at or before their first input, step
 // the reference's float32 recurrence forward to it and replay their own
-// inputs, bit-exactly (contraction off).  k_resamp3 (the default) turns the replay into a
+// inputs, bit-exactly (contraction off).  Complex streams at 1 < r < 2 with a
+// power-of-two bank count run k_resamp4 (csrc/k_resamp4.hip, an output plan
+// instead); every other shape comes here: k_resamp3 turns the replay into a
 // dense per-wave-tile output list and evaluates it with coalesced stores;
 // k_resamp / k_resamp_generic cover shapes whose tables do not fit LDS and
 // rates whose outputs overflow a wave tile (r > ~52).
@@ -246,18 +248,8 @@ __device__ __forceinline__ rs_ref rs_locate_near(const lqk_rs_plan &pl, unsigned
     return rs_ref{(unsigned)(j / LQK_RS_CK), (int)(j & (LQK_RS_CK - 1)), c};
 }
 
-#ifndef RS_ALD
-#define RS_ALD 1   // evaluation reads as single ds_read_b64 (relaxed workgroup atomics: never paired into ds_read2_b64)
-#endif
-#ifndef RS_RSC
-#define RS_RSC 1   // pair-table row stride a compile-time constant (npfb <= 64: 33) -> immediate tap offsets
-#endif
-#ifndef RS_STAUX
-#define RS_STAUX 2  // cache policy of the output stores: non-temporal (A/B on one box: 0.197 vs 0.206 ms)
-#endif
-#ifndef RS_LDAUX
-#define RS_LDAUX 0  // cache policy of the input loads
-#endif
+// output stores non-temporal (A/B in round 4 on one box: 0.197 vs 0.206 ms)
+constexpr int RS_STAUX = 2;
 // pair-table row stride (8-byte slots per half row): RSC, or npfb/2 + 1 at run time
 template <int RSC>
 __host__ __device__ inline int rs2_rs(int npfb) { return RSC ? RSC : (npfb >> 1) + 1; }
@@ -267,7 +259,6 @@ __host__ __device__ inline int rs2_rs(int npfb) { return RSC ? RSC : (npfb >> 1)
 template <typename T>
 __device__ __forceinline__ T lds_rd(const T *p)
 {
-#if RS_ALD
     if constexpr (sizeof(T) == 8) {
         const unsigned long long u = __hip_atomic_load(reinterpret_cast<unsigned long long *>(const_cast<T *>(p)),
                                                        __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
@@ -277,20 +268,8 @@ __device__ __forceinline__ T lds_rd(const T *p)
                                              __HIP_MEMORY_SCOPE_WORKGROUP);
         return __builtin_bit_cast(T, u);
     }
-#else
-    return *p;
-#endif
 }
 
-// PR (rates >= 1: consecutive outputs at most one input apart): each lane
-// evaluates two consecutive outputs A, B (inputs iA, iB = iA + d, d in {0, 1})
-// over one shared window W[p'] = x[iA - L + p'], p' <= L + 1: A's taps are rows
-// p' of the pair table, B's rows p' - d, the table padded with a zero row on
-// either side, so each window sample is read once for both outputs (16 + 15 +
-// 16 LDS reads per pair at L = 14 instead of 2 x 30) and the pair leaves as one
-// 16-byte store.  Terms outside an output's window are zero taps times a
-// sample; the samples there are replaced by 0, so a non-finite input never
-// reaches an output the reference keeps finite.
 // acc + c w for a real coefficient and a complex (packed FMA) or real sample
 __device__ __forceinline__ float2 rs_fma(float c, float2 w, float2 acc)
 {
@@ -371,65 +350,23 @@ __global__ __launch_bounds__(NT) void k_resamp_generic(lqk_rs_plan pl, unsigned 
 // 1024-input tile, as the round-3 form (k_resamp2: wave 0 replayed 16-input
 // spans for all four waves) did: 0.197 -> 0.184 ms per 2^25 inputs at
 // r = 1.037 on one box.
-#ifndef RS3_BLK
-#define RS3_BLK 5
-#endif
-#ifndef RS3_NT
-#define RS3_NT 256
-#endif
-constexpr int NT3 = RS3_NT;       // threads per k_resamp3 workgroup (waves own their tiles)
+constexpr int RS3_BLK = 5;       // resident workgroups per CU (four and six measured slower, round 4)
+constexpr int NT3 = 256;         // threads per k_resamp3 workgroup (waves own their tiles)
 constexpr int W3_TIN = 64 * 4;   // inputs per wave tile (64 lanes x 4)
-#ifndef RS3_CAP
-#define RS3_CAP 320
-#endif
-constexpr int W3_CAP = RS3_CAP;  // output slots per wave tile
-#ifndef RS3_FIT
-#define RS3_FIT 15
-#endif
-#ifndef RS3_SU
-#define RS3_SU 1
-#endif
-#ifndef RS3_NPF
-#define RS3_NPF 1
-#endif
-#ifndef RS3_PAIR
-#define RS3_PAIR 0
-#endif
-#ifndef RS3_PK
-#define RS3_PK 0
-#endif
-#ifndef RS3_SWZ
-#define RS3_SWZ 0   // output-list slot o stored at o + o / 16 (spreads the replay's strided writes over the banks)
-#endif
-// output-list slots per wave (RS3_SWZ: one pad slot per 16)
-constexpr int rs3_slots() { return RS3_SWZ ? (W3_CAP + 2) + (W3_CAP + 2) / 16 + 1 : W3_CAP + 2; }
-__device__ __forceinline__ int rs3_slot(int o) { return RS3_SWZ ? o + (o >> 4) : o; }
-#ifndef RS3_SLU
-#define RS3_SLU 1   // the evaluation's slot loop unrolled
-#endif
-// table rows (float2 units) of k_resamp3: PR pads a zero row on either side;
-// PK packs taps 2q, 2q + 1 of a bank as one 16-byte entry (h, h', dh, dh'),
-// ceil((L + 1) / 2) entries per bank
-template <int L, bool PR>
-constexpr int rs3_rows() { return PR ? L + 3 : (RS3_PK ? (L + 2) / 2 * 2 : L + 1); }
-// PR: the pair-table rows padded with a zero row on either side (pair mode)
-template <int L, typename S, int RSC, bool PR = false>
+constexpr int W3_CAP = 320;      // output slots per wave tile
+constexpr int RS3_FIT = 15;      // a tile's fixed cost in evaluation passes x 10 (tile fitting, launch_rs)
+// table rows (float2 units) of k_resamp3
+template <int L>
+constexpr int rs3_rows() { return L + 1; }
+template <int L, typename S, int RSC>
 inline size_t rs3_lds_bytes(int npfb)
 {
     constexpr int TS = W3_TIN + L + 2;
-    return (size_t)2 * rs3_rows<L, PR>() * rs2_rs<RSC>(npfb) * sizeof(float2) +
-           (size_t)(NT3 / 64) * (((TS + 2) * sizeof(S) + 15) / 16 * 16 + rs3_slots() * 8);
+    return (size_t)2 * rs3_rows<L>() * rs2_rs<RSC>(npfb) * sizeof(float2) +
+           (size_t)(NT3 / 64) * (((TS + 2) * sizeof(S) + 15) / 16 * 16 + (W3_CAP + 2) * 8);
 }
 
-// PR (rates > 1: consecutive outputs at most one input apart, see
-// launch_rs): each lane evaluates two consecutive outputs A, B (inputs iA,
-// iB = iA + d, d in {0, 1}) over one shared window W[p'] = x[iA - L + p'],
-// p' <= L + 1; A's taps are table rows p', B's rows p' - d, the table padded
-// with a zero row on either side, so each window sample is read once for
-// both outputs (16 + 15 + 16 LDS reads per pair at L = 14 instead of
-// 2 x 30); the sample outside B's window enters as 0, so a non-finite input
-// there never reaches B
-template <int L, typename S, int RSC, bool PR>
+template <int L, typename S, int RSC>
 __global__ __launch_bounds__(NT3, RS3_BLK) void k_resamp3(lqk_rs_plan pl, unsigned long long g0, unsigned long long K0,
                                                        int npfb, float del, const float2 *__restrict__ taps2,
                                                        const S *__restrict__ hist, const S *__restrict__ x,
@@ -439,38 +376,25 @@ __global__ __launch_bounds__(NT3, RS3_BLK) void k_resamp3(lqk_rs_plan pl, unsign
     constexpr int SPAN = 4;
     constexpr int LP = (L + 2 + 1) & ~1;          // pair stride of taps2 (host layout)
     constexpr int TS = W3_TIN + L + 2;            // window samples of a tile
-    constexpr int WB = ((TS + 2) * (int)sizeof(S) + 15) / 16 * 16 + rs3_slots() * 8;   // bytes per wave
+    constexpr int WB = ((TS + 2) * (int)sizeof(S) + 15) / 16 * 16 + (W3_CAP + 2) * 8;   // bytes per wave
     constexpr int NXV = (TS + 63) / 64;           // window samples per lane
     constexpr int NSLOT = W3_CAP / 64;            // output slots per lane
+    constexpr int NROW = rs3_rows<L>();
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     const int RS = rs2_rs<RSC>(npfb);
-    constexpr int ROFF = PR ? 1 : 0;              // tap row p lives at table row p + ROFF
-    constexpr int NROW = rs3_rows<L, PR>();
-    constexpr bool PK = RS3_PK && !PR;
-    constexpr int NQ = (L + 2) / 2;               // PK: tap pairs per bank
     float2 *tpl = reinterpret_cast<float2 *>(smem);
-    float4 *tq = reinterpret_cast<float4 *>(smem);
     // the wave index through readfirstlane: the compiler then knows every
     // tile-level quantity (tile, i0, the plan position and its 64-bit period
     // division) is wave-uniform and computes it on the scalar unit
-    const int tid = threadIdx.x, lane = tid & 63, wave = RS3_SU ? __builtin_amdgcn_readfirstlane(tid >> 6) : tid >> 6;
+    const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     unsigned char *wbase = smem + (size_t)2 * NROW * RS * sizeof(float2) + (size_t)wave * WB;
     S *cw = reinterpret_cast<S *>(wbase);
     uint2 *dsc = reinterpret_cast<uint2 *>(wbase + ((TS + 2) * (int)sizeof(S) + 15) / 16 * 16);   // dsc[W3_CAP]: sink
     const float fnpfb = (float)npfb;
-    if constexpr (PK) {
-        for (int t = tid; t < (npfb + 1) * NQ; t += NT3) {
-            const int b = t / NQ, q = t % NQ;
-            const float2 v0 = taps2[b * LP + 2 * q];
-            const float2 v1 = 2 * q + 1 <= L ? taps2[b * LP + 2 * q + 1] : make_float2(0.0f, 0.0f);
-            tq[(2 * q + (b & 1)) * RS + (b >> 1)] = make_float4(v0.x, v1.x, v0.y - v0.x, v1.y - v1.x);
-        }
-    } else {
-        for (int t = tid; t < (npfb + 1) * NROW; t += NT3) {
-            const int b = t / NROW, rr = t % NROW, p = rr - ROFF;
-            const float2 v = (p >= 0 && p <= L) ? taps2[b * LP + p] : make_float2(0.0f, 0.0f);
-            tpl[(2 * rr + (b & 1)) * RS + (b >> 1)] = make_float2(v.x, v.y - v.x);
-        }
+    for (int t = tid; t < (npfb + 1) * NROW; t += NT3) {
+        const int b = t / NROW, p = t % NROW;
+        const float2 v = taps2[b * LP + p];
+        tpl[(2 * p + (b & 1)) * RS + (b >> 1)] = make_float2(v.x, v.y - v.x);
     }
     __syncthreads();   // the only workgroup barrier
 
@@ -485,9 +409,9 @@ __global__ __launch_bounds__(NT3, RS3_BLK) void k_resamp3(lqk_rs_plan pl, unsign
     auto ld = [&](__amdgpu_buffer_rsrc_t r, int e) -> S {
         const unsigned off = e < 0 ? 0xFFFFFFF0u : (unsigned)e * (unsigned)sizeof(S);
         if constexpr (sizeof(S) == 8)
-            return __builtin_bit_cast(S, __builtin_amdgcn_raw_buffer_load_b64(r, off, 0, RS_LDAUX));
+            return __builtin_bit_cast(S, __builtin_amdgcn_raw_buffer_load_b64(r, off, 0, 0));
         else
-            return __builtin_bit_cast(S, __builtin_amdgcn_raw_buffer_load_b32(r, off, 0, RS_LDAUX));
+            return __builtin_bit_cast(S, __builtin_amdgcn_raw_buffer_load_b32(r, off, 0, 0));
     };
     struct Pre {
         S xa[NXV], xh;
@@ -523,24 +447,23 @@ __global__ __launch_bounds__(NT3, RS3_BLK) void k_resamp3(lqk_rs_plan pl, unsign
         __builtin_amdgcn_wave_barrier();
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
     };
-    // RS3_NPF tiles of loads in flight per wave (register sets pa [, pb])
-    constexpr int NPF = RS3_NPF;
-    Pre pa, pb;
+    // one tile of loads in flight per wave (a second set measured slower:
+    // 82 VGPRs; the CU's other waves hide the latency)
+    Pre pa;
     fetch(gw, pa);
-    if constexpr (NPF > 1) fetch(gw + GW, pb);
-    auto body = [&](long long tile, Pre &cur) {
+    for (long long tile = gw; tile < ntiles; tile += GW) {
         const long long i0 = tile * tin;
         const long long ie = (i0 + tin < n) ? i0 + tin : n;
-        const lqk_rs_entry e = cur.e;
-        const unsigned long long cyc = cur.cyc;
-        const int skip = cur.skip;
+        const lqk_rs_entry e = pa.e;
+        const unsigned long long cyc = pa.cyc;
+        const int skip = pa.skip;
         wave_fence();   // the previous tile's evaluation has read the window
 #pragma unroll
         for (int u = 0; u < NXV; u++) {
             const int t = lane + 64 * u;
-            if (t < TS) cw[t] = u == 0 ? cur.xa[0] + cur.xh : cur.xa[u];
+            if (t < TS) cw[t] = u == 0 ? pa.xa[0] + pa.xh : pa.xa[u];
         }
-        fetch(tile + NPF * GW, cur);
+        fetch(tile + GW, pa);
         // replay: lane j, inputs ia .. ia + nin - 1
         const long long ia = i0 + (long long)lane * SPAN;
         const int nin = ia < ie ? (int)((ie - ia) < SPAN ? (ie - ia) : SPAN) : 0;
@@ -567,7 +490,7 @@ __global__ __launch_bounds__(NT3, RS3_BLK) void k_resamp3(lqk_rs_plan pl, unsign
         const int o0 = o64 < (1ull << 30) ? (int)o64 : (1 << 30);
         int o = o0;
         auto put = [&](int iloc, int bank, float mu) {
-            dsc[rs3_slot((unsigned)o < (unsigned)W3_CAP ? o : W3_CAP)] =
+            dsc[(unsigned)o < (unsigned)W3_CAP ? o : W3_CAP] =
                 make_uint2(__float_as_uint(mu), (unsigned)iloc | ((unsigned)bank << 12));
             o++;
         };
@@ -601,93 +524,34 @@ __global__ __launch_bounds__(NT3, RS3_BLK) void k_resamp3(lqk_rs_plan pl, unsign
             }
         }
         // outputs of the tile: those before the last replaying lane's end
+        // (at most W3_CAP by the host's tile sizing, launch_rs; clamped so a
+        // violated bound can never read past the output list)
         const int last = (int)((ie - i0 - 1) / SPAN);
-        const int nr = __builtin_amdgcn_readlane(o, last);
+        int nr = __builtin_amdgcn_readlane(o, last);
+        nr = nr < W3_CAP ? nr : W3_CAP;
         const unsigned ob = (unsigned)(Kb - K0);
         wave_fence();   // the output list is written
-        if constexpr (PR) {
-            // pairs q = lane + 64 k: outputs 2q, 2q + 1
-            constexpr int NPS = (W3_CAP / 2 + 63) / 64;
-#pragma unroll
-            for (int kq = 0; kq < NPS; kq++) {
-                const int q = lane + 64 * kq, oa = 2 * q;
-                S va{}, vb{};
-                if (oa < nr) {
-                    const uint2 da = lds_rd(&dsc[rs3_slot(oa)]), db = lds_rd(&dsc[rs3_slot(oa + 1)]);
-                    const bool hb = oa + 1 < nr;
-                    const int ia = (int)(da.y & 4095u), bA = (int)(da.y >> 12);
-                    const int dd = hb ? (((int)(db.y & 4095u) - ia) & 1) : 0;
-                    const int bB = hb ? (int)(db.y >> 12) : 0;
-                    const float muA = __uint_as_float(da.x), muB = hb ? __uint_as_float(db.x) : 0.0f;
-                    const S *wv = cw + ia + 1;
-                    const float2 *tA = tpl + (2 * ROFF + (bA & 1)) * RS + (bA >> 1);
-                    const float2 *tB = tpl + (2 * (ROFF - dd) + (bB & 1)) * RS + (bB >> 1);
-#pragma unroll
-                    for (int pp = 0; pp <= L + 1; pp++) {
-                        const S w = lds_rd(wv + pp);
-                        const float2 tb = lds_rd(tB + 2 * pp * RS);
-                        const float cb = fmaf(muB, tb.y, tb.x);
-                        // B's window is W[dd .. dd + L]: the sample outside it enters as 0
-                        const S wb = ((pp == 0 && dd == 1) || (pp == L + 1 && dd == 0)) ? S{} : w;
-                        if (pp <= L) {
-                            const float2 ta = lds_rd(tA + 2 * pp * RS);
-                            const float ca = fmaf(muA, ta.y, ta.x);
-                            va = rs_fma(ca, w, va);
-                        }
-                        vb = rs_fma(cb, wb, vb);
-                    }
-                }
-                const unsigned o2 = (ob + (unsigned)oa) * (unsigned)sizeof(S);
-                rs_store1(ry, oa < nr ? o2 : 0xFFFFFFF0u, va);
-                rs_store1(ry, oa + 1 < nr ? o2 + (unsigned)sizeof(S) : 0xFFFFFFF0u, vb);
-            }
-        } else {
         auto dot = [&](const S *wv, int bb, float mu) -> S {
             S acc{};
-            if constexpr (PK) {
-                // one 16-byte read and one packed FMA (c, c') = (h, h') + mu (dh, dh')
-                // per two taps; the terms in the same order as below
-                const float4 *tp = tq + (bb & 1) * RS + (bb >> 1);
+            const float2 *tp = tpl + (bb & 1) * RS + (bb >> 1);
 #pragma unroll
-                for (int q = 0; q < NQ; q++) {
-                    const float4 t = tp[2 * q * RS];
-                    const v2f cc = __builtin_elementwise_fma(v2f{mu, mu}, v2f{t.z, t.w}, v2f{t.x, t.y});
-                    acc = rs_fma(cc.x, lds_rd(wv + 2 * q), acc);
-                    if (2 * q + 1 <= L) acc = rs_fma(cc.y, lds_rd(wv + 2 * q + 1), acc);
-                }
-            } else {
-                const float2 *tp = tpl + (bb & 1) * RS + (bb >> 1);
-#pragma unroll
-                for (int p = 0; p <= L; p++) {
-                    const float2 t = lds_rd(tp + 2 * p * RS);
-                    const float c = fmaf(mu, t.y, t.x);
-                    const S w = lds_rd(wv + p);
-                    acc = rs_fma(c, w, acc);
-                }
+            for (int p = 0; p <= L; p++) {
+                const float2 t = lds_rd(tp + 2 * p * RS);
+                const float c = fmaf(mu, t.y, t.x);
+                const S w = lds_rd(wv + p);
+                acc = rs_fma(c, w, acc);
             }
             return acc;
         };
-#if RS3_SLU
 #pragma unroll
-#else
-#pragma unroll 1
-#endif
         for (int q = 0; q < NSLOT; q++) {
             const int oo = lane + 64 * q;
             S v{};
             if (oo < nr) {
-                const uint2 dd = dsc[rs3_slot(oo)];
+                const uint2 dd = dsc[oo];
                 v = dot(cw + (int)(dd.y & 4095u) + 1, (int)(dd.y >> 12), __uint_as_float(dd.x));
             }
             rs_store1(ry, oo < nr ? (ob + (unsigned)oo) * (unsigned)sizeof(S) : 0xFFFFFFF0u, v);
-        }
-        }
-    };
-    for (long long tile = gw; tile < ntiles; tile += NPF * GW) {
-        body(tile, pa);
-        if constexpr (NPF > 1) {
-            if (tile + GW >= ntiles) break;
-            body(tile + GW, pb);
         }
     }
 }
@@ -697,17 +561,9 @@ void launch_rs(const lqk_rs_plan &pl, unsigned long long g0, unsigned long long 
                const float2 *taps, const float2 *taps2, const S *hist, const S *x, long long n, S *y,
                unsigned long long nout, hipStream_t st)
 {
-    constexpr int RSC = RS_RSC ? 33 : 0;       // constant stride for npfb <= 64
-    const bool cst = RSC && npfb <= 2 * (RSC - 1);
-    // pairs of outputs per lane (constant-stride tables) when consecutive
-    // outputs are at most one input apart: tau moves by del per output and
-    // by -1 per input, and an input emits while tau < 1 - 1/npfb, so after
-    // an output at tau_k < 1 - 1/npfb the next input emits if
-    // tau_k + del - 1 < 1 - 1/npfb: del <= 1, with a margin for the float32
-    // rounding of tau_k + del
-    const bool pr = RS3_PAIR && cst && del <= 1.0f - 0x1p-22f;
-    const size_t lds3 = pr ? rs3_lds_bytes<L, S, RSC, true>(npfb)
-                      : cst ? rs3_lds_bytes<L, S, RSC>(npfb) : rs3_lds_bytes<L, S, 0>(npfb);
+    constexpr int RSC = 33;                    // constant pair-table stride for npfb <= 64 (immediate tap offsets)
+    const bool cst = npfb <= 2 * (RSC - 1);
+    const size_t lds3 = cst ? rs3_lds_bytes<L, S, RSC>(npfb) : rs3_lds_bytes<L, S, 0>(npfb);
     if (taps2 != nullptr && lds3 <= 80 * 1024 && pl.P < (1ull << 31) && (pl.pre < (1ull << 62) || pl.end < (1ull << 62))) {
         // inputs per wave tile (a multiple of 4): its outputs, at most
         // (tin + 2) r + 2 (tau moves by 1/r per output and by -1 per input
@@ -715,7 +571,6 @@ void launch_rs(const lqk_rs_plan &pl, unsigned long long g0, unsigned long long 
         const double r = 1.0 / (double)del;
         int tin = W3_TIN;
         while (tin > 4 && std::ceil((tin + 2) * r) + 2 > W3_CAP) tin -= 4;
-#if RS3_FIT
         // then the tile size with the fewest evaluation passes (64 outputs
         // each, a pass runs only where a lane has an output) per input,
         // counting the tile's fixed cost (window store, replay) as RS3_FIT / 10
@@ -733,20 +588,16 @@ void launch_rs(const lqk_rs_plan &pl, unsigned long long g0, unsigned long long 
             }
             tin = bt;
         }
-#endif
         if (std::ceil((tin + 2) * r) + 2 <= W3_CAP) {   // else (r > ~52): the per-input kernel below
             const long long ntiles = (n + tin - 1) / tin;
             const long long wgs = (ntiles + NT3 / 64 - 1) / (NT3 / 64);
             const int blk = lds3 <= 160 * 1024 / RS3_BLK ? RS3_BLK : (int)(160 * 1024 / lds3);
             const unsigned nb = (unsigned)(wgs < 256 * blk ? wgs : 256 * blk);   // persistent: blk per CU
-            if (pr)
-                hipLaunchKernelGGL((k_resamp3<L, S, RSC, true>), dim3(nb), dim3(NT3), lds3, st, pl, g0, K0, npfb, del,
-                                   taps2, hist, x, n, y, (int)nout, tin);
-            else if (cst)
-                hipLaunchKernelGGL((k_resamp3<L, S, RSC, false>), dim3(nb), dim3(NT3), lds3, st, pl, g0, K0, npfb, del,
+            if (cst)
+                hipLaunchKernelGGL((k_resamp3<L, S, RSC>), dim3(nb), dim3(NT3), lds3, st, pl, g0, K0, npfb, del,
                                    taps2, hist, x, n, y, (int)nout, tin);
             else
-                hipLaunchKernelGGL((k_resamp3<L, S, 0, false>), dim3(nb), dim3(NT3), lds3, st, pl, g0, K0, npfb, del,
+                hipLaunchKernelGGL((k_resamp3<L, S, 0>), dim3(nb), dim3(NT3), lds3, st, pl, g0, K0, npfb, del,
                                    taps2, hist, x, n, y, (int)nout, tin);
             return;
         }

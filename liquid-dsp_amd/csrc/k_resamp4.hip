@@ -1,0 +1,402 @@
+// k_resamp4.hip -- resamp_crcf / resamp_cccf for rates 1 < r < 2 with a
+// power-of-two filter-bank count (BASELINE configs[4]: r = 1.037, npfb = 64,
+// m = 7).
+//
+// Reference: src/filter/src/resamp.c:245-311 (execute: per input, while
+// b < npfb emit y = (1-mu) y_b + mu y_{b+1} and advance the timing), :352-363
+// (update_timing_state: tau += 1/r, b = floor(tau npfb), mu = tau npfb - b),
+// src/filter/src/firpfb.c:325-345 (bank output y_b(i) = sum_n h[b + n npfb]
+// x[i - n]).
+//
+// For 1 < r < 2 every input emits one or two outputs, so the output sequence
+// has a simple serial form: output k is emitted at (tau_k, i_k); then
+// tau += 1/r and, when tau reaches 1 - 1/npfb, tau -= 1 and the next input
+// begins (host/resamp.c checks the one-or-two property over the whole plan).
+// The host tabulates (tau_k, i_k) for every fourth output of the float32
+// schedule (the "output plan", periodic: r = 1.037 repeats after 2^20 outputs,
+// a 2 MB table read from L2 at 2 B per output), and the kernel replays it
+// bit-exactly:
+//   * a wave tile is 256 consecutive outputs; lane j owns outputs 4j .. 4j+3,
+//     so its replay is four straight-line steps from its own table entry
+//     (no per-input loop, no output list) and its four outputs leave as two
+//     16-byte non-temporal stores -- each wave instruction writes 1 KB of
+//     whole 128-byte lines;
+//   * the lane's four outputs lie on inputs i_a .. i_a + 3, so the window
+//     W[q] = x[i_a - L + q], q <= L + 3, is read once from LDS into registers,
+//     and output s (input i_a + d_s) is sum_q c_s[q - d_s] W[q]: its taps come
+//     from a table padded with two zero rows on either side, read at a lane
+//     offset, so every window index is a compile-time register index.  With
+//     one or two outputs per input d_0 = 0, d_1 <= 1, 1 <= d_2 <= 2,
+//     1 <= d_3 <= 3: 15 + 16 + 16 + 17 taps for four outputs;
+//   * a tap is c = h_b[p] + mu (h_{b+1}[p] - h_b[p]) -- the (y0, y1)
+//     interpolation of resamp.c:292-295 folded into the coefficient -- from
+//     one 8-byte LDS read, then one packed FMA on the complex sample.  Bank
+//     npfb is the BOUNDARY pair (h_{npfb-1} on the window one input older,
+//     h_0; resamp.c:263-279), so both timing states are one dot product;
+//   * the tile's input window is loaded a tile ahead into registers and
+//     written to the wave's LDS in a transposed order (sample t at
+//     (t & 3) * N4 + t / 4), where the lanes' window reads, about 4/r samples
+//     apart, fall on distinct banks (r = 1.037: about one 2-way conflict per
+//     32-lane group) and the stores on distinct banks.
+// Taps outside an output's own window are zero, so finite samples there add
+// exactly 0; a non-finite sample reaches the outputs whose register window
+// (L + 4 samples) holds it -- a superset of the reference's, as for the
+// zero-padded tap rows of k_resamp3 (resamp is not tested on non-finite input).
+#include <hip/hip_runtime.h>
+
+#include "lq_device.h"
+#include "lq_kernels.h"
+
+#include <cstdio>
+#include <cstdlib>
+
+namespace {
+
+constexpr int NT4 = 256;       // 4 waves per workgroup; each wave owns its tiles end to end
+constexpr int TOUT = 256;      // outputs per wave tile (4 per lane)
+constexpr int N4 = 88;         // slots per residue class of the transposed window (>= (L + 259) / 4)
+// resident workgroups per CU: five (<= 96 VGPRs) while the register window
+// (2L + 8 VGPRs) allows, else four (<= 128)
+template <int L>
+constexpr int rs4_blk() { return L <= 18 ? 5 : 4; }
+
+// window samples of a tile: outputs k0 .. k0+255 lie on inputs i_e .. i_e+255
+// (i_e: input of the tile's table entry, at most 3 outputs before k0), and the
+// lane windows reach L samples back and 3 forward
+template <int L>
+constexpr int rs4_tsw() { return L + 259; }
+
+template <int L>
+constexpr int rs4_rows() { return L + 5; }   // tap rows -2 .. L+2
+
+// one 8-byte LDS read, volatile: issued as its own ds_read_b64 (2 LDS cycles
+// per wave instruction), never paired into a ds_read2_b64 (8 cycles)
+__device__ __forceinline__ float2 lds_rd8(const float2 *p)
+{
+    typedef const volatile unsigned long long __attribute__((address_space(3))) *lp;
+    const unsigned long long u = *(lp)(p);
+    return __builtin_bit_cast(float2, u);
+}
+
+__device__ __forceinline__ void wave_fence()
+{
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+template <int L, int NPC>
+__global__ __launch_bounds__(NT4, rs4_blk<L>()) void k_resamp4(lqk_rs4_plan pl, unsigned long long g0,
+                                                      unsigned long long K0, int npfb, float del,
+                                                      const float2 *__restrict__ taps2,
+                                                      const float2 *__restrict__ hist,
+                                                      const float2 *__restrict__ x, int n,
+                                                      float2 *__restrict__ y, int nout, bool al16)
+{
+    constexpr int NR = rs4_rows<L>();
+    constexpr int LP = (L + 3) & ~1;                 // pair stride of taps2 (host layout)
+    constexpr int TSW = rs4_tsw<L>();
+    constexpr int NXV = (TSW + 63) / 64;             // window samples per lane
+    constexpr int NW = L + 4;                        // register window per lane
+    static_assert(TSW <= 4 * N4, "window exceeds the transposed layout");
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    const int RS = NPC ? NPC + 1 : npfb + 1;         // table row stride (== 1 mod 32 for npfb >= 32)
+    float2 *tt = reinterpret_cast<float2 *>(smem);   // tt[(p + 2) RS + b] = (h_b[p], h_{b+1}[p] - h_b[p])
+    const int tbytes = (NR * RS * 8 + 15) & ~15;
+    const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    for (int e = tid; e < NR * RS; e += NT4) {
+        const int rr = e / RS, b = e - rr * RS, p = rr - 2;
+        float2 v = make_float2(0.0f, 0.0f);
+        if (p >= 0 && p <= L && b <= npfb) {
+            const float2 t = taps2[b * LP + p];
+            v = make_float2(t.x, t.y - t.x);
+        }
+        tt[e] = v;
+    }
+    __syncthreads();   // the only workgroup barrier
+
+    const int ntiles = (nout + TOUT - 1) / TOUT;
+    const int GW = (int)gridDim.x * (NT4 / 64), gw = (int)blockIdx.x * (NT4 / 64) + wave;
+    if (gw >= ntiles) return;
+    float2 *win = reinterpret_cast<float2 *>(smem + tbytes) + wave * (4 * N4);
+
+    const __amdgpu_buffer_rsrc_t ry = __builtin_amdgcn_make_buffer_rsrc((void *)y, (short)0, nout * 8, 0x00020000);
+    const __amdgpu_buffer_rsrc_t rt =
+        __builtin_amdgcn_make_buffer_rsrc((void *)pl.tab, (short)0, (int)(pl.ntab * 8), 0x00020000);
+    typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
+    typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+    auto ld8 = [&](__amdgpu_buffer_rsrc_t r, int e) -> float2 {
+        const unsigned off = e < 0 ? 0xFFFFFFF0u : (unsigned)e * 8u;
+        return __builtin_bit_cast(float2, __builtin_amdgcn_raw_buffer_load_b64(r, off, 0, 0));
+    };
+
+    // Table entries.  Lane j of tile T reads the state at plan output
+    // kb + 4j, kb = the tile's first output rounded down to a multiple of 4;
+    // outputs >= pre repeat with period QT (PT inputs), QT a multiple of 4 and
+    // >= 256, so a tile wraps at most once.  A wave walks its tiles GW apart,
+    // so the tile's periodic position (r0 = (kb - pre) mod QT, q0 periods) is
+    // stepped by the constant (GW 256) mod QT on the scalar unit instead of
+    // divided per tile.  The entry's input index becomes call-relative only
+    // when it is used (i = entry word + off), so nothing waits on the load.
+    struct Ent {
+        float2 raw;   // (tau, plan input as bits)
+        int off;      // + (periods) PT - g0, modulo 2^32
+    };
+    struct Cur {
+        unsigned long long kb, r0, q0;
+        bool per;
+    };
+    const unsigned long long STEP = (unsigned long long)GW * TOUT;
+    unsigned long long dQ = 0, dR = 0;
+    if (pl.pre != ~0ull) {
+        dQ = STEP / pl.QT;
+        dR = STEP - dQ * pl.QT;
+    }
+    auto cur_fix = [&](Cur &c) {
+        c.per = c.kb >= pl.pre;
+        if (c.per) {
+            const unsigned long long dt = c.kb - pl.pre;
+            c.q0 = dt / pl.QT;
+            c.r0 = dt - c.q0 * pl.QT;
+        }
+    };
+    auto cur_next = [&](Cur &c) {
+        c.kb += STEP;
+        if (c.per) {
+            c.r0 += dR;
+            c.q0 += dQ;
+            if (c.r0 >= pl.QT) {
+                c.r0 -= pl.QT;
+                c.q0++;
+            }
+        } else {
+            cur_fix(c);
+        }
+    };
+    auto entry = [&](int tile, const Cur &c) -> Ent {
+        if (tile >= ntiles) return Ent{make_float2(0.0f, 0.0f), 0};
+        unsigned long long idx = (c.kb >> 2) + (unsigned)lane;
+        int off = -(int)(unsigned)g0;
+        if (c.per) {
+            const bool w = c.r0 + 4ull * (unsigned)lane >= pl.QT;
+            idx = ((pl.pre + c.r0) >> 2) + (unsigned)lane - (w ? (pl.QT >> 2) : 0ull);
+            off = (int)(unsigned)(c.q0 * pl.PT - g0) + (w ? (int)(unsigned)pl.PT : 0);
+        }
+        return Ent{ld8(rt, idx < pl.ntab ? (int)idx : -1), off};
+    };
+    auto ent_i = [](const Ent &e) { return (int)__float_as_uint(e.raw.y) + e.off; };
+    // prefetched window of a tile: window sample t is input ws + t,
+    // ws = (the tile's lane-0 entry input) - L.  Both forms issue NXV loads
+    // into the same registers (so the loop's wait counts stay static).
+    // Samples past the call's last input are never weighted (the evaluation
+    // zeroes window samples outside an output's own window).
+    struct Win {
+        float2 v[NXV];
+    };
+    auto fetch = [&](int tile, int ws, Win &w) {
+        const bool live = tile < ntiles;
+        if (ws >= 0) {   // (wave-uniform) the usual case: a descriptor based at x[ws], constant lane offsets
+            const long long rem = (long long)n - ws;
+            const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc(
+                (void *)(x + ws), (short)0, live && rem > 0 ? (int)(rem * 8) : 0, 0x00020000);
+#pragma unroll
+            for (int u = 0; u < NXV; u++)
+                w.v[u] = ld8(r, lane + 64 * u < TSW ? lane + 64 * u : -1);
+        } else {         // the call's first tile(s): inputs before the call come from the history
+#pragma unroll
+            for (int u = 0; u < NXV; u++) {
+                const int idx = ws + lane + 64 * u;
+                const float2 *p = idx < 0 ? hist + (L + (idx < -L ? -L : idx)) : (idx < n ? x + idx : hist);
+                w.v[u] = *p;
+            }
+        }
+    };
+
+    const float fnpfb = (float)npfb, z = 1.0f - 1.0f / fnpfb;
+    auto put_window = [&](const Win &w) {   // the window into the wave's LDS, transposed
+        float2 *wp = win + (lane & 3) * N4 + (lane >> 2);
+#pragma unroll
+        for (int u = 0; u < NXV; u++)
+            if (lane + 64 * u < TSW) wp[16 * u] = w.v[u];
+    };
+    // Pipeline per wave: while tile t is evaluated, the window of tile t+1
+    // and the table entries of tile t+2 are in flight; after the evaluation
+    // one wait covers both (and the stores of tile t-1), window t+1 goes to
+    // LDS, tile t's outputs are stored, and the loads for t+2 / t+3 issue.
+    Cur cc;
+    cc.kb = (K0 & ~3ull) + (unsigned long long)gw * TOUT;
+    cur_fix(cc);
+    Ent ec = entry(gw, cc);
+    cur_next(cc);
+    Ent en = entry(gw + GW, cc);
+    cur_next(cc);
+    Ent enn = entry(gw + 2 * GW, cc);
+    cur_next(cc);
+    Win wa;
+    fetch(gw, __builtin_amdgcn_readfirstlane(ent_i(ec)) - L, wa);
+    put_window(wa);
+    fetch(gw + GW, __builtin_amdgcn_readfirstlane(ent_i(en)) - L, wa);
+
+    for (int tile = gw; tile < ntiles; tile += GW) {
+        // replay: the lane's entry stepped (k0 & 3) outputs, then its four
+        // outputs (bank, mu, input offset d)
+        const unsigned long long k0 = K0 + (unsigned long long)tile * TOUT;
+        const int skip = (int)(k0 & 3ull);
+        const int i_e = __builtin_amdgcn_readfirstlane(ent_i(ec));   // input of the lane-0 entry
+        float tau = ec.raw.x;
+        int ii = ent_i(ec);
+        auto step = [&]() {
+#pragma clang fp contract(off)
+            tau = tau + del;
+            if (!(tau < z)) {
+                tau = tau - 1.0f;
+                ii++;
+            }
+        };
+        for (int s = 0; s < skip; s++) step();
+        const int ia = ii;
+        int bk[4], dd[4];
+        float mu[4];
+#pragma unroll
+        for (int s = 0; s < 4; s++) {
+#pragma clang fp contract(off)
+            const float bf = tau * fnpfb;
+            const float fb = __builtin_floorf(bf);
+            bk[s] = tau < 0.0f ? npfb : (int)fb;
+            mu[s] = bf - fb;
+            dd[s] = ii - ia;
+            if (s < 3) step();
+        }
+        // lane window W[q] = x[ia - L + q] = window sample a + q
+        int a = ia - i_e;
+        a = a < 0 ? 0 : (a > TOUT - 1 ? TOUT - 1 : a);   // lanes past the call's outputs
+        wave_fence();   // the window is in LDS
+        v2f W[NW];
+        {
+            const float2 *wb[4];
+#pragma unroll
+            for (int c = 0; c < 4; c++) wb[c] = win + ((a + c) & 3) * N4 + ((a + c) >> 2);
+#pragma unroll
+            for (int q = 0; q < NW; q++) W[q] = pk(lds_rd8(wb[q & 3] + (q >> 2)));
+        }
+        // four outputs: pass s over q in [lo, hi] (d_0 = 0, d_1 <= 1, 1 <= d_2 <= 2, 1 <= d_3 <= 3)
+        v2f acc[4];
+#pragma unroll
+        for (int s = 0; s < 4; s++) {
+            constexpr int LO[4] = {0, 0, 1, 1};
+            const int lo = LO[s], hi = L + s;
+            const float2 *tb = tt + (2 - dd[s]) * RS + bk[s];
+            const float m = mu[s];
+            v2f sacc = {0.0f, 0.0f};
+#pragma unroll
+            for (int q = lo; q <= hi; q++) {
+                const float2 t = lds_rd8(tb + q * RS);
+                const float cf = __builtin_fmaf(m, t.y, t.x);
+                sacc = v2f{cf, cf} * W[q] + sacc;
+            }
+            // the pass completes here (an empty asm on the result): without
+            // it the compiler hoists all 64 tap reads ahead of the arithmetic
+            // and spills them
+            asm volatile("" : "+v"(sacc));
+            acc[s] = sacc;
+        }
+        // the next tile's window into LDS (this tile's window reads are done)
+        wave_fence();
+        put_window(wa);
+        const int ws2 = __builtin_amdgcn_readfirstlane(ent_i(enn)) - L;   // the window after it
+        // stores: outputs tile*256 + 4 lane + s, two 16-byte stores per lane
+        {
+            const int ko = tile * TOUT + 4 * lane;
+            u32x4 s01, s23;
+            s01.x = __float_as_uint(acc[0].x);
+            s01.y = __float_as_uint(acc[0].y);
+            s01.z = __float_as_uint(acc[1].x);
+            s01.w = __float_as_uint(acc[1].y);
+            s23.x = __float_as_uint(acc[2].x);
+            s23.y = __float_as_uint(acc[2].y);
+            s23.z = __float_as_uint(acc[3].x);
+            s23.w = __float_as_uint(acc[3].y);
+            if (ko + 4 <= nout && al16) {
+                __builtin_amdgcn_raw_buffer_store_b128(s01, ry, (unsigned)ko * 8u, 0, 2);
+                __builtin_amdgcn_raw_buffer_store_b128(s23, ry, (unsigned)ko * 8u + 16u, 0, 2);
+            } else if (ko < nout) {   // the call's ragged end (one lane of one wave), or y not 16-byte aligned
+                for (int s = 0; s < 4; s++)
+                    if (ko + s < nout)
+                        __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2, acc[s]), ry,
+                                                              (unsigned)(ko + s) * 8u, 0, 2);
+            }
+        }
+        fetch(tile + 2 * GW, ws2, wa);
+        ec = en;
+        en = enn;
+        enn = entry(tile + 3 * GW, cc);
+        cur_next(cc);
+    }
+}
+
+template <int L>
+void launch_rs4(const lqk_rs4_plan &pl, unsigned long long g0, unsigned long long K0, int npfb, float del,
+                const float2 *taps2, const float2 *hist, const float2 *x, int n, float2 *y, int nout, hipStream_t st)
+{
+    const bool al16 = ((unsigned long long)y & 15) == 0;   // 16-byte output stores
+    const int RS = npfb + 1;
+    const size_t lds = (size_t)((rs4_rows<L>() * RS * 8 + 15) & ~15) + (size_t)(NT4 / 64) * 4 * N4 * 8;
+    const int ntiles = (nout + TOUT - 1) / TOUT;
+    const int wgs = (ntiles + NT4 / 64 - 1) / (NT4 / 64);
+    constexpr int B = rs4_blk<L>();
+    const int blk = lds * B <= 160 * 1024 ? B : (int)(160 * 1024 / lds);
+    const int nb = wgs < 256 * blk ? wgs : 256 * blk;   // persistent: blk per CU
+    if (npfb == 64)
+        hipLaunchKernelGGL((k_resamp4<L, 64>), dim3(nb), dim3(NT4), lds, st, pl, g0, K0, npfb, del, taps2, hist, x,
+                           n, y, nout, al16);
+    else
+        hipLaunchKernelGGL((k_resamp4<L, 0>), dim3(nb), dim3(NT4), lds, st, pl, g0, K0, npfb, del, taps2, hist, x,
+                           n, y, nout, al16);
+}
+
+} // namespace
+
+extern "C" int lqk_resamp4_supported(unsigned int npfb, unsigned int L)
+{
+    // power-of-two banks up to 256 (table in LDS), even L up to 32
+    return npfb >= 2 && npfb <= 256 && (npfb & (npfb - 1)) == 0 && L >= 2 && L <= 32 && (L % 2) == 0;
+}
+
+extern "C" void lqk_resamp4(const lqk_rs4_plan *pl, unsigned long long g0, unsigned long long K0, unsigned int npfb,
+                            unsigned int L, float del, const void *taps2, const void *hist, const void *x,
+                            unsigned long long n, void *y, unsigned long long nout, void *stream)
+{
+    if (n == 0 || nout == 0) return;
+    if (!lqk_resamp4_supported(npfb, L) || n > LQK_RS_MAXN || nout * 8ull >= (1ull << 31) || pl->ntab * 8ull >= (1ull << 31) ||
+        !(pl->pre == ~0ull || (pl->pre % 4 == 0 && pl->QT % 4 == 0 && pl->QT >= TOUT))) {
+        fprintf(stderr, "error: liquid-mi355x: resamp4 launch outside its shape (npfb %u, L %u, %llu inputs)\n", npfb, L, n);
+        exit(1);
+    }
+    hipStream_t st = (hipStream_t)stream;
+    const float2 *t2 = (const float2 *)taps2, *h = (const float2 *)hist, *xi = (const float2 *)x;
+    float2 *yo = (float2 *)y;
+#define LQ_RS4_CASE(LL)                                                                                 \
+    case LL:                                                                                            \
+        launch_rs4<LL>(*pl, g0, K0, (int)npfb, del, t2, h, xi, (int)n, yo, (int)nout, st);              \
+        break;
+    switch (L) {
+        LQ_RS4_CASE(2)
+        LQ_RS4_CASE(4)
+        LQ_RS4_CASE(6)
+        LQ_RS4_CASE(8)
+        LQ_RS4_CASE(10)
+        LQ_RS4_CASE(12)
+        LQ_RS4_CASE(14)
+        LQ_RS4_CASE(16)
+        LQ_RS4_CASE(18)
+        LQ_RS4_CASE(20)
+        LQ_RS4_CASE(22)
+        LQ_RS4_CASE(24)
+        LQ_RS4_CASE(26)
+        LQ_RS4_CASE(28)
+        LQ_RS4_CASE(30)
+        LQ_RS4_CASE(32)
+    }
+#undef LQ_RS4_CASE
+    LQ_CHECK_LAUNCH();
+}

@@ -196,6 +196,28 @@ void lqk_resamp(int real_io, const lqk_rs_plan *pl, unsigned long long g0, unsig
                 unsigned long long n, void *y, unsigned long long nout, void *stream);
 /* taps2: (npfb+1) x LP pairs, LP = (L+3) & ~1: row b < npfb (h_b[L-p], h_{b+1}[L-p]) for p = 1..L, row
  * npfb the BOUNDARY pair (h_{npfb-1}[L-1-p], h_0[L-p]); zero elsewhere (NULL: untiled kernel) */
+/* Output plan of k_resamp4 (csrc/k_resamp4.hip: complex samples, power-of-two
+ * npfb, 1 < r < 2 with one or two outputs per input over the whole plan):
+ * tab[c] = {tau, i} = the timing phase at which plan output 4c is emitted and
+ * the plan input it belongs to.  Outputs k >= pre repeat with period QT
+ * outputs / PT inputs (pre and QT multiples of 4, QT >= 256): state(k) =
+ * state(pre + (k - pre) % QT) with i += PT per period; pre = ~0: no period
+ * (a direct plan; ntab entries cover the plan's outputs). */
+typedef struct {
+    float tau;
+    unsigned int i;
+} lqk_rs4_entry;
+typedef struct {
+    const void *tab;              /* device lqk_rs4_entry[ntab] */
+    unsigned long long ntab;
+    unsigned long long pre, QT, PT;
+} lqk_rs4_plan;
+int lqk_resamp4_supported(unsigned int npfb, unsigned int L);
+/* n complex inputs x (plan inputs g0 .. g0+n) -> the nout outputs y[k - K0]
+ * for plan outputs k = K0 .. K0+nout-1; taps2 and hist as lqk_resamp */
+void lqk_resamp4(const lqk_rs4_plan *pl, unsigned long long g0, unsigned long long K0, unsigned int npfb,
+                 unsigned int L, float del, const void *taps2, const void *hist, const void *x, unsigned long long n,
+                 void *y, unsigned long long nout, void *stream);
 /* firpfb_execute(i): y = scale * sum_n hpoly[i*L + n] win[L-1-n] (win: L samples, oldest first) */
 void lqk_firpfb_single(int kind, const void *hpoly, unsigned int L, unsigned int i, const void *win,
                        float scale_re, float scale_im, void *y, unsigned *flag, unsigned seq, void *stream);

@@ -166,10 +166,12 @@ static void lq_fftf_exec_host(lq_fftf *q, const void *x, unsigned int n, void *y
     lq_mirror_commit(&q->hm, n);
 }
 
-static void lq_fftf_block(lq_fftf *q, const void *x, unsigned long long n, void *y)
+/* single: the call is fftfilt_*_execute (the reference's one n-sample block);
+ * the execute_block extension always runs on the GPU */
+static void lq_fftf_block(lq_fftf *q, const void *x, unsigned long long n, void *y, int single)
 {
     if (n == 0) return;
-    if (lq_small_host() && !q->direct && n * (unsigned long long)q->h_len <= LQ_FFTF_HOST_MACS) {
+    if (single && lq_small_host() && !q->direct && n * (unsigned long long)q->h_len <= LQ_FFTF_HOST_MACS) {
         lq_fftf_exec_host(q, x, (unsigned int)n, y);
         return;
     }
@@ -204,10 +206,10 @@ static void lq_fftf_block(lq_fftf *q, const void *x, unsigned long long n, void 
     }                                                                                               \
     unsigned int NAME##_get_length(NAME _q) { return _q->e->h_len; }                                \
     /* fftfilt.c:193-260: exactly n samples in and out */                                           \
-    void NAME##_execute(NAME _q, TI *_x, TO *_y) { lq_fftf_block(_q->e, _x, _q->e->n, _y); }          \
+    void NAME##_execute(NAME _q, TI *_x, TO *_y) { lq_fftf_block(_q->e, _x, _q->e->n, _y, 1); }       \
     void NAME##_execute_block(NAME _q, TI *_x, unsigned long long _n, TO *_y)                       \
     {                                                                                               \
-        lq_fftf_block(_q->e, _x, _n, _y);                                                           \
+        lq_fftf_block(_q->e, _x, _n, _y, 0);                                                        \
     }                                                                                               \
     void NAME##_execute_block_dev(NAME _q, const TI *_dx, unsigned long long _n, TO *_dy)           \
     {                                                                                               \

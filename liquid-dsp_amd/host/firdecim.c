@@ -146,10 +146,11 @@ static void lq_decim_exec1_host(lq_decim *q, const void *x, void *y)
     lq_mirror_commit(&q->hm, q->M);
 }
 
-static void lq_decim_block(lq_decim *q, const void *x, unsigned long long nout, void *y)
+/* single: the call is firdecim_*_execute; execute_block always runs on the GPU */
+static void lq_decim_block(lq_decim *q, const void *x, unsigned long long nout, void *y, int single)
 {
     if (nout == 0) return;
-    if (nout == 1 && lq_small_host()) {
+    if (single && lq_small_host()) {
         lq_decim_exec1_host(q, x, y);
         return;
     }
@@ -207,10 +208,10 @@ static void lq_decim_block(lq_decim *q, const void *x, unsigned long long nout, 
     }                                                                                               \
     void NAME##_print(NAME _q) { lq_decim_print(_q->e); }                                           \
     void NAME##_clear(NAME _q) { lq_decim_clear(_q->e); }                                           \
-    void NAME##_execute(NAME _q, TI *_x, TO *_y) { lq_decim_block(_q->e, _x, 1, _y); }              \
+    void NAME##_execute(NAME _q, TI *_x, TO *_y) { lq_decim_block(_q->e, _x, 1, _y, 1); }           \
     void NAME##_execute_block(NAME _q, TI *_x, unsigned int _n, TO *_y)                             \
     {                                                                                               \
-        lq_decim_block(_q->e, _x, _n, _y);                                                          \
+        lq_decim_block(_q->e, _x, _n, _y, 0);                                                       \
     }                                                                                               \
     void NAME##_execute_block_dev(NAME _q, const TI *_dx, unsigned long long _n, TO *_dy)           \
     {                                                                                               \
@@ -337,10 +338,11 @@ static void lq_interp_exec1_host(lq_interp *q, const void *x, void *y)
     lq_mirror_commit(&q->hm, 1);
 }
 
-static void lq_interp_block(lq_interp *q, const void *x, unsigned long long n, void *y)
+/* single: the call is firinterp_*_execute; execute_block always runs on the GPU */
+static void lq_interp_block(lq_interp *q, const void *x, unsigned long long n, void *y, int single)
 {
     if (n == 0) return;
-    if (n == 1 && lq_small_host()) {
+    if (single && lq_small_host()) {
         lq_interp_exec1_host(q, x, y);
         return;
     }
@@ -398,10 +400,10 @@ static void lq_interp_block(lq_interp *q, const void *x, unsigned long long n, v
     }                                                                                               \
     void NAME##_print(NAME _q) { lq_interp_print(_q->e); }                                          \
     void NAME##_reset(NAME _q) { lq_interp_reset(_q->e); }                                          \
-    void NAME##_execute(NAME _q, TI _x, TO *_y) { lq_interp_block(_q->e, &_x, 1, _y); }             \
+    void NAME##_execute(NAME _q, TI _x, TO *_y) { lq_interp_block(_q->e, &_x, 1, _y, 1); }          \
     void NAME##_execute_block(NAME _q, TI *_x, unsigned int _n, TO *_y)                             \
     {                                                                                               \
-        lq_interp_block(_q->e, _x, _n, _y);                                                         \
+        lq_interp_block(_q->e, _x, _n, _y, 0);                                                      \
     }                                                                                               \
     void NAME##_execute_block_dev(NAME _q, const TI *_dx, unsigned long long _n, TO *_dy)           \
     {                                                                                               \

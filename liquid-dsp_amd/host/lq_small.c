@@ -1,22 +1,22 @@
 /*
- * lq_small.c -- the opt-in host path for single-sample / single-vector calls.
+ * lq_small.c -- the host path for single-sample / single-vector calls.
  *
  * The per-call API (one sample, one dot product, one decimated output per
- * call: firfilt_*_push + _execute, dotprod_*_execute / _run, firdecim_*_execute,
- * firinterp_*_execute, resamp_*_execute, and fftfilt_*_execute on its short
- * n-sample block, n h_len <= 65536) is what unchanged liquid-dsp programs
- * call in their inner loops.  On the GPU each such call is a launch plus two
- * PCIe crossings (~10 us); the reference does it in 20-60 ns.
- * With the small-call mode set to host -- environment LQ_SMALL_CALLS=host, or
- * liquid_mi355x_set_small_calls(1) -- these calls compute their few outputs on
- * the host with the routines below, while every block call
- * (*_execute_block[_dev], the channelizers, fftfilt, ...) stays on the GPU.
- * The default is the GPU for every call.  The host routines are this
- * library's own (not the test oracle), follow the reference's definitions
- * (cited per routine) and keep the objects' state coherent with the GPU path
- * through host mirrors of the device histories (lq_mirror below), so a program
- * may mix per-sample and block calls on one object.  A GPU is still required:
- * objects cannot be created without one.
+ * call: firfilt_*_push + _execute, dotprod_*_execute / _run / _run4,
+ * firdecim_*_execute, firinterp_*_execute, resamp_*_execute, and
+ * fftfilt_*_execute on its short n-sample block, n h_len <= 65536) is what
+ * unchanged liquid-dsp programs call in their inner loops.  On the GPU each
+ * such call is a launch plus two PCIe crossings (~10 us); the
+ * reference does it in 20-60 ns.  So by default these entry points compute
+ * their few outputs on the host with the routines below, while every block
+ * call (*_execute_block[_dev], the channelizers, fftfilt_*_execute on longer
+ * blocks, FFT plans, spgram) runs on the GPU.  Environment LQ_SMALL_CALLS=gpu
+ * (or liquid_mi355x_set_small_calls(0)) sends every call to the GPU instead.
+ * The host routines are this library's own (not the test oracle), follow the
+ * reference's definitions (cited per routine) and keep the objects' state
+ * coherent with the GPU path through host mirrors of the device histories
+ * (lq_mirror below), so a program may mix per-sample and block calls on one
+ * object.  A GPU is still required: objects cannot be created without one.
  */
 #include <complex.h>
 
@@ -28,7 +28,7 @@ int lq_small_host(void)
 {
     if (g_small < 0) {
         const char *e = getenv("LQ_SMALL_CALLS");
-        g_small = (e && (strcmp(e, "host") == 0 || strcmp(e, "1") == 0)) ? 1 : 0;
+        g_small = (e && (strcmp(e, "gpu") == 0 || strcmp(e, "0") == 0)) ? 0 : 1;
     }
     return g_small;
 }

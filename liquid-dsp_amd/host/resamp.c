@@ -30,21 +30,39 @@
 #define RS_DIRECT_CHUNK (1ull << 24)   /* direct plans cover at most this many inputs */
 #define RS_DIRECT_AHEAD (1ull << 14)   /* ... and at least this many (built ahead for short calls) */
 #define RS_EARLY 4                     /* a cycle may start at any of the first RS_EARLY states */
+#define RS_HCK 16                      /* host checkpoints: one per RS_HCK inputs */
+#define RS_REC_CAP (1ull << 22)        /* device entries recorded during the period search (<= 64 MB) */
+#define RS_D4_MAXOUT (1ull << 26)      /* output plans cover at most this many outputs (128 MB of entries) */
 
 enum { RS_BOUNDARY = 0, RS_INTERP = 1 };
+enum { RS_D3 = 3, RS_D4 = 4 };        /* device plan: input checkpoints (k_resamp3) / output plan (k_resamp4) */
 
 typedef struct {
     float tau, mu;
     int b, st;
 } rs_state;
 
+/* a device table being recorded on the host (freed once uploaded) */
+typedef struct {
+    int kind;                     /* RS_D3 or RS_D4 */
+    int p2;                       /* RS_D3: lqk_rs_entry_p2 entries, else lqk_rs_entry */
+    unsigned char *buf;
+    size_t n, cap, esz, max;
+    int overflow;                 /* more than `max` entries were due */
+    int d4_ok;                    /* RS_D4: every input after the first output emitted one or two outputs */
+} rs_rec;
+
 typedef struct {
     int valid, periodic;
     rs_state origin;
-    lqk_rs_entry *tab;            /* host copy: checkpoint c = state at plan position c * LQK_RS_CK */
+    lqk_rs_entry *tab;            /* host: state at plan position c * RS_HCK (K lookups) */
     size_t nck, cap;
-    lq_devbuf d_tab;
     unsigned long long pre, P, Q, end;
+    int dk;                       /* device table kind (RS_D3 / RS_D4) */
+    rs_rec rec;                   /* its host copy until uploaded */
+    lq_devbuf d_tab;
+    unsigned long long d_n;       /* entries on the device */
+    unsigned long long opre, QT, PT;   /* RS_D4: outputs >= opre repeat every QT outputs / PT inputs */
 } rs_plan;
 
 struct lq_rs_s {
@@ -144,6 +162,15 @@ static int rs_pow2(unsigned int npfb) { return (npfb & (npfb - 1)) == 0; }
  * the full state, whose unsigned loop test stops a negative b (rs_step). */
 static int rs_p2(const lq_rs *q) { return rs_pow2(q->npfb) && q->del * (float)q->npfb >= 1.0f; }
 
+/* the output-plan kernel (k_resamp4): complex samples, tau-only timing,
+ * 1 < r < 2 (del in (0.5, 1)); the walk confirms one or two outputs per input */
+static int rs_d4_shape(const lq_rs *q)
+{
+    const char *e = getenv("LQ_RESAMP_INPUT_PLAN");   /* 1: always the input-checkpoint kernel (k_resamp3) */
+    if (e && strcmp(e, "1") == 0) return 0;
+    return q->kind != LQ_RRRF && rs_p2(q) && q->del > 0.5f && q->del < 1.0f && lqk_resamp4_supported(q->npfb, q->L);
+}
+
 static void rs_put(lqk_rs_entry *e, const rs_state *s, unsigned long long K)
 {
     e->tau = s->tau;
@@ -171,8 +198,59 @@ static void rs_plan_reserve(rs_plan *pl, size_t n)
     }
 }
 
-/* state and K at plan position g: the checkpoint at or before g, then the
- * remaining (< LQK_RS_CK) inputs stepped -- as k_resamp does on the GPU */
+/* ---- device-table recording */
+static void rs_rec_init(rs_rec *r, int kind, int p2, size_t max)
+{
+    free(r->buf);
+    memset(r, 0, sizeof(*r));
+    r->kind = kind;
+    r->p2 = p2;
+    r->esz = kind == RS_D4 ? sizeof(lqk_rs4_entry) : (p2 ? sizeof(lqk_rs_entry_p2) : sizeof(lqk_rs_entry));
+    r->max = max;
+    r->d4_ok = 1;
+}
+
+static void rs_rec_free(rs_rec *r)
+{
+    free(r->buf);
+    r->buf = NULL;
+    r->n = r->cap = 0;
+}
+
+static void *rs_rec_push(rs_rec *r)
+{
+    if (r->n >= r->max) {
+        r->overflow = 1;
+        return NULL;
+    }
+    if (r->n == r->cap) {
+        size_t c = r->cap ? r->cap * 2 : 4096;
+        unsigned char *b = (unsigned char *)lq_xmalloc(c * r->esz);
+        if (r->buf) memcpy(b, r->buf, r->n * r->esz);
+        free(r->buf);
+        r->buf = b;
+        r->cap = c;
+    }
+    return r->buf + (r->n++) * r->esz;
+}
+
+/* RS_D3 checkpoint before input i (i a multiple of LQK_RS_CK) */
+static void rs_rec3(rs_rec *r, const rs_state *s, float tau, unsigned long long K)
+{
+    if (r->p2) {
+        lqk_rs_entry_p2 *e = (lqk_rs_entry_p2 *)rs_rec_push(r);
+        if (e) {
+            e->tau = tau;
+            e->K = (unsigned int)K;
+        }
+    } else {
+        lqk_rs_entry *e = (lqk_rs_entry *)rs_rec_push(r);
+        if (e) rs_put(e, s, K);
+    }
+}
+
+/* state and K at plan position g: the host checkpoint at or before g, then
+ * the remaining (< RS_HCK) inputs stepped */
 static rs_state rs_plan_at(const rs_plan *pl, unsigned long long g, float del, unsigned int npfb,
                            unsigned long long *K)
 {
@@ -183,97 +261,73 @@ static rs_state rs_plan_at(const rs_plan *pl, unsigned long long g, float del, u
         j = pl->pre + (t - c * pl->P);
         add = c * pl->Q;
     }
-    const lqk_rs_entry *e = &pl->tab[j / LQK_RS_CK];
+    const lqk_rs_entry *e = &pl->tab[j / RS_HCK];
     rs_state s = rs_get(e);
     unsigned long long k = (unsigned long long)e->K + add;
-    for (unsigned long long i = j & ~(unsigned long long)(LQK_RS_CK - 1); i < j; i++) k += rs_step(&s, del, npfb);
+    for (unsigned long long i = j & ~(unsigned long long)(RS_HCK - 1); i < j; i++) k += rs_step(&s, del, npfb);
     *K = k;
     return s;
 }
 
 static void rs_plan_upload(lq_rs *q)
 {
-    if (rs_p2(q)) {                  /* (tau, K): 8 B per LQK_RS_CK inputs */
-        size_t bytes = q->pl.nck * sizeof(lqk_rs_entry_p2);
-        lqk_rs_entry_p2 *t = (lqk_rs_entry_p2 *)lq_xmalloc(bytes);
-        for (size_t c = 0; c < q->pl.nck; c++) {
-            t[c].tau = q->pl.tab[c].tau;
-            t[c].K = q->pl.tab[c].K;
-        }
-        void *d = lq_devbuf_get(&q->pl.d_tab, bytes);
-        lqrt_h2d(d, t, bytes, q->ctx.stream);
-        lqrt_sync(q->ctx.stream);
-        free(t);
-        return;
-    }
-    size_t bytes = q->pl.nck * sizeof(lqk_rs_entry);
-    void *d = lq_devbuf_get(&q->pl.d_tab, bytes);
-    lqrt_h2d(d, q->pl.tab, bytes, q->ctx.stream);
+    rs_rec *r = &q->pl.rec;
+    size_t bytes = r->n * r->esz;
+    void *d = lq_devbuf_get(&q->pl.d_tab, bytes ? bytes : 8);
+    if (bytes) lqrt_h2d(d, r->buf, bytes, q->ctx.stream);
     lqrt_sync(q->ctx.stream);
+    q->pl.d_n = r->n;
+    rs_rec_free(r);
 }
 
-/* walk n inputs from x0 recording a checkpoint every LQK_RS_CK of them (from
- * the plan's first); with `early` set, stop as soon as the state returns to one
- * of the first RS_EARLY states (a cycle without a pre-period beyond them):
- * returns the position of the return (or n), *q0 the state index it returned to */
+/* walk n inputs from x0, recording a host checkpoint every RS_HCK inputs
+ * (from the plan's first) and, with rec, the device table: RS_D3 a
+ * checkpoint every LQK_RS_CK inputs, RS_D4 the (tau, input) of every fourth
+ * output.  With `early` set, stop as soon as the state returns to one of the
+ * first RS_EARLY states (a cycle without a pre-period beyond them) or meets
+ * Brent's tortoise: returns the position of the return (or n), *q0 the state
+ * index it returned to (RS_BRENT: a cycle of length *lam_out) */
 #define RS_BRENT (~1ull)
 
 static unsigned long long rs_walk(lq_rs *q, rs_state x0, unsigned long long n, int early, unsigned long long *q0,
-                                  unsigned long long *Kend, unsigned long long *lam_out)
+                                  unsigned long long *Kend, unsigned long long *lam_out, rs_rec *rec)
 {
     rs_plan *pl = &q->pl;
-    const unsigned long long CK = LQK_RS_CK;
     pl->nck = 0;
     unsigned long long K = 0, i = 0;
+    const int r3 = rec && rec->kind == RS_D3, r4 = rec && rec->kind == RS_D4;
     if (rs_p2(q)) {
-        /* the hot loop: runs of steps between checkpoints; with `early`, the
-         * first RS_EARLY states are compared with each other, and every later
-         * state (branch-free) with the first and with Brent's tortoise, the
-         * state at position 2^k - 1: a pure cycle ends the walk on its first
-         * return, any other once the tortoise sits on the cycle (r = 1.037:
-         * 1 011 163 steps, ~3 ms) */
+        /* every state is compared (branch-free) with the first and with
+         * Brent's tortoise, the state at position 2^k - 1 (and the first
+         * RS_EARLY states with each other): a pure cycle ends the walk on its
+         * first return, any other once the tortoise sits on the cycle
+         * (r = 1.037: 1 011 163 steps, ~3 ms) */
         const float del = q->del, z = 1.0f - 1.0f / (float)q->npfb;
         float t = x0.tau;
         unsigned int eb[RS_EARLY], tort;
         unsigned long long tpos = 0, reset = 1;
         for (int k = 0; k < RS_EARLY; k++) eb[k] = 0x7fc00001u;
         memcpy(&tort, &t, 4);
-        for (;;) {
-            if ((i & (CK - 1)) == 0) {
+        for (;; i++) {
+            if ((i & (RS_HCK - 1)) == 0) {
                 rs_plan_reserve(pl, pl->nck + 1);
                 rs_state s = i == 0 ? x0 : rs_from_tau(t, q->npfb);
                 rs_put(&pl->tab[pl->nck++], &s, K);
             }
+            if (r3 && (i & (LQK_RS_CK - 1)) == 0) rs_rec3(rec, NULL, t, K);
             if (K > 0xffffffffull || i == n) break;
-            unsigned long long stop = (n - i) < CK - (i & (CK - 1)) ? n : (i | (CK - 1)) + 1;
-            if (!early) {
-                for (; i < stop; i++) K += rs_step_p2(&t, del, z);
-                continue;
-            }
-            if (i < RS_EARLY) {                     /* position i: compare, record, step */
+            if (early) {
                 unsigned int tb;
                 memcpy(&tb, &t, 4);
-                for (unsigned long long k = 0; k < i; k++)
-                    if (eb[k] == tb) {
-                        *q0 = k;
-                        *Kend = K;
-                        return i;
-                    }
-                eb[i] = tb;
-                if (i == reset) {
-                    tort = eb[i];
-                    tpos = i;
-                    reset = 2 * i + 1;
-                }
-                K += rs_step_p2(&t, del, z);
-                i++;
-                continue;
-            }
-            if (stop > reset + 1) stop = reset + 1;
-            for (; i < stop; i++) {
-                unsigned int tb;
-                memcpy(&tb, &t, 4);
-                if ((tb == eb[0]) | (tb == tort)) {
+                if (i < RS_EARLY) {
+                    for (unsigned long long k = 0; k < i; k++)
+                        if (eb[k] == tb) {
+                            *q0 = k;
+                            *Kend = K;
+                            return i;
+                        }
+                    eb[i] = tb;
+                } else if ((tb == eb[0]) | (tb == tort)) {
                     for (int k = RS_EARLY - 1; k >= 0; k--)
                         if (eb[k] == tb) {
                             *q0 = (unsigned long long)k;
@@ -290,19 +344,39 @@ static unsigned long long rs_walk(lq_rs *q, rs_state x0, unsigned long long n, i
                     tpos = i;
                     reset = 2 * i + 1;
                 }
+            }
+            if (r4) {   /* the output plan: (tau, input) at every fourth output */
+                float x = t;
+                unsigned int c = 0;
+                while (x < z) {
+                    if ((K & 3) == 0) {
+                        lqk_rs4_entry *e = (lqk_rs4_entry *)rs_rec_push(rec);
+                        if (e) {
+                            e->tau = x;
+                            e->i = (unsigned int)i;
+                        }
+                    }
+                    x += del;
+                    K++;
+                    c++;
+                }
+                t = x - 1.0f;
+                if (c > 2 || (c == 0 && K > 0) || i > 0xffffffffull) rec->d4_ok = 0;
+            } else {
                 K += rs_step_p2(&t, del, z);
             }
         }
     } else {
         rs_state s = x0, e[RS_EARLY];
         int ne = 0;
+        if (r4) rec->d4_ok = 0;
         for (;;) {
-            if ((i & (CK - 1)) == 0) {
+            if ((i & (RS_HCK - 1)) == 0) {
                 rs_plan_reserve(pl, pl->nck + 1);
                 rs_put(&pl->tab[pl->nck++], &s, K);
-                if (K > 0xffffffffull) break;
             }
-            if (i == n) break;
+            if (r3 && (i & (LQK_RS_CK - 1)) == 0) rs_rec3(rec, &s, s.tau, K);
+            if (K > 0xffffffffull || i == n) break;
             if (early) {
                 for (int k = 0; k < ne; k++)
                     if (rs_eq(&e[k], &s)) {
@@ -334,6 +408,64 @@ static unsigned long long rs_K_lin(lq_rs *q, unsigned long long g)
     return K;
 }
 
+/* a walk of n inputs from the plan's origin that records the device table
+ * (at most max entries; the host checkpoints it rewrites are the ones
+ * recorded before, same origin); 0 if the walk or the one-or-two-outputs
+ * check of an output plan fails */
+static int rs_rec_walk(lq_rs *q, unsigned long long n, int kind, size_t max)
+{
+    unsigned long long q0, Kend, lam;
+    rs_rec_init(&q->pl.rec, kind, rs_p2(q), max);
+    if (rs_walk(q, q->pl.origin, n, 0, &q0, &Kend, &lam, &q->pl.rec) != n) return 0;
+    return kind != RS_D4 || q->pl.rec.d4_ok;
+}
+
+/* the device table of a plan whose host part (origin, pre, P, Q or end) is
+ * built; `have` = the search walk's recording already holds it */
+static int rs_plan_device(lq_rs *q, int have)
+{
+    rs_plan *pl = &q->pl;
+    const int d4 = pl->rec.kind == RS_D4 && pl->rec.d4_ok;
+    if (pl->rec.kind == RS_D4 && d4) {
+        if (pl->periodic) {
+            /* outputs >= opre repeat every QT = mQ outputs (mP inputs): opre and
+             * QT multiples of 4 (a tile's lanes all skip k0 mod 4 outputs from
+             * their entries) and QT >= 256 (a 256-output tile wraps at most once) */
+            const unsigned long long Kpre = rs_K_lin(q, pl->pre), Q = pl->Q;
+            unsigned long long m = 1;
+            while ((m * Q) % 4 != 0 || m * Q < 256) m++;
+            pl->opre = (Kpre + 3) & ~3ull;
+            pl->QT = m * Q;
+            pl->PT = m * pl->P;
+            const unsigned long long need = (pl->opre + pl->QT) / 4;
+            if (Q > 0 && need <= RS_D4_MAXOUT / 4) {
+                if (!(have && pl->rec.n >= need))
+                    if (!rs_rec_walk(q, pl->pre + (m + 1) * pl->P + 4, RS_D4, (size_t)need)) goto d3;
+                if (pl->rec.n >= need) {
+                    pl->rec.n = need;
+                    pl->dk = RS_D4;
+                    return 1;
+                }
+            }
+        } else if (have && !pl->rec.overflow) {
+            pl->opre = ~0ull;
+            pl->QT = pl->PT = 0;
+            pl->dk = RS_D4;
+            return 1;
+        }
+    }
+d3:
+    {
+        const unsigned long long n = pl->periodic ? pl->pre + pl->P : pl->end;
+        const size_t need = (size_t)(n / LQK_RS_CK + 1);
+        if (!(have && pl->rec.kind == RS_D3 && pl->rec.n >= need))
+            if (!rs_rec_walk(q, n, RS_D3, need) || pl->rec.n < need) return 0;
+        pl->rec.n = need;
+        pl->dk = RS_D3;
+        return 1;
+    }
+}
+
 /* Periodic plan from q->now.  The timing state visits a finite set, so the
  * walk is eventually periodic; usually the orbit returns to one of its first
  * states (r = 1.037: to the initial state after 1 011 163 inputs), found in
@@ -343,8 +475,10 @@ static int rs_plan_build_periodic(lq_rs *q)
 {
     const rs_state x0 = q->now;
     unsigned long long q0, Kend, lam = 0;
-    unsigned long long n = rs_walk(q, x0, RS_MAX_PERIOD + RS_EARLY, 1, &q0, &Kend, &lam);
+    rs_rec_init(&q->pl.rec, rs_d4_shape(q) ? RS_D4 : RS_D3, rs_p2(q), RS_REC_CAP);
+    unsigned long long n = rs_walk(q, x0, RS_MAX_PERIOD + RS_EARLY, 1, &q0, &Kend, &lam, &q->pl.rec);
     unsigned long long pre, P;
+    int have = 1;
     if (q0 != ~0ull && q0 != RS_BRENT) {
         pre = q0;
         P = n - q0;
@@ -357,7 +491,7 @@ static int rs_plan_build_periodic(lq_rs *q)
             rs_step(&hare, q->del, q->npfb);
             while (!rs_eq(&tort, &hare)) {
                 if (power == lam) {
-                    if (power > RS_MAX_PERIOD) return 0;
+                    if (power > RS_MAX_PERIOD) goto fail;
                     tort = hare;
                     power *= 2;
                     lam = 0;
@@ -373,7 +507,7 @@ static int rs_plan_build_periodic(lq_rs *q)
             float a = x0.tau, h = x0.tau;
             for (unsigned long long i = 0; i < lam; i++) rs_step_p2(&h, q->del, z);
             while (memcmp(&a, &h, 4) != 0) {
-                if (mu > RS_MAX_PERIOD) return 0;
+                if (mu > RS_MAX_PERIOD) goto fail;
                 rs_step_p2(&a, q->del, z);
                 rs_step_p2(&h, q->del, z);
                 mu++;
@@ -382,7 +516,7 @@ static int rs_plan_build_periodic(lq_rs *q)
             rs_state tort = x0, hare = x0;
             for (unsigned long long i = 0; i < lam; i++) rs_step(&hare, q->del, q->npfb);
             while (!rs_eq(&tort, &hare)) {
-                if (mu > RS_MAX_PERIOD) return 0;
+                if (mu > RS_MAX_PERIOD) goto fail;
                 rs_step(&tort, q->del, q->npfb);
                 rs_step(&hare, q->del, q->npfb);
                 mu++;
@@ -390,7 +524,10 @@ static int rs_plan_build_periodic(lq_rs *q)
         }
         pre = mu;
         P = lam;
-        if (!recorded && rs_walk(q, x0, pre + P, 0, &q0, &Kend, &lam) != pre + P) return 0;
+        if (!recorded) {
+            rs_rec_init(&q->pl.rec, q->pl.rec.kind, rs_p2(q), RS_REC_CAP);
+            if (rs_walk(q, x0, pre + P, 0, &q0, &Kend, &lam, &q->pl.rec) != pre + P) goto fail;
+        }
     }
     q->pl.pre = pre;
     q->pl.P = P;
@@ -398,9 +535,13 @@ static int rs_plan_build_periodic(lq_rs *q)
     q->pl.Q = rs_K_lin(q, pre + P) - rs_K_lin(q, pre);
     q->pl.origin = x0;
     q->pl.periodic = 1;
+    if (!rs_plan_device(q, have)) goto fail;
     q->pl.valid = 1;
     q->gpos = 0;
     return 1;
+fail:
+    rs_rec_free(&q->pl.rec);
+    return 0;
 }
 
 /* plan covering exactly the next nx inputs (nx <= RS_DIRECT_CHUNK) */
@@ -408,7 +549,8 @@ static void rs_plan_build_direct(lq_rs *q, unsigned long long nx)
 {
     unsigned long long q0, Kend;
     unsigned long long lam;
-    if (rs_walk(q, q->now, nx, 0, &q0, &Kend, &lam) != nx || Kend > 0xffffffffull)
+    rs_rec_init(&q->pl.rec, rs_d4_shape(q) ? RS_D4 : RS_D3, rs_p2(q), (size_t)-1);
+    if (rs_walk(q, q->now, nx, 0, &q0, &Kend, &lam, &q->pl.rec) != nx || Kend > 0xffffffffull)
         LQ_FAIL("error: resamp_%s: too many outputs for one call\n", lq_ext[q->kind]);
     q->pl.pre = nx + 1;
     q->pl.P = 1;
@@ -416,6 +558,7 @@ static void rs_plan_build_direct(lq_rs *q, unsigned long long nx)
     q->pl.end = nx;
     q->pl.origin = q->now;
     q->pl.periodic = 0;
+    if (!rs_plan_device(q, 1)) LQ_FAIL("error: resamp_%s: timing plan\n", lq_ext[q->kind]);
     q->pl.valid = 1;
     q->gpos = 0;
 }
@@ -558,6 +701,7 @@ void lq_rs_destroy(lq_rs *_q)
     lq_mirror_free(&_q->hm);
     free(_q->hbank);
     free(_q->pl.tab);
+    rs_rec_free(&_q->pl.rec);
     free(_q);
 }
 
@@ -652,10 +796,16 @@ void lq_rs_block_dev(lq_rs *_q, const void *_dxv, unsigned long long _nx, void *
     while (_nx > 0) {
         unsigned long long c = rs_ensure_plan(_q, _nx < cmax ? _nx : cmax);
         unsigned long long K0 = rs_K(_q, _q->gpos), K1 = rs_K(_q, _q->gpos + c);
-        lqk_rs_plan kp = {_q->pl.d_tab.p, _q->pl.pre, _q->pl.P, _q->pl.Q, _q->pl.end, rs_p2(_q)};
         void *hold = _q->d_hist[_q->cur], *hnew = _q->d_hist[_q->cur ^ 1];
-        lqk_resamp(_q->kind == LQ_RRRF, &kp, _q->gpos, K0, _q->npfb, _q->L, _q->del, _q->d_taps, _q->d_taps2, hold, _dx, c,
-                   _dy, K1 - K0, _q->ctx.stream);
+        if (_q->pl.dk == RS_D4) {
+            lqk_rs4_plan kp = {_q->pl.d_tab.p, _q->pl.d_n, _q->pl.opre, _q->pl.QT, _q->pl.PT};
+            lqk_resamp4(&kp, _q->gpos, K0, _q->npfb, _q->L, _q->del, _q->d_taps2, hold, _dx, c, _dy, K1 - K0,
+                        _q->ctx.stream);
+        } else {
+            lqk_rs_plan kp = {_q->pl.d_tab.p, _q->pl.pre, _q->pl.P, _q->pl.Q, _q->pl.end, rs_p2(_q)};
+            lqk_resamp(_q->kind == LQ_RRRF, &kp, _q->gpos, K0, _q->npfb, _q->L, _q->del, _q->d_taps, _q->d_taps2,
+                       hold, _dx, c, _dy, K1 - K0, _q->ctx.stream);
+        }
         lqk_window_append(_q->kind != LQ_RRRF, hold, _q->L, _dx, c, hnew, _q->ctx.stream);
         _q->cur ^= 1;
         _q->gpos += c;
@@ -726,13 +876,14 @@ static void lq_rs_exec1_host(lq_rs *q, const void *x, void *y, unsigned int *ny)
     *ny = n;
 }
 
-static void lq_rs_block(lq_rs *_q, const void *_x, unsigned int _nx, void *_y, unsigned int *_ny)
+/* single: the call is resamp_*_execute (one input); execute_block always runs on the GPU */
+static void lq_rs_block(lq_rs *_q, const void *_x, unsigned int _nx, void *_y, unsigned int *_ny, int single)
 {
     if (_nx == 0) {
         *_ny = 0;
         return;
     }
-    if (_nx == 1 && lq_small_host()) {
+    if (single && lq_small_host()) {
         lq_rs_exec1_host(_q, _x, _y, _ny);
         return;
     }
@@ -786,11 +937,11 @@ lq_ctx *lq_rs_ctx(lq_rs *q) { return &q->ctx; }
     }                                                                                               \
     void NAME##_execute_block(NAME _q, T *_x, unsigned int _nx, T *_y, unsigned int *_ny)           \
     {                                                                                               \
-        lq_rs_block(_q->e, _x, _nx, _y, _ny);                                                       \
+        lq_rs_block(_q->e, _x, _nx, _y, _ny, 0);                                                    \
     }                                                                                               \
     void NAME##_execute(NAME _q, T _x, T *_y, unsigned int *_num_written)                           \
     {                                                                                               \
-        lq_rs_block(_q->e, &_x, 1, _y, _num_written);                                               \
+        lq_rs_block(_q->e, &_x, 1, _y, _num_written, 1);                                            \
     }                                                                                               \
     void NAME##_set_stream(NAME _q, void *_s) { lq_ctx_set_stream(&_q->e->ctx, _s); }               \
     void NAME##_synchronize(NAME _q) { lqrt_sync(_q->e->ctx.stream); }
@@ -824,6 +975,7 @@ long long liquid_mi355x_resamp_schedule(float _rate, unsigned int _npfb, unsigne
     } else {
         rs_plan_build_direct(&q, _nx);
     }
+    rs_rec_free(&q.pl.rec);
     if (_pre) *_pre = q.pl.pre;
     if (_period) *_period = q.pl.P;
     unsigned long long k = 0;
@@ -852,4 +1004,74 @@ long long liquid_mi355x_resamp_schedule(float _rate, unsigned int _npfb, unsigne
     }
     free(q.pl.tab);
     return (long long)k;
+}
+
+/* Host-only check of the output plan (no GPU): builds the plan a complex
+ * resampler with 2m = 14 taps per bank would use from the initial state
+ * (periodic if `periodic`, else direct over nx inputs) and, when it is an
+ * output plan (k_resamp4), expands every output exactly as k_resamp4 does:
+ * the entry of output k & ~3 (periods unwrapped), k & 3 steps, then bank
+ * (-1: BOUNDARY), mu and input index.  Returns the number of outputs of the
+ * first nx inputs, -1 if no plan, -3 if the plan is not an output plan. */
+long long liquid_mi355x_resamp_schedule4(float _rate, unsigned int _npfb, unsigned long long _nx, int _periodic,
+                                         int *_b, float *_mu, unsigned int *_idx, unsigned long long _cap,
+                                         unsigned long long *_pre, unsigned long long *_period)
+{
+    lq_rs q;
+    memset(&q, 0, sizeof(q));
+    q.kind = LQ_CRCF;
+    q.rate = _rate;
+    q.del = 1.0f / _rate;
+    q.npfb = _npfb;
+    q.L = 14;
+    q.now = rs_initial;
+    if (_periodic) {
+        if (!rs_plan_build_periodic(&q)) {
+            free(q.pl.tab);
+            return -1;
+        }
+    } else {
+        rs_plan_build_direct(&q, _nx);
+    }
+    if (q.pl.dk != RS_D4) {
+        rs_rec_free(&q.pl.rec);
+        free(q.pl.tab);
+        return -3;
+    }
+    if (_pre) *_pre = q.pl.opre;
+    if (_period) *_period = q.pl.QT;
+    unsigned long long Kn;
+    rs_plan_at(&q.pl, _nx, q.del, q.npfb, &Kn);
+    const lqk_rs4_entry *t = (const lqk_rs4_entry *)q.pl.rec.buf;
+    const float z = 1.0f - 1.0f / (float)_npfb, fn = (float)_npfb;
+    long long ret = (long long)Kn;
+    for (unsigned long long k = 0; k < Kn && k < _cap; k++) {
+        const unsigned long long kb = k & ~3ull;
+        unsigned long long idx = kb >> 2, add = 0;
+        if (kb >= q.pl.opre) {
+            const unsigned long long dt = kb - q.pl.opre, c = dt / q.pl.QT;
+            idx = (q.pl.opre + (dt - c * q.pl.QT)) >> 2;
+            add = c * q.pl.PT;
+        }
+        if (idx >= q.pl.rec.n) {
+            ret = -2;
+            break;
+        }
+        float tau = t[idx].tau;
+        unsigned long long i = t[idx].i + add;
+        for (unsigned s = 0; s < (unsigned)(k & 3); s++) {
+            tau = tau + q.del;
+            if (!(tau < z)) {
+                tau = tau - 1.0f;
+                i++;
+            }
+        }
+        const float bf = tau * fn, fb = floorf(bf);
+        _b[k] = tau < 0.0f ? -1 : (int)fb;
+        _mu[k] = bf - fb;
+        _idx[k] = (unsigned int)i;
+    }
+    rs_rec_free(&q.pl.rec);
+    free(q.pl.tab);
+    return ret;
 }

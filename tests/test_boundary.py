@@ -10,6 +10,7 @@ No compute call is made here (no GPU in the build container).
 import ctypes as C
 import os
 import subprocess
+import sys
 
 import pytest
 
@@ -99,3 +100,19 @@ def test_liquid_msb_index_known_answers():
         assert f(1 << k) == k + 1
     for x, b in ((3, 2), (126, 7), (127, 7), (128, 8), (129, 8), (253, 8), (255, 8), (0xFFFFFFFF, 32)):
         assert f(x) == b
+
+
+@pytest.mark.parametrize("env,expect", [(None, 1), ("gpu", 0), ("0", 0), ("host", 1)])
+def test_small_call_mode_default(env, expect):
+    """Single-sample calls run on the host unless LQ_SMALL_CALLS=gpu (or 0):
+    the mode the library reads at load, in a fresh process (no GPU needed)."""
+    code = ("import ctypes,sys; L=ctypes.CDLL(sys.argv[1]); "
+            "print(L.liquid_mi355x_get_small_calls())")
+    e = dict(os.environ)
+    e.pop("LQ_SMALL_CALLS", None)
+    if env is not None:
+        e["LQ_SMALL_CALLS"] = env
+    out = subprocess.run([sys.executable, "-c", code, LQ.LIB_PATH], capture_output=True, text=True, env=e,
+                         timeout=60)
+    assert out.returncode == 0, out.stderr
+    assert int(out.stdout.strip()) == expect

@@ -1059,12 +1059,13 @@ REF_EX = os.path.join(LQ.ROOT, "build", "ref_examples")
 @pytest.mark.parametrize("small_calls", ["gpu", "host"])
 def test_reference_examples_run(exe, small_calls, tmp_path):
     """liquid-dsp's own example programs, compiled unchanged against the
-    drop-in header, run to completion on the GPU (they write .m files); and
-    again with the opt-in host path for single-sample calls (LQ_SMALL_CALLS)."""
+    drop-in header, run to completion with every call on the GPU
+    (LQ_SMALL_CALLS=gpu), and in the library's default mode (single-sample
+    calls on the host, block calls on the GPU)."""
     env = dict(os.environ)
     env.pop("LQ_SMALL_CALLS", None)
-    if small_calls == "host":
-        env["LQ_SMALL_CALLS"] = "host"
+    if small_calls == "gpu":
+        env["LQ_SMALL_CALLS"] = "gpu"
     res = subprocess.run([os.path.join(REF_EX, exe)], capture_output=True, text=True, timeout=120, cwd=tmp_path,
                          env=env)
     print(res.stdout[-2000:], res.stderr[-2000:])

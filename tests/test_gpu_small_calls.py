@@ -1,6 +1,6 @@
-"""The opt-in small-call mode (LQ_SMALL_CALLS=host, liquid_mi355x_set_small_calls):
-single-sample calls computed on the host by host/lq_small.c, block calls on
-the GPU.  Same bar as the GPU path: the reference's golden vectors at their
+"""The small-call mode (the library's default; LQ_SMALL_CALLS=gpu or
+liquid_mi355x_set_small_calls(0) turns it off): single-sample calls computed
+on the host by host/lq_small.c, block calls on the GPU.  Same bar as the GPU path: the reference's golden vectors at their
 tolerances, and normwise 1e-5 against the oracle over streams that mix
 per-sample (host) and block (GPU) calls on one object, so the history
 mirrors and the resampler's timing state are exercised in both directions."""

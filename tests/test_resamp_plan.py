@@ -106,3 +106,56 @@ def test_rate_above_npfb_stops():
     assert len(ob) < 2 * rate and oidx.max() <= 1
     b, _, idx, _, _ = _lib_schedule(rate, 64, 1000, 0)
     assert len(b) == len(ob)
+
+
+# ---------------------------------------------------------------- output plans (k_resamp4)
+def _lib_schedule4(rate, npfb, nx, periodic):
+    L = LM.lib()
+    fn = L.liquid_mi355x_resamp_schedule4
+    fn.restype = C.c_longlong
+    fn.argtypes = [C.c_float, C.c_uint, C.c_ulonglong, C.c_int, C.c_void_p, C.c_void_p, C.c_void_p,
+                   C.c_ulonglong, C.POINTER(C.c_ulonglong), C.POINTER(C.c_ulonglong)]
+    cap = int(np.ceil(nx * rate)) + 16
+    b = np.zeros(cap, np.int32)
+    mu = np.zeros(cap, np.float32)
+    idx = np.zeros(cap, np.uint32)
+    pre, per = C.c_ulonglong(0), C.c_ulonglong(0)
+    k = fn(rate, npfb, nx, periodic, LM.ptr(b), LM.ptr(mu), LM.ptr(idx), cap, C.byref(pre), C.byref(per))
+    return k, b[:max(k, 0)], mu[:max(k, 0)], idx[:max(k, 0)], pre.value, per.value
+
+
+@pytest.mark.parametrize("rate,npfb,nx", [
+    (1.037, 64, 2_200_000),      # config 5: period 2^20 outputs, crossed twice
+    (1.27115323, 64, 400_000),   # autotest_resamp_crcf's rate: period 2^23 outputs
+    (1.5, 64, 20_000),           # period 3 outputs: the table repeats 256 outputs
+    (1.9, 64, 300_000),
+    (1.0001, 64, 300_000),
+    (1.3, 32, 300_000),
+    (1.7, 256, 300_000),
+])
+@pytest.mark.parametrize("periodic", [1, 0])
+def test_output_plan_matches_oracle_schedule(rate, npfb, nx, periodic):
+    """the output plan that k_resamp4 replays (an entry every fourth output,
+    then up to three straight-line steps) reproduces the reference's float32
+    schedule bit for bit: bank (BOUNDARY = -1), mu and input of every output"""
+    rate = float(np.float32(rate))
+    if not periodic:
+        nx = min(nx, 200_000)
+    k, b, mu, idx, pre, per = _lib_schedule4(rate, npfb, nx, periodic)
+    if periodic and k == -1:
+        pytest.skip("no period within the search limit")
+    assert k >= 0, "output plan not built (%d)" % k
+    if periodic:
+        assert pre % 4 == 0 and per % 4 == 0 and per >= 256
+    ob, omu, oidx = O.resamp_schedule(rate, npfb, nx)
+    assert len(b) == len(ob)
+    np.testing.assert_array_equal(b, ob)
+    np.testing.assert_array_equal(mu.view(np.uint32), omu.view(np.uint32))
+    np.testing.assert_array_equal(idx, oidx)
+
+
+@pytest.mark.parametrize("rate", [0.97, 2.5, 3.7])
+def test_output_plan_only_between_one_and_two(rate):
+    """rates outside (1, 2) keep the input-checkpoint plan (k_resamp3)"""
+    k, *_ = _lib_schedule4(float(np.float32(rate)), 64, 10_000, 0)
+    assert k == -3
