@@ -7,7 +7,8 @@ TAG=${1:-prof}
 export TMPDIR=/tmp
 OUT=gpurun_out/$TAG; rm -rf $OUT; mkdir -p $OUT
 python -c "import __graft_entry__ as g; g.build()" > $OUT/build.log 2>&1 || exit 1
-timeout -k 10 600 rocprofv3 --kernel-trace --stats -d $OUT/trace -o run --output-format csv -- python3 bench.py --steps 50 --warmup 20 --no-cpu-baseline > $OUT/bench_under_rocprof.log 2>&1 || { tail -20 $OUT/bench_under_rocprof.log; exit 1; }
+# the driver's command (--steps 20 --warmup 5; bench.py adds its warm-up floor)
+timeout -k 10 600 rocprofv3 --kernel-trace --stats -d $OUT/trace -o run --output-format csv -- python3 bench.py --steps 20 --warmup 5 --no-cpu-baseline --no-percall > $OUT/bench_under_rocprof.log 2>&1 || { tail -20 $OUT/bench_under_rocprof.log; exit 1; }
 for C in FETCH_SIZE WRITE_SIZE; do
   timeout -k 10 300 rocprofv3 --pmc $C --output-format csv -d $OUT/$C -o run -- python3 tools/prof_run.py --what all --iters 2 > $OUT/$C.log 2>&1 || { tail -5 $OUT/$C.log; exit 1; }
 done
@@ -39,8 +40,8 @@ json.dump({"firpfbch2_bytes_per_launch": traffic.get("firpfbch2", {}).get("total
            "fftfilt_bytes_per_launch": traffic.get("fftfilt", {}).get("total_bytes"),
            "detail": traffic,
            "launch_shapes": {"firpfbch2": "M=1024 m=4, 2^27 input samples", "firfilt": "h=64, 2^28 samples",
-                             "resamp": "r=1.037 m=7 npfb=64, 2^25 input samples (8-byte loads: the x2 FETCH "
-                                       "correction is calibrated for 16-byte streams only)",
+                             "resamp": "r=1.037 m=7 npfb=64, 2^25 input samples (k_resamp4: 8-byte loads, "
+                                       "16-byte stores; the x2 FETCH correction is calibrated for 16-byte streams)",
                              "fftfilt": "h=512, 4096-point overlap-save, 2^26 samples"},
            "method": "rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE in separate passes over tools/prof_run.py; "
                      "FETCH_SIZE doubled per the gfx950 correction",
@@ -49,8 +50,8 @@ json.dump({"firpfbch2_bytes_per_launch": traffic.get("firpfbch2", {}).get("total
 print(json.dumps(traffic))
 PY
 find $OUT/trace -name "*kernel_stats.csv" -exec cp {} $OUT/kernel_stats.csv \;
-# the bench's timed window: the last 50 dispatches of each hot kernel (the
-# 20 warm-up dispatches before them are in kernel_stats.csv's average)
+# the bench's timed window: the last 20 dispatches of each hot kernel (the
+# warm-up dispatches before them are in kernel_stats.csv's average)
 python3 - $OUT <<'PY'
 import csv, glob, json, os, sys, collections
 out = sys.argv[1]
@@ -62,10 +63,10 @@ res = {}
 for k, v in d.items():
     key = "firpfbch2" if "pfb2" in k else ("firfilt" if ("k_firfilt<" in k or "k_firfilt_mx" in k) else
                                            ("resamp" if "k_resamp" in k else ("fftfilt" if "k_fftfilt" in k else None)))
-    if not key or len(v) < 50:
+    if not key or len(v) < 20:
         continue
     v.sort()
-    last = [e - s for s, e in v[-50:]]
+    last = [e - s for s, e in v[-20:]]
     res[key] = {"kernel": k[:120], "dispatches": len(v), "timed_window_avg_us": sum(last) / len(last) / 1e3,
                 "timed_window_min_us": min(last) / 1e3, "timed_window_max_us": max(last) / 1e3,
                 "all_avg_us": sum(e - s for s, e in v) / len(v) / 1e3}
