@@ -338,227 +338,6 @@ __global__ __launch_bounds__(NT, 1) void k_pfb2_an1024(Params P, const float *__
     }
 }
 
-// ---------------------------------------------------------------- two workgroups per CU
-// k_pfb2_an1024w: the same analyzer as two 8-wave workgroups per CU
-// (r05 pattern sweep, profiles/r05d_mb_pat12.txt: the bare 1 read : 2 write
-// pattern ran 0.628 ms as one 16-wave workgroup per CU -- the kernel's form
-// -- and 0.578 ms as two 8-wave workgroups per CU with the next tile's loads
-// issued between the stores).
-//  * Lane t owns columns 2t and 2t+1 (both lo for t < 256, both hi above):
-//    one 16-byte load per row, taps held as float4s.
-//  * A group is 4 rows = 8 blocks; block b0 + i lives in LDS buffer i (no
-//    ring rotation); the hi half of the next group's first block (the last
-//    row's second product on the hi lanes) waits in registers and is written
-//    at the next group's start, so 8 buffers + the twiddle tables fit 78 KB.
-//  * Wave w transforms block b0 + w (the register 16 x 16 x 4 transform of
-//    k_pfb2_an1024); ILV: the next group's rows are loaded between the
-//    stores (else right after the dot phase).
-//  * The row ring (8 rows per column) keeps compile-time slots: the group
-//    loop runs two groups per iteration (ring slots 0-3, then 4-7); the
-//    workgroups' group ranges start on even groups.
-constexpr int NT2 = 512;
-constexpr int NBUF2 = 8;
-
-template <int L, bool ILV>
-__global__ __launch_bounds__(NT2) __attribute__((amdgpu_waves_per_eu(4, 4))) void k_pfb2_an1024w(Params P, const float *__restrict__ hsub,
-                                                         const float2 *__restrict__ tw4096)
-{
-    static_assert(L <= NS, "ring too small");
-    __shared__ __attribute__((aligned(16))) float2 xb[NBUF2 * BSTR];
-    __shared__ __attribute__((aligned(16))) float2 tw1[16 * 64]; // W_1024^{+t k1}
-    __shared__ __attribute__((aligned(16))) float2 tw2[16 * 4];  // W_64^{+b r}
-    typedef float v4f __attribute__((ext_vector_type(4)));
-
-    const int tid = threadIdx.x;
-    const int lane = tid & 63;
-    const int wave = tid >> 6;
-
-#pragma unroll
-    for (int e = tid; e < 1024; e += NT2) {
-        const int k1 = e >> 6, t = e & 63;
-        const float2 w = tw4096[(4 * t * k1) & 4095];
-        tw1[e] = make_float2(w.x, -w.y);
-    }
-    if (tid < 64) {
-        const int r = tid >> 2, b = tid & 3;
-        const float2 w = tw4096[(64 * b * r) & 4095];
-        tw2[tid] = make_float2(w.x, -w.y);
-    }
-
-    // columns 2t (bin j0) and 2t+1 (bin j1 = j0 - 1)
-    const bool lo = tid < M2 / 2;
-    const int j0 = lo ? (M2 - 1 - 2 * tid) : (3 * M2 - 1 - 2 * tid), j1 = j0 - 1;
-    const int dA = lo ? 0 : 1;
-    // ta*: taps of the first block a row feeds, tb*: of the second (as k_pfb2_an1024)
-    float ta0[L], tb0[L], ta1[L], tb1[L];
-    auto load_taps = [&]() {
-        int oa0 = (lo ? j0 : (j0 ^ M2)) * L, ob0 = (lo ? (j0 ^ M2) : j0) * L;
-        int oa1 = (lo ? j1 : (j1 ^ M2)) * L, ob1 = (lo ? (j1 ^ M2) : j1) * L;
-        asm volatile("" : "+v"(oa0), "+v"(ob0), "+v"(oa1), "+v"(ob1)); // keep the reload inside the loop
-#pragma unroll
-        for (int q = 0; q < L / 4; q++) {
-            const v4f a0 = *reinterpret_cast<const v4f *>(hsub + oa0 + 4 * q);
-            const v4f b0 = *reinterpret_cast<const v4f *>(hsub + ob0 + 4 * q);
-            const v4f a1 = *reinterpret_cast<const v4f *>(hsub + oa1 + 4 * q);
-            const v4f b1 = *reinterpret_cast<const v4f *>(hsub + ob1 + 4 * q);
-#pragma unroll
-            for (int e = 0; e < 4; e++) {
-                ta0[4 * q + e] = a0[e];
-                tb0[4 * q + e] = b0[e];
-                ta1[4 * q + e] = a1[e];
-                tb1[4 * q + e] = b1[e];
-            }
-        }
-    };
-    load_taps();
-
-    float2 w0[NS], w1[NS];   // ring of the two columns: row c in slot c mod 8
-#pragma unroll
-    for (int s = 0; s < NS; s++) w0[s] = w1[s] = make_float2(0.f, 0.f);
-
-    const long long gs = P.gs0 + (long long)blockIdx.x * P.gpw;   // even
-    long long ge = gs + P.gpw;
-    if (ge > P.gend) ge = P.gend;
-    const long long HL = 2 * (L / 2) * M - M2;
-    // local index of row (4gs - NS)'s first sample
-    const long long ls0 = (4 * gs - NS) * M - P.B0 * M2;
-    const unsigned long long ah = (unsigned long long)(uintptr_t)(P.hist + HL);
-    const unsigned long long ax = (unsigned long long)(uintptr_t)P.x;
-    const unsigned long long az = (unsigned long long)(uintptr_t)P.zero;
-    // row c, columns 2t and 2t+1: one 16-byte load from the history, x or
-    // the zero words (integer selects, no branch around the load)
-    auto fetch2 = [&](long long c) -> v4f {
-        const long long li = ls0 + (c - (4 * gs - NS)) * M + 2 * tid;
-        const bool neg = li < 0;
-        const bool in = neg ? (li >= -HL) : (li < P.n_in);
-        unsigned long long a = (neg ? ah : ax) + (unsigned long long)(li * 8);
-        a = in ? a : az;
-        typedef const v4f __attribute__((address_space(1))) *gptr;
-        return __builtin_nontemporal_load(reinterpret_cast<gptr>(a));
-    };
-    auto dot = [&](const float2 (&w)[NS], int newest, const float (&h)[L]) -> float2 {
-        float2 acc = make_float2(0.f, 0.f);
-#pragma unroll
-        for (int n = 0; n < L; n++) {
-            const float2 v = w[(newest - n) & (NS - 1)];
-            acc.x = fmaf(h[n], v.x, acc.x);
-            acc.y = fmaf(h[n], v.y, acc.y);
-        }
-        return acc;
-    };
-    // warm-up: rows 4gs-8 .. 4gs-1 (4gs = 0 mod 8: slots 0..7); the last
-    // gives the hi half of block 8gs (hi lanes, second product)
-#pragma unroll
-    for (int s = 0; s < NS; s++) {
-        const v4f v = fetch2(4 * gs - NS + s);
-        w0[s] = make_float2(v.x, v.y);
-        w1[s] = make_float2(v.z, v.w);
-    }
-    float2 carry0 = dot(w0, NS - 1, tb0), carry1 = dot(w1, NS - 1, tb1);
-    v4f pf[4];
-#pragma unroll
-    for (int r = 0; r < 4; r++) pf[r] = fetch2(4 * gs + r);
-    __syncthreads();                 // twiddle tables ready
-    __builtin_amdgcn_s_waitcnt(0);   // an empty queue at the loop head (see k_pfb2_an1024)
-
-    const __amdgpu_buffer_rsrc_t ry =
-        __builtin_amdgcn_make_buffer_rsrc((void *)P.Y, (short)0, (int)(P.nblk * M * 8), 0x00020000);
-
-    // one group: rows 4g .. 4g+3 in ring slots RO .. RO+3
-    auto group = [&](long long g, auto ro_c) {
-        constexpr int RO = decltype(ro_c)::value;
-        const long long b0 = 8 * g;
-        // ILV: the taps reload at the dot phase (it waits for this group's
-        // rows, issued after the previous group's stores, anyway)
-        if (ILV) load_taps();
-        if (!lo) {   // the hi half of block b0, computed from the previous group's last row
-            xb[j0] = carry0;
-            xb[j1] = carry1;
-        }
-#pragma unroll
-        for (int r = 0; r < 4; r++) {
-            const v4f v = pf[r];
-            w0[RO + r] = make_float2(v.x, v.y);
-            w1[RO + r] = make_float2(v.z, v.w);
-            const int s1 = 2 * r + dA;   // first block of row 4g + r, local index
-            xb[s1 * BSTR + j0] = dot(w0, RO + r, ta0);
-            xb[s1 * BSTR + j1] = dot(w1, RO + r, ta1);
-            const float2 q0 = dot(w0, RO + r, tb0), q1 = dot(w1, RO + r, tb1);
-            if (r < 3 || lo) {
-                xb[(s1 + 1) * BSTR + j0] = q0;
-                xb[(s1 + 1) * BSTR + j1] = q1;
-            } else {
-                carry0 = q0;
-                carry1 = q1;
-            }
-        }
-        if (!ILV && g + 1 < ge) {
-#pragma unroll
-            for (int r = 0; r < 4; r++) pf[r] = fetch2(4 * (g + 1) + r);
-        }
-        lds_barrier();
-        {
-            const long long b = b0 + wave;
-            float2 *B = xb + wave * BSTR;
-            v2f v[16];
-#pragma unroll
-            for (int k = 0; k < 16; k++) v[k] = pk(B[lane + 64 * k]);
-            pk_dft16<-1>(v);
-#pragma unroll
-            for (int k1 = 1; k1 < 16; k1++) {
-                if ((k1 & 3) == 0) __builtin_amdgcn_sched_barrier(0);
-                v[k1] = pk_cmul(v[k1], pk(tw1[k1 * 64 + lane]));
-            }
-            lds_fence();
-#pragma unroll
-            for (int k1 = 0; k1 < 16; k1++) B[k1 * TSTR + lane] = unpk(v[k1]);
-            lds_fence();
-            const int k1 = lane >> 2, bq = lane & 3;
-#pragma unroll
-            for (int a = 0; a < 16; a++) v[a] = pk(B[k1 * TSTR + 4 * a + bq]);
-            pk_dft16<-1>(v);
-#pragma unroll
-            for (int r = 1; r < 16; r++) {
-                if ((r & 3) == 0) __builtin_amdgcn_sched_barrier(0);
-                v[r] = pk_cmul(v[r], pk(tw2[r * 4 + bq]));
-            }
-            lds_fence();
-#pragma unroll
-            for (int r = 0; r < 16; r++) B[k1 + 16 * r + 260 * bq] = unpk(v[r]);
-            lds_fence();
-            if (!ILV) load_taps();   // before the stores (vmcnt counts stores too, see k_pfb2_an1024)
-            __builtin_amdgcn_sched_barrier(0);
-            const int t2 = lane >> 3, p2 = lane & 7;
-            const unsigned yo = (unsigned)((b - P.B0) * (M * 8)) + (unsigned)(8 * (2 * p2 + 16 * t2));
-#pragma unroll
-            for (int u = 0; u < 2; u++) {
-                v4f c[4];
-#pragma unroll
-                for (int q = 0; q < 4; q++)
-                    c[q] = *reinterpret_cast<const v4f *>(B + 2 * p2 + 16 * (t2 + 8 * u) + 260 * q);
-                v2f e0[4] = {c[0].xy, c[1].xy, c[2].xy, c[3].xy};
-                v2f e1[4] = {c[0].zw, c[1].zw, c[2].zw, c[3].zw};
-                pk_dft4<-1>(e0[0], e0[1], e0[2], e0[3]);
-                pk_dft4<-1>(e1[0], e1[1], e1[2], e1[3]);
-#pragma unroll
-                for (int sidx = 0; sidx < 4; sidx++) {
-                    const v4f val = {e0[sidx].x, e0[sidx].y, e1[sidx].x, e1[sidx].y};
-                    __builtin_amdgcn_raw_buffer_store_b128(val, ry, yo + 8 * (128 * u + 256 * sidx), 0, 2);
-                    if (ILV && (sidx & 1)) {   // the next group's rows between the stores
-                        const int r = 2 * u + (sidx >> 1);
-                        if (g + 1 < ge) pf[r] = fetch2(4 * (g + 1) + r);
-                    }
-                }
-            }
-        }
-        lds_barrier();
-    };
-    for (long long g = gs; g < ge; g += 2) {
-        group(g, std::integral_constant<int, 0>{});
-        if (g + 1 < ge) group(g + 1, std::integral_constant<int, 4>{});
-    }
-}
-
 // ---------------------------------------------------------------- firpfbch analyzer
 // Critically sampled analyzer (firpfbch_crcf, M = 1024, real taps), the same
 // structure for the reference's firpfbch.c:346-409: row b = x[bM .. bM+M),
@@ -972,27 +751,7 @@ extern "C" int lqk_firpfbch2_analyzer_fast(unsigned int Mch, unsigned int m, con
         P.gend = glast + 1;
         // paired 16-byte row loads need x and the history 16-byte aligned
         const bool pair = ((uintptr_t)P.x & 15) == 0 && ((uintptr_t)(P.hist + HL) & 15) == 0;
-        static const int wmode = getenv("LQ_PFB2_W") ? atoi(getenv("LQ_PFB2_W")) : 0;
-        if (wmode && pair) {
-            // two 8-wave workgroups per CU, 8-block groups, workgroup ranges on even groups
-            Params Q = P;
-            const long long g8first = (P.B0 / 8) & ~1LL, g8last = (P.B0 + nb - 1) / 8;
-            const long long ng8 = g8last - g8first + 1;
-            long long gpw8 = (ng8 + 511) / 512;
-            gpw8 = gpw8 < 8 ? 8 : (gpw8 + 1) & ~1LL;
-            const long long nwg8 = (ng8 + gpw8 - 1) / gpw8;
-            Q.gs0 = g8first;
-            Q.gpw = (int)gpw8;
-            Q.gend = g8last + 1;
-            if (m == 4 && wmode == 1)
-                hipLaunchKernelGGL((k_pfb2_an1024w<8, false>), dim3((unsigned)nwg8), dim3(NT2), 0, st, Q, (const float *)hsub, tw);
-            else if (m == 4)
-                hipLaunchKernelGGL((k_pfb2_an1024w<8, true>), dim3((unsigned)nwg8), dim3(NT2), 0, st, Q, (const float *)hsub, tw);
-            else if (wmode == 1)
-                hipLaunchKernelGGL((k_pfb2_an1024w<4, false>), dim3((unsigned)nwg8), dim3(NT2), 0, st, Q, (const float *)hsub, tw);
-            else
-                hipLaunchKernelGGL((k_pfb2_an1024w<4, true>), dim3((unsigned)nwg8), dim3(NT2), 0, st, Q, (const float *)hsub, tw);
-        } else if (m == 4 && pair)
+        if (m == 4 && pair)
             hipLaunchKernelGGL((k_pfb2_an1024<8, true>), dim3((unsigned)nwg), dim3(NT), 0, st, P, (const float *)hsub, tw);
         else if (m == 4)
             hipLaunchKernelGGL((k_pfb2_an1024<8, false>), dim3((unsigned)nwg), dim3(NT), 0, st, P, (const float *)hsub, tw);
