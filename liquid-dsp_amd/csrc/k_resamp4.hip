@@ -15,7 +15,8 @@
 // The host tabulates (tau_k, i_k) for every fourth output of the float32
 // schedule (the "output plan", periodic: r = 1.037 repeats after 2^20 outputs,
 // a 2 MB table read from L2 at 2 B per output), and the kernel replays it
-// bit-exactly:
+// bit-exactly (a lane steps at most three outputs from the entry at or before
+// its first output):
 //   * a wave tile is 256 consecutive outputs; lane j owns outputs 4j .. 4j+3,
 //     so its replay is four straight-line steps from its own table entry
 //     (no per-input loop, no output list) and its four outputs leave as two
@@ -58,7 +59,7 @@ constexpr int N4 = 88;         // slots per residue class of the transposed wind
 // resident workgroups per CU: five (<= 96 VGPRs) while the register window
 // (2L + 8 VGPRs) allows, else four (<= 128)
 template <int L>
-constexpr int rs4_blk() { return L <= 18 ? 5 : 4; }
+constexpr int rs4_blk() { return L <= 16 ? 5 : 4; }
 
 // window samples of a tile: outputs k0 .. k0+255 lie on inputs i_e .. i_e+255
 // (i_e: input of the tile's table entry, at most 3 outputs before k0), and the
@@ -130,20 +131,23 @@ __global__ __launch_bounds__(NT4, rs4_blk<L>()) void k_resamp4(lqk_rs4_plan pl, 
         return __builtin_bit_cast(float2, __builtin_amdgcn_raw_buffer_load_b64(r, off, 0, 0));
     };
 
-    // Table entries.  Lane j of tile T reads the state at plan output
-    // kb + 4j, kb = the tile's first output rounded down to a multiple of 4;
-    // outputs >= pre repeat with period QT (PT inputs), QT a multiple of 4 and
-    // >= 256, so a tile wraps at most once.  A wave walks its tiles GW apart,
-    // so the tile's periodic position (r0 = (kb - pre) mod QT, q0 periods) is
-    // stepped by the constant (GW 256) mod QT on the scalar unit instead of
-    // divided per tile.  The entry's input index becomes call-relative only
-    // when it is used (i = entry word + off), so nothing waits on the load.
+    // Table entries.  The table holds the state at outputs 0, 4, 8, ... below
+    // pre (npre entries), then at pre, pre + 4, ... within one period of QT
+    // outputs (PT inputs; QT >= 256, so a 256-output tile wraps at most
+    // once).  Lane j of a tile (first output k0) reads the entry at or
+    // before its output k = k0 + 4j and steps `skip` = 0..3 outputs from it.
+    // A wave walks its tiles GW apart, so the tile's periodic position
+    // (r0 = (k0 - pre) mod QT, q0 periods) is stepped by the constant
+    // (GW 256) mod QT on the scalar unit instead of divided per tile.  The
+    // entry's input index becomes call-relative only when it is used
+    // (i = entry word + off), so nothing waits on the load.
     struct Ent {
         float2 raw;   // (tau, plan input as bits)
         int off;      // + (periods) PT - g0, modulo 2^32
+        int skip;     // outputs from the entry to the lane's first output
     };
     struct Cur {
-        unsigned long long kb, r0, q0;
+        unsigned long long k0, r0, q0;
         bool per;
     };
     const unsigned long long STEP = (unsigned long long)GW * TOUT;
@@ -153,15 +157,15 @@ __global__ __launch_bounds__(NT4, rs4_blk<L>()) void k_resamp4(lqk_rs4_plan pl, 
         dR = STEP - dQ * pl.QT;
     }
     auto cur_fix = [&](Cur &c) {
-        c.per = c.kb >= pl.pre;
+        c.per = c.k0 >= pl.pre;
         if (c.per) {
-            const unsigned long long dt = c.kb - pl.pre;
+            const unsigned long long dt = c.k0 - pl.pre;
             c.q0 = dt / pl.QT;
             c.r0 = dt - c.q0 * pl.QT;
         }
     };
     auto cur_next = [&](Cur &c) {
-        c.kb += STEP;
+        c.k0 += STEP;
         if (c.per) {
             c.r0 += dR;
             c.q0 += dQ;
@@ -174,15 +178,27 @@ __global__ __launch_bounds__(NT4, rs4_blk<L>()) void k_resamp4(lqk_rs4_plan pl, 
         }
     };
     auto entry = [&](int tile, const Cur &c) -> Ent {
-        if (tile >= ntiles) return Ent{make_float2(0.0f, 0.0f), 0};
-        unsigned long long idx = (c.kb >> 2) + (unsigned)lane;
+        if (tile >= ntiles) return Ent{make_float2(0.0f, 0.0f), 0, 0};
+        const unsigned long long k = c.k0 + 4ull * (unsigned)lane;
+        unsigned long long idx;
+        unsigned r4;                               // position whose low bits are the skip
         int off = -(int)(unsigned)g0;
         if (c.per) {
-            const bool w = c.r0 + 4ull * (unsigned)lane >= pl.QT;
-            idx = ((pl.pre + c.r0) >> 2) + (unsigned)lane - (w ? (pl.QT >> 2) : 0ull);
+            unsigned long long r = c.r0 + 4ull * (unsigned)lane;
+            const bool w = r >= pl.QT;
+            r -= w ? pl.QT : 0ull;
+            idx = pl.npre + (r >> 2);
+            r4 = (unsigned)r;
             off = (int)(unsigned)(c.q0 * pl.PT - g0) + (w ? (int)(unsigned)pl.PT : 0);
+        } else if (k < pl.pre) {
+            idx = k >> 2;
+            r4 = (unsigned)k;
+        } else {                                   // k - pre < 256 <= QT: the first period
+            const unsigned long long r = k - pl.pre;
+            idx = pl.npre + (r >> 2);
+            r4 = (unsigned)r;
         }
-        return Ent{ld8(rt, idx < pl.ntab ? (int)idx : -1), off};
+        return Ent{ld8(rt, idx < pl.ntab ? (int)idx : -1), off, (int)(r4 & 3u)};
     };
     auto ent_i = [](const Ent &e) { return (int)__float_as_uint(e.raw.y) + e.off; };
     // prefetched window of a tile: window sample t is input ws + t,
@@ -224,7 +240,7 @@ __global__ __launch_bounds__(NT4, rs4_blk<L>()) void k_resamp4(lqk_rs4_plan pl, 
     // one wait covers both (and the stores of tile t-1), window t+1 goes to
     // LDS, tile t's outputs are stored, and the loads for t+2 / t+3 issue.
     Cur cc;
-    cc.kb = (K0 & ~3ull) + (unsigned long long)gw * TOUT;
+    cc.k0 = K0 + (unsigned long long)gw * TOUT;
     cur_fix(cc);
     Ent ec = entry(gw, cc);
     cur_next(cc);
@@ -238,10 +254,9 @@ __global__ __launch_bounds__(NT4, rs4_blk<L>()) void k_resamp4(lqk_rs4_plan pl, 
     fetch(gw + GW, __builtin_amdgcn_readfirstlane(ent_i(en)) - L, wa);
 
     for (int tile = gw; tile < ntiles; tile += GW) {
-        // replay: the lane's entry stepped (k0 & 3) outputs, then its four
+        // replay: the lane's entry stepped `skip` outputs, then its four
         // outputs (bank, mu, input offset d)
-        const unsigned long long k0 = K0 + (unsigned long long)tile * TOUT;
-        const int skip = (int)(k0 & 3ull);
+        const int skip = ec.skip;
         const int i_e = __builtin_amdgcn_readfirstlane(ent_i(ec));   // input of the lane-0 entry
         float tau = ec.raw.x;
         int ii = ent_i(ec);
@@ -253,7 +268,9 @@ __global__ __launch_bounds__(NT4, rs4_blk<L>()) void k_resamp4(lqk_rs4_plan pl, 
                 ii++;
             }
         };
-        for (int s = 0; s < skip; s++) step();
+#pragma unroll
+        for (int s = 0; s < 3; s++)
+            if (s < skip) step();
         const int ia = ii;
         int bk[4], dd[4];
         float mu[4];
@@ -368,7 +385,7 @@ extern "C" void lqk_resamp4(const lqk_rs4_plan *pl, unsigned long long g0, unsig
 {
     if (n == 0 || nout == 0) return;
     if (!lqk_resamp4_supported(npfb, L) || n > LQK_RS_MAXN || nout * 8ull >= (1ull << 31) || pl->ntab * 8ull >= (1ull << 31) ||
-        !(pl->pre == ~0ull || (pl->pre % 4 == 0 && pl->QT % 4 == 0 && pl->QT >= TOUT))) {
+        !(pl->pre == ~0ull || (pl->QT >= TOUT && pl->npre == (pl->pre + 3) / 4))) {
         fprintf(stderr, "error: liquid-mi355x: resamp4 launch outside its shape (npfb %u, L %u, %llu inputs)\n", npfb, L, n);
         exit(1);
     }

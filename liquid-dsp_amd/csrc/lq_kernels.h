@@ -198,11 +198,12 @@ void lqk_resamp(int real_io, const lqk_rs_plan *pl, unsigned long long g0, unsig
  * npfb the BOUNDARY pair (h_{npfb-1}[L-1-p], h_0[L-p]); zero elsewhere (NULL: untiled kernel) */
 /* Output plan of k_resamp4 (csrc/k_resamp4.hip: complex samples, power-of-two
  * npfb, 1 < r < 2 with one or two outputs per input over the whole plan):
- * tab[c] = {tau, i} = the timing phase at which plan output 4c is emitted and
- * the plan input it belongs to.  Outputs k >= pre repeat with period QT
- * outputs / PT inputs (pre and QT multiples of 4, QT >= 256): state(k) =
- * state(pre + (k - pre) % QT) with i += PT per period; pre = ~0: no period
- * (a direct plan; ntab entries cover the plan's outputs). */
+ * entries {tau, i} = the timing phase at which a plan output is emitted and
+ * the plan input it belongs to -- tab[c] for output 4c (c < npre =
+ * ceil(pre / 4)), then tab[npre + c] for output pre + 4c within one period.
+ * Outputs k >= pre repeat with period QT outputs / PT inputs (QT >= 256):
+ * state(k) = state(pre + (k - pre) % QT) with i += PT per period; pre = ~0:
+ * no period (a direct plan; ntab entries cover the plan's outputs). */
 typedef struct {
     float tau;
     unsigned int i;
@@ -210,7 +211,7 @@ typedef struct {
 typedef struct {
     const void *tab;              /* device lqk_rs4_entry[ntab] */
     unsigned long long ntab;
-    unsigned long long pre, QT, PT;
+    unsigned long long pre, npre, QT, PT;
 } lqk_rs4_plan;
 int lqk_resamp4_supported(unsigned int npfb, unsigned int L);
 /* n complex inputs x (plan inputs g0 .. g0+n) -> the nout outputs y[k - K0]

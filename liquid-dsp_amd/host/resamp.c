@@ -50,6 +50,8 @@ typedef struct {
     size_t n, cap, esz, max;
     int overflow;                 /* more than `max` entries were due */
     int d4_ok;                    /* RS_D4: every input after the first output emitted one or two outputs */
+    unsigned long long opre;      /* RS_D4: outputs 0, 4, .. below opre, then opre, opre + 4, .. */
+    unsigned long long kmax;      /* RS_D4: ... below kmax */
 } rs_rec;
 
 typedef struct {
@@ -62,7 +64,7 @@ typedef struct {
     rs_rec rec;                   /* its host copy until uploaded */
     lq_devbuf d_tab;
     unsigned long long d_n;       /* entries on the device */
-    unsigned long long opre, QT, PT;   /* RS_D4: outputs >= opre repeat every QT outputs / PT inputs */
+    unsigned long long opre, npre, QT, PT;   /* RS_D4: outputs >= opre repeat every QT outputs / PT inputs */
 } rs_plan;
 
 struct lq_rs_s {
@@ -208,6 +210,8 @@ static void rs_rec_init(rs_rec *r, int kind, int p2, size_t max)
     r->esz = kind == RS_D4 ? sizeof(lqk_rs4_entry) : (p2 ? sizeof(lqk_rs_entry_p2) : sizeof(lqk_rs_entry));
     r->max = max;
     r->d4_ok = 1;
+    r->opre = ~0ull;
+    r->kmax = ~0ull;
 }
 
 static void rs_rec_free(rs_rec *r)
@@ -349,7 +353,7 @@ static unsigned long long rs_walk(lq_rs *q, rs_state x0, unsigned long long n, i
                 float x = t;
                 unsigned int c = 0;
                 while (x < z) {
-                    if ((K & 3) == 0) {
+                    if (K < rec->kmax && ((K < rec->opre ? K : K - rec->opre) & 3) == 0) {
                         lqk_rs4_entry *e = (lqk_rs4_entry *)rs_rec_push(rec);
                         if (e) {
                             e->tau = x;
@@ -409,13 +413,17 @@ static unsigned long long rs_K_lin(lq_rs *q, unsigned long long g)
 }
 
 /* a walk of n inputs from the plan's origin that records the device table
- * (at most max entries; the host checkpoints it rewrites are the ones
- * recorded before, same origin); 0 if the walk or the one-or-two-outputs
- * check of an output plan fails */
-static int rs_rec_walk(lq_rs *q, unsigned long long n, int kind, size_t max)
+ * (at most max entries; an output plan's entries at outputs 0, 4, .. below
+ * opre and opre, opre + 4, .. below kmax; the host checkpoints it rewrites
+ * are the ones recorded before, same origin); 0 if the walk or the
+ * one-or-two-outputs check of an output plan fails */
+static int rs_rec_walk(lq_rs *q, unsigned long long n, int kind, size_t max, unsigned long long opre,
+                       unsigned long long kmax)
 {
     unsigned long long q0, Kend, lam;
     rs_rec_init(&q->pl.rec, kind, rs_p2(q), max);
+    q->pl.rec.opre = opre;
+    q->pl.rec.kmax = kmax;
     if (rs_walk(q, q->pl.origin, n, 0, &q0, &Kend, &lam, &q->pl.rec) != n) return 0;
     return kind != RS_D4 || q->pl.rec.d4_ok;
 }
@@ -428,19 +436,22 @@ static int rs_plan_device(lq_rs *q, int have)
     const int d4 = pl->rec.kind == RS_D4 && pl->rec.d4_ok;
     if (pl->rec.kind == RS_D4 && d4) {
         if (pl->periodic) {
-            /* outputs >= opre repeat every QT = mQ outputs (mP inputs): opre and
-             * QT multiples of 4 (a tile's lanes all skip k0 mod 4 outputs from
-             * their entries) and QT >= 256 (a 256-output tile wraps at most once) */
-            const unsigned long long Kpre = rs_K_lin(q, pl->pre), Q = pl->Q;
+            /* entries at outputs 0, 4, .. below opre = K(pre), then opre,
+             * opre + 4, .. over one period of QT = mQ outputs (mP inputs),
+             * QT >= 256 so a 256-output tile wraps at most once.  A pure cycle
+             * (pre = 0) with Q >= 256 is exactly what the search walk recorded */
+            const unsigned long long Q = pl->Q;
             unsigned long long m = 1;
-            while ((m * Q) % 4 != 0 || m * Q < 256) m++;
-            pl->opre = (Kpre + 3) & ~3ull;
+            while (m * Q < 256) m++;
+            pl->opre = rs_K_lin(q, pl->pre);
+            pl->npre = (pl->opre + 3) / 4;
             pl->QT = m * Q;
             pl->PT = m * pl->P;
-            const unsigned long long need = (pl->opre + pl->QT) / 4;
+            const unsigned long long need = pl->npre + (pl->QT + 3) / 4;
             if (Q > 0 && need <= RS_D4_MAXOUT / 4) {
-                if (!(have && pl->rec.n >= need))
-                    if (!rs_rec_walk(q, pl->pre + (m + 1) * pl->P + 4, RS_D4, (size_t)need)) goto d3;
+                if (!(have && pl->opre == 0 && m == 1 && pl->rec.n >= need))
+                    if (!rs_rec_walk(q, pl->pre + m * pl->P + 1, RS_D4, (size_t)need, pl->opre, pl->opre + pl->QT))
+                        goto d3;
                 if (pl->rec.n >= need) {
                     pl->rec.n = need;
                     pl->dk = RS_D4;
@@ -449,6 +460,7 @@ static int rs_plan_device(lq_rs *q, int have)
             }
         } else if (have && !pl->rec.overflow) {
             pl->opre = ~0ull;
+            pl->npre = 0;
             pl->QT = pl->PT = 0;
             pl->dk = RS_D4;
             return 1;
@@ -459,7 +471,7 @@ d3:
         const unsigned long long n = pl->periodic ? pl->pre + pl->P : pl->end;
         const size_t need = (size_t)(n / LQK_RS_CK + 1);
         if (!(have && pl->rec.kind == RS_D3 && pl->rec.n >= need))
-            if (!rs_rec_walk(q, n, RS_D3, need) || pl->rec.n < need) return 0;
+            if (!rs_rec_walk(q, n, RS_D3, need, ~0ull, ~0ull) || pl->rec.n < need) return 0;
         pl->rec.n = need;
         pl->dk = RS_D3;
         return 1;
@@ -798,7 +810,7 @@ void lq_rs_block_dev(lq_rs *_q, const void *_dxv, unsigned long long _nx, void *
         unsigned long long K0 = rs_K(_q, _q->gpos), K1 = rs_K(_q, _q->gpos + c);
         void *hold = _q->d_hist[_q->cur], *hnew = _q->d_hist[_q->cur ^ 1];
         if (_q->pl.dk == RS_D4) {
-            lqk_rs4_plan kp = {_q->pl.d_tab.p, _q->pl.d_n, _q->pl.opre, _q->pl.QT, _q->pl.PT};
+            lqk_rs4_plan kp = {_q->pl.d_tab.p, _q->pl.d_n, _q->pl.opre, _q->pl.npre, _q->pl.QT, _q->pl.PT};
             lqk_resamp4(&kp, _q->gpos, K0, _q->npfb, _q->L, _q->del, _q->d_taps2, hold, _dx, c, _dy, K1 - K0,
                         _q->ctx.stream);
         } else {
@@ -1010,8 +1022,8 @@ long long liquid_mi355x_resamp_schedule(float _rate, unsigned int _npfb, unsigne
  * resampler with 2m = 14 taps per bank would use from the initial state
  * (periodic if `periodic`, else direct over nx inputs) and, when it is an
  * output plan (k_resamp4), expands every output exactly as k_resamp4 does:
- * the entry of output k & ~3 (periods unwrapped), k & 3 steps, then bank
- * (-1: BOUNDARY), mu and input index.  Returns the number of outputs of the
+ * the entry at or before output k (periods unwrapped), up to three steps,
+ * then bank (-1: BOUNDARY), mu and input index.  Returns the number of outputs of the
  * first nx inputs, -1 if no plan, -3 if the plan is not an output plan. */
 long long liquid_mi355x_resamp_schedule4(float _rate, unsigned int _npfb, unsigned long long _nx, int _periodic,
                                          int *_b, float *_mu, unsigned int *_idx, unsigned long long _cap,
@@ -1046,11 +1058,11 @@ long long liquid_mi355x_resamp_schedule4(float _rate, unsigned int _npfb, unsign
     const float z = 1.0f - 1.0f / (float)_npfb, fn = (float)_npfb;
     long long ret = (long long)Kn;
     for (unsigned long long k = 0; k < Kn && k < _cap; k++) {
-        const unsigned long long kb = k & ~3ull;
-        unsigned long long idx = kb >> 2, add = 0;
-        if (kb >= q.pl.opre) {
-            const unsigned long long dt = kb - q.pl.opre, c = dt / q.pl.QT;
-            idx = (q.pl.opre + (dt - c * q.pl.QT)) >> 2;
+        unsigned long long idx = k >> 2, add = 0, skip = k & 3;
+        if (k >= q.pl.opre) {
+            const unsigned long long dt = k - q.pl.opre, c = dt / q.pl.QT, r = dt - c * q.pl.QT;
+            idx = q.pl.npre + (r >> 2);
+            skip = r & 3;
             add = c * q.pl.PT;
         }
         if (idx >= q.pl.rec.n) {
@@ -1059,7 +1071,7 @@ long long liquid_mi355x_resamp_schedule4(float _rate, unsigned int _npfb, unsign
         }
         float tau = t[idx].tau;
         unsigned long long i = t[idx].i + add;
-        for (unsigned s = 0; s < (unsigned)(k & 3); s++) {
+        for (unsigned s = 0; s < (unsigned)skip; s++) {
             tau = tau + q.del;
             if (!(tau < z)) {
                 tau = tau - 1.0f;

@@ -44,7 +44,8 @@ def plan_kind(request):
 
 
 @pytest.mark.parametrize("rate,m,npfb", [(1.037, 7, 64), (1.27115323, 13, 64), (1.5, 4, 64), (1.9, 7, 32),
-                                         (1.0001, 2, 64), (1.3, 16, 256), (1.7, 10, 128), (1.11, 1, 8)])
+                                         (1.0001, 2, 64), (1.3, 16, 256), (1.7, 10, 128), (1.11, 1, 8),
+                                         (1.00624001, 7, 64), (1.02353001, 5, 64)])
 def test_resamp4_ragged_calls(plan_kind, rate, m, npfb):
     rate = float(np.float32(rate))
     r = np.random.default_rng(int(rate * 1000) + m + npfb)
@@ -76,10 +77,12 @@ def g_num(rate, npfb, a, b):
     return int(np.searchsorted(idx, b) - np.searchsorted(idx, a))
 
 
-def test_resamp4_cccf_and_long_stream(plan_kind):
+@pytest.mark.parametrize("rate", [1.037, 1.00624001])
+def test_resamp4_cccf_and_long_stream(plan_kind, rate):
     # cccf runs the complex kernel (real taps, resamp.c:117-132); 3M inputs in
-    # calls of 700 001 cross the r = 1.037 plan period (2^20 outputs) twice
-    rate = float(np.float32(1.037))
+    # calls of 700 001 cross the plan period twice (r = 1.037: 2^20 outputs;
+    # r = 1.00624001: a 3-input pre-period, then 1 389 431 inputs)
+    rate = float(np.float32(rate))
     r = np.random.default_rng(99)
     x = cx(r, 3_000_000)
     g = LQ.Resamp(rate, 7, 0.25, 60.0, 64, t=LQ.CCCF)
