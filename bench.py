@@ -365,12 +365,14 @@ def bench_resamp(args, world, rank, stream):
     rate = 1.037
     x = synth_complex(n, 4242 + rank)
     y = torch.empty(2 * (int(n * rate) + 4096), dtype=torch.float32, device="cuda")
-    # the kernels' first launch in the process, on another object and rate
-    w = LQ.Resamp(0.77, 7, 0.25, 60.0, 64)
-    w.set_stream(stream.cuda_stream)
-    w.execute_block_dev(x.data_ptr(), 1 << 16, y.data_ptr())
-    stream.synchronize()
-    w.destroy()
+    # the kernels' first launches in the process (code-object loading), on
+    # other objects and rates: 1.23 runs k_resamp4 as 1.037 does, 0.77 k_resamp3
+    for wr in (1.23, 0.77):
+        w = LQ.Resamp(wr, 7, 0.25, 60.0, 64)
+        w.set_stream(stream.cuda_stream)
+        w.execute_block_dev(x.data_ptr(), 1 << 15, y.data_ptr())
+        stream.synchronize()
+        w.destroy()
     q = LQ.Resamp(rate, 7, 0.25, 60.0, 64)
     q.set_stream(stream.cuda_stream)
     nys = []

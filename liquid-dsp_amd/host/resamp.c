@@ -305,71 +305,88 @@ static unsigned long long rs_walk(lq_rs *q, rs_state x0, unsigned long long n, i
          * Brent's tortoise, the state at position 2^k - 1 (and the first
          * RS_EARLY states with each other): a pure cycle ends the walk on its
          * first return, any other once the tortoise sits on the cycle
-         * (r = 1.037: 1 011 163 steps, ~3 ms) */
+         * (r = 1.037: 1 011 163 steps).  The hot loop runs between events
+         * (host checkpoints every RS_HCK inputs, tortoise resets), with the
+         * device records and the returns tested inline. */
         const float del = q->del, z = 1.0f - 1.0f / (float)q->npfb;
         float t = x0.tau;
         unsigned int eb[RS_EARLY], tort;
         unsigned long long tpos = 0, reset = 1;
         for (int k = 0; k < RS_EARLY; k++) eb[k] = 0x7fc00001u;
         memcpy(&tort, &t, 4);
-        for (;; i++) {
+        for (;;) {
             if ((i & (RS_HCK - 1)) == 0) {
                 rs_plan_reserve(pl, pl->nck + 1);
                 rs_state s = i == 0 ? x0 : rs_from_tau(t, q->npfb);
                 rs_put(&pl->tab[pl->nck++], &s, K);
             }
-            if (r3 && (i & (LQK_RS_CK - 1)) == 0) rs_rec3(rec, NULL, t, K);
             if (K > 0xffffffffull || i == n) break;
-            if (early) {
+            if (early && i < RS_EARLY) {           /* position i: compare, record, step */
                 unsigned int tb;
                 memcpy(&tb, &t, 4);
-                if (i < RS_EARLY) {
-                    for (unsigned long long k = 0; k < i; k++)
-                        if (eb[k] == tb) {
-                            *q0 = k;
-                            *Kend = K;
-                            return i;
-                        }
-                    eb[i] = tb;
-                } else if ((tb == eb[0]) | (tb == tort)) {
-                    for (int k = RS_EARLY - 1; k >= 0; k--)
-                        if (eb[k] == tb) {
-                            *q0 = (unsigned long long)k;
-                            *Kend = K;
-                            return i;
-                        }
-                    *q0 = RS_BRENT;
-                    *lam_out = i - tpos;
-                    *Kend = K;
-                    return i;
-                }
+                for (unsigned long long k = 0; k < i; k++)
+                    if (eb[k] == tb) {
+                        *q0 = k;
+                        *Kend = K;
+                        return i;
+                    }
+                eb[i] = tb;
                 if (i == reset) {
-                    tort = tb;
+                    tort = eb[i];
                     tpos = i;
                     reset = 2 * i + 1;
                 }
             }
-            if (r4) {   /* the output plan: (tau, input) at every fourth output */
-                float x = t;
-                unsigned int c = 0;
-                while (x < z) {
-                    if (K < rec->kmax && ((K < rec->opre ? K : K - rec->opre) & 3) == 0) {
-                        lqk_rs4_entry *e = (lqk_rs4_entry *)rs_rec_push(rec);
-                        if (e) {
-                            e->tau = x;
-                            e->i = (unsigned int)i;
-                        }
+            /* run: inputs i .. stop-1, no host checkpoint inside */
+            unsigned long long stop = (i | (RS_HCK - 1)) + 1;
+            if (stop > n) stop = n;
+            if (early && i < RS_EARLY) stop = i + 1;
+            for (; i < stop; i++) {
+                if (early && i >= RS_EARLY) {
+                    unsigned int tb;
+                    memcpy(&tb, &t, 4);
+                    if ((tb == eb[0]) | (tb == tort)) {
+                        for (int k = RS_EARLY - 1; k >= 0; k--)
+                            if (eb[k] == tb) {
+                                *q0 = (unsigned long long)k;
+                                *Kend = K;
+                                return i;
+                            }
+                        *q0 = RS_BRENT;
+                        *lam_out = i - tpos;
+                        *Kend = K;
+                        return i;
                     }
-                    x += del;
-                    K++;
-                    c++;
+                    if (i == reset) {   /* the tortoise moves to position 2^k - 1 */
+                        tort = tb;
+                        tpos = i;
+                        reset = 2 * i + 1;
+                    }
                 }
-                t = x - 1.0f;
-                if (c > 2 || (c == 0 && K > 0) || i > 0xffffffffull) rec->d4_ok = 0;
-            } else {
-                K += rs_step_p2(&t, del, z);
+                if (r3 && (i & (LQK_RS_CK - 1)) == 0) rs_rec3(rec, NULL, t, K);
+                if (r4) {   /* the output plan: (tau, input) at the recorded outputs */
+                    float x = t;
+                    unsigned int c = 0;
+                    while (x < z) {
+                        if (K < rec->kmax && ((K < rec->opre ? K : K - rec->opre) & 3) == 0) {
+                            lqk_rs4_entry *e = (lqk_rs4_entry *)rs_rec_push(rec);
+                            if (e) {
+                                e->tau = x;
+                                e->i = (unsigned int)i;
+                            }
+                        }
+                        x += del;
+                        K++;
+                        c++;
+                    }
+                    t = x - 1.0f;
+                    if (c > 2 || (c == 0 && K > 0) || i > 0xffffffffull) rec->d4_ok = 0;
+                } else {
+                    K += rs_step_p2(&t, del, z);
+                }
             }
         }
+        if (r3 && (i & (LQK_RS_CK - 1)) == 0) rs_rec3(rec, NULL, t, K);   /* the checkpoint at the end */
     } else {
         rs_state s = x0, e[RS_EARLY];
         int ne = 0;
