@@ -1,6 +1,6 @@
-// k_resamp4.hip -- resamp_crcf / resamp_cccf for rates 1 < r < 2 with a
+// k_resamp4.hip -- resamp_crcf / resamp_cccf for rates 1/2 < r < 2 with a
 // power-of-two filter-bank count (BASELINE configs[4]: r = 1.037, npfb = 64,
-// m = 7).
+// m = 7; msresamp's arbitrary stage runs at r_a in (1/2, 1)).
 //
 // Reference: src/filter/src/resamp.c:245-311 (execute: per input, while
 // b < npfb emit y = (1-mu) y_b + mu y_{b+1} and advance the timing), :352-363
@@ -39,6 +39,15 @@
 //     (t & 3) * N4 + t / 4), where the lanes' window reads, about 4/r samples
 //     apart, fall on distinct banks (r = 1.037: about one 2-way conflict per
 //     32-lane group) and the stores on distinct banks.
+// Rates 1/2 < r < 1 (the template's !UP class) run the same pipeline with
+// an output every one or two inputs: the step is tau += 1/r, the emitting
+// input ends (tau -= 1, exact: tau + 1/r >= 1 > z), and a silent input
+// follows when tau is still >= z; so s <= d_s <= 2s, the register window is
+// L + 7 samples, the passes run over q in [s, L + 2s] (15 + 16 + 17 + 18 taps
+// at L = 14), the tap table carries three zero rows either side, and a tile
+// spans up to 517 inputs (transposed with 160 slots per residue class: about
+// one 2-way conflict per 32-lane group at every rate in (1/2, 1), from a
+// simulation of the lanes' bank pattern).
 // Taps outside an output's own window are zero, so finite samples there add
 // exactly 0; a non-finite sample reaches the outputs whose register window
 // (L + 4 samples) holds it -- a superset of the reference's, as for the
@@ -55,20 +64,28 @@ namespace {
 
 constexpr int NT4 = 256;       // 4 waves per workgroup; each wave owns its tiles end to end
 constexpr int TOUT = 256;      // outputs per wave tile (4 per lane)
-constexpr int N4 = 88;         // slots per residue class of the transposed window (>= (L + 259) / 4)
+// Two rate classes share the kernel (UP = 1 < r <= 2: one or two outputs per
+// input; !UP = 1/2 < r < 1: an output every one or two inputs).  Per class:
+// slots per residue class of the transposed window (>= TSW / 4)
+template <bool UP>
+constexpr int rs4_n4() { return UP ? 88 : 160; }
 // resident workgroups per CU: five (<= 96 VGPRs) while the register window
-// (2L + 8 VGPRs) allows, else four (<= 128)
-template <int L>
-constexpr int rs4_blk() { return L <= 16 ? 5 : 4; }
+// (2 NW VGPRs) allows, else four (<= 128)
+template <int L, bool UP>
+constexpr int rs4_blk() { return UP ? (L <= 16 ? 5 : 4) : (L <= 6 ? 5 : (L <= 22 ? 4 : 3)); }
 
 // window samples of a tile: outputs k0 .. k0+255 lie on inputs i_e .. i_e+255
-// (i_e: input of the tile's table entry, at most 3 outputs before k0), and the
-// lane windows reach L samples back and 3 forward
-template <int L>
-constexpr int rs4_tsw() { return L + 259; }
+// (UP; i_e: input of the tile's table entry, at most 3 outputs before k0) or
+// i_e .. i_e+516 (!UP, two inputs per output at most), and the lane windows
+// reach L samples back and 3 (UP) or 6 (!UP) forward
+template <int L, bool UP>
+constexpr int rs4_tsw() { return UP ? L + 259 : L + 517; }
 
-template <int L>
-constexpr int rs4_rows() { return L + 5; }   // tap rows -2 .. L+2
+template <bool UP>
+constexpr int rs4_pad() { return UP ? 2 : 3; }   // zero tap rows either side
+
+template <int L, bool UP>
+constexpr int rs4_rows() { return L + 1 + 2 * rs4_pad<UP>(); }
 
 // one 8-byte LDS read, volatile: issued as its own ds_read_b64 (2 LDS cycles
 // per wave instruction), never paired into a ds_read2_b64 (8 cycles)
@@ -86,27 +103,30 @@ __device__ __forceinline__ void wave_fence()
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
-template <int L, int NPC>
-__global__ __launch_bounds__(NT4, rs4_blk<L>()) void k_resamp4(lqk_rs4_plan pl, unsigned long long g0,
+template <int L, int NPC, bool UP>
+__global__ __launch_bounds__(NT4, (rs4_blk<L, UP>())) void k_resamp4(lqk_rs4_plan pl, unsigned long long g0,
                                                       unsigned long long K0, int npfb, float del,
                                                       const float2 *__restrict__ taps2,
                                                       const float2 *__restrict__ hist,
                                                       const float2 *__restrict__ x, int n,
                                                       float2 *__restrict__ y, int nout, bool al16)
 {
-    constexpr int NR = rs4_rows<L>();
+    constexpr int NR = rs4_rows<L, UP>();
+    constexpr int PAD = rs4_pad<UP>();
+    constexpr int N4 = rs4_n4<UP>();
     constexpr int LP = (L + 3) & ~1;                 // pair stride of taps2 (host layout)
-    constexpr int TSW = rs4_tsw<L>();
+    constexpr int TSW = rs4_tsw<L, UP>();
     constexpr int NXV = (TSW + 63) / 64;             // window samples per lane
-    constexpr int NW = L + 4;                        // register window per lane
+    constexpr int NW = UP ? L + 4 : L + 7;           // register window per lane
+    constexpr int AMAX = TSW - NW;                   // last lane window start
     static_assert(TSW <= 4 * N4, "window exceeds the transposed layout");
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     const int RS = NPC ? NPC + 1 : npfb + 1;         // table row stride (== 1 mod 32 for npfb >= 32)
-    float2 *tt = reinterpret_cast<float2 *>(smem);   // tt[(p + 2) RS + b] = (h_b[p], h_{b+1}[p] - h_b[p])
+    float2 *tt = reinterpret_cast<float2 *>(smem);   // tt[(p + PAD) RS + b] = (h_b[p], h_{b+1}[p] - h_b[p])
     const int tbytes = (NR * RS * 8 + 15) & ~15;
     const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     for (int e = tid; e < NR * RS; e += NT4) {
-        const int rr = e / RS, b = e - rr * RS, p = rr - 2;
+        const int rr = e / RS, b = e - rr * RS, p = rr - PAD;
         float2 v = make_float2(0.0f, 0.0f);
         if (p >= 0 && p <= L && b <= npfb) {
             const float2 t = taps2[b * LP + p];
@@ -263,6 +283,10 @@ __global__ __launch_bounds__(NT4, rs4_blk<L>()) void k_resamp4(lqk_rs4_plan pl, 
         auto step = [&]() {
 #pragma clang fp contract(off)
             tau = tau + del;
+            if (!UP) {   // the emitting input ends (tau + del >= 1 > z)
+                tau = tau - 1.0f;
+                ii++;
+            }
             if (!(tau < z)) {
                 tau = tau - 1.0f;
                 ii++;
@@ -286,7 +310,7 @@ __global__ __launch_bounds__(NT4, rs4_blk<L>()) void k_resamp4(lqk_rs4_plan pl, 
         }
         // lane window W[q] = x[ia - L + q] = window sample a + q
         int a = ia - i_e;
-        a = a < 0 ? 0 : (a > TOUT - 1 ? TOUT - 1 : a);   // lanes past the call's outputs
+        a = a < 0 ? 0 : (a > AMAX ? AMAX : a);   // lanes past the call's outputs
         wave_fence();   // the window is in LDS
         v2f W[NW];
         {
@@ -296,13 +320,14 @@ __global__ __launch_bounds__(NT4, rs4_blk<L>()) void k_resamp4(lqk_rs4_plan pl, 
 #pragma unroll
             for (int q = 0; q < NW; q++) W[q] = pk(lds_rd8(wb[q & 3] + (q >> 2)));
         }
-        // four outputs: pass s over q in [lo, hi] (d_0 = 0, d_1 <= 1, 1 <= d_2 <= 2, 1 <= d_3 <= 3)
+        // four outputs: pass s over q in [lo, hi] (UP: d_0 = 0, d_1 <= 1,
+        // 1 <= d_2 <= 2, 1 <= d_3 <= 3; !UP: s <= d_s <= 2s)
         v2f acc[4];
 #pragma unroll
         for (int s = 0; s < 4; s++) {
             constexpr int LO[4] = {0, 0, 1, 1};
-            const int lo = LO[s], hi = L + s;
-            const float2 *tb = tt + (2 - dd[s]) * RS + bk[s];
+            const int lo = UP ? LO[s] : s, hi = UP ? L + s : L + 2 * s;
+            const float2 *tb = tt + (PAD - dd[s]) * RS + bk[s];
             const float m = mu[s];
             v2f sacc = {0.0f, 0.0f};
 #pragma unroll
@@ -351,24 +376,35 @@ __global__ __launch_bounds__(NT4, rs4_blk<L>()) void k_resamp4(lqk_rs4_plan pl, 
     }
 }
 
-template <int L>
-void launch_rs4(const lqk_rs4_plan &pl, unsigned long long g0, unsigned long long K0, int npfb, float del,
+template <int L, bool UP>
+void launch_rs4_c(const lqk_rs4_plan &pl, unsigned long long g0, unsigned long long K0, int npfb, float del,
                 const float2 *taps2, const float2 *hist, const float2 *x, int n, float2 *y, int nout, hipStream_t st)
 {
     const bool al16 = ((unsigned long long)y & 15) == 0;   // 16-byte output stores
     const int RS = npfb + 1;
-    const size_t lds = (size_t)((rs4_rows<L>() * RS * 8 + 15) & ~15) + (size_t)(NT4 / 64) * 4 * N4 * 8;
+    const size_t lds =
+        (size_t)((rs4_rows<L, UP>() * RS * 8 + 15) & ~15) + (size_t)(NT4 / 64) * 4 * rs4_n4<UP>() * 8;
     const int ntiles = (nout + TOUT - 1) / TOUT;
     const int wgs = (ntiles + NT4 / 64 - 1) / (NT4 / 64);
-    constexpr int B = rs4_blk<L>();
+    constexpr int B = rs4_blk<L, UP>();
     const int blk = lds * B <= 160 * 1024 ? B : (int)(160 * 1024 / lds);
     const int nb = wgs < 256 * blk ? wgs : 256 * blk;   // persistent: blk per CU
     if (npfb == 64)
-        hipLaunchKernelGGL((k_resamp4<L, 64>), dim3(nb), dim3(NT4), lds, st, pl, g0, K0, npfb, del, taps2, hist, x,
-                           n, y, nout, al16);
+        hipLaunchKernelGGL((k_resamp4<L, 64, UP>), dim3(nb), dim3(NT4), lds, st, pl, g0, K0, npfb, del, taps2, hist,
+                           x, n, y, nout, al16);
     else
-        hipLaunchKernelGGL((k_resamp4<L, 0>), dim3(nb), dim3(NT4), lds, st, pl, g0, K0, npfb, del, taps2, hist, x,
+        hipLaunchKernelGGL((k_resamp4<L, 0, UP>), dim3(nb), dim3(NT4), lds, st, pl, g0, K0, npfb, del, taps2, hist, x,
                            n, y, nout, al16);
+}
+
+template <int L>
+void launch_rs4(const lqk_rs4_plan &pl, unsigned long long g0, unsigned long long K0, int npfb, float del,
+                const float2 *taps2, const float2 *hist, const float2 *x, int n, float2 *y, int nout, hipStream_t st)
+{
+    if (del <= 1.0f)
+        launch_rs4_c<L, true>(pl, g0, K0, npfb, del, taps2, hist, x, n, y, nout, st);
+    else
+        launch_rs4_c<L, false>(pl, g0, K0, npfb, del, taps2, hist, x, n, y, nout, st);
 }
 
 } // namespace

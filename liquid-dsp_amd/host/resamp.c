@@ -165,12 +165,13 @@ static int rs_pow2(unsigned int npfb) { return (npfb & (npfb - 1)) == 0; }
 static int rs_p2(const lq_rs *q) { return rs_pow2(q->npfb) && q->del * (float)q->npfb >= 1.0f; }
 
 /* the output-plan kernel (k_resamp4): complex samples, tau-only timing,
- * 1 < r < 2 (del in (0.5, 1)); the walk confirms one or two outputs per input */
+ * 1/2 < r < 2 (del in (0.5, 2)); the walk confirms one or two outputs per
+ * input (del <= 1) or an output every one or two inputs (del > 1) */
 static int rs_d4_shape(const lq_rs *q)
 {
     const char *e = getenv("LQ_RESAMP_INPUT_PLAN");   /* 1: always the input-checkpoint kernel (k_resamp3) */
     if (e && strcmp(e, "1") == 0) return 0;
-    return q->kind != LQ_RRRF && rs_p2(q) && q->del > 0.5f && q->del < 1.0f && lqk_resamp4_supported(q->npfb, q->L);
+    return q->kind != LQ_RRRF && rs_p2(q) && q->del > 0.5f && q->del < 2.0f && lqk_resamp4_supported(q->npfb, q->L);
 }
 
 static void rs_put(lqk_rs_entry *e, const rs_state *s, unsigned long long K)
@@ -310,7 +311,7 @@ static unsigned long long rs_walk(lq_rs *q, rs_state x0, unsigned long long n, i
          * device records and the returns tested inline. */
         const float del = q->del, z = 1.0f - 1.0f / (float)q->npfb;
         float t = x0.tau;
-        unsigned int eb[RS_EARLY], tort;
+        unsigned int eb[RS_EARLY], tort, zr = 0;   /* zr: silent inputs in a row (output plan check) */
         unsigned long long tpos = 0, reset = 1;
         for (int k = 0; k < RS_EARLY; k++) eb[k] = 0x7fc00001u;
         memcpy(&tort, &t, 4);
@@ -380,7 +381,13 @@ static unsigned long long rs_walk(lq_rs *q, rs_state x0, unsigned long long n, i
                         c++;
                     }
                     t = x - 1.0f;
-                    if (c > 2 || (c == 0 && K > 0) || i > 0xffffffffull) rec->d4_ok = 0;
+                    if (del <= 1.0f) {
+                        if (c > 2 || (c == 0 && K > 0)) rec->d4_ok = 0;
+                    } else {   /* no two silent inputs in a row once outputs began */
+                        zr = c == 0 && K > 0 ? zr + 1 : 0;
+                        if (c > 1 || zr > 1) rec->d4_ok = 0;
+                    }
+                    if (i > 0xffffffffull) rec->d4_ok = 0;
                 } else {
                     K += rs_step_p2(&t, del, z);
                 }
@@ -1088,8 +1095,12 @@ long long liquid_mi355x_resamp_schedule4(float _rate, unsigned int _npfb, unsign
         }
         float tau = t[idx].tau;
         unsigned long long i = t[idx].i + add;
-        for (unsigned s = 0; s < (unsigned)skip; s++) {
+        for (unsigned s = 0; s < (unsigned)skip; s++) {   /* the kernel's step (k_resamp4.hip) */
             tau = tau + q.del;
+            if (q.del > 1.0f) {
+                tau = tau - 1.0f;
+                i++;
+            }
             if (!(tau < z)) {
                 tau = tau - 1.0f;
                 i++;

@@ -1,4 +1,4 @@
-"""k_resamp4 (csrc/k_resamp4.hip): resamp_crcf / _cccf at rates 1 < r < 2
+"""k_resamp4 (csrc/k_resamp4.hip): resamp_crcf / _cccf at rates 1/2 < r < 2
 with a power-of-two bank count, against the oracle (`-m gpu`).
 
 The kernel replays an output plan (an entry every fourth output, then up to
@@ -45,7 +45,10 @@ def plan_kind(request):
 
 @pytest.mark.parametrize("rate,m,npfb", [(1.037, 7, 64), (1.27115323, 13, 64), (1.5, 4, 64), (1.9, 7, 32),
                                          (1.0001, 2, 64), (1.3, 16, 256), (1.7, 10, 128), (1.11, 1, 8),
-                                         (1.00624001, 7, 64), (1.02353001, 5, 64)])
+                                         (1.00624001, 7, 64), (1.02353001, 5, 64),
+                                         # 1/2 < r < 1 (the kernel's second rate class)
+                                         (0.97, 7, 64), (0.51, 7, 64), (0.6, 13, 32), (0.825, 7, 64),
+                                         (0.75, 4, 128), (0.99, 16, 256), (0.5001, 1, 8), (0.9, 12, 64)])
 def test_resamp4_ragged_calls(plan_kind, rate, m, npfb):
     rate = float(np.float32(rate))
     r = np.random.default_rng(int(rate * 1000) + m + npfb)
@@ -77,7 +80,7 @@ def g_num(rate, npfb, a, b):
     return int(np.searchsorted(idx, b) - np.searchsorted(idx, a))
 
 
-@pytest.mark.parametrize("rate", [1.037, 1.00624001])
+@pytest.mark.parametrize("rate", [1.037, 1.00624001, 0.97])
 def test_resamp4_cccf_and_long_stream(plan_kind, rate):
     # cccf runs the complex kernel (real taps, resamp.c:117-132); 3M inputs in
     # calls of 700 001 cross the plan period twice (r = 1.037: 2^20 outputs;
@@ -93,11 +96,11 @@ def test_resamp4_cccf_and_long_stream(plan_kind, rate):
     assert G.nrm_err(y, ref) < NRM
 
 
-@pytest.mark.parametrize("off", [0, 8])
-def test_resamp4_device_pointers(off):
+@pytest.mark.parametrize("off,rate", [(0, 1.037), (8, 1.037), (0, 0.8), (8, 0.8)])
+def test_resamp4_device_pointers(off, rate):
     # device-resident call; off = 8: output pointer 8 bytes past a 16-byte
     # boundary (the kernel then stores 8 bytes at a time)
-    rate = float(np.float32(1.037))
+    rate = float(np.float32(rate))
     n = 1_000_003
     r = np.random.default_rng(5 + off)
     x = cx(r, n)
@@ -116,10 +119,11 @@ def test_resamp4_device_pointers(off):
     assert G.nrm_err(y, ref) < NRM
 
 
-def test_resamp4_matches_input_plan_kernel_bitwise_count():
+@pytest.mark.parametrize("rate", [1.037, 0.83])
+def test_resamp4_matches_input_plan_kernel_bitwise_count(rate):
     # both kernels on the same stream: identical output counts, and values
     # within float32 rounding of each other
-    rate = float(np.float32(1.037))
+    rate = float(np.float32(rate))
     r = np.random.default_rng(123)
     x = cx(r, 400_000)
     a = LQ.Resamp(rate, 7, 0.25, 60.0, 64).execute_block(x)

@@ -134,6 +134,13 @@ def _lib_schedule4(rate, npfb, nx, periodic):
     (1.7, 256, 300_000),
     (1.00624001, 64, 3_000_000),  # pre-period of 3 inputs: entries below pre, then the period's own phase
     (1.02353001, 64, 1_500_000),  # pre-period of 2 inputs
+    (0.97, 64, 300_000),          # 1/2 < r < 1: an output every one or two inputs
+    (0.51, 64, 300_000),
+    (0.6, 32, 300_000),
+    (0.825, 64, 300_000),         # msresamp r = 3.3's arbitrary stage
+    (0.75, 128, 20_000),
+    (0.99, 256, 300_000),
+    (0.9999999, 64, 9_000_000),   # period 8 388 609 inputs
 ])
 @pytest.mark.parametrize("periodic", [1, 0])
 def test_output_plan_matches_oracle_schedule(rate, npfb, nx, periodic):
@@ -156,8 +163,8 @@ def test_output_plan_matches_oracle_schedule(rate, npfb, nx, periodic):
     np.testing.assert_array_equal(idx, oidx)
 
 
-@pytest.mark.parametrize("rate", [0.97, 2.5, 3.7])
-def test_output_plan_only_between_one_and_two(rate):
-    """rates outside (1, 2) keep the input-checkpoint plan (k_resamp3)"""
+@pytest.mark.parametrize("rate", [0.45, 2.5, 3.7])
+def test_output_plan_only_between_half_and_two(rate):
+    """rates outside (1/2, 2) keep the input-checkpoint plan (k_resamp3)"""
     k, *_ = _lib_schedule4(float(np.float32(rate)), 64, 10_000, 0)
     assert k == -3
