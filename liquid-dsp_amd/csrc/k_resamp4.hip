@@ -64,15 +64,28 @@ namespace {
 
 constexpr int NT4 = 256;       // 4 waves per workgroup; each wave owns its tiles end to end
 constexpr int TOUT = 256;      // outputs per wave tile (4 per lane)
+// tap reads per group in flight: the next group is issued before the current
+// one is consumed (the volatile reads, one at a time, exposed the LDS latency
+// per tap: 0.127 -> 0.124 ms at config 5, profiles/r05_ab_experiments.txt)
+// (1 < r <= 2, L <= 16 with the two windows in flight; elsewhere the
+// grouping's register pressure spilled, and a pass issues its reads one by one)
+template <int L, bool UP, int HM>
+constexpr int rs4_rg() { return UP && HM == 0 && L <= 16 ? 4 : 1; }
+// tile windows in flight per wave: two for 1 < r <= 2 at L <= 16 (0.124 ->
+// 0.117 ms at config 5; four workgroups per CU), else one (the second set of
+// window registers spills there)
+template <int L, bool UP, int HM>
+constexpr int rs4_pf() { return UP && HM == 0 && L <= 16 ? 2 : 1; }
 // Two rate classes share the kernel (UP = 1 < r <= 2: one or two outputs per
 // input; !UP = 1/2 < r < 1: an output every one or two inputs).  Per class:
 // slots per residue class of the transposed window (>= TSW / 4)
 template <bool UP>
 constexpr int rs4_n4() { return UP ? 88 : 160; }
-// resident workgroups per CU: five (<= 96 VGPRs) while the register window
-// (2 NW VGPRs) allows, else four (<= 128)
+// resident workgroups per CU: four (<= 128 VGPRs: the register window, 2 NW
+// VGPRs, and at 1 < r <= 2 two prefetched tile windows), five at 1/2 < r < 1
+// for L <= 4, three for L > 22
 template <int L, bool UP>
-constexpr int rs4_blk() { return UP ? (L <= 16 ? 5 : 4) : (L <= 6 ? 5 : (L <= 22 ? 4 : 3)); }
+constexpr int rs4_blk() { return UP ? 4 : (L <= 4 ? 5 : (L <= 22 ? 4 : 3)); }
 
 // window samples of a tile: outputs k0 .. k0+255 lie on inputs i_e .. i_e+255
 // (UP; i_e: input of the tile's table entry, at most 3 outputs before k0) or
@@ -103,14 +116,23 @@ __device__ __forceinline__ void wave_fence()
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
-template <int L, int NPC, bool UP>
-__global__ __launch_bounds__(NT4, (rs4_blk<L, UP>())) void k_resamp4(lqk_rs4_plan pl, unsigned long long g0,
+template <int L, int NPC, bool UP, int HM>
+__global__ __launch_bounds__(NT4, (HM ? 4 : rs4_blk<L, UP>())) void k_resamp4(lqk_rs4_plan pl, unsigned long long g0,
                                                       unsigned long long K0, int npfb, float del,
                                                       const float2 *__restrict__ taps2,
                                                       const float2 *__restrict__ hist,
                                                       const float2 *__restrict__ x, int n,
-                                                      float2 *__restrict__ y, int nout, bool al16)
+                                                      float2 *__restrict__ y, int nout, bool al16, lqk_rs4_hb hb)
 {
+    // HM > 0: the half-band interpolator stage (semi-length HM, 2 HM taps on
+    // the odd branch) fused behind the resampler.  A tile then computes its
+    // 256 resampler outputs starting HALO >= 2 HM - 1 outputs early, so the
+    // stage's window for the tile's TS = 256 - HALO new outputs is complete
+    // (the HALO outputs are the previous tile's, recomputed: 4.7 % at HM = 6)
+    constexpr int HW = 2 * HM;
+    constexpr int HALO = HM ? ((HW - 1 + 3) & ~3) : 0;
+    constexpr int TS = TOUT - HALO;
+    static_assert(HM == 0 || (UP && HALO >= HW && HALO < 64), "fused half-band stage shape");
     constexpr int NR = rs4_rows<L, UP>();
     constexpr int PAD = rs4_pad<UP>();
     constexpr int N4 = rs4_n4<UP>();
@@ -119,6 +141,8 @@ __global__ __launch_bounds__(NT4, (rs4_blk<L, UP>())) void k_resamp4(lqk_rs4_pla
     constexpr int NXV = (TSW + 63) / 64;             // window samples per lane
     constexpr int NW = UP ? L + 4 : L + 7;           // register window per lane
     constexpr int AMAX = TSW - NW;                   // last lane window start
+    constexpr int PF = rs4_pf<L, UP, HM>();
+    constexpr int RG = rs4_rg<L, UP, HM>();
     static_assert(TSW <= 4 * N4, "window exceeds the transposed layout");
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     const int RS = NPC ? NPC + 1 : npfb + 1;         // table row stride (== 1 mod 32 for npfb >= 32)
@@ -136,12 +160,13 @@ __global__ __launch_bounds__(NT4, (rs4_blk<L, UP>())) void k_resamp4(lqk_rs4_pla
     }
     __syncthreads();   // the only workgroup barrier
 
-    const int ntiles = (nout + TOUT - 1) / TOUT;
+    const int ntiles = (nout + TS - 1) / TS;
     const int GW = (int)gridDim.x * (NT4 / 64), gw = (int)blockIdx.x * (NT4 / 64) + wave;
     if (gw >= ntiles) return;
     float2 *win = reinterpret_cast<float2 *>(smem + tbytes) + wave * (4 * N4);
 
-    const __amdgpu_buffer_rsrc_t ry = __builtin_amdgcn_make_buffer_rsrc((void *)y, (short)0, nout * 8, 0x00020000);
+    const __amdgpu_buffer_rsrc_t ry =
+        __builtin_amdgcn_make_buffer_rsrc((void *)y, (short)0, nout * (HM ? 16 : 8), 0x00020000);
     const __amdgpu_buffer_rsrc_t rt =
         __builtin_amdgcn_make_buffer_rsrc((void *)pl.tab, (short)0, (int)(pl.ntab * 8), 0x00020000);
     typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
@@ -167,25 +192,26 @@ __global__ __launch_bounds__(NT4, (rs4_blk<L, UP>())) void k_resamp4(lqk_rs4_pla
         int skip;     // outputs from the entry to the lane's first output
     };
     struct Cur {
-        unsigned long long k0, r0, q0;
+        long long k0;   // negative: the halo of a stream's first tile (no outputs there)
+        unsigned long long r0, q0;
         bool per;
     };
-    const unsigned long long STEP = (unsigned long long)GW * TOUT;
+    const unsigned long long STEP = (unsigned long long)GW * TS;
     unsigned long long dQ = 0, dR = 0;
     if (pl.pre != ~0ull) {
         dQ = STEP / pl.QT;
         dR = STEP - dQ * pl.QT;
     }
     auto cur_fix = [&](Cur &c) {
-        c.per = c.k0 >= pl.pre;
+        c.per = c.k0 >= 0 && (unsigned long long)c.k0 >= pl.pre;
         if (c.per) {
-            const unsigned long long dt = c.k0 - pl.pre;
+            const unsigned long long dt = (unsigned long long)c.k0 - pl.pre;
             c.q0 = dt / pl.QT;
             c.r0 = dt - c.q0 * pl.QT;
         }
     };
     auto cur_next = [&](Cur &c) {
-        c.k0 += STEP;
+        c.k0 += (long long)STEP;
         if (c.per) {
             c.r0 += dR;
             c.q0 += dQ;
@@ -198,8 +224,9 @@ __global__ __launch_bounds__(NT4, (rs4_blk<L, UP>())) void k_resamp4(lqk_rs4_pla
         }
     };
     auto entry = [&](int tile, const Cur &c) -> Ent {
-        if (tile >= ntiles) return Ent{make_float2(0.0f, 0.0f), 0, 0};
-        const unsigned long long k = c.k0 + 4ull * (unsigned)lane;
+        const long long ks = c.k0 + 4ll * lane;
+        if (tile >= ntiles || ks < 0) return Ent{make_float2(0.0f, 0.0f), -(int)(unsigned)g0, 0};
+        const unsigned long long k = (unsigned long long)ks;
         unsigned long long idx;
         unsigned r4;                               // position whose low bits are the skip
         int off = -(int)(unsigned)g0;
@@ -260,7 +287,7 @@ __global__ __launch_bounds__(NT4, (rs4_blk<L, UP>())) void k_resamp4(lqk_rs4_pla
     // one wait covers both (and the stores of tile t-1), window t+1 goes to
     // LDS, tile t's outputs are stored, and the loads for t+2 / t+3 issue.
     Cur cc;
-    cc.k0 = K0 + (unsigned long long)gw * TOUT;
+    cc.k0 = (long long)K0 + (long long)gw * TS - HALO;
     cur_fix(cc);
     Ent ec = entry(gw, cc);
     cur_next(cc);
@@ -268,12 +295,21 @@ __global__ __launch_bounds__(NT4, (rs4_blk<L, UP>())) void k_resamp4(lqk_rs4_pla
     cur_next(cc);
     Ent enn = entry(gw + 2 * GW, cc);
     cur_next(cc);
-    Win wa;
+    Win wa, wb;
     fetch(gw, __builtin_amdgcn_readfirstlane(ent_i(ec)) - L, wa);
     put_window(wa);
     fetch(gw + GW, __builtin_amdgcn_readfirstlane(ent_i(en)) - L, wa);
+    Ent e3;
+    if constexpr (PF == 2) {   // a second window in flight
+        fetch(gw + 2 * GW, __builtin_amdgcn_readfirstlane(ent_i(enn)) - L, wb);
+        e3 = entry(gw + 3 * GW, cc);
+        cur_next(cc);
+    }
 
-    for (int tile = gw; tile < ntiles; tile += GW) {
+    const float2 *hbh = (const float2 *)hb.hist;
+    // one tile; wbuf holds the window of tile + GW and receives the window of
+    // tile + (PF + 1) GW
+    auto body = [&](const int tile, Win &wbuf) {
         // replay: the lane's entry stepped `skip` outputs, then its four
         // outputs (bank, mu, input offset d)
         const int skip = ec.skip;
@@ -330,11 +366,36 @@ __global__ __launch_bounds__(NT4, (rs4_blk<L, UP>())) void k_resamp4(lqk_rs4_pla
             const float2 *tb = tt + (PAD - dd[s]) * RS + bk[s];
             const float m = mu[s];
             v2f sacc = {0.0f, 0.0f};
+            // tap reads in groups of RG, the next group issued before the
+            // current one is consumed (one read at a time exposed the LDS
+            // latency per tap: the volatile reads are never hoisted)
+            if constexpr (RG == 1) {
 #pragma unroll
-            for (int q = lo; q <= hi; q++) {
-                const float2 t = lds_rd8(tb + q * RS);
-                const float cf = __builtin_fmaf(m, t.y, t.x);
-                sacc = v2f{cf, cf} * W[q] + sacc;
+                for (int q = lo; q <= hi; q++) {
+                    const float2 t = lds_rd8(tb + q * RS);
+                    const float cf = __builtin_fmaf(m, t.y, t.x);
+                    sacc = v2f{cf, cf} * W[q] + sacc;
+                }
+            } else {
+            float2 tg[2][RG];
+#pragma unroll
+            for (int g = 0; g < RG; g++)
+                if (lo + g <= hi) tg[0][g] = lds_rd8(tb + (lo + g) * RS);
+            __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+            for (int q0 = lo, c = 0; q0 <= hi; q0 += RG, c ^= 1) {
+#pragma unroll
+                for (int g = 0; g < RG; g++)
+                    if (q0 + RG + g <= hi) tg[c ^ 1][g] = lds_rd8(tb + (q0 + RG + g) * RS);
+                __builtin_amdgcn_sched_barrier(0);   // the group's reads stay ahead of the arithmetic
+#pragma unroll
+                for (int g = 0; g < RG; g++) {
+                    if (q0 + g > hi) break;
+                    const float2 t = tg[c][g];
+                    const float cf = __builtin_fmaf(m, t.y, t.x);
+                    sacc = v2f{cf, cf} * W[q0 + g] + sacc;
+                }
+            }
             }
             // the pass completes here (an empty asm on the result): without
             // it the compiler hoists all 64 tap reads ahead of the arithmetic
@@ -342,13 +403,79 @@ __global__ __launch_bounds__(NT4, (rs4_blk<L, UP>())) void k_resamp4(lqk_rs4_pla
             asm volatile("" : "+v"(sacc));
             acc[s] = sacc;
         }
+        const int ko = tile * TS - HALO + 4 * lane;   // call output of acc[0]
+        if constexpr (HM > 0) {
+            // the half-band stage (resamp2.c:345-360 per resampler output,
+            // msresamp.c:289-300): outputs before the call come from its window
+            if (tile == 0) {
+#pragma unroll
+                for (int s = 0; s < 4; s++) {
+                    const int k = ko + s;
+                    if (k < 0) acc[s] = k >= -HW ? pk(hbh[HW + k]) : v2f{0.0f, 0.0f};
+                }
+            }
+            if (tile == ntiles - 1) {
+                // the stage's windows after the call: u[nout - HW .. nout-1],
+                // all in the call's last tile (HALO >= HW), from history where k < 0
+                float2 *h0 = (float2 *)hb.hist_new0, *h1 = (float2 *)hb.hist_new1;
+#pragma unroll
+                for (int s = 0; s < 4; s++) {
+                    const int k = ko + s;
+                    if (k >= nout - HW && k < nout) {
+                        h0[HW - nout + k] = make_float2(acc[s].x, acc[s].y);
+                        h1[HW - nout + k] = make_float2(acc[s].x, acc[s].y);
+                    }
+                }
+            }
+            // u[t] (tile output t = 4 lane + s) through the wave's LDS; lane j
+            // then evaluates the stage at t = j + 64 s, so its two outputs per
+            // t leave as one 16-byte store and each store instruction writes
+            // 1 KB contiguous
+            wave_fence();
+            {
+                float4 *u4 = reinterpret_cast<float4 *>(win);
+                u4[2 * lane] = make_float4(acc[0].x, acc[0].y, acc[1].x, acc[1].y);
+                u4[2 * lane + 1] = make_float4(acc[2].x, acc[2].y, acc[3].x, acc[3].y);
+            }
+            wave_fence();
+            // then per t: the odd-tap dot product and the delay sample, and
+            // the two outputs 2k, 2k+1 of resampler output k = tile TS + t -
+            // HALO as one 16-byte store (the halo's t < HALO store nothing)
+#pragma unroll
+            for (int s = 0; s < 4; s++) {
+                const float2 *ub = win + lane + 64 * s - (HW - 1);   // u[t - (HW-1) + q]
+                v2f a = {0.0f, 0.0f}, d = {0.0f, 0.0f};
+#pragma unroll
+                for (int j = 0; j < HW; j++) {   // the odd-tap branch, in the order of k_resamp2
+                    const v2f v = pk(lds_rd8(ub + j));
+                    const float h = hb.h1[j];
+                    a = v2f{h, h} * v + a;
+                    if (j == HM - 1) d = v;   // the delay branch u[t - m]
+                }
+                asm volatile("" : "+v"(a));   // the pass completes here (no hoisted reads)
+                const int t = lane + 64 * s, k = tile * TS + t - HALO;
+                if (t >= HALO && k < nout) {
+                    if (al16) {
+                        u32x4 v;
+                        v.x = __float_as_uint(d.x);
+                        v.y = __float_as_uint(d.y);
+                        v.z = __float_as_uint(a.x);
+                        v.w = __float_as_uint(a.y);
+                        __builtin_amdgcn_raw_buffer_store_b128(v, ry, (unsigned)k * 16u, 0, 2);
+                    } else {
+                        __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2, d), ry, (unsigned)k * 16u, 0, 2);
+                        __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2, a), ry,
+                                                              (unsigned)k * 16u + 8u, 0, 2);
+                    }
+                }
+            }
+        }
         // the next tile's window into LDS (this tile's window reads are done)
         wave_fence();
-        put_window(wa);
-        const int ws2 = __builtin_amdgcn_readfirstlane(ent_i(enn)) - L;   // the window after it
-        // stores: outputs tile*256 + 4 lane + s, two 16-byte stores per lane
-        {
-            const int ko = tile * TOUT + 4 * lane;
+        put_window(wbuf);
+        const int ws2 = __builtin_amdgcn_readfirstlane(ent_i(PF == 2 ? e3 : enn)) - L;   // the window to fetch
+        if constexpr (HM == 0) {
+            // stores: outputs tile*256 + 4 lane + s, two 16-byte stores per lane
             u32x4 s01, s23;
             s01.x = __float_as_uint(acc[0].x);
             s01.y = __float_as_uint(acc[0].y);
@@ -368,43 +495,58 @@ __global__ __launch_bounds__(NT4, (rs4_blk<L, UP>())) void k_resamp4(lqk_rs4_pla
                                                               (unsigned)(ko + s) * 8u, 0, 2);
             }
         }
-        fetch(tile + 2 * GW, ws2, wa);
+        fetch(tile + (PF + 1) * GW, ws2, wbuf);
         ec = en;
         en = enn;
-        enn = entry(tile + 3 * GW, cc);
+        if constexpr (PF == 2) {
+            enn = e3;
+            e3 = entry(tile + 4 * GW, cc);
+        } else {
+            enn = entry(tile + 3 * GW, cc);
+        }
         cur_next(cc);
+    };
+    for (int tile = gw; tile < ntiles; tile += PF * GW) {
+        body(tile, wa);
+        if constexpr (PF == 2) {
+            if (tile + GW >= ntiles) break;
+            body(tile + GW, wb);
+        }
     }
 }
 
-template <int L, bool UP>
+template <int L, bool UP, int HM>
 void launch_rs4_c(const lqk_rs4_plan &pl, unsigned long long g0, unsigned long long K0, int npfb, float del,
-                const float2 *taps2, const float2 *hist, const float2 *x, int n, float2 *y, int nout, hipStream_t st)
+                  const float2 *taps2, const float2 *hist, const float2 *x, int n, float2 *y, int nout,
+                  const lqk_rs4_hb &hb, hipStream_t st)
 {
     const bool al16 = ((unsigned long long)y & 15) == 0;   // 16-byte output stores
     const int RS = npfb + 1;
     const size_t lds =
         (size_t)((rs4_rows<L, UP>() * RS * 8 + 15) & ~15) + (size_t)(NT4 / 64) * 4 * rs4_n4<UP>() * 8;
-    const int ntiles = (nout + TOUT - 1) / TOUT;
+    constexpr int TS = TOUT - (HM ? ((2 * HM - 1 + 3) & ~3) : 0);
+    const int ntiles = (nout + TS - 1) / TS;
     const int wgs = (ntiles + NT4 / 64 - 1) / (NT4 / 64);
-    constexpr int B = rs4_blk<L, UP>();
+    constexpr int B = HM ? 4 : rs4_blk<L, UP>();   // the fused stage's window needs the VGPRs of a fifth
     const int blk = lds * B <= 160 * 1024 ? B : (int)(160 * 1024 / lds);
     const int nb = wgs < 256 * blk ? wgs : 256 * blk;   // persistent: blk per CU
     if (npfb == 64)
-        hipLaunchKernelGGL((k_resamp4<L, 64, UP>), dim3(nb), dim3(NT4), lds, st, pl, g0, K0, npfb, del, taps2, hist,
-                           x, n, y, nout, al16);
-    else
-        hipLaunchKernelGGL((k_resamp4<L, 0, UP>), dim3(nb), dim3(NT4), lds, st, pl, g0, K0, npfb, del, taps2, hist, x,
-                           n, y, nout, al16);
+        hipLaunchKernelGGL((k_resamp4<L, 64, UP, HM>), dim3(nb), dim3(NT4), lds, st, pl, g0, K0, npfb, del, taps2,
+                           hist, x, n, y, nout, al16, hb);
+    else if constexpr (HM == 0)
+        hipLaunchKernelGGL((k_resamp4<L, 0, UP, 0>), dim3(nb), dim3(NT4), lds, st, pl, g0, K0, npfb, del, taps2,
+                           hist, x, n, y, nout, al16, hb);
 }
 
 template <int L>
 void launch_rs4(const lqk_rs4_plan &pl, unsigned long long g0, unsigned long long K0, int npfb, float del,
                 const float2 *taps2, const float2 *hist, const float2 *x, int n, float2 *y, int nout, hipStream_t st)
 {
+    const lqk_rs4_hb none{};
     if (del <= 1.0f)
-        launch_rs4_c<L, true>(pl, g0, K0, npfb, del, taps2, hist, x, n, y, nout, st);
+        launch_rs4_c<L, true, 0>(pl, g0, K0, npfb, del, taps2, hist, x, n, y, nout, none, st);
     else
-        launch_rs4_c<L, false>(pl, g0, K0, npfb, del, taps2, hist, x, n, y, nout, st);
+        launch_rs4_c<L, false, 0>(pl, g0, K0, npfb, del, taps2, hist, x, n, y, nout, none, st);
 }
 
 } // namespace
@@ -415,19 +557,39 @@ extern "C" int lqk_resamp4_supported(unsigned int npfb, unsigned int L)
     return npfb >= 2 && npfb <= 256 && (npfb & (npfb - 1)) == 0 && L >= 2 && L <= 32 && (L % 2) == 0;
 }
 
+extern "C" int lqk_resamp4_hb_supported(unsigned int npfb, unsigned int L, float del, int m)
+{
+    return npfb == 64 && L == 14 && del > 0.5f && del <= 1.0f && m >= 3 && m <= LQK_RS4_HB_MAXM;
+}
+
 extern "C" void lqk_resamp4(const lqk_rs4_plan *pl, unsigned long long g0, unsigned long long K0, unsigned int npfb,
                             unsigned int L, float del, const void *taps2, const void *hist, const void *x,
-                            unsigned long long n, void *y, unsigned long long nout, void *stream)
+                            unsigned long long n, void *y, unsigned long long nout, const lqk_rs4_hb *hb,
+                            void *stream)
 {
     if (n == 0 || nout == 0) return;
-    if (!lqk_resamp4_supported(npfb, L) || n > LQK_RS_MAXN || nout * 8ull >= (1ull << 31) || pl->ntab * 8ull >= (1ull << 31) ||
-        !(pl->pre == ~0ull || (pl->QT >= TOUT && pl->npre == (pl->pre + 3) / 4))) {
+    if (!lqk_resamp4_supported(npfb, L) || n > LQK_RS_MAXN || nout * (hb ? 16ull : 8ull) >= (1ull << 31) ||
+        pl->ntab * 8ull >= (1ull << 31) || !(pl->pre == ~0ull || (pl->QT >= TOUT && pl->npre == (pl->pre + 3) / 4)) ||
+        (hb && !lqk_resamp4_hb_supported(npfb, L, del, hb->m))) {
         fprintf(stderr, "error: liquid-mi355x: resamp4 launch outside its shape (npfb %u, L %u, %llu inputs)\n", npfb, L, n);
         exit(1);
     }
     hipStream_t st = (hipStream_t)stream;
     const float2 *t2 = (const float2 *)taps2, *h = (const float2 *)hist, *xi = (const float2 *)x;
     float2 *yo = (float2 *)y;
+    if (hb) {
+        switch (hb->m) {
+#define LQ_RS4_HB(MM)                                                                                   \
+    case MM:                                                                                            \
+        launch_rs4_c<14, true, MM>(*pl, g0, K0, 64, del, t2, h, xi, (int)n, yo, (int)nout, *hb, st);    \
+        break;
+            LQ_RS4_HB(3) LQ_RS4_HB(4) LQ_RS4_HB(5) LQ_RS4_HB(6) LQ_RS4_HB(7)
+            LQ_RS4_HB(8) LQ_RS4_HB(9) LQ_RS4_HB(10) LQ_RS4_HB(11) LQ_RS4_HB(12)
+#undef LQ_RS4_HB
+        }
+        LQ_CHECK_LAUNCH();
+        return;
+    }
 #define LQ_RS4_CASE(LL)                                                                                 \
     case LL:                                                                                            \
         launch_rs4<LL>(*pl, g0, K0, (int)npfb, del, t2, h, xi, (int)n, yo, (int)nout, st);              \

@@ -197,7 +197,8 @@ void lqk_resamp(int real_io, const lqk_rs_plan *pl, unsigned long long g0, unsig
 /* taps2: (npfb+1) x LP pairs, LP = (L+3) & ~1: row b < npfb (h_b[L-p], h_{b+1}[L-p]) for p = 1..L, row
  * npfb the BOUNDARY pair (h_{npfb-1}[L-1-p], h_0[L-p]); zero elsewhere (NULL: untiled kernel) */
 /* Output plan of k_resamp4 (csrc/k_resamp4.hip: complex samples, power-of-two
- * npfb, 1 < r < 2 with one or two outputs per input over the whole plan):
+ * npfb, 1/2 < r < 2 with one or two outputs per input, or an output every one
+ * or two inputs, over the whole plan):
  * entries {tau, i} = the timing phase at which a plan output is emitted and
  * the plan input it belongs to -- tab[c] for output 4c (c < npre =
  * ceil(pre / 4)), then tab[npre + c] for output pre + 4c within one period.
@@ -213,12 +214,29 @@ typedef struct {
     unsigned long long ntab;
     unsigned long long pre, npre, QT, PT;
 } lqk_rs4_plan;
+/* msresamp's interpolating chain fused into k_resamp4: the resampler's
+ * outputs u feed one half-band interpolator stage (resamp2 interp mode,
+ * src/filter/src/resamp2.c:330-360) in registers -- y[2k] = u[k - m],
+ * y[2k+1] = sum_j h1[j] u[k+1+j-2m] -- and never reach HBM.  hist: the
+ * stage's window before the call (2m samples, oldest first, both of its
+ * windows hold the same pushes in interp mode); hist_new0 / hist_new1: its two
+ * windows after the call (written by the kernel; nout >= 1). */
+#define LQK_RS4_HB_MAXM 12
+typedef struct {
+    int m;                        /* semi-length: 3 .. LQK_RS4_HB_MAXM */
+    float h1[2 * LQK_RS4_HB_MAXM];/* odd taps h1[j] = h[4m-1-2j] (real) */
+    const void *hist;
+    void *hist_new0, *hist_new1;
+} lqk_rs4_hb;
 int lqk_resamp4_supported(unsigned int npfb, unsigned int L);
+/* the fused chain's shapes: L = 14, npfb = 64, 1 < r < 2, m in 3 .. LQK_RS4_HB_MAXM */
+int lqk_resamp4_hb_supported(unsigned int npfb, unsigned int L, float del, int m);
 /* n complex inputs x (plan inputs g0 .. g0+n) -> the nout outputs y[k - K0]
- * for plan outputs k = K0 .. K0+nout-1; taps2 and hist as lqk_resamp */
+ * for plan outputs k = K0 .. K0+nout-1; taps2 and hist as lqk_resamp.  hb
+ * (NULL: none): y receives the half-band stage's 2 nout outputs instead */
 void lqk_resamp4(const lqk_rs4_plan *pl, unsigned long long g0, unsigned long long K0, unsigned int npfb,
                  unsigned int L, float del, const void *taps2, const void *hist, const void *x, unsigned long long n,
-                 void *y, unsigned long long nout, void *stream);
+                 void *y, unsigned long long nout, const lqk_rs4_hb *hb, void *stream);
 /* firpfb_execute(i): y = scale * sum_n hpoly[i*L + n] win[L-1-n] (win: L samples, oldest first) */
 void lqk_firpfb_single(int kind, const void *hpoly, unsigned int L, unsigned int i, const void *win,
                        float scale_re, float scale_im, void *y, unsigned *flag, unsigned seq, void *stream);

@@ -123,6 +123,19 @@ void lq_rs_destroy(lq_rs *q);
 void lq_rs_reset(lq_rs *q);
 unsigned long long lq_rs_num_output(lq_rs *q, unsigned long long nx);
 void lq_rs_block_dev(lq_rs *q, const void *dx, unsigned long long nx, void *dy, unsigned long long *ny);
+/* msresamp's interpolating chain: the resampler followed by one half-band
+ * interpolator stage (resamp2 interp mode), fused into k_resamp4 where the
+ * plan allows (lqk_resamp4_hb_supported) and run as two kernels otherwise */
+typedef struct {
+    int m;                        /* the stage's semi-length */
+    float h1[LQK_RS4_HB_MAXM * 2];/* its odd taps (real) */
+    void *w[2][2];                /* its ping-pong windows [buffer][window] */
+    int *cur;                     /* its current buffer, flipped per fused launch */
+    void (*run)(void *ctx, const void *u, unsigned long long n, void *y);   /* the stage alone: n -> 2n */
+    void *ctx;
+} lq_rs_hb;
+void lq_rs_block_dev_hb(lq_rs *q, const void *dx, unsigned long long nx, void *dy, unsigned long long *ny,
+                        const lq_rs_hb *hb);
 lq_ctx *lq_rs_ctx(lq_rs *q);
 
 /* generic dotprod engine */

@@ -86,7 +86,7 @@ struct lq_rs_s {
     rs_state hs;                  /* timing state of the host path, valid while hs_valid */
     int hs_valid;
     lq_ctx ctx;
-    lq_devbuf xbuf, ybuf;
+    lq_devbuf xbuf, ybuf, ubuf;   /* ubuf: resampler outputs of an unfused chain chunk */
 };
 
 static const char *lq_ext[] = {"rrrf", "crcf", "cccf"};
@@ -733,6 +733,7 @@ void lq_rs_destroy(lq_rs *_q)
     lq_devbuf_free(&_q->pl.d_tab);
     lq_devbuf_free(&_q->xbuf);
     lq_devbuf_free(&_q->ybuf);
+    lq_devbuf_free(&_q->ubuf);
     lq_ctx_free(&_q->ctx);
     lq_mirror_free(&_q->hm);
     free(_q->hbank);
@@ -816,8 +817,13 @@ unsigned long long lq_rs_num_output(lq_rs *_q, unsigned long long _nx)
     return total;
 }
 
-void lq_rs_block_dev(lq_rs *_q, const void *_dxv, unsigned long long _nx, void *_dyv,
-                            unsigned long long *_ny)
+void lq_rs_block_dev(lq_rs *_q, const void *_dxv, unsigned long long _nx, void *_dyv, unsigned long long *_ny)
+{
+    lq_rs_block_dev_hb(_q, _dxv, _nx, _dyv, _ny, NULL);
+}
+
+void lq_rs_block_dev_hb(lq_rs *_q, const void *_dxv, unsigned long long _nx, void *_dyv, unsigned long long *_ny,
+                        const lq_rs_hb *hb)
 {
     const char *_dx = (const char *)_dxv;
     char *_dy = (char *)_dyv;
@@ -833,21 +839,36 @@ void lq_rs_block_dev(lq_rs *_q, const void *_dxv, unsigned long long _nx, void *
         unsigned long long c = rs_ensure_plan(_q, _nx < cmax ? _nx : cmax);
         unsigned long long K0 = rs_K(_q, _q->gpos), K1 = rs_K(_q, _q->gpos + c);
         void *hold = _q->d_hist[_q->cur], *hnew = _q->d_hist[_q->cur ^ 1];
+        const unsigned long long nk = K1 - K0;
+        const int fuse = hb && nk > 0 && _q->pl.dk == RS_D4 && lqk_resamp4_hb_supported(_q->npfb, _q->L, _q->del, hb->m);
+        /* an unfused chain chunk: the resampler's outputs through ubuf */
+        char *uy = hb && !fuse ? (char *)lq_devbuf_get(&_q->ubuf, (size_t)(nk ? nk : 1) * _q->esz) : _dy;
         if (_q->pl.dk == RS_D4) {
             lqk_rs4_plan kp = {_q->pl.d_tab.p, _q->pl.d_n, _q->pl.opre, _q->pl.npre, _q->pl.QT, _q->pl.PT};
-            lqk_resamp4(&kp, _q->gpos, K0, _q->npfb, _q->L, _q->del, _q->d_taps2, hold, _dx, c, _dy, K1 - K0,
-                        _q->ctx.stream);
+            lqk_rs4_hb kh;
+            if (fuse) {
+                const int c0 = *hb->cur;
+                kh.m = hb->m;
+                memcpy(kh.h1, hb->h1, sizeof(kh.h1));
+                kh.hist = hb->w[c0][0];
+                kh.hist_new0 = hb->w[c0 ^ 1][0];
+                kh.hist_new1 = hb->w[c0 ^ 1][1];
+                *hb->cur = c0 ^ 1;
+            }
+            lqk_resamp4(&kp, _q->gpos, K0, _q->npfb, _q->L, _q->del, _q->d_taps2, hold, _dx, c, uy, nk,
+                        fuse ? &kh : NULL, _q->ctx.stream);
         } else {
             lqk_rs_plan kp = {_q->pl.d_tab.p, _q->pl.pre, _q->pl.P, _q->pl.Q, _q->pl.end, rs_p2(_q)};
             lqk_resamp(_q->kind == LQ_RRRF, &kp, _q->gpos, K0, _q->npfb, _q->L, _q->del, _q->d_taps, _q->d_taps2,
-                       hold, _dx, c, _dy, K1 - K0, _q->ctx.stream);
+                       hold, _dx, c, uy, nk, _q->ctx.stream);
         }
+        if (hb && !fuse && nk > 0) hb->run(hb->ctx, uy, nk, _dy);
         lqk_window_append(_q->kind != LQ_RRRF, hold, _q->L, _dx, c, hnew, _q->ctx.stream);
         _q->cur ^= 1;
         _q->gpos += c;
         _dx += c * _q->esz;
-        _dy += (K1 - K0) * _q->esz;
-        total += K1 - K0;
+        _dy += (hb ? 2 : 1) * nk * _q->esz;
+        total += (hb ? 2 : 1) * nk;
         _nx -= c;
     }
     rs_sync_now(_q);

@@ -500,12 +500,47 @@ static unsigned long long lq_ms_num_output(lq_ms *q, unsigned long long nx)
     return lq_rs_num_output(q->rs, (q->bi + nx) / q->M);
 }
 
+static void lq_ms_hb_run(void *ctx, const void *u, unsigned long long n, void *y)
+{
+    lq_r2_run_dev((lq_r2 *)ctx, LQK_R2_INTERP, u, n, y, NULL, 1.0f);
+}
+
 static void lq_ms_block_dev(lq_ms *q, const void *dx, unsigned long long nx, void *dy, unsigned long long *ny)
 {
     unsigned long long n = 0;
     if (nx > 0 && q->type == LIQUID_RESAMP_INTERP) {
+        lq_r2 *h = q->ns ? q->hb->st[q->ns - 1] : NULL;   /* the first half-band stage applied */
         if (q->ns == 0) {
             lq_rs_block_dev(q->rs, dx, nx, dy, &n);
+        } else if (q->kind != LQ_RRRF && h->m <= LQK_RS4_HB_MAXM) {
+            /* the resampler and the first half-band stage as one chain
+             * (msresamp.c:289-300: every resampler output straight into the
+             * half-band interpolator), the later stages after it */
+            lq_rs_hb hb;
+            memset(&hb, 0, sizeof(hb));
+            hb.m = (int)h->m;
+            const unsigned int cw = h->csz / 4;   /* cccf: (re, im) taps, im = 0 (f0 = 0) */
+            for (unsigned int j = 0; j < 2 * h->m; j++) hb.h1[j] = h->h[(h->h_len - 2 * j - 2) * cw];
+            for (int b = 0; b < 2; b++)
+                for (int w = 0; w < 2; w++) hb.w[b][w] = h->d_w[b][w];
+            hb.cur = &h->cur;
+            hb.run = lq_ms_hb_run;
+            hb.ctx = h;
+            const unsigned long long K = lq_rs_num_output(q->rs, nx);
+            void *t = q->ns > 1 ? lq_devbuf_get(&q->s0, (size_t)(K ? 2 * K : 1) * q->esz) : dy;
+            unsigned long long k2 = 0;
+            lq_rs_block_dev_hb(q->rs, dx, nx, t, &k2, &hb);
+            const void *in = t;
+            void *b2[2] = {NULL, NULL};
+            for (unsigned int s = 1; s < q->ns; s++) {
+                const int last = s == q->ns - 1;
+                if (!last && !b2[s & 1])
+                    b2[s & 1] = lq_devbuf_get(&q->hb->buf[s & 1], (size_t)(k2 << s) * q->esz);
+                void *out = last ? dy : b2[s & 1];
+                lq_r2_run_dev(q->hb->st[q->ns - s - 1], LQK_R2_INTERP, in, k2 << (s - 1), out, NULL, 1.0f);
+                in = out;
+            }
+            n = (k2 / 2) * q->M;
         } else {
             const unsigned long long K = lq_rs_num_output(q->rs, nx);
             void *t = lq_devbuf_get(&q->s0, (size_t)(K ? K : 1) * q->esz);

@@ -1211,6 +1211,35 @@ def test_msresamp_device_long_stream():
     assert G.nrm_err(y, ref) < NRM
 
 
+@pytest.mark.parametrize("rate,As", [(3.3, 60.0), (2.2, 40.0), (3.9, 80.0), (7.1, 100.0), (3.3, 120.0)])
+def test_msresamp_interp_chain_device_stream(rate, As):
+    # the interpolating chain (resampler + first half-band stage fused into
+    # k_resamp4, stage m = 3 .. 12; As = 120 gives m = 13: two kernels) on a
+    # 2M-sample device stream in ragged calls, two objects' outputs compared
+    # with the oracle
+    rate = float(np.float32(rate))
+    n = 1 << 21
+    r = rng(int(rate * 100 + As))
+    x = cx(r, n)
+    o = O.MsResamp(rate, As)
+    for t in (LQ.CRCF, LQ.CCCF):
+        g = LQ.MsResamp(rate, As, t=t)
+        cuts = [0, 1, 7, 300, 301, 70_001, 1_000_000, n]
+        dx = LQ.DeviceBuffer.from_array(x)
+        ys = []
+        for a, b in zip(cuts[:-1], cuts[1:]):
+            nout = g.num_output(b - a)
+            dy = LQ.DeviceBuffer(max(1, nout) * 8 + 8)
+            ny = g.execute_block_dev(dx.p + 8 * a, b - a, dy.p)
+            g.synchronize()
+            assert ny == nout
+            ys.append(dy.to_array(np.complex64, ny))
+        y = np.concatenate(ys)
+        ref = o.execute(x) if t == LQ.CRCF else ref
+        assert len(y) == len(ref)
+        assert G.nrm_err(y, ref) < NRM
+
+
 # ------------------------------------------------------------ FFT plan API
 FFTG = G.load("fft")
 R2RG = G.load("fft_r2r")

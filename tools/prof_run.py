@@ -13,7 +13,7 @@ import liquidmi as LQ  # noqa: E402
 
 p = argparse.ArgumentParser()
 p.add_argument("--iters", type=int, default=3)
-p.add_argument("--what", default="both", choices=["both", "all", "pfb2", "fir", "resamp", "fftfilt"])
+p.add_argument("--what", default="both", choices=["both", "all", "pfb2", "fir", "resamp", "fftfilt", "rs165", "ms33"])
 a = p.parse_args()
 s = torch.cuda.Stream()
 if a.what in ("both", "all", "pfb2"):
@@ -44,6 +44,26 @@ if a.what in ("all", "resamp"):
     r = LQ.Resamp(1.037, 7, 0.25, 60.0, 64)
     r.set_stream(s.cuda_stream)
     r.num_output(n)
+    for _ in range(a.iters):
+        r.execute_block_dev(x.data_ptr(), n, y.data_ptr())
+    r.synchronize()
+    r.destroy()
+if a.what == "rs165":   # the resampler alone at msresamp r = 3.3's arbitrary rate
+    n = 1 << 24
+    x = torch.rand(2 * n, device="cuda") - 0.5
+    y = torch.empty(2 * (int(n * 1.65) + 4096), device="cuda")
+    r = LQ.Resamp(1.65, 7, 0.4, 60.0, 64)
+    r.set_stream(s.cuda_stream)
+    for _ in range(a.iters):
+        r.execute_block_dev(x.data_ptr(), n, y.data_ptr())
+    r.synchronize()
+    r.destroy()
+if a.what == "ms33":   # msresamp r = 3.3: the resampler + half-band chain
+    n = 1 << 24
+    x = torch.rand(2 * n, device="cuda") - 0.5
+    y = torch.empty(2 * (int(n * 3.3) + 4096), device="cuda")
+    r = LQ.MsResamp(3.3, 60.0)
+    r.set_stream(s.cuda_stream)
     for _ in range(a.iters):
         r.execute_block_dev(x.data_ptr(), n, y.data_ptr())
     r.synchronize()
