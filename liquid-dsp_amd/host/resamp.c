@@ -577,6 +577,9 @@ static int rs_plan_build_periodic(lq_rs *q)
     return 1;
 fail:
     rs_rec_free(&q->pl.rec);
+    free(q->pl.tab);   /* the search's host checkpoints (up to RS_MAX_PERIOD / RS_HCK entries) */
+    q->pl.tab = NULL;
+    q->pl.cap = q->pl.nck = 0;
     return 0;
 }
 
@@ -1006,6 +1009,32 @@ lq_ctx *lq_rs_ctx(lq_rs *q) { return &q->ctx; }
 LQ_RESAMP_FRONT(resamp_rrrf, LQ_RRRF, float)
 LQ_RESAMP_FRONT(resamp_crcf, LQ_CRCF, liquid_float_complex)
 LQ_RESAMP_FRONT(resamp_cccf, LQ_CCCF, liquid_float_complex)
+
+/* ----------------------------------------------------------------- test hook
+ * Host-only plan memory (no GPU): builds the periodic plan of a fresh
+ * crcf object at this rate and reports the host checkpoint table's allocation
+ * and the device table's size (what the first call would upload).  Returns 1
+ * (periodic plan), 0 (none within RS_MAX_PERIOD; then *_host is what is left
+ * allocated after the failed search). */
+int liquid_mi355x_resamp_plan_bytes(float _rate, unsigned int _npfb, unsigned long long *_host,
+                                    unsigned long long *_dev, unsigned long long *_period)
+{
+    lq_rs q;
+    memset(&q, 0, sizeof(q));
+    q.kind = LQ_CRCF;
+    q.rate = _rate;
+    q.del = 1.0f / _rate;
+    q.npfb = _npfb;
+    q.L = 14;
+    q.now = rs_initial;
+    const int ok = rs_plan_build_periodic(&q);
+    *_host = (unsigned long long)q.pl.cap * sizeof(lqk_rs_entry);
+    *_dev = ok ? (unsigned long long)q.pl.rec.n * q.pl.rec.esz : 0;
+    *_period = ok ? q.pl.P : 0;
+    rs_rec_free(&q.pl.rec);
+    free(q.pl.tab);
+    return ok;
+}
 
 /* ----------------------------------------------------------------- test hook
  * Host-only check of the timing plan (no GPU): builds the plan the object

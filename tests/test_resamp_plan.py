@@ -168,3 +168,28 @@ def test_output_plan_only_between_half_and_two(rate):
     """rates outside (1/2, 2) keep the input-checkpoint plan (k_resamp3)"""
     k, *_ = _lib_schedule4(float(np.float32(rate)), 64, 10_000, 0)
     assert k == -3
+
+
+@pytest.mark.parametrize("rate,npfb", [(1.037, 64), (0.9999999, 64), (1.27115323, 64), (3.7, 64)])
+def test_plan_memory(rate, npfb):
+    """plan memory: host checkpoints every 16 inputs
+    (16-byte entries, grown by doubling) over the search walk and, for the
+    device, an entry per 4 outputs (output plan) or per 4 inputs (input
+    plan) -- r = 0.9999999 (period 8 388 609 inputs): at most 16 MB host and
+    24 MB device"""
+    L = LM.lib()
+    fn = L.liquid_mi355x_resamp_plan_bytes
+    fn.restype = C.c_int
+    fn.argtypes = [C.c_float, C.c_uint, C.POINTER(C.c_ulonglong), C.POINTER(C.c_ulonglong),
+                   C.POINTER(C.c_ulonglong)]
+    h, d, P = C.c_ulonglong(0), C.c_ulonglong(0), C.c_ulonglong(0)
+    ok = fn(float(np.float32(rate)), npfb, C.byref(h), C.byref(d), C.byref(P))
+    assert ok == 1
+    per = P.value
+    # the host table covers the search walk (Brent's tortoise runs past the
+    # period when the orbit does not return to its first states)
+    assert h.value <= 16 << 20
+    rmax = max(rate, 1.0)
+    assert d.value <= 8 * (rmax * per / 4 + 1024) + 16 * (per / 4 + 1024)
+    if rate == float(np.float32(0.9999999)):
+        assert h.value <= 16 << 20 and d.value <= 24 << 20
