@@ -192,6 +192,7 @@ __global__ __launch_bounds__(NT) void k_resamp2_tiled_b(R2Args a, const C *__res
                                                         const S *__restrict__ hist0, const S *__restrict__ hist1,
                                                         const S *__restrict__ x, S *__restrict__ y0)
 {
+    const bool al16 = ((unsigned long long)y0 & 15) == 0;
     constexpr int CT = NT * R;
     constexpr int NU = (CT + 32 - 1 + NT - 1) / NT;   // staging slots per lane (2m <= 32)
     extern __shared__ __attribute__((aligned(16))) unsigned char r2_smem[];
@@ -262,12 +263,24 @@ __global__ __launch_bounds__(NT) void k_resamp2_tiled_b(R2Args a, const C *__res
         const S yq = acc[r], yd = e0[l0 + NT * r];
         if constexpr (MODE == LQK_R2_DECIM) {
             y0[i] = r2_scale(a.scale, r2_add(yd, yq));
-        } else if constexpr (MODE == LQK_R2_ANALYZER) {
-            y0[2 * i] = r2_add(yq, yd);
-            y0[2 * i + 1] = r2_sub(yq, yd);
         } else {
-            y0[2 * i] = yd;
-            y0[2 * i + 1] = yq;
+            const S o0 = MODE == LQK_R2_ANALYZER ? r2_add(yq, yd) : yd;
+            const S o1 = MODE == LQK_R2_ANALYZER ? r2_sub(yq, yd) : yq;
+            if constexpr (sizeof(S) == 8) {
+                // the call's two outputs as one 16-byte store: each store
+                // instruction then writes 1 KB contiguous (two 8-byte stores
+                // 16 bytes apart each covered half of every line)
+                if (al16) {
+                    typedef float v4f_ __attribute__((ext_vector_type(4)));
+                    *reinterpret_cast<v4f_ *>(y0 + 2 * i) = v4f_{o0.x, o0.y, o1.x, o1.y};
+                } else {
+                    y0[2 * i] = o0;
+                    y0[2 * i + 1] = o1;
+                }
+            } else {
+                y0[2 * i] = o0;
+                y0[2 * i + 1] = o1;
+            }
         }
     }
 }
