@@ -208,6 +208,13 @@ int lg2(unsigned long long n)
     return lg;
 }
 
+template <int DIR, bool PRE>
+void bs_cols(int N1, const float2 *src, float2 *work, long long n, long long M, int N2, const float2 *ct,
+             const float2 *tfine, int sh, long long batch, hipStream_t st);
+template <int DIR, int POST>
+void bs_rows(int N2, const float2 *work, float2 *dst, long long n, long long M, int N1, const float2 *mulv, float inv,
+             long long batch, hipStream_t st);
+
 void fft_four_step(unsigned n, int dir, const void *x, void *y, long long batch, void *work, const float2 *fine,
                    hipStream_t st)
 {
@@ -215,9 +222,17 @@ void fft_four_step(unsigned n, int dir, const void *x, void *y, long long batch,
     // the larger factor on the column pass (N2 <= N1 <= 4096 for n <= 2^24): for odd lg the
     // 2^k-point column transforms with the twiddle run in registers
     const int N1 = 1 << ((lg + 1) / 2), N2 = (int)(n / (unsigned)N1);
+    // 64- / 128-point passes in registers (fft_small16xR, the Bluestein
+    // split's kernels; the LDS Stockham forms ran n = 8192 at 1.15 ms per
+    // 2^26 points)
+    const float2 *xs = (const float2 *)x;
+    float2 *ws = (float2 *)work, *ys = (float2 *)y;
     switch (N1) {
-    case 64: launch_cols<64>(x, work, n, N2, dir, batch, fine, sh, st); break;
-    case 128: launch_cols<128>(x, work, n, N2, dir, batch, fine, sh, st); break;
+    case 64:
+    case 128:
+        if (dir > 0) bs_cols<+1, false>(N1, xs, ws, n, n, N2, nullptr, fine, sh, batch, st);
+        else bs_cols<-1, false>(N1, xs, ws, n, n, N2, nullptr, fine, sh, batch, st);
+        break;
     case 256: launch_cols_r<1>(x, work, n, N2, dir, batch, fine, sh, st); break;
     case 512: launch_cols_r<2>(x, work, n, N2, dir, batch, fine, sh, st); break;
     case 1024: launch_cols_r<4>(x, work, n, N2, dir, batch, fine, sh, st); break;
@@ -225,8 +240,11 @@ void fft_four_step(unsigned n, int dir, const void *x, void *y, long long batch,
     default: launch_cols_r<16>(x, work, n, N2, dir, batch, fine, sh, st); break;
     }
     switch (N2) {
-    case 64: launch_rows<64>(work, y, n, N1, dir, batch, st); break;
-    case 128: launch_rows<128>(work, y, n, N1, dir, batch, st); break;
+    case 64:
+    case 128:
+        if (dir > 0) bs_rows<+1, 0>(N2, ws, ys, n, n, N1, nullptr, 1.0f, batch, st);
+        else bs_rows<-1, 0>(N2, ws, ys, n, n, N1, nullptr, 1.0f, batch, st);
+        break;
     case 256: launch_rows_r<1>(work, y, n, N1, dir, batch, st); break;
     case 512: launch_rows_r<2>(work, y, n, N1, dir, batch, st); break;
     case 1024: launch_rows_r<4>(work, y, n, N1, dir, batch, st); break;
@@ -430,7 +448,8 @@ __global__ __launch_bounds__(NT) void k_bs_rows_s(const float2 *__restrict__ wor
         const int k2 = e / G, gg = e - k2 * G;
         const long long k = k10 + gg + (long long)N1 * k2;
         const float2 w = lds[e];
-        if (POST == 1) dst[z * M + k] = cmul(w, mulv[k]);
+        if (POST == 0) dst[z * M + k] = w;   // the plain four-step's rows (fft_four_step)
+        else if (POST == 1) dst[z * M + k] = cmul(w, mulv[k]);
         else if (k < n) dst[z * n + k] = cscale(cmul(w, mulv[k]), inv);
     }
 }

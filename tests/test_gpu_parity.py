@@ -1267,7 +1267,7 @@ def test_fft_r2r_golden(case):
     assert np.max(np.abs(y - np.asarray(case["y"]))) < case["tol"]
 
 
-@pytest.mark.parametrize("n", [32, 64, 128, 256, 512, 2048, 4096, 8192, 1 << 15, 65536, 1 << 17, 1 << 20, 1000, 4099, 12345,
+@pytest.mark.parametrize("n", [32, 64, 128, 256, 512, 2048, 4096, 8192, 1 << 14, 1 << 15, 65536, 1 << 17, 1 << 20, 1000, 4099, 12345,
                                100003, 17,
                                3 * 4096])
 @pytest.mark.parametrize("direction", [+1, -1])

@@ -195,7 +195,7 @@ def main():
                "8 B/input + 8 B/output")
         ms_.destroy()
     # FFT API batches
-    for N in (256, 512, 1024, 2048, 4096, 65536, 12345):
+    for N in (256, 512, 1024, 2048, 4096, 8192, 16384, 65536, 12345):
         B = (1 << 26) // N
         Z = cbuf(B * N)
         pl = L.fft_create_plan(N, None, None, 1, 0)
