@@ -405,7 +405,11 @@ __global__ __launch_bounds__(NT, 2) void k_firfilt_mx(const v2f *__restrict__ wi
             const v4f r = CC ? v4f{a.x * sre - a.y * sim, a.x * sim + a.y * sre, a.z * sre - a.w * sim,
                                    a.z * sim + a.w * sre}
                              : a * sre;   // crcf: real scale per component (firfilt.c:337)
-            __builtin_amdgcn_raw_buffer_store_b128(r, ry, c < nch ? o0 + 8u * o : OOB, 0, 2);
+            // default cache policy: over five fresh buffer pairs the kernel ran
+            // 0.835-0.905 ms (mean 0.877) against 0.819-0.927 (0.891) with
+            // non-temporal stores (its time depends on where the 2 GB buffers
+            // land, r05n_firfilt_alloc.txt / r05_ab_experiments.txt)
+            __builtin_amdgcn_raw_buffer_store_b128(r, ry, c < nch ? o0 + 8u * o : OOB, 0, 0);
         }
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
         __builtin_amdgcn_wave_barrier();
