@@ -87,6 +87,58 @@ __global__ __launch_bounds__(256, WPC) void k_pat(const f4 *__restrict__ x, f4 *
     }
 }
 
+// DMA: the chunk span reaches LDS by LDS-DMA (global_load_lds_dwordx4, no
+// VGPR staging) into a ring of DEP+1 buffers, DEP chunks ahead; each chunk is
+// read back from LDS (one barrier per chunk) and stored as in the kernel.
+// Waits are explicit: after chunk k's loads a wave has issued its stores of
+// that iteration and (DEP-1) further iterations of 4 loads + 4 stores.
+template <int WPC, int DEP>
+__global__ __launch_bounds__(256, WPC) void k_dma(const f4 *__restrict__ x, f4 *__restrict__ y, long long nch)
+{
+    __shared__ f4 st[(DEP + 1) * 1056];
+    const int tid = threadIdx.x, wave = tid >> 6;
+    const long long G = gridDim.x, w = blockIdx.x;
+    const long long cnt = (nch - w + G - 1) / G;
+    auto issue = [&](long long k) {
+        const long long c = w + (k < cnt ? k : cnt - 1) * G;   // past the end: re-load the last chunk
+        f4 *buf = st + (int)(k % (DEP + 1)) * 1056;
+        if (wave == 0 && tid < 32) {
+            const f4 *hp = c > 0 ? x + c * 1024 - 32 + tid : x + tid;
+            __builtin_amdgcn_global_load_lds((const void *)hp, (__attribute__((address_space(3))) void *)(buf), 16, 0, 0);
+        }
+        const f4 *p = x + c * 1024 + tid;
+#pragma unroll
+        for (int i = 0; i < 4; i++)
+            __builtin_amdgcn_global_load_lds((const void *)(p + 256 * i),
+                                             (__attribute__((address_space(3))) void *)(buf + 32 + 256 * i + 64 * wave), 16, 0, 0);
+    };
+#pragma unroll
+    for (int d = 0; d < DEP; d++) issue(d);
+    constexpr int N = 4 + 8 * (DEP - 1);
+    constexpr int WT = (N & 15) | ((N >> 4) << 14) | (7 << 4) | (15 << 8);
+    for (long long k = 0; k < cnt; k++) {
+        __builtin_amdgcn_s_waitcnt(WT);
+        __builtin_amdgcn_s_barrier();
+        // LDS reads in asm: the compiler would otherwise wait for every
+        // outstanding LDS-DMA (vmcnt(0)) before them
+        const unsigned a0 = (unsigned)(size_t)(st + (int)(k % (DEP + 1)) * 1056);
+        const unsigned ab = a0 + 16u * (32 + tid), ah = a0 + 16u * (tid & 31);
+        f4 c[5];
+        asm volatile("ds_read_b128 %0, %1" : "=v"(c[0]) : "v"(ab));
+        asm volatile("ds_read_b128 %0, %1 offset:4096" : "=v"(c[1]) : "v"(ab));
+        asm volatile("ds_read_b128 %0, %1 offset:8192" : "=v"(c[2]) : "v"(ab));
+        asm volatile("ds_read_b128 %0, %1 offset:12288" : "=v"(c[3]) : "v"(ab));
+        asm volatile("ds_read_b128 %0, %1" : "=v"(c[4]) : "v"(ah));
+        asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(c[0]), "+v"(c[1]), "+v"(c[2]), "+v"(c[3]), "+v"(c[4]));
+        issue(k + DEP);
+        const long long ch = w + k * G;
+        f4 *q = y + ch * 1024 + tid;
+#pragma unroll
+        for (int i = 0; i < 4; i++) __builtin_nontemporal_store(c[i] + c[4], q + 256 * i);
+    }
+    __builtin_amdgcn_s_waitcnt(0xc07f & ~0xc00f);
+}
+
 struct Var {
     const char *name;
     void (*launch)(const f4 *, f4 *, long long);
@@ -97,6 +149,13 @@ void launch(const f4 *x, f4 *y, long long nch)
 {
     hipLaunchKernelGGL((k_pat<WPC, DEP, ILV, NTS, LDS>), dim3(256 * WPC), dim3(256), 0, 0, x, y, nch);
 }
+
+template <int WPC, int DEP>
+void launch_dma(const f4 *x, f4 *y, long long nch)
+{
+    hipLaunchKernelGGL((k_dma<WPC, DEP>), dim3(256 * WPC), dim3(256), 0, 0, x, y, nch);
+}
+#define D(WPC, DEP) Var{"dma wpc" #WPC " dep" #DEP, launch_dma<WPC, DEP>}
 
 #define V(WPC, DEP, ILV, NTS, LDS) Var{"wpc" #WPC " dep" #DEP " ilv" #ILV " nts" #NTS " lds" #LDS, launch<WPC, DEP, ILV, NTS, LDS>}
 
@@ -109,13 +168,18 @@ int main()
     CK(hipMalloc(&y, n * 8));
     CK(hipMemset(x, 1, n * 8));
     CK(hipMemset(y, 0, n * 8));
-    std::vector<Var> vs = {
-        V(2, 3, false, true, true),  // the kernel's pattern
-        V(2, 3, false, true, false), V(2, 3, true, true, true),  V(2, 2, true, true, true),  V(2, 1, true, true, true),
-        V(1, 3, false, true, true),  V(1, 3, true, true, true),  V(3, 2, false, true, true), V(3, 2, true, true, true),
-        V(4, 2, false, true, true),  V(4, 2, true, true, true),  V(4, 1, true, true, true),  V(2, 3, false, false, true),
-        V(2, 3, true, false, true),  V(1, 2, true, true, false), V(2, 2, true, true, false),
-    };
+    std::vector<Var> vs;
+    if (getenv("MB_DMA_ONLY") == nullptr)
+        vs = {
+            V(2, 3, false, true, true),  // the kernel's pattern
+            V(2, 3, false, true, false), V(2, 3, true, true, true),  V(2, 2, true, true, true),  V(2, 1, true, true, true),
+            V(1, 3, false, true, true),  V(1, 3, true, true, true),  V(3, 2, false, true, true), V(3, 2, true, true, true),
+            V(4, 2, false, true, true),  V(4, 2, true, true, true),  V(4, 1, true, true, true),  V(2, 3, false, false, true),
+            V(2, 3, true, false, true),  V(1, 2, true, true, false), V(2, 2, true, true, false),
+        };
+    else
+        vs = {V(2, 3, false, true, true), V(2, 1, true, true, true)};
+    for (Var v : {D(1, 2), D(1, 3), D(1, 4), D(2, 1), D(2, 2), D(2, 3), D(3, 1), D(3, 2), D(4, 1), D(4, 2)}) vs.push_back(v);
     hipEvent_t e0, e1;
     CK(hipEventCreate(&e0));
     CK(hipEventCreate(&e1));
