@@ -46,7 +46,6 @@
 
 #include <cstdint>
 #include <cstdio>
-#include <cstdlib>
 
 // crcf 33..64 taps: persistent workgroups, two per CU (A/B on one box: 0.804 ms
 // vs 0.822-0.826 at three per CU with two chunks in flight, 0.819-0.821 two
@@ -92,7 +91,8 @@ template <bool CC, int KB>
 constexpr int nal_kb() { return KB > 2 ? 3 : 0; }
 // chunks of loads in flight per workgroup (register sets): three for crcf
 // 33..64 taps, two for 65..256 taps and for cccf (two workgroups per CU each;
-// four measured the same as three)
+// four measured the same as three, and so did staging the span by LDS-DMA
+// into one raw LDS buffer, r05q in profiles/r05_ab_experiments.txt)
 template <bool CC, int KB>
 constexpr int nbuf_kb() { return CC ? 2 : (KB == 1 ? 3 : 2); }
 // elements between the eight shifted copies: at least NAL GL, and 16 mod 128
@@ -440,165 +440,6 @@ __global__ __launch_bounds__(NT, 2) void k_firfilt_mx(const v2f *__restrict__ wi
     }
 }
 
-// A/B (LQ_FMX_DMA=1): crcf 33..64 taps with the chunk span staged by LDS-DMA
-// (buffer_load_dwordx4 ... lds) into one raw buffer instead of three VGPR
-// sets.  The raw buffer holds the chunk's 16-byte units permuted within each
-// 64-byte group (unit 4t + q of lane t's 8 samples sits at 4t + ((q + t/4) & 3)),
-// so the lane-per-8-samples read-back is conflict-free.  The DMA of chunk k+1
-// is issued after step k's planes are built; step k+1 waits for it with an
-// explicit vmcnt (the step's 4 stores follow it).
-constexpr int RAW_OFF = lds_bytes_mx<false, 1>() + 80;
-constexpr int LDS_DMA = RAW_OFF + CH * 8 + 64 * 8;
-static_assert(2 * LDS_DMA <= 160 * 1024, "two workgroups per CU");
-
-__global__ __launch_bounds__(NT, 2) void k_firfilt_mx_dma(const v2f *__restrict__ win, const v2f *__restrict__ x,
-                                                          long long n, v2f *__restrict__ y,
-                                                          const float *__restrict__ hpad, float sre, long long nch,
-                                                          int hlen)
-{
-    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-    constexpr int HALO = 64, NS = 6, PLB = plb_kb<1>();
-    unsigned *sbad = reinterpret_cast<unsigned *>(smem + lds_bytes_mx<false, 1>());
-    unsigned char *planes = smem;
-    unsigned char *raw = smem + RAW_OFF;           // 2048 samples, then the 64-sample halo
-    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    const int r32 = lane & 31, hh = lane >> 5;
-    float *stage = reinterpret_cast<float *>(smem + 6 * PLB) + wave * 16 * SSTR;
-
-    bf16x8 A[3][NS];
-#pragma unroll
-    for (int s = 0; s < NS; s++) {
-        bf16x2 t[3][4];
-#pragma unroll
-        for (int q = 0; q < 4; q++) {
-            float hv[2];
-#pragma unroll
-            for (int u = 0; u < 2; u++) {
-                const int k = r32 + HALO - (16 * s + 8 * hh + 2 * q + u);
-                hv[u] = (k >= 0 && k < HALO) ? hpad[k] : 0.f;
-            }
-            split3(v2f{hv[0], hv[1]}, t[0][q], t[1][q], t[2][q]);
-        }
-#pragma unroll
-        for (int p = 0; p < 3; p++)
-            A[p][s] = bf16x8{t[p][0].x, t[p][0].y, t[p][1].x, t[p][1].y, t[p][2].x, t[p][2].y, t[p][3].x, t[p][3].y};
-    }
-    const long long G = gridDim.x, w = blockIdx.x;
-    if (w >= nch) return;
-    const long long cnt = (nch - w + G - 1) / G;
-    if (tid < 3) sbad[tid] = 0u;
-    unsigned *bad_mask = sbad + 4;
-    if (tid < 16) bad_mask[tid] = 0u;
-    const __amdgpu_buffer_rsrc_t rx = __builtin_amdgcn_make_buffer_rsrc((void *)x, (short)0, (int)(n * 8), 0x00020000);
-    const __amdgpu_buffer_rsrc_t ry = __builtin_amdgcn_make_buffer_rsrc((void *)y, (short)0, (int)(n * 8), 0x00020000);
-    const unsigned OOB = 0xfffff000u;
-    // DMA op i of this wave: LDS unit m = 256 i + 64 wave + lane holds global
-    // unit 4 (m >> 2) + (((m & 3) - (m >> 4)) & 3) of the chunk
-    auto dma = [&](long long k) {
-        const long long c = w + k * G;
-        const bool in = c < nch;
-        if (wave == 0 && lane < 32)
-            __builtin_amdgcn_raw_ptr_buffer_load_lds(
-                rx, (__attribute__((address_space(3))) void *)(raw + CH * 8),
-                16, (c > 0 && in) ? (unsigned)(CH * c - HALO) * 8u + 16u * lane : OOB, 0, 0, 0);
-#pragma unroll
-        for (int i = 0; i < 4; i++) {
-            const int m = 256 * i + 64 * wave + lane;
-            const int gu = 4 * (m >> 2) + (((m & 3) - (m >> 4)) & 3);
-            __builtin_amdgcn_raw_ptr_buffer_load_lds(
-                rx, (__attribute__((address_space(3))) void *)(raw + (256 * i + 64 * wave) * 16), 16,
-                in ? (unsigned)(CH * c) * 8u + 16u * gu : OOB, 0, 0, 0);
-        }
-    };
-    __syncthreads();
-    if (w == 0 && tid < HALO) {
-        const v2f hv = win[tid];
-        put1(planes, PLB, tid, hv);
-        if (unsafe_bits(hv.x) | unsafe_bits(hv.y)) atomicOr(&sbad[0], 1u);
-    }
-    dma(0);
-    __builtin_amdgcn_s_waitcnt(0);   // the loop's vmcnt(4) counts on a previous step's stores
-    const int sg = r32 & 15, comp = r32 >> 4;
-    const unsigned rbase = (unsigned)(size_t)(raw) + 64u * tid;
-    const int rot = (tid >> 2) & 3;
-    for (long long k = 0; k < cnt; k++) {
-        const long long c = w + k * G;
-        // this wave's DMA of chunk k is done (its 4 stores of step k-1 may
-        // still be in flight); after the barrier every wave's is, and the
-        // previous chunk's plane reads are done
-        __builtin_amdgcn_s_waitcnt((4 & 15) | (7 << 4) | (15 << 8));
-        __builtin_amdgcn_s_barrier();
-        const int cs = (int)(k % 3);
-        v4f xv[4];
-        asm volatile("ds_read_b128 %0, %1" : "=v"(xv[0]) : "v"(rbase + 16u * ((0 + rot) & 3)));
-        asm volatile("ds_read_b128 %0, %1" : "=v"(xv[1]) : "v"(rbase + 16u * ((1 + rot) & 3)));
-        asm volatile("ds_read_b128 %0, %1" : "=v"(xv[2]) : "v"(rbase + 16u * ((2 + rot) & 3)));
-        asm volatile("ds_read_b128 %0, %1" : "=v"(xv[3]) : "v"(rbase + 16u * ((3 + rot) & 3)));
-        v2f hv = {0.f, 0.f};
-        if (tid < HALO) asm volatile("ds_read_b64 %0, %1" : "=v"(hv) : "v"((unsigned)(size_t)(raw + CH * 8) + 8u * tid));
-        asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(xv[0]), "+v"(xv[1]), "+v"(xv[2]), "+v"(xv[3]), "+v"(hv));
-        if (tid < HALO && c != 0) {
-            put1(planes, PLB, tid, hv);
-            if (unsafe_bits(hv.x) | unsafe_bits(hv.y)) atomicOr(&sbad[cs], 1u);
-        }
-        put8(planes, PLB, HALO + 8 * tid, xv);
-        if (unsafe4(xv[0]) | unsafe4(xv[1]) | unsafe4(xv[2]) | unsafe4(xv[3])) atomicOr(&sbad[cs], 1u);
-        if (tid == 0) sbad[(cs + 1) % 3] = 0u;
-        // planes built, raw buffer free: an LDS-only barrier (a workgroup
-        // fence would also wait for the previous chunk's stores)
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-        __builtin_amdgcn_s_waitcnt(0xc07f);   // lgkmcnt(0)
-        __builtin_amdgcn_s_barrier();
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-        dma(k + 1);
-        if (tid == 0 && sbad[cs] && c < nch) bad_mask[k >> 5] |= 1u << (k & 31);
-
-        f32x16 C = {};
-#pragma unroll
-        for (int s = 0; s < NS; s++) {
-            const int pos = 512 * wave + 32 * sg + 16 * s + 8 * hh;
-            const unsigned char *bp = planes + comp * PLB + poff(pos);
-            const bf16x8 b0 = *reinterpret_cast<const bf16x8 *>(bp);
-            const bf16x8 b1 = *reinterpret_cast<const bf16x8 *>(bp + 2 * PLB);
-            const bf16x8 b2 = *reinterpret_cast<const bf16x8 *>(bp + 4 * PLB);
-            C = __builtin_amdgcn_mfma_f32_32x32x16_bf16(A[0][s], b2, C, 0, 0, 0);
-            C = __builtin_amdgcn_mfma_f32_32x32x16_bf16(A[1][s], b1, C, 0, 0, 0);
-            C = __builtin_amdgcn_mfma_f32_32x32x16_bf16(A[2][s], b0, C, 0, 0, 0);
-            C = __builtin_amdgcn_mfma_f32_32x32x16_bf16(A[0][s], b1, C, 0, 0, 0);
-            C = __builtin_amdgcn_mfma_f32_32x32x16_bf16(A[1][s], b0, C, 0, 0, 0);
-            C = __builtin_amdgcn_mfma_f32_32x32x16_bf16(A[0][s], b0, C, 0, 0, 0);
-        }
-#pragma unroll
-        for (int r = 0; r < 16; r++) stage[sg * SSTR + 2 * ((r & 3) + 8 * (r >> 2) + 4 * hh) + comp] = C[r];
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-        __builtin_amdgcn_wave_barrier();
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-        const unsigned o0 = (unsigned)(CH * c + 512 * wave) * 8u;
-#pragma unroll
-        for (int q = 0; q < 4; q++) {
-            const int o = 2 * (lane + 64 * q);
-            const v4f a = *reinterpret_cast<const v4f *>(stage + (o >> 5) * SSTR + 2 * (o & 31)) * sre;
-            __builtin_amdgcn_raw_buffer_store_b128(a, ry, c < nch ? o0 + 8u * o : OOB, 0, 0);
-        }
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-        __builtin_amdgcn_wave_barrier();
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-    }
-    __builtin_amdgcn_s_waitcnt(0);
-    __syncthreads();
-    unsigned anybad = 0;
-#pragma unroll
-    for (int i = 0; i < 16; i++) anybad |= bad_mask[i];
-    if (anybad) {
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-        __syncthreads();
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
-        for (int k = 0; k < (int)cnt; k++)
-            if (bad_mask[k >> 5] & (1u << (k & 31)))
-                exact_chunk_c<false, HALO>(win, x, n, y, hpad, hlen, CH * (w + k * G) + 8 * tid, 8, sre, 0.f);
-    }
-}
-
 // ---------------------------------------------------------------- rrrf
 // Real samples: the 32 columns of a tile are 32 segments, so a wave's tile is
 // 1024 outputs and a chunk 4096; three bf16 planes.
@@ -834,9 +675,6 @@ static void launch_mx(const lqk_fir_desc *d, const void *hist, const void *x, lo
         hipLaunchKernelGGL((k_firfilt_mx<true, 1>), grid, dim3(NT), lds_bytes_mx<true>() + 80, st, (const v2f *)hist,
                            (const v2f *)x, n, (v2f *)y, (const float *)d->hpad, d->scale_re, d->scale_im, nch,
                            (int)d->hlen);
-    else if (getenv("LQ_FMX_DMA") != nullptr)
-        hipLaunchKernelGGL(k_firfilt_mx_dma, grid, dim3(NT), LDS_DMA, st, (const v2f *)hist, (const v2f *)x, n,
-                           (v2f *)y, (const float *)d->hpad, d->scale_re, nch, (int)d->hlen);
     else
         hipLaunchKernelGGL((k_firfilt_mx<false, 1>), grid, dim3(NT), lds_bytes_mx<false>() + 80, st, (const v2f *)hist,
                            (const v2f *)x, n, (v2f *)y, (const float *)d->hpad, d->scale_re, d->scale_im, nch,
