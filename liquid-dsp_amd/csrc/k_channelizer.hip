@@ -2175,6 +2175,75 @@ __global__ __launch_bounds__(256, 2) void k_fft4096_batch(const float2 *__restri
     }
 }
 
+// batched 8192-point transforms in one pass, one 256-thread workgroup each:
+// decimation in time over two 4096-point register transforms, X[j] = E[j] +
+// W_8192^j O[j], X[j + 4096] = E[j] - W_8192^j O[j] (E, O: the transforms of
+// the even / odd samples).  Thread t loads the pairs (x[2i], x[2i+1]), i = t +
+// 256 n, as 16-byte loads, runs fft4096_r16 on each half through the same LDS
+// scratch and combines in registers (E[t + 256 k], O[t + 256 k] are its own):
+// one read and one write of the data, where the four-step form
+// (fft_four_step) makes two of each.  W_8192^(t + 256 k) = W_8192^t W_32^k:
+// the first from sincospi in double once per thread, the second constants.
+__device__ __constant__ float2 c_w32[16] = {
+    {1.000000000f, -0.000000000f},  {0.980785280f, -0.195090322f},  {0.923879533f, -0.382683432f},
+    {0.831469612f, -0.555570233f},  {0.707106781f, -0.707106781f},  {0.555570233f, -0.831469612f},
+    {0.382683432f, -0.923879533f},  {0.195090322f, -0.980785280f},  {0.000000000f, -1.000000000f},
+    {-0.195090322f, -0.980785280f}, {-0.382683432f, -0.923879533f}, {-0.555570233f, -0.831469612f},
+    {-0.707106781f, -0.707106781f}, {-0.831469612f, -0.555570233f}, {-0.923879533f, -0.382683432f},
+    {-0.980785280f, -0.195090322f}};
+template <int DIR, bool A16>
+__global__ __launch_bounds__(256, 2) void k_fft8192_batch(const float2 *__restrict__ x, float2 *__restrict__ y,
+                                                           long long batch, float s1, float s2, int use_s1,
+                                                           int use_s2, const float2 *__restrict__ tw4096)
+{
+    __shared__ __attribute__((aligned(16))) float2 lds[FFT4096_LDS];
+    typedef float v4f __attribute__((ext_vector_type(4)));
+    const int t = threadIdx.x;
+    const tw16x2 w16 = fft4096_tw(tw4096, t);
+    double sn, cs;
+    sincospi((double)t / 4096.0, &sn, &cs);
+    const float2 wt = make_float2((float)cs, DIR > 0 ? (float)-sn : (float)sn);
+    for (long long b = blockIdx.x; b < batch; b += gridDim.x) {
+        float2 ve[16], vo[16];
+        if constexpr (A16) {
+            const v4f *xb = reinterpret_cast<const v4f *>(x + b * 8192);
+#pragma unroll
+            for (int n = 0; n < 16; n++) {
+                const v4f q = xb[t + 256 * n];
+                ve[n] = make_float2(q.x, q.y);
+                vo[n] = make_float2(q.z, q.w);
+            }
+        } else {   // x only 8-byte aligned
+            const float2 *xb = x + b * 8192;
+#pragma unroll
+            for (int n = 0; n < 16; n++) {
+                ve[n] = xb[2 * (t + 256 * n)];
+                vo[n] = xb[2 * (t + 256 * n) + 1];
+            }
+        }
+        fft4096_r16<DIR>(ve, lds, w16, t);
+        fft4096_r16<DIR>(vo, lds, w16, t);
+        float2 *yb = y + b * 8192;
+#pragma unroll
+        for (int k = 0; k < 16; k++) {
+            const float2 c = c_w32[k];
+            const float2 o = cmul(vo[k], cmul(wt, make_float2(c.x, DIR > 0 ? c.y : -c.y)));
+            float2 u0 = cadd(ve[k], o), u1 = csub(ve[k], o);
+            if (use_s1) {
+                u0 = cscale(u0, s1);
+                u1 = cscale(u1, s1);
+            }
+            if (use_s2) {
+                u0 = cscale(u0, s2);
+                u1 = cscale(u1, s2);
+            }
+            yb[t + 256 * k] = u0;
+            yb[4096 + t + 256 * k] = u1;
+        }
+        __syncthreads();   // lds is reused by the next transform
+    }
+}
+
 // batched N = 256 R point transforms (R = 1, 2, 8: 256, 512, 2048 points),
 // 16 R threads per transform, 16 / R transforms per 256-thread workgroup,
 // register passes (fft_r16x16xR); persistent over the batch
@@ -2326,6 +2395,17 @@ void fft_batch_scaled(unsigned n, int dir, const void *x, void *y, long long bat
         else
             hipLaunchKernelGGL(k_fft4096_batch<-1>, dim3(grid), dim3(256), 0, st, (const float2 *)x, (float2 *)y,
                                batch, s1, s2, u1, u2, (const float2 *)lqrt_twiddles());
+        LQ_CHECK_LAUNCH();
+        return;
+    }
+    case 8192: {
+        const unsigned grid = (unsigned)(batch < 2048 ? batch : 2048);
+        const bool a16 = ((uintptr_t)x & 15) == 0;
+        void (*k)(const float2 *, float2 *, long long, float, float, int, int, const float2 *) =
+            dir > 0 ? (a16 ? k_fft8192_batch<+1, true> : k_fft8192_batch<+1, false>)
+                    : (a16 ? k_fft8192_batch<-1, true> : k_fft8192_batch<-1, false>);
+        hipLaunchKernelGGL(k, dim3(grid), dim3(256), 0, st, (const float2 *)x, (float2 *)y, batch, s1, s2, u1, u2,
+                           (const float2 *)lqrt_twiddles());
         LQ_CHECK_LAUNCH();
         return;
     }

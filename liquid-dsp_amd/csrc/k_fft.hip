@@ -257,7 +257,7 @@ void fft_four_step(unsigned n, int dir, const void *x, void *y, long long batch,
 void fft_pow2(unsigned n, int dir, const void *x, void *y, long long batch, void *work, const float2 *fine,
               hipStream_t st)
 {
-    if (n <= 4096) lqk_fft_batch(n, dir, x, y, (unsigned long long)batch, st);
+    if (n <= 8192) lqk_fft_batch(n, dir, x, y, (unsigned long long)batch, st);   // 8192: one pass (k_fft8192_batch)
     else fft_four_step(n, dir, x, y, batch, work, fine, st);
 }
 
@@ -563,7 +563,7 @@ __global__ void k_r2r(int type, int n, const float *__restrict__ x, float *__res
 
 extern "C" size_t lqk_fft_work_bytes(unsigned int n, unsigned long long batch)
 {
-    if (n <= 4096 && (n & (n - 1)) == 0) return 0;
+    if (n <= 8192 && (n & (n - 1)) == 0) return 0;
     if ((n & (n - 1)) == 0) return (size_t)(n * batch + n / 4096) * sizeof(float2);
     if (n <= 16) return 0;
     unsigned long long M = 1;
@@ -584,7 +584,7 @@ extern "C" void lqk_fft_any(unsigned int n, int dir, const void *x, void *y, uns
         exit(1);
     }
     if (pow2) {
-        const float2 *fine = n > 4096 ? fine_table(n, (float2 *)work + (size_t)n * batch, st) : nullptr;
+        const float2 *fine = n > 8192 ? fine_table(n, (float2 *)work + (size_t)n * batch, st) : nullptr;
         fft_pow2(n, dir, x, y, (long long)batch, work, fine, st);
         return;
     }

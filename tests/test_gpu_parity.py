@@ -1314,6 +1314,29 @@ def test_fft_plan_binds_arrays_and_device_batch():
     assert G.nrm_err(Y, np.fft.ifft(X.astype(np.complex128), axis=1) * 1024) < NRM
 
 
+@pytest.mark.parametrize("off", [0, 1])
+@pytest.mark.parametrize("direction", [+1, -1])
+def test_fft8192_one_pass_inplace_offsets(off, direction):
+    # n = 8192 runs one pass (k_fft8192_batch: 16-byte pair loads when x is
+    # 16-byte aligned, 8-byte loads otherwise); in place on a device batch
+    # starting off samples into the allocation
+    n, batch = 8192, 37
+    r = rng(8192 + off)
+    X = cx(r, batch * n).reshape(batch, n)
+    host = np.zeros(batch * n + 1, np.complex64)
+    host[off:off + batch * n] = X.reshape(-1)
+    dX = LQ.DeviceBuffer.from_array(host)
+    L = LQ.lib()
+    q = L.fft_create_plan(n, None, None, direction, 0)
+    L.fft_execute_batch_dev(q, dX.p + 8 * off, dX.p + 8 * off, batch)
+    L.liquid_mi355x_device_synchronize()
+    L.fft_destroy_plan(q)
+    Y = dX.to_array(np.complex64, batch * n + 1)[off:off + batch * n].reshape(batch, n)
+    ref = np.fft.fft(X.astype(np.complex128), axis=1) if direction > 0 else \
+        np.fft.ifft(X.astype(np.complex128), axis=1) * n
+    assert G.nrm_err(Y, ref) < NRM
+
+
 # ------------------------------------------------------------ spgram
 def _db_close(a, b):
     # dB outputs compared in linear power, normwise (NRM)
