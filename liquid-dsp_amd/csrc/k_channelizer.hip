@@ -2224,10 +2224,12 @@ __global__ __launch_bounds__(256, 2) void k_fft8192_batch(const float2 *__restri
         fft4096_r16<DIR>(ve, lds, w16, t);
         fft4096_r16<DIR>(vo, lds, w16, t);
         float2 *yb = y + b * 8192;
+        float2 wtv = wt;   // through an empty asm: the twiddles are not hoisted out of the loop
+        asm volatile("" : "+v"(wtv.x), "+v"(wtv.y));
 #pragma unroll
         for (int k = 0; k < 16; k++) {
             const float2 c = c_w32[k];
-            const float2 o = cmul(vo[k], cmul(wt, make_float2(c.x, DIR > 0 ? c.y : -c.y)));
+            const float2 o = cmul(vo[k], cmul(wtv, make_float2(c.x, DIR > 0 ? c.y : -c.y)));
             float2 u0 = cadd(ve[k], o), u1 = csub(ve[k], o);
             if (use_s1) {
                 u0 = cscale(u0, s1);
@@ -2239,6 +2241,143 @@ __global__ __launch_bounds__(256, 2) void k_fft8192_batch(const float2 *__restri
             }
             yb[t + 256 * k] = u0;
             yb[4096 + t + 256 * k] = u1;
+        }
+        __syncthreads();   // lds is reused by the next transform
+    }
+}
+
+// batched 16384-point transforms in one pass, one 512-thread workgroup each:
+// radix-4 decimation in time over four 4096-point register transforms F_r of
+// x[4i + r].  Half h of the workgroup (threads 256 h ..) loads the pairs
+// (x[4i + 2h], x[4i + 2h + 1]) and transforms both (F_2h, F_2h+1, each half
+// on its own LDS scratch); with G_r = W_16384^(r k) F_r[k], k = t + 256 m,
+//   X[k + 4096 q] = P_q + Q_q,  P_q = G_0 + (-j)^q G_1,  Q_q = (-1)^q G_2 + j^q G_3
+// (forward; the inverse conjugates), so half 0 forms P, half 1 Q, and each
+// hands the other the two it needs (P_2, P_3 / Q_0, Q_1) through the LDS the
+// transforms used, eight m at a time (64 KB); half 0 writes X[k], X[k+4096],
+// half 1 X[k+8192], X[k+12288].  252 VGPRs: one workgroup per CU.
+__device__ __constant__ float2 c_w64[16] = {
+    {1.000000000f, -0.000000000f}, {0.995184727f, -0.098017140f}, {0.980785280f, -0.195090322f},
+    {0.956940336f, -0.290284677f}, {0.923879533f, -0.382683432f}, {0.881921264f, -0.471396737f},
+    {0.831469612f, -0.555570233f}, {0.773010453f, -0.634393284f}, {0.707106781f, -0.707106781f},
+    {0.634393284f, -0.773010453f}, {0.555570233f, -0.831469612f}, {0.471396737f, -0.881921264f},
+    {0.382683432f, -0.923879533f}, {0.290284677f, -0.956940336f}, {0.195090322f, -0.980785280f},
+    {0.098017140f, -0.995184727f}};
+constexpr int FFT16K_LDS = 2 * FFT4096_LDS > 8192 ? 2 * FFT4096_LDS : 8192;
+template <int DIR, bool A16>
+__global__ __launch_bounds__(512, 1) void k_fft16384_batch(const float2 *__restrict__ x, float2 *__restrict__ y,
+                                                            long long batch, float s1, float s2, int use_s1,
+                                                            int use_s2, const float2 *__restrict__ tw4096)
+{
+    __shared__ __attribute__((aligned(16))) float2 lds[FFT16K_LDS];
+    typedef float v4f __attribute__((ext_vector_type(4)));
+    // h is wave-uniform: in a scalar register its branches are scalar
+    const int h = __builtin_amdgcn_readfirstlane(threadIdx.x >> 8), t = threadIdx.x & 255;
+    const tw16x2 w16 = fft4096_tw(tw4096, t);
+    double sn, cs;
+    sincospi((double)t / 8192.0, &sn, &cs);
+    const float2 wt = make_float2((float)cs, DIR > 0 ? (float)-sn : (float)sn);   // W_16384^t
+    // P_q / Q_q of 8 m go to xch[(q' 8 + m') 256 + t], q' = 0, 1 (half 0
+    // writes P_2, P_3 at 0, half 1 Q_0, Q_1 at 4096)
+    float2 *xch = lds;
+    // the next transform's loads are issued right after this one's register
+    // transforms, so they are in flight during the exchange and the stores
+    // (0.275 -> 0.264 ms per 2^26 points; issued before the transforms, with
+    // 64 more VGPRs live through them: 0.292; the same prefetch in the 8192
+    // kernel: 0.2105 -> 0.2146, not kept)
+    auto load = [&](long long bb, float2 (&a)[16], float2 (&c)[16]) {
+        if constexpr (A16) {
+            const v4f *xb = reinterpret_cast<const v4f *>(x + bb * 16384 + 2 * h);
+#pragma unroll
+            for (int n = 0; n < 16; n++) {
+                const v4f q = xb[2 * (t + 256 * n)];
+                a[n] = make_float2(q.x, q.y);
+                c[n] = make_float2(q.z, q.w);
+            }
+        } else {
+            const float2 *xb = x + bb * 16384 + 2 * h;
+#pragma unroll
+            for (int n = 0; n < 16; n++) {
+                a[n] = xb[4 * (t + 256 * n)];
+                c[n] = xb[4 * (t + 256 * n) + 1];
+            }
+        }
+    };
+    float2 na[16], nb[16];
+    if (blockIdx.x < batch) load(blockIdx.x, na, nb);
+    for (long long b = blockIdx.x; b < batch; b += gridDim.x) {
+        float2 va[16], vb[16];
+#pragma unroll
+        for (int n = 0; n < 16; n++) {
+            va[n] = na[n];
+            vb[n] = nb[n];
+        }
+        float2 *scr = lds + h * FFT4096_LDS;
+        fft4096_r16<DIR>(va, scr, w16, t);
+        fft4096_r16<DIR>(vb, scr, w16, t);
+        if (b + gridDim.x < batch) load(b + gridDim.x, na, nb);
+        float2 *yb = y + b * 16384 + 8192 * h;
+        // P_q / Q_q of k = t + 256 m: g0, g1 = G_2h, G_2h+1; jg = (-j) g1
+        // forward, j g1 inverse.  Half 0: P_0 = g0 + g1, P_1 = g0 + jg,
+        // P_2 = g0 - g1, P_3 = g0 - jg; half 1: Q_0 = g0 + g1, Q_1 = -g0 - jg,
+        // Q_2 = g0 - g1, Q_3 = -g0 + jg.  sel 0: the two this half sends, 1:
+        // the two it keeps (recomputed after the exchange rather than held:
+        // 32 VGPRs)
+        // wt through an empty asm: the twiddles stay inside the batch loop
+        // (hoisted, 48 of them took 96 VGPRs and spilled)
+        float2 wtv = wt;
+        asm volatile("" : "+v"(wtv.x), "+v"(wtv.y));
+        auto pq = [&](int m, int sel, float2 &a, float2 &c) {
+            const float2 cw = c_w64[m];
+            const float2 w1 = cmul(wtv, make_float2(cw.x, DIR > 0 ? cw.y : -cw.y));   // W^k
+            float2 g0, g1;
+            if (h == 0) {
+                g0 = va[m];
+                g1 = cmul(vb[m], w1);
+            } else {
+                const float2 w2 = cmul(w1, w1);
+                g0 = cmul(va[m], w2);
+                g1 = cmul(vb[m], cmul(w2, w1));
+            }
+            const float2 jg = DIR > 0 ? make_float2(g1.y, -g1.x) : make_float2(-g1.y, g1.x);
+            const bool first = (h == 0) == (sel == 1);   // P_0, P_1 / Q_0, Q_1
+            if (first) {
+                a = cadd(g0, g1);
+                c = h == 0 ? cadd(g0, jg) : make_float2(-g0.x - jg.x, -g0.y - jg.y);
+            } else {
+                a = csub(g0, g1);
+                c = h == 0 ? csub(g0, jg) : make_float2(-g0.x + jg.x, -g0.y + jg.y);
+            }
+        };
+#pragma unroll
+        for (int r = 0; r < 2; r++) {
+            __syncthreads();   // the transforms' (or the previous round's) LDS reads are done
+#pragma unroll
+            for (int mm = 0; mm < 8; mm++) {
+                float2 a, c;
+                pq(8 * r + mm, 0, a, c);
+                xch[4096 * h + mm * 256 + t] = a;
+                xch[4096 * h + 2048 + mm * 256 + t] = c;
+            }
+            __syncthreads();
+#pragma unroll
+            for (int mm = 0; mm < 8; mm++) {
+                const int k = t + 256 * (8 * r + mm);
+                float2 a, c;
+                pq(8 * r + mm, 1, a, c);
+                float2 u0 = cadd(a, xch[4096 * (1 - h) + mm * 256 + t]);
+                float2 u1 = cadd(c, xch[4096 * (1 - h) + 2048 + mm * 256 + t]);
+                if (use_s1) {
+                    u0 = cscale(u0, s1);
+                    u1 = cscale(u1, s1);
+                }
+                if (use_s2) {
+                    u0 = cscale(u0, s2);
+                    u1 = cscale(u1, s2);
+                }
+                yb[k] = u0;
+                yb[4096 + k] = u1;
+            }
         }
         __syncthreads();   // lds is reused by the next transform
     }
@@ -2405,6 +2544,17 @@ void fft_batch_scaled(unsigned n, int dir, const void *x, void *y, long long bat
             dir > 0 ? (a16 ? k_fft8192_batch<+1, true> : k_fft8192_batch<+1, false>)
                     : (a16 ? k_fft8192_batch<-1, true> : k_fft8192_batch<-1, false>);
         hipLaunchKernelGGL(k, dim3(grid), dim3(256), 0, st, (const float2 *)x, (float2 *)y, batch, s1, s2, u1, u2,
+                           (const float2 *)lqrt_twiddles());
+        LQ_CHECK_LAUNCH();
+        return;
+    }
+    case 16384: {
+        const unsigned grid = (unsigned)(batch < 1024 ? batch : 1024);
+        const bool a16 = ((uintptr_t)x & 15) == 0;
+        void (*k)(const float2 *, float2 *, long long, float, float, int, int, const float2 *) =
+            dir > 0 ? (a16 ? k_fft16384_batch<+1, true> : k_fft16384_batch<+1, false>)
+                    : (a16 ? k_fft16384_batch<-1, true> : k_fft16384_batch<-1, false>);
+        hipLaunchKernelGGL(k, dim3(grid), dim3(512), 0, st, (const float2 *)x, (float2 *)y, batch, s1, s2, u1, u2,
                            (const float2 *)lqrt_twiddles());
         LQ_CHECK_LAUNCH();
         return;

@@ -222,17 +222,12 @@ void fft_four_step(unsigned n, int dir, const void *x, void *y, long long batch,
     // the larger factor on the column pass (N2 <= N1 <= 4096 for n <= 2^24): for odd lg the
     // 2^k-point column transforms with the twiddle run in registers
     const int N1 = 1 << ((lg + 1) / 2), N2 = (int)(n / (unsigned)N1);
-    // 64- / 128-point passes in registers (fft_small16xR, the Bluestein
-    // split's kernels; the LDS Stockham forms ran n = 8192 at 1.15 ms per
-    // 2^26 points)
-    const float2 *xs = (const float2 *)x;
+    // n >= 32768 here (8192 and 16384 run in one pass): N1 >= 256; N2 = 128
+    // (n = 32768) runs its row pass in registers (fft_small16xR, the
+    // Bluestein split's kernel; with the LDS Stockham passes the four-step
+    // n = 8192 took 1.15 ms per 2^26 points, with register passes 0.43)
     float2 *ws = (float2 *)work, *ys = (float2 *)y;
     switch (N1) {
-    case 64:
-    case 128:
-        if (dir > 0) bs_cols<+1, false>(N1, xs, ws, n, n, N2, nullptr, fine, sh, batch, st);
-        else bs_cols<-1, false>(N1, xs, ws, n, n, N2, nullptr, fine, sh, batch, st);
-        break;
     case 256: launch_cols_r<1>(x, work, n, N2, dir, batch, fine, sh, st); break;
     case 512: launch_cols_r<2>(x, work, n, N2, dir, batch, fine, sh, st); break;
     case 1024: launch_cols_r<4>(x, work, n, N2, dir, batch, fine, sh, st); break;
@@ -257,7 +252,7 @@ void fft_four_step(unsigned n, int dir, const void *x, void *y, long long batch,
 void fft_pow2(unsigned n, int dir, const void *x, void *y, long long batch, void *work, const float2 *fine,
               hipStream_t st)
 {
-    if (n <= 8192) lqk_fft_batch(n, dir, x, y, (unsigned long long)batch, st);   // 8192: one pass (k_fft8192_batch)
+    if (n <= 16384) lqk_fft_batch(n, dir, x, y, (unsigned long long)batch, st);   // 8192, 16384: one pass
     else fft_four_step(n, dir, x, y, batch, work, fine, st);
 }
 
@@ -563,7 +558,7 @@ __global__ void k_r2r(int type, int n, const float *__restrict__ x, float *__res
 
 extern "C" size_t lqk_fft_work_bytes(unsigned int n, unsigned long long batch)
 {
-    if (n <= 8192 && (n & (n - 1)) == 0) return 0;
+    if (n <= 16384 && (n & (n - 1)) == 0) return 0;
     if ((n & (n - 1)) == 0) return (size_t)(n * batch + n / 4096) * sizeof(float2);
     if (n <= 16) return 0;
     unsigned long long M = 1;
@@ -584,7 +579,7 @@ extern "C" void lqk_fft_any(unsigned int n, int dir, const void *x, void *y, uns
         exit(1);
     }
     if (pow2) {
-        const float2 *fine = n > 8192 ? fine_table(n, (float2 *)work + (size_t)n * batch, st) : nullptr;
+        const float2 *fine = n > 16384 ? fine_table(n, (float2 *)work + (size_t)n * batch, st) : nullptr;
         fft_pow2(n, dir, x, y, (long long)batch, work, fine, st);
         return;
     }

@@ -1314,14 +1314,15 @@ def test_fft_plan_binds_arrays_and_device_batch():
     assert G.nrm_err(Y, np.fft.ifft(X.astype(np.complex128), axis=1) * 1024) < NRM
 
 
+@pytest.mark.parametrize("n", [8192, 16384])
 @pytest.mark.parametrize("off", [0, 1])
 @pytest.mark.parametrize("direction", [+1, -1])
-def test_fft8192_one_pass_inplace_offsets(off, direction):
-    # n = 8192 runs one pass (k_fft8192_batch: 16-byte pair loads when x is
-    # 16-byte aligned, 8-byte loads otherwise); in place on a device batch
-    # starting off samples into the allocation
-    n, batch = 8192, 37
-    r = rng(8192 + off)
+def test_fft_one_pass_large_inplace_offsets(n, off, direction):
+    # n = 8192 / 16384 run one pass (k_fft8192_batch / k_fft16384_batch:
+    # 16-byte pair loads when x is 16-byte aligned, 8-byte loads otherwise);
+    # in place on a device batch starting off samples into the allocation
+    batch = 37
+    r = rng(n + off)
     X = cx(r, batch * n).reshape(batch, n)
     host = np.zeros(batch * n + 1, np.complex64)
     host[off:off + batch * n] = X.reshape(-1)

@@ -10,7 +10,7 @@ import bench_widened as W  # noqa: E402
 
 L = W.LQ.lib()
 out = {}
-for N in (8192, 65536, 1 << 20):
+for N in (4096, 8192, 16384, 65536, 1 << 20):
     B = (1 << 26) // N
     Z = W.cbuf(B * N)
     pl = L.fft_create_plan(N, None, None, 1, 0)
