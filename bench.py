@@ -713,7 +713,7 @@ def main():
                                        "warmup_ms": fir["warm"]["warmup_ms"],
                                        "arith": ("f32-accurate: taps and samples split into three bf16 terms, "
                                                  "six exact products accumulated in f32 on "
-                                                 "v_mfma_f32_32x32x16_bf16 (k_firfilt_mx); "
+                                                 "v_mfma_f32_16x16x32_bf16 (k_firfilt_mx16); "
                                                  "LQ_FIRFILT_NO_MFMA=1 selects the f32 VALU kernel")}
         if rs is not None:
             rl_ms = g_rs / args.steps

@@ -1,35 +1,36 @@
-// k_firfilt_mx.hip -- firfilt_crcf for filters of 33..64 taps on the matrix
-// cores (the BASELINE config-1 shape, h = 64).
+// k_firfilt_mx.hip -- firfilt on the matrix cores: crcf / cccf with 33..64
+// taps (the BASELINE config-1 shape, h = 64) on 16x16x32 tiles, crcf with
+// 65..256 taps on 32x32x16 tiles, rrrf with 33..64 taps.
 //
 // Reference: src/filter/src/firfilt.c:322-359 (execute / execute_block),
 // y[t] = scale * sum_{k<h} h[k] x[t-k].  The VALU kernel (k_firfilt.hip)
 // spends 64 v_pk_fma_f32 per output and co-limits with HBM; here the
-// convolution runs as a banded-Toeplitz GEMM on v_mfma_f32_32x32x16_bf16:
+// convolution runs as a banded-Toeplitz GEMM on bf16 MFMA:
 //
-//   C[i][n] = sum_{j<96} H[i][j] B[j][n],  H[i][j] = h[i + 64 - j] (0 outside
-//   0..63),  B[j][n] = x_comp(n)[s_seg(n) - 64 + j]
+//   C[i][n] = sum_k H[i][k] B[k][n],  H[i][k] = h[i + 64 KB - k] (0 outside
+//   0..64 KB - 1),  B[k][n] = x_comp(n)[s_seg(n) - 64 KB + k]
 //
-// i = output within a 32-sample segment, n = (segment, re/im) column, so one
-// 32x32 tile is 16 segments x 2 components = 512 complex outputs, six K = 16
-// steps.  float32 accuracy is kept by splitting both operands into three
-// bf16 terms (x = x1 + x2 + x3, each the round-to-nearest bf16 of the
-// remaining residual, exact to 2^-24 relative; products of bf16 terms are
-// exact in the fp32 accumulator) and summing the six products whose order is
-// at most 2^-16: x1h1, x1h2, x2h1, x1h3, x2h2, x3h1.  The dropped terms and
-// the representation error are below 3 * 2^-24 |x||h| per tap -- the size of
-// float32 rounding; tests hold the output to the same 1e-5 normwise bound as
-// every other kernel (tests/test_gpu_parity.py).
+// i = output within a segment, n = (segment, re/im) column.  16x16x32
+// (k_firfilt_mx16): 16-output segments, a tile is 8 segments x 2 components
+// = 128 outputs, K = 96 in three steps.  32x32x16 (k_firfilt_mx): 32-output
+// segments, a tile is 16 segments x 2 = 512 outputs, 2 + 4 KB steps of 16.
+// float32 accuracy is kept by splitting both operands into three bf16 terms
+// (x = x1 + x2 + x3, each the round-to-nearest bf16 of the remaining
+// residual, exact to 2^-24 relative; products of bf16 terms are exact in the
+// fp32 accumulator) and summing the six products whose order is at most
+// 2^-16: x1h1, x1h2, x2h1, x1h3, x2h2, x3h1.  The dropped terms and the
+// representation error are below 3 * 2^-24 |x||h| per tap -- the size of
+// float32 rounding; tests hold the output to 2e-6 against a float64
+// convolution and to the same 1e-5 normwise bound as every other kernel
+// (tests/test_gpu_parity.py).
 //
-// Workgroup: 4 waves, persistent over a contiguous run of 2048-output chunks.
-// Each iteration: the 8 samples a lane prefetched are split into six bf16
-// planes (3 terms x re/im) of the chunk's 2112-sample span in LDS (16 bytes of
-// pad per 32 samples: the B-operand reads of the 16 segments of a tile land
-// on 16 distinct bank groups; the 64-sample halo comes from a small buffer the
-// previous iteration's tail lanes filled), the loads of the chunk after next
-// are issued (two chunks, 32 KB per workgroup, stay in flight), then each wave
-// runs 36 MFMAs for its 512 outputs, stages the accumulator through LDS and
-// writes 16-byte stores.  The taps' A fragments (3 terms x 6 K steps, 72
-// VGPRs) are built once per workgroup from the padded fp32 taps.
+// Workgroup: 4 waves, persistent over grid-stride 2048-output chunks.  Each
+// iteration: the 8 samples a lane prefetched are split into six bf16 planes
+// (3 terms x re/im) of the chunk's span in LDS (the 64 KB-sample halo comes
+// with the chunk), the next chunk's loads are issued, then each wave runs the
+// MFMAs for its 512 outputs and writes 16-byte stores (16x16: straight from
+// the accumulators after two DPP swaps; 32x32: staged through LDS).  The
+// taps' A fragments are built once per workgroup from the padded fp32 taps.
 //
 // Range guard.  The split is float32-accurate only for finite values whose
 // bf16 terms stay normal, and the band's zero entries multiply every sample
@@ -47,10 +48,6 @@
 #include <cstdint>
 #include <cstdio>
 
-// crcf 33..64 taps: persistent workgroups, two per CU (A/B on one box: 0.804 ms
-// vs 0.822-0.826 at three per CU with two chunks in flight, 0.819-0.821 two
-// per CU with two; profiles/r04_ab_experiments.txt)
-constexpr int FMX_WGS = 512;
 
 namespace {
 
@@ -72,9 +69,8 @@ constexpr int CH = 2048;          // outputs per chunk (4 tiles of 512)
 template <int KB>
 constexpr int plb_kb() { return ((CH + 64 * KB) * 2 + 16 * ((CH + 64 * KB) / 32) + 255) & ~255; }
 constexpr int SSTR = 68;          // floats per staged segment (32 x re/im + pad)
-// crcf: one staged accumulator per wave (49664 B: three workgroups per CU;
-// KB = 2: 53504 B and 219 VGPRs, two per CU); cccf: two (the real- and
-// imaginary-tap products; 67072 B: two per CU)
+// one staged accumulator per wave (KB = 2: 53504 B and 219 VGPRs, two
+// workgroups per CU)
 // KB > 2 (129..256 taps, crcf): the A fragments (3 terms x 2 + 4 KB steps,
 // 216 VGPRs at KB = 4) come from LDS instead: the band H[i][j] = h[i + 64 KB -
 // j] is Toeplitz, so lane row i's fragment of step s is 8 consecutive entries
@@ -87,27 +83,22 @@ constexpr int glen_kb() { return 16 * (2 + 4 * KB) + 32; }
 // taps (KB > 2), none below (taking terms 2 and 3 from LDS at KB = 1 to free
 // registers for a third chunk measured 0.915-0.925 ms against 0.803-0.805:
 // the fragment reads sit on the MFMA chain, DESIGN (f)3)
-template <bool CC, int KB>
+template <int KB>
 constexpr int nal_kb() { return KB > 2 ? 3 : 0; }
-// chunks of loads in flight per workgroup (register sets): three for crcf
-// 33..64 taps, two for 65..256 taps and for cccf (two workgroups per CU each;
-// four measured the same as three, and so did staging the span by LDS-DMA
-// into one raw LDS buffer, r05q in profiles/r05_ab_experiments.txt)
-template <bool CC, int KB>
-constexpr int nbuf_kb() { return CC ? 2 : (KB == 1 ? 3 : 2); }
+// two chunks of loads in flight per workgroup (register sets; a third
+// measured the same at KB >= 2, r04p)
 // elements between the eight shifted copies: at least NAL GL, and 16 mod 128
 // (32 B mod 256), so the 16 lanes of a ds_read_b128 pass -- eight copies at
 // two bases 16 B apart -- land on 16 distinct bank groups (a stride that is
 // a multiple of 256 B put all eight copies on the same banks)
-template <bool CC, int KB>
-constexpr int acs_kb() { return nal_kb<CC, KB>() ? ((nal_kb<CC, KB>() * glen_kb<KB>() - 16 + 127) / 128) * 128 + 16 : 0; }
-template <bool CC, int KB>
-constexpr int acp_bytes() { return 8 * acs_kb<CC, KB>() * 2; }
-template <bool CC, int KB = 1>
-constexpr int lds_bytes_mx() { return 6 * plb_kb<KB>() + (CC ? 2 : 1) * 4 * 16 * SSTR * 4 + acp_bytes<CC, KB>(); }
+template <int KB>
+constexpr int acs_kb() { return nal_kb<KB>() ? ((nal_kb<KB>() * glen_kb<KB>() - 16 + 127) / 128) * 128 + 16 : 0; }
+template <int KB>
+constexpr int acp_bytes() { return 8 * acs_kb<KB>() * 2; }
+template <int KB>
+constexpr int lds_bytes_mx() { return 6 * plb_kb<KB>() + 4 * 16 * SSTR * 4 + acp_bytes<KB>(); }
 
-static_assert(3 * (lds_bytes_mx<false, 1>() + 80) <= 160 * 1024, "crcf KB = 1: three workgroups per CU");
-static_assert(2 * (lds_bytes_mx<false, 4>() + 80) <= 160 * 1024, "crcf KB = 4: two workgroups per CU");
+static_assert(2 * (lds_bytes_mx<4>() + 80) <= 160 * 1024, "KB = 4: two workgroups per CU");
 
 __device__ __forceinline__ int poff(int pos) { return 2 * pos + 16 * (pos >> 5); }
 
@@ -215,33 +206,29 @@ __device__ __forceinline__ void load8b(__amdgpu_buffer_rsrc_t rx, unsigned off, 
     for (int q = 0; q < 4; q++) v[q] = __builtin_amdgcn_raw_buffer_load_b128(rx, off + 16 * q, 0, 0);
 }
 
-// CC: complex taps (cccf).  Then H = Hr + j Hi and the tile keeps two
-// accumulators, C1 = Hr [Xr | Xi] and C2 = Hi [Xr | Xi]; y = (C1.re - C2.im,
-// C1.im + C2.re) is formed when the staged accumulators are read back.
-template <bool CC, int KB>
+// crcf, 65..256 taps (KB = 2..4 64-tap blocks)
+template <int KB>
 __global__ __launch_bounds__(NT, 2) void k_firfilt_mx(const v2f *__restrict__ win,
                                                               const v2f *__restrict__ x, long long n,
                                                               v2f *__restrict__ y, const float *__restrict__ hpad,
-                                                              float sre, float sim, long long nch, int hlen)
+                                                              float sre, long long nch, int hlen)
 {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     // per step k % 3: nonzero if the chunk's span holds an unsafe sample;
     // kept after the dynamic region so its base stays 16-byte aligned
     constexpr int HALO = 64 * KB, NS = 2 + 4 * KB, PLB = plb_kb<KB>();
-    unsigned *sbad = reinterpret_cast<unsigned *>(smem + lds_bytes_mx<CC, KB>());
+    unsigned *sbad = reinterpret_cast<unsigned *>(smem + lds_bytes_mx<KB>());
     unsigned char *planes = smem;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int r32 = lane & 31, hh = lane >> 5;
-    constexpr int NA = CC ? 2 : 1;   // tap matrices
-    float *stage = reinterpret_cast<float *>(smem + 6 * PLB) + wave * NA * 16 * SSTR;
+    float *stage = reinterpret_cast<float *>(smem + 6 * PLB) + wave * 16 * SSTR;
 
-    // A fragments: lane (row i = r32, k half hh) holds H[i][16s + 8hh + e]
-    // (cccf: hpad holds (re, im) pairs; matrix a takes component a); terms
-    // NAR.. come from LDS per step
-    constexpr int NAL = nal_kb<CC, KB>(), NAR = 3 - NAL;
-    bf16x8 A[NA][NAR > 0 ? NAR : 1][NAR > 0 ? NS : 1];
-    __bf16 *acp = reinterpret_cast<__bf16 *>(smem + 6 * PLB + NA * 4 * 16 * SSTR * 4);
-    constexpr int GL = glen_kb<KB>(), ACS = acs_kb<CC, KB>();
+    // A fragments: lane (row i = r32, k half hh) holds H[i][16s + 8hh + e];
+    // terms NAR.. come from LDS per step
+    constexpr int NAL = nal_kb<KB>(), NAR = 3 - NAL;
+    bf16x8 A[NAR > 0 ? NAR : 1][NAR > 0 ? NS : 1];
+    __bf16 *acp = reinterpret_cast<__bf16 *>(smem + 6 * PLB + 4 * 16 * SSTR * 4);
+    constexpr int GL = glen_kb<KB>(), ACS = acs_kb<KB>();
     if constexpr (NAL > 0) {
         // copy c, term p >= NAR: G[c][p - NAR][k] = term p of g[k + c], g[k] = h[HALO + 31 - k]
         for (int e = tid; e < 8 * GL; e += NT) {
@@ -256,8 +243,6 @@ __global__ __launch_bounds__(NT, 2) void k_firfilt_mx(const v2f *__restrict__ wi
     }
     if constexpr (NAR > 0) {
 #pragma unroll
-    for (int a = 0; a < NA; a++)
-#pragma unroll
         for (int s = 0; s < NS; s++) {
             bf16x2 t[3][4];
 #pragma unroll
@@ -266,14 +251,13 @@ __global__ __launch_bounds__(NT, 2) void k_firfilt_mx(const v2f *__restrict__ wi
 #pragma unroll
                 for (int u = 0; u < 2; u++) {
                     const int k = r32 + HALO - (16 * s + 8 * hh + 2 * q + u);
-                    hv[u] = (k >= 0 && k < HALO) ? hpad[CC ? 2 * k + a : k] : 0.f;
+                    hv[u] = (k >= 0 && k < HALO) ? hpad[k] : 0.f;
                 }
                 split3(v2f{hv[0], hv[1]}, t[0][q], t[1][q], t[2][q]);
             }
 #pragma unroll
             for (int p = 0; p < NAR; p++)
-                A[a][p][s] =
-                    bf16x8{t[p][0].x, t[p][0].y, t[p][1].x, t[p][1].y, t[p][2].x, t[p][2].y, t[p][3].x, t[p][3].y};
+                A[p][s] = bf16x8{t[p][0].x, t[p][0].y, t[p][1].x, t[p][1].y, t[p][2].x, t[p][2].y, t[p][3].x, t[p][3].y};
         }
     }
     // this lane's copy (31 - r32) mod 8 and its fragment base (+ 16 s: step s; + (p - NAR) GL: term p)
@@ -317,24 +301,16 @@ __global__ __launch_bounds__(NT, 2) void k_firfilt_mx(const v2f *__restrict__ wi
         put1(planes, PLB, tid, hv);
         if (unsafe_bits(hv.x) | unsafe_bits(hv.y)) atomicOr(&sbad[0], 1u);
     }
-    // NB chunks in flight per workgroup: register sets (xa, ha) / (xb, hb)
-    // [/ (xc, hc)] rotate (the loop is unrolled by NB so no set is ever
-    // copied, which would wait on its loads early)
-    constexpr int NB = nbuf_kb<CC, KB>();
-    v4f xa[4], xb[4], xc[4], xd[4];
-    v2f ha, hb, hc, hd;
+    // two chunks in flight per workgroup: register sets (xa, ha) / (xb, hb)
+    // rotate (the loop is unrolled by two so no set is ever copied, which
+    // would wait on its loads early)
+    constexpr int NB = 2;
+    v4f xa[4], xb[4];
+    v2f ha, hb;
     load8b(rx, main_off(0), xa);
     ha = ldh(halo_off(0));
     load8b(rx, main_off(1), xb);
     hb = ldh(halo_off(1));
-    if constexpr (NB > 2) {
-        load8b(rx, main_off(2), xc);
-        hc = ldh(halo_off(2));
-    }
-    if constexpr (NB > 3) {
-        load8b(rx, main_off(3), xd);
-        hd = ldh(halo_off(3));
-    }
 
     // B operand: lane column n = r32 -> segment sg = n & 15, component n >> 4
     const int sg = r32 & 15, comp = r32 >> 4;
@@ -355,9 +331,7 @@ __global__ __launch_bounds__(NT, 2) void k_firfilt_mx(const v2f *__restrict__ wi
         __syncthreads();
         if (tid == 0 && sbad[cs] && c < nch) bad_mask[k >> 5] |= 1u << (k & 31);
 
-        f32x16 C[NA];
-#pragma unroll
-        for (int a = 0; a < NA; a++) C[a] = f32x16{};
+        f32x16 C = {};
 #pragma unroll
         for (int s = 0; s < NS; s++) {
             const int pos = 512 * wave + 32 * sg + 16 * s + 8 * hh;
@@ -369,26 +343,20 @@ __global__ __launch_bounds__(NT, 2) void k_firfilt_mx(const v2f *__restrict__ wi
             bf16x8 al[NAL > 0 ? NAL : 1];
 #pragma unroll
             for (int p = 0; p < NAL; p++) al[p] = *reinterpret_cast<const bf16x8 *>(acl + p * GL + 16 * s);
+            bf16x8 af[3];
 #pragma unroll
-            for (int a = 0; a < NA; a++) {
-                bf16x8 af[3];
-#pragma unroll
-                for (int p = 0; p < 3; p++) af[p] = p < NAR ? A[a][p < NAR ? p : 0][NAR > 0 ? s : 0] : al[p >= NAR ? p - NAR : 0];
-                C[a] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[0], b2, C[a], 0, 0, 0);
-                C[a] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[1], b1, C[a], 0, 0, 0);
-                C[a] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[2], b0, C[a], 0, 0, 0);
-                C[a] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[0], b1, C[a], 0, 0, 0);
-                C[a] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[1], b0, C[a], 0, 0, 0);
-                C[a] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[0], b0, C[a], 0, 0, 0);
-            }
+            for (int p = 0; p < 3; p++) af[p] = p < NAR ? A[p < NAR ? p : 0][NAR > 0 ? s : 0] : al[p >= NAR ? p - NAR : 0];
+            C = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[0], b2, C, 0, 0, 0);
+            C = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[1], b1, C, 0, 0, 0);
+            C = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[2], b0, C, 0, 0, 0);
+            C = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[0], b1, C, 0, 0, 0);
+            C = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[1], b0, C, 0, 0, 0);
+            C = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[0], b0, C, 0, 0, 0);
         }
 
-        // accumulator (col r32, row (r&3) + 8(r>>2) + 4hh) -> stage[a][sg][i][comp]
+        // accumulator (col r32, row (r&3) + 8(r>>2) + 4hh) -> stage[sg][i][comp]
 #pragma unroll
-        for (int a = 0; a < NA; a++)
-#pragma unroll
-            for (int r = 0; r < 16; r++)
-                stage[a * 16 * SSTR + sg * SSTR + 2 * ((r & 3) + 8 * (r >> 2) + 4 * hh) + comp] = C[a][r];
+        for (int r = 0; r < 16; r++) stage[sg * SSTR + 2 * ((r & 3) + 8 * (r >> 2) + 4 * hh) + comp] = C[r];
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
         __builtin_amdgcn_wave_barrier();
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
@@ -398,14 +366,8 @@ __global__ __launch_bounds__(NT, 2) void k_firfilt_mx(const v2f *__restrict__ wi
 #pragma unroll
         for (int q = 0; q < 4; q++) {
             const int o = 2 * (lane + 64 * q);
-            v4f a = *reinterpret_cast<const v4f *>(stage + (o >> 5) * SSTR + 2 * (o & 31));
-            if constexpr (CC) {
-                const v4f b = *reinterpret_cast<const v4f *>(stage + 16 * SSTR + (o >> 5) * SSTR + 2 * (o & 31));
-                a = v4f{a.x - b.y, a.y + b.x, a.z - b.w, a.w + b.z};
-            }
-            const v4f r = CC ? v4f{a.x * sre - a.y * sim, a.x * sim + a.y * sre, a.z * sre - a.w * sim,
-                                   a.z * sim + a.w * sre}
-                             : a * sre;   // crcf: real scale per component (firfilt.c:337)
+            const v4f r = *reinterpret_cast<const v4f *>(stage + (o >> 5) * SSTR + 2 * (o & 31)) *
+                          sre;   // crcf: real scale per component (firfilt.c:337)
             // default cache policy: over five fresh buffer pairs the kernel ran
             // 0.835-0.905 ms (mean 0.877) against 0.819-0.927 (0.891) with
             // non-temporal stores (its time depends on where the 2 GB buffers
@@ -419,13 +381,210 @@ __global__ __launch_bounds__(NT, 2) void k_firfilt_mx(const v2f *__restrict__ wi
     for (long long k = 0; k < cnt; k += NB) {
         step(k, xa, ha);
         step(k + 1, xb, hb);
-        if constexpr (NB > 2) step(k + 2, xc, hc);
-        if constexpr (NB > 3) step(k + 3, xd, hd);
     }
     // the range guard's chunks: the exact float32 outputs overwrite what the
     // matrix path stored for them.  Only workgroup-scope ordering is needed
     // (the same workgroup wrote them); no fence at all in the common case (a
     // device-scope fence here writes back L2 in every workgroup: +12 %)
+    __syncthreads();
+    unsigned anybad = 0;
+#pragma unroll
+    for (int i = 0; i < 16; i++) anybad |= bad_mask[i];
+    if (anybad) {
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+        __syncthreads();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+        for (int k = 0; k < (int)cnt; k++)
+            if (bad_mask[k >> 5] & (1u << (k & 31)))
+                exact_chunk_c<false, HALO>(win, x, n, y, hpad, hlen, CH * (w + k * G) + 8 * tid, 8, sre, 0.f);
+    }
+}
+
+// ---------------------------------------------------------------- 16x16 tiles
+// k_firfilt_mx16: 33..64 taps on v_mfma_f32_16x16x32_bf16.  A tile is 16
+// outputs x 16 columns (8 segments of 16 outputs x re/im), K = 96 in three
+// steps of 32 (the band H[i][k] = h[i + 64 - k] again), so a tap matrix's
+// fragments take 3 terms x 3 steps x 4 = 36 VGPRs (72 for cccf) against 72
+// (144) for the 32x32 form, and the 16x16 accumulator needs no LDS staging:
+// lane (col n = 2 seg + comp, row group g) holds rows 4g .. 4g+3 of one
+// component, so two DPP swaps with the partner lane (n ^ 1) pair re / im
+// (cccf: one more forms C1 -/+ C2 of the other component first), and each
+// store instruction writes 128 consecutive outputs (1 KB).  Without the stage
+// the LDS is the six bf16 planes only (26 KB): three workgroups per CU.
+// Planes: no row pad, the component-1 plane 176 mod 256 bytes after
+// component 0 (the 16 lanes of a B-operand ds_read_b128 -- 8 segments 32 B
+// apart x 2 components -- land on 16 distinct bank groups).
+constexpr int PL16 = 4272;   // >= (2112 + 16) x 2 B, == 176 mod 256
+constexpr int LDS16 = 6 * PL16 + 80;
+
+__device__ __forceinline__ void put8_16(unsigned char *planes, int pos, const v4f (&v)[4])
+{
+    bf16x2 t[3][2][4];
+#pragma unroll
+    for (int q = 0; q < 4; q++) {
+        split3(v2f{v[q].x, v[q].z}, t[0][0][q], t[1][0][q], t[2][0][q]);
+        split3(v2f{v[q].y, v[q].w}, t[0][1][q], t[1][1][q], t[2][1][q]);
+    }
+#pragma unroll
+    for (int p = 0; p < 3; p++)
+#pragma unroll
+        for (int c = 0; c < 2; c++) {
+            const u32x4 w = {__builtin_bit_cast(unsigned, t[p][c][0]), __builtin_bit_cast(unsigned, t[p][c][1]),
+                             __builtin_bit_cast(unsigned, t[p][c][2]), __builtin_bit_cast(unsigned, t[p][c][3])};
+            *reinterpret_cast<u32x4 *>(planes + (2 * p + c) * PL16 + 2 * pos) = w;
+        }
+}
+__device__ __forceinline__ void put1_16(unsigned char *planes, int pos, v2f v)
+{
+    bf16x2 t1, t2, t3;
+    split3(v, t1, t2, t3);
+    const bf16x2 t[3] = {t1, t2, t3};
+#pragma unroll
+    for (int p = 0; p < 3; p++) {
+        *reinterpret_cast<__bf16 *>(planes + (2 * p) * PL16 + 2 * pos) = t[p].x;
+        *reinterpret_cast<__bf16 *>(planes + (2 * p + 1) * PL16 + 2 * pos) = t[p].y;
+    }
+}
+// the value of lane ^ 1 (DPP quad_perm [1, 0, 3, 2])
+__device__ __forceinline__ float swap1(float v)
+{
+    return __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, v), 0xB1, 0xF, 0xF, true));
+}
+
+template <bool CC, int WPC>
+__global__ __launch_bounds__(NT, WPC) void k_firfilt_mx16(const v2f *__restrict__ win, const v2f *__restrict__ x,
+                                                        long long n, v2f *__restrict__ y,
+                                                        const float *__restrict__ hpad, float sre, float sim,
+                                                        long long nch, int hlen)
+{
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    constexpr int HALO = 64;
+    unsigned char *planes = smem;
+    unsigned *sbad = reinterpret_cast<unsigned *>(smem + 6 * PL16);
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int r16 = lane & 15, kg = lane >> 4;
+    constexpr int NA = CC ? 2 : 1;
+    typedef float f32x4 __attribute__((ext_vector_type(4)));
+
+    // A fragments: lane (row i = r16, k group kg) holds H[i][32 s + 8 kg + e]
+    bf16x8 A[NA][3][3];
+#pragma unroll
+    for (int a = 0; a < NA; a++)
+#pragma unroll
+        for (int s = 0; s < 3; s++) {
+            bf16x2 t[3][4];
+#pragma unroll
+            for (int q = 0; q < 4; q++) {
+                float hv[2];
+#pragma unroll
+                for (int u = 0; u < 2; u++) {
+                    const int k = r16 + HALO - (32 * s + 8 * kg + 2 * q + u);
+                    hv[u] = (k >= 0 && k < HALO) ? hpad[CC ? 2 * k + a : k] : 0.f;
+                }
+                split3(v2f{hv[0], hv[1]}, t[0][q], t[1][q], t[2][q]);
+            }
+#pragma unroll
+            for (int p = 0; p < 3; p++)
+                A[a][p][s] = bf16x8{t[p][0].x, t[p][0].y, t[p][1].x, t[p][1].y, t[p][2].x, t[p][2].y, t[p][3].x, t[p][3].y};
+        }
+
+    const long long G = gridDim.x, w = blockIdx.x;
+    if (w >= nch) return;
+    const long long cnt = (nch - w + G - 1) / G;
+    if (tid < 3) sbad[tid] = 0u;
+    unsigned *bad_mask = sbad + 4;
+    if (tid < 16) bad_mask[tid] = 0u;
+    // the last tile's K = 96 window reaches 16 positions past the span
+    // (H is zero there): zero them once, so 0 * garbage cannot make a NaN
+    if (tid < 6 * 24) *reinterpret_cast<__bf16 *>(planes + (tid / 24) * PL16 + 2 * (HALO + CH + tid % 24)) = __bf16(0.f);
+    const __amdgpu_buffer_rsrc_t rx = __builtin_amdgcn_make_buffer_rsrc((void *)x, (short)0, (int)(n * 8), 0x00020000);
+    const __amdgpu_buffer_rsrc_t ry = __builtin_amdgcn_make_buffer_rsrc((void *)y, (short)0, (int)(n * 8), 0x00020000);
+    const unsigned OOB = 0xfffff000u;
+    auto main_off = [&](long long k) -> unsigned {
+        const long long c = w + k * G;
+        return c < nch ? (unsigned)(CH * c + 8 * tid) * 8u : OOB;
+    };
+    auto halo_off = [&](long long k) -> unsigned {
+        const long long c = w + k * G;
+        return (c > 0 && c < nch && tid < HALO) ? (unsigned)(CH * c - HALO + tid) * 8u : OOB;
+    };
+    auto ldh = [&](unsigned off) -> v2f { return __builtin_bit_cast(v2f, __builtin_amdgcn_raw_buffer_load_b64(rx, off, 0, 0)); };
+    __syncthreads();
+    if (w == 0 && tid < HALO) {
+        const v2f hv = win[tid];
+        put1_16(planes, tid, hv);
+        if (unsafe_bits(hv.x) | unsafe_bits(hv.y)) atomicOr(&sbad[0], 1u);
+    }
+    // one chunk of loads in flight per workgroup (issued as the previous
+    // chunk's planes are written; with two or three register sets in flight
+    // the kernel measured 0.5-1.5 % / 3 % slower, r05x)
+    v4f xa[4];
+    v2f ha;
+    load8b(rx, main_off(0), xa);
+    ha = ldh(halo_off(0));
+
+    const int comp = r16 & 1, seg = r16 >> 1;
+    auto step = [&](long long k, v4f (&xv)[4], v2f &hv) {
+        const long long c = w + k * G;
+        __syncthreads();   // the previous chunk's B-operand reads are done
+        const int cs = (int)(k % 3);
+        if (tid < HALO && c != 0) {
+            put1_16(planes, tid, hv);
+            if (unsafe_bits(hv.x) | unsafe_bits(hv.y)) atomicOr(&sbad[cs], 1u);
+        }
+        put8_16(planes, HALO + 8 * tid, xv);
+        if (unsafe4(xv[0]) | unsafe4(xv[1]) | unsafe4(xv[2]) | unsafe4(xv[3])) atomicOr(&sbad[cs], 1u);
+        if (tid == 0) sbad[(cs + 1) % 3] = 0u;
+        load8b(rx, main_off(k + 1), xv);
+        hv = ldh(halo_off(k + 1));
+        __syncthreads();
+        if (tid == 0 && sbad[cs] && c < nch) bad_mask[k >> 5] |= 1u << (k & 31);
+
+#pragma unroll
+        for (int tt = 0; tt < 4; tt++) {
+            const int base = 512 * wave + 128 * tt;
+            f32x4 C[NA];
+#pragma unroll
+            for (int a = 0; a < NA; a++) C[a] = f32x4{};
+#pragma unroll
+            for (int s = 0; s < 3; s++) {
+                const unsigned char *bp = planes + comp * PL16 + 2 * (base + 16 * seg + 32 * s + 8 * kg);
+                const bf16x8 b0 = *reinterpret_cast<const bf16x8 *>(bp);
+                const bf16x8 b1 = *reinterpret_cast<const bf16x8 *>(bp + 2 * PL16);
+                const bf16x8 b2 = *reinterpret_cast<const bf16x8 *>(bp + 4 * PL16);
+#pragma unroll
+                for (int a = 0; a < NA; a++) {
+                    C[a] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(A[a][0][s], b2, C[a], 0, 0, 0);
+                    C[a] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(A[a][1][s], b1, C[a], 0, 0, 0);
+                    C[a] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(A[a][2][s], b0, C[a], 0, 0, 0);
+                    C[a] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(A[a][0][s], b1, C[a], 0, 0, 0);
+                    C[a] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(A[a][1][s], b0, C[a], 0, 0, 0);
+                    C[a] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(A[a][0][s], b0, C[a], 0, 0, 0);
+                }
+            }
+            // this lane: rows 4 kg .. 4 kg + 3 of component comp; cccf:
+            // re = Hr xr - Hi xi (C1 here, C2 of the partner), im = Hr xi + Hi xr
+            float v[4];
+#pragma unroll
+            for (int r = 0; r < 4; r++) {
+                if constexpr (CC) {
+                    const float o = swap1(C[1][r]);
+                    v[r] = comp ? C[0][r] + o : C[0][r] - o;
+                } else {
+                    v[r] = C[0][r];
+                }
+            }
+            // comp 0 keeps rows 4kg, 4kg+1 and takes their im; comp 1 rows
+            // 4kg+2, 4kg+3 and takes their re
+            const float r0 = swap1(comp ? v[0] : v[2]), r1 = swap1(comp ? v[1] : v[3]);
+            v4f o = comp ? v4f{r0, v[2], r1, v[3]} : v4f{v[0], r0, v[1], r1};
+            o = CC ? v4f{o.x * sre - o.y * sim, o.x * sim + o.y * sre, o.z * sre - o.w * sim, o.z * sim + o.w * sre}
+                   : o * sre;   // crcf: real scale per component (firfilt.c:337)
+            const unsigned off = (unsigned)(CH * c + base + 16 * seg + 4 * kg + 2 * comp) * 8u;
+            __builtin_amdgcn_raw_buffer_store_b128(o, ry, c < nch ? off : OOB, 0, 0);
+        }
+    };
+    for (long long k = 0; k < cnt; k++) step(k, xa, ha);
     __syncthreads();
     unsigned anybad = 0;
 #pragma unroll
@@ -650,35 +809,36 @@ static void launch_mx(const lqk_fir_desc *d, const void *hist, const void *x, lo
         LQ_CHECK_LAUNCH();
         return;
     }
-    const bool cc = d->kind == 2;
-    const bool kb2 = d->nchunk == 2;   // crcf, 65..128 taps
-    const int kb = (int)d->nchunk;     // crcf: 129..192 / 193..256 taps with the A fragments in LDS
     const long long nch = (n + CH - 1) / CH;
-    const long long wgs = (cc || kb2) ? 512 : FMX_WGS;   // resident workgroups (two / three per CU)
-    const dim3 grid((unsigned)(nch < wgs ? nch : wgs));
-    constexpr int lds_kb2 = lds_bytes_mx<false, 2>() + 80;
-    if (!cc && kb > 2) {
-        const dim3 g2((unsigned)(nch < 512 ? nch : 512));
-        if (kb == 3)
-            hipLaunchKernelGGL((k_firfilt_mx<false, 3>), g2, dim3(NT), (lds_bytes_mx<false, 3>() + 80), st,
-                               (const v2f *)hist, (const v2f *)x, n, (v2f *)y, (const float *)d->hpad, d->scale_re,
-                               d->scale_im, nch, (int)d->hlen);
-        else
-            hipLaunchKernelGGL((k_firfilt_mx<false, 4>), g2, dim3(NT), (lds_bytes_mx<false, 4>() + 80), st,
-                               (const v2f *)hist, (const v2f *)x, n, (v2f *)y, (const float *)d->hpad, d->scale_re,
-                               d->scale_im, nch, (int)d->hlen);
-    } else if (kb2)
-        hipLaunchKernelGGL((k_firfilt_mx<false, 2>), grid, dim3(NT), lds_kb2, st,
-                           (const v2f *)hist, (const v2f *)x, n, (v2f *)y, (const float *)d->hpad, d->scale_re,
-                           d->scale_im, nch, (int)d->hlen);
-    else if (cc)
-        hipLaunchKernelGGL((k_firfilt_mx<true, 1>), grid, dim3(NT), lds_bytes_mx<true>() + 80, st, (const v2f *)hist,
-                           (const v2f *)x, n, (v2f *)y, (const float *)d->hpad, d->scale_re, d->scale_im, nch,
-                           (int)d->hlen);
+    const int kb = (int)d->nchunk;   // 64-tap blocks
+    if (kb == 1) {
+        // crcf / cccf, 33..64 taps: the 16x16 kernel, one chunk of loads in
+        // flight, four (crcf, 94 VGPRs) / three (cccf, 155) workgroups per CU
+        if (d->kind == 2) {
+            const dim3 g((unsigned)(nch < 768 ? nch : 768));
+            hipLaunchKernelGGL((k_firfilt_mx16<true, 3>), g, dim3(NT), LDS16, st, (const v2f *)hist,
+                               (const v2f *)x, n, (v2f *)y, (const float *)d->hpad, d->scale_re, d->scale_im, nch,
+                               (int)d->hlen);
+        } else {
+            const dim3 g((unsigned)(nch < 1024 ? nch : 1024));
+            hipLaunchKernelGGL((k_firfilt_mx16<false, 4>), g, dim3(NT), LDS16, st, (const v2f *)hist,
+                               (const v2f *)x, n, (v2f *)y, (const float *)d->hpad, d->scale_re, d->scale_im, nch,
+                               (int)d->hlen);
+        }
+        LQ_CHECK_LAUNCH();
+        return;
+    }
+    // crcf, 65..256 taps: the 32x32 kernel, two workgroups per CU
+    const dim3 g2((unsigned)(nch < 512 ? nch : 512));
+    if (kb == 2)
+        hipLaunchKernelGGL((k_firfilt_mx<2>), g2, dim3(NT), (lds_bytes_mx<2>() + 80), st, (const v2f *)hist,
+                           (const v2f *)x, n, (v2f *)y, (const float *)d->hpad, d->scale_re, nch, (int)d->hlen);
+    else if (kb == 3)
+        hipLaunchKernelGGL((k_firfilt_mx<3>), g2, dim3(NT), (lds_bytes_mx<3>() + 80), st, (const v2f *)hist,
+                           (const v2f *)x, n, (v2f *)y, (const float *)d->hpad, d->scale_re, nch, (int)d->hlen);
     else
-        hipLaunchKernelGGL((k_firfilt_mx<false, 1>), grid, dim3(NT), lds_bytes_mx<false>() + 80, st, (const v2f *)hist,
-                           (const v2f *)x, n, (v2f *)y, (const float *)d->hpad, d->scale_re, d->scale_im, nch,
-                           (int)d->hlen);
+        hipLaunchKernelGGL((k_firfilt_mx<4>), g2, dim3(NT), (lds_bytes_mx<4>() + 80), st, (const v2f *)hist,
+                           (const v2f *)x, n, (v2f *)y, (const float *)d->hpad, d->scale_re, nch, (int)d->hlen);
     LQ_CHECK_LAUNCH();
 }
 
