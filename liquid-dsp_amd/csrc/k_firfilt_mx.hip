@@ -58,47 +58,7 @@ typedef float v4f __attribute__((ext_vector_type(4)));
 typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
 
 constexpr int NT = 256;           // 4 waves
-constexpr int CH = 2048;          // outputs per chunk (4 tiles of 512)
-// Span: the samples a chunk's tiles read, CH plus a halo of 64 KB samples
-// (KB = 1: 33..64 taps, every type; KB = 2: 65..128 taps, crcf -- a
-// 160-wide band, ten K steps instead of six).  Bytes per plane: the span
-// (5280 for KB = 1) rounded up to 256 B, so the planes of the two components
-// start on the same bank -- with the 5280-byte stride every 16-lane group of
-// a B-operand ds_read_b128 had a 2-way bank conflict (SQ_LDS_BANK_CONFLICT
-// was half of the LDS-active cycles).
-template <int KB>
-constexpr int plb_kb() { return ((CH + 64 * KB) * 2 + 16 * ((CH + 64 * KB) / 32) + 255) & ~255; }
-constexpr int SSTR = 68;          // floats per staged segment (32 x re/im + pad)
-// one staged accumulator per wave (KB = 2: 53504 B and 219 VGPRs, two
-// workgroups per CU)
-// KB > 2 (129..256 taps, crcf): the A fragments (3 terms x 2 + 4 KB steps,
-// 216 VGPRs at KB = 4) come from LDS instead: the band H[i][j] = h[i + 64 KB -
-// j] is Toeplitz, so lane row i's fragment of step s is 8 consecutive entries
-// of g[k] = h[64 KB + 31 - k] from k = 31 - i + 16 s + 8 hh; eight copies of
-// each term's g shifted by c = (31 - i) mod 8 make every fragment one aligned
-// 16-byte read
-template <int KB>
-constexpr int glen_kb() { return 16 * (2 + 4 * KB) + 32; }
-// bf16 terms of the taps whose A fragments come from LDS: all three past 128
-// taps (KB > 2), none below (taking terms 2 and 3 from LDS at KB = 1 to free
-// registers for a third chunk measured 0.915-0.925 ms against 0.803-0.805:
-// the fragment reads sit on the MFMA chain, DESIGN (f)3)
-template <int KB>
-constexpr int nal_kb() { return KB > 2 ? 3 : 0; }
-// two chunks of loads in flight per workgroup (register sets; a third
-// measured the same at KB >= 2, r04p)
-// elements between the eight shifted copies: at least NAL GL, and 16 mod 128
-// (32 B mod 256), so the 16 lanes of a ds_read_b128 pass -- eight copies at
-// two bases 16 B apart -- land on 16 distinct bank groups (a stride that is
-// a multiple of 256 B put all eight copies on the same banks)
-template <int KB>
-constexpr int acs_kb() { return nal_kb<KB>() ? ((nal_kb<KB>() * glen_kb<KB>() - 16 + 127) / 128) * 128 + 16 : 0; }
-template <int KB>
-constexpr int acp_bytes() { return 8 * acs_kb<KB>() * 2; }
-template <int KB>
-constexpr int lds_bytes_mx() { return 6 * plb_kb<KB>() + 4 * 16 * SSTR * 4 + acp_bytes<KB>(); }
-
-static_assert(2 * (lds_bytes_mx<4>() + 80) <= 160 * 1024, "KB = 4: two workgroups per CU");
+constexpr int CH = 2048;          // outputs per chunk (512 per wave)
 
 __device__ __forceinline__ int poff(int pos) { return 2 * pos + 16 * (pos >> 5); }
 
@@ -123,42 +83,6 @@ __device__ __forceinline__ void split3(v2f a, bf16x2 &t1, bf16x2 &t2, bf16x2 &t3
     t2 = __builtin_convertvector(r1, bf16x2);
     const v2f r2 = r1 - __builtin_convertvector(t2, v2f);
     t3 = __builtin_convertvector(r2, bf16x2);
-}
-
-// write 8 consecutive complex samples (ring position pos, a multiple of 8)
-// into the six planes: plane (p, c) = term p of component c.  v[q] holds
-// samples 2q and 2q+1 as (re, im, re, im).
-__device__ __forceinline__ void put8(unsigned char *planes, int pstride, int pos, const v4f (&v)[4])
-{
-    bf16x2 t[3][2][4];
-#pragma unroll
-    for (int q = 0; q < 4; q++) {
-        split3(v2f{v[q].x, v[q].z}, t[0][0][q], t[1][0][q], t[2][0][q]);
-        split3(v2f{v[q].y, v[q].w}, t[0][1][q], t[1][1][q], t[2][1][q]);
-    }
-    const int o = poff(pos);
-#pragma unroll
-    for (int p = 0; p < 3; p++)
-#pragma unroll
-        for (int c = 0; c < 2; c++) {
-            const u32x4 w = {__builtin_bit_cast(unsigned, t[p][c][0]), __builtin_bit_cast(unsigned, t[p][c][1]),
-                             __builtin_bit_cast(unsigned, t[p][c][2]), __builtin_bit_cast(unsigned, t[p][c][3])};
-            *reinterpret_cast<u32x4 *>(planes + (2 * p + c) * pstride + o) = w;
-        }
-}
-
-// one complex sample at ring position pos into the six planes
-__device__ __forceinline__ void put1(unsigned char *planes, int pstride, int pos, v2f v)
-{
-    bf16x2 t1, t2, t3;
-    split3(v, t1, t2, t3);   // (re, im) terms
-    const int o = poff(pos);
-    const bf16x2 t[3] = {t1, t2, t3};
-#pragma unroll
-    for (int p = 0; p < 3; p++) {
-        *reinterpret_cast<__bf16 *>(planes + (2 * p) * pstride + o) = t[p].x;
-        *reinterpret_cast<__bf16 *>(planes + (2 * p + 1) * pstride + o) = t[p].y;
-    }
 }
 
 // 8 complex samples of the stream starting at s (a multiple of 8); ext[t<0]
@@ -206,200 +130,6 @@ __device__ __forceinline__ void load8b(__amdgpu_buffer_rsrc_t rx, unsigned off, 
     for (int q = 0; q < 4; q++) v[q] = __builtin_amdgcn_raw_buffer_load_b128(rx, off + 16 * q, 0, 0);
 }
 
-// crcf, 65..256 taps (KB = 2..4 64-tap blocks)
-template <int KB>
-__global__ __launch_bounds__(NT, 2) void k_firfilt_mx(const v2f *__restrict__ win,
-                                                              const v2f *__restrict__ x, long long n,
-                                                              v2f *__restrict__ y, const float *__restrict__ hpad,
-                                                              float sre, long long nch, int hlen)
-{
-    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-    // per step k % 3: nonzero if the chunk's span holds an unsafe sample;
-    // kept after the dynamic region so its base stays 16-byte aligned
-    constexpr int HALO = 64 * KB, NS = 2 + 4 * KB, PLB = plb_kb<KB>();
-    unsigned *sbad = reinterpret_cast<unsigned *>(smem + lds_bytes_mx<KB>());
-    unsigned char *planes = smem;
-    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    const int r32 = lane & 31, hh = lane >> 5;
-    float *stage = reinterpret_cast<float *>(smem + 6 * PLB) + wave * 16 * SSTR;
-
-    // A fragments: lane (row i = r32, k half hh) holds H[i][16s + 8hh + e];
-    // terms NAR.. come from LDS per step
-    constexpr int NAL = nal_kb<KB>(), NAR = 3 - NAL;
-    bf16x8 A[NAR > 0 ? NAR : 1][NAR > 0 ? NS : 1];
-    __bf16 *acp = reinterpret_cast<__bf16 *>(smem + 6 * PLB + 4 * 16 * SSTR * 4);
-    constexpr int GL = glen_kb<KB>(), ACS = acs_kb<KB>();
-    if constexpr (NAL > 0) {
-        // copy c, term p >= NAR: G[c][p - NAR][k] = term p of g[k + c], g[k] = h[HALO + 31 - k]
-        for (int e = tid; e < 8 * GL; e += NT) {
-            const int c = e / GL, k = e - c * GL;
-            const int hk = HALO + 31 - (k + c);
-            const float hv = (hk >= 0 && hk < HALO) ? hpad[hk] : 0.f;
-            bf16x2 t[3];
-            split3(v2f{hv, 0.f}, t[0], t[1], t[2]);
-#pragma unroll
-            for (int p = NAR; p < 3; p++) acp[c * ACS + (p - NAR) * GL + k] = t[p].x;
-        }
-    }
-    if constexpr (NAR > 0) {
-#pragma unroll
-        for (int s = 0; s < NS; s++) {
-            bf16x2 t[3][4];
-#pragma unroll
-            for (int q = 0; q < 4; q++) {
-                float hv[2];
-#pragma unroll
-                for (int u = 0; u < 2; u++) {
-                    const int k = r32 + HALO - (16 * s + 8 * hh + 2 * q + u);
-                    hv[u] = (k >= 0 && k < HALO) ? hpad[k] : 0.f;
-                }
-                split3(v2f{hv[0], hv[1]}, t[0][q], t[1][q], t[2][q]);
-            }
-#pragma unroll
-            for (int p = 0; p < NAR; p++)
-                A[p][s] = bf16x8{t[p][0].x, t[p][0].y, t[p][1].x, t[p][1].y, t[p][2].x, t[p][2].y, t[p][3].x, t[p][3].y};
-        }
-    }
-    // this lane's copy (31 - r32) mod 8 and its fragment base (+ 16 s: step s; + (p - NAR) GL: term p)
-    const __bf16 *acl = NAL > 0 ? acp + ((31 - r32) & 7) * ACS + ((31 - r32) & ~7) + 8 * hh : nullptr;
-
-    // Chunks are dealt grid-stride (workgroup w takes chunks w, w + G, ...):
-    // the chip then streams one contiguous window of the input at a time.
-    // Contiguous runs of chunks per workgroup put ~800 concurrent streams on
-    // addresses a run apart and ran the same memory pattern 9 % slower
-    // (0.80 vs 0.73 ms per 2^28 samples, tools/mb/mb_bw4.hip).  So a chunk's
-    // 64-sample halo (the previous chunk's tail, another workgroup's) is
-    // loaded with it: wave 0 fetches one sample per lane.  Plane position
-    // p of chunk c = stream sample CH c - 64 + p.
-    const long long G = gridDim.x, w = blockIdx.x;
-    if (w >= nch) return;
-    const long long cnt = (nch - w + G - 1) / G;
-    if (tid < 3) sbad[tid] = 0u;
-    unsigned *bad_mask = sbad + 4;   // steps k of this workgroup that need the exact path
-    if (tid < 16) bad_mask[tid] = 0u;
-    // The loop's memory operations are branch-free -- range-checked buffer
-    // loads and stores; a step past the workgroup's last chunk (odd counts)
-    // lands out of range -- so the compiler's vmcnt waits only for the rows a
-    // step consumes and earlier stores stay in flight.  The host keeps n * 8
-    // bytes below 2^31 per launch.
-    const __amdgpu_buffer_rsrc_t rx = __builtin_amdgcn_make_buffer_rsrc((void *)x, (short)0, (int)(n * 8), 0x00020000);
-    const __amdgpu_buffer_rsrc_t ry = __builtin_amdgcn_make_buffer_rsrc((void *)y, (short)0, (int)(n * 8), 0x00020000);
-    const unsigned OOB = 0xfffff000u;   // an offset past any launch's range
-    auto main_off = [&](long long k) -> unsigned {
-        const long long c = w + k * G;
-        return c < nch ? (unsigned)(CH * c + 8 * tid) * 8u : OOB;
-    };
-    // halo sample of lane tid < 64; chunk 0's halo is the history (prologue)
-    auto halo_off = [&](long long k) -> unsigned {
-        const long long c = w + k * G;
-        return (c > 0 && c < nch && tid < HALO) ? (unsigned)(CH * c - HALO + tid) * 8u : OOB;
-    };
-    auto ldh = [&](unsigned off) -> v2f { return __builtin_bit_cast(v2f, __builtin_amdgcn_raw_buffer_load_b64(rx, off, 0, 0)); };
-    __syncthreads();
-    if (w == 0 && tid < HALO) {
-        const v2f hv = win[tid];
-        put1(planes, PLB, tid, hv);
-        if (unsafe_bits(hv.x) | unsafe_bits(hv.y)) atomicOr(&sbad[0], 1u);
-    }
-    // two chunks in flight per workgroup: register sets (xa, ha) / (xb, hb)
-    // rotate (the loop is unrolled by two so no set is ever copied, which
-    // would wait on its loads early)
-    constexpr int NB = 2;
-    v4f xa[4], xb[4];
-    v2f ha, hb;
-    load8b(rx, main_off(0), xa);
-    ha = ldh(halo_off(0));
-    load8b(rx, main_off(1), xb);
-    hb = ldh(halo_off(1));
-
-    // B operand: lane column n = r32 -> segment sg = n & 15, component n >> 4
-    const int sg = r32 & 15, comp = r32 >> 4;
-    auto step = [&](long long k, v4f (&xv)[4], v2f &hv) {
-        const long long c = w + k * G;
-        __syncthreads();   // the previous chunk's MFMA reads are done
-        const int cs = (int)(k % 3);
-        // chunk 0's halo planes came from the history in the prologue
-        if (tid < HALO && c != 0) {
-            put1(planes, PLB, tid, hv);
-            if (unsafe_bits(hv.x) | unsafe_bits(hv.y)) atomicOr(&sbad[cs], 1u);
-        }
-        put8(planes, PLB, HALO + 8 * tid, xv);
-        if (unsafe4(xv[0]) | unsafe4(xv[1]) | unsafe4(xv[2]) | unsafe4(xv[3])) atomicOr(&sbad[cs], 1u);
-        if (tid == 0) sbad[(cs + 1) % 3] = 0u;   // step k+1's slot (last read in step k-2)
-        load8b(rx, main_off(k + NB), xv);
-        hv = ldh(halo_off(k + NB));
-        __syncthreads();
-        if (tid == 0 && sbad[cs] && c < nch) bad_mask[k >> 5] |= 1u << (k & 31);
-
-        f32x16 C = {};
-#pragma unroll
-        for (int s = 0; s < NS; s++) {
-            const int pos = 512 * wave + 32 * sg + 16 * s + 8 * hh;
-            const unsigned char *bp = planes + comp * PLB + poff(pos);
-            const bf16x8 b0 = *reinterpret_cast<const bf16x8 *>(bp);
-            const bf16x8 b1 = *reinterpret_cast<const bf16x8 *>(bp + 2 * PLB);
-            const bf16x8 b2 = *reinterpret_cast<const bf16x8 *>(bp + 4 * PLB);
-            // terms of order 2^-16 first, then 2^-8, then the leading product
-            bf16x8 al[NAL > 0 ? NAL : 1];
-#pragma unroll
-            for (int p = 0; p < NAL; p++) al[p] = *reinterpret_cast<const bf16x8 *>(acl + p * GL + 16 * s);
-            bf16x8 af[3];
-#pragma unroll
-            for (int p = 0; p < 3; p++) af[p] = p < NAR ? A[p < NAR ? p : 0][NAR > 0 ? s : 0] : al[p >= NAR ? p - NAR : 0];
-            C = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[0], b2, C, 0, 0, 0);
-            C = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[1], b1, C, 0, 0, 0);
-            C = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[2], b0, C, 0, 0, 0);
-            C = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[0], b1, C, 0, 0, 0);
-            C = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[1], b0, C, 0, 0, 0);
-            C = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[0], b0, C, 0, 0, 0);
-        }
-
-        // accumulator (col r32, row (r&3) + 8(r>>2) + 4hh) -> stage[sg][i][comp]
-#pragma unroll
-        for (int r = 0; r < 16; r++) stage[sg * SSTR + 2 * ((r & 3) + 8 * (r >> 2) + 4 * hh) + comp] = C[r];
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-        __builtin_amdgcn_wave_barrier();
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-        // 16-byte pairs; a pair straddling n (odd n) keeps its in-range half
-        // (the range check is per dword)
-        const unsigned o0 = (unsigned)(CH * c + 512 * wave) * 8u;
-#pragma unroll
-        for (int q = 0; q < 4; q++) {
-            const int o = 2 * (lane + 64 * q);
-            const v4f r = *reinterpret_cast<const v4f *>(stage + (o >> 5) * SSTR + 2 * (o & 31)) *
-                          sre;   // crcf: real scale per component (firfilt.c:337)
-            // default cache policy: over five fresh buffer pairs the kernel ran
-            // 0.835-0.905 ms (mean 0.877) against 0.819-0.927 (0.891) with
-            // non-temporal stores (its time depends on where the 2 GB buffers
-            // land, r05n_firfilt_alloc.txt / r05_ab_experiments.txt)
-            __builtin_amdgcn_raw_buffer_store_b128(r, ry, c < nch ? o0 + 8u * o : OOB, 0, 0);
-        }
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-        __builtin_amdgcn_wave_barrier();
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-    };
-    for (long long k = 0; k < cnt; k += NB) {
-        step(k, xa, ha);
-        step(k + 1, xb, hb);
-    }
-    // the range guard's chunks: the exact float32 outputs overwrite what the
-    // matrix path stored for them.  Only workgroup-scope ordering is needed
-    // (the same workgroup wrote them); no fence at all in the common case (a
-    // device-scope fence here writes back L2 in every workgroup: +12 %)
-    __syncthreads();
-    unsigned anybad = 0;
-#pragma unroll
-    for (int i = 0; i < 16; i++) anybad |= bad_mask[i];
-    if (anybad) {
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-        __syncthreads();
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
-        for (int k = 0; k < (int)cnt; k++)
-            if (bad_mask[k >> 5] & (1u << (k & 31)))
-                exact_chunk_c<false, HALO>(win, x, n, y, hpad, hlen, CH * (w + k * G) + 8 * tid, 8, sre, 0.f);
-    }
-}
-
 // ---------------------------------------------------------------- 16x16 tiles
 // k_firfilt_mx16: 33..64 taps on v_mfma_f32_16x16x32_bf16.  A tile is 16
 // outputs x 16 columns (8 segments of 16 outputs x re/im), K = 96 in three
@@ -414,11 +144,16 @@ __global__ __launch_bounds__(NT, 2) void k_firfilt_mx(const v2f *__restrict__ wi
 // Planes: no row pad, the component-1 plane 176 mod 256 bytes after
 // component 0 (the 16 lanes of a B-operand ds_read_b128 -- 8 segments 32 B
 // apart x 2 components -- land on 16 distinct bank groups).
-constexpr int PL16 = 4272;   // >= (2112 + 16) x 2 B, == 176 mod 256
-constexpr int LDS16 = 6 * PL16 + 80;
+template <int KB>
+constexpr int pl16() { return (((CH + 64 * KB + 16) * 2 - 176 + 255) & ~255) + 176; }   // >= span + 16, == 176 mod 256
+template <int KB>
+constexpr int lds16() { return 6 * pl16<KB>() + 80; }
+static_assert(pl16<1>() == 4272 && pl16<4>() % 256 == 176, "plane stride");
 
+template <int KB>
 __device__ __forceinline__ void put8_16(unsigned char *planes, int pos, const v4f (&v)[4])
 {
+    constexpr int PL16 = pl16<KB>();
     bf16x2 t[3][2][4];
 #pragma unroll
     for (int q = 0; q < 4; q++) {
@@ -434,8 +169,10 @@ __device__ __forceinline__ void put8_16(unsigned char *planes, int pos, const v4
             *reinterpret_cast<u32x4 *>(planes + (2 * p + c) * PL16 + 2 * pos) = w;
         }
 }
+template <int KB>
 __device__ __forceinline__ void put1_16(unsigned char *planes, int pos, v2f v)
 {
+    constexpr int PL16 = pl16<KB>();
     bf16x2 t1, t2, t3;
     split3(v, t1, t2, t3);
     const bf16x2 t[3] = {t1, t2, t3};
@@ -451,14 +188,15 @@ __device__ __forceinline__ float swap1(float v)
     return __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, v), 0xB1, 0xF, 0xF, true));
 }
 
-template <bool CC, int WPC>
+template <bool CC, int KB, int WPC>
 __global__ __launch_bounds__(NT, WPC) void k_firfilt_mx16(const v2f *__restrict__ win, const v2f *__restrict__ x,
                                                         long long n, v2f *__restrict__ y,
                                                         const float *__restrict__ hpad, float sre, float sim,
                                                         long long nch, int hlen)
 {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-    constexpr int HALO = 64;
+    constexpr int HALO = 64 * KB, PL16 = pl16<KB>();
+    constexpr int NS = (16 + HALO + 31) / 32;   // K steps of 32 over the 16 + HALO band
     unsigned char *planes = smem;
     unsigned *sbad = reinterpret_cast<unsigned *>(smem + 6 * PL16);
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -467,11 +205,11 @@ __global__ __launch_bounds__(NT, WPC) void k_firfilt_mx16(const v2f *__restrict_
     typedef float f32x4 __attribute__((ext_vector_type(4)));
 
     // A fragments: lane (row i = r16, k group kg) holds H[i][32 s + 8 kg + e]
-    bf16x8 A[NA][3][3];
+    bf16x8 A[NA][3][NS];
 #pragma unroll
     for (int a = 0; a < NA; a++)
 #pragma unroll
-        for (int s = 0; s < 3; s++) {
+        for (int s = 0; s < NS; s++) {
             bf16x2 t[3][4];
 #pragma unroll
             for (int q = 0; q < 4; q++) {
@@ -494,9 +232,9 @@ __global__ __launch_bounds__(NT, WPC) void k_firfilt_mx16(const v2f *__restrict_
     if (tid < 3) sbad[tid] = 0u;
     unsigned *bad_mask = sbad + 4;
     if (tid < 16) bad_mask[tid] = 0u;
-    // the last tile's K = 96 window reaches 16 positions past the span
-    // (H is zero there): zero them once, so 0 * garbage cannot make a NaN
-    if (tid < 6 * 24) *reinterpret_cast<__bf16 *>(planes + (tid / 24) * PL16 + 2 * (HALO + CH + tid % 24)) = __bf16(0.f);
+    // the last tile's K window reaches 16 positions past the span (H is
+    // zero there): zero them once, so 0 * garbage cannot make a NaN
+    if (tid < 6 * 16) *reinterpret_cast<__bf16 *>(planes + (tid / 16) * PL16 + 2 * (HALO + CH + tid % 16)) = __bf16(0.f);
     const __amdgpu_buffer_rsrc_t rx = __builtin_amdgcn_make_buffer_rsrc((void *)x, (short)0, (int)(n * 8), 0x00020000);
     const __amdgpu_buffer_rsrc_t ry = __builtin_amdgcn_make_buffer_rsrc((void *)y, (short)0, (int)(n * 8), 0x00020000);
     const unsigned OOB = 0xfffff000u;
@@ -512,7 +250,7 @@ __global__ __launch_bounds__(NT, WPC) void k_firfilt_mx16(const v2f *__restrict_
     __syncthreads();
     if (w == 0 && tid < HALO) {
         const v2f hv = win[tid];
-        put1_16(planes, tid, hv);
+        put1_16<KB>(planes, tid, hv);
         if (unsafe_bits(hv.x) | unsafe_bits(hv.y)) atomicOr(&sbad[0], 1u);
     }
     // one chunk of loads in flight per workgroup (issued as the previous
@@ -529,10 +267,10 @@ __global__ __launch_bounds__(NT, WPC) void k_firfilt_mx16(const v2f *__restrict_
         __syncthreads();   // the previous chunk's B-operand reads are done
         const int cs = (int)(k % 3);
         if (tid < HALO && c != 0) {
-            put1_16(planes, tid, hv);
+            put1_16<KB>(planes, tid, hv);
             if (unsafe_bits(hv.x) | unsafe_bits(hv.y)) atomicOr(&sbad[cs], 1u);
         }
-        put8_16(planes, HALO + 8 * tid, xv);
+        put8_16<KB>(planes, HALO + 8 * tid, xv);
         if (unsafe4(xv[0]) | unsafe4(xv[1]) | unsafe4(xv[2]) | unsafe4(xv[3])) atomicOr(&sbad[cs], 1u);
         if (tid == 0) sbad[(cs + 1) % 3] = 0u;
         load8b(rx, main_off(k + 1), xv);
@@ -547,7 +285,7 @@ __global__ __launch_bounds__(NT, WPC) void k_firfilt_mx16(const v2f *__restrict_
 #pragma unroll
             for (int a = 0; a < NA; a++) C[a] = f32x4{};
 #pragma unroll
-            for (int s = 0; s < 3; s++) {
+            for (int s = 0; s < NS; s++) {
                 const unsigned char *bp = planes + comp * PL16 + 2 * (base + 16 * seg + 32 * s + 8 * kg);
                 const bf16x8 b0 = *reinterpret_cast<const bf16x8 *>(bp);
                 const bf16x8 b1 = *reinterpret_cast<const bf16x8 *>(bp + 2 * PL16);
@@ -811,34 +549,21 @@ static void launch_mx(const lqk_fir_desc *d, const void *hist, const void *x, lo
     }
     const long long nch = (n + CH - 1) / CH;
     const int kb = (int)d->nchunk;   // 64-tap blocks
-    if (kb == 1) {
-        // crcf / cccf, 33..64 taps: the 16x16 kernel, one chunk of loads in
-        // flight, four (crcf, 94 VGPRs) / three (cccf, 155) workgroups per CU
-        if (d->kind == 2) {
-            const dim3 g((unsigned)(nch < 768 ? nch : 768));
-            hipLaunchKernelGGL((k_firfilt_mx16<true, 3>), g, dim3(NT), LDS16, st, (const v2f *)hist,
-                               (const v2f *)x, n, (v2f *)y, (const float *)d->hpad, d->scale_re, d->scale_im, nch,
-                               (int)d->hlen);
-        } else {
-            const dim3 g((unsigned)(nch < 1024 ? nch : 1024));
-            hipLaunchKernelGGL((k_firfilt_mx16<false, 4>), g, dim3(NT), LDS16, st, (const v2f *)hist,
-                               (const v2f *)x, n, (v2f *)y, (const float *)d->hpad, d->scale_re, d->scale_im, nch,
-                               (int)d->hlen);
-        }
-        LQ_CHECK_LAUNCH();
-        return;
-    }
-    // crcf, 65..256 taps: the 32x32 kernel, two workgroups per CU
-    const dim3 g2((unsigned)(nch < 512 ? nch : 512));
-    if (kb == 2)
-        hipLaunchKernelGGL((k_firfilt_mx<2>), g2, dim3(NT), (lds_bytes_mx<2>() + 80), st, (const v2f *)hist,
-                           (const v2f *)x, n, (v2f *)y, (const float *)d->hpad, d->scale_re, nch, (int)d->hlen);
-    else if (kb == 3)
-        hipLaunchKernelGGL((k_firfilt_mx<3>), g2, dim3(NT), (lds_bytes_mx<3>() + 80), st, (const v2f *)hist,
-                           (const v2f *)x, n, (v2f *)y, (const float *)d->hpad, d->scale_re, nch, (int)d->hlen);
-    else
-        hipLaunchKernelGGL((k_firfilt_mx<4>), g2, dim3(NT), (lds_bytes_mx<4>() + 80), st, (const v2f *)hist,
-                           (const v2f *)x, n, (v2f *)y, (const float *)d->hpad, d->scale_re, nch, (int)d->hlen);
+    // workgroups per CU by VGPRs: crcf 94 / 118 / 164 / 166 at 1..4 blocks
+    // (four, four, three, three), cccf 155 (three).  Against the 32x32x16
+    // kernel with its LDS stage (two per CU): cccf h = 64 0.65 -> 0.56 ms,
+    // crcf h = 128 / 192 / 256 0.555 / 0.71 / 0.85 -> 0.50 / 0.62 / 0.75 ms
+    // per 2^27 samples (r05x, r05za in profiles/r05_ab_experiments.txt)
+    auto go = [&](auto kern, int wpc, int lds) {
+        const long long g = nch < 256LL * wpc ? nch : 256LL * wpc;
+        hipLaunchKernelGGL(kern, dim3((unsigned)g), dim3(NT), lds, st, (const v2f *)hist, (const v2f *)x, n,
+                           (v2f *)y, (const float *)d->hpad, d->scale_re, d->scale_im, nch, (int)d->hlen);
+    };
+    if (d->kind == 2) go(k_firfilt_mx16<true, 1, 3>, 3, lds16<1>());
+    else if (kb == 1) go(k_firfilt_mx16<false, 1, 4>, 4, lds16<1>());
+    else if (kb == 2) go(k_firfilt_mx16<false, 2, 4>, 4, lds16<2>());
+    else if (kb == 3) go(k_firfilt_mx16<false, 3, 3>, 3, lds16<3>());
+    else go(k_firfilt_mx16<false, 4, 3>, 3, lds16<4>());
     LQ_CHECK_LAUNCH();
 }
 
