@@ -1,6 +1,6 @@
-// k_firfilt_mx.hip -- firfilt on the matrix cores: crcf / cccf with 33..64
-// taps (the BASELINE config-1 shape, h = 64) on 16x16x32 tiles, crcf with
-// 65..256 taps on 32x32x16 tiles, rrrf with 33..64 taps.
+// k_firfilt_mx.hip -- firfilt on the matrix cores (v_mfma_f32_16x16x32_bf16):
+// crcf with 33..256 taps (h = 64 is the BASELINE config-1 shape), cccf and
+// rrrf with 33..64 taps.
 //
 // Reference: src/filter/src/firfilt.c:322-359 (execute / execute_block),
 // y[t] = scale * sum_{k<h} h[k] x[t-k].  The VALU kernel (k_firfilt.hip)
@@ -10,10 +10,11 @@
 //   C[i][n] = sum_k H[i][k] B[k][n],  H[i][k] = h[i + 64 KB - k] (0 outside
 //   0..64 KB - 1),  B[k][n] = x_comp(n)[s_seg(n) - 64 KB + k]
 //
-// i = output within a segment, n = (segment, re/im) column.  16x16x32
-// (k_firfilt_mx16): 16-output segments, a tile is 8 segments x 2 components
-// = 128 outputs, K = 96 in three steps.  32x32x16 (k_firfilt_mx): 32-output
-// segments, a tile is 16 segments x 2 = 512 outputs, 2 + 4 KB steps of 16.
+// i = output within a 16-output segment, n = (segment, re/im) column: a
+// tile is 8 segments x 2 components = 128 complex outputs (rrrf: 16
+// segments, 256 outputs), K = 16 + 64 KB in steps of 32.  (The 32x32x16 form
+// of rounds 1-4 -- 512 outputs per tile, the accumulator staged through LDS
+// for coalesced stores -- ran 1-15 % slower, r05w-r05zc.)
 // float32 accuracy is kept by splitting both operands into three bf16 terms
 // (x = x1 + x2 + x3, each the round-to-nearest bf16 of the remaining
 // residual, exact to 2^-24 relative; products of bf16 terms are exact in the
@@ -28,8 +29,8 @@
 // iteration: the 8 samples a lane prefetched are split into six bf16 planes
 // (3 terms x re/im) of the chunk's span in LDS (the 64 KB-sample halo comes
 // with the chunk), the next chunk's loads are issued, then each wave runs the
-// MFMAs for its 512 outputs and writes 16-byte stores (16x16: straight from
-// the accumulators after two DPP swaps; 32x32: staged through LDS).  The
+// MFMAs for its outputs and writes 16-byte stores straight from the
+// accumulators (complex: after two DPP swaps with the partner lane).  The
 // taps' A fragments are built once per workgroup from the padded fp32 taps.
 //
 // Range guard.  The split is float32-accurate only for finite values whose
@@ -53,14 +54,11 @@ namespace {
 
 typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
-typedef float f32x16 __attribute__((ext_vector_type(16)));
 typedef float v4f __attribute__((ext_vector_type(4)));
 typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
 
 constexpr int NT = 256;           // 4 waves
 constexpr int CH = 2048;          // outputs per chunk (512 per wave)
-
-__device__ __forceinline__ int poff(int pos) { return 2 * pos + 16 * (pos >> 5); }
 
 // 1 if v is outside the split's safe class: NaN, +-Inf, or a nonzero |v|
 // outside [2^-50, 2^50] (integer compare on the magnitude bits; NaN and Inf
@@ -338,50 +336,15 @@ __global__ __launch_bounds__(NT, WPC) void k_firfilt_mx16(const v2f *__restrict_
 }
 
 // ---------------------------------------------------------------- rrrf
-// Real samples: the 32 columns of a tile are 32 segments, so a wave's tile is
-// 1024 outputs and a chunk 4096; three bf16 planes.
+// Real samples: a wave's 1024 outputs, a chunk of 4096; three bf16 planes.
 constexpr int CHR = 4096;
 constexpr int SPANR = CHR + 64;
-constexpr int PLBR = SPANR * 2 + 16 * (SPANR / 32);   // 10400
-constexpr int SSTRR = 36;                              // floats per staged segment (32 + pad)
-constexpr int LDS_BYTES_R = 3 * PLBR + 4 * 32 * SSTRR * 4;
 
 __device__ __forceinline__ float rsample_at(const float *__restrict__ win, const float *__restrict__ x, long long n,
                                             long long t)
 {
     return t < 0 ? win[64 + t] : (t < n ? x[t] : 0.f);
 }
-// 8 real samples (v4f pair) into the three planes at pos (a multiple of 8)
-__device__ __forceinline__ void put8r(unsigned char *planes, int pstride, int pos, v4f a, v4f b)
-{
-    bf16x2 t[3][4];
-    split3(v2f{a.x, a.y}, t[0][0], t[1][0], t[2][0]);
-    split3(v2f{a.z, a.w}, t[0][1], t[1][1], t[2][1]);
-    split3(v2f{b.x, b.y}, t[0][2], t[1][2], t[2][2]);
-    split3(v2f{b.z, b.w}, t[0][3], t[1][3], t[2][3]);
-    const int o = poff(pos);
-#pragma unroll
-    for (int p = 0; p < 3; p++) {
-        const u32x4 w = {__builtin_bit_cast(unsigned, t[p][0]), __builtin_bit_cast(unsigned, t[p][1]),
-                         __builtin_bit_cast(unsigned, t[p][2]), __builtin_bit_cast(unsigned, t[p][3])};
-        *reinterpret_cast<u32x4 *>(planes + p * pstride + o) = w;
-    }
-}
-
-// 4 real samples into the three planes at pos (a multiple of 4)
-__device__ __forceinline__ void put4r(unsigned char *planes, int pstride, int pos, v4f a)
-{
-    bf16x2 t[3][2];
-    split3(v2f{a.x, a.y}, t[0][0], t[1][0], t[2][0]);
-    split3(v2f{a.z, a.w}, t[0][1], t[1][1], t[2][1]);
-    const int o = poff(pos);
-    typedef unsigned u32x2 __attribute__((ext_vector_type(2)));
-#pragma unroll
-    for (int p = 0; p < 3; p++)
-        *reinterpret_cast<u32x2 *>(planes + p * pstride + o) =
-            u32x2{__builtin_bit_cast(unsigned, t[p][0]), __builtin_bit_cast(unsigned, t[p][1])};
-}
-
 __device__ __attribute__((noinline)) void exact_chunk_r(const float *__restrict__ win, const float *__restrict__ x,
                                                         long long n, float *__restrict__ y,
                                                         const float *__restrict__ hpad, int hlen, long long t0,
@@ -402,33 +365,71 @@ __device__ __forceinline__ void load16rb(__amdgpu_buffer_rsrc_t rx, unsigned off
     for (int q = 0; q < 4; q++) v[q] = __builtin_amdgcn_raw_buffer_load_b128(rx, off + 16 * q, 0, 0);
 }
 
-__global__ __launch_bounds__(NT, 3) void k_firfilt_mx_r(const float *__restrict__ win, const float *__restrict__ x,
-                                                       long long n, float *__restrict__ y,
-                                                       const float *__restrict__ hpad, float sre, long long nch,
-                                                       int hlen)
+// rrrf on 16x16x32 tiles: the 16 columns of a tile are 16 segments of 16
+// outputs (a wave's 1024 outputs are four tiles), K = 96 in three steps, and
+// lane (segment n, row group g) holds outputs 16 n + 4 g .. + 3 -- one
+// 16-byte store, and a store instruction writes the tile's 256 outputs (1 KB)
+// contiguously, straight from the accumulator.  Planes: 16 B of pad per 16
+// samples, so the 16 lanes of a B-operand ds_read_b128 (segments 32 B apart)
+// land on 16 distinct bank groups.
+__device__ __forceinline__ int poffr16(int pos) { return 2 * pos + 16 * (pos >> 4); }
+constexpr int PLR16 = (((SPANR + 16) * 2 + 16 * ((SPANR + 16) >> 4)) + 255) & ~255;
+constexpr int LDSR16 = 3 * PLR16 + 80;
+
+__device__ __forceinline__ void put8r16(unsigned char *planes, int pos, v4f a, v4f b)
+{
+    bf16x2 t[3][4];
+    split3(v2f{a.x, a.y}, t[0][0], t[1][0], t[2][0]);
+    split3(v2f{a.z, a.w}, t[0][1], t[1][1], t[2][1]);
+    split3(v2f{b.x, b.y}, t[0][2], t[1][2], t[2][2]);
+    split3(v2f{b.z, b.w}, t[0][3], t[1][3], t[2][3]);
+    const int o = poffr16(pos);
+#pragma unroll
+    for (int p = 0; p < 3; p++) {
+        const u32x4 w = {__builtin_bit_cast(unsigned, t[p][0]), __builtin_bit_cast(unsigned, t[p][1]),
+                         __builtin_bit_cast(unsigned, t[p][2]), __builtin_bit_cast(unsigned, t[p][3])};
+        *reinterpret_cast<u32x4 *>(planes + p * PLR16 + o) = w;
+    }
+}
+__device__ __forceinline__ void put4r16(unsigned char *planes, int pos, v4f a)
+{
+    bf16x2 t[3][2];
+    split3(v2f{a.x, a.y}, t[0][0], t[1][0], t[2][0]);
+    split3(v2f{a.z, a.w}, t[0][1], t[1][1], t[2][1]);
+    const int o = poffr16(pos);
+    typedef unsigned u32x2 __attribute__((ext_vector_type(2)));
+#pragma unroll
+    for (int p = 0; p < 3; p++)
+        *reinterpret_cast<u32x2 *>(planes + p * PLR16 + o) =
+            u32x2{__builtin_bit_cast(unsigned, t[p][0]), __builtin_bit_cast(unsigned, t[p][1])};
+}
+
+template <int WPC>
+__global__ __launch_bounds__(NT, WPC) void k_firfilt_mx16_r(const float *__restrict__ win,
+                                                            const float *__restrict__ x, long long n,
+                                                            float *__restrict__ y, const float *__restrict__ hpad,
+                                                            float sre, long long nch, int hlen)
 {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-    unsigned *sbad = reinterpret_cast<unsigned *>(smem + LDS_BYTES_R);   // as k_firfilt_mx
+    unsigned *sbad = reinterpret_cast<unsigned *>(smem + 3 * PLR16);
     unsigned char *planes = smem;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    const int r32 = lane & 31, hh = lane >> 5;
-    float *stage = reinterpret_cast<float *>(smem + 3 * PLBR) + wave * 32 * SSTRR;
-    // grid-stride chunks, each with its own 64-sample halo (lanes 0..15, four
-    // samples each), as k_firfilt_mx
+    const int r16 = lane & 15, kg = lane >> 4;
+    typedef float f32x4 __attribute__((ext_vector_type(4)));
     const long long G = gridDim.x, w = blockIdx.x;
     if (w >= nch) return;
     const long long cnt = (nch - w + G - 1) / G;
 
-    bf16x8 A[3][6];
+    bf16x8 A[3][3];   // [term][step]: lane (row i = r16, k group kg) holds H[i][32 s + 8 kg + e]
 #pragma unroll
-    for (int s = 0; s < 6; s++) {
+    for (int s = 0; s < 3; s++) {
         bf16x2 t[3][4];
 #pragma unroll
         for (int q = 0; q < 4; q++) {
             float hv[2];
 #pragma unroll
             for (int u = 0; u < 2; u++) {
-                const int k = r32 + 64 - (16 * s + 8 * hh + 2 * q + u);
+                const int k = r16 + 64 - (32 * s + 8 * kg + 2 * q + u);
                 hv[u] = (k >= 0 && k < 64) ? hpad[k] : 0.f;
             }
             split3(v2f{hv[0], hv[1]}, t[0][q], t[1][q], t[2][q]);
@@ -440,6 +441,8 @@ __global__ __launch_bounds__(NT, 3) void k_firfilt_mx_r(const float *__restrict_
     if (tid < 3) sbad[tid] = 0u;
     unsigned *bad_mask = sbad + 4;
     if (tid < 16) bad_mask[tid] = 0u;
+    // the last tile's K window reaches 16 positions past the span (H is zero there)
+    if (tid < 3 * 16) *reinterpret_cast<__bf16 *>(planes + (tid / 16) * PLR16 + poffr16(SPANR + tid % 16)) = __bf16(0.f);
     const __amdgpu_buffer_rsrc_t rx = __builtin_amdgcn_make_buffer_rsrc((void *)x, (short)0, (int)(n * 4), 0x00020000);
     const __amdgpu_buffer_rsrc_t ry = __builtin_amdgcn_make_buffer_rsrc((void *)y, (short)0, (int)(n * 4), 0x00020000);
     const unsigned OOB = 0xfffff000u;
@@ -454,66 +457,48 @@ __global__ __launch_bounds__(NT, 3) void k_firfilt_mx_r(const float *__restrict_
     __syncthreads();
     if (w == 0 && tid < 16) {
         const v4f hv = {win[4 * tid], win[4 * tid + 1], win[4 * tid + 2], win[4 * tid + 3]};
-        put4r(planes, PLBR, 4 * tid, hv);
+        put4r16(planes, 4 * tid, hv);
         if (unsafe4(hv)) atomicOr(&sbad[0], 1u);
     }
-    v4f xa[4], xb[4], ha, hb;
+    v4f xa[4], ha;   // one chunk of loads in flight
     load16rb(rx, main_off(0), xa);
     ha = __builtin_amdgcn_raw_buffer_load_b128(rx, halo_off(0), 0, 0);
-    load16rb(rx, main_off(1), xb);
-    hb = __builtin_amdgcn_raw_buffer_load_b128(rx, halo_off(1), 0, 0);
-    const int sg = r32;   // B column = segment
-    auto step = [&](long long k, v4f (&xv)[4], v4f &hv) {
+    for (long long k = 0; k < cnt; k++) {
         const long long c = w + k * G;
-        __syncthreads();
+        __syncthreads();   // the previous chunk's B-operand reads are done
         const int cs = (int)(k % 3);
         if (tid < 16 && c != 0) {
-            put4r(planes, PLBR, 4 * tid, hv);
-            if (unsafe4(hv)) atomicOr(&sbad[cs], 1u);
+            put4r16(planes, 4 * tid, ha);
+            if (unsafe4(ha)) atomicOr(&sbad[cs], 1u);
         }
-        put8r(planes, PLBR, 64 + 16 * tid, xv[0], xv[1]);
-        put8r(planes, PLBR, 64 + 16 * tid + 8, xv[2], xv[3]);
-        if (unsafe4(xv[0]) | unsafe4(xv[1]) | unsafe4(xv[2]) | unsafe4(xv[3]))
-            atomicOr(&sbad[cs], 1u);
+        put8r16(planes, 64 + 16 * tid, xa[0], xa[1]);
+        put8r16(planes, 64 + 16 * tid + 8, xa[2], xa[3]);
+        if (unsafe4(xa[0]) | unsafe4(xa[1]) | unsafe4(xa[2]) | unsafe4(xa[3])) atomicOr(&sbad[cs], 1u);
         if (tid == 0) sbad[(cs + 1) % 3] = 0u;
-        load16rb(rx, main_off(k + 2), xv);
-        hv = __builtin_amdgcn_raw_buffer_load_b128(rx, halo_off(k + 2), 0, 0);
+        load16rb(rx, main_off(k + 1), xa);
+        ha = __builtin_amdgcn_raw_buffer_load_b128(rx, halo_off(k + 1), 0, 0);
         __syncthreads();
         if (tid == 0 && sbad[cs] && c < nch) bad_mask[k >> 5] |= 1u << (k & 31);
-        f32x16 C = {};
 #pragma unroll
-        for (int s = 0; s < 6; s++) {
-            const int pos = 1024 * wave + 32 * sg + 16 * s + 8 * hh;
-            const unsigned char *bp = planes + poff(pos);
-            const bf16x8 b0 = *reinterpret_cast<const bf16x8 *>(bp);
-            const bf16x8 b1 = *reinterpret_cast<const bf16x8 *>(bp + PLBR);
-            const bf16x8 b2 = *reinterpret_cast<const bf16x8 *>(bp + 2 * PLBR);
-            C = __builtin_amdgcn_mfma_f32_32x32x16_bf16(A[0][s], b2, C, 0, 0, 0);
-            C = __builtin_amdgcn_mfma_f32_32x32x16_bf16(A[1][s], b1, C, 0, 0, 0);
-            C = __builtin_amdgcn_mfma_f32_32x32x16_bf16(A[2][s], b0, C, 0, 0, 0);
-            C = __builtin_amdgcn_mfma_f32_32x32x16_bf16(A[0][s], b1, C, 0, 0, 0);
-            C = __builtin_amdgcn_mfma_f32_32x32x16_bf16(A[1][s], b0, C, 0, 0, 0);
-            C = __builtin_amdgcn_mfma_f32_32x32x16_bf16(A[0][s], b0, C, 0, 0, 0);
+        for (int tt = 0; tt < 4; tt++) {
+            const int base = 1024 * wave + 256 * tt;
+            f32x4 C = {};
+#pragma unroll
+            for (int s = 0; s < 3; s++) {
+                const unsigned char *bp = planes + poffr16(base + 16 * r16 + 32 * s + 8 * kg);
+                const bf16x8 b0 = *reinterpret_cast<const bf16x8 *>(bp);
+                const bf16x8 b1 = *reinterpret_cast<const bf16x8 *>(bp + PLR16);
+                const bf16x8 b2 = *reinterpret_cast<const bf16x8 *>(bp + 2 * PLR16);
+                C = __builtin_amdgcn_mfma_f32_16x16x32_bf16(A[0][s], b2, C, 0, 0, 0);
+                C = __builtin_amdgcn_mfma_f32_16x16x32_bf16(A[1][s], b1, C, 0, 0, 0);
+                C = __builtin_amdgcn_mfma_f32_16x16x32_bf16(A[2][s], b0, C, 0, 0, 0);
+                C = __builtin_amdgcn_mfma_f32_16x16x32_bf16(A[0][s], b1, C, 0, 0, 0);
+                C = __builtin_amdgcn_mfma_f32_16x16x32_bf16(A[1][s], b0, C, 0, 0, 0);
+                C = __builtin_amdgcn_mfma_f32_16x16x32_bf16(A[0][s], b0, C, 0, 0, 0);
+            }
+            const unsigned off = (unsigned)(CHR * c + base + 16 * r16 + 4 * kg) * 4u;
+            __builtin_amdgcn_raw_buffer_store_b128(C * sre, ry, c < nch ? off : OOB, 0, 0);
         }
-#pragma unroll
-        for (int r = 0; r < 16; r++) stage[sg * SSTRR + (r & 3) + 8 * (r >> 2) + 4 * hh] = C[r];
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-        __builtin_amdgcn_wave_barrier();
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-        const unsigned o0 = (unsigned)(CHR * c + 1024 * wave) * 4u;
-#pragma unroll
-        for (int q = 0; q < 4; q++) {
-            const int o = 4 * (lane + 64 * q);
-            const v4f a = *reinterpret_cast<const v4f *>(stage + (o >> 5) * SSTRR + (o & 31)) * sre;
-            __builtin_amdgcn_raw_buffer_store_b128(a, ry, c < nch ? o0 + 4u * o : OOB, 0, 2);
-        }
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-        __builtin_amdgcn_wave_barrier();
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-    };
-    for (long long k = 0; k < cnt; k += 2) {
-        step(k, xa, ha);
-        step(k + 1, xb, hb);
     }
     __syncthreads();
     unsigned anybad = 0;
@@ -539,10 +524,10 @@ __global__ __launch_bounds__(NT, 3) void k_firfilt_mx_r(const float *__restrict_
 static void launch_mx(const lqk_fir_desc *d, const void *hist, const void *x, long long n, void *y,
                       hipStream_t st)
 {
-    if (d->kind == 0) {   // rrrf: 4096-output chunks, three workgroups per CU
+    if (d->kind == 0) {   // rrrf: 4096-output chunks, four workgroups per CU (112 VGPRs, 38 KB of LDS)
         const long long nch = (n + CHR - 1) / CHR;
-        const long long nwg = nch < 768 ? nch : 768;
-        hipLaunchKernelGGL(k_firfilt_mx_r, dim3((unsigned)nwg), dim3(NT), LDS_BYTES_R + 80, st, (const float *)hist,
+        const long long nwg = nch < 1024 ? nch : 1024;
+        hipLaunchKernelGGL(k_firfilt_mx16_r<4>, dim3((unsigned)nwg), dim3(NT), LDSR16, st, (const float *)hist,
                            (const float *)x, n, (float *)y, (const float *)d->hpad, d->scale_re, nch, (int)d->hlen);
         LQ_CHECK_LAUNCH();
         return;

@@ -1,7 +1,9 @@
 """firfilt crcf with 65..256 taps: 16x16x32 tiles (LQ_FMX16KB=<workgroups per
 CU>) against the 32x32x16 kernel, same process and buffers (dev tool):
 normwise agreement with a float64 convolution on streamed / ragged inputs and
-matching Inf/NaN masks, then alternated timings on 2^27 samples."""
+matching Inf/NaN masks, then alternated timings on 2^27 samples.  The LQ_FMX16KB switch lived
+only in the A/B build (the working tree before the commit that made the
+16x16 kernel the product path); the product build has no switch."""
 import os
 import sys
 
