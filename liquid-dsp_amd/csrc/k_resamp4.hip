@@ -1,6 +1,7 @@
-// k_resamp4.hip -- resamp_crcf / resamp_cccf for rates 1/2 < r < 2 with a
+// k_resamp4.hip -- resamp_crcf / resamp_cccf for rates 1/2 < r < 4 with a
 // power-of-two filter-bank count (BASELINE configs[4]: r = 1.037, npfb = 64,
-// m = 7; msresamp's arbitrary stage runs at r_a in (1/2, 1)).
+// m = 7; msresamp's arbitrary stage runs at r_a in (1/2, 1)).  Three rate
+// classes: 1 < r <= 2 (UP), 2 < r < 4 (UP, R4) and 1/2 < r < 1 (!UP).
 //
 // Reference: src/filter/src/resamp.c:245-311 (execute: per input, while
 // b < npfb emit y = (1-mu) y_b + mu y_{b+1} and advance the timing), :352-363
@@ -39,6 +40,10 @@
 //     (t & 3) * N4 + t / 4), where the lanes' window reads, about 4/r samples
 //     apart, fall on distinct banks (r = 1.037: about one 2-way conflict per
 //     32-lane group) and the stores on distinct banks.
+// Rates 2 < r < 4 (R4) take the same step (tau still crosses 1 - 1/npfb at
+// most once per output) with up to four outputs per input: d_1, d_2 <= 1,
+// d_3 <= 2 (three steps add less than 1.5), no lower bound, so the passes
+// run over q in [0, L + {0, 1, 1, 2}] -- the same 15 + 16 + 16 + 17 taps.
 // Rates 1/2 < r < 1 (the template's !UP class) run the same pipeline with
 // an output every one or two inputs: the step is tau += 1/r, the emitting
 // input ends (tau -= 1, exact: tau + 1/r >= 1 > z), and a silent input
@@ -116,7 +121,7 @@ __device__ __forceinline__ void wave_fence()
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
-template <int L, int NPC, bool UP, int HM>
+template <int L, int NPC, bool UP, int HM, bool R4 = false>
 __global__ __launch_bounds__(NT4, (HM ? 4 : rs4_blk<L, UP>())) void k_resamp4(lqk_rs4_plan pl, unsigned long long g0,
                                                       unsigned long long K0, int npfb, float del,
                                                       const float2 *__restrict__ taps2,
@@ -357,12 +362,13 @@ __global__ __launch_bounds__(NT4, (HM ? 4 : rs4_blk<L, UP>())) void k_resamp4(lq
             for (int q = 0; q < NW; q++) W[q] = pk(lds_rd8(wb[q & 3] + (q >> 2)));
         }
         // four outputs: pass s over q in [lo, hi] (UP: d_0 = 0, d_1 <= 1,
-        // 1 <= d_2 <= 2, 1 <= d_3 <= 3; !UP: s <= d_s <= 2s)
+        // 1 <= d_2 <= 2, 1 <= d_3 <= 3; R4: 0 <= d_s <= {0, 1, 1, 2}; !UP:
+        // s <= d_s <= 2s)
         v2f acc[4];
 #pragma unroll
         for (int s = 0; s < 4; s++) {
-            constexpr int LO[4] = {0, 0, 1, 1};
-            const int lo = UP ? LO[s] : s, hi = UP ? L + s : L + 2 * s;
+            constexpr int LO[4] = {0, 0, 1, 1}, H4[4] = {0, 1, 1, 2};
+            const int lo = UP ? (R4 ? 0 : LO[s]) : s, hi = UP ? (R4 ? L + H4[s] : L + s) : L + 2 * s;
             const float2 *tb = tt + (PAD - dd[s]) * RS + bk[s];
             const float m = mu[s];
             v2f sacc = {0.0f, 0.0f};
@@ -515,7 +521,7 @@ __global__ __launch_bounds__(NT4, (HM ? 4 : rs4_blk<L, UP>())) void k_resamp4(lq
     }
 }
 
-template <int L, bool UP, int HM>
+template <int L, bool UP, int HM, bool R4 = false>
 void launch_rs4_c(const lqk_rs4_plan &pl, unsigned long long g0, unsigned long long K0, int npfb, float del,
                   const float2 *taps2, const float2 *hist, const float2 *x, int n, float2 *y, int nout,
                   const lqk_rs4_hb &hb, hipStream_t st)
@@ -531,11 +537,11 @@ void launch_rs4_c(const lqk_rs4_plan &pl, unsigned long long g0, unsigned long l
     const int blk = lds * B <= 160 * 1024 ? B : (int)(160 * 1024 / lds);
     const int nb = wgs < 256 * blk ? wgs : 256 * blk;   // persistent: blk per CU
     if (npfb == 64)
-        hipLaunchKernelGGL((k_resamp4<L, 64, UP, HM>), dim3(nb), dim3(NT4), lds, st, pl, g0, K0, npfb, del, taps2,
-                           hist, x, n, y, nout, al16, hb);
+        hipLaunchKernelGGL((k_resamp4<L, 64, UP, HM, R4>), dim3(nb), dim3(NT4), lds, st, pl, g0, K0, npfb, del,
+                           taps2, hist, x, n, y, nout, al16, hb);
     else if constexpr (HM == 0)
-        hipLaunchKernelGGL((k_resamp4<L, 0, UP, 0>), dim3(nb), dim3(NT4), lds, st, pl, g0, K0, npfb, del, taps2,
-                           hist, x, n, y, nout, al16, hb);
+        hipLaunchKernelGGL((k_resamp4<L, 0, UP, 0, R4>), dim3(nb), dim3(NT4), lds, st, pl, g0, K0, npfb, del,
+                           taps2, hist, x, n, y, nout, al16, hb);
 }
 
 template <int L>
@@ -543,7 +549,9 @@ void launch_rs4(const lqk_rs4_plan &pl, unsigned long long g0, unsigned long lon
                 const float2 *taps2, const float2 *hist, const float2 *x, int n, float2 *y, int nout, hipStream_t st)
 {
     const lqk_rs4_hb none{};
-    if (del <= 1.0f)
+    if (del < 0.5f)   // 2 < r < 4: up to four outputs per input
+        launch_rs4_c<L, true, 0, true>(pl, g0, K0, npfb, del, taps2, hist, x, n, y, nout, none, st);
+    else if (del <= 1.0f)
         launch_rs4_c<L, true, 0>(pl, g0, K0, npfb, del, taps2, hist, x, n, y, nout, none, st);
     else
         launch_rs4_c<L, false, 0>(pl, g0, K0, npfb, del, taps2, hist, x, n, y, nout, none, st);

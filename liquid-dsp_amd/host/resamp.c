@@ -165,13 +165,14 @@ static int rs_pow2(unsigned int npfb) { return (npfb & (npfb - 1)) == 0; }
 static int rs_p2(const lq_rs *q) { return rs_pow2(q->npfb) && q->del * (float)q->npfb >= 1.0f; }
 
 /* the output-plan kernel (k_resamp4): complex samples, tau-only timing,
- * 1/2 < r < 2 (del in (0.5, 2)); the walk confirms one or two outputs per
- * input (del <= 1) or an output every one or two inputs (del > 1) */
+ * 1/2 < r < 4 (del in (0.25, 2)); the walk confirms one or two outputs per
+ * input (1/2 <= del <= 1), at most four (del < 1/2) or an output every one
+ * or two inputs (del > 1) */
 static int rs_d4_shape(const lq_rs *q)
 {
     const char *e = getenv("LQ_RESAMP_INPUT_PLAN");   /* 1: always the input-checkpoint kernel (k_resamp3) */
     if (e && strcmp(e, "1") == 0) return 0;
-    return q->kind != LQ_RRRF && rs_p2(q) && q->del > 0.5f && q->del < 2.0f && lqk_resamp4_supported(q->npfb, q->L);
+    return q->kind != LQ_RRRF && rs_p2(q) && q->del > 0.25f && q->del < 2.0f && lqk_resamp4_supported(q->npfb, q->L);
 }
 
 static void rs_put(lqk_rs_entry *e, const rs_state *s, unsigned long long K)
@@ -381,8 +382,8 @@ static unsigned long long rs_walk(lq_rs *q, rs_state x0, unsigned long long n, i
                         c++;
                     }
                     t = x - 1.0f;
-                    if (del <= 1.0f) {
-                        if (c > 2 || (c == 0 && K > 0)) rec->d4_ok = 0;
+                    if (del <= 1.0f) {   /* one or two outputs per input (2 < r < 4: up to four) */
+                        if (c > (del < 0.5f ? 4u : 2u) || (c == 0 && K > 0)) rec->d4_ok = 0;
                     } else {   /* no two silent inputs in a row once outputs began */
                         zr = c == 0 && K > 0 ? zr + 1 : 0;
                         if (c > 1 || zr > 1) rec->d4_ok = 0;
@@ -588,7 +589,9 @@ static void rs_plan_build_direct(lq_rs *q, unsigned long long nx)
 {
     unsigned long long q0, Kend;
     unsigned long long lam;
-    rs_rec_init(&q->pl.rec, rs_d4_shape(q) ? RS_D4 : RS_D3, rs_p2(q), (size_t)-1);
+    /* an output plan is capped at RS_D4_MAXOUT outputs (past it the walk
+     * records an input plan instead) */
+    rs_rec_init(&q->pl.rec, rs_d4_shape(q) ? RS_D4 : RS_D3, rs_p2(q), rs_d4_shape(q) ? RS_D4_MAXOUT / 4 : (size_t)-1);
     if (rs_walk(q, q->now, nx, 0, &q0, &Kend, &lam, &q->pl.rec) != nx || Kend > 0xffffffffull)
         LQ_FAIL("error: resamp_%s: too many outputs for one call\n", lq_ext[q->kind]);
     q->pl.pre = nx + 1;

@@ -1,4 +1,4 @@
-"""k_resamp4 (csrc/k_resamp4.hip): resamp_crcf / _cccf at rates 1/2 < r < 2
+"""k_resamp4 (csrc/k_resamp4.hip): resamp_crcf / _cccf at rates 1/2 < r < 4
 with a power-of-two bank count, against the oracle (`-m gpu`).
 
 The kernel replays an output plan (an entry every fourth output, then up to
@@ -48,7 +48,10 @@ def plan_kind(request):
                                          (1.00624001, 7, 64), (1.02353001, 5, 64),
                                          # 1/2 < r < 1 (the kernel's second rate class)
                                          (0.97, 7, 64), (0.51, 7, 64), (0.6, 13, 32), (0.825, 7, 64),
-                                         (0.75, 4, 128), (0.99, 16, 256), (0.5001, 1, 8), (0.9, 12, 64)])
+                                         (0.75, 4, 128), (0.99, 16, 256), (0.5001, 1, 8), (0.9, 12, 64),
+                                         # 2 < r < 4 (the third class: up to four outputs per input)
+                                         (2.5, 7, 64), (3.7, 7, 64), (2.01, 13, 32), (3.99, 4, 128),
+                                         (3.3, 16, 256), (2.2, 1, 8)])
 def test_resamp4_ragged_calls(plan_kind, rate, m, npfb):
     rate = float(np.float32(rate))
     r = np.random.default_rng(int(rate * 1000) + m + npfb)
@@ -96,7 +99,7 @@ def test_resamp4_cccf_and_long_stream(plan_kind, rate):
     assert G.nrm_err(y, ref) < NRM
 
 
-@pytest.mark.parametrize("off,rate", [(0, 1.037), (8, 1.037), (0, 0.8), (8, 0.8)])
+@pytest.mark.parametrize("off,rate", [(0, 1.037), (8, 1.037), (0, 0.8), (8, 0.8), (0, 3.7), (8, 3.7)])
 def test_resamp4_device_pointers(off, rate):
     # device-resident call; off = 8: output pointer 8 bytes past a 16-byte
     # boundary (the kernel then stores 8 bytes at a time)

@@ -141,6 +141,11 @@ def _lib_schedule4(rate, npfb, nx, periodic):
     (0.75, 128, 20_000),
     (0.99, 256, 300_000),
     (0.9999999, 64, 9_000_000),   # period 8 388 609 inputs
+    (2.5, 64, 300_000),           # 2 < r < 4: up to four outputs per input
+    (3.7, 64, 300_000),           # pre-period before the cycle
+    (2.01, 32, 300_000),
+    (3.99, 64, 300_000),
+    (2.2, 256, 20_000),
 ])
 @pytest.mark.parametrize("periodic", [1, 0])
 def test_output_plan_matches_oracle_schedule(rate, npfb, nx, periodic):
@@ -163,9 +168,9 @@ def test_output_plan_matches_oracle_schedule(rate, npfb, nx, periodic):
     np.testing.assert_array_equal(idx, oidx)
 
 
-@pytest.mark.parametrize("rate", [0.45, 2.5, 3.7])
-def test_output_plan_only_between_half_and_two(rate):
-    """rates outside (1/2, 2) keep the input-checkpoint plan (k_resamp3)"""
+@pytest.mark.parametrize("rate", [0.45, 4.5, 60.0])
+def test_output_plan_only_between_half_and_four(rate):
+    """rates outside (1/2, 4) keep the input-checkpoint plan (k_resamp3 / k_resamp)"""
     k, *_ = _lib_schedule4(float(np.float32(rate)), 64, 10_000, 0)
     assert k == -3
 
@@ -189,7 +194,10 @@ def test_plan_memory(rate, npfb):
     # the host table covers the search walk (Brent's tortoise runs past the
     # period when the orbit does not return to its first states)
     assert h.value <= 16 << 20
+    # the output plan holds the pre-period's entries too (r = 3.7: 864 961
+    # inputs before the cycle, test_periodic_plan_matches_oracle_schedule above)
     rmax = max(rate, 1.0)
-    assert d.value <= 8 * (rmax * per / 4 + 1024) + 16 * (per / 4 + 1024)
+    span = per + {float(np.float32(3.7)): 864_961}.get(float(np.float32(rate)), 0)
+    assert d.value <= 8 * (rmax * span / 4 + 1024) + 16 * (span / 4 + 1024)
     if rate == float(np.float32(0.9999999)):
         assert h.value <= 16 << 20 and d.value <= 24 << 20

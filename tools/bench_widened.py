@@ -173,9 +173,10 @@ def main():
                       "ms": round(dt * 1e3, 4), "value": nc / dt / 1e6, "unit": "M input samples/s"}))
     rs.destroy()
     del x, y
-    # resamp at rates outside k_resamp4's (1/2, 2): r = 0.3 and 3.7 (k_resamp3,
-    # input checkpoints) and r = 60 (above ~52: the per-input k_resamp);
-    # device-resident calls on a cached periodic plan, kernel time from HIP events
+    # resamp away from config 5: r = 0.3 (k_resamp3, input checkpoints), r = 3.7
+    # (k_resamp4's 2 < r < 4 class since r05ze) and r = 60 (above ~52: the
+    # per-input k_resamp); device-resident calls on a cached periodic plan,
+    # kernel time from HIP events
     for rate, nin in ((0.3, 1 << 24), (3.7, 1 << 22), (60.0, 1 << 18)):
         rs = LQ.Resamp(rate, 7, 0.4, 60.0, 64)
         rs.set_stream(S)
@@ -183,7 +184,8 @@ def main():
         nout = rs.num_output(nin)
         y = torch.empty(2 * (nout + 64), device="cuda")
         ms = timed(lambda: rs.execute_block_dev(x.data_ptr(), nin, y.data_ptr()))
-        report("resamp_crcf r=%g m=7 (%s)" % (rate, "k_resamp" if rate > 52 else "k_resamp3"), ms, nout,
+        kern = "k_resamp" if rate > 52 else ("k_resamp4" if 0.5 < rate < 4 else "k_resamp3")
+        report("resamp_crcf r=%g m=7 (%s)" % (rate, kern), ms, nout,
                "output samples", 8 * nin + 8 * nout, "8 B/input + 8 B/output")
         rs.destroy()
     del x, y
