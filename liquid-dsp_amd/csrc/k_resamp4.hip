@@ -1,7 +1,7 @@
-// k_resamp4.hip -- resamp_crcf / resamp_cccf for rates 1/2 < r < 4 with a
-// power-of-two filter-bank count (BASELINE configs[4]: r = 1.037, npfb = 64,
-// m = 7; msresamp's arbitrary stage runs at r_a in (1/2, 1)).  Three rate
-// classes: 1 < r <= 2 (UP), 2 < r < 4 (UP, R4) and 1/2 < r < 1 (!UP).
+// k_resamp4.hip -- resamp_crcf / resamp_cccf for rates 1/2 < r <= npfb with
+// a power-of-two filter-bank count (BASELINE configs[4]: r = 1.037, npfb =
+// 64, m = 7; msresamp's arbitrary stage runs at r_a in (1/2, 1)).  Three rate
+// classes: 1 < r <= 2 (UP), r > 2 (UP, R4) and 1/2 < r < 1 (!UP).
 //
 // Reference: src/filter/src/resamp.c:245-311 (execute: per input, while
 // b < npfb emit y = (1-mu) y_b + mu y_{b+1} and advance the timing), :352-363
@@ -40,8 +40,8 @@
 //     (t & 3) * N4 + t / 4), where the lanes' window reads, about 4/r samples
 //     apart, fall on distinct banks (r = 1.037: about one 2-way conflict per
 //     32-lane group) and the stores on distinct banks.
-// Rates 2 < r < 4 (R4) take the same step (tau still crosses 1 - 1/npfb at
-// most once per output) with up to four outputs per input: d_1, d_2 <= 1,
+// Rates r > 2 (R4) take the same step (tau still crosses 1 - 1/npfb at most
+// once per output) with any number of outputs per input: d_1, d_2 <= 1,
 // d_3 <= 2 (three steps add less than 1.5), no lower bound, so the passes
 // run over q in [0, L + {0, 1, 1, 2}] -- the same 15 + 16 + 16 + 17 taps.
 // Rates 1/2 < r < 1 (the template's !UP class) run the same pipeline with
@@ -549,7 +549,7 @@ void launch_rs4(const lqk_rs4_plan &pl, unsigned long long g0, unsigned long lon
                 const float2 *taps2, const float2 *hist, const float2 *x, int n, float2 *y, int nout, hipStream_t st)
 {
     const lqk_rs4_hb none{};
-    if (del < 0.5f)   // 2 < r < 4: up to four outputs per input
+    if (del < 0.5f)   // r > 2: more than two outputs per input
         launch_rs4_c<L, true, 0, true>(pl, g0, K0, npfb, del, taps2, hist, x, n, y, nout, none, st);
     else if (del <= 1.0f)
         launch_rs4_c<L, true, 0>(pl, g0, K0, npfb, del, taps2, hist, x, n, y, nout, none, st);

@@ -1,4 +1,4 @@
-"""k_resamp4 (csrc/k_resamp4.hip): resamp_crcf / _cccf at rates 1/2 < r < 4
+"""k_resamp4 (csrc/k_resamp4.hip): resamp_crcf / _cccf at rates 1/2 < r <= npfb
 with a power-of-two bank count, against the oracle (`-m gpu`).
 
 The kernel replays an output plan (an entry every fourth output, then up to
@@ -49,9 +49,10 @@ def plan_kind(request):
                                          # 1/2 < r < 1 (the kernel's second rate class)
                                          (0.97, 7, 64), (0.51, 7, 64), (0.6, 13, 32), (0.825, 7, 64),
                                          (0.75, 4, 128), (0.99, 16, 256), (0.5001, 1, 8), (0.9, 12, 64),
-                                         # 2 < r < 4 (the third class: up to four outputs per input)
+                                         # r > 2 (the third class: more than two outputs per input)
                                          (2.5, 7, 64), (3.7, 7, 64), (2.01, 13, 32), (3.99, 4, 128),
-                                         (3.3, 16, 256), (2.2, 1, 8)])
+                                         (3.3, 16, 256), (2.2, 1, 8), (5.5, 7, 32), (10.0, 7, 64),
+                                         (60.0, 4, 64), (7.3, 1, 8)])
 def test_resamp4_ragged_calls(plan_kind, rate, m, npfb):
     rate = float(np.float32(rate))
     r = np.random.default_rng(int(rate * 1000) + m + npfb)

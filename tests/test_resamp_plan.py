@@ -146,6 +146,9 @@ def _lib_schedule4(rate, npfb, nx, periodic):
     (2.01, 32, 300_000),
     (3.99, 64, 300_000),
     (2.2, 256, 20_000),
+    (5.5, 32, 100_000),           # r > 4 on the same class
+    (10.0, 64, 50_000),
+    (60.0, 64, 10_000),
 ])
 @pytest.mark.parametrize("periodic", [1, 0])
 def test_output_plan_matches_oracle_schedule(rate, npfb, nx, periodic):
@@ -168,9 +171,10 @@ def test_output_plan_matches_oracle_schedule(rate, npfb, nx, periodic):
     np.testing.assert_array_equal(idx, oidx)
 
 
-@pytest.mark.parametrize("rate", [0.45, 4.5, 60.0])
-def test_output_plan_only_between_half_and_four(rate):
-    """rates outside (1/2, 4) keep the input-checkpoint plan (k_resamp3 / k_resamp)"""
+@pytest.mark.parametrize("rate", [0.45, 0.3, 65.0, 130.0])
+def test_output_plan_only_above_half_up_to_npfb(rate):
+    """rates below 1/2 or above npfb (bank-index timing) keep the
+    input-checkpoint plan (k_resamp3 / k_resamp)"""
     k, *_ = _lib_schedule4(float(np.float32(rate)), 64, 10_000, 0)
     assert k == -3
 
