@@ -1,7 +1,8 @@
-// k_resamp4.hip -- resamp_crcf / resamp_cccf for rates 1/2 < r <= npfb with
+// k_resamp4.hip -- resamp_crcf / resamp_cccf for rates 1/4 < r <= npfb with
 // a power-of-two filter-bank count (BASELINE configs[4]: r = 1.037, npfb =
-// 64, m = 7; msresamp's arbitrary stage runs at r_a in (1/2, 1)).  Three rate
-// classes: 1 < r <= 2 (UP), r > 2 (UP, R4) and 1/2 < r < 1 (!UP).
+// 64, m = 7; msresamp's arbitrary stage runs at r_a in (1/2, 1)).  Four rate
+// classes: 1 < r <= 2 (UP), r > 2 (UP, R4), 1/2 < r < 1 (!UP) and
+// 1/4 < r <= 1/2 (!UP, DN).
 //
 // Reference: src/filter/src/resamp.c:245-311 (execute: per input, while
 // b < npfb emit y = (1-mu) y_b + mu y_{b+1} and advance the timing), :352-363
@@ -53,6 +54,12 @@
 // spans up to 517 inputs (transposed with 160 slots per residue class: about
 // one 2-way conflict per 32-lane group at every rate in (1/2, 1), from a
 // simulation of the lanes' bank pattern).
+// Rates 1/4 < r <= 1/2 (DN) extend the !UP step by up to two more silent
+// inputs (2 <= 1/r < 4: two to four inputs per output), so 2s <= d_s <= 4s:
+// an L + 13 register window, passes over q in [2s, L + 4s] (15 + 17 + 19 +
+// 21 taps at L = 14), six zero tap rows either side, a tile spans up to
+// L + 1037 inputs (272 slots per residue class), three workgroups per CU up
+// to L = 8 and two above (the window registers).
 // Taps outside an output's own window are zero, so finite samples there add
 // exactly 0; a non-finite sample reaches the outputs whose register window
 // (L + 4 samples) holds it -- a superset of the reference's, as for the
@@ -84,26 +91,26 @@ constexpr int rs4_pf() { return UP && HM == 0 && L <= 16 ? 2 : 1; }
 // Two rate classes share the kernel (UP = 1 < r <= 2: one or two outputs per
 // input; !UP = 1/2 < r < 1: an output every one or two inputs).  Per class:
 // slots per residue class of the transposed window (>= TSW / 4)
-template <bool UP>
-constexpr int rs4_n4() { return UP ? 88 : 160; }
+template <bool UP, bool DN = false>
+constexpr int rs4_n4() { return UP ? 88 : (DN ? 272 : 160); }
 // resident workgroups per CU: four (<= 128 VGPRs: the register window, 2 NW
 // VGPRs, and at 1 < r <= 2 two prefetched tile windows), five at 1/2 < r < 1
 // for L <= 4, three for L > 22
-template <int L, bool UP>
-constexpr int rs4_blk() { return UP ? 4 : (L <= 4 ? 5 : (L <= 22 ? 4 : 3)); }
+template <int L, bool UP, bool DN = false>
+constexpr int rs4_blk() { return UP ? 4 : (DN ? (L <= 8 ? 3 : 2) : (L <= 4 ? 5 : (L <= 22 ? 4 : 3))); }
 
 // window samples of a tile: outputs k0 .. k0+255 lie on inputs i_e .. i_e+255
 // (UP; i_e: input of the tile's table entry, at most 3 outputs before k0) or
 // i_e .. i_e+516 (!UP, two inputs per output at most), and the lane windows
 // reach L samples back and 3 (UP) or 6 (!UP) forward
-template <int L, bool UP>
-constexpr int rs4_tsw() { return UP ? L + 259 : L + 517; }
+template <int L, bool UP, bool DN = false>
+constexpr int rs4_tsw() { return UP ? L + 259 : (DN ? L + 1037 : L + 517); }
 
-template <bool UP>
-constexpr int rs4_pad() { return UP ? 2 : 3; }   // zero tap rows either side
+template <bool UP, bool DN = false>
+constexpr int rs4_pad() { return UP ? 2 : (DN ? 6 : 3); }   // zero tap rows either side
 
-template <int L, bool UP>
-constexpr int rs4_rows() { return L + 1 + 2 * rs4_pad<UP>(); }
+template <int L, bool UP, bool DN = false>
+constexpr int rs4_rows() { return L + 1 + 2 * rs4_pad<UP, DN>(); }
 
 // one 8-byte LDS read, volatile: issued as its own ds_read_b64 (2 LDS cycles
 // per wave instruction), never paired into a ds_read2_b64 (8 cycles)
@@ -121,8 +128,8 @@ __device__ __forceinline__ void wave_fence()
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
-template <int L, int NPC, bool UP, int HM, bool R4 = false>
-__global__ __launch_bounds__(NT4, (HM ? 4 : rs4_blk<L, UP>())) void k_resamp4(lqk_rs4_plan pl, unsigned long long g0,
+template <int L, int NPC, bool UP, int HM, bool R4 = false, bool DN = false>
+__global__ __launch_bounds__(NT4, (HM ? 4 : rs4_blk<L, UP, DN>())) void k_resamp4(lqk_rs4_plan pl, unsigned long long g0,
                                                       unsigned long long K0, int npfb, float del,
                                                       const float2 *__restrict__ taps2,
                                                       const float2 *__restrict__ hist,
@@ -138,13 +145,13 @@ __global__ __launch_bounds__(NT4, (HM ? 4 : rs4_blk<L, UP>())) void k_resamp4(lq
     constexpr int HALO = HM ? ((HW - 1 + 3) & ~3) : 0;
     constexpr int TS = TOUT - HALO;
     static_assert(HM == 0 || (UP && HALO >= HW && HALO < 64), "fused half-band stage shape");
-    constexpr int NR = rs4_rows<L, UP>();
-    constexpr int PAD = rs4_pad<UP>();
-    constexpr int N4 = rs4_n4<UP>();
+    constexpr int NR = rs4_rows<L, UP, DN>();
+    constexpr int PAD = rs4_pad<UP, DN>();
+    constexpr int N4 = rs4_n4<UP, DN>();
     constexpr int LP = (L + 3) & ~1;                 // pair stride of taps2 (host layout)
-    constexpr int TSW = rs4_tsw<L, UP>();
+    constexpr int TSW = rs4_tsw<L, UP, DN>();
     constexpr int NXV = (TSW + 63) / 64;             // window samples per lane
-    constexpr int NW = UP ? L + 4 : L + 7;           // register window per lane
+    constexpr int NW = UP ? L + 4 : (DN ? L + 13 : L + 7);   // register window per lane
     constexpr int AMAX = TSW - NW;                   // last lane window start
     constexpr int PF = rs4_pf<L, UP, HM>();
     constexpr int RG = rs4_rg<L, UP, HM>();
@@ -332,6 +339,14 @@ __global__ __launch_bounds__(NT4, (HM ? 4 : rs4_blk<L, UP>())) void k_resamp4(lq
                 tau = tau - 1.0f;
                 ii++;
             }
+            if constexpr (DN) {   // 2 <= del < 4: up to two more silent inputs
+#pragma unroll
+                for (int e = 0; e < 2; e++)
+                    if (!(tau < z)) {
+                        tau = tau - 1.0f;
+                        ii++;
+                    }
+            }
         };
 #pragma unroll
         for (int s = 0; s < 3; s++)
@@ -368,7 +383,8 @@ __global__ __launch_bounds__(NT4, (HM ? 4 : rs4_blk<L, UP>())) void k_resamp4(lq
 #pragma unroll
         for (int s = 0; s < 4; s++) {
             constexpr int LO[4] = {0, 0, 1, 1}, H4[4] = {0, 1, 1, 2};
-            const int lo = UP ? (R4 ? 0 : LO[s]) : s, hi = UP ? (R4 ? L + H4[s] : L + s) : L + 2 * s;
+            const int lo = UP ? (R4 ? 0 : LO[s]) : (DN ? 2 * s : s),
+                      hi = UP ? (R4 ? L + H4[s] : L + s) : (DN ? L + 4 * s : L + 2 * s);
             const float2 *tb = tt + (PAD - dd[s]) * RS + bk[s];
             const float m = mu[s];
             v2f sacc = {0.0f, 0.0f};
@@ -521,7 +537,7 @@ __global__ __launch_bounds__(NT4, (HM ? 4 : rs4_blk<L, UP>())) void k_resamp4(lq
     }
 }
 
-template <int L, bool UP, int HM, bool R4 = false>
+template <int L, bool UP, int HM, bool R4 = false, bool DN = false>
 void launch_rs4_c(const lqk_rs4_plan &pl, unsigned long long g0, unsigned long long K0, int npfb, float del,
                   const float2 *taps2, const float2 *hist, const float2 *x, int n, float2 *y, int nout,
                   const lqk_rs4_hb &hb, hipStream_t st)
@@ -529,18 +545,18 @@ void launch_rs4_c(const lqk_rs4_plan &pl, unsigned long long g0, unsigned long l
     const bool al16 = ((unsigned long long)y & 15) == 0;   // 16-byte output stores
     const int RS = npfb + 1;
     const size_t lds =
-        (size_t)((rs4_rows<L, UP>() * RS * 8 + 15) & ~15) + (size_t)(NT4 / 64) * 4 * rs4_n4<UP>() * 8;
+        (size_t)((rs4_rows<L, UP, DN>() * RS * 8 + 15) & ~15) + (size_t)(NT4 / 64) * 4 * rs4_n4<UP, DN>() * 8;
     constexpr int TS = TOUT - (HM ? ((2 * HM - 1 + 3) & ~3) : 0);
     const int ntiles = (nout + TS - 1) / TS;
     const int wgs = (ntiles + NT4 / 64 - 1) / (NT4 / 64);
-    constexpr int B = HM ? 4 : rs4_blk<L, UP>();   // the fused stage's window needs the VGPRs of a fifth
+    constexpr int B = HM ? 4 : rs4_blk<L, UP, DN>();   // the fused stage's window needs the VGPRs of a fifth
     const int blk = lds * B <= 160 * 1024 ? B : (int)(160 * 1024 / lds);
     const int nb = wgs < 256 * blk ? wgs : 256 * blk;   // persistent: blk per CU
     if (npfb == 64)
-        hipLaunchKernelGGL((k_resamp4<L, 64, UP, HM, R4>), dim3(nb), dim3(NT4), lds, st, pl, g0, K0, npfb, del,
+        hipLaunchKernelGGL((k_resamp4<L, 64, UP, HM, R4, DN>), dim3(nb), dim3(NT4), lds, st, pl, g0, K0, npfb, del,
                            taps2, hist, x, n, y, nout, al16, hb);
     else if constexpr (HM == 0)
-        hipLaunchKernelGGL((k_resamp4<L, 0, UP, 0, R4>), dim3(nb), dim3(NT4), lds, st, pl, g0, K0, npfb, del,
+        hipLaunchKernelGGL((k_resamp4<L, 0, UP, 0, R4, DN>), dim3(nb), dim3(NT4), lds, st, pl, g0, K0, npfb, del,
                            taps2, hist, x, n, y, nout, al16, hb);
 }
 
@@ -553,6 +569,8 @@ void launch_rs4(const lqk_rs4_plan &pl, unsigned long long g0, unsigned long lon
         launch_rs4_c<L, true, 0, true>(pl, g0, K0, npfb, del, taps2, hist, x, n, y, nout, none, st);
     else if (del <= 1.0f)
         launch_rs4_c<L, true, 0>(pl, g0, K0, npfb, del, taps2, hist, x, n, y, nout, none, st);
+    else if (del >= 2.0f)   // 1/4 < r <= 1/2: an output every two to four inputs
+        launch_rs4_c<L, false, 0, false, true>(pl, g0, K0, npfb, del, taps2, hist, x, n, y, nout, none, st);
     else
         launch_rs4_c<L, false, 0>(pl, g0, K0, npfb, del, taps2, hist, x, n, y, nout, none, st);
 }

@@ -197,8 +197,9 @@ void lqk_resamp(int real_io, const lqk_rs_plan *pl, unsigned long long g0, unsig
 /* taps2: (npfb+1) x LP pairs, LP = (L+3) & ~1: row b < npfb (h_b[L-p], h_{b+1}[L-p]) for p = 1..L, row
  * npfb the BOUNDARY pair (h_{npfb-1}[L-1-p], h_0[L-p]); zero elsewhere (NULL: untiled kernel) */
 /* Output plan of k_resamp4 (csrc/k_resamp4.hip: complex samples, power-of-two
- * npfb, 1/2 < r <= npfb with one or two outputs per input (any number past
- * r = 2), or an output every one or two inputs, over the whole plan):
+ * npfb, 1/4 < r <= npfb with one or two outputs per input (any number past
+ * r = 2), or an output every one or two (two to four below r = 1/2) inputs,
+ * over the whole plan):
  * entries {tau, i} = the timing phase at which a plan output is emitted and
  * the plan input it belongs to -- tab[c] for output 4c (c < npre =
  * ceil(pre / 4)), then tab[npre + c] for output pre + 4c within one period.

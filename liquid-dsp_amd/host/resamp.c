@@ -165,15 +165,15 @@ static int rs_pow2(unsigned int npfb) { return (npfb & (npfb - 1)) == 0; }
 static int rs_p2(const lq_rs *q) { return rs_pow2(q->npfb) && q->del * (float)q->npfb >= 1.0f; }
 
 /* the output-plan kernel (k_resamp4): complex samples, tau-only timing,
- * r > 1/2 (del < 2; tau-only timing needs del npfb >= 1, r <= npfb); the walk
+ * r > 1/4 (del < 4; tau-only timing needs del npfb >= 1, r <= npfb); the walk
  * confirms one or two outputs per input (1/2 <= del <= 1) or an output every
- * one or two inputs (del > 1); past r = 2 any count works (the kernel's R4
- * class) */
+ * one or two (1 < del < 2) / two to four (2 <= del < 4) inputs; past r = 2
+ * any count works (the kernel's R4 class) */
 static int rs_d4_shape(const lq_rs *q)
 {
     const char *e = getenv("LQ_RESAMP_INPUT_PLAN");   /* 1: always the input-checkpoint kernel (k_resamp3) */
     if (e && strcmp(e, "1") == 0) return 0;
-    return q->kind != LQ_RRRF && rs_p2(q) && q->del < 2.0f && lqk_resamp4_supported(q->npfb, q->L);
+    return q->kind != LQ_RRRF && rs_p2(q) && q->del < 4.0f && lqk_resamp4_supported(q->npfb, q->L);
 }
 
 static void rs_put(lqk_rs_entry *e, const rs_state *s, unsigned long long K)
@@ -385,9 +385,9 @@ static unsigned long long rs_walk(lq_rs *q, rs_state x0, unsigned long long n, i
                     t = x - 1.0f;
                     if (del <= 1.0f) {   /* one or two outputs per input (r > 2: any number) */
                         if ((del >= 0.5f && c > 2) || (c == 0 && K > 0)) rec->d4_ok = 0;
-                    } else {   /* no two silent inputs in a row once outputs began */
+                    } else {   /* at most one (del < 2) / three silent inputs in a row once outputs began */
                         zr = c == 0 && K > 0 ? zr + 1 : 0;
-                        if (c > 1 || zr > 1) rec->d4_ok = 0;
+                        if (c > 1 || zr > (del >= 2.0f ? 3 : 1)) rec->d4_ok = 0;
                     }
                     if (i > 0xffffffffull) rec->d4_ok = 0;
                 } else {
@@ -1159,6 +1159,11 @@ long long liquid_mi355x_resamp_schedule4(float _rate, unsigned int _npfb, unsign
                 tau = tau - 1.0f;
                 i++;
             }
+            for (int e = 0; e < 2 && q.del >= 2.0f; e++)   /* 2 <= del < 4: up to two more silent inputs */
+                if (!(tau < z)) {
+                    tau = tau - 1.0f;
+                    i++;
+                }
         }
         const float bf = tau * fn, fb = floorf(bf);
         _b[k] = tau < 0.0f ? -1 : (int)fb;

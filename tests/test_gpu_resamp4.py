@@ -1,4 +1,4 @@
-"""k_resamp4 (csrc/k_resamp4.hip): resamp_crcf / _cccf at rates 1/2 < r <= npfb
+"""k_resamp4 (csrc/k_resamp4.hip): resamp_crcf / _cccf at rates 1/4 < r <= npfb
 with a power-of-two bank count, against the oracle (`-m gpu`).
 
 The kernel replays an output plan (an entry every fourth output, then up to
@@ -52,7 +52,10 @@ def plan_kind(request):
                                          # r > 2 (the third class: more than two outputs per input)
                                          (2.5, 7, 64), (3.7, 7, 64), (2.01, 13, 32), (3.99, 4, 128),
                                          (3.3, 16, 256), (2.2, 1, 8), (5.5, 7, 32), (10.0, 7, 64),
-                                         (60.0, 4, 64), (7.3, 1, 8)])
+                                         (60.0, 4, 64), (7.3, 1, 8),
+                                         # 1/4 < r <= 1/2 (an output every two to four inputs)
+                                         (0.3, 7, 64), (0.45, 13, 32), (0.26, 4, 128), (0.5, 7, 64),
+                                         (0.33, 16, 256), (0.4, 1, 8)])
 def test_resamp4_ragged_calls(plan_kind, rate, m, npfb):
     rate = float(np.float32(rate))
     r = np.random.default_rng(int(rate * 1000) + m + npfb)
@@ -100,7 +103,8 @@ def test_resamp4_cccf_and_long_stream(plan_kind, rate):
     assert G.nrm_err(y, ref) < NRM
 
 
-@pytest.mark.parametrize("off,rate", [(0, 1.037), (8, 1.037), (0, 0.8), (8, 0.8), (0, 3.7), (8, 3.7)])
+@pytest.mark.parametrize("off,rate", [(0, 1.037), (8, 1.037), (0, 0.8), (8, 0.8), (0, 3.7), (8, 3.7), (0, 0.3),
+                                      (8, 0.3)])
 def test_resamp4_device_pointers(off, rate):
     # device-resident call; off = 8: output pointer 8 bytes past a 16-byte
     # boundary (the kernel then stores 8 bytes at a time)

@@ -149,6 +149,11 @@ def _lib_schedule4(rate, npfb, nx, periodic):
     (5.5, 32, 100_000),           # r > 4 on the same class
     (10.0, 64, 50_000),
     (60.0, 64, 10_000),
+    (0.45, 64, 300_000),          # 1/4 < r <= 1/2: an output every two to four inputs
+    (0.3, 64, 300_000),
+    (0.26, 32, 300_000),
+    (0.5, 64, 100_000),
+    (0.4, 256, 20_000),
 ])
 @pytest.mark.parametrize("periodic", [1, 0])
 def test_output_plan_matches_oracle_schedule(rate, npfb, nx, periodic):
@@ -171,9 +176,9 @@ def test_output_plan_matches_oracle_schedule(rate, npfb, nx, periodic):
     np.testing.assert_array_equal(idx, oidx)
 
 
-@pytest.mark.parametrize("rate", [0.45, 0.3, 65.0, 130.0])
-def test_output_plan_only_above_half_up_to_npfb(rate):
-    """rates below 1/2 or above npfb (bank-index timing) keep the
+@pytest.mark.parametrize("rate", [0.25, 0.2, 65.0, 130.0])
+def test_output_plan_only_above_quarter_up_to_npfb(rate):
+    """rates up to 1/4 or above npfb (bank-index timing) keep the
     input-checkpoint plan (k_resamp3 / k_resamp)"""
     k, *_ = _lib_schedule4(float(np.float32(rate)), 64, 10_000, 0)
     assert k == -3

@@ -173,9 +173,9 @@ def main():
                       "ms": round(dt * 1e3, 4), "value": nc / dt / 1e6, "unit": "M input samples/s"}))
     rs.destroy()
     del x, y
-    # resamp away from config 5: r = 0.3 (k_resamp3, input checkpoints), r = 3.7
-    # and 60 (k_resamp4's r > 2 class since r05ze / r05zi); device-resident calls
-    # on a cached periodic plan, kernel time from HIP events
+    # resamp away from config 5: r = 0.3 (k_resamp4's 1/4 < r <= 1/2 class since
+    # r05zj), r = 3.7 and 60 (its r > 2 class since r05ze / r05zi);
+    # device-resident calls on a cached periodic plan, kernel time from HIP events
     for rate, nin in ((0.3, 1 << 24), (3.7, 1 << 22), (60.0, 1 << 18)):
         rs = LQ.Resamp(rate, 7, 0.4, 60.0, 64)
         rs.set_stream(S)
@@ -183,7 +183,7 @@ def main():
         nout = rs.num_output(nin)
         y = torch.empty(2 * (nout + 64), device="cuda")
         ms = timed(lambda: rs.execute_block_dev(x.data_ptr(), nin, y.data_ptr()))
-        kern = "k_resamp4" if rate > 0.5 else "k_resamp3"
+        kern = "k_resamp4" if rate > 0.25 else "k_resamp3"
         report("resamp_crcf r=%g m=7 (%s)" % (rate, kern), ms, nout,
                "output samples", 8 * nin + 8 * nout, "8 B/input + 8 B/output")
         rs.destroy()
