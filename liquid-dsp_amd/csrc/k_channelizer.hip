@@ -448,9 +448,14 @@ bool launch_pfb2_an2048(const void *hsub, const void *hist, const void *x, long 
     const int cmin = (p0 - 1) >> 1;
     const int cmax = (int)((p0 + nb - 1) >> 1);
     const int rows = cmax - cmin + 1;
-    // one workgroup per CU: runs of S rows (a multiple of 8), about 256 runs
+    // one workgroup per CU: runs of S rows (a multiple of 8), about 256 runs.
+    // A remainder of a few rows past 256 full runs goes to one short extra
+    // run rather than stretching every run to the next multiple of 8 (2^27
+    // inputs: 65 537 rows, 256 x 256 + 1 instead of 249 x 264 -- 7 CUs idle)
     long long S = ((long long)rows + 255) / 256;
     S = (S + 7) / 8 * 8;
+    const long long S8 = (long long)rows / 2048 * 8;
+    if (S8 >= 32 && rows - 256 * S8 <= S8 / 4) S = S8;
     if (S < 32) S = 32;
     const long long nseg = (rows + S - 1) / S;
     hipLaunchKernelGGL((k_pfb2_an2048<L>), dim3((unsigned)nseg), dim3(1024), 0, st, (const float *)hsub,

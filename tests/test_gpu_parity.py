@@ -391,6 +391,22 @@ def test_firpfbch2_analyzer_m2048_fused_vs_oracle(m):
     assert G.nrm_err(y, o.execute_block(x)) < NRM
 
 
+@pytest.mark.parametrize("m", [2, 4])
+def test_firpfbch2_analyzer_m2048_short_extra_run(m):
+    # a call of 16 384 blocks + 2 (8 194 rows): 256 runs of 32 rows and one
+    # extra run of 2 rows (launch_pfb2_an2048's balance rule), both parities
+    M = 2048
+    r = rng(11 * M + m)
+    nblocks = 16384 + 2
+    x = cx(r, nblocks * M // 2)
+    g = LQ.FirPfbch2(LQ.LIQUID_ANALYZER, M, m, 60.0)
+    o = O.FirPfbch2(O.ANALYZER, M, m, 60.0)
+    cuts = [0, 1, nblocks]
+    step = M // 2
+    y = np.concatenate([g.execute_block(x[a * step:b * step]) for a, b in zip(cuts[:-1], cuts[1:])])
+    assert G.nrm_err(y, o.execute_block(x)) < NRM
+
+
 @pytest.mark.parametrize("m", [1, 2, 3, 4])
 def test_firpfbch2_analyzer_m4096_fused_vs_oracle(m):
     # M = 4096 with m <= 4: the fused kernel (k_pfb2_an4096, four columns per
