@@ -282,8 +282,12 @@ bool launch_pfb2_an256(const void *hsub, const void *hist, const void *x, long l
     const int cmax = (int)((p0 + nb - 1) >> 1);
     const int rows = cmax - cmin + 1;
     // runs of S rows (a multiple of 8): about 1024 workgroups on long calls
+    // (a remainder of a few rows goes to one short extra run, as in
+    // launch_pfb2_an2048)
     long long S = ((long long)rows + 1023) / 1024;
     S = (S + 7) / 8 * 8;
+    const long long S8 = (long long)rows / 8192 * 8;
+    if (S8 >= 32 && rows - 1024 * S8 <= S8 / 4) S = S8;
     if (S < 32) S = 32;
     const long long nseg = (rows + S - 1) / S;
     hipLaunchKernelGGL((k_pfb2_an256<L, R>), dim3((unsigned)nseg), dim3(256 * R), 0, st, (const float *)hsub,
