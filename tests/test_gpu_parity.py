@@ -391,13 +391,14 @@ def test_firpfbch2_analyzer_m2048_fused_vs_oracle(m):
     assert G.nrm_err(y, o.execute_block(x)) < NRM
 
 
-@pytest.mark.parametrize("M,m", [(2048, 2), (2048, 4), (256, 4), (512, 3)])
+@pytest.mark.parametrize("M,m", [(2048, 2), (2048, 4), (256, 4), (512, 3), (64, 4), (128, 2)])
 def test_firpfbch2_analyzer_short_extra_run(M, m):
     # M = 2048: 16 384 blocks + 2 (8 194 rows), 256 runs of 32 rows and one
     # extra run of 2 rows (launch_pfb2_an2048's balance rule); M = 256 / 512:
-    # 65 536 blocks + 2, 1024 runs of 32 rows and one of 2 (launch_pfb2_an256)
+    # 65 536 blocks + 2, 1024 runs of 32 rows and one of 2 (launch_pfb2_an256);
+    # M = 64 / 128: 131 072 blocks + 2 (sets of 40 rows: no extra run there)
     r = rng(11 * M + m)
-    nblocks = (16384 if M == 2048 else 65536) + 2
+    nblocks = {2048: 16384, 256: 65536, 512: 65536, 64: 131072, 128: 131072}[M] + 2
     x = cx(r, nblocks * M // 2)
     g = LQ.FirPfbch2(LQ.LIQUID_ANALYZER, M, m, 60.0)
     o = O.FirPfbch2(O.ANALYZER, M, m, 60.0)
