@@ -2,9 +2,9 @@
 32x32x16 one it replaced, same process and buffers (dev tool, r05w / r05x):
 normwise agreement with a float64 convolution on streamed / ragged /
 non-finite inputs, then alternated timings.  LQ_FMX16=<10 workgroups per CU
-+ chunks in flight> selected the 16x16 kernel in the A/B build (commit
-"firfilt: 16x16x32 matrix-core kernel (A/B)"); the product build has no
-switch, so every setting below now runs the same kernel."""
++ chunks in flight> selected the 16x16 kernel in the A/B build (the tree
+before commit 7f72544, which made it the product path without a switch), so
+every setting below now runs the same kernel."""
 import os
 import sys
 
