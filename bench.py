@@ -38,6 +38,14 @@ independent stream (C = the box's CPU share, stated in `cores`), beside the
 one-core figure; bounded samples (~10 s + ~5 s).  The secondary legs carry
 their own one-core oracle rates (firfilt, resamp, fftfilt, dotprod n=64).
 
+Output: two JSON lines.  The first ("aux") holds the secondary records
+(per-call legs, dotprod legs, the measured ceilings' launch shapes, the CPU
+baseline detail); the LAST line is the headline record, kept short, with
+firfilt_crcf_h64 as its final key.  Measured ceilings: hand-written HIP copy /
+read / pattern kernels (tools/mb/bw_probe.hip) warmed up like the legs; each
+roofline carries frac (of the 8 TB/s spec) beside frac_of_measured_copy and,
+for the two headline kernels and fftfilt, frac_of_measured_pattern.
+
 per_call: the reference's own per-call benchmark bodies
 (src/*/bench/*_benchmark.c: push/execute one sample, one firpfbch2 block,
 one dot product per call) compiled unchanged against this library by
@@ -398,24 +406,47 @@ def bench_resamp(args, world, rank, stream):
     return res
 
 
-def copy_bandwidth():
-    """Measured device copy rate (read+write GB/s) as a practical HBM ceiling."""
-    a = torch.empty(1 << 28, dtype=torch.float32, device="cuda")
-    b = torch.empty_like(a)
-    for _ in range(3):
-        b.copy_(a)
+PROBE_SO = os.path.join(ROOT, "tools", "mb", "bin", "libbwprobe.so")
+
+
+def measured_ceilings(stream):
+    """Hand-written HIP streaming kernels (tools/mb/bw_probe.hip), each a few
+    launch shapes, every shape warmed up for the same 150 ms floor as the
+    legs: the box's own rate for a plain 16-byte/lane copy, a read-only
+    stream, firpfbch2's 1 read : 2 write tile pattern and firfilt's 1:1
+    chunk pattern, with no arithmetic.  GB/s of algorithmic bytes, best shape."""
+    import ctypes
+    if not os.path.exists(PROBE_SO):
+        return {"error": "tools/mb/bin/libbwprobe.so not built"}
+    lib = ctypes.CDLL(PROBE_SO)
+    lib.bwprobe_run.restype = ctypes.c_int
+    lib.bwprobe_run.argtypes = [ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_longlong, ctypes.c_void_p,
+                                ctypes.c_double, ctypes.c_int, ctypes.POINTER(ctypes.c_double),
+                                ctypes.POINTER(ctypes.c_double), ctypes.c_char_p, ctypes.c_int]
+    src = torch.empty(1 << 29, dtype=torch.float32, device="cuda")   # 2 GiB
+    dst = torch.empty(1 << 30, dtype=torch.float32, device="cuda")   # 4 GiB
+    src.fill_(0.25)
     torch.cuda.synchronize()
-    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    e0.record()
-    for _ in range(10):
-        b.copy_(a)
-    e1.record()
-    torch.cuda.synchronize()
-    ms = e0.elapsed_time(e1) / 10
-    gbps = 2 * a.numel() * 4 / (ms * 1e-3) / 1e9
-    del a, b
+    out, shapes = {}, {}
+    # (key, probe kind, source bytes): copy / read over 1 GiB; the firpfbch2
+    # pattern over the bench's 2^27 samples (1 GiB in, 2 GiB out); the firfilt
+    # pattern over its 2^28 samples (2 GiB in, 2 GiB out)
+    for key, kind, nbytes in (("copy", 0, 1 << 30), ("read", 1, 1 << 30), ("pfb2_pattern", 2, 1 << 30),
+                              ("fir_pattern", 3, 1 << 31)):
+        g, ms = ctypes.c_double(), ctypes.c_double()
+        name = ctypes.create_string_buffer(512)
+        rc = lib.bwprobe_run(kind, src.data_ptr(), dst.data_ptr(), nbytes, stream.cuda_stream, WARMUP_FLOOR_MS, 20,
+                             ctypes.byref(g), ctypes.byref(ms), name, 512)
+        if rc != 0:
+            out[key] = None
+            shapes[key] = "error %d" % rc
+            continue
+        out[key] = g.value
+        shapes[key] = name.value.decode()
+    del src, dst
     torch.cuda.empty_cache()
-    return gbps
+    return {"copy_GBps": out["copy"], "read_GBps": out["read"], "pfb2_pattern_GBps": out["pfb2_pattern"],
+            "fir_pattern_GBps": out["fir_pattern"], "shapes": shapes}
 
 
 def _cpu_pfb2_worker(seconds, seed, start_evt, out_q):
@@ -630,7 +661,7 @@ def main():
         dp_t = {n: (allreduce_max(r["wall"], world), allreduce_max(r["gpu_ms"], world)) for n, r in dp["runs"].items()}
         ff_t = (allreduce_max(ff["wall"], world), allreduce_max(ff["gpu_ms"], world))
 
-    copy_gbps = copy_bandwidth() if rank == 0 else None
+    ceil = measured_ceilings(stream) if rank == 0 else None
     percall = percall_gpu = None
     if rank == 0 and world == 1 and not args.no_percall:
         percall = percall_baseline()
@@ -641,26 +672,59 @@ def main():
         cpu2 = cpu_baselines_secondary(args.cpu_seconds / 4)
 
     if rank == 0:
-        # dominant kernel: firpfbch2 analyzer, one launch per step (+ a tiny
-        # history-window update launch on the same stream)
-        launch_ms = g_pfb / args.steps
-        alg_bytes = 24.0 * pfb["n"]
-        achieved = alg_bytes / (launch_ms * 1e-3) / 1e9
-        traffic = fir_traffic = rs_traffic = ff_traffic = None
-        tsrc = None
+        tj, tsrc = {}, None
         if os.path.exists(args.traffic_json):
             with open(args.traffic_json) as f:
                 tj = json.load(f)
-            # the PMC bytes are not counted in this timed run: a separate
-            # rocprofv3 --pmc pass over the same launch shapes wrote them
-            tsrc = ("HBM bytes per launch from %s: rocprofv3 --pmc FETCH_SIZE (x2, gfx950) + WRITE_SIZE in "
-                    "separate passes over the same launch shapes (tools/profile_round.sh), not counted in this "
-                    "timed run%s" % (os.path.relpath(args.traffic_json, ROOT),
-                                     (", measured " + tj["measured"]) if tj.get("measured") else ""))
-            traffic = tj.get("firpfbch2_bytes_per_launch")
-            fir_traffic = tj.get("firfilt_bytes_per_launch")
-            rs_traffic = tj.get("resamp_bytes_per_launch")
-            ff_traffic = tj.get("fftfilt_bytes_per_launch")
+            # the PMC bytes are not counted in this timed run: separate
+            # rocprofv3 --pmc passes over the same launch shapes wrote them
+            tsrc = "%s (rocprofv3 --pmc FETCH_SIZE x2 + WRITE_SIZE, separate passes%s)" % (
+                os.path.relpath(args.traffic_json, ROOT), (", " + tj["measured"]) if tj.get("measured") else "")
+        copy_gbps = ceil.get("copy_GBps") if ceil else None
+
+        def roof(alg_bytes, launch_ms, traffic, pattern_key=None):
+            ach = alg_bytes / (launch_ms * 1e-3) / 1e9
+            r = {"bound": "hbm", "achieved": ach, "peak": HBM_PEAK_GBPS, "unit": "GB/s", "frac": ach / HBM_PEAK_GBPS,
+                 "traffic": traffic, "launch_ms": launch_ms, "alg_bytes": alg_bytes}
+            if copy_gbps:
+                r["frac_of_measured_copy"] = ach / copy_gbps
+            if pattern_key and ceil and ceil.get(pattern_key):
+                r["frac_of_measured_pattern"] = ach / ceil[pattern_key]
+            return r
+
+        # ---- secondary records first, on their own stdout line, so the final
+        # line (the one the driver parses from its stdout tail) stays short
+        aux = {"aux": "bench.py secondary records (the headline line follows)"}
+        if ceil:
+            aux["measured_ceilings"] = ceil
+        if dp is not None:
+            legs = {}
+            for key, (tw, tg) in dp_t.items():
+                ms = tg / args.steps
+                n, nv = dp["runs"][key]["n"], dp["runs"][key]["nvec"]
+                legs["n%s" % key] = {"value": world * nv * args.steps / tw / 1e6, "unit": "M dot products/s",
+                                     "vectors": nv, "working_set_MB": (8.0 * n + 8.0) * nv / 1e6,
+                                     "launch_ms": ms, "achieved_GBps": (8.0 * n + 8.0) * nv / (ms * 1e-3) / 1e9,
+                                     "frac": (8.0 * n + 8.0) * nv / (ms * 1e-3) / 1e9 / HBM_PEAK_GBPS,
+                                     "warmup_launches": dp["runs"][key]["warm"]["warmup_launches"]}
+            aux["dotprod_cccf"] = {"workload": "dotprod_cccf batched, %d vectors/GPU (BASELINE configs[1]); n16_hbm: "
+                                               "n=16 on 8x the vectors (beyond the 256 MB Infinity Cache)"
+                                               % dp["nvec"], "bytes_per_unit": "8n+8 B/vector", "legs": legs}
+            if cpu2 and "dotprod_cccf_n64" in cpu2:
+                aux["dotprod_cccf"]["cpu_baseline"] = cpu2["dotprod_cccf_n64"]
+        if percall is not None:
+            aux["per_call"] = {"what": "the reference's per-call benchmark loops (src/*/bench/*_benchmark.c) linked "
+                                       "against this library, default mode (single-sample calls on the host, "
+                                       "host/lq_small.c; block calls on the GPU); wall clock", "runs": percall}
+        if percall_gpu is not None:
+            aux["per_call_gpu"] = {"what": "the same loops with LQ_SMALL_CALLS=gpu: every call one GPU round trip",
+                                   "runs": percall_gpu}
+        if cpu is not None:
+            aux["cpu_baseline_detail"] = cpu
+        print(json.dumps(aux), flush=True)
+
+        # ---- the headline line
+        launch_ms = g_pfb / args.steps
         out = {
             "metric": "Msamples/s: firfilt_crcf h=64 & firpfbch2_crcf M=1024; %HBM roofline",
             "value": tot_pfb / t_pfb / 1e6,
@@ -677,106 +741,62 @@ def main():
             "config": {"workload": "firpfbch2_crcf analyzer M=1024 m=4 As=60, %d samples/GPU (BASELINE configs[3])"
                                    % pfb["n"], "M": 1024, "m": 4, "samples_per_gpu": pfb["n"],
                        "blocks_per_step": pfb["nblocks"], "parallelism": "stream-per-gpu x%d" % world},
-            "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBPS, "unit": "GB/s",
-                         "frac": achieved / HBM_PEAK_GBPS, "traffic": traffic, "traffic_source": tsrc,
-                         "bytes_per_unit": "24 B/input sample (8 read + 16 write)",
-                         "launch_ms": launch_ms, "measured_copy_GBps": copy_gbps},
+            "roofline": dict(roof(24.0 * pfb["n"], launch_ms, tj.get("firpfbch2_bytes_per_launch"), "pfb2_pattern_GBps"),
+                             bytes_per_unit="24 B/input sample (8 read + 16 write)", traffic_source=tsrc),
+            "measured_copy_GBps": copy_gbps,
+            "measured_pfb2_pattern_GBps": ceil.get("pfb2_pattern_GBps") if ceil else None,
+            "measured_fir_pattern_GBps": ceil.get("fir_pattern_GBps") if ceil else None,
+            "measured_read_GBps": ceil.get("read_GBps") if ceil else None,
             "warmup_floor": {"floor_ms": WARMUP_FLOOR_MS, "launches": pfb["warm"]["warmup_launches"],
-                             "ms": pfb["warm"]["warmup_ms"],
-                             "what": "untimed launches before the timed steps of every leg: --warmup W, then "
-                                     "more until floor_ms of wall time has passed (clock ramp)"},
-            "cpu_baseline": cpu,
+                             "ms": pfb["warm"]["warmup_ms"]},
         }
+        if cpu is not None:
+            out["cpu_baseline"] = {k: cpu[k] for k in ("value", "unit", "cores", "kind", "sample")}
+            out["cpu_baseline"]["single_core"] = cpu["single_core"]["value"]
+            out["cpu_baseline"]["what"] = ("oracle/oracle.c port of firpfbch2.c:244-282 (the reference is not "
+                                           "buildable here); detail on the preceding aux line")
         if shd is not None:
             out["firpfbch2_sharded_stream"] = {
                 "value": owned_shd * args.steps / t_shd / 1e6, "unit": "Msamples/s", "scaling": "strong",
-                "workload": "ONE firpfbch2_crcf analyzer stream (M=1024 m=4) of %d samples split over %d rank(s)"
-                            % (shd["total"], world),
-                "plan": "liquid-dsp_amd/lqshard.py firpfbch2_plan: even-block shard starts, %d-block warm-up "
-                        "halo recomputed per shard, no data-path collective" % shd["halo_blocks"],
+                "total_samples": shd["total"], "ranks": world, "halo_blocks": shd["halo_blocks"],
                 "ms_per_step": t_shd / args.steps * 1e3, "launch_ms": g_shd / args.steps,
-                "warmup_launches": shd["warm"]["warmup_launches"],
-                "owned_samples": int(owned_shd),
-                "output_checksum": csum_shd,
-                "checksum_def": "sum of the int32 bit patterns of every owned output (fresh object, one pass); "
-                                "equal for every N iff the shards reproduce the single-stream outputs"}
-        if fir is not None:
-            fl_ms = g_fir / args.steps
-            fach = 16.0 * fir["n"] / (fl_ms * 1e-3) / 1e9
-            out["firfilt_crcf_h64"] = {"value": tot_fir / t_fir / 1e6, "unit": "Msamples/s",
-                                       "samples_per_gpu": fir["n"], "ms_per_step": t_fir / args.steps * 1e3,
-                                       "roofline": {"bound": "hbm", "achieved": fach, "peak": HBM_PEAK_GBPS,
-                                                    "unit": "GB/s", "frac": fach / HBM_PEAK_GBPS,
-                                                    "traffic": fir_traffic, "traffic_source": tsrc,
-                                                    "bytes_per_unit": "16 B/sample", "launch_ms": fl_ms},
-                                       "warmup_launches": fir["warm"]["warmup_launches"],
-                                       "warmup_ms": fir["warm"]["warmup_ms"],
-                                       "arith": ("f32-accurate: taps and samples split into three bf16 terms, "
-                                                 "six exact products accumulated in f32 on "
-                                                 "v_mfma_f32_16x16x32_bf16 (k_firfilt_mx16); "
-                                                 "LQ_FIRFILT_NO_MFMA=1 selects the f32 VALU kernel")}
+                "owned_samples": int(owned_shd), "output_checksum": csum_shd}
         if rs is not None:
             rl_ms = g_rs / args.steps
-            rbytes = 8.0 * rs["n"] + 8.0 * rs["nout"] / args.steps
-            rach = rbytes / (rl_ms * 1e-3) / 1e9
             out["resamp_crcf_r1037"] = {"value": tot_rs / t_rs / 1e6, "unit": "Msamples/s (input)",
                                         "workload": "resamp_crcf r=1.037 m=7 npfb=64 (BASELINE configs[4])",
                                         "samples_per_gpu": rs["n"], "outputs_per_step": rs["nout"] / args.steps,
-                                        "ms_per_step": t_rs / args.steps * 1e3,
-                                        "first_call_ms": first_rs,
-                                        "first_call": "a fresh object's first execute_block_dev over the "
-                                                      "whole input (timing plan built on the host + upload + "
-                                                      "kernel), wall clock",
-                                        "roofline": {"bound": "hbm", "achieved": rach, "peak": HBM_PEAK_GBPS,
-                                                     "unit": "GB/s", "frac": rach / HBM_PEAK_GBPS,
-                                                     "traffic": rs_traffic, "traffic_source": tsrc,
-                                                     "bytes_per_unit": "8 B/input + 8 B/output",
-                                                     "launch_ms": rl_ms},
-                                        "warmup_launches": rs["warm"]["warmup_launches"],
-                                        "warmup_ms": rs["warm"]["warmup_ms"]}
-        if dp is not None:
-            legs = {}
-            for key, (tw, tg) in dp_t.items():
-                ms = tg / args.steps
-                n, nv = dp["runs"][key]["n"], dp["runs"][key]["nvec"]
-                legs["n%s" % key] = {"value": world * nv * args.steps / tw / 1e6, "unit": "M dot products/s",
-                                     "vectors": nv, "working_set_MB": (8.0 * n + 8.0) * nv / 1e6,
-                                     "launch_ms": ms, "achieved_GBps": (8.0 * n + 8.0) * nv / (ms * 1e-3) / 1e9,
-                                     "frac": (8.0 * n + 8.0) * nv / (ms * 1e-3) / 1e9 / HBM_PEAK_GBPS,
-                                     "warmup_launches": dp["runs"][key]["warm"]["warmup_launches"]}
-            out["dotprod_cccf"] = {"workload": "dotprod_cccf batched, %d vectors/GPU (BASELINE configs[1])"
-                                   % dp["nvec"], "bytes_per_unit": "8n+8 B/vector", "legs": legs}
+                                        "ms_per_step": t_rs / args.steps * 1e3, "first_call_ms": first_rs,
+                                        "roofline": dict(roof(8.0 * rs["n"] + 8.0 * rs["nout"] / args.steps, rl_ms,
+                                                              tj.get("resamp_bytes_per_launch")),
+                                                         bytes_per_unit="8 B/input + 8 B/output")}
+            if cpu2 and "resamp_crcf_r1037" in cpu2:
+                out["resamp_crcf_r1037"]["cpu_baseline"] = cpu2["resamp_crcf_r1037"]
+        if ff is not None:
             ms = ff_t[1] / args.steps
             out["fftfilt_crcf_h512"] = {"value": world * ff["n"] * args.steps / ff_t[0] / 1e6, "unit": "Msamples/s",
                                         "workload": "fftfilt_crcf h=512 overlap-save, %d samples/GPU "
                                                     "(BASELINE configs[2])" % ff["n"],
-                                        "launch_ms": ms, "achieved_GBps": 16.0 * ff["n"] / (ms * 1e-3) / 1e9,
-                                        "frac": 16.0 * ff["n"] / (ms * 1e-3) / 1e9 / HBM_PEAK_GBPS,
-                                        "bytes_per_unit": "16 B/sample",
-                                        "roofline": {"bound": "hbm",
-                                                     "achieved": 16.0 * ff["n"] / (ms * 1e-3) / 1e9,
-                                                     "peak": HBM_PEAK_GBPS, "unit": "GB/s",
-                                                     "frac": 16.0 * ff["n"] / (ms * 1e-3) / 1e9 / HBM_PEAK_GBPS,
-                                                     "traffic": ff_traffic, "traffic_source": tsrc, "bytes_per_unit": "16 B/sample",
-                                                     "launch_ms": ms},
-                                        "warmup_launches": ff["warm"]["warmup_launches"],
-                                        "warmup_ms": ff["warm"]["warmup_ms"]}
-        if percall is not None:
-            out["per_call"] = {"what": "the reference's per-call benchmark loops (src/*/bench/*_benchmark.c) "
-                                       "linked against this library, default mode: single-sample calls on the "
-                                       "host (host/lq_small.c), block calls (firpfbch/firpfbch2 blocks) on the "
-                                       "GPU; wall clock",
-                               "runs": percall}
-        if percall_gpu is not None:
-            out["per_call_gpu"] = {
-                "what": "the same loops with LQ_SMALL_CALLS=gpu: every call one GPU round trip",
-                "runs": percall_gpu}
-        if cpu2:
-            for leg, c in cpu2.items():
-                key = "dotprod_cccf" if leg == "dotprod_cccf_n64" else leg
-                if key in out:
-                    out[key]["cpu_baseline"] = c
-        print(json.dumps(out))
+                                        "roofline": dict(roof(16.0 * ff["n"], ms, tj.get("fftfilt_bytes_per_launch"),
+                                                              "fir_pattern_GBps"), bytes_per_unit="16 B/sample")}
+            if cpu2 and "fftfilt_crcf_h512" in cpu2:
+                out["fftfilt_crcf_h512"]["cpu_baseline"] = cpu2["fftfilt_crcf_h512"]
+        if dp is not None:
+            out["dotprod_cccf_frac"] = {k: round(v["frac"], 4) for k, v in aux["dotprod_cccf"]["legs"].items()}
+        if fir is not None:
+            # last key of the line: the second headline workload
+            fl_ms = g_fir / args.steps
+            out["firfilt_crcf_h64"] = {"value": tot_fir / t_fir / 1e6, "unit": "Msamples/s",
+                                       "workload": "firfilt_crcf h=64 execute_block_dev, %d samples/GPU" % fir["n"],
+                                       "samples_per_gpu": fir["n"], "ms_per_step": t_fir / args.steps * 1e3,
+                                       "warmup_launches": fir["warm"]["warmup_launches"],
+                                       "arith": "f32-accurate three-term bf16 split on v_mfma_f32_16x16x32_bf16",
+                                       "roofline": dict(roof(16.0 * fir["n"], fl_ms, tj.get("firfilt_bytes_per_launch"),
+                                                             "fir_pattern_GBps"), bytes_per_unit="16 B/sample",
+                                                        traffic_source=tsrc)}
+            if cpu2 and "firfilt_crcf_h64" in cpu2:
+                out["firfilt_crcf_h64"]["cpu_baseline"] = cpu2["firfilt_crcf_h64"]
+        print(json.dumps(out), flush=True)
     if world > 1:
         dist.barrier()
         dist.destroy_process_group()

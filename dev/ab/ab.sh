@@ -1,10 +1,10 @@
 #!/bin/bash
 # A/B timing of alternative library builds on one box (dev tool).  Each
 # argument is a directory holding a libliquid_mi355x.so built from a variant
-# (tools/ab_build.sh); the bench runs alternate A B A B ... so box drift hits
+# (dev/ab/ab_build.sh); the bench runs alternate A B A B ... so box drift hits
 # every variant alike.  Extra bench flags come from $AB_FLAGS.
 set -o pipefail
-cd "$(dirname "$0")/.."
+cd "$(dirname "$0")/../.."
 mkdir -p gpurun_out
 FLAGS=${AB_FLAGS:---no-extra --no-shard --no-percall --no-cpu-baseline}
 for rep in 1 2; do

@@ -1,7 +1,7 @@
 """msresamp interpolating / decimating chains and their resampler stage alone,
 device resident (dev tool): kernel time per call from HIP events on the
 objects' stream, 20 warm-up + 30 timed calls.
-    python tools/ab_msresamp.py
+    python dev/ab/ab_msresamp.py
 """
 import json
 import os
@@ -9,7 +9,7 @@ import sys
 
 import torch
 
-ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 sys.path.insert(0, os.path.join(ROOT, "liquid-dsp_amd"))
 import liquidmi as LQ  # noqa: E402
 

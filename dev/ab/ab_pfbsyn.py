@@ -1,11 +1,11 @@
 """firpfbch_crcf synthesizer kernel time for given (M, m) on 2^27 samples
-(dev A/B tool; the library comes from LQ_LIB_PATH as in tools/ab.sh)."""
+(dev A/B tool; the library comes from LQ_LIB_PATH as in dev/ab/ab.sh)."""
 import os
 import sys
 
 import torch
 
-sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "tools"))
+sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))), "tools"))
 import bench_widened as W  # noqa: E402
 
 L = W.LQ.lib()

@@ -1,10 +1,10 @@
 #!/bin/bash
-# A/B of library variants on tools/ab_msresamp.py (dev tool): ab_rs.sh dir1 dir2 ...
-cd "$(dirname "$0")/.."
+# A/B of library variants on dev/ab/ab_msresamp.py (dev tool): ab_rs.sh dir1 dir2 ...
+cd "$(dirname "$0")/../.."
 mkdir -p gpurun_out
 for rep in 1 2 3; do
   for d in "$@"; do
-    LQ_LIB_PATH=$d/libliquid_mi355x.so timeout -k 10 120 python tools/ab_msresamp.py > gpurun_out/ab_rs.log 2>&1 || { tail -5 gpurun_out/ab_rs.log; exit 1; }
+    LQ_LIB_PATH=$d/libliquid_mi355x.so timeout -k 10 120 python dev/ab/ab_msresamp.py > gpurun_out/ab_rs.log 2>&1 || { tail -5 gpurun_out/ab_rs.log; exit 1; }
     python3 -c "
 import json
 out = {}

@@ -1,11 +1,11 @@
 """spgramcf estimate_psd kernel time, nfft = 1024 on 2^26 samples (dev A/B
-tool; the library comes from LQ_LIB_PATH as in tools/ab.sh)."""
+tool; the library comes from LQ_LIB_PATH as in dev/ab/ab.sh)."""
 import os
 import sys
 
 import torch
 
-sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "tools"))
+sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))), "tools"))
 import bench_widened as W  # noqa: E402
 
 L = W.LQ.lib()

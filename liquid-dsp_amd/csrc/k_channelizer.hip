@@ -488,9 +488,6 @@ bool launch_pfb2_an2048(const void *hsub, const void *hist, const void *x, long 
 // prefetch registers sit beside the ring and a transform (10 -> 2 spilled
 // VGPRs: 1.13 -> 1.11 ms per 2^27 samples; m <= 3 keep the early prefetch,
 // 0.995 vs 1.07 ms at m = 2)
-#ifndef A4_PF_LATE
-#define A4_PF_LATE (L > 6)
-#endif
 constexpr int A4_QS = 1092;            // quarter stride: 1088-float2 transform scratch; 1092 * 8 = 32 mod 128 B
 constexpr int A4_BSTR = 4 * A4_QS;     //   puts the four quarters of a dot-phase write on distinct bank groups
 template <int L>
@@ -577,7 +574,7 @@ __global__ __launch_bounds__(1024, 1) void k_pfb2_an4096(const float *__restrict
             } else {
                 wo[q] = pf[q];
             }
-            if (!A4_PF_LATE) pf[q] = row_sample(c + 1, tid + 1024 * q);
+            if (!(L > 6)) pf[q] = row_sample(c + 1, tid + 1024 * q);
         }
         {
             float2 *B0 = xr + slot(2 * c) * A4_BSTR, *B1 = xr + slot(2 * c + 1) * A4_BSTR,
@@ -615,7 +612,7 @@ __global__ __launch_bounds__(1024, 1) void k_pfb2_an4096(const float *__restrict
             fft1024_wave_rt<-1>(v, Bq, a1, a4, tw2, lane);   // natural order at k + 4 (k >> 8)
         }
         __syncthreads();   // every quarter of both blocks transformed
-        if (A4_PF_LATE) {   // the next row's loads, issued after the transforms (no prefetch registers across them)
+        if ((L > 6)) {   // the next row's loads, issued after the transforms (no prefetch registers across them)
 #pragma unroll
             for (int q = 0; q < 4; q++) pf[q] = row_sample(c + 1, tid + 1024 * q);
         }
@@ -1248,10 +1245,7 @@ bool launch_pfb_an_fused(int M, int p, const void *hsub, const void *hist, const
 // then combine
 //     Y[k + 1024 s] = sum_r W_4096^(r k) Q_r[k] (-i)^(r s)
 // into 8-byte coalesced stores.  The ring keeps its oldest row in LDS.
-#ifndef A4_G
-#define A4_G 3
-#endif
-template <int P, typename TC, int G = A4_G>
+template <int P, typename TC, int G = 3>
 __global__ __launch_bounds__(1024, 1) void k_pfb_an4096(const TC *__restrict__ hsub, const float2 *__restrict__ hist,
                                                         const float2 *__restrict__ x, int n_in, int nb, int S,
                                                         float2 *__restrict__ Y, const float2 *__restrict__ tw4096)
@@ -1585,10 +1579,8 @@ bool launch_pfb_syn_fused(int M, int p, const void *hsub, const void *state, con
 // further LDS traffic.  Runs warm up on the blocks before them (transformed
 // again, outputs dropped) or, for the call's first run, on the object's last
 // p-1 transforms (state); the z of the call's last p-1 blocks go to znew.
-#ifndef A4_SYN_G8
-#define A4_SYN_G8 3   // p = 8: three-block groups spill 18 VGPRs and still beat two-block groups (0.585 vs 0.615 ms)
-#endif
-template <int P, typename TC, int G = (P > 6 ? A4_SYN_G8 : 3)>
+// (p = 8: three-block groups spill 18 VGPRs and still beat two-block groups, 0.585 vs 0.615 ms)
+template <int P, typename TC, int G = 3>
 __global__ __launch_bounds__(1024, 1) void k_pfb_syn4096(const TC *__restrict__ hsub, const float2 *__restrict__ state,
                                                          const float2 *__restrict__ X, int nb, int S,
                                                          float2 *__restrict__ y, float2 *__restrict__ znew,
@@ -2589,6 +2581,20 @@ void fft_batch_scaled(unsigned n, int dir, const void *x, void *y, long long bat
     LQ_CHECK_LAUNCH();
 }
 
+// Diagnostic switches (DESIGN.md (a) history): LQ_PFB2_TWO_PASS /
+// LQ_PFB_TWO_PASS in the environment route the fused channelizer sizes
+// through the generic two-pass path.  Read once per process.
+bool pfb2_two_pass()
+{
+    static const bool v = getenv("LQ_PFB2_TWO_PASS") != nullptr;
+    return v;
+}
+bool pfb_two_pass()
+{
+    static const bool v = getenv("LQ_PFB_TWO_PASS") != nullptr;
+    return v;
+}
+
 } // namespace
 
 extern "C" void lqk_fft_batch(unsigned int n, int dir, const void *x, void *y, unsigned long long batch,
@@ -2622,7 +2628,7 @@ extern "C" void lqk_firpfbch2_analyzer(unsigned int M, unsigned int m, const voi
             const float2 *xc = (const float2 *)x + b0 * M2;
             const void *hc = b0 == 0 ? hist : (const void *)(xc - HL);
             float2 *Yc = (float2 *)Y + b0 * M;
-            if ((M == 256 || M == 512) && 2 * m <= 8 && !getenv("LQ_PFB2_TWO_PASS")) {
+            if ((M == 256 || M == 512) && 2 * m <= 8 && !pfb2_two_pass()) {
                 bool f = false;
 #define LQ_F(LL)                                                                                           \
     case LL:                                                                                               \
@@ -2636,7 +2642,7 @@ extern "C" void lqk_firpfbch2_analyzer(unsigned int M, unsigned int m, const voi
 #undef LQ_F
                 if (f) continue;
             }
-            if (M == 2048 && 2 * m <= 8 && !getenv("LQ_PFB2_TWO_PASS")) {
+            if (M == 2048 && 2 * m <= 8 && !pfb2_two_pass()) {
                 bool f = false;
                 switch (2 * m) {
                 case 2: f = launch_pfb2_an2048<2>(hsub, hc, xc, nbc, p0, Yc, st); break;
@@ -2647,7 +2653,7 @@ extern "C" void lqk_firpfbch2_analyzer(unsigned int M, unsigned int m, const voi
                 }
                 if (f) continue;
             }
-            if (M == 4096 && 2 * m <= 8 && !getenv("LQ_PFB2_TWO_PASS")) {
+            if (M == 4096 && 2 * m <= 8 && !pfb2_two_pass()) {
                 bool f = false;
                 switch (2 * m) {
                 case 2: f = launch_pfb2_an4096<2>(hsub, hc, xc, nbc, p0, Yc, st); break;
@@ -2658,7 +2664,7 @@ extern "C" void lqk_firpfbch2_analyzer(unsigned int M, unsigned int m, const voi
                 }
                 if (f) continue;
             }
-            if ((M == 64 || M == 128) && 2 * m <= 8 && !getenv("LQ_PFB2_TWO_PASS")) {
+            if ((M == 64 || M == 128) && 2 * m <= 8 && !pfb2_two_pass()) {
                 bool f = false;
 #define LQ_F(LL)                                                                                           \
     case LL:                                                                                               \
@@ -2728,12 +2734,12 @@ extern "C" void lqk_firpfbch2_synthesizer(unsigned int M, unsigned int m, const 
     hipStream_t st = (hipStream_t)stream;
     const long long HB = 4 * (long long)m - 1;
     float2 *Z = (float2 *)zscratch;
-    if (!getenv("LQ_PFB2_TWO_PASS") && M == 4096 &&
+    if (!pfb2_two_pass() && M == 4096 &&
         launch_pfb2_syn4096((int)m, hsub, state, X, (long long)nblocks, p0, Y, Z, st)) {
         LQ_CHECK(hipMemcpyAsync(state, Z, HB * M * sizeof(float2), hipMemcpyDeviceToDevice, st));
         return;
     }
-    if (!getenv("LQ_PFB2_TWO_PASS") &&
+    if (!pfb2_two_pass() &&
         launch_pfb2_syn_fused((int)M, (int)m, hsub, state, X, (long long)nblocks, p0, Y, Z, st)) {
         LQ_CHECK(hipMemcpyAsync(state, Z, HB * M * sizeof(float2), hipMemcpyDeviceToDevice, st));
         return;
@@ -2767,15 +2773,15 @@ extern "C" void lqk_firpfbch_analyzer(int ctaps, unsigned int M, unsigned int p,
     if (nblocks == 0) return;
     if (lqk_firpfbch_analyzer_fast(ctaps, M, p, hsub, hist, x, nblocks, Y, stream)) return;
     hipStream_t st = (hipStream_t)stream;
-    if (!getenv("LQ_PFB_TWO_PASS") &&
+    if (!pfb_two_pass() &&
         (ctaps ? launch_pfb_an_fused<float2>((int)M, (int)p, hsub, hist, x, (long long)nblocks, Y, st)
                : launch_pfb_an_fused<float>((int)M, (int)p, hsub, hist, x, (long long)nblocks, Y, st)))
         return;
-    if (M == 4096 && !getenv("LQ_PFB_TWO_PASS") &&
+    if (M == 4096 && !pfb_two_pass() &&
         (ctaps ? launch_pfb_an4096<float2>((int)p, hsub, hist, x, (long long)nblocks, Y, st)
                : launch_pfb_an4096<float>((int)p, hsub, hist, x, (long long)nblocks, Y, st)))
         return;
-    if (!getenv("LQ_PFB_TWO_PASS") &&
+    if (!pfb_two_pass() &&
         (ctaps ? launch_pfb_an_small<float2>((int)M, (int)p, hsub, hist, x, (long long)nblocks, Y, st)
                : launch_pfb_an_small<float>((int)M, (int)p, hsub, hist, x, (long long)nblocks, Y, st)))
         return;
@@ -2806,19 +2812,19 @@ extern "C" void lqk_firpfbch_synthesizer(int ctaps, unsigned int M, unsigned int
     float2 *Z = (float2 *)zscratch;
     // fused M = 256 / 512: the last p-1 transforms land in the scratch, then
     // become the state (every workgroup reads the old state first)
-    if (!getenv("LQ_PFB_TWO_PASS") &&
+    if (!pfb_two_pass() &&
         (ctaps ? launch_pfb_syn_fused<float2>((int)M, (int)p, hsub, state, X, (long long)nblocks, y, Z, st)
                : launch_pfb_syn_fused<float>((int)M, (int)p, hsub, state, X, (long long)nblocks, y, Z, st))) {
         if (HB > 0) LQ_CHECK(hipMemcpyAsync(state, Z, HB * M * sizeof(float2), hipMemcpyDeviceToDevice, st));
         return;
     }
-    if (M == 4096 && !getenv("LQ_PFB_TWO_PASS") &&
+    if (M == 4096 && !pfb_two_pass() &&
         (ctaps ? launch_pfb_syn4096<float2>((int)p, hsub, state, X, (long long)nblocks, y, Z, st)
                : launch_pfb_syn4096<float>((int)p, hsub, state, X, (long long)nblocks, y, Z, st))) {
         if (HB > 0) LQ_CHECK(hipMemcpyAsync(state, Z, HB * M * sizeof(float2), hipMemcpyDeviceToDevice, st));
         return;
     }
-    if (!getenv("LQ_PFB_TWO_PASS") &&
+    if (!pfb_two_pass() &&
         (ctaps ? launch_pfb_syn_small<float2>((int)M, (int)p, hsub, state, X, (long long)nblocks, y, Z, st)
                : launch_pfb_syn_small<float>((int)M, (int)p, hsub, state, X, (long long)nblocks, y, Z, st))) {
         if (HB > 0) LQ_CHECK(hipMemcpyAsync(state, Z, HB * M * sizeof(float2), hipMemcpyDeviceToDevice, st));

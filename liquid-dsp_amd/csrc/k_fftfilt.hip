@@ -1,6 +1,5 @@
 // k_fftfilt.hip -- FFT fast convolution for fftfilt_{crcf,rrrf,cccf}.
-// Default kernel: k_fftfilt_r16 (register radix-16 transforms, persistent
-// grid); k_fftfilt (LDS Stockham) is the earlier form, kept for comparison.
+// Kernel: k_fftfilt_r16 (register radix-16 transforms, persistent grid).
 //
 // Reference: src/filter/src/fftfilt.c:193-260 runs overlap-ADD with a 2n-point
 // transform per n-sample call; its output is the causal linear convolution
@@ -23,79 +22,26 @@ namespace {
 
 constexpr int NT = 256;
 constexpr int NFFT = 4096;
-// k_fftfilt_r16 configuration (tools/mb/mb_fftfilt.hip, h=512, 2^26 samples):
-// with the packed transforms (lq_device.h) and buffer-descriptor loads /
-// stores (no per-sample branches or 64-bit addresses) the kernel needs 128
-// VGPRs including the filter spectrum held in registers, so four waves per
-// SIMD; 4096 persistent workgroups: 0.253 ms (float2 pointer loads with
-// branches and ~220 VGPRs: 0.283 ms; a second, history, load for every
-// segment instead of the first only: 0.367 ms)
-#ifndef FF_HREG
-#define FF_HREG true
-#endif
-#ifndef FF_WPE
-#define FF_WPE 4
-#endif
-#ifndef FF_STAUX
-#define FF_STAUX 2   // cache policy of the output stores: non-temporal (A/B on one box: 0.2503 vs 0.2538 ms)
-#endif
-#ifndef FF_EXP
-#define FF_EXP 0   // timing experiments (wrong outputs): 1 no transforms (the kernel's memory pattern alone)
-#endif
-
-// kind 0: real input/output (rrrf), otherwise complex
-template <bool REAL>
-__global__ __launch_bounds__(NT) void k_fftfilt(int hm1, const float2 *__restrict__ H, const void *__restrict__ hist,
-                                                const void *__restrict__ xin, long long n, void *__restrict__ yout,
-                                                float sre, float sim, const float2 *__restrict__ tw)
-{
-    __shared__ __attribute__((aligned(16))) float2 a[NFFT];
-    __shared__ __attribute__((aligned(16))) float2 b[NFFT];
-    const int L = NFFT - hm1;
-    const long long s0 = (long long)blockIdx.x * L;
-    for (int u = threadIdx.x; u < NFFT; u += NT) {
-        const long long s = s0 - hm1 + u;
-        float2 v = make_float2(0.f, 0.f);
-        if (REAL) {
-            const float *x = (const float *)xin;
-            const float *hs = (const float *)hist;
-            if (s < 0) v.x = hs[hm1 + s];
-            else if (s < n) v.x = x[s];
-        } else {
-            const float2 *x = (const float2 *)xin;
-            const float2 *hs = (const float2 *)hist;
-            if (s < 0) v = hs[hm1 + s];
-            else if (s < n) v = x[s];
-        }
-        a[u] = v;
-    }
-    __syncthreads();
-    float2 *F = lds_fft<NFFT, 1, NT>(a, b, tw, +1);
-    for (int u = threadIdx.x; u < NFFT; u += NT) F[u] = cmul(F[u], H[u]);
-    __syncthreads();
-    float2 *other = (F == a) ? b : a;
-    float2 *T = lds_fft<NFFT, 1, NT>(F, other, tw, -1);
-    for (int k = threadIdx.x; k < L; k += NT) {
-        const long long t = s0 + k;
-        if (t >= n) break;
-        const float2 r = T[hm1 + k];
-        if (REAL) {
-            ((float *)yout)[t] = r.x * sre;
-        } else {
-            ((float2 *)yout)[t] = make_float2(r.x * sre - r.y * sim, r.x * sim + r.y * sre);
-        }
-    }
-}
+// k_fftfilt_r16 (tools/mb/mb_fftfilt.hip, h=512, 2^26 samples): with the
+// packed transforms (lq_device.h) and buffer-descriptor loads / stores (no
+// per-sample branches or 64-bit addresses) the kernel needs 128 VGPRs
+// including the filter spectrum held in registers, so four waves per SIMD;
+// 4096 persistent workgroups: 0.253 ms (float2 pointer loads with branches
+// and ~220 VGPRs: 0.283 ms; a second, history, load for every segment
+// instead of the first only: 0.367 ms).  Output stores are non-temporal
+// (0.2503 vs 0.2538 ms default policy).
+constexpr int FF_WPE = 4;        // resident workgroups per CU
+constexpr int FF_STAUX = 2;      // store cache policy: non-temporal
 
 __device__ __forceinline__ float2 to_c2(float a) { return make_float2(a, 0.f); }
 __device__ __forceinline__ float2 to_c2(float2 a) { return a; }
 
-// Register form (default): 256 threads, thread t holds segment samples
+// Register form: 256 threads, thread t holds segment samples
 // t + 256 n; forward 4096-point FFT (fft4096_r16), x H, inverse, all with the
 // data in registers and two LDS transposes per transform (35 KB LDS, four
 // workgroups per CU); loads and stores are coalesced across t.
-template <bool REAL, bool HREG, int WPE>
-__global__ __launch_bounds__(NT, WPE) void k_fftfilt_r16(int hm1, const float2 *__restrict__ H,
+template <bool REAL>
+__global__ __launch_bounds__(NT, FF_WPE) void k_fftfilt_r16(int hm1, const float2 *__restrict__ H,
                                                     const void *__restrict__ hist, const void *__restrict__ xin,
                                                     long long n, void *__restrict__ yout, float sre, float sim,
                                                     const float2 *__restrict__ tw)
@@ -105,11 +51,9 @@ __global__ __launch_bounds__(NT, WPE) void k_fftfilt_r16(int hm1, const float2 *
     const int t = threadIdx.x;
     const long long nseg = (n + L - 1) / L;
     // persistent: the filter spectrum stays in registers across segments
-    float2 hv[HREG ? 16 : 1];
-    if (HREG) {
+    float2 hv[16];
 #pragma unroll
-        for (int k = 0; k < 16; k++) hv[k] = H[t + 256 * k];
-    }
+    for (int k = 0; k < 16; k++) hv[k] = H[t + 256 * k];
     using S = typename std::conditional<REAL, float, float2>::type;
     constexpr int ES = (int)sizeof(S);
     // range-checked buffer descriptors replace the per-sample branches (and
@@ -155,10 +99,10 @@ __global__ __launch_bounds__(NT, WPE) void k_fftfilt_r16(int hm1, const float2 *
                 v[q] = __builtin_bit_cast(float2, __builtin_amdgcn_raw_buffer_load_b64(rx, ox, 0, 0));
         }
     }
-    if (!(FF_EXP & 1)) fft4096_r16<+1>(v, lds, w16, t);
+    fft4096_r16<+1>(v, lds, w16, t);
 #pragma unroll
-    for (int k = 0; k < 16; k++) v[k] = unpk(pk_cmul(pk(v[k]), pk(HREG ? hv[k & (HREG ? 15 : 0)] : H[t + 256 * k])));
-    if (!(FF_EXP & 1)) fft4096_r16<-1>(v, lds, w16, t);
+    for (int k = 0; k < 16; k++) v[k] = unpk(pk_cmul(pk(v[k]), pk(hv[k])));
+    fft4096_r16<-1>(v, lds, w16, t);
 #pragma unroll
     for (int q = 0; q < 16; q++) {
         const int i = t + 256 * q;
@@ -202,10 +146,10 @@ extern "C" void lqk_fftfilt_run(int real_io, unsigned int hlen, const void *H, c
         const long long nsegc = ((long long)nc + L - 1) / L;
         const unsigned grid = (unsigned)(nsegc < 4096 ? nsegc : 4096);   // persistent, four resident per CU
         if (real_io)
-            hipLaunchKernelGGL((k_fftfilt_r16<true, FF_HREG, FF_WPE>), dim3(grid), dim3(NT), 0, st, hm1,
+            hipLaunchKernelGGL((k_fftfilt_r16<true>), dim3(grid), dim3(NT), 0, st, hm1,
                                (const float2 *)H, hc, (const void *)xc, (long long)nc, yc, scale_re, scale_im, tw);
         else
-            hipLaunchKernelGGL((k_fftfilt_r16<false, FF_HREG, FF_WPE>), dim3(grid), dim3(NT), 0, st, hm1,
+            hipLaunchKernelGGL((k_fftfilt_r16<false>), dim3(grid), dim3(NT), 0, st, hm1,
                                (const float2 *)H, hc, (const void *)xc, (long long)nc, yc, scale_re, scale_im, tw);
         LQ_CHECK_LAUNCH();
     }

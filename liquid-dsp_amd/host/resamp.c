@@ -468,7 +468,7 @@ static int rs_plan_device(lq_rs *q, int have)
              * (pre = 0) with Q >= 256 is exactly what the search walk recorded */
             const unsigned long long Q = pl->Q;
             unsigned long long m = 1;
-            while (m * Q < 256) m++;
+            while (Q > 0 && m * Q < 256) m++;
             pl->opre = rs_K_lin(q, pl->pre);
             pl->npre = (pl->opre + 3) / 4;
             pl->QT = m * Q;

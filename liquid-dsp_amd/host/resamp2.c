@@ -534,8 +534,9 @@ static void lq_ms_block_dev(lq_ms *q, const void *dx, unsigned long long nx, voi
             void *b2[2] = {NULL, NULL};
             for (unsigned int s = 1; s < q->ns; s++) {
                 const int last = s == q->ns - 1;
-                if (!last && !b2[s & 1])
-                    b2[s & 1] = lq_devbuf_get(&q->hb->buf[s & 1], (size_t)(k2 << s) * q->esz);
+                /* stage s writes k2 << s samples: grow the buffer for every
+                 * stage (the one of index s & 1 served stage s - 2 with half) */
+                if (!last) b2[s & 1] = lq_devbuf_get(&q->hb->buf[s & 1], (size_t)(k2 << s) * q->esz);
                 void *out = last ? dy : b2[s & 1];
                 lq_r2_run_dev(q->hb->st[q->ns - s - 1], LQK_R2_INTERP, in, k2 << (s - 1), out, NULL, 1.0f);
                 in = out;

@@ -19,7 +19,7 @@ import numpy as np
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(HERE)
-# LQ_LIB_PATH: an alternative build of the same library (tools/ab.sh A/B runs)
+# LQ_LIB_PATH: an alternative build of the same library (dev/ab/ab.sh A/B runs)
 LIB_PATH = os.environ.get("LQ_LIB_PATH") or os.path.join(HERE, "lib", "libliquid_mi355x.so")
 HEADER = os.path.join(ROOT, "include", "liquid_mi355x.h")
 

@@ -1262,6 +1262,34 @@ def test_msresamp_interp_chain_device_stream(rate, As):
         assert G.nrm_err(y, ref) < NRM
 
 
+@pytest.mark.parametrize("rate", [40.0, 70.0, 150.0])
+def test_msresamp_interp_chain_many_stages(rate):
+    # five to seven half-band stages after the fused resampler + first stage:
+    # the later stages ping-pong between two buffers that must grow with every
+    # stage (stage s writes 2^s times the fused kernel's output count;
+    # round-5 advisor finding on host/resamp2.c)
+    rate = float(np.float32(rate))
+    n = 1 << 15
+    r = rng(int(rate))
+    x = cx(r, n)
+    o = O.MsResamp(rate, 60.0)
+    ref = o.execute(x)
+    for t in (LQ.CRCF, LQ.CCCF):
+        g = LQ.MsResamp(rate, 60.0, t=t)
+        dx = LQ.DeviceBuffer.from_array(x)
+        ys = []
+        for a, b in ((0, 3), (3, 5000), (5000, n)):
+            nout = g.num_output(b - a)
+            dy = LQ.DeviceBuffer(max(1, nout) * 8)
+            ny = g.execute_block_dev(dx.p + 8 * a, b - a, dy.p)
+            g.synchronize()
+            assert ny == nout
+            ys.append(dy.to_array(np.complex64, ny))
+        y = np.concatenate(ys)
+        assert len(y) == len(ref)
+        assert G.nrm_err(y, ref) < NRM
+
+
 # ------------------------------------------------------------ FFT plan API
 FFTG = G.load("fft")
 R2RG = G.load("fft_r2r")
