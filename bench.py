@@ -92,6 +92,7 @@ def parse():
                    help="length of the ONE firpfbch2 stream split across ranks (sharded leg)")
     p.add_argument("--no-shard", action="store_true", help="skip the single-stream sharded leg")
     p.add_argument("--no-percall", action="store_true", help="skip the per-call latency leg")
+    p.add_argument("--no-ceilings", action="store_true", help="skip the measured HBM ceilings (probe kernels)")
     p.add_argument("--cpu-procs", type=int, default=0,
                    help="processes for the aggregate CPU baseline (0: the host CPU share, at most 16)")
     p.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic.json"),
@@ -661,7 +662,7 @@ def main():
         dp_t = {n: (allreduce_max(r["wall"], world), allreduce_max(r["gpu_ms"], world)) for n, r in dp["runs"].items()}
         ff_t = (allreduce_max(ff["wall"], world), allreduce_max(ff["gpu_ms"], world))
 
-    ceil = measured_ceilings(stream) if rank == 0 else None
+    ceil = measured_ceilings(stream) if rank == 0 and not args.no_ceilings else None
     percall = percall_gpu = None
     if rank == 0 and world == 1 and not args.no_percall:
         percall = percall_baseline()

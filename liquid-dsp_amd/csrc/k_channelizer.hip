@@ -32,6 +32,16 @@ namespace {
 
 constexpr int NT = 256;
 
+// Workgroup barrier for LDS hand-offs only: waits for this wave's LDS
+// operations, not its global loads and stores (__syncthreads() also drains
+// vmcnt: every store and prefetch in flight)
+__device__ __forceinline__ void lds_barrier_w()
+{
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+}
+
 __device__ __forceinline__ float2 ext_load(const float2 *__restrict__ hist, int HL, const float2 *__restrict__ x,
                                            long long t)
 {
@@ -476,31 +486,40 @@ bool launch_pfb2_an2048(const void *hsub, const void *hist, const void *x, long 
 // four tap sets A_q = taps(j_q), B_q = taps(j_q ^ 2048), q = 0, 1:
 //     lo q, row c:  block 2c   += A_q . column,  block 2c+1 += B_q . column
 //     hi q, row c:  block 2c+1 += A_q . column,  block 2c+2 += B_q . column
-// A 32 KB block leaves room for a 3-buffer LDS ring only, so a group is one
-// row: it completes blocks 2c and 2c+1, whose buffers hold the four
-// 1024-point quarters of bins j = r (mod 4).  Waves 0-7 inverse-transform one
-// quarter each in registers (fft1024_wave_rt), and after a barrier all 16
-// waves combine their block's quarters (radix 4):
+// A 32 KB block leaves room for two block buffers, so a group is one row: it
+// completes blocks 2c and 2c+1, whose buffers hold the four 1024-point
+// quarters of bins j = r (mod 4), and starts 2c+2, whose hi half waits in a
+// compact 16 KB carry buffer that each lane copies into the block-2c buffer
+// at the next row (its own positions, no barrier).  Waves 0-7
+// inverse-transform one quarter each in registers (fft1024_wave_rt), and
+// after a barrier all 16 waves combine their block's quarters (radix 4):
 //     Y[k + 1024 s] = sum_r W_4096^-(r k) Q_r[k] i^(r s)   (W^- : e^{+2 pi i ...})
-// times 1/M, stored as 16-byte rows.  The row ring is shifted in registers
-// (one row per loop iteration keeps the transform and combine code single).
-// m = 4: the next row's loads are issued after the transforms, so no
-// prefetch registers sit beside the ring and a transform (10 -> 2 spilled
-// VGPRs: 1.13 -> 1.11 ms per 2^27 samples; m <= 3 keep the early prefetch,
-// 0.995 vs 1.07 ms at m = 2)
+// times 1/M, stored as 16-byte rows.  The row ring is shifted in registers,
+// its oldest row kept in LDS (8 VGPRs fewer, which m = 4 needs to fit a
+// transform beside the ring in 128).
+//   Row c+1 reaches an LDS row buffer by LDS-DMA (global_load_lds_dwordx4,
+// no VGPRs) right after row c's dot phase and lands during the transforms
+// and the combine.  Round 5 loaded row c+1 into registers after row c's
+// transforms and crossed three __syncthreads per row (each draining vmcnt):
+// one row in flight per CU, 1.106 ms per 2^27 samples; this form 0.869 ms
+// (profiles/r06_ab_experiments.txt).  The barriers wait for LDS only.  LDS:
+// 2 x 34.9 (blocks) + 16 (carry) + 32 (oldest ring row) + 32 (row) KB.
 constexpr int A4_QS = 1092;            // quarter stride: 1088-float2 transform scratch; 1092 * 8 = 32 mod 128 B
 constexpr int A4_BSTR = 4 * A4_QS;     //   puts the four quarters of a dot-phase write on distinct bank groups
 template <int L>
 __global__ __launch_bounds__(1024, 1) void k_pfb2_an4096(const float *__restrict__ hsub,
-                                                         const float2 *__restrict__ hist,
-                                                         const float2 *__restrict__ x, int n_in, int p0, int nb,
-                                                         int cmin, int cmax, int S, float2 *__restrict__ Y,
-                                                         const float2 *__restrict__ tw4096)
+                                                          const float2 *__restrict__ hist,
+                                                          const float2 *__restrict__ x, int n_in, int p0, int nb,
+                                                          int cmin, int cmax, int S, float2 *__restrict__ Y,
+                                                          const float2 *__restrict__ tw4096)
 {
-    constexpr int M = 4096, M2 = 2048, HL = L * M - M2, NS = L, NBUF = 3;
-    __shared__ __attribute__((aligned(16))) float2 xr[NBUF * A4_BSTR];
+    constexpr int M = 4096, M2 = 2048, HL = L * M - M2, NS = L;
+    __shared__ __attribute__((aligned(16))) float2 xb[2 * A4_BSTR];   // blocks 2c, 2c+1
+    __shared__ __attribute__((aligned(16))) float2 hc[2048];          // hi half of block 2c+2
+    __shared__ __attribute__((aligned(16))) float2 wold[4 * 1024];    // each column's oldest ring row
+    __shared__ __attribute__((aligned(16))) float2 rb[4096];          // row c+1 (LDS-DMA)
     __shared__ __attribute__((aligned(16))) float2 tw2[64];
-    __shared__ __attribute__((aligned(16))) float2 wold[4 * 1024];   // each column's oldest ring row
+    typedef float v4f __attribute__((ext_vector_type(4)));
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     if (tid < 64) {   // W_64^{-b r} (inverse transform)
         const float2 u = tw4096[(64 * (tid & 3) * (tid >> 2)) & 4095];
@@ -508,38 +527,74 @@ __global__ __launch_bounds__(1024, 1) void k_pfb2_an4096(const float *__restrict
     }
     const float2 a1 = tw4096[(4 * lane) & 4095], a4 = tw4096[(16 * lane) & 4095];
     const int j0 = M2 - 1 - tid, j1 = M2 / 2 - 1 - tid;   // lo bins; hi bins j ^ M2
-    // split position of bin j in its block: quarter j & 3, index j >> 2
     auto qpos = [](int j) { return (j & 3) * A4_QS + (j >> 2); };
+    auto hpos = [](int j) { return (j & 3) * 512 + ((j >> 2) - 512); };   // hi bin j in hc
     const int pl0 = qpos(j0), pl1 = qpos(j1), ph0 = qpos(j0 ^ M2), ph1 = qpos(j1 ^ M2);
+    const int hc0 = hpos(j0 ^ M2), hc1 = hpos(j1 ^ M2);
     const __amdgpu_buffer_rsrc_t ry = __builtin_amdgcn_make_buffer_rsrc((void *)Y, (short)0, nb * M * 8, 0x00020000);
-    const float2 *zero = tw4096 + LQ_TW_N;   // lqrt_zeros(): the table's zero tail
+    const float2 *zero = tw4096 + LQ_TW_N;   // lqrt_zeros(): the table's zero tail (256 B)
     auto row_sample = [&](int r, int col) -> float2 {
         const int t = r * M + col - p0 * M2;
         return lq_load_hx(hist + HL, x, zero, t, HL, n_in);
     };
-    // Row ring of column q: the NS - 1 newest rows in registers, w[q][u] =
-    // row (newest - NS + 2 + u), and the oldest in LDS (wold[q][tid], private
-    // to the lane): 8 VGPRs fewer, which m = 4 needs to fit a transform
-    // beside the ring in 128
-    float2 w[4][NS - 1], pf[4], wo[4];
-    auto dot = [&](int q, const float *__restrict__ h) -> float2 {
+    // row r into rb: lane t's 16 bytes are samples 2 (t + 1024 u) and + 1
+    // (HL, n_in and the row starts are even: a pair never straddles the
+    // history / x / zero boundary); wave-uniform LDS base per instruction
+    auto dma_row = [&](int r) {
+        int to = tid;
+        asm volatile("" : "+v"(to));   // addresses recomputed per row (not hoisted into live VGPRs)
+#pragma unroll
+        for (int u = 0; u < 2; u++) {
+            const long long t = (long long)r * M + 2 * (to + 1024 * u) - (long long)p0 * M2;
+            const bool neg = t < 0;
+            const bool in = neg ? (t >= -HL) : (t < n_in);
+            unsigned long long a = (unsigned long long)(uintptr_t)(neg ? hist + HL : x) + (unsigned long long)(t * 8);
+            a = in ? a : (unsigned long long)(uintptr_t)zero;
+            __builtin_amdgcn_global_load_lds((const void *)a,
+                                             (__attribute__((address_space(3))) void *)(rb + 2 * (64 * wave + 1024 * u)),
+                                             16, 0, 0);
+        }
+    };
+    // rb[tid + 1024 q] through asm: a compiler-visible LDS read of rb would
+    // wait for every outstanding vector-memory operation (the DMA's counter
+    // is vmcnt) -- the explicit wait before the row's barrier covers it
+    auto rb_read = [&](int q) -> float2 {
+        const unsigned a = (unsigned)(uintptr_t)(rb + tid);
+        v2f v;
+        if (q == 0) asm volatile("ds_read_b64 %0, %1" : "=v"(v) : "v"(a));
+        if (q == 1) asm volatile("ds_read_b64 %0, %1 offset:8192" : "=v"(v) : "v"(a));
+        if (q == 2) asm volatile("ds_read_b64 %0, %1 offset:16384" : "=v"(v) : "v"(a));
+        if (q == 3) asm volatile("ds_read_b64 %0, %1 offset:24576" : "=v"(v) : "v"(a));
+        return make_float2(v.x, v.y);
+    };
+    float2 w[4][NS - 1], wo[4];
+    auto dot = [&](int q, const float (&h)[NS]) -> float2 {
         float2 acc = make_float2(0.f, 0.f);
 #pragma unroll
         for (int n = 0; n < NS; n++) {
-            const float hn = h[n];
             const float2 v = n < NS - 1 ? w[q][NS - 2 - n] : wo[q];
-            acc.x = fmaf(hn, v.x, acc.x);
-            acc.y = fmaf(hn, v.y, acc.y);
+            acc.x = fmaf(h[n], v.x, acc.x);
+            acc.y = fmaf(h[n], v.y, acc.y);
         }
         return acc;
     };
-    auto slot = [](int b) { return ((b % NBUF) + NBUF) % NBUF; };
+    // the lane's four tap sets (A0 = taps(j0), Bt0 = taps(j0 ^ M2), A1, Bt1),
+    // re-read (L1 / L2 hits) one set at a time in the dot phase: 8 VGPRs of
+    // taps live, not 32 (loaded before the previous row's stores instead, all
+    // four sets beside the ring spilled 16 VGPRs)
+    float th[NS];
+    auto load_set = [&](int j) {
+        int o = j * L;
+        asm volatile("" : "+v"(o));   // reloaded per row, not hoisted
+#pragma unroll
+        for (int n = 0; n < NS; n++) th[n] = hsub[o + n];
+    };
     const float inv = 1.0f / (float)M;
-    typedef float v4f __attribute__((ext_vector_type(4)));
 
     const int cs = cmin + (int)blockIdx.x * S;
     int ce = cs + S;
     if (ce > cmax + 1) ce = cmax + 1;
+    dma_row(cs);
     // rows cs-NS .. cs-1 fill the ring; the last gives the hi half of block 2cs
 #pragma unroll
     for (int q = 0; q < 4; q++) {
@@ -547,83 +602,74 @@ __global__ __launch_bounds__(1024, 1) void k_pfb2_an4096(const float *__restrict
 #pragma unroll
         for (int u = 0; u < NS - 1; u++) w[q][u] = row_sample(cs - NS + 1 + u, tid + 1024 * q);
     }
-    {
-        float2 *B = xr + slot(2 * cs) * A4_BSTR;
-        B[ph0] = dot(2, hsub + (j0 ^ M2) * L);
-        B[ph1] = dot(3, hsub + (j1 ^ M2) * L);
-    }
+    load_set(j0 ^ M2);
+    hc[hc0] = dot(2, th);
+    load_set(j1 ^ M2);
+    hc[hc1] = dot(3, th);
     if constexpr (NS > 1) {   // row cs - NS + 1: the oldest of row cs's dots
 #pragma unroll
         for (int q = 0; q < 4; q++) wold[q * 1024 + tid] = w[q][0];
     }
-#pragma unroll
-    for (int q = 0; q < 4; q++) pf[q] = row_sample(cs, tid + 1024 * q);
-    __syncthreads();   // tw2 ready
+    __builtin_amdgcn_s_waitcnt(0);
+    __syncthreads();   // tw2, row cs in rb
     const int qb = wave >> 2, qq = wave & 3;   // transform phase: block 2c + qb, quarter qq (waves 0-7)
     const int cb = wave >> 3, wb = wave & 7;   // combine phase: block 2c + cb, pairs lane + 64 wb
+    float2 *B0 = xb, *B1 = xb + A4_BSTR;
     for (int c = cs; c < ce; c++) {
+        float2 nr[4];
+#pragma unroll
+        for (int q = 0; q < 4; q++) nr[q] = rb_read(q);
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
 #pragma unroll
         for (int q = 0; q < 4; q++) {
-            // wold holds row c - NS + 1 (stored after the previous row's
-            // dots, below); w[q][0] died there, so the registers shift down
             wo[q] = wold[q * 1024 + tid];
             if constexpr (NS > 1) {
 #pragma unroll
                 for (int u = 0; u < NS - 2; u++) w[q][u] = w[q][u + 1];
-                w[q][NS - 2] = pf[q];
+                w[q][NS - 2] = nr[q];
             } else {
-                wo[q] = pf[q];
+                wo[q] = nr[q];
             }
-            if (!(L > 6)) pf[q] = row_sample(c + 1, tid + 1024 * q);
         }
-        {
-            float2 *B0 = xr + slot(2 * c) * A4_BSTR, *B1 = xr + slot(2 * c + 1) * A4_BSTR,
-                   *B2 = xr + slot(2 * c + 2) * A4_BSTR;
-            // taps re-read (L1 / L2 hits) every row instead of held across
-            // the transforms: the opaque offsets keep the loads in the loop
-            int o0 = j0 * L, o1 = j1 * L, o2 = (j0 ^ M2) * L, o3 = (j1 ^ M2) * L;
-            asm volatile("" : "+v"(o0), "+v"(o1), "+v"(o2), "+v"(o3));
-            const float *A0 = hsub + o0, *A1 = hsub + o1, *Bt0 = hsub + o2, *Bt1 = hsub + o3;
-            // one tap set at a time (8 VGPRs of taps live, not 32)
-            B0[pl0] = dot(0, A0);
-            B1[ph0] = dot(2, A0);
-            asm volatile("" ::: "memory");
-            B1[pl0] = dot(0, Bt0);
-            B2[ph0] = dot(2, Bt0);
-            asm volatile("" ::: "memory");
-            B0[pl1] = dot(1, A1);
-            B1[ph1] = dot(3, A1);
-            asm volatile("" ::: "memory");
-            B1[pl1] = dot(1, Bt1);
-            B2[ph1] = dot(3, Bt1);
-            // the next row's oldest (row c - NS + 2) waits in LDS, not in
-            // registers, across the transforms
-            if constexpr (NS > 1) {
+        // block 2c's hi half, carried from row c - 1 (this lane's positions)
+        B0[ph0] = hc[hc0];
+        B0[ph1] = hc[hc1];
+        load_set(j0);
+        B0[pl0] = dot(0, th);
+        B1[ph0] = dot(2, th);
+        asm volatile("" ::: "memory");
+        load_set(j0 ^ M2);
+        B1[pl0] = dot(0, th);
+        hc[hc0] = dot(2, th);
+        asm volatile("" ::: "memory");
+        load_set(j1);
+        B0[pl1] = dot(1, th);
+        B1[ph1] = dot(3, th);
+        asm volatile("" ::: "memory");
+        load_set(j1 ^ M2);
+        B1[pl1] = dot(1, th);
+        hc[hc1] = dot(3, th);
+        if constexpr (NS > 1) {
 #pragma unroll
-                for (int q = 0; q < 4; q++) wold[q * 1024 + tid] = w[q][0];
-            }
+            for (int q = 0; q < 4; q++) wold[q * 1024 + tid] = w[q][0];
         }
-        __syncthreads();
+        lds_barrier_w();   // blocks complete, rb consumed by every wave
+        if (c + 1 < ce) dma_row(c + 1);
         if (wave < 8) {
-            float2 *Bq = xr + slot(2 * c + qb) * A4_BSTR + qq * A4_QS;
+            float2 *Bq = (qb ? B1 : B0) + qq * A4_QS;
             float2 v[16];
 #pragma unroll
             for (int n = 0; n < 16; n++) v[n] = Bq[lane + 64 * n];
             fft1024_wave_rt<-1>(v, Bq, a1, a4, tw2, lane);   // natural order at k + 4 (k >> 8)
         }
-        __syncthreads();   // every quarter of both blocks transformed
-        if ((L > 6)) {   // the next row's loads, issued after the transforms (no prefetch registers across them)
-#pragma unroll
-            for (int q = 0; q < 4; q++) pf[q] = row_sample(c + 1, tid + 1024 * q);
-        }
+        lds_barrier_w();   // every quarter of both blocks transformed
         {
             const int b = 2 * c + cb;
-            const float2 *Bb = xr + slot(b) * A4_BSTR;
+            const float2 *Bb = cb ? B1 : B0;
             const int gb = b - p0;
             const bool keep = gb >= 0 && gb < nb && b < 2 * ce;
-            // a dropped block's base: 2^31 (the launch's range is below it)
             const unsigned base = keep ? (unsigned)gb * (unsigned)(M * 8) : 0x80000000u;
-            const int k = 2 * (lane + 64 * wb);   // bins k, k + 1 of each quarter
+            const int k = 2 * (lane + 64 * wb);
             const int pos = k + 4 * (k >> 8);
             v2f T[4][2];
 #pragma unroll
@@ -636,7 +682,7 @@ __global__ __launch_bounds__(1024, 1) void k_pfb2_an4096(const float *__restrict
             for (int e = 0; e < 2; e++)
 #pragma unroll
                 for (int r = 1; r < 4; r++) {
-                    const float2 u = tw4096[r * (k + e)];   // W_4096^(r k), r k < 4096 (L1 / L2 hits)
+                    const float2 u = tw4096[r * (k + e)];
                     T[r][e] = pk_cmul(T[r][e], v2f{u.x, -u.y});
                 }
             v2f Yo[4][2];
@@ -644,7 +690,7 @@ __global__ __launch_bounds__(1024, 1) void k_pfb2_an4096(const float *__restrict
             for (int e = 0; e < 2; e++) {
                 const v2f s02 = T[0][e] + T[2][e], d02 = T[0][e] - T[2][e];
                 const v2f s13 = T[1][e] + T[3][e], d13 = T[1][e] - T[3][e];
-                const v2f jd13 = v2f{-d13.y, d13.x};   // i (T1 - T3)
+                const v2f jd13 = v2f{-d13.y, d13.x};
                 Yo[0][e] = (s02 + s13) * inv;
                 Yo[1][e] = (d02 + jd13) * inv;
                 Yo[2][e] = (s02 - s13) * inv;
@@ -655,7 +701,9 @@ __global__ __launch_bounds__(1024, 1) void k_pfb2_an4096(const float *__restrict
                 __builtin_amdgcn_raw_buffer_store_b128(v4f{Yo[sq][0].x, Yo[sq][0].y, Yo[sq][1].x, Yo[sq][1].y}, ry,
                                                        base + (unsigned)(k + 1024 * sq) * 8u, 0, 2);
         }
-        __syncthreads();   // the combine's reads are done before the next row's writes
+        // the DMA has landed; only the four stores may be in flight
+        asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+        lds_barrier_w();   // combine reads done; row c+1 in rb for every wave
     }
 }
 

@@ -134,7 +134,7 @@ __global__ __launch_bounds__(NT4, (HM ? 4 : rs4_blk<L, UP, DN>())) void k_resamp
                                                       const float2 *__restrict__ taps2,
                                                       const float2 *__restrict__ hist,
                                                       const float2 *__restrict__ x, int n,
-                                                      float2 *__restrict__ y, int nout, bool al16, lqk_rs4_hb hb)
+                                                      float2 *__restrict__ y, int nout, int smode, lqk_rs4_hb hb)
 {
     // HM > 0: the half-band interpolator stage (semi-length HM, 2 HM taps on
     // the odd branch) fused behind the resampler.  A tile then computes its
@@ -477,7 +477,7 @@ __global__ __launch_bounds__(NT4, (HM ? 4 : rs4_blk<L, UP, DN>())) void k_resamp
                 asm volatile("" : "+v"(a));   // the pass completes here (no hoisted reads)
                 const int t = lane + 64 * s, k = tile * TS + t - HALO;
                 if (t >= HALO && k < nout) {
-                    if (al16) {
+                    if (smode) {
                         u32x4 v;
                         v.x = __float_as_uint(d.x);
                         v.y = __float_as_uint(d.y);
@@ -507,7 +507,23 @@ __global__ __launch_bounds__(NT4, (HM ? 4 : rs4_blk<L, UP, DN>())) void k_resamp
             s23.y = __float_as_uint(acc[2].y);
             s23.z = __float_as_uint(acc[3].x);
             s23.w = __float_as_uint(acc[3].y);
-            if (ko + 4 <= nout && al16) {
+            if (smode == 2 && tile * TOUT + TOUT <= nout) {
+                // whole 128-byte lines per store instruction: lanes j and j ^ 4
+                // (quads A, B of an 8-lane group; outputs 32 g .. 32 g + 31)
+                // swap one 16-byte half, so the first store writes quad A's
+                // line (A: its outputs 0-1, B: A's outputs 2-3) and the second
+                // quad B's line
+                const int b2 = (lane >> 2) & 1;
+                const u32x4 snd = b2 ? s01 : s23;
+                u32x4 rcv;
+                rcv.x = (unsigned)__builtin_amdgcn_ds_swizzle((int)snd.x, 0x101F);   // lane ^ 4
+                rcv.y = (unsigned)__builtin_amdgcn_ds_swizzle((int)snd.y, 0x101F);
+                rcv.z = (unsigned)__builtin_amdgcn_ds_swizzle((int)snd.z, 0x101F);
+                rcv.w = (unsigned)__builtin_amdgcn_ds_swizzle((int)snd.w, 0x101F);
+                const unsigned o1 = (unsigned)(tile * TOUT + 32 * (lane >> 3) + 4 * (lane & 3) + 2 * b2) * 8u;
+                __builtin_amdgcn_raw_buffer_store_b128(b2 ? rcv : s01, ry, o1, 0, 2);
+                __builtin_amdgcn_raw_buffer_store_b128(b2 ? s23 : rcv, ry, o1 + 128u, 0, 2);
+            } else if (ko + 4 <= nout && smode) {
                 __builtin_amdgcn_raw_buffer_store_b128(s01, ry, (unsigned)ko * 8u, 0, 2);
                 __builtin_amdgcn_raw_buffer_store_b128(s23, ry, (unsigned)ko * 8u + 16u, 0, 2);
             } else if (ko < nout) {   // the call's ragged end (one lane of one wave), or y not 16-byte aligned
@@ -542,7 +558,8 @@ void launch_rs4_c(const lqk_rs4_plan &pl, unsigned long long g0, unsigned long l
                   const float2 *taps2, const float2 *hist, const float2 *x, int n, float2 *y, int nout,
                   const lqk_rs4_hb &hb, hipStream_t st)
 {
-    const bool al16 = ((unsigned long long)y & 15) == 0;   // 16-byte output stores
+    static const int dev_sm = getenv("LQ_DEV_RS4ST") ? atoi(getenv("LQ_DEV_RS4ST")) : 1;   // DEV A/B
+    const int smode = ((unsigned long long)y & 15) ? 0 : dev_sm;   // 16-byte output stores
     const int RS = npfb + 1;
     const size_t lds =
         (size_t)((rs4_rows<L, UP, DN>() * RS * 8 + 15) & ~15) + (size_t)(NT4 / 64) * 4 * rs4_n4<UP, DN>() * 8;
@@ -554,10 +571,10 @@ void launch_rs4_c(const lqk_rs4_plan &pl, unsigned long long g0, unsigned long l
     const int nb = wgs < 256 * blk ? wgs : 256 * blk;   // persistent: blk per CU
     if (npfb == 64)
         hipLaunchKernelGGL((k_resamp4<L, 64, UP, HM, R4, DN>), dim3(nb), dim3(NT4), lds, st, pl, g0, K0, npfb, del,
-                           taps2, hist, x, n, y, nout, al16, hb);
+                           taps2, hist, x, n, y, nout, smode, hb);
     else if constexpr (HM == 0)
         hipLaunchKernelGGL((k_resamp4<L, 0, UP, 0, R4, DN>), dim3(nb), dim3(NT4), lds, st, pl, g0, K0, npfb, del,
-                           taps2, hist, x, n, y, nout, al16, hb);
+                           taps2, hist, x, n, y, nout, smode, hb);
 }
 
 template <int L>

@@ -152,13 +152,22 @@ void lqk_firpfbch_synthesizer(int ctaps, unsigned int M, unsigned int p, const v
 /* batched complex FFT of power-of-two size n (2..4096): dir +1 forward, -1 backward */
 void lqk_fft_batch(unsigned int n, int dir, const void *x, void *y, unsigned long long batch,
                    void *stream);
-/* overlap-save fast convolution (fixed 4096-point transform, hlen <= 2049):
- * y[t] = scale * sum_k h[k] ext[t-k], t < n; H = FFT_4096(h zero padded) (unscaled);
- * scale = user scale / 4096; hist = previous hlen-1 inputs.  x must not alias y. */
-void lqk_fftfilt_run(int real_io, unsigned int hlen, const void *H, const void *hist, const void *x,
-                     unsigned long long n, void *y, float scale_re, float scale_im, void *stream);
-void lqk_fftfilt_make_H(const void *h_dev, unsigned int hlen, int is_complex, void *H, void *stream);
-unsigned int lqk_fftfilt_nfft(void);
+/* overlap-save fast convolution: y[t] = scale * sum_k h[k] ext[t-k], t < n;
+ * nfft = lqk_fftfilt_nfft(real_io, hlen) (4096-point segments up to 2049
+ * taps, 8192 for complex I/O up to 4097 taps, 0: too long);
+ * H = FFT_nfft(h zero padded) (unscaled, lqk_fftfilt_make_H); scale = the
+ * user scale; hist = previous hlen-1 inputs.  x must not alias y.
+ * guard (complex I/O only): 0 fftfilt; 1 / 2 firfilt crcf / cccf --
+ * segments whose inputs hold Inf / NaN, |v| > 2^100 or nonzero |v| < 2^-60
+ * are recomputed as the direct convolution over hx (the natural-order taps,
+ * hlen); flags: device scratch of lqk_fftfilt_flag_bytes(). */
+unsigned int lqk_fftfilt_nfft(int real_io, unsigned int hlen);
+size_t lqk_fftfilt_flag_bytes(unsigned int hlen, unsigned int nfft, unsigned long long n);
+void lqk_fftfilt_run(int real_io, unsigned int hlen, unsigned int nfft, const void *H, const void *hist,
+                     const void *x, unsigned long long n, void *y, float scale_re, float scale_im,
+                     const float *hx, int guard, void *flags, void *stream);
+void lqk_fftfilt_make_H(const void *h_dev, unsigned int hlen, int is_complex, unsigned int nfft, void *H,
+                        void *stream);
 
 /* ---------------------------------------------------------------- resamp / firpfb
  * Timing plan: checkpoint c = the resampler's timing state before plan input

@@ -7,16 +7,17 @@
  * convolution, zero initial state); set_scale(s) (:182-187).
  *
  * The reference evaluates this with a 2n-point overlap-add per call; the
- * kernel (csrc/k_fftfilt.hip) uses fixed 4096-point overlap-save segments,
- * which gives the same convolution for any n and lets a long stream
- * (execute_block extension) run all segments in parallel.  rrrf runs the
- * real-I/O form of the kernel; crcf and cccf share the complex form (H is
- * the transform of real or complex taps).
+ * kernels (csrc/k_fftfilt.hip) use fixed overlap-save segments, which give
+ * the same convolution for any n and let a long stream (execute_block
+ * extension) run all segments in parallel: 4096-point segments up to 2049
+ * taps (rrrf in the real-I/O form of the kernel; crcf and cccf share the
+ * complex form, H the transform of real or complex taps), crcf / cccf
+ * 8192-point segments up to 4097 taps.
  *
- * Filters longer than the transform allows (h_len - 1 > 2048, which the
- * reference accepts for any n >= h_len - 1) run the same convolution as a
- * direct FIR (the firfilt engine, csrc/k_firfilt.hip) on the object's
- * stream: y = s * (h * x) either way, to float32 rounding.
+ * Filters longer than the transforms allow (h_len - 1 > 4096 complex, > 2048
+ * rrrf, which the reference accepts for any n >= h_len - 1) run the same
+ * convolution as a direct FIR (the firfilt engine, csrc/k_firfilt.hip) on the
+ * object's stream: y = s * (h * x) either way, to float32 rounding.
  */
 #include <complex.h>
 
@@ -28,6 +29,7 @@ typedef struct {
     int kind;
     size_t esz, csz;
     unsigned int h_len, n;
+    unsigned int nfft;  /* segment transform size (lqk_fftfilt_nfft); 0: direct */
     float *h;
     void *d_h, *d_H;
     void *d_hist[2];    /* previous h_len-1 inputs */
@@ -56,17 +58,18 @@ static lq_fftf *lq_fftf_create(int kind, const float *h, unsigned int h_len, uns
     memcpy(q->h, h, h_len * q->csz);
     lq_ctx_init(&q->ctx);
     q->d_h = lqrt_malloc(h_len * q->csz);
-    q->d_H = lqrt_malloc((size_t)lqk_fftfilt_nfft() * 8);
+    q->nfft = lqk_fftfilt_nfft(kind == LQ_RRRF, h_len);
+    q->d_H = lqrt_malloc((size_t)(q->nfft ? q->nfft : 1) * 8);
     q->d_hist[0] = lqrt_malloc((size_t)h_len * q->esz);
     q->d_hist[1] = lqrt_malloc((size_t)h_len * q->esz);
     lq_mirror_init(&q->hm, h_len - 1, q->esz);
     lqrt_h2d(q->d_h, q->h, h_len * q->csz, q->ctx.stream);
-    if (h_len - 1 > lqk_fftfilt_nfft() / 2) {
+    if (q->nfft == 0) {
         static const char *who[] = {"fftfilt_rrrf", "fftfilt_crcf", "fftfilt_cccf"};
         q->direct = lq_firfilt_create(kind, h, h_len, who[kind]);
         lq_ctx_set_stream(lq_firfilt_ctx(q->direct), q->ctx.stream);
     } else {
-        lqk_fftfilt_make_H(q->d_h, h_len, kind == LQ_CCCF, q->d_H, q->ctx.stream);
+        lqk_fftfilt_make_H(q->d_h, h_len, kind == LQ_CCCF, q->nfft, q->d_H, q->ctx.stream);
     }
     lqrt_sync(q->ctx.stream);
     q->sre = 1.0f;
@@ -130,8 +133,8 @@ static void lq_fftf_block_dev(lq_fftf *q, const void *dx, unsigned long long n, 
     }
     const unsigned int hm1 = q->h_len - 1;
     void *hold = q->d_hist[q->cur], *hnew = q->d_hist[q->cur ^ 1];
-    const float nf = (float)lqk_fftfilt_nfft();
-    lqk_fftfilt_run(q->kind == LQ_RRRF, q->h_len, q->d_H, hold, x, n, dy, q->sre / nf, q->sim / nf, q->ctx.stream);
+    lqk_fftfilt_run(q->kind == LQ_RRRF, q->h_len, q->nfft, q->d_H, hold, x, n, dy, q->sre, q->sim, NULL, 0, NULL,
+                    q->ctx.stream);
     if (hm1) {
         lqk_window_append(q->kind != LQ_RRRF, hold, hm1, x, n, hnew, q->ctx.stream);
         q->cur ^= 1;

@@ -27,13 +27,18 @@ struct lq_firfilt_s {
     void *d_hpad;      /* device, zero padded to HP */
     lqk_fir_desc d;
     void *d_win[2];    /* device windows, HP samples each */
+    void *d_H8;        /* long complex filters: the overlap-save path's spectrum (else NULL) */
+    unsigned int fft_n; /* its transform size (lqk_fftfilt_nfft) */
     int cur;
     unsigned char *h_win; /* host mirror */
     int host_valid, dev_valid;
     lq_ctx ctx;
-    lq_devbuf xbuf, ybuf, scratch, one;
+    lq_devbuf xbuf, ybuf, scratch, one, flags;
     const char *who;   /* the public object name, for error messages */
 };
+
+#define LQ_FIR_FFT_MIN_TAPS 64u     /* longer complex filters take the overlap-save path ... */
+#define LQ_FIR_FFT_MIN_N 8192ull    /* ... on device blocks of at least this many samples */
 
 static void lq_firfilt_layout(lq_firfilt *q, unsigned int n)
 {
@@ -61,6 +66,7 @@ static void lq_firfilt_layout(lq_firfilt *q, unsigned int n)
 static void lq_firfilt_alloc_state(lq_firfilt *q)
 {
     q->d_hpad = lqrt_malloc((size_t)q->HP * q->csz);
+    q->d_H8 = NULL;
     q->d_win[0] = lqrt_malloc((size_t)q->HP * q->esz);
     q->d_win[1] = lqrt_malloc((size_t)q->HP * q->esz);
     /* pinned: the per-sample execute() reads it in place (zero copy) */
@@ -72,6 +78,8 @@ static void lq_firfilt_alloc_state(lq_firfilt *q)
 
 static void lq_firfilt_free_state(lq_firfilt *q)
 {
+    if (q->d_H8) lqrt_free(q->d_H8);
+    q->d_H8 = NULL;
     lqrt_free(q->d_hpad);
     lqrt_free(q->d_win[0]);
     lqrt_free(q->d_win[1]);
@@ -96,6 +104,22 @@ static void lq_firfilt_upload_coefs(lq_firfilt *q)
     for (unsigned int i = 0; i < nv; i++) {
         const float a = fabsf(q->h[i]);
         if (!(a <= 0x1p50f) || (a != 0.0f && a < 0x1p-50f)) q->d.mx_ok = 0;
+    }
+    const int fft_ok = q->d.mx_ok;   /* the same tap class for the transform path */
+    /* complex streams through long filters (crcf / cccf, more than
+     * LQ_FIR_FFT_MIN_TAPS taps): the same convolution by 4096-point (8192
+     * past 2049 taps) overlap-save segments (csrc/k_fftfilt.hip, the guarded
+     * form: segments
+     * with non-finite, huge or tiny inputs fall back to the direct sum) -- HBM-bound
+     * where the direct kernels are bound by their arithmetic (crcf h = 256:
+     * six bf16 matrix products per tap; cccf past 64 taps: the VALU kernel) */
+    if (q->d_H8) lqrt_free(q->d_H8);
+    q->d_H8 = NULL;
+    q->fft_n = lqk_fftfilt_nfft(0, q->hlen);
+    if (q->kind != LQ_RRRF && q->hlen > LQ_FIR_FFT_MIN_TAPS && fft_ok && q->fft_n) {
+        q->d_H8 = lqrt_malloc((size_t)q->fft_n * 8);
+        lqk_fftfilt_make_H(q->d_hpad, q->hlen, q->kind == LQ_CCCF, q->fft_n, q->d_H8, q->ctx.stream);
+        lqrt_sync(q->ctx.stream);
     }
 }
 
@@ -146,6 +170,7 @@ void lq_firfilt_destroy(lq_firfilt *q)
     lq_devbuf_free(&q->ybuf);
     lq_devbuf_free(&q->scratch);
     lq_devbuf_free(&q->one);
+    lq_devbuf_free(&q->flags);
     lq_ctx_free(&q->ctx);
     free(q->h);
     free(q);
@@ -243,6 +268,22 @@ void lq_firfilt_execute_block_dev(lq_firfilt *q, const void *dx, unsigned long l
     void *wold = q->d_win[q->cur];
     void *wnew = q->d_win[q->cur ^ 1];
     lqk_window_append(q->kind != LQ_RRRF, wold, q->HP, dx, n, wnew, q->ctx.stream);
+    if (q->d_H8 && n >= LQ_FIR_FFT_MIN_N) {
+        const void *x = dx;
+        if (dx == dy) {   /* segments read overlapping halos: filter a copy */
+            void *c = lq_devbuf_get(&q->scratch, (size_t)n * q->esz);
+            lqrt_d2d(c, dx, (size_t)n * q->esz, q->ctx.stream);
+            x = c;
+        }
+        /* the history: the window's last hlen - 1 samples */
+        const void *hist = (const char *)wold + (size_t)(q->HP - (q->hlen - 1)) * q->esz;
+        void *fl = lq_devbuf_get(&q->flags, lqk_fftfilt_flag_bytes(q->hlen, q->fft_n, n));
+        lqk_fftfilt_run(0, q->hlen, q->fft_n, q->d_H8, hist, x, n, dy, q->d.scale_re, q->d.scale_im,
+                        (const float *)q->d_hpad, q->kind == LQ_CCCF ? 2 : 1, fl, q->ctx.stream);
+        q->cur ^= 1;
+        q->host_valid = 0;
+        return;
+    }
     void *scr = NULL;
     if (dx == dy) scr = lq_devbuf_get(&q->scratch, lqk_firfilt_scratch_bytes(&q->d, n));
     lqk_firfilt(&q->d, wold, dx, n, dy, scr, q->ctx.stream);

@@ -185,16 +185,20 @@ def test_firfilt_crcf_matrix_core_path_long_stream(t, hlen):
     # three-term bf16 split is float32-accurate, not bf16-accurate).
     r = rng(100 + hlen)
     h = coefs(r, t, hlen)
-    n1, n2 = (3 << 20) + 12345, 777
-    x = samples(r, t, n1 + n2)
+    # complex filters past 64 taps on blocks of >= 8192 samples take the
+    # 8192-point overlap-save path (k_fftfilt8k, guarded form); the 6000-sample
+    # first call keeps the matrix-core kernels of 65..256 taps covered
+    n0, n1, n2 = 6000, (3 << 20) + 12345, 777
+    x = samples(r, t, n0 + n1 + n2)
     esz = x.itemsize
     g = LQ.FirFilt(t, h)
     s = (0.7 - 0.2j) if t == "cccf" else 0.7
     g.set_scale(s)
     bx = LQ.DeviceBuffer.from_array(x)
     by = LQ.DeviceBuffer(x.nbytes)
-    g.execute_block_dev(bx.p, n1, by.p)
-    g.execute_block_dev(bx.p + n1 * esz, n2, by.p + n1 * esz)   # second call 4- or 8-byte aligned: VALU kernel
+    g.execute_block_dev(bx.p, n0, by.p)
+    g.execute_block_dev(bx.p + n0 * esz, n1, by.p + n0 * esz)
+    g.execute_block_dev(bx.p + (n0 + n1) * esz, n2, by.p + (n0 + n1) * esz)   # 4- or 8-byte aligned: VALU kernel
     g.synchronize()
     y = by.to_array(x.dtype, len(x))
     o = O.FirFilt(TYPES[t], h)
@@ -303,7 +307,8 @@ def test_firinterp_vs_oracle(M, m, t):
 
 
 @pytest.mark.parametrize("t", ["rrrf", "crcf", "cccf"])
-@pytest.mark.parametrize("hlen,n", [(4, 4), (23, 32), (512, 2048), (2049, 2048)])
+@pytest.mark.parametrize("hlen,n", [(4, 4), (23, 32), (512, 2048), (2049, 2048), (2050, 2100), (4097, 4096),
+                                    (4098, 4097)])
 def test_fftfilt_vs_oracle(hlen, n, t):
     r = rng(hlen)
     h = coefs(r, t, hlen)
@@ -1490,6 +1495,41 @@ def test_channelizer_launch_chunk_boundary(which):
     y2 = np.concatenate([q.execute_block(x[: cut * per]), q.execute_block(x[cut * per:])])
     assert y1.shape == y2.shape
     assert np.array_equal(y1, y2)
+
+
+@pytest.mark.parametrize("t", ["crcf", "cccf"])
+@pytest.mark.parametrize("hlen", [1, 2, 64, 512, 2049, 2050, 3001, 4097])
+@pytest.mark.parametrize("off", [0, 8])
+def test_fftfilt_segments_device_stream(t, hlen, off):
+    # complex I/O: 4096-point segments up to 2049 taps, 8192-point segments
+    # (k_fftfilt8k) up to 4097: 16-byte pair loads / stores when x and y are
+    # 16-byte aligned (off = 0), 8-byte ones otherwise; odd stream lengths (a
+    # pair straddling the end in the last segment), ragged calls, the first
+    # segment's history
+    r = rng(hlen * 3 + off)
+    h = coefs(r, t, hlen)
+    n = 300_001
+    x = cx(r, n)
+    o = O.FftFilt(TYPES[t], h, max(hlen - 1, 1))
+    ref = o.execute_stream(x)
+    g = LQ.FftFilt(h, max(hlen - 1, 1), t=t)
+    dx = LQ.DeviceBuffer(8 * n + 16)
+    LQ.lib().liquid_mi355x_memcpy_h2d(dx.p + off, LQ.ptr(x), x.nbytes)
+    dy = LQ.DeviceBuffer(8 * n + 16)
+    for a, b in ((0, 7), (7, 70_001), (70_001, 70_002), (70_002, n)):
+        g.execute_block_dev(dx.p + off + 8 * a, b - a, dy.p + off + 8 * a)
+    LQ.lib().liquid_mi355x_device_synchronize()
+    yb = np.empty(n + 2, np.complex64)
+    LQ.lib().liquid_mi355x_memcpy_d2h(LQ.ptr(yb), dy.p, yb.nbytes)
+    y = yb.view(np.uint8)[off:off + 8 * n].view(np.complex64)
+    assert len(ref) > n - 4097
+    assert G.nrm_err(y[:len(ref)], ref) < NRM
+    # in place: the block call copies the input first (segments read overlapping halos)
+    g2 = LQ.FftFilt(h, max(hlen - 1, 1), t=t)
+    g2.execute_block_dev(dx.p + off, n, dx.p + off)
+    LQ.lib().liquid_mi355x_device_synchronize()
+    LQ.lib().liquid_mi355x_memcpy_d2h(LQ.ptr(yb), dx.p, yb.nbytes)
+    assert G.nrm_err(yb.view(np.uint8)[off:off + 8 * n].view(np.complex64)[:len(ref)], ref) < NRM
 
 
 def test_fftfilt_launch_chunk_boundary():

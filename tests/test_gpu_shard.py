@@ -72,13 +72,15 @@ def test_firfilt_sharded_objects_bit_exact():
 def _bench(gpus):
     cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", str(gpus), "--steps", "2", "--warmup", "1",
            "--samples", str(1 << 20), "--shard-samples", str(1 << 21), "--no-firfilt", "--no-resamp",
-           "--no-extra", "--no-cpu-baseline", "--no-percall"]
+           "--no-extra", "--no-cpu-baseline", "--no-percall", "--no-ceilings"]
     env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
     out = subprocess.run(cmd, capture_output=True, text=True, timeout=300, env=env)
     assert out.returncode == 0, out.stderr[-2000:]
-    lines = [ln for ln in out.stdout.splitlines() if ln.startswith("{")]
-    assert len(lines) == 1, out.stdout
-    return json.loads(lines[0])
+    # the headline record is the last JSON line (an "aux" line precedes it)
+    lines = [json.loads(ln) for ln in out.stdout.splitlines() if ln.startswith("{")]
+    head = [d for d in lines if "metric" in d]
+    assert len(head) == 1 and lines[-1] is head[0], out.stdout
+    return head[0]
 
 
 def test_bench_spawns_ranks_and_sharded_checksum_is_invariant():
