@@ -87,6 +87,24 @@ def main():
             nout[0] = q.execute_block_dev(x.data_ptr(), n, y.data_ptr())
         ms = timed(step)
         nb = 8.0 * n + 8.0 * nout[0]
+    elif what == "fft":
+        N = int(arg)
+        B = (1 << 26) // N
+        Z = cbuf(B * N)
+        L = LQ.lib()
+        pl = L.fft_create_plan(N, None, None, 1, 0)
+        L.fft_set_stream(pl, ST.cuda_stream)
+        ms = timed(lambda: L.fft_execute_batch_dev(pl, Z.data_ptr(), Z.data_ptr(), B))
+        nb = 16.0 * B * N
+    elif what == "pfbsyn":   # firpfbch2 synthesizer M, m=4, 2^26 outputs
+        M = int(arg)
+        nout = 1 << 26
+        nblk = nout // (M // 2)
+        X, y = cbuf(nblk * M), torch.empty(2 * nout, device="cuda")
+        q = LQ.FirPfbch2(LQ.LIQUID_SYNTHESIZER, M, 4, 60.0)
+        q.set_stream(ST.cuda_stream)
+        ms = timed(lambda: q.execute_block_dev(X.data_ptr(), nblk, y.data_ptr()))
+        nb = 8.0 * nblk * M + 8.0 * nout
     else:
         sys.exit("unknown workload " + what)
     best = min(ms)

@@ -23,6 +23,17 @@ __device__ __forceinline__ void lq_signal(unsigned *flag, unsigned seq)
     __hip_atomic_store(flag, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
+// Workgroup barrier for LDS hand-offs: waits for this wave's LDS operations
+// only.  __syncthreads() also waits for every global load and store in
+// flight (vmcnt(0)), so a transform between a segment's stores and the next
+// segment's would hold the stores up at its first barrier.
+__device__ __forceinline__ void lq_lds_sync()
+{
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+}
+
 __device__ __forceinline__ float2 cadd(float2 a, float2 b) { return make_float2(a.x + b.x, a.y + b.y); }
 __device__ __forceinline__ float2 csub(float2 a, float2 b) { return make_float2(a.x - b.x, a.y - b.y); }
 __device__ __forceinline__ float2 cmul(float2 a, float2 b)
@@ -381,19 +392,19 @@ __device__ __forceinline__ void fft_r16x16xR(float2 (&v)[16], float2 *lds, const
     constexpr int S1 = fftr16_s1<R>(), S2 = fftr16_s2<R, TIGHT>();
     dft16<DIR>(v);
     twiddle16v<DIR>(v, w.p1a, w.p1b);   // W_N^{t k2}
-    __syncthreads();
+    lq_lds_sync();
 #pragma unroll
     for (int k = 0; k < 16; k++) lds[k * S1 + t] = v[k];
-    __syncthreads();
+    lq_lds_sync();
     const int k2 = t & 15, a = t >> 4;
 #pragma unroll
     for (int b = 0; b < 16; b++) v[b] = lds[k2 * S1 + a + R * b];
     dft16<DIR>(v);
     if constexpr (R > 1) twiddle16v<DIR>(v, w.p2a, w.p2b);   // W_T^{a q1}
-    __syncthreads();
+    lq_lds_sync();
 #pragma unroll
     for (int q1 = 0; q1 < 16; q1++) lds[(k2 + 16 * q1) * S2 + a] = v[q1];
-    __syncthreads();
+    lq_lds_sync();
     // unit k2 + 16 q1 with q1 = (t >> 4) + R s is t + T s
 #pragma unroll
     for (int s = 0; s < 16 / R; s++)
@@ -416,10 +427,10 @@ __device__ __forceinline__ void fft_small16xR(float2 (&v)[16], float2 *lds, floa
     constexpr int S = R + 1;
     dft16<DIR>(v);
     twiddle16v<DIR>(v, a1, a4);   // W_N^{t k2}
-    __syncthreads();
+    lq_lds_sync();
 #pragma unroll
     for (int k = 0; k < 16; k++) lds[k * S + t] = v[k];
-    __syncthreads();
+    lq_lds_sync();
     constexpr int U = 16 / R;
 #pragma unroll
     for (int u = 0; u < U; u++)
@@ -446,19 +457,19 @@ __device__ __forceinline__ void fft4096_r16(float2 (&v)[16], float2 *lds, const 
 {
     dft16<DIR>(v);
     twiddle16v<DIR>(v, w.p1a, w.p1b);   // W_4096^{t k}
-    __syncthreads();
+    lq_lds_sync();
 #pragma unroll
     for (int k = 0; k < 16; k++) lds[k * 272 + t] = v[k];   // row pad 16: conflict-free reads below
-    __syncthreads();
+    lq_lds_sync();
     const int m0 = t & 15, k2 = t >> 4;
 #pragma unroll
     for (int m = 0; m < 16; m++) v[m] = lds[k2 * 272 + m0 + 16 * m];
     dft16<DIR>(v);
     twiddle16v<DIR>(v, w.p2a, w.p2b);   // W_256^{m0 j} = W_4096^{16 m0 j}
-    __syncthreads();
+    lq_lds_sync();
 #pragma unroll
     for (int j = 0; j < 16; j++) lds[(k2 + 16 * j) * 17 + m0] = v[j];
-    __syncthreads();
+    lq_lds_sync();
 #pragma unroll
     for (int m = 0; m < 16; m++) v[m] = lds[t * 17 + m];
     dft16<DIR>(v);
