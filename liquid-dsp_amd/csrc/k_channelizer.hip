@@ -258,7 +258,7 @@ __global__ __launch_bounds__(256 * R, R == 1 ? 2 : 1) void k_pfb2_an256(const fl
             xr[slot(2 * c + dA) * M + j] = dot(w, u, ta);
             xr[slot(2 * c + dA + 1) * M + j] = dot(w, u, tb);
         }
-        __syncthreads();
+        lds_barrier_w();
         // blocks 2 r0 .. 2 r0 + 15 are complete: one transform per 16 lanes
         const int b = 2 * r0 + g;
         float2 v[16];
@@ -412,7 +412,7 @@ __global__ __launch_bounds__(1024, 1) void k_pfb2_an2048(const float *__restrict
             xr[slot(2 * c + 1) * A2_BSTR + pl_hi] = dot(wh, s0 + u, ta);
             xr[slot(2 * c + 2) * A2_BSTR + pl_hi] = dot(wh, s0 + u, tb);
         }
-        __syncthreads();
+        lds_barrier_w();
         const int b = 2 * r0 + hb;
         float2 *Bb = xr + slot(b) * A2_BSTR;
         {
@@ -422,7 +422,7 @@ __global__ __launch_bounds__(1024, 1) void k_pfb2_an2048(const float *__restrict
             for (int n = 0; n < 16; n++) v[n] = Bh[lane + 64 * n];
             fft1024_wave_rt<-1>(v, Bh, a1, a4, tw2, lane);   // natural order at k + 4 (k >> 8)
         }
-        __syncthreads();   // both halves of every block transformed
+        lds_barrier_w();   // both halves of every block transformed
         const int gb = b - p0;
         const bool keep = gb >= 0 && gb < nb && b < 2 * ce;
         // a dropped block's base: 2^31 (the launch's range is below it, and
@@ -443,7 +443,7 @@ __global__ __launch_bounds__(1024, 1) void k_pfb2_an2048(const float *__restrict
             __builtin_amdgcn_raw_buffer_store_b128(v4f{s0v.x, s0v.y, s1v.x, s1v.y}, ry, base + (unsigned)k * 8u, 0, 2);
             __builtin_amdgcn_raw_buffer_store_b128(v4f{d0.x, d0.y, d1.x, d1.y}, ry, base + (unsigned)(k + 1024) * 8u, 0, 2);
         }
-        __syncthreads();   // the combine's reads are done before the next group's writes
+        lds_barrier_w();   // the combine's reads are done before the next group's writes
     };
     // S is a multiple of 8 rows: the ring slot of row r0 + u is u (first
     // group) or 4 + u (second)
@@ -810,7 +810,7 @@ __global__ __launch_bounds__(256, 2) void k_pfb2_an_small(const float *__restric
             xs[slot(2 * c + dA) * M + j] = dot(w, u, ta);
             xs[slot(2 * c + dA + 1) * M + j] = dot(w, u, tb);
         }
-        __syncthreads();
+        lds_barrier_w();
         // blocks 2 r0 .. 2 r0 + 15 of every set are complete
         const int tr0 = tcs + g0;
         const int b = 2 * tr0 + tb16;
@@ -1239,7 +1239,7 @@ __global__ __launch_bounds__(256 * R, R == 1 ? 2 : 1) void k_pfb_an_fused(const 
             for (int n = 0; n < P; n++) acc = pfb_mac(h[n], w[(u - n) & (NS - 1)], acc);
             xr[u * M + j] = acc;
         }
-        __syncthreads();
+        lds_barrier_w();
         float2 v[16];
 #pragma unroll
         for (int n = 0; n < 16; n++) v[n] = xr[g * M + t + 16 * R * n];
@@ -1355,7 +1355,7 @@ __global__ __launch_bounds__(1024, 1) void k_pfb_an4096(const TC *__restrict__ h
 #pragma unroll
             for (int q = 0; q < 4; q++) wold[q * 1024 + tid] = w[q][0];
         }
-        __syncthreads();
+        lds_barrier_w();
         if (wave < 4 * G) {   // block b0 + wave / 4, quarter wave % 4
             float2 *Bq = xr + (wave >> 2) * A4_BSTR + (wave & 3) * A4_QS;
             float2 v[16];
@@ -1363,7 +1363,7 @@ __global__ __launch_bounds__(1024, 1) void k_pfb_an4096(const TC *__restrict__ h
             for (int n = 0; n < 16; n++) v[n] = Bq[lane + 64 * n];
             fft1024_wave_rt<+1>(v, Bq, a1, a4, tw2, lane);   // natural order at k + 4 (k >> 8)
         }
-        __syncthreads();
+        lds_barrier_w();
 #pragma unroll
         for (int g = 0; g < G; g++)
 #pragma unroll
@@ -1393,7 +1393,7 @@ __global__ __launch_bounds__(1024, 1) void k_pfb_an4096(const TC *__restrict__ h
                                                           base + (unsigned)(k + 1024 * sq) * 8u, 0, 2);
             }
         }
-        __syncthreads();   // the combine's reads are done before the next group's writes
+        lds_barrier_w();   // the combine's reads are done before the next group's writes
     }
 }
 
@@ -1469,7 +1469,7 @@ __global__ __launch_bounds__(256, 2) void k_pfb_an_small(const TC *__restrict__ 
             for (int n = 0; n < P; n++) acc = pfb_mac(h[n], w[(u - n) & (NS - 1)], acc);
             xs[u * M + j] = acc;
         }
-        __syncthreads();
+        lds_barrier_w();
         float2 v[16];
         const float2 *B = xr + tset * (NS * M) + tb16 * M;
 #pragma unroll
@@ -1574,7 +1574,7 @@ __global__ __launch_bounds__(256 * R, R == 1 ? 2 : 1) void k_pfb_syn_fused(const
                     if (b >= nb - HB && b < nb && b >= cs && b < ce) znew[(b - (nb - HB)) * M + k] = v[sidx * R + q];
                 }
         }
-        __syncthreads();
+        lds_barrier_w();
 #pragma unroll
         for (int u = 0; u < NS; u++) {
             w[u] = zr[u * M + i];
@@ -1584,7 +1584,7 @@ __global__ __launch_bounds__(256 * R, R == 1 ? 2 : 1) void k_pfb_syn_fused(const
             for (int n = 0; n < P; n++) acc = pfb_mac(h[n], w[(u - n) & (NS - 1)], acc);
             if (b >= cs && b < ce) y[(long long)b * M + i] = acc;
         }
-        __syncthreads();   // zr is rewritten by the next group's transforms
+        lds_barrier_w();   // zr is rewritten by the next group's transforms
     }
 }
 
@@ -1683,7 +1683,7 @@ __global__ __launch_bounds__(1024, 1) void k_pfb_syn4096(const TC *__restrict__ 
             float2 *Bq = xr + g * A4_BSTR + rq * A4_QS;
             fft1024_wave_rt<-1>(v, Bq, a1, a4, tw2, lane);   // natural order at k + 4 (k >> 8)
         }
-        __syncthreads();
+        lds_barrier_w();
         {
             const int k = tid, pos = k + 4 * (k >> 8);
             v2f W[4];
@@ -1731,7 +1731,7 @@ __global__ __launch_bounds__(1024, 1) void k_pfb_syn4096(const TC *__restrict__ 
                 }
             }
         }
-        __syncthreads();   // the combine's reads are done before the next group's transforms
+        lds_barrier_w();   // the combine's reads are done before the next group's transforms
     }
 }
 
@@ -1808,7 +1808,7 @@ __global__ __launch_bounds__(256, 2) void k_pfb_syn_small(const TC *__restrict__
                     if (b >= nb - HB && b < nb && b >= tcs && b < tce) znew[(b - (nb - HB)) * M + k] = z;
                 }
         }
-        __syncthreads();
+        lds_barrier_w();
 #pragma unroll
         for (int u = 0; u < NS; u++) {
             w[u] = zr[set * (NS * M) + u * M + i];
@@ -1818,7 +1818,7 @@ __global__ __launch_bounds__(256, 2) void k_pfb_syn_small(const TC *__restrict__
             for (int n = 0; n < P; n++) acc = pfb_mac(h[n], w[(u - n) & (NS - 1)], acc);
             if (b >= cs && b < ce) y[(long long)b * M + i] = acc;
         }
-        __syncthreads();   // zr is rewritten by the next group's transforms
+        lds_barrier_w();   // zr is rewritten by the next group's transforms
     }
 }
 
@@ -1916,7 +1916,7 @@ __global__ __launch_bounds__(256 * R, R == 1 ? 2 : 1) void k_pfb2_syn_fused(cons
                     if (b >= nb - HB && b < nb && b >= cs && b < ce) znew[(b - (nb - HB)) * M + k] = z;
                 }
         }
-        __syncthreads();
+        lds_barrier_w();
         if (outl) {
 #pragma unroll
             for (int u = 0; u < NS; u++) {
@@ -1938,7 +1938,7 @@ __global__ __launch_bounds__(256 * R, R == 1 ? 2 : 1) void k_pfb2_syn_fused(cons
                 if (b >= cs && b < ce) y[(long long)b * M2 + i] = cadd(acc0, acc1);
             }
         }
-        __syncthreads();
+        lds_barrier_w();
     }
 }
 
@@ -2028,7 +2028,7 @@ __global__ __launch_bounds__(1024, 1) void k_pfb2_syn4096(const float *__restric
             float2 *Bq = xr + g * A4_BSTR + rq * A4_QS;
             fft1024_wave_rt<-1>(v, Bq, a1, a4, tw2, lane);   // natural order at k + 4 (k >> 8)
         }
-        __syncthreads();
+        lds_barrier_w();
         {
             const int k = tid, pos = k + 4 * (k >> 8);
             v2f W[4];
@@ -2059,7 +2059,7 @@ __global__ __launch_bounds__(1024, 1) void k_pfb2_syn4096(const float *__restric
                 }
             }
         }
-        __syncthreads();   // the combine's reads are done before the next group's transforms
+        lds_barrier_w();   // the combine's reads are done before the next group's transforms
     }
 }
 
@@ -2223,7 +2223,7 @@ __global__ __launch_bounds__(256, 2) void k_fft4096_batch(const float2 *__restri
             if (use_s2) w = cscale(w, s2);
             yb[t + 256 * k] = w;
         }
-        __syncthreads();   // lds is reused by the next transform
+        lds_barrier_w();   // lds is reused by the next transform
     }
 }
 
@@ -2294,7 +2294,7 @@ __global__ __launch_bounds__(256, 2) void k_fft8192_batch(const float2 *__restri
             yb[t + 256 * k] = u0;
             yb[4096 + t + 256 * k] = u1;
         }
-        __syncthreads();   // lds is reused by the next transform
+        lds_barrier_w();   // lds is reused by the next transform
     }
 }
 
@@ -2403,7 +2403,7 @@ __global__ __launch_bounds__(512, 1) void k_fft16384_batch(const float2 *__restr
         };
 #pragma unroll
         for (int r = 0; r < 2; r++) {
-            __syncthreads();   // the transforms' (or the previous round's) LDS reads are done
+            lds_barrier_w();   // the transforms' (or the previous round's) LDS reads are done
 #pragma unroll
             for (int mm = 0; mm < 8; mm++) {
                 float2 a, c;
@@ -2411,7 +2411,7 @@ __global__ __launch_bounds__(512, 1) void k_fft16384_batch(const float2 *__restr
                 xch[4096 * h + mm * 256 + t] = a;
                 xch[4096 * h + 2048 + mm * 256 + t] = c;
             }
-            __syncthreads();
+            lds_barrier_w();
 #pragma unroll
             for (int mm = 0; mm < 8; mm++) {
                 const int k = t + 256 * (8 * r + mm);
@@ -2431,7 +2431,7 @@ __global__ __launch_bounds__(512, 1) void k_fft16384_batch(const float2 *__restr
                 yb[4096 + k] = u1;
             }
         }
-        __syncthreads();   // lds is reused by the next transform
+        lds_barrier_w();   // lds is reused by the next transform
     }
 }
 
@@ -2502,7 +2502,7 @@ __global__ __launch_bounds__(256) void k_fftsmall_batch(const float2 *__restrict
                     yb[t * (16 / R) + u + 16 * q] = w;
                 }
         }
-        __syncthreads();   // lds is reused by the next batch of transforms
+        lds_barrier_w();   // lds is reused by the next batch of transforms
     }
 }
 

@@ -31,7 +31,7 @@ constexpr int NFFT = 4096;
 // instead of the first only: 0.367 ms).  Output stores are non-temporal
 // (0.2503 vs 0.2538 ms default policy).
 constexpr int FF_WPE = 4;        // resident workgroups per CU
-constexpr int FF_STAUX = 2;      // store cache policy: non-temporal
+constexpr int FF_STAUX = 2;      // store cache policy: non-temporal (default policy: 0.2233-0.2243 vs 0.2206-0.2212 ms, r06d)
 
 __device__ __forceinline__ float2 to_c2(float a) { return make_float2(a, 0.f); }
 __device__ __forceinline__ float2 to_c2(float2 a) { return a; }
@@ -53,7 +53,8 @@ __device__ __forceinline__ unsigned ff_unsafe1(float v)
 }
 __device__ __forceinline__ unsigned ff_unsafe(float2 v) { return ff_unsafe1(v.x) | ff_unsafe1(v.y); }
 // this wave's verdict on segment seg (lane 0 stores it): eight slots per
-// segment; 4-wave kernels clear the other four
+// segment (the repair kernel reads them as two 16-byte words), the other
+// four cleared
 __device__ __forceinline__ void ff_flag(unsigned *flags, long long seg, unsigned bad)
 {
     const unsigned long long any = __ballot(bad);
@@ -149,121 +150,6 @@ __global__ __launch_bounds__(NT, FF_WPE) void k_fftfilt_r16(int hm1, const float
             __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2, o), ry, oy, 0, FF_STAUX);
         }
     }
-    }
-}
-
-// 8192-point overlap-save segments on a 512-thread workgroup, one 4096-point
-// half per 256 threads (complex I/O; k_fftfilt8h).  Both transforms are split
-// by decimation in frequency, so each half runs plain fft4096_r16 with the
-// register budget of the 4096-point kernel (the spectrum half in registers):
-//   forward:  a[n] = x[n] + x[n+4096],  b[n] = (x[n] - x[n+4096]) W_8192^n
-//             X[2k] = FFT_4096(a)[k],   X[2k+1] = FFT_4096(b)[k]
-//   product:  half h holds Y_h[k] = X[2k+h] H[2k+h]
-//   inverse:  e = IFFT_4096(Y_0),  o = IFFT_4096(Y_1) W_8192^-n
-//             y[n] = e[n] + o[n],  y[n+4096] = e[n] - o[n]
-// Half h loads segment samples 4096 h + n (n = t + 256 q) and stores outputs
-// 4096 h + n; the two sum / difference steps swap the halves' vectors through
-// their transform scratch (write, barrier, read the partner's, barrier).  A
-// segment keeps L = 8192 - (h - 1) new outputs: the halo re-read is
-// (h - 1) / L (6.7 % at h = 512, 14 % with 4096-point segments).  Two
-// workgroups per CU (16 waves, 70 KB of LDS each).
-__global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4, 4)))
-void k_fftfilt8h(int hm1, const float2 *__restrict__ H, const void *__restrict__ hist,
-                 const void *__restrict__ xin, long long n, void *__restrict__ yout, float sre, float sim,
-                 const float2 *__restrict__ tw, unsigned *__restrict__ flags)
-{
-    __shared__ __attribute__((aligned(16))) float2 lds[2 * FFT4096_LDS];
-    typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
-    constexpr float C32[16] = {1.000000000f,  0.980785280f,  0.923879533f,  0.831469612f,
-                               0.707106781f,  0.555570233f,  0.382683432f,  0.195090322f,
-                               0.000000000f,  -0.195090322f, -0.382683432f, -0.555570233f,
-                               -0.707106781f, -0.831469612f, -0.923879533f, -0.980785280f};
-    constexpr float S32[16] = {0.000000000f, 0.195090322f, 0.382683432f, 0.555570233f,
-                               0.707106781f, 0.831469612f, 0.923879533f, 0.980785280f,
-                               1.000000000f, 0.980785280f, 0.923879533f, 0.831469612f,
-                               0.707106781f, 0.555570233f, 0.382683432f, 0.195090322f};
-    const int L = 8192 - hm1;
-    const int h = __builtin_amdgcn_readfirstlane((int)threadIdx.x >> 8), t = threadIdx.x & 255;
-    float2 *my = lds + h * FFT4096_LDS, *other = lds + (h ^ 1) * FFT4096_LDS;
-    const long long nseg = (n + L - 1) / L;
-    float2 hv[16];   // Y_h[k] = X[2k+h] H[2k+h], k = t + 256 m
-#pragma unroll
-    for (int m = 0; m < 16; m++) hv[m] = H[2 * (t + 256 * m) + h];
-    const __amdgpu_buffer_rsrc_t rx = __builtin_amdgcn_make_buffer_rsrc((void *)xin, (short)0, (int)(n * 8), 0x00020000);
-    const __amdgpu_buffer_rsrc_t rh = __builtin_amdgcn_make_buffer_rsrc((void *)hist, (short)0, hm1 * 8, 0x00020000);
-    const __amdgpu_buffer_rsrc_t ry = __builtin_amdgcn_make_buffer_rsrc(yout, (short)0, (int)(n * 8), 0x00020000);
-    const tw16x2 w16 = fft4096_tw(tw, t);
-    double sn, cs;
-    sincospi((double)t / 4096.0, &sn, &cs);
-    const v2f wt0 = v2f{(float)cs, (float)-sn};   // W_8192^t; W_8192^(t + 256 q) = W_8192^t W_32^q
-    for (long long seg = blockIdx.x; seg < nseg; seg += gridDim.x) {
-        const int sb = (int)(seg * L) - hm1 + 4096 * h;   // stream index of this half's sample 0
-        int tt = t;
-        asm volatile("" : "+v"(tt));   // per-thread offsets recomputed per segment (not hoisted, spilled)
-        float2 v[16];
-        if (seg == 0) {
-#pragma unroll
-            for (int q = 0; q < 16; q++) {
-                const int si = sb + tt + 256 * q;
-                const unsigned ox = si < 0 ? 0xFFFFFFF0u : (unsigned)si * 8u, oh = (unsigned)(si + hm1) * 8u;
-                const float2 a = __builtin_bit_cast(float2, __builtin_amdgcn_raw_buffer_load_b64(rx, ox, 0, 0));
-                const float2 b = __builtin_bit_cast(float2, __builtin_amdgcn_raw_buffer_load_b64(rh, oh, 0, 0));
-                v[q] = make_float2(a.x + b.x, a.y + b.y);
-            }
-        } else {
-#pragma unroll
-            for (int q = 0; q < 16; q++)
-                v[q] = __builtin_bit_cast(float2, __builtin_amdgcn_raw_buffer_load_b64(rx, (unsigned)(sb + tt + 256 * q) * 8u, 0, 0));
-        }
-        if (flags) {   // (uniform) firfilt: flag segments with unsafe inputs for k_ff_repair
-            unsigned bad = 0;
-#pragma unroll
-            for (int q = 0; q < 16; q++) bad |= ff_unsafe(v[q]);
-            const unsigned long long any = __ballot(bad);
-            if ((threadIdx.x & 63) == 0) flags[8 * seg + (threadIdx.x >> 6)] = any != 0ull;
-        }
-        // ---- forward DIF split: half 0 a = x0 + x1, half 1 b = (x0 - x1) W^n
-        __syncthreads();   // the previous segment's reads of both scratches are done
-#pragma unroll
-        for (int q = 0; q < 16; q++) my[tt + 256 * q] = v[q];
-        __syncthreads();
-        v2f wt = wt0;
-        asm volatile("" : "+v"(wt));
-#pragma unroll
-        for (int q = 0; q < 16; q++) {
-            const v2f p = pk(other[tt + 256 * q]);
-            if (h == 0) {
-                v[q] = unpk(pk(v[q]) + p);
-            } else {
-                const v2f w = q == 0 ? wt : pk_cmulk(wt, v2f{C32[q], -S32[q]});
-                v[q] = unpk(pk_cmul(p - pk(v[q]), w));   // (x0 - x1) W_8192^n, x0 = the partner's
-            }
-        }
-        fft4096_r16<+1>(v, my, w16, t);   // (its first barrier orders the reads above before the scratch writes)
-#pragma unroll
-        for (int m = 0; m < 16; m++) v[m] = unpk(pk_cmul(pk(v[m]), pk(hv[m])));
-        fft4096_r16<-1>(v, my, w16, t);
-        // ---- inverse DIT combine: o' = o W^-n (half 1), then e +- o'
-        if (h == 1) {
-#pragma unroll
-            for (int q = 0; q < 16; q++) {
-                const v2f w = q == 0 ? wt : pk_cmulk(wt, v2f{C32[q], -S32[q]});
-                v[q] = unpk(pk_cmul(pk(v[q]), v2f{w.x, -w.y}));
-            }
-        }
-        __syncthreads();   // the inverse transforms' scratch reads are done
-#pragma unroll
-        for (int q = 0; q < 16; q++) my[tt + 256 * q] = v[q];
-        __syncthreads();
-#pragma unroll
-        for (int q = 0; q < 16; q++) {
-            const v2f p = pk(other[tt + 256 * q]);
-            const v2f r = h == 0 ? pk(v[q]) + p : p - pk(v[q]);   // e + o' | e - o' (e = the partner's)
-            const int i = 4096 * h + tt + 256 * q;   // segment output position
-            const unsigned oy = i < hm1 ? 0xFFFFFFF0u : (unsigned)(sb + tt + 256 * q) * 8u;
-            const float2 o = make_float2(r.x * sre - r.y * sim, r.x * sim + r.y * sre);
-            __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2, o), ry, oy, 0, FF_STAUX);
-        }
     }
 }
 
@@ -449,14 +335,16 @@ __global__ __launch_bounds__(NT) void k_ff_repair(const unsigned *__restrict__ f
 
 // transform size for a filter: 4096-point segments up to 2049 taps; complex
 // I/O up to 4097 taps in 8192-point segments; 0: too long for the kernels
-// (the host runs the direct FIR).  (The 8192-point kernel halves the halo
-// re-read but needs ~170 VGPRs, three workgroups per CU with spills: h = 512
-// on 2^26 samples 0.257-0.270 ms against 0.223 for 4096-point segments,
-// profiles/r06_ab_experiments.txt; it serves the filters 4096 points cannot.)
+// (the host runs the direct FIR).  (8192-point segments halve the halo
+// re-read, but neither form keeps the 4096-point kernel's occupancy: 256
+// threads with ~170 VGPRs, three workgroups per CU with spills, 0.257-0.270
+// ms at h = 512 on 2^26 samples; two 4096-point halves on 512 threads with
+// two sum/difference exchanges through LDS, 0.278-0.281 ms; 4096-point
+// segments 0.221-0.223 ms, profiles/r06_ab_experiments.txt.  The 8192-point
+// kernel serves the filters 4096 points cannot.)
 extern "C" unsigned int lqk_fftfilt_nfft(int real_io, unsigned int hlen)
 {
     if (hlen < 1) return 0;
-    if (!real_io && getenv("LQ_DEV_FF8ALL") && hlen - 1 <= 4096) return 8192;   // DEV A/B
     if (hlen - 1 <= NFFT / 2) return NFFT;
     return !real_io && hlen - 1 <= 4096 ? 8192 : 0;
 }
@@ -500,19 +388,6 @@ extern "C" void lqk_fftfilt_run(int real_io, unsigned int hlen, unsigned int nff
         if (nfft == 8192) {
             const int hd = (hm1 + 1) & ~1;   // discarded outputs per segment: even, >= h - 1
             const long long nsegc = ((long long)nc + (8192 - hd) - 1) / (8192 - hd);
-            static const bool h8 = getenv("LQ_DEV_FF8H") != nullptr;   // DEV A/B
-            if (h8) {
-                const long long nsegh = ((long long)nc + (8192 - hm1) - 1) / (8192 - hm1);
-                const unsigned gridh = (unsigned)(nsegh < 512 ? nsegh : 512);   // persistent, two resident per CU
-                hipLaunchKernelGGL(k_fftfilt8h, dim3(gridh), dim3(512), 0, st, hm1, (const float2 *)H, hc,
-                                   (const void *)xc, (long long)nc, yc, sre, sim, tw,
-                                   guard ? (unsigned *)flags : nullptr);
-                LQ_CHECK_LAUNCH();
-                if (guard)
-                    hipLaunchKernelGGL(k_ff_repair, dim3(256), dim3(NT), 0, st, (const unsigned *)flags, nsegh,
-                                       8192 - hm1, (const float2 *)xc, (const float2 *)hc, hm1, (long long)nc,
-                                       (float2 *)yc, hx, (int)hlen, guard == 2, scale_re, scale_im);
-            } else {
             const unsigned grid = (unsigned)(nsegc < 768 ? nsegc : 768);   // persistent, three resident per CU
             const bool a16 = (((uintptr_t)xc | (uintptr_t)yc) & 15) == 0;
             hipLaunchKernelGGL(a16 ? k_fftfilt8k<true> : k_fftfilt8k<false>, dim3(grid), dim3(NT), 0, st, hd, hm1,
@@ -523,7 +398,6 @@ extern "C" void lqk_fftfilt_run(int real_io, unsigned int hlen, unsigned int nff
                 hipLaunchKernelGGL(k_ff_repair, dim3(256), dim3(NT), 0, st, (const unsigned *)flags, nsegc, 8192 - hd,
                                    (const float2 *)xc, (const float2 *)hc, hm1, (long long)nc, (float2 *)yc, hx,
                                    (int)hlen, guard == 2, scale_re, scale_im);
-            }
         } else {
             const int L = NFFT - hm1;
             const long long nsegc = ((long long)nc + L - 1) / L;

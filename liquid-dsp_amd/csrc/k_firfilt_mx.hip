@@ -545,7 +545,7 @@ static void launch_mx(const lqk_fir_desc *d, const void *hist, const void *x, lo
                            (v2f *)y, (const float *)d->hpad, d->scale_re, d->scale_im, nch, (int)d->hlen);
     };
     if (d->kind == 2) go(k_firfilt_mx16<true, 1, 3>, 3, lds16<1>());
-    else if (kb == 1) go(k_firfilt_mx16<false, 1, 4>, 4, lds16<1>());
+    else if (kb == 1) go(k_firfilt_mx16<false, 1, 4>, 4, lds16<1>());   // (five per CU: same time, r06d)
     else if (kb == 2) go(k_firfilt_mx16<false, 2, 4>, 4, lds16<2>());
     else if (kb == 3) go(k_firfilt_mx16<false, 3, 3>, 3, lds16<3>());
     else go(k_firfilt_mx16<false, 4, 3>, 3, lds16<4>());

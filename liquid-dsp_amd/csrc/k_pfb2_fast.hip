@@ -51,9 +51,6 @@ constexpr int NS = 8;      // register ring depth (rows)
 constexpr int NBUF = 17;   // LDS block buffers (writes b0..b0+16, FFT reads b0..b0+15)
 constexpr int BSTR = 1088; // floats2 per block buffer (16 x 68 transpose)
 constexpr int TSTR = 68;
-#ifndef PFB2_EXP
-#define PFB2_EXP 0   // DEV A/B (round 6): 1 resident taps, 2 no transform math, 3 no dot math, 4 late prefetch, 5 plain stores
-#endif
 
 __device__ __forceinline__ void lds_fence()
 {
@@ -260,17 +257,13 @@ __global__ __launch_bounds__(NT, 1) void k_pfb2_an1024(Params P, const float *__
             s1 -= (s1 >= NBUF) ? NBUF : 0;
             int s2 = s1 + 1;
             s2 -= (s2 >= NBUF) ? NBUF : 0;
-            if (PFB2_EXP == 3) {
-                xb[s1 * BSTR + j] = w[r];
-                xb[s2 * BSTR + j] = w[(r + 3) & 7];
-            } else {
-                xb[s1 * BSTR + j] = dot(r, ta);
-                xb[s2 * BSTR + j] = dot(r, tb);
-            }
+            xb[s1 * BSTR + j] = dot(r, ta);
+            xb[s2 * BSTR + j] = dot(r, tb);
         }
-        if (PFB2_EXP != 4 && g + 1 < ge) fetch_group(g + 1, pf);
         lds_barrier();
-        if (PFB2_EXP == 4 && g + 1 < ge) fetch_group(g + 1, pf);
+        // the next group's rows, issued after the barrier (before it: 0.635
+        // -> 0.624 ms per 2^27 samples, r06c in profiles/r06_ab_experiments.txt)
+        if (g + 1 < ge) fetch_group(g + 1, pf);
 
         // ---- one 1024-point IFFT per wave: block b0 + wave
         {
@@ -286,11 +279,11 @@ __global__ __launch_bounds__(NT, 1) void k_pfb2_an1024(Params P, const float *__
             v2f v[16];
 #pragma unroll
             for (int k = 0; k < 16; k++) v[k] = pk(B[lane + 64 * k]);
-            if (PFB2_EXP != 2) pk_dft16<-1>(v);
+            pk_dft16<-1>(v);
 #pragma unroll
             for (int k1 = 1; k1 < 16; k1++) {
                 if ((k1 & 3) == 0) __builtin_amdgcn_sched_barrier(0);
-                if (PFB2_EXP != 2) v[k1] = pk_cmul(v[k1], pk(tw1[k1 * 64 + lane]));
+                v[k1] = pk_cmul(v[k1], pk(tw1[k1 * 64 + lane]));
             }
             lds_fence();
 #pragma unroll
@@ -299,11 +292,11 @@ __global__ __launch_bounds__(NT, 1) void k_pfb2_an1024(Params P, const float *__
             const int k1 = lane >> 2, bq = lane & 3;
 #pragma unroll
             for (int a = 0; a < 16; a++) v[a] = pk(B[k1 * TSTR + 4 * a + bq]);
-            if (PFB2_EXP != 2) pk_dft16<-1>(v);
+            pk_dft16<-1>(v);
 #pragma unroll
             for (int r = 1; r < 16; r++) {
                 if ((r & 3) == 0) __builtin_amdgcn_sched_barrier(0);
-                if (PFB2_EXP != 2) v[r] = pk_cmul(v[r], pk(tw2[r * 4 + bq]));
+                v[r] = pk_cmul(v[r], pk(tw2[r * 4 + bq]));
             }
             {
                 // C[k1][bq][r] at k1 + 16 r + 260 bq: the b64 writes of each
@@ -317,7 +310,7 @@ __global__ __launch_bounds__(NT, 1) void k_pfb2_an1024(Params P, const float *__
                 // output stores: vmcnt counts stores too, so a tap load issued
                 // after them (at the top of the dot phase) would make the dot
                 // phase wait until every store of the block had drained.
-                if (PFB2_EXP != 1) load_taps();
+                load_taps();
                 __builtin_amdgcn_sched_barrier(0);
                 typedef float v4f __attribute__((ext_vector_type(4)));
                 // lane (t2, p2): bins k1 = 2 p2 + {0, 1}, r = t2 + 8u
@@ -331,16 +324,15 @@ __global__ __launch_bounds__(NT, 1) void k_pfb2_an1024(Params P, const float *__
                         c[q] = *reinterpret_cast<const v4f *>(B + 2 * p2 + 16 * (t2 + 8 * u) + 260 * q);
                     v2f e0[4] = {c[0].xy, c[1].xy, c[2].xy, c[3].xy};
                     v2f e1[4] = {c[0].zw, c[1].zw, c[2].zw, c[3].zw};
-                    if (PFB2_EXP != 2) {
-                        pk_dft4<-1>(e0[0], e0[1], e0[2], e0[3]);
-                        pk_dft4<-1>(e1[0], e1[1], e1[2], e1[3]);
-                    }
+                    pk_dft4<-1>(e0[0], e0[1], e0[2], e0[3]);
+                    pk_dft4<-1>(e1[0], e1[1], e1[2], e1[3]);
                     // Y[k1 + 16 r + 256 s], streaming (non-temporal) stores
 #pragma unroll
                     for (int sidx = 0; sidx < 4; sidx++) {
                         const v4f val = {e0[sidx].x, e0[sidx].y, e1[sidx].x, e1[sidx].y};
-                        __builtin_amdgcn_raw_buffer_store_b128(val, ry, yo + 8 * (128 * u + 256 * sidx), 0,
-                                                               PFB2_EXP == 5 ? 0 : 2);
+                        // default cache policy: 0.635 -> 0.620 ms against
+                        // non-temporal stores (r06c)
+                        __builtin_amdgcn_raw_buffer_store_b128(val, ry, yo + 8 * (128 * u + 256 * sidx), 0, 0);
                     }
                 }
             }

@@ -558,8 +558,11 @@ void launch_rs4_c(const lqk_rs4_plan &pl, unsigned long long g0, unsigned long l
                   const float2 *taps2, const float2 *hist, const float2 *x, int n, float2 *y, int nout,
                   const lqk_rs4_hb &hb, hipStream_t st)
 {
-    static const int dev_sm = getenv("LQ_DEV_RS4ST") ? atoi(getenv("LQ_DEV_RS4ST")) : 1;   // DEV A/B
-    const int smode = ((unsigned long long)y & 15) ? 0 : dev_sm;   // 16-byte output stores
+    // 16-byte output stores, whole 128-byte lines per store instruction
+    // (2; 1: two 16-byte stores 32 B apart per lane, kept for the call's
+    // ragged last tile): 0.1117-0.1120 -> 0.1099-0.1112 ms at config 5
+    // (profiles/r06_ab_experiments.txt, r06d); 0: y only 8-byte aligned
+    const int smode = ((unsigned long long)y & 15) ? 0 : 2;
     const int RS = npfb + 1;
     const size_t lds =
         (size_t)((rs4_rows<L, UP, DN>() * RS * 8 + 15) & ~15) + (size_t)(NT4 / 64) * 4 * rs4_n4<UP, DN>() * 8;

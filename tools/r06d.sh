@@ -11,6 +11,16 @@ for i in 1 2; do
     ab LQ_LIB_PATH=$B AB_TAG=base python dev/ab_r06.py $w
     ab LQ_LIB_PATH=$S AB_TAG=ldsync python dev/ab_r06.py $w
   done
+  ab LQ_LIB_PATH=/root/repo/ab/e0/libliquid_mi355x.so AB_TAG=pfb_e0 python dev/ab_r06.py pfb2 1024
+  ab LQ_LIB_PATH=/root/repo/ab/e6/libliquid_mi355x.so AB_TAG=pfb_e6 python dev/ab_r06.py pfb2 1024
+  ab LQ_LIB_PATH=$S AB_TAG=nt python dev/ab_r06.py resamp 1.037
+  ab LQ_LIB_PATH=/root/repo/ab/plain/libliquid_mi355x.so AB_TAG=plain python dev/ab_r06.py resamp 1.037
+  ab LQ_LIB_PATH=$S LQ_DEV_RS4ST=2 AB_TAG=nt_st2 python dev/ab_r06.py resamp 1.037
+  ab LQ_LIB_PATH=/root/repo/ab/plain/libliquid_mi355x.so LQ_DEV_RS4ST=2 AB_TAG=plain_st2 python dev/ab_r06.py resamp 1.037
+  ab LQ_LIB_PATH=/root/repo/ab/plain/libliquid_mi355x.so AB_TAG=plain python dev/ab_r06.py fftfilt 512
+  ab LQ_LIB_PATH=$S AB_TAG=fw4 python dev/ab_r06.py firfilt 64
+  ab LQ_LIB_PATH=/root/repo/ab/fw5/libliquid_mi355x.so AB_TAG=fw5 python dev/ab_r06.py firfilt 64
+  ab LQ_LIB_PATH=/root/repo/ab/fw6/libliquid_mi355x.so AB_TAG=fw6 python dev/ab_r06.py firfilt 64
   ab LQ_LIB_PATH=$S LQ_DEV_FF8ALL=1 LQ_DEV_FF8H=1 AB_TAG=ff8h python dev/ab_r06.py fftfilt 512
   ab LQ_LIB_PATH=$S LQ_DEV_FF8ALL=1 LQ_DEV_FF8H=1 AB_TAG=ff8h python dev/ab_r06.py fftfilt 64
   ab LQ_LIB_PATH=$S LQ_DEV_FF8ALL=1 LQ_DEV_FF8H=1 AB_TAG=ff8h python dev/ab_r06.py firfilt 256
