@@ -37,7 +37,10 @@ struct lq_firfilt_s {
     const char *who;   /* the public object name, for error messages */
 };
 
-#define LQ_FIR_FFT_MIN_TAPS 64u     /* longer complex filters take the overlap-save path ... */
+/* longer complex filters take the overlap-save path (crcf past 128 taps: at
+ * 65..128 the matrix-core band is as fast, 0.49-0.50 vs 0.51 ms per 2^27
+ * samples at h = 128; cccf past 64, where its matrix-core kernel stops) ... */
+#define LQ_FIR_FFT_MIN_TAPS(kind) ((kind) == LQ_CRCF ? 128u : 64u)
 #define LQ_FIR_FFT_MIN_N 8192ull    /* ... on device blocks of at least this many samples */
 
 static void lq_firfilt_layout(lq_firfilt *q, unsigned int n)
@@ -116,7 +119,7 @@ static void lq_firfilt_upload_coefs(lq_firfilt *q)
     if (q->d_H8) lqrt_free(q->d_H8);
     q->d_H8 = NULL;
     q->fft_n = lqk_fftfilt_nfft(0, q->hlen);
-    if (q->kind != LQ_RRRF && q->hlen > LQ_FIR_FFT_MIN_TAPS && fft_ok && q->fft_n) {
+    if (q->kind != LQ_RRRF && q->hlen > LQ_FIR_FFT_MIN_TAPS(q->kind) && fft_ok && q->fft_n) {
         q->d_H8 = lqrt_malloc((size_t)q->fft_n * 8);
         lqk_fftfilt_make_H(q->d_hpad, q->hlen, q->kind == LQ_CCCF, q->fft_n, q->d_H8, q->ctx.stream);
         lqrt_sync(q->ctx.stream);

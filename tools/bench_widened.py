@@ -21,10 +21,18 @@ STREAM = torch.cuda.Stream()
 S = STREAM.cuda_stream
 
 
-def timed(fn, it=30, w=20):
+def timed(fn, it=30, w=20, floor_ms=150.0):
+    """w warm-up calls, then more until floor_ms of wall time (clock ramp, as
+    bench.py), then `it` timed calls"""
+    import time
+    t0 = time.perf_counter()
     for _ in range(w):
         fn()
     torch.cuda.synchronize()
+    while (time.perf_counter() - t0) * 1e3 < floor_ms:
+        for _ in range(4):
+            fn()
+        torch.cuda.synchronize()
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     e0.record(STREAM)
     for _ in range(it):
