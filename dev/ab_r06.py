@@ -4,6 +4,7 @@
     python dev/ab_r06.py firfilt 64         # firfilt_crcf h=64, 2^28 samples
     python dev/ab_r06.py pfb2 1024          # firpfbch2 analyzer M=1024 m=4, 2^27 samples
     python dev/ab_r06.py resamp 1.037       # resamp_crcf r m=7 npfb=64, 2^25 samples
+    python dev/ab_r06.py spgram 1024        # spgramcf estimate_psd, 2^26 samples
 
 Each workload: launches until 150 ms of warm-up have passed, then three
 passes of 20 timed launches (HIP events on the object's stream); prints the
@@ -105,6 +106,14 @@ def main():
         q.set_stream(ST.cuda_stream)
         ms = timed(lambda: q.execute_block_dev(X.data_ptr(), nblk, y.data_ptr()))
         nb = 8.0 * nblk * M + 8.0 * nout
+    elif what == "spgram":   # spgramcf estimate_psd, nfft = arg (default window), 2^26 samples
+        n = 1 << 26
+        x, psd = cbuf(n), torch.empty(int(arg), device="cuda")
+        sg = LQ.Spgram(int(arg), default=True)
+        L = LQ.lib()
+        L.spgramcf_set_stream(sg.q, ST.cuda_stream)
+        ms = timed(lambda: L.spgramcf_estimate_psd_dev(sg.q, x.data_ptr(), n, psd.data_ptr()))
+        nb = 8.0 * n
     else:
         sys.exit("unknown workload " + what)
     best = min(ms)

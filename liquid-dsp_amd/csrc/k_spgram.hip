@@ -110,27 +110,96 @@ __global__ __launch_bounds__(NT) void k_spg_fold(const float *__restrict__ part,
     else out[(long long)blockIdx.y * nfft + k] = p;
 }
 
+// First radix-4 stage of pk_dft16 for inputs v[8..15] = 0 (a window of at
+// most 512 samples): each column's butterfly has two zero inputs.  The
+// results equal pk_dft16's but for the sign of zero terms, which |X|^2 does
+// not see.
+template <int DIR>
+__device__ __forceinline__ void pk_dft16_h(v2f (&v)[16])
+{
+    constexpr float C[16] = {1.0f,         0.92387953f,  0.70710678f,  0.38268343f,  0.0f,        -0.38268343f,
+                             -0.70710678f, -0.92387953f, -1.0f,        -0.92387953f, -0.70710678f, -0.38268343f,
+                             0.0f,         0.38268343f,  0.70710678f,  0.92387953f};
+    constexpr float S[16] = {0.0f,  0.38268343f,  0.70710678f,  0.92387953f,  1.0f,         0.92387953f,
+                             0.70710678f,  0.38268343f,  0.0f,  -0.38268343f, -0.70710678f, -0.92387953f,
+                             -1.0f, -0.92387953f, -0.70710678f, -0.38268343f};
+    v2f t[16];
+#pragma unroll
+    for (int q = 0; q < 4; q++) {
+        const v2f b = v[q], d = v[4 + q];
+        const v2f a0 = b + d, a2 = b - d;
+        const v2f a1 = DIR > 0 ? pk_subpj(b, d) : pk_addpj(b, d);
+        const v2f a3 = DIR > 0 ? pk_addpj(b, d) : pk_subpj(b, d);
+        t[q] = a0;
+        t[4 + q] = q == 0 ? a1 : pk_cmulk(a1, v2f{C[q], -DIR * S[q]});
+        t[8 + q] = (q == 0 || q == 2) ? a2 : pk_cmulk(a2, v2f{C[2 * q], -DIR * S[2 * q]});
+        t[12 + q] = q == 0 ? a3 : pk_cmulk(a3, v2f{C[(3 * q) & 15], -DIR * S[(3 * q) & 15]});
+    }
+#pragma unroll
+    for (int k0 = 0; k0 < 4; k0++) {
+        v2f b0 = t[4 * k0 + 0], b1 = t[4 * k0 + 1], b2 = t[4 * k0 + 2], b3 = t[4 * k0 + 3];
+        if (k0 == 2) {
+            const v2f a = DIR > 0 ? pk_subpj(b0, b2) : pk_addpj(b0, b2);
+            const v2f b = DIR > 0 ? pk_addpj(b0, b2) : pk_subpj(b0, b2);
+            const v2f c = b1 + b3, d = b1 - b3;
+            b0 = a + c;
+            b2 = a - c;
+            b1 = DIR > 0 ? pk_subpj(b, d) : pk_addpj(b, d);
+            b3 = DIR > 0 ? pk_addpj(b, d) : pk_subpj(b, d);
+        } else {
+            pk_dft4<DIR>(b0, b1, b2, b3);
+        }
+        v[k0] = b0;
+        v[k0 + 4] = b1;
+        v[k0 + 8] = b2;
+        v[k0 + 12] = b3;
+    }
+}
+
 // nfft = 1024, fused: one wave per chunk of SPG_TC consecutive transforms
 // gathers each window straight from (hist | x) into registers, runs the
-// wave-level 1024-point transform (lq_fft1024.h) and folds |X[k]|^2 into
-// per-lane partials -- no transform batch staged through HBM.  Transform t
-// ends at e0 + t*hop (the last one at elast).  Writes part[chunk][k] for
-// k_spg_fold, exactly as k_spg_part does.
-// HALF: W <= 512, so window samples r >= 8 of a lane (i = lane + 64 r) are
-// zero: they are neither loaded nor weighted
-template <typename S, bool HALF>
+// wave-level 1024-point transform (the lq_fft1024.h transform, forward) and
+// folds |X[k]|^2 into per-lane partials -- no transform batch staged through
+// HBM.  Transform t ends at e0 + t*hop (the last one at elast).  Writes
+// part[chunk][k] for k_spg_fold, exactly as k_spg_part does.
+//  * Only |X[k]|^2 per bin is needed, in transform order per bin, and which
+//    lane owns which bin is free: the last radix-4 pass leaves lane (t2, p2)
+//    the bins K = 2 p2 + e + 16 (t2 + 8 u) + 256 s (e, u < 2, s < 4), so the
+//    partials accumulate there, in registers -- no write-back of the spectrum
+//    through LDS and no re-read in natural order;
+//  * TR: the first pass's twiddles W_1024^{lane k1} stay in registers (30
+//    VGPRs, loaded once), so a transform reads LDS only for its two
+//    transposes and the 4-entry second-pass twiddles (complex input with a
+//    window of <= 512 samples; the other forms read the LDS table: their
+//    register windows leave no room);
+//  (0.365 -> 0.303 ms per 2^26 samples at nfft = 1024, W = 512; with the
+//  LDS twiddle table 0.315: profiles/r06_ab_experiments.txt, r06g)
+//  * HALF: W <= 512, so window samples r >= 8 of a lane (i = lane + 64 r)
+//    are zero: neither loaded nor weighted, and the first radix-4 stage runs
+//    on the eight nonzero rows (pk_dft16_h).
+template <typename S, bool HALF, bool TR>
 __global__ __launch_bounds__(NT, 3) void k_spg_fused1024(const S *__restrict__ hist, int W, const S *__restrict__ x,
                                                       long long e0, long long hop, long long T, long long elast,
                                                       const float *__restrict__ w, int accum, float alpha,
                                                       const float2 *__restrict__ tw4096, float *__restrict__ part)
 {
 #pragma clang fp contract(off)
-    __shared__ __attribute__((aligned(16))) float2 tw1[1024];
+    __shared__ __attribute__((aligned(16))) float2 tw1[TR ? 1 : 1024];
     __shared__ __attribute__((aligned(16))) float2 tw2[64];
     __shared__ __attribute__((aligned(16))) float2 Bs[NT / 64][1088];
-    f1k_tables<+1>(tw1, tw2, tw4096);
-    __syncthreads();
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    v2f T1[15];   // TR: W_1024^{lane k1}, k1 = 1..15 (forward: the table's own sign)
+    if constexpr (TR) {
+        if (threadIdx.x < 64) {
+            const int r = threadIdx.x >> 2, b = threadIdx.x & 3;
+            tw2[threadIdx.x] = tw4096[(64 * b * r) & 4095];   // W_64^{b r}, forward
+        }
+#pragma unroll
+        for (int k1 = 1; k1 < 16; k1++) T1[k1 - 1] = pk(tw4096[(4 * lane * k1) & 4095]);
+    } else {
+        f1k_tables<+1>(tw1, tw2, tw4096);
+    }
+    __syncthreads();
     const long long chunk = (long long)blockIdx.x * (NT / 64) + wave;
     const long long t0 = chunk * SPG_TC;
     if (t0 >= T) return;
@@ -187,23 +256,61 @@ __global__ __launch_bounds__(NT, 3) void k_spg_fused1024(const S *__restrict__ h
     };
     float2 nx[RW];
     gather(t0, nx);
+    const int k1 = lane >> 2, bq = lane & 3;     // second pass: lane (k1, bq)
+    const int t2 = lane >> 3, p2 = lane & 7;     // last pass: lane (t2, p2)
+    typedef float v4f __attribute__((ext_vector_type(4)));
     for (long long t = t0; t < t1; t++) {
-        float2 v[16];
+        v2f v[16];
 #pragma unroll
         for (int r = 0; r < 16; r++)
-            v[r] = r < RW ? make_float2(nx[r < RW ? r : 0].x * wv[r < RW ? r : 0], nx[r < RW ? r : 0].y * wv[r < RW ? r : 0])
-                          : make_float2(0.0f, 0.0f);
+            v[r] = r < RW ? v2f{nx[r < RW ? r : 0].x * wv[r < RW ? r : 0], nx[r < RW ? r : 0].y * wv[r < RW ? r : 0]}
+                          : v2f{0.0f, 0.0f};
         if (t + 1 < t1) gather(t + 1, nx);
-        fft1024_wave<+1>(v, B, tw1, tw2, lane);
+        // 1024 = 16 x 16 x 4 (lq_fft1024.h's fft1024_wave, forward)
+        if constexpr (HALF) pk_dft16_h<+1>(v);
+        else pk_dft16<+1>(v);
 #pragma unroll
-        for (int r = 0; r < 16; r++) {
-            const float pw = pwr(B[lane + 64 * r + 4 * (r >> 2)]);
-            p[r] = accum ? (1.0f - alpha) * p[r] + alpha * pw : p[r] + pw;
+        for (int k = 1; k < 16; k++) v[k] = pk_cmul(v[k], TR ? T1[k - 1] : pk(tw1[k * 64 + lane]));
+        f1k_wave_fence();
+#pragma unroll
+        for (int k = 0; k < 16; k++) B[k * 68 + lane] = unpk(v[k]);
+        f1k_wave_fence();
+#pragma unroll
+        for (int a = 0; a < 16; a++) v[a] = pk(B[k1 * 68 + 4 * a + bq]);
+        pk_dft16<+1>(v);
+#pragma unroll
+        for (int r = 1; r < 16; r++) v[r] = pk_cmul(v[r], pk(tw2[r * 4 + bq]));
+        f1k_wave_fence();
+#pragma unroll
+        for (int r = 0; r < 16; r++) B[k1 + 16 * r + 260 * bq] = unpk(v[r]);
+        f1k_wave_fence();
+#pragma unroll
+        for (int u = 0; u < 2; u++) {
+            v4f c[4];
+#pragma unroll
+            for (int q = 0; q < 4; q++)
+                c[q] = *reinterpret_cast<const v4f *>(B + 2 * p2 + 16 * (t2 + 8 * u) + 260 * q);
+            v2f e0[4] = {c[0].xy, c[1].xy, c[2].xy, c[3].xy};
+            v2f e1[4] = {c[0].zw, c[1].zw, c[2].zw, c[3].zw};
+            pk_dft4<+1>(e0[0], e0[1], e0[2], e0[3]);
+            pk_dft4<+1>(e1[0], e1[1], e1[2], e1[3]);
+            // bins 2 p2 + {0, 1} + 16 (t2 + 8 u) + 256 s -> p[8 u + 2 s + {0, 1}]
+#pragma unroll
+            for (int s = 0; s < 4; s++) {
+                const float pa = pwr(unpk(e0[s])), pb = pwr(unpk(e1[s]));
+                float &qa = p[8 * u + 2 * s], &qb = p[8 * u + 2 * s + 1];
+                qa = accum ? (1.0f - alpha) * qa + alpha * pa : qa + pa;
+                qb = accum ? (1.0f - alpha) * qb + alpha * pb : qb + pb;
+            }
         }
         f1k_wave_fence();   // B is rewritten by the next transform
     }
 #pragma unroll
-    for (int r = 0; r < 16; r++) part[chunk * 1024 + lane + 64 * r] = p[r];
+    for (int u = 0; u < 2; u++)
+#pragma unroll
+        for (int s = 0; s < 4; s++)
+            *reinterpret_cast<float2 *>(part + chunk * 1024 + 2 * p2 + 16 * (t2 + 8 * u) + 256 * s) =
+                make_float2(p[8 * u + 2 * s], p[8 * u + 2 * s + 1]);
 }
 
 // mode 0: out[(k+n/2)%n] = 10 log10(|X[k]|^2 + 1e-16)   (execute_psd)
@@ -304,13 +411,13 @@ extern "C" void lqk_spgram_fused1024(int real_in, const void *hist, unsigned int
     // (0.427-0.451 -> 0.410-0.424 ms per 2^26 inputs, identical output; r05zr)
     const bool half = W <= 512;
     if (real_in)
-        hipLaunchKernelGGL((half ? k_spg_fused1024<float, true> : k_spg_fused1024<float, false>), dim3(nwg), dim3(NT),
-                           0, (hipStream_t)stream, (const float *)hist, (int)W, (const float *)x, e0, hop,
-                           (long long)T, elast, w, accum, alpha, tw, (float *)work);
+        hipLaunchKernelGGL((half ? k_spg_fused1024<float, true, false> : k_spg_fused1024<float, false, false>),
+                           dim3(nwg), dim3(NT), 0, (hipStream_t)stream, (const float *)hist, (int)W, (const float *)x,
+                           e0, hop, (long long)T, elast, w, accum, alpha, tw, (float *)work);
     else
-        hipLaunchKernelGGL((half ? k_spg_fused1024<float2, true> : k_spg_fused1024<float2, false>), dim3(nwg),
-                           dim3(NT), 0, (hipStream_t)stream, (const float2 *)hist, (int)W, (const float2 *)x, e0, hop,
-                           (long long)T, elast, w, accum, alpha, tw, (float *)work);
+        hipLaunchKernelGGL((half ? k_spg_fused1024<float2, true, true> : k_spg_fused1024<float2, false, false>),
+                           dim3(nwg), dim3(NT), 0, (hipStream_t)stream, (const float2 *)hist, (int)W,
+                           (const float2 *)x, e0, hop, (long long)T, elast, w, accum, alpha, tw, (float *)work);
     LQ_CHECK_LAUNCH();
     spg_fold(T, 1024, accum, alpha, dst, work, (hipStream_t)stream);
 }
