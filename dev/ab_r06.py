@@ -106,6 +106,15 @@ def main():
         q.set_stream(ST.cuda_stream)
         ms = timed(lambda: q.execute_block_dev(X.data_ptr(), nblk, y.data_ptr()))
         nb = 8.0 * nblk * M + 8.0 * nout
+    elif what == "pfbsyn1":   # firpfbch synthesizer M, m=4, 2^27 samples
+        M = int(arg)
+        nblk = (1 << 27) // M
+        X, y = cbuf(nblk * M), torch.empty(2 * nblk * M, device="cuda")
+        q = LQ.FirPfbch(LQ.LIQUID_SYNTHESIZER, M, m=4, As=60.0)
+        q.set_stream(ST.cuda_stream)
+        L = LQ.lib()
+        ms = timed(lambda: L.firpfbch_crcf_execute_block_dev(q.q, X.data_ptr(), nblk, y.data_ptr()))
+        nb = 16.0 * nblk * M
     elif what == "spgram":   # spgramcf estimate_psd, nfft = arg (default window), 2^26 samples
         n = 1 << 26
         x, psd = cbuf(n), torch.empty(int(arg), device="cuda")

@@ -519,7 +519,7 @@ __global__ __launch_bounds__(NT, 1) void k_pfb_an1024(const float2 *hist, const 
 // ---------------------------------------------------------------- firpfbch synthesizer
 // firpfbch.c:314-336 mirrored: Z_b = IFFT(X_b) (unnormalised), y_b[i] =
 // sum_{n<P} h[i P + n] Z_{b-n}[i].  Per iteration the 16 waves transform 16
-// blocks of X (prefetched into registers one iteration ahead) into LDS; then
+// blocks of X into LDS; then
 // lane i pulls column i of the 16 results through a register ring of the
 // last 8 Z values and writes y_b[i] (64 consecutive samples per wave
 // instruction).  A workgroup rebuilds its first blocks' history by
@@ -571,16 +571,15 @@ __global__ __launch_bounds__(NT, 1) void k_pfb_syn1024(const float2 *__restrict_
         const long long c = b0 - s;   // buffer (P-1) - s
         zr[c & 7] = c < 0 ? state[(P - 1 + c) * M + tid] : zb[(P - 1 - s) * BSTR + zi];
     }
-    float2 xv[16];
-    if (b0 + wave < nblk) load_block(b0 + wave, xv);
     __syncthreads();   // history buffers consumed
 
     for (long long g = gs; g < ge; g++) {
         const long long b = 16 * g + wave;
+        // the block is loaded when its transform starts: holding the next
+        // block in registers across the transform (one iteration ahead) ran
+        // 0.446-0.449 against 0.430-0.433 ms per 2^27 samples (r06j)
         float2 v[16];
-#pragma unroll
-        for (int k = 0; k < 16; k++) v[k] = xv[k];
-        if (g + 1 < ge && b + 16 < nblk) load_block(b + 16, xv);
+        if (b < nblk) load_block(b, v);
         if (b < nblk) fft1024_wave<-1>(v, zb + wave * BSTR, tw1, tw2, lane);
         lds_barrier();
 #pragma unroll
@@ -607,7 +606,9 @@ __global__ __launch_bounds__(NT, 1) void k_pfb_syn1024(const float2 *__restrict_
 // c = i + f M/2: every term comes from the one column c, so lane c owns it
 // (a 16-deep register ring of z_b[c]) and writes y for the blocks whose
 // parity matches its half.  16 inverse transforms per iteration as in the
-// firpfbch synthesizer; history from the 15 X blocks before the range.
+// firpfbch synthesizer, the two scalings applied in the transform's last
+// pass (a separate pass over the LDS result before: 0.402 -> 0.372 ms per
+// 2^26 outputs, r06h); history from the 15 X blocks before the range.
 template <int L>
 __global__ __launch_bounds__(NT, 1) void k_pfb2_syn1024(const float2 *__restrict__ X, long long nblk, int p0,
                                                         int gpw, const float *__restrict__ hsub,
@@ -645,18 +646,10 @@ __global__ __launch_bounds__(NT, 1) void k_pfb2_syn1024(const float2 *__restrict
 #pragma unroll
         for (int k = 0; k < 16; k++) v[k] = Xb[64 * k];
     };
-    // the next block's first PFX values are prefetched during the column phase
-    constexpr int PFX = 8;
-    // 0.5 IFFT of one block into B (natural order, padded)
+    // 0.5 IFFT of one block into B (natural order, padded): x 1/M then x M/2
+    // (firpfbch2.c:303-307) applied in the transform's last pass
     auto zform = [&](float2 (&v)[16], float2 *B) {
-        fft1024_wave<-1>(v, B, tw1, tw2, lane);
-#pragma unroll
-        for (int k = 0; k < 16; k++) {
-            const int o = lane + 64 * k;
-            float2 *p = B + o + 4 * (o >> 8);
-            *p = make_float2(p->x * (1.0f / M) * (float)M2, p->y * (1.0f / M) * (float)M2);
-        }
-        f1k_wave_fence();
+        fft1024_wave<-1, true>(v, B, tw1, tw2, lane, 1.0f / M, (float)M2);
     };
     __syncthreads();   // twiddle tables ready
     // history z_{b0-15} .. z_{b0-1}: wave w < 15 forms z_{b0-15+w}
@@ -674,27 +667,20 @@ __global__ __launch_bounds__(NT, 1) void k_pfb2_syn1024(const float2 *__restrict
         const long long cb = b0 - s;   // buffer HB - s
         zr[cb & 15] = cb < 0 ? state[(HB + cb) * M + c] : zb[(HB - s) * BSTR + zi];
     }
-    float2 xv[PFX];
-    if (b0 + wave < nblk) {
-#pragma unroll
-        for (int q = 0; q < PFX; q++) xv[q] = X[(b0 + wave) * M + lane + 64 * q];
-    }
     __syncthreads();   // history buffers consumed
 
     for (long long g = gs; g < ge; g++) {
         const long long b = 16 * g + wave;
         if (b < nblk) {
+            // loaded when the transform starts: the first 8 (or 12, 16) of
+            // the block's values prefetched during the column phase ran
+            // 0.372-0.374 (0.397, 0.450) against 0.351-0.356 ms (r06h, r06i)
             float2 v[16];
-#pragma unroll
-            for (int q = 0; q < 16; q++) v[q] = q < PFX ? xv[q] : X[b * M + lane + 64 * q];
+            load_block(b, v);
             zform(v, zb + wave * BSTR);
         }
         lds_barrier();
         load_taps();
-        if (g + 1 < ge && b + 16 < nblk) {
-#pragma unroll
-            for (int q = 0; q < PFX; q++) xv[q] = X[(b + 16) * M + lane + 64 * q];
-        }
 #pragma unroll
         for (int r = 0; r < 16; r++) {
             const long long bb = 16 * g + r;

@@ -36,9 +36,11 @@ __device__ __forceinline__ void f1k_tables(float2 *tw1, float2 *tw2, const float
 // (B: 1088 float2 per wave).  1024 = 16 x 16 x 4 with packed arithmetic
 // (lq_device.h): DFT16, twiddle, transpose, DFT16, twiddle, transpose, four
 // DFT4 per lane; the same transform as the firpfbch2 fast path.
-template <int DIR>
+// SC: every output leaves multiplied by s1, then by s2 (the synthesizers'
+// IFFT scalings, in the reference's order), in the last pass's registers.
+template <int DIR, bool SC = false>
 __device__ __forceinline__ void fft1024_wave(float2 (&v)[16], float2 *B, const float2 *tw1, const float2 *tw2,
-                                             int lane)
+                                             int lane, float s1 = 1.0f, float s2 = 1.0f)
 {
     v2f p[16];
 #pragma unroll
@@ -80,6 +82,10 @@ __device__ __forceinline__ void fft1024_wave(float2 (&v)[16], float2 *B, const f
         // Y[K], K = 2 p2 + 16 (t2 + 8u) + 256 s, at K + 4 s
 #pragma unroll
         for (int sidx = 0; sidx < 4; sidx++) {
+            if constexpr (SC) {
+                e0[sidx] = (e0[sidx] * v2f{s1, s1}) * v2f{s2, s2};
+                e1[sidx] = (e1[sidx] * v2f{s1, s1}) * v2f{s2, s2};
+            }
             const v4f val = {e0[sidx].x, e0[sidx].y, e1[sidx].x, e1[sidx].y};
             *reinterpret_cast<v4f *>(B + 2 * p2 + 16 * (t2 + 8 * u) + 260 * sidx) = val;
         }
