@@ -115,6 +115,15 @@ def main():
         L = LQ.lib()
         ms = timed(lambda: L.firpfbch_crcf_execute_block_dev(q.q, X.data_ptr(), nblk, y.data_ptr()))
         nb = 16.0 * nblk * M
+    elif what == "pfban1":   # firpfbch analyzer M, m=4, 2^27 samples
+        M = int(arg)
+        nblk = (1 << 27) // M
+        x, Y = cbuf(nblk * M), torch.empty(2 * nblk * M, device="cuda")
+        q = LQ.FirPfbch(LQ.LIQUID_ANALYZER, M, m=4, As=60.0)
+        q.set_stream(ST.cuda_stream)
+        L = LQ.lib()
+        ms = timed(lambda: L.firpfbch_crcf_execute_block_dev(q.q, x.data_ptr(), nblk, Y.data_ptr()))
+        nb = 16.0 * nblk * M
     elif what == "spgram":   # spgramcf estimate_psd, nfft = arg (default window), 2^26 samples
         n = 1 << 26
         x, psd = cbuf(n), torch.empty(int(arg), device="cuda")

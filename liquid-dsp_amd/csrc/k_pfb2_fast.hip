@@ -14,10 +14,11 @@
 //    SIMD) owns all 1024 columns, one per lane, with the column's even- and
 //    odd-block taps and an 8-deep register ring.  Rows stream through the
 //    ring, so every input sample is read from HBM once per workgroup
-//    segment.  Eight rows per iteration complete sixteen blocks; all eight
-//    rows of the next iteration are prefetched into registers while the FFTs
-//    run (the tap selection is per lane, outside the loop, so the row loop
-//    carries no per-lane selects: 108 VGPRs, no spills).
+//    segment.  Eight rows per iteration complete sixteen blocks; six rows
+//    of the next iteration are prefetched into registers while the FFTs run
+//    and the last two load in the dot phase (the tap selection is per lane,
+//    outside the loop, so the row loop carries no per-lane selects: 112
+//    VGPRs, no spills).
 //  * X of each block goes to an LDS ring (17 block buffers, 148 KB); after a
 //    barrier each wave runs one 1024-point IFFT in registers, 1024 = 16x16x4:
 //    16-point DFT over the lane's 16 bins (j = lane + 64k), twiddle, LDS
@@ -214,7 +215,10 @@ __global__ __launch_bounds__(NT, 1) void k_pfb2_an1024(Params P, const float *__
         rn = odd ? make_float2(v.z, v.w) : make_float2(sx, sy);
     };
     typedef typename std::conditional<PAIR, v4f_, float2>::type PfT;
-    constexpr int NPF = PAIR ? 4 : 8;
+    // Six of the group's eight rows are prefetched; the last two are loaded
+    // in the dot phase itself (all eight ahead: 0.630 ms, six: 0.620, four:
+    // 0.635 per 2^27 samples, r06l)
+    constexpr int NPF = PAIR ? 3 : 6;   // prefetch registers (PAIR: row pairs)
     auto fetch_group = [&](long long g, PfT (&pf)[NPF]) {
 #pragma unroll
         for (int q = 0; q < NPF; q++) {
@@ -248,10 +252,10 @@ __global__ __launch_bounds__(NT, 1) void k_pfb2_an1024(Params P, const float *__
             if constexpr (PAIR) {
                 // (the odd row waits in nxt: its ring slot still holds row
                 // r-7, which row r's dot product reads)
-                if ((r & 1) == 0) split(pf[r >> 1], w[r], nxt);
+                if ((r & 1) == 0) split((r >> 1) < NPF ? pf[(r >> 1) < NPF ? r >> 1 : 0] : fetch2(8 * g + r), w[r], nxt);
                 else w[r] = nxt;
             } else {
-                w[r] = pf[r];
+                w[r] = r < NPF ? pf[r < NPF ? r : 0] : fetch(8 * g + r);
             }
             int s1 = slot0 + 2 * r + dA;
             s1 -= (s1 >= NBUF) ? NBUF : 0;
@@ -508,8 +512,14 @@ __global__ __launch_bounds__(NT, 1) void k_pfb_an1024(const float2 *hist, const 
             }
             xb[r * BSTR + tid] = acc;   // X[j], j = the lane's column
         }
-        if (g + 1 < ge) fetch_pf(g + 1, pf);
+        // the next group's first PF rows: at p = 8 eight of 16, issued after
+        // the barrier (0.387 ms per 2^27 samples against 0.395 for twelve
+        // issued before it, 0.403-0.416 for twelve after, 0.411 for four,
+        // r06k / r06l); at p = 4 all sixteen, before it
+        constexpr bool after = PF < 16;
+        if (!after && g + 1 < ge) fetch_pf(g + 1, pf);
         lds_barrier();
+        if (after && g + 1 < ge) fetch_pf(g + 1, pf);
         const long long b = 16 * g + wave;
         if (b < nblk) fft1k_wave_store<+1>(xb + wave * BSTR, tw1, tw2, lane, Y + b * M);
         lds_barrier();
@@ -779,10 +789,10 @@ extern "C" int lqk_firpfbch_analyzer_fast(int ctaps, unsigned int Mch, unsigned 
         const float2 *zero = (const float2 *)lqrt_zeros();
         const bool pair = ((uintptr_t)xs & 15) == 0 && ((uintptr_t)hs & 15) == 0;
         if (p == 8 && pair)
-            hipLaunchKernelGGL((k_pfb_an1024<8, 12, true>), dim3(nwg), dim3(NT), 0, st, hs, xs, nb, (int)gpw,
+            hipLaunchKernelGGL((k_pfb_an1024<8, 8, true>), dim3(nwg), dim3(NT), 0, st, hs, xs, nb, (int)gpw,
                                (const float *)hsub, tw, (float2 *)Y + ob * M, zero);
         else if (p == 8)
-            hipLaunchKernelGGL((k_pfb_an1024<8, 12, false>), dim3(nwg), dim3(NT), 0, st, hs, xs, nb, (int)gpw,
+            hipLaunchKernelGGL((k_pfb_an1024<8, 8, false>), dim3(nwg), dim3(NT), 0, st, hs, xs, nb, (int)gpw,
                                (const float *)hsub, tw, (float2 *)Y + ob * M, zero);
         else if (pair)
             hipLaunchKernelGGL((k_pfb_an1024<4, 16, true>), dim3(nwg), dim3(NT), 0, st, hs, xs, nb, (int)gpw,
