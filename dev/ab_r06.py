@@ -68,6 +68,18 @@ def main():
         q.set_stream(ST.cuda_stream)
         ms = timed(lambda: q.execute_block_dev(x.data_ptr(), n, y.data_ptr()))
         nb = 16.0 * n
+    elif what in ("firfilt_rrrf", "firfilt_cccf"):   # 2^27 samples
+        n = 1 << 27
+        real = what.endswith("rrrf")
+        x = (torch.rand(n if real else 2 * n, device="cuda") - 0.5)
+        y = torch.empty_like(x)
+        h = (torch.rand(int(arg) * (1 if real else 2)) - 0.5).numpy()
+        if not real:
+            h = (h[0::2] + 1j * h[1::2]).astype("complex64")
+        q = LQ.FirFilt(what[-4:], h)
+        q.set_stream(ST.cuda_stream)
+        ms = timed(lambda: q.execute_block_dev(x.data_ptr(), n, y.data_ptr()))
+        nb = (8.0 if real else 16.0) * n
     elif what == "pfb2":
         M, m = int(arg), 4
         n = 1 << 27
