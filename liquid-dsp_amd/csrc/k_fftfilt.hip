@@ -72,9 +72,12 @@ template <bool REAL>
 __global__ __launch_bounds__(NT, FF_WPE) void k_fftfilt_r16(int hm1, const float2 *__restrict__ H,
                                                     const void *__restrict__ hist, const void *__restrict__ xin,
                                                     long long n, void *__restrict__ yout, float sre, float sim,
-                                                    const float2 *__restrict__ tw, unsigned *__restrict__ flags)
+                                                    const float2 *__restrict__ tw, unsigned *__restrict__ flags,
+                                                    lqk_hist_job hj)
 {
     __shared__ __attribute__((aligned(16))) float2 lds[FFT4096_LDS];
+    if constexpr (REAL) lq_hist_job_run<float>(hj);   // the object's next history
+    else lq_hist_job_run<float2>(hj);
     const int L = NFFT - hm1;
     const int t = threadIdx.x;
     const long long nseg = (n + L - 1) / L;
@@ -176,9 +179,11 @@ template <bool A16>
 __global__ __launch_bounds__(NT, 3) void k_fftfilt8k(int hd, int hm1, const float2 *__restrict__ H,
                                                     const void *__restrict__ hist, const void *__restrict__ xin,
                                                     long long n, void *__restrict__ yout, float sre, float sim,
-                                                    const float2 *__restrict__ tw, unsigned *__restrict__ flags)
+                                                    const float2 *__restrict__ tw, unsigned *__restrict__ flags,
+                                                    lqk_hist_job hj)
 {
     __shared__ __attribute__((aligned(16))) float2 lds[FFT4096_LDS];
+    lq_hist_job_run<float2>(hj);   // the object's next history
     typedef float v4f __attribute__((ext_vector_type(4)));
     typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
     constexpr float C32[16] = {1.000000000f,  0.980785280f,  0.923879533f,  0.831469612f,
@@ -361,7 +366,7 @@ extern "C" size_t lqk_fftfilt_flag_bytes(unsigned int hlen, unsigned int nfft, u
 
 extern "C" void lqk_fftfilt_run(int real_io, unsigned int hlen, unsigned int nfft, const void *H, const void *hist,
                                 const void *x, unsigned long long n, void *y, float scale_re, float scale_im,
-                                const float *hx, int guard, void *flags, void *stream)
+                                const float *hx, int guard, void *flags, const lqk_hist_job *job, void *stream)
 {
     if (guard && (real_io || !hx || !flags)) {
         fprintf(stderr, "error: fftfilt: guarded form needs complex I/O, the taps and a flag buffer\n");
@@ -385,6 +390,8 @@ extern "C" void lqk_fftfilt_run(int real_io, unsigned int hlen, unsigned int nff
         const char *xc = (const char *)x + c0 * es;
         const void *hc = c0 == 0 ? hist : (const void *)(xc - (size_t)hm1 * es);
         void *yc = (char *)y + c0 * es;
+        // the history update rides on the first launch
+        const lqk_hist_job hj = (c0 == 0 && job) ? *job : lqk_hist_job{nullptr, nullptr, 0ull, nullptr, 0u};
         if (nfft == 8192) {
             const int hd = (hm1 + 1) & ~1;   // discarded outputs per segment: even, >= h - 1
             const long long nsegc = ((long long)nc + (8192 - hd) - 1) / (8192 - hd);
@@ -392,7 +399,7 @@ extern "C" void lqk_fftfilt_run(int real_io, unsigned int hlen, unsigned int nff
             const bool a16 = (((uintptr_t)xc | (uintptr_t)yc) & 15) == 0;
             hipLaunchKernelGGL(a16 ? k_fftfilt8k<true> : k_fftfilt8k<false>, dim3(grid), dim3(NT), 0, st, hd, hm1,
                                (const float2 *)H, hc, (const void *)xc, (long long)nc, yc, sre, sim, tw,
-                               guard ? (unsigned *)flags : nullptr);
+                               guard ? (unsigned *)flags : nullptr, hj);
             LQ_CHECK_LAUNCH();
             if (guard)
                 hipLaunchKernelGGL(k_ff_repair, dim3(256), dim3(NT), 0, st, (const unsigned *)flags, nsegc, 8192 - hd,
@@ -404,12 +411,12 @@ extern "C" void lqk_fftfilt_run(int real_io, unsigned int hlen, unsigned int nff
             const unsigned grid = (unsigned)(nsegc < 4096 ? nsegc : 4096);   // persistent, four resident per CU
             if (real_io)
                 hipLaunchKernelGGL((k_fftfilt_r16<true>), dim3(grid), dim3(NT), 0, st, hm1, (const float2 *)H, hc,
-                                   (const void *)xc, (long long)nc, yc, sre, sim, tw, nullptr);
+                                   (const void *)xc, (long long)nc, yc, sre, sim, tw, nullptr, hj);
             else
             {
                 hipLaunchKernelGGL((k_fftfilt_r16<false>), dim3(grid), dim3(NT), 0, st, hm1, (const float2 *)H, hc,
                                    (const void *)xc, (long long)nc, yc, sre, sim, tw,
-                                   guard ? (unsigned *)flags : nullptr);
+                                   guard ? (unsigned *)flags : nullptr, hj);
                 LQ_CHECK_LAUNCH();
                 if (guard)
                     hipLaunchKernelGGL(k_ff_repair, dim3(256), dim3(NT), 0, st, (const unsigned *)flags, nsegc, L,

@@ -899,13 +899,15 @@ extern "C" size_t lqk_firfilt_scratch_bytes(const lqk_fir_desc *d, unsigned long
 }
 
 extern "C" void lqk_firfilt(const lqk_fir_desc *d, const void *hist, const void *x, unsigned long long n,
-                            void *y, void *scratch, void *stream)
+                            void *y, void *scratch, const lqk_hist_job *job, void *stream)
 {
     if (n == 0) return;
     // LQ_FIRFILT_NO_MFMA=1 keeps crcf h<=64 on the VALU kernel (comparisons)
     static int no_mx = -1;
     if (no_mx < 0) no_mx = getenv("LQ_FIRFILT_NO_MFMA") != nullptr;
-    if (!no_mx && lqk_firfilt_mx(d, hist, x, n, y, stream)) return;
+    if (!no_mx && lqk_firfilt_mx(d, hist, x, n, y, job, stream)) return;
+    // the VALU kernel may run in place: the window update reads x first
+    if (job && job->dst) lqk_window_append(d->kind != 0, job->src, job->L, job->x, job->n, job->dst, stream);
     hipStream_t st = (hipStream_t)stream;
     const void *halo = nullptr;
     if (x == y) {

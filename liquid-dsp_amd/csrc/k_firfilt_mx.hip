@@ -190,9 +190,10 @@ template <bool CC, int KB, int WPC>
 __global__ __launch_bounds__(NT, WPC) void k_firfilt_mx16(const v2f *__restrict__ win, const v2f *__restrict__ x,
                                                         long long n, v2f *__restrict__ y,
                                                         const float *__restrict__ hpad, float sre, float sim,
-                                                        long long nch, int hlen)
+                                                        long long nch, int hlen, lqk_hist_job hj)
 {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    lq_hist_job_run<v2f>(hj);   // the object's next window (no launch of its own)
     constexpr int HALO = 64 * KB, PL16 = pl16<KB>();
     constexpr int NS = (16 + HALO + 31) / 32;   // K steps of 32 over the 16 + HALO band
     unsigned char *planes = smem;
@@ -408,9 +409,10 @@ template <int WPC>
 __global__ __launch_bounds__(NT, WPC) void k_firfilt_mx16_r(const float *__restrict__ win,
                                                             const float *__restrict__ x, long long n,
                                                             float *__restrict__ y, const float *__restrict__ hpad,
-                                                            float sre, long long nch, int hlen)
+                                                            float sre, long long nch, int hlen, lqk_hist_job hj)
 {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    lq_hist_job_run<float>(hj);   // the object's next window (no launch of its own)
     unsigned *sbad = reinterpret_cast<unsigned *>(smem + 3 * PLR16);
     unsigned char *planes = smem;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -522,13 +524,13 @@ __global__ __launch_bounds__(NT, WPC) void k_firfilt_mx16_r(const float *__restr
 // range-checked load offsets fit 32 bits; a later launch takes its 64-sample
 // history straight from the preceding input.
 static void launch_mx(const lqk_fir_desc *d, const void *hist, const void *x, long long n, void *y,
-                      hipStream_t st)
+                      const lqk_hist_job &hj, hipStream_t st)
 {
     if (d->kind == 0) {   // rrrf: 4096-output chunks, four workgroups per CU (112 VGPRs, 38 KB of LDS)
         const long long nch = (n + CHR - 1) / CHR;
         const long long nwg = nch < 1024 ? nch : 1024;
         hipLaunchKernelGGL(k_firfilt_mx16_r<4>, dim3((unsigned)nwg), dim3(NT), LDSR16, st, (const float *)hist,
-                           (const float *)x, n, (float *)y, (const float *)d->hpad, d->scale_re, nch, (int)d->hlen);
+                           (const float *)x, n, (float *)y, (const float *)d->hpad, d->scale_re, nch, (int)d->hlen, hj);
         LQ_CHECK_LAUNCH();
         return;
     }
@@ -542,7 +544,7 @@ static void launch_mx(const lqk_fir_desc *d, const void *hist, const void *x, lo
     auto go = [&](auto kern, int wpc, int lds) {
         const long long g = nch < 256LL * wpc ? nch : 256LL * wpc;
         hipLaunchKernelGGL(kern, dim3((unsigned)g), dim3(NT), lds, st, (const v2f *)hist, (const v2f *)x, n,
-                           (v2f *)y, (const float *)d->hpad, d->scale_re, d->scale_im, nch, (int)d->hlen);
+                           (v2f *)y, (const float *)d->hpad, d->scale_re, d->scale_im, nch, (int)d->hlen, hj);
     };
     if (d->kind == 2) go(k_firfilt_mx16<true, 1, 3>, 3, lds16<1>());
     else if (kb == 1) go(k_firfilt_mx16<false, 1, 4>, 4, lds16<1>());   // (five per CU: same time, r06d)
@@ -556,7 +558,7 @@ static void launch_mx(const lqk_fir_desc *d, const void *hist, const void *x, lo
 // 33..64 taps (HP = 64, one chunk), taps in the split's safe range, not in
 // place, 16-byte aligned x and y.
 extern "C" int lqk_firfilt_mx(const lqk_fir_desc *d, const void *hist, const void *x, unsigned long long n,
-                              void *y, void *stream)
+                              void *y, const lqk_hist_job *job, void *stream)
 {
     // 33..64 taps (one 64-tap block) for every type; 65..128 (two) for crcf
     if (d->hc != 64 || !(d->nchunk == 1 || (d->nchunk <= 4 && d->kind == 1)) || x == y || !d->mx_ok) return 0;
@@ -567,8 +569,10 @@ extern "C" int lqk_firfilt_mx(const lqk_fir_desc *d, const void *hist, const voi
     for (long long o = 0; o < (long long)n; o += LCH) {
         const long long nn = ((long long)n - o) < LCH ? ((long long)n - o) : LCH;
         const char *xo = (const char *)x + o * es;
+        // the window update rides on the first launch
+        const lqk_hist_job hj = (o == 0 && job) ? *job : lqk_hist_job{nullptr, nullptr, 0ull, nullptr, 0u};
         launch_mx(d, o == 0 ? hist : (const void *)(xo - (size_t)64 * d->nchunk * es), xo, nn, (char *)y + o * es,
-                  (hipStream_t)stream);
+                  hj, (hipStream_t)stream);
     }
     return 1;
 }

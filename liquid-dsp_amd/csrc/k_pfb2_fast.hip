@@ -81,6 +81,7 @@ struct Params {
     long long gend;   // one past the last group needed
     float2 *Y;
     const float2 *zero; // >= 8 bytes of zeros (lqrt_zeros)
+    lqk_hist_job hj;    // the object's history update (first launch of a call)
 };
 
 template <int L, bool PAIR>
@@ -95,6 +96,7 @@ __global__ __launch_bounds__(NT, 1) void k_pfb2_an1024(Params P, const float *__
     const int tid = threadIdx.x;
     const int lane = tid & 63;
     const int wave = tid >> 6;
+    lq_hist_job_run<float2>(P.hj);   // (its loads and stores drain at the s_waitcnt below)
 
     {
         const int k1 = tid >> 6, t = tid & 63;
@@ -719,7 +721,7 @@ __global__ __launch_bounds__(NT, 1) void k_pfb2_syn1024(const float2 *__restrict
 // their history straight from the preceding input.
 extern "C" int lqk_firpfbch2_analyzer_fast(unsigned int Mch, unsigned int m, const void *hsub, const void *hist,
                                            const void *x, unsigned long long nblocks, long long B0, void *Y,
-                                           void *stream)
+                                           const lqk_hist_job *job, void *stream)
 {
     if (Mch != (unsigned)M || !(m == 4 || m == 2)) return 0;
     // x / hist: 8-byte sample loads; Y: 16-byte (two-bin) non-temporal stores
@@ -739,6 +741,8 @@ extern "C" int lqk_firpfbch2_analyzer_fast(unsigned int Mch, unsigned int m, con
         P.nblk = nb;
         P.Y = (float2 *)Y + ob * M;
         P.zero = (const float2 *)lqrt_zeros();
+        P.hj = {nullptr, nullptr, 0ull, nullptr, 0u};
+        if (ob == 0 && job) P.hj = *job;
         const long long gfirst = P.B0 / 16;                // 16-block group containing the first block
         const long long glast = (P.B0 + nb - 1) / 16;      // inclusive
         const long long ngroups = glast - gfirst + 1;

@@ -134,8 +134,10 @@ __global__ __launch_bounds__(NT4, (HM ? 4 : rs4_blk<L, UP, DN>())) void k_resamp
                                                       const float2 *__restrict__ taps2,
                                                       const float2 *__restrict__ hist,
                                                       const float2 *__restrict__ x, int n,
-                                                      float2 *__restrict__ y, int nout, int smode, lqk_rs4_hb hb)
+                                                      float2 *__restrict__ y, int nout, int smode, lqk_rs4_hb hb,
+                                                      lqk_hist_job hj)
 {
+    lq_hist_job_run<float2>(hj);   // the object's next history (no launch of its own)
     // HM > 0: the half-band interpolator stage (semi-length HM, 2 HM taps on
     // the odd branch) fused behind the resampler.  A tile then computes its
     // 256 resampler outputs starting HALO >= 2 HM - 1 outputs early, so the
@@ -556,7 +558,7 @@ __global__ __launch_bounds__(NT4, (HM ? 4 : rs4_blk<L, UP, DN>())) void k_resamp
 template <int L, bool UP, int HM, bool R4 = false, bool DN = false>
 void launch_rs4_c(const lqk_rs4_plan &pl, unsigned long long g0, unsigned long long K0, int npfb, float del,
                   const float2 *taps2, const float2 *hist, const float2 *x, int n, float2 *y, int nout,
-                  const lqk_rs4_hb &hb, hipStream_t st)
+                  const lqk_rs4_hb &hb, const lqk_hist_job &hj, hipStream_t st)
 {
     // 16-byte output stores, whole 128-byte lines per store instruction
     // (2; 1: two 16-byte stores 32 B apart per lane, kept for the call's
@@ -574,25 +576,26 @@ void launch_rs4_c(const lqk_rs4_plan &pl, unsigned long long g0, unsigned long l
     const int nb = wgs < 256 * blk ? wgs : 256 * blk;   // persistent: blk per CU
     if (npfb == 64)
         hipLaunchKernelGGL((k_resamp4<L, 64, UP, HM, R4, DN>), dim3(nb), dim3(NT4), lds, st, pl, g0, K0, npfb, del,
-                           taps2, hist, x, n, y, nout, smode, hb);
+                           taps2, hist, x, n, y, nout, smode, hb, hj);
     else if constexpr (HM == 0)
         hipLaunchKernelGGL((k_resamp4<L, 0, UP, 0, R4, DN>), dim3(nb), dim3(NT4), lds, st, pl, g0, K0, npfb, del,
-                           taps2, hist, x, n, y, nout, smode, hb);
+                           taps2, hist, x, n, y, nout, smode, hb, hj);
 }
 
 template <int L>
 void launch_rs4(const lqk_rs4_plan &pl, unsigned long long g0, unsigned long long K0, int npfb, float del,
-                const float2 *taps2, const float2 *hist, const float2 *x, int n, float2 *y, int nout, hipStream_t st)
+                const float2 *taps2, const float2 *hist, const float2 *x, int n, float2 *y, int nout,
+                const lqk_hist_job &hj, hipStream_t st)
 {
     const lqk_rs4_hb none{};
     if (del < 0.5f)   // r > 2: more than two outputs per input
-        launch_rs4_c<L, true, 0, true>(pl, g0, K0, npfb, del, taps2, hist, x, n, y, nout, none, st);
+        launch_rs4_c<L, true, 0, true>(pl, g0, K0, npfb, del, taps2, hist, x, n, y, nout, none, hj, st);
     else if (del <= 1.0f)
-        launch_rs4_c<L, true, 0>(pl, g0, K0, npfb, del, taps2, hist, x, n, y, nout, none, st);
+        launch_rs4_c<L, true, 0>(pl, g0, K0, npfb, del, taps2, hist, x, n, y, nout, none, hj, st);
     else if (del >= 2.0f)   // 1/4 < r <= 1/2: an output every two to four inputs
-        launch_rs4_c<L, false, 0, false, true>(pl, g0, K0, npfb, del, taps2, hist, x, n, y, nout, none, st);
+        launch_rs4_c<L, false, 0, false, true>(pl, g0, K0, npfb, del, taps2, hist, x, n, y, nout, none, hj, st);
     else
-        launch_rs4_c<L, false, 0>(pl, g0, K0, npfb, del, taps2, hist, x, n, y, nout, none, st);
+        launch_rs4_c<L, false, 0>(pl, g0, K0, npfb, del, taps2, hist, x, n, y, nout, none, hj, st);
 }
 
 } // namespace
@@ -611,9 +614,14 @@ extern "C" int lqk_resamp4_hb_supported(unsigned int npfb, unsigned int L, float
 extern "C" void lqk_resamp4(const lqk_rs4_plan *pl, unsigned long long g0, unsigned long long K0, unsigned int npfb,
                             unsigned int L, float del, const void *taps2, const void *hist, const void *x,
                             unsigned long long n, void *y, unsigned long long nout, const lqk_rs4_hb *hb,
-                            void *stream)
+                            const lqk_hist_job *job, void *stream)
 {
-    if (n == 0 || nout == 0) return;
+    if (n == 0) return;
+    if (nout == 0) {   // no outputs, so no launch: the history update on its own
+        if (job && job->dst) lqk_window_append(1, job->src, job->L, job->x, job->n, job->dst, stream);
+        return;
+    }
+    const lqk_hist_job hj = job ? *job : lqk_hist_job{nullptr, nullptr, 0ull, nullptr, 0u};
     if (!lqk_resamp4_supported(npfb, L) || n > LQK_RS_MAXN || nout * (hb ? 16ull : 8ull) >= (1ull << 31) ||
         pl->ntab * 8ull >= (1ull << 31) || !(pl->pre == ~0ull || (pl->QT >= TOUT && pl->npre == (pl->pre + 3) / 4)) ||
         (hb && !lqk_resamp4_hb_supported(npfb, L, del, hb->m))) {
@@ -627,7 +635,7 @@ extern "C" void lqk_resamp4(const lqk_rs4_plan *pl, unsigned long long g0, unsig
         switch (hb->m) {
 #define LQ_RS4_HB(MM)                                                                                   \
     case MM:                                                                                            \
-        launch_rs4_c<14, true, MM>(*pl, g0, K0, 64, del, t2, h, xi, (int)n, yo, (int)nout, *hb, st);    \
+        launch_rs4_c<14, true, MM>(*pl, g0, K0, 64, del, t2, h, xi, (int)n, yo, (int)nout, *hb, hj, st); \
         break;
             LQ_RS4_HB(3) LQ_RS4_HB(4) LQ_RS4_HB(5) LQ_RS4_HB(6) LQ_RS4_HB(7)
             LQ_RS4_HB(8) LQ_RS4_HB(9) LQ_RS4_HB(10) LQ_RS4_HB(11) LQ_RS4_HB(12)
@@ -638,7 +646,7 @@ extern "C" void lqk_resamp4(const lqk_rs4_plan *pl, unsigned long long g0, unsig
     }
 #define LQ_RS4_CASE(LL)                                                                                 \
     case LL:                                                                                            \
-        launch_rs4<LL>(*pl, g0, K0, (int)npfb, del, t2, h, xi, (int)n, yo, (int)nout, st);              \
+        launch_rs4<LL>(*pl, g0, K0, (int)npfb, del, t2, h, xi, (int)n, yo, (int)nout, hj, st);          \
         break;
     switch (L) {
         LQ_RS4_CASE(2)

@@ -7,6 +7,8 @@
 
 #include <cstdint>
 
+#include "lq_kernels.h"
+
 void lq_check(hipError_t e, const char *what, const char *file, int line);
 #define LQ_CHECK(x) lq_check((x), #x, __FILE__, __LINE__)
 #define LQ_CHECK_LAUNCH() lq_check(hipGetLastError(), "kernel launch", __FILE__, __LINE__)
@@ -68,6 +70,20 @@ __device__ __forceinline__ float2 lq_load_hx(const float2 *hist_end, const float
     typedef const v2f __attribute__((address_space(1))) *gptr;
     const v2f v = __builtin_nontemporal_load(reinterpret_cast<gptr>(a));
     return make_float2(v.x, v.y);
+}
+
+// lqk_hist_job (lq_kernels.h) as a grid-strided slice per workgroup, before
+// the kernel's own work: dst[i] = (src ++ x)[n + i], i < L
+template <typename T>
+__device__ __forceinline__ void lq_hist_job_run(const lqk_hist_job &j)
+{
+    if (j.dst == nullptr) return;
+    const long long L = j.L, n = (long long)j.n, step = (long long)gridDim.x * blockDim.x;
+    for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < L; i += step) {
+        const long long k = i + n;
+        reinterpret_cast<T *>(j.dst)[i] =
+            k < L ? reinterpret_cast<const T *>(j.src)[k] : reinterpret_cast<const T *>(j.x)[k - L];
+    }
 }
 
 __device__ __forceinline__ v2f pk(float2 a) { return v2f{a.x, a.y}; }

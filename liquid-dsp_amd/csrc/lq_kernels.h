@@ -67,12 +67,28 @@ typedef struct {
                               * three-term bf16 split is float32-accurate (k_firfilt_mx.hip) */
 } lqk_fir_desc;
 
+/* A stream object's history update folded into its stream kernel: dst =
+ * the last L samples of (src: L samples) ++ (x: n samples), what
+ * lqk_window_append does as a launch of its own (~5 us per call, measured in
+ * the round-6 rocprof trace).  The kernel's workgroups copy grid-strided
+ * slices of it before their own work; dst == NULL: no job. */
+typedef struct {
+    const void *src;
+    const void *x;
+    unsigned long long n;
+    void *dst;
+    unsigned int L;
+} lqk_hist_job;
+
+/* job (NULL: none): the window update, done inside the matrix-core kernel
+ * when it takes the call, else launched before the VALU kernel (which may
+ * run in place) */
 void lqk_firfilt(const lqk_fir_desc *d, const void *hist, const void *x, unsigned long long n,
-                 void *y, void *scratch, void *stream);
+                 void *y, void *scratch, const lqk_hist_job *job, void *stream);
 /* crcf with 33..64 taps on the matrix cores (k_firfilt_mx.hip); returns 0
  * when the call does not qualify (then lqk_firfilt runs the VALU kernel) */
 int lqk_firfilt_mx(const lqk_fir_desc *d, const void *hist, const void *x, unsigned long long n, void *y,
-                   void *stream);
+                   const lqk_hist_job *job, void *stream);
 /* bytes of scratch lqk_firfilt needs for an in-place call of n samples */
 size_t lqk_firfilt_scratch_bytes(const lqk_fir_desc *d, unsigned long long n);
 /* longest history (padded tap count) the direct FIR kernel can hold in LDS */
@@ -128,9 +144,10 @@ int lqk_firpfbch2_synthesizer_fast(unsigned int M, unsigned int m, const void *h
 /* batched transforms with the two sequential output scales of fft_batch_scaled (k_channelizer.hip) */
 void lqk_fft_batch_scaled(unsigned int n, int dir, const void *x, void *y, unsigned long long batch, float s1,
                           float s2, void *stream);
+/* job (NULL: none) is done only when the call is handled (returns 1) */
 int lqk_firpfbch2_analyzer_fast(unsigned int M, unsigned int m, const void *hsub, const void *hist,
                                 const void *x, unsigned long long nblocks, long long B0, void *Y,
-                                void *stream);
+                                const lqk_hist_job *job, void *stream);
 /* synthesizer: nblocks x M channel inputs -> nblocks x M/2 outputs.
  * state: the previous 4m-1 IFFT vectors (M each), zscratch (4m-1+nblocks)*M;
  * see csrc/k_channelizer.hip */
@@ -165,7 +182,7 @@ unsigned int lqk_fftfilt_nfft(int real_io, unsigned int hlen);
 size_t lqk_fftfilt_flag_bytes(unsigned int hlen, unsigned int nfft, unsigned long long n);
 void lqk_fftfilt_run(int real_io, unsigned int hlen, unsigned int nfft, const void *H, const void *hist,
                      const void *x, unsigned long long n, void *y, float scale_re, float scale_im,
-                     const float *hx, int guard, void *flags, void *stream);
+                     const float *hx, int guard, void *flags, const lqk_hist_job *job, void *stream);
 void lqk_fftfilt_make_H(const void *h_dev, unsigned int hlen, int is_complex, unsigned int nfft, void *H,
                         void *stream);
 
@@ -246,7 +263,7 @@ int lqk_resamp4_hb_supported(unsigned int npfb, unsigned int L, float del, int m
  * (NULL: none): y receives the half-band stage's 2 nout outputs instead */
 void lqk_resamp4(const lqk_rs4_plan *pl, unsigned long long g0, unsigned long long K0, unsigned int npfb,
                  unsigned int L, float del, const void *taps2, const void *hist, const void *x, unsigned long long n,
-                 void *y, unsigned long long nout, const lqk_rs4_hb *hb, void *stream);
+                 void *y, unsigned long long nout, const lqk_rs4_hb *hb, const lqk_hist_job *job, void *stream);
 /* firpfb_execute(i): y = scale * sum_n hpoly[i*L + n] win[L-1-n] (win: L samples, oldest first) */
 void lqk_firpfb_single(int kind, const void *hpoly, unsigned int L, unsigned int i, const void *win,
                        float scale_re, float scale_im, void *y, unsigned *flag, unsigned seq, void *stream);

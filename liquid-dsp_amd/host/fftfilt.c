@@ -133,12 +133,11 @@ static void lq_fftf_block_dev(lq_fftf *q, const void *dx, unsigned long long n, 
     }
     const unsigned int hm1 = q->h_len - 1;
     void *hold = q->d_hist[q->cur], *hnew = q->d_hist[q->cur ^ 1];
+    /* the transform kernel also writes the next history (no launch of its own) */
+    const lqk_hist_job job = {hold, x, n, hnew, hm1};
     lqk_fftfilt_run(q->kind == LQ_RRRF, q->h_len, q->nfft, q->d_H, hold, x, n, dy, q->sre, q->sim, NULL, 0, NULL,
-                    q->ctx.stream);
-    if (hm1) {
-        lqk_window_append(q->kind != LQ_RRRF, hold, hm1, x, n, hnew, q->ctx.stream);
-        q->cur ^= 1;
-    }
+                    hm1 ? &job : NULL, q->ctx.stream);
+    if (hm1) q->cur ^= 1;
 }
 
 /* small-call mode: one short call (n h_len <= LQ_FFTF_HOST_MACS) on the host

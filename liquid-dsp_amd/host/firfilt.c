@@ -270,8 +270,8 @@ void lq_firfilt_execute_block_dev(lq_firfilt *q, const void *dx, unsigned long l
     lq_firfilt_need_dev(q);
     void *wold = q->d_win[q->cur];
     void *wnew = q->d_win[q->cur ^ 1];
-    lqk_window_append(q->kind != LQ_RRRF, wold, q->HP, dx, n, wnew, q->ctx.stream);
     if (q->d_H8 && n >= LQ_FIR_FFT_MIN_N) {
+        lqk_window_append(q->kind != LQ_RRRF, wold, q->HP, dx, n, wnew, q->ctx.stream);
         const void *x = dx;
         if (dx == dy) {   /* segments read overlapping halos: filter a copy */
             void *c = lq_devbuf_get(&q->scratch, (size_t)n * q->esz);
@@ -282,14 +282,16 @@ void lq_firfilt_execute_block_dev(lq_firfilt *q, const void *dx, unsigned long l
         const void *hist = (const char *)wold + (size_t)(q->HP - (q->hlen - 1)) * q->esz;
         void *fl = lq_devbuf_get(&q->flags, lqk_fftfilt_flag_bytes(q->hlen, q->fft_n, n));
         lqk_fftfilt_run(0, q->hlen, q->fft_n, q->d_H8, hist, x, n, dy, q->d.scale_re, q->d.scale_im,
-                        (const float *)q->d_hpad, q->kind == LQ_CCCF ? 2 : 1, fl, q->ctx.stream);
+                        (const float *)q->d_hpad, q->kind == LQ_CCCF ? 2 : 1, fl, NULL, q->ctx.stream);
         q->cur ^= 1;
         q->host_valid = 0;
         return;
     }
     void *scr = NULL;
     if (dx == dy) scr = lq_devbuf_get(&q->scratch, lqk_firfilt_scratch_bytes(&q->d, n));
-    lqk_firfilt(&q->d, wold, dx, n, dy, scr, q->ctx.stream);
+    /* the window update: inside the matrix-core kernel, else launched first */
+    const lqk_hist_job job = {wold, dx, n, wnew, q->HP};
+    lqk_firfilt(&q->d, wold, dx, n, dy, scr, &job, q->ctx.stream);
     q->cur ^= 1;
     q->host_valid = 0;
 }

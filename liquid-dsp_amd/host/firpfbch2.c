@@ -132,10 +132,14 @@ void firpfbch2_crcf_execute_block_dev(firpfbch2_crcf _q, const liquid_float_comp
     if (_nblocks == 0) return;
     if (_q->type == LIQUID_ANALYZER) {
         void *hold = _q->d_hist[_q->cur], *hnew = _q->d_hist[_q->cur ^ 1];
-        if (!lqk_firpfbch2_analyzer_fast(_q->M, _q->m, _q->d_hsub_s, hold, _dx, _nblocks, _q->flag, _dy,
-                                         _q->ctx.stream))
+        const unsigned long long nin = _nblocks * (_q->M / 2);
+        /* the fast kernel also writes the next history (no launch of its own) */
+        const lqk_hist_job job = {hold, _dx, nin, hnew, _q->HL};
+        if (!lqk_firpfbch2_analyzer_fast(_q->M, _q->m, _q->d_hsub_s, hold, _dx, _nblocks, _q->flag, _dy, &job,
+                                         _q->ctx.stream)) {
             lqk_firpfbch2_analyzer(_q->M, _q->m, _q->d_hsub, hold, _dx, _nblocks, _q->flag, _dy, _q->ctx.stream);
-        lqk_window_append(1, hold, _q->HL, _dx, _nblocks * (_q->M / 2), hnew, _q->ctx.stream);
+            lqk_window_append(1, hold, _q->HL, _dx, nin, hnew, _q->ctx.stream);
+        }
         _q->cur ^= 1;
     } else {
         size_t zb = (size_t)(4 * _q->m - 1 + _nblocks) * _q->M * 8;

@@ -862,15 +862,17 @@ void lq_rs_block_dev_hb(lq_rs *_q, const void *_dxv, unsigned long long _nx, voi
                 kh.hist_new1 = hb->w[c0 ^ 1][1];
                 *hb->cur = c0 ^ 1;
             }
+            /* the kernel also writes the next history (no launch of its own) */
+            const lqk_hist_job job = {hold, _dx, c, hnew, _q->L};
             lqk_resamp4(&kp, _q->gpos, K0, _q->npfb, _q->L, _q->del, _q->d_taps2, hold, _dx, c, uy, nk,
-                        fuse ? &kh : NULL, _q->ctx.stream);
+                        fuse ? &kh : NULL, &job, _q->ctx.stream);
         } else {
             lqk_rs_plan kp = {_q->pl.d_tab.p, _q->pl.pre, _q->pl.P, _q->pl.Q, _q->pl.end, rs_p2(_q)};
             lqk_resamp(_q->kind == LQ_RRRF, &kp, _q->gpos, K0, _q->npfb, _q->L, _q->del, _q->d_taps, _q->d_taps2,
                        hold, _dx, c, uy, nk, _q->ctx.stream);
         }
         if (hb && !fuse && nk > 0) hb->run(hb->ctx, uy, nk, _dy);
-        lqk_window_append(_q->kind != LQ_RRRF, hold, _q->L, _dx, c, hnew, _q->ctx.stream);
+        if (_q->pl.dk != RS_D4) lqk_window_append(_q->kind != LQ_RRRF, hold, _q->L, _dx, c, hnew, _q->ctx.stream);
         _q->cur ^= 1;
         _q->gpos += c;
         _dx += c * _q->esz;
