@@ -1495,6 +1495,12 @@ def test_channelizer_launch_chunk_boundary(which):
     y2 = np.concatenate([q.execute_block(x[: cut * per]), q.execute_block(x[cut * per:])])
     assert y1.shape == y2.shape
     assert np.array_equal(y1, y2)
+    # a call of several launches, then a short one: the history the first
+    # call's kernel writes (on its first launch, from the whole call) carries
+    cut2 = nb - 70
+    q3 = make()
+    y3 = np.concatenate([q3.execute_block(x[: cut2 * per]), q3.execute_block(x[cut2 * per:])])
+    assert np.array_equal(y1, y3)
 
 
 @pytest.mark.parametrize("t", ["crcf", "cccf"])
@@ -1541,3 +1547,8 @@ def test_fftfilt_launch_chunk_boundary():
     q = LQ.FftFilt(h, 2048)
     y2 = np.concatenate([q.execute_block(x[:cut]), q.execute_block(x[cut:])])
     assert G.nrm_err(y1, y2) < 1e-6
+    # a two-launch call, then a short one (the history from the first call)
+    q3 = LQ.FftFilt(h, 2048)
+    cut2 = n - 4001
+    y3 = np.concatenate([q3.execute_block(x[:cut2]), q3.execute_block(x[cut2:])])
+    assert G.nrm_err(y1, y3) < 1e-6
