@@ -528,6 +528,55 @@ __global__ __launch_bounds__(NT, 1) void k_pfb_an1024(const float2 *hist, const 
     }
 }
 
+// ---------------------------------------------------------------- firpfbch2 analyzer, a few blocks
+// Calls of at most 16 blocks (the reference's execute() is one): the
+// streaming kernel above would compute a whole 16-block group after an
+// 8-row warm-up for them.  Here lane j forms X_b[j] of every block of the
+// call straight from the closed form (the history's last HL samples, then
+// x; taps pre-scaled by 1/M), and wave b transforms block b -- one launch,
+// which also writes the next history and, into pinned host memory, raises
+// the call's completion flag.
+template <int L>
+__global__ __launch_bounds__(NT, 1) void k_pfb2_an1024_few(const float *__restrict__ hsub,
+                                                           const float2 *__restrict__ hist,
+                                                           const float2 *__restrict__ x, int nb, int p0, float2 *Y,
+                                                           unsigned *flag, unsigned seq, lqk_hist_job hj,
+                                                           const float2 *__restrict__ tw4096)
+{
+    __shared__ __attribute__((aligned(16))) float2 xb[16 * BSTR];
+    __shared__ __attribute__((aligned(16))) float2 tw1[16 * 64];
+    __shared__ __attribute__((aligned(16))) float2 tw2[16 * 4];
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    lq_hist_job_run<float2>(hj);
+    fft1k_tables<-1>(tw1, tw2, tw4096, tid);
+    constexpr int HL = L * M - M2;
+    const int j = tid;
+    const int base = j < M2 ? (M2 - 1 - j) : (3 * M2 - 1 - j);
+    for (int b = 0; b < nb; b++) {   // firpfbch2.c:244-282 in closed form (k_channelizer.hip, k_pfb2_an)
+        const int bt = p0 + b;
+        const int i = (j - (bt & 1) * M2) & (M - 1);
+        const int c = j < M2 ? (bt >> 1) : ((bt - 1) >> 1);
+        const int t0 = c * M + base - p0 * M2;
+        float2 acc = make_float2(0.f, 0.f);
+#pragma unroll
+        for (int n = 0; n < L; n++) {
+            const int t = t0 - n * M;
+            const float2 v = t < 0 ? hist[HL + t] : x[t];
+            const float h = hsub[i * L + n];
+            acc.x = fmaf(h, v.x, acc.x);
+            acc.y = fmaf(h, v.y, acc.y);
+        }
+        xb[b * BSTR + j] = acc;
+    }
+    __syncthreads();
+    if (wave < nb) fft1k_wave_store<-1>(xb + wave * BSTR, tw1, tw2, lane, Y + (long long)wave * M);
+    if (flag) {   // Y is pinned host memory: the completion flag once every store is visible
+        __threadfence_system();
+        __syncthreads();
+        if (tid == 0) __hip_atomic_store(flag, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
+}
+
 // ---------------------------------------------------------------- firpfbch synthesizer
 // firpfbch.c:314-336 mirrored: Z_b = IFFT(X_b) (unnormalised), y_b[i] =
 // sum_{n<P} h[i P + n] Z_{b-n}[i].  Per iteration the 16 waves transform 16
@@ -721,7 +770,7 @@ __global__ __launch_bounds__(NT, 1) void k_pfb2_syn1024(const float2 *__restrict
 // their history straight from the preceding input.
 extern "C" int lqk_firpfbch2_analyzer_fast(unsigned int Mch, unsigned int m, const void *hsub, const void *hist,
                                            const void *x, unsigned long long nblocks, long long B0, void *Y,
-                                           const lqk_hist_job *job, void *stream)
+                                           const lqk_hist_job *job, unsigned *flag, unsigned seq, void *stream)
 {
     if (Mch != (unsigned)M || !(m == 4 || m == 2)) return 0;
     // x / hist: 8-byte sample loads; Y: 16-byte (two-bin) non-temporal stores
@@ -729,8 +778,23 @@ extern "C" int lqk_firpfbch2_analyzer_fast(unsigned int Mch, unsigned int m, con
     if (nblocks == 0) return 1;
     hipStream_t st = (hipStream_t)stream;
     const float2 *tw = (const float2 *)lqrt_twiddles();
+    if (nblocks <= 16) {   // a few blocks: one workgroup, no warm-up rows
+        const lqk_hist_job hj = job ? *job : lqk_hist_job{nullptr, nullptr, 0ull, nullptr, 0u};
+        const int p0 = (int)(B0 & 1);
+        if (m == 4)
+            hipLaunchKernelGGL((k_pfb2_an1024_few<8>), dim3(1), dim3(NT), 0, st, (const float *)hsub,
+                               (const float2 *)hist, (const float2 *)x, (int)nblocks, p0, (float2 *)Y, flag, seq, hj,
+                               tw);
+        else
+            hipLaunchKernelGGL((k_pfb2_an1024_few<4>), dim3(1), dim3(NT), 0, st, (const float *)hsub,
+                               (const float2 *)hist, (const float2 *)x, (int)nblocks, p0, (float2 *)Y, flag, seq, hj,
+                               tw);
+        LQ_CHECK_LAUNCH();
+        return 1;
+    }
     const long long HL = 2LL * m * M - M2;
     const long long CH = 1LL << 18;
+    if (flag) return 0;   // (the signalling form is the few-block kernel's)
     for (long long ob = 0; ob < (long long)nblocks; ob += CH) {
         const long long nb = ((long long)nblocks - ob) < CH ? ((long long)nblocks - ob) : CH;
         Params P;

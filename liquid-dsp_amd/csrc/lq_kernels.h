@@ -144,10 +144,13 @@ int lqk_firpfbch2_synthesizer_fast(unsigned int M, unsigned int m, const void *h
 /* batched transforms with the two sequential output scales of fft_batch_scaled (k_channelizer.hip) */
 void lqk_fft_batch_scaled(unsigned int n, int dir, const void *x, void *y, unsigned long long batch, float s1,
                           float s2, void *stream);
-/* job (NULL: none) is done only when the call is handled (returns 1) */
+/* job (NULL: none) is done only when the call is handled (returns 1).
+ * flag (NULL: none): Y is pinned host memory, and the kernel raises *flag =
+ * seq (system scope) once Y is visible to the host -- for calls that take a
+ * single workgroup (a few blocks), else 0 is returned before any launch */
 int lqk_firpfbch2_analyzer_fast(unsigned int M, unsigned int m, const void *hsub, const void *hist,
                                 const void *x, unsigned long long nblocks, long long B0, void *Y,
-                                const lqk_hist_job *job, void *stream);
+                                const lqk_hist_job *job, unsigned *flag, unsigned seq, void *stream);
 /* synthesizer: nblocks x M channel inputs -> nblocks x M/2 outputs.
  * state: the previous 4m-1 IFFT vectors (M each), zscratch (4m-1+nblocks)*M;
  * see csrc/k_channelizer.hip */

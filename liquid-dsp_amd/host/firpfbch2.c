@@ -126,20 +126,31 @@ void firpfbch2_crcf_print(firpfbch2_crcf _q)
     printf("    semi-length :   %u\n", _q->m);
 }
 
+/* the analyzer on the fast kernel (M = 1024), which also writes the next
+ * history; flag (NULL: none): y is pinned host memory and the kernel raises
+ * the call's completion flag.  0: not handled, nothing launched */
+static int firpfbch2_an_fast(firpfbch2_crcf _q, const void *_dx, unsigned long long _nblocks, void *_dy,
+                             unsigned *flag, unsigned seq)
+{
+    void *hold = _q->d_hist[_q->cur], *hnew = _q->d_hist[_q->cur ^ 1];
+    const lqk_hist_job job = {hold, _dx, _nblocks * (_q->M / 2), hnew, _q->HL};
+    if (!lqk_firpfbch2_analyzer_fast(_q->M, _q->m, _q->d_hsub_s, hold, _dx, _nblocks, _q->flag, _dy, &job, flag, seq,
+                                     _q->ctx.stream))
+        return 0;
+    _q->cur ^= 1;
+    _q->flag = (int)((_q->flag + _nblocks) & 1);
+    return 1;
+}
+
 void firpfbch2_crcf_execute_block_dev(firpfbch2_crcf _q, const liquid_float_complex *_dx,
                                       unsigned long long _nblocks, liquid_float_complex *_dy)
 {
     if (_nblocks == 0) return;
     if (_q->type == LIQUID_ANALYZER) {
+        if (firpfbch2_an_fast(_q, _dx, _nblocks, _dy, NULL, 0)) return;
         void *hold = _q->d_hist[_q->cur], *hnew = _q->d_hist[_q->cur ^ 1];
-        const unsigned long long nin = _nblocks * (_q->M / 2);
-        /* the fast kernel also writes the next history (no launch of its own) */
-        const lqk_hist_job job = {hold, _dx, nin, hnew, _q->HL};
-        if (!lqk_firpfbch2_analyzer_fast(_q->M, _q->m, _q->d_hsub_s, hold, _dx, _nblocks, _q->flag, _dy, &job,
-                                         _q->ctx.stream)) {
-            lqk_firpfbch2_analyzer(_q->M, _q->m, _q->d_hsub, hold, _dx, _nblocks, _q->flag, _dy, _q->ctx.stream);
-            lqk_window_append(1, hold, _q->HL, _dx, nin, hnew, _q->ctx.stream);
-        }
+        lqk_firpfbch2_analyzer(_q->M, _q->m, _q->d_hsub, hold, _dx, _nblocks, _q->flag, _dy, _q->ctx.stream);
+        lqk_window_append(1, hold, _q->HL, _dx, _nblocks * (_q->M / 2), hnew, _q->ctx.stream);
         _q->cur ^= 1;
     } else {
         size_t zb = (size_t)(4 * _q->m - 1 + _nblocks) * _q->M * 8;
@@ -157,6 +168,17 @@ void firpfbch2_crcf_execute_block(firpfbch2_crcf _q, liquid_float_complex *_x, u
     size_t nin = (size_t)_nblocks * (_q->type == LIQUID_ANALYZER ? _q->M / 2 : _q->M);
     size_t nout = (size_t)_nblocks * (_q->type == LIQUID_ANALYZER ? _q->M : _q->M / 2);
     const void *dx = lq_call_in(&_q->ctx, &_q->xbuf, _x, nin * 8);
+    if (_q->type == LIQUID_ANALYZER && nout * 8 <= LQRT_COPYOUT_MAX) {
+        /* a few blocks (the reference's execute() is one): the kernel writes
+         * the pinned output buffer and raises the completion flag itself --
+         * one launch per call, no copy-out kernel */
+        unsigned *flag, seq;
+        void *py = lq_sig_out(&_q->ctx, nout * 8, &flag, &seq);
+        if (firpfbch2_an_fast(_q, dx, _nblocks, py, flag, seq)) {
+            lq_sig_wait(&_q->ctx, _y, nout * 8, seq);
+            return;
+        }
+    }
     void *dy = lq_devbuf_get(&_q->ybuf, nout * 8);
     firpfbch2_crcf_execute_block_dev(_q, (const liquid_float_complex *)dx, _nblocks, (liquid_float_complex *)dy);
     lq_call_out(&_q->ctx, _y, dy, nout * 8);

@@ -346,6 +346,35 @@ def test_firpfbch2_analyzer_vs_oracle(M, m):
     assert G.nrm_err(y, o.execute_block(x)) < NRM
 
 
+@pytest.mark.parametrize("m", [2, 4])
+@pytest.mark.parametrize("dev", [False, True])
+def test_firpfbch2_m1024_few_block_calls(m, dev):
+    # M = 1024: calls of at most 16 blocks take k_pfb2_an1024_few (the
+    # per-call API's path; host-pointer calls of up to 8 blocks also raise
+    # the completion flag from the kernel), longer ones the streaming kernel;
+    # mixed on one object, both block parities, against the oracle
+    M = 1024
+    r = rng(400 + m + dev)
+    sizes = [1, 1, 2, 3, 16, 17, 1, 5, 8, 9, 100, 1, 15, 2]
+    nb = sum(sizes)
+    x = cx(r, nb * M // 2)
+    g = LQ.FirPfbch2(LQ.LIQUID_ANALYZER, M, m, 60.0)
+    o = O.FirPfbch2(O.ANALYZER, M, m, 60.0)
+    ys, a = [], 0
+    for k in sizes:
+        xs = x[a * M // 2:(a + k) * M // 2]
+        if dev:
+            dx = LQ.DeviceBuffer.from_array(xs)
+            dy = LQ.DeviceBuffer(k * M * 8)
+            g.execute_block_dev(dx.p, k, dy.p)
+            g.synchronize()
+            ys.append(dy.to_array(np.complex64, k * M))
+        else:
+            ys.append(g.execute_block(xs))
+        a += k
+    assert G.nrm_err(np.concatenate(ys), o.execute_block(x)) < NRM
+
+
 @pytest.mark.parametrize("M,m", [(64, 4), (128, 1), (256, 4), (512, 3), (1024, 5), (2048, 4), (4096, 6), (256, 8)])
 def test_firpfbch2_analyzer_polyphase_pass_vs_oracle(M, m):
     # power-of-two M other than the fused M=1024/m=4 path: polyphase pass
