@@ -577,6 +577,45 @@ __global__ __launch_bounds__(NT, 1) void k_pfb2_an1024_few(const float *__restri
     }
 }
 
+// firpfbch analyzer, M = 1024, p in {4, 8}, calls of at most 16 blocks: as
+// k_pfb2_an1024_few, X_b[j] = sum_n h[(M-1-j) p + n] x[(b-n) M + j]
+// (firpfbch.c:346-409), wave b's forward transform of block b.  One
+// workgroup reads all of x before any store, so the call may run in place.
+template <int P>
+__global__ __launch_bounds__(NT, 1) void k_pfb_an1024_few(const float *__restrict__ hsub,
+                                                          const float2 *__restrict__ hist, const float2 *x, int nb,
+                                                          float2 *Y, unsigned *flag, unsigned seq, lqk_hist_job hj,
+                                                          const float2 *__restrict__ tw4096)
+{
+    __shared__ __attribute__((aligned(16))) float2 xb[16 * BSTR];
+    __shared__ __attribute__((aligned(16))) float2 tw1[16 * 64];
+    __shared__ __attribute__((aligned(16))) float2 tw2[16 * 4];
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    lq_hist_job_run<float2>(hj);
+    fft1k_tables<+1>(tw1, tw2, tw4096, tid);
+    constexpr int HL = (P - 1) * M;
+    const int j = tid;
+    for (int b = 0; b < nb; b++) {
+        float2 acc = make_float2(0.f, 0.f);
+#pragma unroll
+        for (int n = 0; n < P; n++) {
+            const int t = (b - n) * M + j;
+            const float2 v = t < 0 ? hist[HL + t] : x[t];
+            const float h = hsub[(M - 1 - j) * P + n];
+            acc.x = fmaf(h, v.x, acc.x);
+            acc.y = fmaf(h, v.y, acc.y);
+        }
+        xb[b * BSTR + j] = acc;
+    }
+    __syncthreads();   // (every read of x is done: in-place calls are safe)
+    if (wave < nb) fft1k_wave_store<+1>(xb + wave * BSTR, tw1, tw2, lane, Y + (long long)wave * M);
+    if (flag) {   // Y is pinned host memory: the completion flag once every store is visible
+        __threadfence_system();
+        __syncthreads();
+        if (tid == 0) __hip_atomic_store(flag, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
+}
+
 // ---------------------------------------------------------------- firpfbch synthesizer
 // firpfbch.c:314-336 mirrored: Z_b = IFFT(X_b) (unnormalised), y_b[i] =
 // sum_{n<P} h[i P + n] Z_{b-n}[i].  Per iteration the 16 waves transform 16
@@ -870,6 +909,29 @@ extern "C" int lqk_firpfbch_analyzer_fast(int ctaps, unsigned int Mch, unsigned 
                                (const float *)hsub, tw, (float2 *)Y + ob * M, zero);
         LQ_CHECK_LAUNCH();
     }
+    return 1;
+}
+
+// firpfbch_crcf analyzer, M = 1024, p in {4, 8}, calls of at most 16
+// blocks: one workgroup (k_pfb_an1024_few), which also does the history job
+// and, with a flag, raises it once Y (pinned host memory) is written.
+// Returns 0 (nothing launched) when the call does not qualify.
+extern "C" int lqk_firpfbch_analyzer_few(int ctaps, unsigned int Mch, unsigned int p, const void *hsub,
+                                         const void *hist, const void *x, unsigned long long nblocks, void *Y,
+                                         const lqk_hist_job *job, unsigned *flag, unsigned seq, void *stream)
+{
+    if (ctaps || Mch != (unsigned)M || !(p == 8 || p == 4) || nblocks == 0 || nblocks > 16) return 0;
+    if (((uintptr_t)x & 7) || ((uintptr_t)hist & 7) || ((uintptr_t)Y & 15)) return 0;
+    hipStream_t st = (hipStream_t)stream;
+    const float2 *tw = (const float2 *)lqrt_twiddles();
+    const lqk_hist_job hj = job ? *job : lqk_hist_job{nullptr, nullptr, 0ull, nullptr, 0u};
+    if (p == 8)
+        hipLaunchKernelGGL((k_pfb_an1024_few<8>), dim3(1), dim3(NT), 0, st, (const float *)hsub, (const float2 *)hist,
+                           (const float2 *)x, (int)nblocks, (float2 *)Y, flag, seq, hj, tw);
+    else
+        hipLaunchKernelGGL((k_pfb_an1024_few<4>), dim3(1), dim3(NT), 0, st, (const float *)hsub, (const float2 *)hist,
+                           (const float2 *)x, (int)nblocks, (float2 *)Y, flag, seq, hj, tw);
+    LQ_CHECK_LAUNCH();
     return 1;
 }
 

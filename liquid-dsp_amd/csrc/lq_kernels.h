@@ -162,6 +162,12 @@ void lqk_firpfbch2_synthesizer(unsigned int M, unsigned int m, const void *hsub_
  * analyzer: block b consumes x[bM .. bM+M); window i receives x[bM + M-1-i]
  * X[M-1-i] = sum_n h[i + n*M] win_i, Y = FFT_forward(X).  hsub[i*p + n] = h[i+n*M];
  * ctaps: hsub holds complex taps (cccf), else real (crcf) */
+/* firpfbch analyzer M = 1024 (crcf, p in {4, 8}), calls of <= 16 blocks in
+ * one workgroup, with the history job and, optionally, the completion flag
+ * (Y pinned host memory; see lqk_firpfbch2_analyzer_fast); 0: not handled */
+int lqk_firpfbch_analyzer_few(int ctaps, unsigned int M, unsigned int p, const void *hsub, const void *hist,
+                              const void *x, unsigned long long nblocks, void *Y, const lqk_hist_job *job,
+                              unsigned *flag, unsigned seq, void *stream);
 void lqk_firpfbch_analyzer(int ctaps, unsigned int M, unsigned int p, const void *hsub, const void *hist,
                            const void *x, unsigned long long nblocks, void *Y, void *stream);
 void lqk_firpfbch_synthesizer(int ctaps, unsigned int M, unsigned int p, const void *hsub, void *state,

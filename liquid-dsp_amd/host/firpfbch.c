@@ -152,11 +152,28 @@ static void lq_pfbch_print(lq_pfbch *q)
     }
 }
 
+/* the analyzer's few-block kernel (M = 1024, crcf): one launch that also
+ * writes the next history and, with flag, raises the call's completion flag
+ * (dy pinned host memory); 0: not handled, nothing launched */
+static int lq_pfbch_an_few(lq_pfbch *q, const void *dx, unsigned long long nblocks, void *dy, unsigned *flag,
+                           unsigned seq)
+{
+    const unsigned int HL = (q->p - 1) * q->M;
+    void *hold = q->d_hist[q->cur], *hnew = q->d_hist[q->cur ^ 1];
+    const lqk_hist_job job = {hold, dx, nblocks * q->M, hnew, HL};
+    if (!lqk_firpfbch_analyzer_few(q->kind == LQ_CCCF, q->M, q->p, q->d_hsub, hold, dx, nblocks, dy, HL ? &job : NULL,
+                                   flag, seq, q->ctx.stream))
+        return 0;
+    if (HL) q->cur ^= 1;
+    return 1;
+}
+
 static void lq_pfbch_block_dev(lq_pfbch *q, const void *dx, unsigned long long nblocks, void *dy)
 {
     if (nblocks == 0) return;
     const int ctaps = q->kind == LQ_CCCF;
     if (q->type == LIQUID_ANALYZER) {
+        if (lq_pfbch_an_few(q, dx, nblocks, dy, NULL, 0)) return;
         void *hold = q->d_hist[q->cur], *hnew = q->d_hist[q->cur ^ 1];
         const unsigned int HL = (q->p - 1) * q->M;
         if (HL) lqk_window_append(1, hold, HL, dx, nblocks * q->M, hnew, q->ctx.stream);
@@ -173,6 +190,16 @@ static void lq_pfbch_block(lq_pfbch *q, const void *x, unsigned long long nblock
     if (nblocks == 0) return;
     size_t bytes = (size_t)nblocks * q->M * 8;
     const void *dx = lq_call_in(&q->ctx, &q->xbuf, x, bytes);
+    if (q->type == LIQUID_ANALYZER && bytes <= LQRT_COPYOUT_MAX) {
+        /* a few blocks (the reference's execute() is one): the kernel writes
+         * the pinned output buffer and raises the completion flag itself */
+        unsigned *flag, seq;
+        void *py = lq_sig_out(&q->ctx, bytes, &flag, &seq);
+        if (lq_pfbch_an_few(q, dx, nblocks, py, flag, seq)) {
+            lq_sig_wait(&q->ctx, y, bytes, seq);
+            return;
+        }
+    }
     void *dy = lq_devbuf_get(&q->ybuf, bytes);
     lq_pfbch_block_dev(q, dx, nblocks, dy);
     lq_call_out(&q->ctx, y, dy, bytes);

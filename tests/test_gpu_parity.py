@@ -644,6 +644,37 @@ def test_firpfbch_m256_512_long_stream(typ, M, m):
     assert G.nrm_err(y, ref) < NRM
 
 
+@pytest.mark.parametrize("m", [2, 4])
+@pytest.mark.parametrize("mode", ["host", "dev", "inplace"])
+def test_firpfbch_m1024_few_block_calls(m, mode):
+    # M = 1024 crcf: calls of at most 16 blocks take k_pfb_an1024_few (host
+    # calls of up to 8 blocks raise the completion flag from the kernel),
+    # longer ones the streaming kernel; mixed on one object against the
+    # oracle, device calls also in place
+    M = 1024
+    r = rng(500 + m + len(mode))
+    sizes = [1, 1, 2, 3, 16, 17, 1, 5, 8, 9, 40, 1, 15]
+    nb = sum(sizes)
+    x = cx(r, nb * M)
+    g = LQ.FirPfbch(LQ.LIQUID_ANALYZER, M, m=m, As=60.0)
+    o = O.FirPfbch(O.ANALYZER, M, m=m, As=60.0)
+    ys, a = [], 0
+    for k in sizes:
+        xs = x[a * M:(a + k) * M]
+        if mode == "host":
+            ys.append(g.execute_block(xs))
+        else:
+            dx = LQ.DeviceBuffer.from_array(xs)
+            dy = dx if mode == "inplace" else LQ.DeviceBuffer(k * M * 8)
+            LQ.lib().firpfbch_crcf_execute_block_dev(g.q, dx.p, k, dy.p)
+            LQ.lib().liquid_mi355x_device_synchronize()
+            ys.append(dy.to_array(np.complex64, k * M))
+        a += k
+    ref = o.execute_block(x) if hasattr(o, "execute_block") else \
+        np.concatenate([o.execute(x[b * M:(b + 1) * M]) for b in range(nb)])
+    assert G.nrm_err(np.concatenate(ys), ref) < NRM
+
+
 @pytest.mark.parametrize("M,m", [(64, 1), (64, 4), (128, 3), (128, 8)])
 def test_firpfbch_analyzer_small_m_long_stream(M, m):
     # the fused M = 64 / 128 analyzer (k_pfb_an_small: several column sets per
