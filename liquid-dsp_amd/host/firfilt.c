@@ -30,7 +30,8 @@ struct lq_firfilt_s {
     void *d_H8;        /* long complex filters: the overlap-save path's spectrum (else NULL) */
     unsigned int fft_n; /* its transform size (lqk_fftfilt_nfft) */
     int cur;
-    unsigned char *h_win; /* host mirror */
+    unsigned char *h_win; /* host mirror: the window is HP samples at h_win + hoff * esz, */
+    size_t hoff;          /* pushes append after it (capacity LQ_FIR_HCAP windows) */
     int host_valid, dev_valid;
     lq_ctx ctx;
     lq_devbuf xbuf, ybuf, scratch, one, flags;
@@ -40,6 +41,7 @@ struct lq_firfilt_s {
 /* longer complex filters take the overlap-save path (crcf past 128 taps: at
  * 65..128 the matrix-core band is as fast, 0.49-0.50 vs 0.51 ms per 2^27
  * samples at h = 128; cccf past 64, where its matrix-core kernel stops) ... */
+#define LQ_FIR_HCAP 8   /* host window buffer, in windows: a memmove every 7 HP pushes */
 #define LQ_FIR_FFT_MIN_TAPS(kind) ((kind) == LQ_CRCF ? 128u : 64u)
 #define LQ_FIR_FFT_MIN_N 8192ull    /* ... on device blocks of at least this many samples */
 
@@ -73,8 +75,9 @@ static void lq_firfilt_alloc_state(lq_firfilt *q)
     q->d_win[0] = lqrt_malloc((size_t)q->HP * q->esz);
     q->d_win[1] = lqrt_malloc((size_t)q->HP * q->esz);
     /* pinned: the per-sample execute() reads it in place (zero copy) */
-    q->h_win = (unsigned char *)lqrt_host_alloc((size_t)q->HP * q->esz);
+    q->h_win = (unsigned char *)lqrt_host_alloc((size_t)LQ_FIR_HCAP * q->HP * q->esz);
     memset(q->h_win, 0, (size_t)q->HP * q->esz);
+    q->hoff = 0;
     q->cur = 0;
     q->host_valid = q->dev_valid = 1;
 }
@@ -184,6 +187,7 @@ void lq_firfilt_reset(lq_firfilt *q)
     lqrt_memset(q->d_win[0], (size_t)q->HP * q->esz, q->ctx.stream);
     lqrt_memset(q->d_win[1], (size_t)q->HP * q->esz, q->ctx.stream);
     lqrt_sync(q->ctx.stream);
+    q->hoff = 0;
     memset(q->h_win, 0, (size_t)q->HP * q->esz);
     q->host_valid = q->dev_valid = 1;
 }
@@ -213,6 +217,7 @@ void lq_firfilt_set_scale(lq_firfilt *q, float re, float im)
 static void lq_firfilt_need_host(lq_firfilt *q)
 {
     if (q->host_valid) return;
+    q->hoff = 0;
     lqrt_d2h(q->h_win, q->d_win[q->cur], (size_t)q->HP * q->esz, q->ctx.stream);
     lqrt_sync(q->ctx.stream);
     q->host_valid = 1;
@@ -221,15 +226,23 @@ static void lq_firfilt_need_host(lq_firfilt *q)
 static void lq_firfilt_need_dev(lq_firfilt *q)
 {
     if (q->dev_valid) return;
-    lqrt_h2d(q->d_win[q->cur], q->h_win, (size_t)q->HP * q->esz, q->ctx.stream);
+    lqrt_h2d(q->d_win[q->cur], q->h_win + q->hoff * q->esz, (size_t)q->HP * q->esz, q->ctx.stream);
     q->dev_valid = 1;
 }
 
 void lq_firfilt_push(lq_firfilt *q, const void *x)
 {
     lq_firfilt_need_host(q);
-    memmove(q->h_win, q->h_win + q->esz, (size_t)(q->HP - 1) * q->esz);
-    memcpy(q->h_win + (size_t)(q->HP - 1) * q->esz, x, q->esz);
+    /* append after the window; the window moves up one sample, and only
+     * when the buffer is full do its last HP-1 samples move back to the
+     * start (the reference's window.c does the same with its 2^k + len - 1
+     * buffer) */
+    if (q->hoff + q->HP == (size_t)LQ_FIR_HCAP * q->HP) {
+        memmove(q->h_win, q->h_win + (q->hoff + 1) * q->esz, (size_t)(q->HP - 1) * q->esz);
+        q->hoff = (size_t)-1;
+    }
+    memcpy(q->h_win + (q->hoff + q->HP) * q->esz, x, q->esz);
+    q->hoff++;
     q->dev_valid = 0;
 }
 
@@ -243,7 +256,7 @@ void lq_firfilt_execute(lq_firfilt *q, void *y)
     if (lq_small_host()) {   /* opt-in host path (lq_small.c): the window's newest sample is h_win[HP-1] */
         lq_firfilt_need_host(q);
         float v[2];
-        lq_host_conv(q->kind, q->h, q->h_win, q->HP - 1, q->hlen, v);
+        lq_host_conv(q->kind, q->h, q->h_win + q->hoff * q->esz, q->HP - 1, q->hlen, v);
         if (q->kind == LQ_RRRF) {
             *(float *)y = v[0] * q->d.scale_re;
         } else if (q->kind == LQ_CRCF) {   /* firfilt.c:337: real scale per component */
@@ -255,7 +268,7 @@ void lq_firfilt_execute(lq_firfilt *q, void *y)
         }
         return;
     }
-    const void *win = q->dev_valid ? q->d_win[q->cur] : (const void *)q->h_win;
+    const void *win = q->dev_valid ? q->d_win[q->cur] : (const void *)(q->h_win + q->hoff * q->esz);
     unsigned *flag, seq;
     void *py = lq_sig_out(&q->ctx, q->esz, &flag, &seq);
     lqk_fir_single(&q->d, win, py, flag, seq, q->ctx.stream);
