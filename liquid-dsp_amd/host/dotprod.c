@@ -15,6 +15,7 @@ struct lq_dotprod_s {
     unsigned int n;
     size_t csz, esz;
     float *h;
+    float *hg;   /* expanded for the host path (lq_host_taps) */
     void *d_h;
     lq_ctx ctx;
     lq_devbuf xbuf, ybuf;
@@ -26,6 +27,8 @@ static void lq_dotprod_set(lq_dotprod *q, const float *h, unsigned int n)
     free(q->h);
     q->h = (float *)lq_xmalloc((size_t)(n ? n : 1) * q->csz);
     if (n) memcpy(q->h, h, (size_t)n * q->csz);
+    free(q->hg);
+    q->hg = lq_host_taps(q->kind, q->h, n, 0);
     if (q->d_h) lqrt_free(q->d_h);
     q->d_h = lqrt_malloc((size_t)(n ? n : 1) * q->csz + 16);
     lqrt_h2d(q->d_h, q->h, (size_t)n * q->csz, q->ctx.stream);
@@ -59,6 +62,7 @@ void lq_dotprod_destroy(lq_dotprod *q)
     lq_devbuf_free(&q->ybuf);
     lq_ctx_free(&q->ctx);
     free(q->h);
+    free(q->hg);
     free(q);
 }
 
@@ -93,7 +97,7 @@ void lq_dotprod_execute_batch(lq_dotprod *q, const void *X, unsigned long long n
 static void lq_dotprod_execute1(lq_dotprod *q, const void *x, void *y)
 {
     if (lq_small_host()) {   /* opt-in host path (lq_small.c) */
-        lq_host_dot(q->kind, q->h, x, q->n, y);
+        lq_host_tdot(q->kind, q->hg, x, q->n, y);
         return;
     }
     const void *dx = lq_call_in(&q->ctx, &q->xbuf, x, (size_t)q->n * q->esz);

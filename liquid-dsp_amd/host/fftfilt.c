@@ -31,6 +31,7 @@ typedef struct {
     unsigned int h_len, n;
     unsigned int nfft;  /* segment transform size (lqk_fftfilt_nfft); 0: direct */
     float *h;
+    float *hg;          /* reversed, expanded for the host path (lq_host_taps) */
     void *d_h, *d_H;
     void *d_hist[2];    /* previous h_len-1 inputs */
     int cur;
@@ -56,6 +57,7 @@ static lq_fftf *lq_fftf_create(int kind, const float *h, unsigned int h_len, uns
     q->n = n;
     q->h = (float *)lq_xmalloc(h_len * q->csz);
     memcpy(q->h, h, h_len * q->csz);
+    q->hg = lq_host_taps(kind, q->h, h_len, 1);
     lq_ctx_init(&q->ctx);
     q->d_h = lqrt_malloc(h_len * q->csz);
     q->nfft = lqk_fftfilt_nfft(kind == LQ_RRRF, h_len);
@@ -92,6 +94,7 @@ static void lq_fftf_destroy(lq_fftf *q)
     lq_devbuf_free(&q->cbuf);
     lq_ctx_free(&q->ctx);
     free(q->h);
+    free(q->hg);
     free(q);
 }
 
@@ -147,13 +150,13 @@ static void lq_fftf_block_dev(lq_fftf *q, const void *dx, unsigned long long n, 
 #define LQ_FFTF_HOST_MACS 65536u
 static void lq_fftf_exec_host(lq_fftf *q, const void *x, unsigned int n, void *y)
 {
-    const unsigned int hm1 = q->h_len - 1;
     lq_mirror_need_host(&q->hm, q->d_hist[q->cur], q->ctx.stream);
     lq_mirror_append(&q->hm, x, n);
     const unsigned char *w = lq_mirror_ptr(&q->hm);
     for (unsigned int t = 0; t < n; t++) {
         float *yt = (float *)((unsigned char *)y + (size_t)t * q->esz);
-        lq_host_conv(q->kind, q->h, w, hm1 + t, q->h_len, yt);
+        /* window samples t .. t + h_len - 1 (oldest first) against the reversed taps */
+        lq_host_tdot(q->kind, q->hg, w + (size_t)t * q->esz, q->h_len, yt);
         if (q->kind == LQ_RRRF) {
             yt[0] *= q->sre;
         } else if (q->kind == LQ_CRCF) {   /* real scale per component */

@@ -27,6 +27,7 @@ typedef struct {
     size_t esz, csz;
     unsigned int M, hlen;
     float *h;          /* host copy, hlen coefficients of csz bytes */
+    float *hg;         /* reversed, expanded for the host path (lq_host_taps) */
     lqk_fir_desc d;
     void *d_hpad;
     void *d_hq;        /* M x QC phase-major taps for the phase-layout kernel */
@@ -51,6 +52,7 @@ static lq_decim *lq_decim_create(int kind, unsigned int M, const float *h, unsig
     q->hlen = hlen;
     q->h = (float *)lq_xmalloc(hlen * q->csz);
     memcpy(q->h, h, hlen * q->csz);
+    q->hg = lq_host_taps(kind, q->h, hlen, 1);
     lq_ctx_init(&q->ctx);
     q->d_hpad = lqrt_malloc(hlen * q->csz);
     lqrt_h2d(q->d_hpad, q->h, hlen * q->csz, q->ctx.stream);
@@ -102,6 +104,7 @@ static void lq_decim_destroy(lq_decim *q)
     lq_ctx_free(&q->ctx);
     lq_mirror_free(&q->hm);
     free(q->h);
+    free(q->hg);
     free(q);
 }
 
@@ -142,7 +145,7 @@ static void lq_decim_exec1_host(lq_decim *q, const void *x, void *y)
 {
     lq_mirror_need_host(&q->hm, q->d_hist[q->cur], q->ctx.stream);
     lq_mirror_append(&q->hm, x, q->M);
-    lq_host_conv(q->kind, q->h, lq_mirror_ptr(&q->hm), q->hlen - 1, q->hlen, y);
+    lq_host_tdot(q->kind, q->hg, lq_mirror_ptr(&q->hm), q->hlen, y);   /* the hlen-sample window, oldest first */
     lq_mirror_commit(&q->hm, q->M);
 }
 
@@ -233,7 +236,9 @@ typedef struct {
     void *d_hpoly;     /* M x L: hpoly[p*L + l] = h'[p + l*M] */
     void *d_hist[2];   /* last L-1 inputs */
     int cur;
-    float *hpoly;      /* host copy of the M x L phase taps (small-call mode) */
+    float *hpoly;      /* host copy of the M x L phase taps */
+    float *hgp;        /* the phases reversed and expanded for the host path, hgs floats apart */
+    size_t hgs;
     lq_mirror hm;      /* host copy of the history (small-call mode) */
     lq_ctx ctx;
     lq_devbuf xbuf, ybuf;
@@ -267,6 +272,13 @@ static lq_interp *lq_interp_create(int kind, unsigned int M, const float *h, uns
     q->d_hist[1] = lqrt_malloc((size_t)q->L * q->esz);
     lqrt_sync(q->ctx.stream);
     q->hpoly = hp;
+    q->hgs = (size_t)q->L * (kind == LQ_RRRF ? 1 : (kind == LQ_CRCF ? 2 : 4));
+    q->hgp = (float *)lq_xmalloc((size_t)M * q->hgs * sizeof(float));
+    for (unsigned int p = 0; p < M; p++) {
+        float *g = lq_host_taps(kind, hp + cf * p * q->L, q->L, 1);
+        memcpy(q->hgp + p * q->hgs, g, q->hgs * sizeof(float));
+        free(g);
+    }
     lq_mirror_init(&q->hm, q->L - 1, q->esz);
     return q;
 }
@@ -293,6 +305,7 @@ static void lq_interp_destroy(lq_interp *q)
     lq_ctx_free(&q->ctx);
     lq_mirror_free(&q->hm);
     free(q->hpoly);
+    free(q->hgp);
     free(q->h);
     free(q);
 }
@@ -332,9 +345,8 @@ static void lq_interp_exec1_host(lq_interp *q, const void *x, void *y)
     lq_mirror_need_host(&q->hm, q->d_hist[q->cur], q->ctx.stream);
     lq_mirror_append(&q->hm, x, 1);
     const unsigned char *w = lq_mirror_ptr(&q->hm);
-    const size_t cf = q->csz / 4;
-    for (unsigned int p = 0; p < q->M; p++)
-        lq_host_conv(q->kind, q->hpoly + cf * p * q->L, w, q->L - 1, q->L, (unsigned char *)y + p * q->esz);
+    for (unsigned int p = 0; p < q->M; p++)   /* bank p over the L-sample window, oldest first */
+        lq_host_tdot(q->kind, q->hgp + p * q->hgs, w, q->L, (unsigned char *)y + p * q->esz);
     lq_mirror_commit(&q->hm, 1);
 }
 

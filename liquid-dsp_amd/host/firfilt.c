@@ -24,6 +24,7 @@ struct lq_firfilt_s {
     size_t esz;        /* sample size: 4 (rrrf) or 8 */
     size_t csz;        /* coefficient size: 4 or 8 (cccf) */
     float *h;          /* natural-order coefficients (host copy) */
+    float *hg;         /* reversed, expanded for the host path (lq_host_taps) */
     void *d_hpad;      /* device, zero padded to HP */
     lqk_fir_desc d;
     void *d_win[2];    /* device windows, HP samples each */
@@ -144,6 +145,7 @@ lq_firfilt *lq_firfilt_create(int kind, const float *h, unsigned int n, const ch
     lq_firfilt_layout(q, n);
     q->h = (float *)lq_xmalloc((size_t)n * q->csz);
     memcpy(q->h, h, (size_t)n * q->csz);
+    q->hg = lq_host_taps(kind, q->h, n, 1);
     lq_ctx_init(&q->ctx);
     lq_firfilt_alloc_state(q);
     lq_firfilt_upload_coefs(q);
@@ -164,6 +166,8 @@ lq_firfilt *lq_firfilt_recreate(lq_firfilt *q, const float *h, unsigned int n)
         lq_firfilt_alloc_state(q);
     }
     memcpy(q->h, h, (size_t)n * q->csz);
+    free(q->hg);
+    q->hg = lq_host_taps(q->kind, q->h, n, 1);
     lq_firfilt_upload_coefs(q);
     return q;
 }
@@ -179,6 +183,7 @@ void lq_firfilt_destroy(lq_firfilt *q)
     lq_devbuf_free(&q->flags);
     lq_ctx_free(&q->ctx);
     free(q->h);
+    free(q->hg);
     free(q);
 }
 
@@ -256,7 +261,8 @@ void lq_firfilt_execute(lq_firfilt *q, void *y)
     if (lq_small_host()) {   /* opt-in host path (lq_small.c): the window's newest sample is h_win[HP-1] */
         lq_firfilt_need_host(q);
         float v[2];
-        lq_host_conv(q->kind, q->h, q->h_win + q->hoff * q->esz, q->HP - 1, q->hlen, v);
+        /* the last hlen window samples, oldest first, against the reversed taps */
+        lq_host_tdot(q->kind, q->hg, q->h_win + (q->hoff + q->HP - q->hlen) * q->esz, q->hlen, v);
         if (q->kind == LQ_RRRF) {
             *(float *)y = v[0] * q->d.scale_re;
         } else if (q->kind == LQ_CRCF) {   /* firfilt.c:337: real scale per component */

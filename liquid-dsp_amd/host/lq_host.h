@@ -76,7 +76,8 @@ void lq_sig_wait(lq_ctx *c, void *y, size_t bytes, unsigned seq);
 /* opt-in host path for single-sample calls (host/lq_small.c) */
 int lq_small_host(void);
 void lq_host_dot(int kind, const float *h, const void *x, unsigned int n, void *y);
-void lq_host_conv(int kind, const float *h, const void *w, unsigned int last, unsigned int n, void *y);
+float *lq_host_taps(int kind, const float *h, unsigned int n, int rev);
+void lq_host_tdot(int kind, const float *g, const void *x, unsigned int n, void *y);
 typedef struct {
     unsigned char *buf;
     size_t n, esz, cap, off;   /* history = n samples at buf + off*esz */

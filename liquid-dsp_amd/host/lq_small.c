@@ -98,60 +98,117 @@ void lq_host_dot(int kind, const float *h, const void *xv, unsigned int n, void 
     }
 }
 
-/* y = sum_{k<n} h[k] w[last - k] over a window w whose newest sample is at
- * index `last` (the filter convolution, src/filter/src/firfilt.c:322-338:
- * the reference runs its dot product over the reversed taps and the window's
- * oldest-first samples, the same terms) */
-void lq_host_conv(int kind, const float *h, const void *wv, unsigned int last, unsigned int n, void *y)
+/* Objects that keep their taps (firfilt, dotprod) run the per-call dot
+ * product over an expanded copy made at create time, so the inner loop is a
+ * plain multiply-add of two contiguous float arrays with no shuffles (the
+ * reference's dotprod_*.mmx.c likewise keep a rearranged copy of the taps):
+ *   rrrf  g[i]                                   n floats
+ *   crcf  (g[i], g[i]) pairs                     2n floats
+ *   cccf  (gr[i], gr[i]) pairs, (-gi[i], gi[i])  4n floats
+ * with g[i] = h[n-1-i] when rev (the filter convolution over the window's
+ * oldest-first samples, firfilt.c:322-338) else h[i] (dotprod.c:42-167). */
+float *lq_host_taps(int kind, const float *h, unsigned int n, int rev)
 {
-    lq_v4 a0 = {0, 0, 0, 0}, a1 = {0, 0, 0, 0};
-    unsigned int k = 0;
-    if (kind == LQ_RRRF) {
-        const float *w = (const float *)wv + last;   /* w[-k]: sample last - k */
-        const lq_v4i rev = {3, 2, 1, 0};
-        for (; k + 8 <= n; k += 8) {
-            a0 += lq_ld4(h + k) * __builtin_shuffle(lq_ld4(w - (long)k - 3), rev);
-            a1 += lq_ld4(h + k + 4) * __builtin_shuffle(lq_ld4(w - (long)k - 7), rev);
+    const unsigned int nf = kind == LQ_RRRF ? n : (kind == LQ_CRCF ? 2 * n : 4 * n);
+    float *g = (float *)lq_xmalloc((size_t)(nf ? nf : 1) * sizeof(float));
+    for (unsigned int i = 0; i < n; i++) {
+        const unsigned int k = rev ? n - 1 - i : i;
+        if (kind == LQ_RRRF) {
+            g[i] = h[k];
+        } else if (kind == LQ_CRCF) {
+            g[2 * i] = g[2 * i + 1] = h[k];
+        } else {
+            g[2 * i] = g[2 * i + 1] = h[2 * k];
+            g[2 * n + 2 * i] = -h[2 * k + 1];
+            g[2 * n + 2 * i + 1] = h[2 * k + 1];
         }
-        a0 += a1;
-        float r = (a0[0] + a0[1]) + (a0[2] + a0[3]);
-        for (; k < n; k++) r += h[k] * w[-(long)k];
-        *(float *)y = r;
-    } else if (kind == LQ_CRCF) {
-        const float *w = (const float *)wv + 2 * (size_t)last;
-        /* the pair (sample last-k-1, sample last-k) loaded as one vector,
-         * swapped to (last-k, last-k-1) against taps (h_k, h_k, h_k+1, h_k+1) */
-        const lq_v4i swp = {2, 3, 0, 1}, dup01 = {0, 0, 1, 1}, dup23 = {2, 2, 3, 3};
-        for (; k + 4 <= n; k += 4) {
-            const lq_v4 hv = lq_ld4(h + k);
-            a0 += __builtin_shuffle(hv, dup01) * __builtin_shuffle(lq_ld4(w - 2 * (long)k - 2), swp);
-            a1 += __builtin_shuffle(hv, dup23) * __builtin_shuffle(lq_ld4(w - 2 * (long)k - 6), swp);
-        }
-        a0 += a1;
-        float re = a0[0] + a0[2], im = a0[1] + a0[3];
-        for (; k < n; k++) {
-            re += h[k] * w[-2 * (long)k];
-            im += h[k] * w[-2 * (long)k + 1];
-        }
-        ((float *)y)[0] = re;
-        ((float *)y)[1] = im;
-    } else {
-        const float *w = (const float *)wv + 2 * (size_t)last;
-        const lq_v4i swp = {2, 3, 0, 1}, re2 = {0, 0, 2, 2}, im2 = {1, 1, 3, 3}, sw = {1, 0, 3, 2};
-        for (; k + 2 <= n; k += 2) {
-            const lq_v4 hv = lq_ld4(h + 2 * k), xv4 = __builtin_shuffle(lq_ld4(w - 2 * (long)k - 2), swp);
-            a0 += __builtin_shuffle(hv, re2) * xv4;
-            a1 += __builtin_shuffle(hv, im2) * __builtin_shuffle(xv4, sw);
-        }
-        float re = (a0[0] + a0[2]) - (a1[0] + a1[2]), im = (a0[1] + a0[3]) + (a1[1] + a1[3]);
-        for (; k < n; k++) {
-            const float hr = h[2 * k], hi = h[2 * k + 1], xr = w[-2 * (long)k], xi = w[-2 * (long)k + 1];
-            re += hr * xr - hi * xi;
-            im += hr * xi + hi * xr;
-        }
-        ((float *)y)[0] = re;
-        ((float *)y)[1] = im;
     }
+    return g;
+}
+
+/* the expanded-tap dot product, for a vector type V of W floats: four
+ * accumulators keep four multiply-add chains in flight over the long part,
+ * single vectors take the rest down to W floats, then scalars */
+#define LQ_TDOT_STEP(A, OFF, V, W, SWAPMASK)                                                       \
+    do {                                                                                            \
+        V t_, u_;                                                                                   \
+        __builtin_memcpy(&t_, g + (OFF), sizeof(V));                                                \
+        __builtin_memcpy(&u_, x + (OFF), sizeof(V));                                                \
+        A += t_ * u_;                                                                               \
+        if (kind == LQ_CCCF) { /* + (-gi, gi) * (xi, xr) */                                         \
+            __builtin_memcpy(&t_, g + 2 * n + (OFF), sizeof(V));                                    \
+            A += t_ * __builtin_shuffle(u_, SWAPMASK);                                              \
+        }                                                                                           \
+    } while (0)
+#define LQ_TDOT_BODY(V, W, SWAPMASK, FOLD)                                                          \
+    const float *x = (const float *)xv;                                                             \
+    V a0 = {0}, a1 = {0}, a2 = {0}, a3 = {0};                                                       \
+    const unsigned int nf = kind == LQ_RRRF ? n : 2 * n;                                            \
+    unsigned int i = 0;                                                                             \
+    for (; i + 4 * (W) <= nf; i += 4 * (W)) {                                                      \
+        LQ_TDOT_STEP(a0, i, V, W, SWAPMASK);                                                        \
+        LQ_TDOT_STEP(a1, i + (W), V, W, SWAPMASK);                                                  \
+        LQ_TDOT_STEP(a2, i + 2 * (W), V, W, SWAPMASK);                                              \
+        LQ_TDOT_STEP(a3, i + 3 * (W), V, W, SWAPMASK);                                              \
+    }                                                                                               \
+    for (; i + 2 * (W) <= nf; i += 2 * (W)) {                                                      \
+        LQ_TDOT_STEP(a0, i, V, W, SWAPMASK);                                                        \
+        LQ_TDOT_STEP(a1, i + (W), V, W, SWAPMASK);                                                  \
+    }                                                                                               \
+    if (i + (W) <= nf) {                                                                            \
+        LQ_TDOT_STEP(a2, i, V, W, SWAPMASK);                                                        \
+        i += (W);                                                                                   \
+    }                                                                                               \
+    a0 += a1;                                                                                       \
+    a2 += a3;                                                                                       \
+    a0 += a2;                                                                                       \
+    FOLD; /* lanes 0, 1: the even / odd partial sums */                                             \
+    float r0 = a0[0], r1 = a0[1];                                                                   \
+    if (kind == LQ_RRRF) {                                                                          \
+        r0 += r1;                                                                                   \
+        for (; i < nf; i++) r0 += g[i] * x[i];                                                      \
+        *(float *)y = r0;                                                                           \
+        return;                                                                                     \
+    }                                                                                               \
+    for (; i < nf; i += 2) {                                                                        \
+        r0 += g[i] * x[i];                                                                          \
+        r1 += g[i + 1] * x[i + 1];                                                                  \
+        if (kind == LQ_CCCF) {                                                                      \
+            r0 += g[2 * n + i] * x[i + 1];                                                          \
+            r1 += g[2 * n + i + 1] * x[i];                                                          \
+        }                                                                                           \
+    }                                                                                               \
+    ((float *)y)[0] = r0;                                                                           \
+    ((float *)y)[1] = r1;
+
+static void lq_tdot_sse(int kind, const float *g, const void *xv, unsigned int n, void *y)
+{
+    LQ_TDOT_BODY(lq_v4, 4, ((lq_v4i){1, 0, 3, 2}), a0 += __builtin_shuffle(a0, ((lq_v4i){2, 3, 0, 1})))
+}
+
+typedef float lq_v8 __attribute__((vector_size(32)));
+typedef int lq_v8i __attribute__((vector_size(32)));
+__attribute__((target("avx2"))) static void lq_tdot_avx2(int kind, const float *g, const void *xv, unsigned int n,
+                                                         void *y)
+{
+    LQ_TDOT_BODY(lq_v8, 8, ((lq_v8i){1, 0, 3, 2, 5, 4, 7, 6}),
+                 a0 += __builtin_shuffle(a0, ((lq_v8i){4, 5, 6, 7, 0, 1, 2, 3}));
+                 a0 += __builtin_shuffle(a0, ((lq_v8i){2, 3, 0, 1, 6, 7, 4, 5})))
+}
+
+static int g_avx2 = -1;
+
+/* y = sum_i g[i] x[i] over the expanded taps of lq_host_taps (n samples) */
+void lq_host_tdot(int kind, const float *g, const void *x, unsigned int n, void *y)
+{
+    if (g_avx2 < 0) g_avx2 = __builtin_cpu_supports("avx2") ? 1 : 0;
+    /* 32-byte vectors from 16 floats up (per-call rates on the box's EPYC
+     * host against the 16-byte form: dotprod crcf / cccf 1.45x / 1.9x,
+     * fftfilt 1.6x, firfilt 0.95x; profiles/r06_ab_experiments.txt, r06host) */
+    if (g_avx2 && (kind == LQ_RRRF ? n : 2 * n) >= 16)
+        lq_tdot_avx2(kind, g, x, n, y);
+    else
+        lq_tdot_sse(kind, g, x, n, y);
 }
 
 /* ------------------------------------------------------------------ mirrors

@@ -81,7 +81,8 @@ struct lq_rs_s {
     rs_state now;                 /* timing state at gpos */
     void *d_hist[2];              /* last L inputs */
     int cur;
-    float *hbank;                 /* host bank taps hbank[b*L + n] = h[b + n*npfb] (small-call mode) */
+    float *hbank;                 /* host bank taps h[b + n*npfb], n < L, reversed and expanded (lq_host_taps), hbs floats per bank */
+    size_t hbs;
     lq_mirror hm;                 /* host copy of the history (small-call mode) */
     rs_state hs;                  /* timing state of the host path, valid while hs_valid */
     int hs_valid;
@@ -717,9 +718,19 @@ lq_rs *lq_rs_create(int kind, float _rate, unsigned int _m, float _fc, float _As
     q->d_hist[1] = lqrt_malloc((size_t)q->L * q->esz);
     lqrt_sync(q->ctx.stream);
     lqrt_sync(q->ctx.stream);
-    q->hbank = (float *)lq_xmalloc(ntap * sizeof(float));
-    for (unsigned int b = 0; b < _npfb; b++)
-        for (unsigned int k = 0; k < q->L; k++) q->hbank[b * q->L + k] = hf[b + k * _npfb];
+    {
+        const int ck = q->kind == LQ_RRRF ? LQ_RRRF : LQ_CRCF;   /* real taps for every type */
+        float *hb = (float *)lq_xmalloc((size_t)q->L * sizeof(float));
+        q->hbs = (size_t)q->L * (ck == LQ_RRRF ? 1 : 2);
+        q->hbank = (float *)lq_xmalloc((size_t)_npfb * q->hbs * sizeof(float));
+        for (unsigned int b = 0; b < _npfb; b++) {
+            for (unsigned int k = 0; k < q->L; k++) hb[k] = hf[b + k * _npfb];
+            float *g = lq_host_taps(ck, hb, q->L, 1);
+            memcpy(q->hbank + b * q->hbs, g, q->hbs * sizeof(float));
+            free(g);
+        }
+        free(hb);
+    }
     lq_mirror_init(&q->hm, q->L, q->esz);
     q->hs_valid = 0;
     free(tp);
@@ -915,11 +926,12 @@ static void lq_rs_exec1_host(lq_rs *q, const void *x, void *y, unsigned int *ny)
         }
         float y0[2] = {0.f, 0.f}, y1[2] = {0.f, 0.f};
         if (s->st == RS_BOUNDARY) {
-            lq_host_conv(ck, q->hbank + (size_t)(npfb - 1) * L, w, L - 1, L, y0);
-            lq_host_conv(ck, q->hbank, w, L, L, y1);
+            /* bank npfb-1 on the window one input older, bank 0 on the newest */
+            lq_host_tdot(ck, q->hbank + (size_t)(npfb - 1) * q->hbs, w, L, y0);
+            lq_host_tdot(ck, q->hbank, w + q->esz, L, y1);
         } else {
-            lq_host_conv(ck, q->hbank + (size_t)s->b * L, w, L, L, y0);
-            lq_host_conv(ck, q->hbank + (size_t)(s->b + 1) * L, w, L, L, y1);
+            lq_host_tdot(ck, q->hbank + (size_t)s->b * q->hbs, w + q->esz, L, y0);
+            lq_host_tdot(ck, q->hbank + (size_t)(s->b + 1) * q->hbs, w + q->esz, L, y1);
         }
         const float a = 1.0f - s->mu;
         float *yo = (float *)((unsigned char *)y + (size_t)n * q->esz);
