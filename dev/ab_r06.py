@@ -109,6 +109,15 @@ def main():
         L.fft_set_stream(pl, ST.cuda_stream)
         ms = timed(lambda: L.fft_execute_batch_dev(pl, Z.data_ptr(), Z.data_ptr(), B))
         nb = 16.0 * B * N
+    elif what == "firdecim":   # firdecim_crcf M = arg, m = 8, 2^27 inputs
+        M = int(arg)
+        n = 1 << 27
+        x, y = cbuf(n), torch.empty(2 * (n // M), device="cuda")
+        q = LQ.FirDecim(M, m=8, As=60.0)
+        q.set_stream(ST.cuda_stream)
+        L = LQ.lib()
+        ms = timed(lambda: L.firdecim_crcf_execute_block_dev(q.q, x.data_ptr(), n // M, y.data_ptr()))
+        nb = 8.0 * n + 8.0 * (n // M)
     elif what == "pfbsyn":   # firpfbch2 synthesizer M, m=4, 2^26 outputs
         M = int(arg)
         nout = 1 << 26

@@ -1049,45 +1049,64 @@ extern "C" unsigned lqk_firdecim_ph_qc(unsigned M, unsigned hlen)
     return (q0 + 3) / 4 * 4;   // k_firdecim_ph2 runs taps in chunks of four
 }
 
+namespace {
+// The persistent prefetching form (k_firdecim_pf) for 16-byte aligned x: R
+// outputs per lane on NTD lanes, TO = R NTD outputs and (TO + QC - 1) M input
+// samples per workgroup in LDS; -1 when the shape does not fit it
+template <int R, int NTD>
+int decim_pf(int kind, unsigned int M, unsigned int QC, const void *hq, unsigned int hl1, const void *hist,
+             const void *x, unsigned long long nout, void *y, hipStream_t st)
+{
+    constexpr int TO2 = R * NTD;
+    const int J = TO2 + (int)QC - 1;
+    const size_t lds = (size_t)M * (R * dph2_q<R>(J) + 1) * elem_size(kind);
+    const int S = J * (int)M + 1;
+    const int vw = 16 / (int)elem_size(kind);
+    const int nl = (S + NTD * vw - 1) / (NTD * vw);
+    if (!((QC % 4) == 0 && lds <= 40 * 1024 && (unsigned long long)(J) * M < (1u << 24) &&
+          ((uintptr_t)x & 15) == 0 && nl <= 12 && nout * M * elem_size(kind) < (1ull << 31)))
+        return -1;
+    const unsigned long long nt = (nout + TO2 - 1) / TO2;
+    const int wpc = (int)((160 * 1024) / lds) < 8 ? (int)((160 * 1024) / lds) : 8;
+    const unsigned nb = (unsigned)(nt < 256ull * wpc ? nt : 256ull * wpc);
+#define LQ_DP(K, NLV)                                                                                      \
+    hipLaunchKernelGGL((k_firdecim_pf<K, R, NTD, NLV>), dim3(nb), dim3(NTD), lds, st, (const kt<K>::T *)hist, \
+                       (int)hl1, (const kt<K>::T *)x, (long long)nout, (int)M, (int)QC, (kt<K>::T *)y,         \
+                       (const kt<K>::TC *)hq);
+#define LQ_DPK(K)                                                                                          \
+    if (nl <= 5) { LQ_DP(K, 5) } else if (nl <= 9) { LQ_DP(K, 9) } else { LQ_DP(K, 12) }
+    switch (kind) {
+    case 0: LQ_DPK(0) break;
+    case 1: LQ_DPK(1) break;
+    default: LQ_DPK(2) break;
+    }
+#undef LQ_DPK
+#undef LQ_DP
+    LQ_CHECK_LAUNCH();
+    return 0;
+}
+} // namespace
+
 extern "C" int lqk_firdecim_ph(int kind, unsigned int M, unsigned int QC, const void *hq, unsigned int hl1,
                                const void *hist, const void *x, unsigned long long nout, void *y, void *stream)
 {
     if (nout == 0) return 0;
     hipStream_t st = (hipStream_t)stream;
+    // the persistent form: at M = 8 (m = 8 crcf, 2^27 inputs: 0.304-0.333 ->
+    // 0.283-0.286 ms against the one-shot form, r05zf) two outputs per lane
+    // on 256 lanes (four per lane on 128: 0.271 -> 0.36 ms); at small M, where
+    // the outputs are many and each is M (QC / 4)(R + 3) / R window reads,
+    // four per lane on 128 lanes (M = 2 / 3 / 4: 0.468 / 0.337 / 0.303 ->
+    // 0.333 / 0.303 / 0.266 ms, r06fd)
+    if ((M <= 4 ? decim_pf<4, 128>(kind, M, QC, hq, hl1, hist, x, nout, y, st)
+                : decim_pf<2, 256>(kind, M, QC, hq, hl1, hist, x, nout, y, st)) == 0)
+        return 0;
     {
-        // 512 outputs and (512 + QC - 1) M input samples per workgroup in LDS:
-        // two outputs per lane, 256 lanes (four per lane on 128 lanes halves
-        // the occupancy: 0.51 vs 0.34 ms for M = 8 m = 8)
+        // one-shot form: 512 outputs per workgroup, two per lane, 256 lanes
         constexpr int LQ_D2R = 2, LQ_D2NT = 256;
         constexpr int TO2 = LQ_D2R * LQ_D2NT;
         const int J = TO2 + (int)QC - 1;
         const size_t lds = (size_t)M * (LQ_D2R * dph2_q<LQ_D2R>(J) + 1) * elem_size(kind);
-        const int S = J * (int)M + 1;
-        const int vw = 16 / (int)elem_size(kind);
-        const int nl = (S + LQ_D2NT * vw - 1) / (LQ_D2NT * vw);
-        // 16-byte aligned x: the persistent prefetching form (M = 8, m = 8
-        // crcf, 2^27 inputs: 0.304-0.333 -> 0.283-0.286 ms, r05zf)
-        if ((QC % 4) == 0 && lds <= 40 * 1024 && (unsigned long long)(J) * M < (1u << 24) &&
-            ((uintptr_t)x & 15) == 0 && nl <= 12 && nout * M * elem_size(kind) < (1ull << 31)) {
-            const unsigned long long nt = (nout + TO2 - 1) / TO2;
-            const int wpc = (int)((160 * 1024) / lds) < 8 ? (int)((160 * 1024) / lds) : 8;
-            const unsigned nb = (unsigned)(nt < 256ull * wpc ? nt : 256ull * wpc);
-#define LQ_DP(K, NLV)                                                                                      \
-    hipLaunchKernelGGL((k_firdecim_pf<K, LQ_D2R, LQ_D2NT, NLV>), dim3(nb), dim3(LQ_D2NT), lds, st,          \
-                       (const kt<K>::T *)hist, (int)hl1, (const kt<K>::T *)x, (long long)nout, (int)M, (int)QC, \
-                       (kt<K>::T *)y, (const kt<K>::TC *)hq);
-#define LQ_DPK(K)                                                                                          \
-    if (nl <= 5) { LQ_DP(K, 5) } else if (nl <= 9) { LQ_DP(K, 9) } else { LQ_DP(K, 12) }
-            switch (kind) {
-            case 0: LQ_DPK(0) break;
-            case 1: LQ_DPK(1) break;
-            default: LQ_DPK(2) break;
-            }
-#undef LQ_DPK
-#undef LQ_DP
-            LQ_CHECK_LAUNCH();
-            return 0;
-        }
         if ((QC % 4) == 0 && lds <= 64 * 1024 && (unsigned long long)(J) * M < (1u << 24)) {
             const unsigned nb = (unsigned)((nout + TO2 - 1) / TO2);
 #define LQ_D2(K)                                                                                          \
@@ -1103,6 +1122,10 @@ extern "C" int lqk_firdecim_ph(int kind, unsigned int M, unsigned int QC, const 
             return 0;
         }
     }
+    // longer spans (M >= 16 at 2 M m taps): the persistent form on 256-output
+    // tiles, one output per lane (M = 16 m = 8: 0.479 -> 0.308 ms; at M = 12
+    // the one-shot form above is faster, 0.306 vs 0.366, r06fd)
+    if (decim_pf<1, 256>(kind, M, QC, hq, hl1, hist, x, nout, y, st) == 0) return 0;
     switch (kind) {
     case 0: return decim_ph_qct<0>(M, QC, hq, hl1, hist, x, (long long)nout, y, st);
     case 1: return decim_ph_qct<1>(M, QC, hq, hl1, hist, x, (long long)nout, y, st);
