@@ -118,6 +118,15 @@ def main():
         L = LQ.lib()
         ms = timed(lambda: L.firdecim_crcf_execute_block_dev(q.q, x.data_ptr(), n // M, y.data_ptr()))
         nb = 8.0 * n + 8.0 * (n // M)
+    elif what == "firinterp":   # firinterp_crcf M = arg, m = 8, 2^27 outputs
+        M = int(arg)
+        n = (1 << 27) // M
+        x, y = cbuf(n), torch.empty(2 * n * M, device="cuda")
+        q = LQ.FirInterp(M, m=8, As=60.0)
+        q.set_stream(ST.cuda_stream)
+        L = LQ.lib()
+        ms = timed(lambda: L.firinterp_crcf_execute_block_dev(q.q, x.data_ptr(), n, y.data_ptr()))
+        nb = 8.0 * n + 8.0 * n * M
     elif what == "pfbsyn":   # firpfbch2 synthesizer M, m=4, 2^26 outputs
         M = int(arg)
         nout = 1 << 26

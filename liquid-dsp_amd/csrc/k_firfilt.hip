@@ -808,7 +808,11 @@ __global__ __launch_bounds__(NT) void k_firinterp_t(const typename kt<KIND>::T *
     T *yw = y + iw * M;
     for (int e = lane * VE; e < nout; e += 64 * VE) {
         if (e + VE <= nout) {
-            *reinterpret_cast<float4 *>(yw + e) = *reinterpret_cast<const float4 *>(st + e);
+            // non-temporal: the outputs are not read back (M = 8 m = 8 crcf,
+            // 2^27 outputs: 0.270 -> 0.244-0.248 ms, M = 4: 0.314 -> 0.244-0.250,
+            // r06fi)
+            typedef float v4nt __attribute__((ext_vector_type(4)));
+            __builtin_nontemporal_store(*reinterpret_cast<const v4nt *>(st + e), reinterpret_cast<v4nt *>(yw + e));
         } else {
             for (int k = 0; k < VE && e + k < nout; k++) yw[e + k] = st[e + k];
         }
