@@ -127,6 +127,28 @@ def main():
         L = LQ.lib()
         ms = timed(lambda: L.firinterp_crcf_execute_block_dev(q.q, x.data_ptr(), n, y.data_ptr()))
         nb = 8.0 * n + 8.0 * n * M
+    elif what == "resamp2":   # resamp2_crcf m = 12, 2^26 inputs: arg 0 decim, 1 interp
+        n = 1 << 26
+        x, y = cbuf(n), torch.empty(2 * 2 * n, device="cuda")
+        q = LQ.Resamp2(12, 0.0, 60.0)
+        q.set_stream(ST.cuda_stream)
+        L = LQ.lib()
+        if arg == 0:
+            ms = timed(lambda: L.resamp2_crcf_execute_block_dev(q.q, LQ.RESAMP2_DECIM, x.data_ptr(), n // 2,
+                                                                 y.data_ptr(), None))
+            nb = 12.0 * n
+        else:
+            ms = timed(lambda: L.resamp2_crcf_execute_block_dev(q.q, LQ.RESAMP2_INTERP, x.data_ptr(), n,
+                                                                 y.data_ptr(), None))
+            nb = 24.0 * n
+    elif what == "msresamp":   # msresamp_crcf rate arg, 2^26 inputs (2^24 for r > 1)
+        n = 1 << 26 if arg < 1 else 1 << 24
+        x, y = cbuf(n), torch.empty(2 * (int(n * arg) + 4096), device="cuda")
+        q = LQ.MsResamp(arg, 60.0)
+        q.set_stream(ST.cuda_stream)
+        nout = q.num_output(n)
+        ms = timed(lambda: q.execute_block_dev(x.data_ptr(), n, y.data_ptr()))
+        nb = 8.0 * n + 8.0 * nout
     elif what == "pfbsyn":   # firpfbch2 synthesizer M, m=4, 2^26 outputs
         M = int(arg)
         nout = 1 << 26

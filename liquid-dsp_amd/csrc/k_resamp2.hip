@@ -262,7 +262,16 @@ __global__ __launch_bounds__(NT) void k_resamp2_tiled_b(R2Args a, const C *__res
         if (i >= a.n) break;
         const S yq = acc[r], yd = e0[l0 + NT * r];
         if constexpr (MODE == LQK_R2_DECIM) {
-            y0[i] = r2_scale(a.scale, r2_add(yd, yq));
+            {   // non-temporal stores (decim 0.159 -> 0.155 ms, interp 0.348 ->
+                // 0.337 ms per 2^26 inputs at m = 12, r06r2)
+                const S v = r2_scale(a.scale, r2_add(yd, yq));
+                if constexpr (sizeof(S) == 8) {
+                    typedef float v2nt __attribute__((ext_vector_type(2)));
+                    __builtin_nontemporal_store(v2nt{v.x, v.y}, reinterpret_cast<v2nt *>(y0 + i));
+                } else {
+                    __builtin_nontemporal_store(v, y0 + i);
+                }
+            }
         } else {
             const S o0 = MODE == LQK_R2_ANALYZER ? r2_add(yq, yd) : yd;
             const S o1 = MODE == LQK_R2_ANALYZER ? r2_sub(yq, yd) : yq;
@@ -272,7 +281,7 @@ __global__ __launch_bounds__(NT) void k_resamp2_tiled_b(R2Args a, const C *__res
                 // 16 bytes apart each covered half of every line)
                 if (al16) {
                     typedef float v4f_ __attribute__((ext_vector_type(4)));
-                    *reinterpret_cast<v4f_ *>(y0 + 2 * i) = v4f_{o0.x, o0.y, o1.x, o1.y};
+                    __builtin_nontemporal_store(v4f_{o0.x, o0.y, o1.x, o1.y}, reinterpret_cast<v4f_ *>(y0 + 2 * i));
                 } else {
                     y0[2 * i] = o0;
                     y0[2 * i + 1] = o1;
